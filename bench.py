@@ -1,0 +1,204 @@
+"""Headline benchmark: edges/s of full-batch GraphSAGE fwd+bwd on the Elliptic shape (BASELINE.json).
+
+Workload (BASELINE.json configs[1]): configs/sage.yaml with symmetrize_edges=true — 2-layer
+SAGE 166->128->2, dropout 0.5, fp32, N=203,769 nodes, E=468,710 symmetrized edges
+(synthetic, seeded; the Elliptic CSVs are LFS pointers in the reference).  One step =
+the reference's train_epoch (src/train_gnn.py:187-209): forward + masked weighted CE +
+backward + clip_grad_norm_(1.0) + Adam; the loss stays on device (no per-step .item()).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): weak scaling.  Each rank owns
+a full Elliptic-shaped timestep partition of an N-times larger graph (no cross-timestep
+edges, so no halo exchange); gradients are summed with one flat RCCL all-reduce per step
+and the loss is normalised by the global train count.  value = edges of all ranks / max
+rank time.
+
+Extra fields: ``roofline`` (dominant libgnnmp kernel: algorithmic bytes per launch / its
+HIP-event-timed average duration, on the launch stream) and ``cpu_baseline`` (the oracle —
+the PyG-2.5.3 ATen op sequence — timed on this host's cores, rank 0 only, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "edges/s full-batch SAGE fwd+bwd, Elliptic 203k/234k/166-feat, 1→8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--degree", default="powerlaw", choices=["powerlaw", "uniform"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def make_inputs(rank: int, degree: str):
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+
+    data = synthetic_elliptic(degree=degree, seed=42 + rank)
+    cfg = dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10)
+    return prepare_inputs(data, cfg)
+
+
+def cpu_baseline(data, state, cw, denom, budget_s: float):
+    """Oracle (PyG-2.5.3 ATen op sequence) train step on the host CPU, same step definition."""
+    from oracle import pyg_ref
+
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in state.items()}
+    opt = torch.optim.Adam(params.values(), lr=0.003, weight_decay=1e-4)
+    x, ei, y, m = data.x, data.edge_index, data.y, data.train_mask
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        logits = pyg_ref.model_forward("sage", params, x, ei, layers=2, dropout=0.5, training=True)
+        loss = torch.nn.functional.cross_entropy(logits[m], y[m], weight=cw, reduction="none").sum() / denom
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
+        opt.step()
+
+    step()  # warm-up (allocator, thread pool)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 50:
+            break
+    return {
+        "value": ei.size(1) * n / el,
+        "unit": "edges/s",
+        "cores": torch.get_num_threads(),
+        "kind": "port",
+        "sample": f"{n} full-size steps (N={x.size(0)}, E={ei.size(1)}), {el:.1f}s, oracle/pyg_ref.py on CPU",
+        "ms_per_step": 1e3 * el / n,
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if not (world == 1 and args.gpus == 1):
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from elliptic_gnn_project_amd import distributed as gdist
+    from elliptic_gnn_project_amd.aggregation import KernelTimer
+    from elliptic_gnn_project_amd.gnn import SAGENet
+    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn
+
+    data_cpu = make_inputs(rank, args.degree)
+    data = data_cpu.to(dev)
+    torch.manual_seed(42)  # identical initial weights on every rank
+    model = SAGENet(data.x.size(1), hidden_dim=128, layers=2, dropout=0.5).to(dev)
+    state0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4)
+    cw, denom = gdist.global_class_weight_and_count(data.y, data.train_mask, dist)
+    loss_fn = _make_loss_fn({}, cw, model, 1, 34)
+    bucket = gdist.GradBucket(model) if dist is not None else None
+
+    def step():
+        model.train()
+        opt.zero_grad(set_to_none=False)
+        logits = model(data.x, data.edge_index)
+        loss = loss_fn(logits[data.train_mask], data.y[data.train_mask], denom=denom)
+        loss.backward()
+        if bucket is not None:
+            bucket.allreduce_(dist)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    E = data.edge_index.size(1)
+    value = E * world * args.steps / el
+
+    roof = None
+    if not args.no_roofline:
+        KernelTimer.start()
+        for _ in range(5):
+            step()
+        recs = KernelTimer.stop()
+        tag, r = max(recs.items(), key=lambda kv: kv[1]["ms"])
+        avg_ms = r["ms"] / r["launches"]
+        bpl = r["bytes"] / r["launches"]
+        achieved = bpl / (avg_ms * 1e-3) / 1e9
+        names = {0: "sum", 1: "mean_fwd", 2: "mean_bwd", 3: "gcn", 4: "edge_w"}
+        roof = {
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": f"agg_rowwave[{names[tag[0]]}, {'csc' if tag[1] else 'csr'}, F={tag[2]}]",
+            "avg_us": round(avg_ms * 1e3, 2), "bytes_per_launch": int(bpl),
+        }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(data_cpu, state0, cw, denom, args.cpu_seconds)
+        cpu["speedup_gpu_over_cpu"] = round(value / cpu["value"], 1)
+
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC,
+            "value": value,
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * el / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic Elliptic-shape ({args.degree} in-degree, seed 42+rank)",
+            "config": {
+                "workload": "configs/sage.yaml + symmetrize_edges=true: SAGE 2L 166->128->2, dropout 0.5, "
+                            "full-batch train step (fwd+masked CE+bwd+clip+Adam)",
+                "nodes_per_gpu": data.x.size(0), "edges_per_gpu": E, "feats": data.x.size(1),
+                "parallelism": f"dp{world} timestep-partitioned" if world > 1 else "single",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

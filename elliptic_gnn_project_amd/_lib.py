@@ -1,0 +1,167 @@
+"""ctypes binding of ``libgnnmp.so`` — the C ABI declared in ``include/gnnmp.h``.
+
+The library is built in-tree (``make -C elliptic_gnn_project_amd/csrc``) and loaded
+from the package directory.  There is no fallback: if the shared object is missing
+or fails to load, every op raises.  ``torch`` is imported first so that the HIP
+runtime torch ships (soname ``libamdhip64.so.7``) is the one the library binds to.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = PKG_DIR / "libgnnmp.so"
+ABI_VERSION = 1
+
+# gnn_status
+GNN_OK = 0
+_STATUS_EXC = {
+    1: ValueError,
+    2: IndexError,
+    3: RuntimeError,
+    4: RuntimeError,
+    5: NotImplementedError,
+}
+
+# gnn_loop_mode
+LOOPS_KEEP = 0
+LOOPS_REPLACE = 1
+
+# gnn_agg_mode
+AGG_SUM = 0
+AGG_MEAN = 1
+AGG_MEAN_BWD = 2
+AGG_GCN = 3
+AGG_EDGE_W = 4
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_ptr = ctypes.c_void_p
+c_size = ctypes.c_size_t
+
+
+class GnnGraph(ctypes.Structure):
+    _fields_ = [
+        ("num_nodes", c_i64),
+        ("num_slots", c_i64),
+        ("rowptr", c_ptr),
+        ("col", c_ptr),
+        ("colptr", c_ptr),
+        ("row", c_ptr),
+        ("csc2csr", c_ptr),
+    ]
+
+
+class GnnAggParams(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int),
+        ("transpose", c_i32),
+        ("nodew", c_ptr),
+        ("ew", c_ptr),
+        ("heads", c_i32),
+        ("addend", c_ptr),
+        ("ld_add", c_i64),
+        ("bias", c_ptr),
+        ("relu", c_i32),
+    ]
+
+
+# name -> (restype, argtypes).  Mirrors include/gnnmp.h one to one; the CPU test
+# suite checks that every function declared in the header appears here and is exported.
+SIGNATURES = {
+    "gnn_abi_version": (ctypes.c_int, []),
+    "gnn_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "gnn_last_error": (ctypes.c_char_p, []),
+    "gnn_graph_workspace_size": (ctypes.c_int, [c_i64, c_i64, ctypes.POINTER(c_size)]),
+    "gnn_graph_build": (
+        ctypes.c_int,
+        [c_ptr, c_i64, c_i64, ctypes.c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_in_degree_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), c_ptr, c_ptr]),
+    "gnn_gcn_norm_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), c_ptr, c_ptr]),
+    "gnn_aggregate_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), ctypes.POINTER(GnnAggParams), c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_sage_mean_fwd_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_sage_mean_bwd_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_gat_scores_f32": (
+        ctypes.c_int,
+        [c_i64, c_i32, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    ),
+    "gnn_gat_fwd_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr,
+         c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_gat_bwd_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, ctypes.POINTER(c_size)]),
+    "gnn_gat_bwd_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
+         c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_colsum_workspace_size": (ctypes.c_int, [c_i64, c_i64, ctypes.POINTER(c_size)]),
+    "gnn_colsum_f32": (ctypes.c_int, [c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
+}
+
+_LIB: ctypes.CDLL | None = None
+
+
+class GnnmpError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libgnnmp.so (once).  Raises if it is missing — there is no fallback path."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not LIB_PATH.exists():
+        raise GnnmpError(
+            f"{LIB_PATH} not found: build it with `make -C {PKG_DIR / 'csrc'}` "
+            "(or __graft_entry__.build()).  The MI355X kernels are required; there is no CPU fallback."
+        )
+    lib = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    ver = lib.gnn_abi_version()
+    if ver != ABI_VERSION:
+        raise GnnmpError(f"libgnnmp ABI {ver} != expected {ABI_VERSION}; rebuild the library")
+    _LIB = lib
+    return lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status == GNN_OK:
+        return
+    lib = load()
+    msg = lib.gnn_last_error().decode(errors="replace")
+    kind = lib.gnn_status_string(status).decode()
+    exc = _STATUS_EXC.get(status, GnnmpError)
+    raise exc(f"libgnnmp {what or 'call'} failed ({kind}): {msg}")
+
+
+def stream_handle(device: torch.device | None = None) -> int:
+    """The caller's current HIP stream (torch.cuda.current_stream), as a raw pointer."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def call(name: str, *args) -> None:
+    lib = load()
+    check(getattr(lib, name)(*args), name)

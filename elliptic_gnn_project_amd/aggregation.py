@@ -1,0 +1,236 @@
+"""Autograd ops over libgnnmp's aggregation kernels (no torch fallback).
+
+Each op mirrors one PyG 2.5.3 propagate pattern used by src/models/gnn.py:
+  mean_aggregate  — SAGEConv aggr='mean'   (gnn.py:41-44 construct, :49,52,187,193 call)
+  gcn_aggregate   — GCNConv norm + 'add'   (gnn.py:20-23, :28,31)
+  gat_attention   — GATConv softmax + 'add' (gnn.py:64-67, :72,75)
+Forward and backward both run as atomic-free segmented reductions (CSR rows for
+forward, CSC columns for the transposed backward), so results are bitwise
+reproducible run to run.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .graph import GraphPlan, get_plan
+
+__all__ = ["mean_aggregate", "gcn_aggregate", "gat_attention", "aggregate", "colsum", "KernelTimer"]
+
+
+class KernelTimer:
+    """Optional HIP-event bracketing of individual libgnnmp launches (bench.py roofline).
+
+    When ``KernelTimer.active`` is set, each aggregation launch records a pair of
+    torch.cuda.Events on the stream it launches on (torch's current stream), tagged
+    (mode, transpose, F).  Off by default: zero overhead on the normal path.
+    """
+
+    active = False
+    records: list = []
+
+    @classmethod
+    def start(cls):
+        cls.records = []
+        cls.active = True
+
+    @classmethod
+    def stop(cls):
+        cls.active = False
+        torch.cuda.synchronize()
+        out = {}
+        for tag, a, b, nbytes in cls.records:
+            ms = a.elapsed_time(b)
+            d = out.setdefault(tag, {"launches": 0, "ms": 0.0, "bytes": 0})
+            d["launches"] += 1
+            d["ms"] += ms
+            d["bytes"] += nbytes
+        cls.records = []
+        return out
+
+_custom_fwd = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+_custom_bwd = torch.amp.custom_bwd(device_type="cuda")
+
+
+def _as_f32_rows(x: torch.Tensor) -> torch.Tensor:
+    if x.dtype != torch.float32:
+        raise TypeError(f"libgnnmp fp32 path got {x.dtype}")
+    if x.dim() != 2:
+        raise ValueError(f"expected [N, F] features, got {tuple(x.shape)}")
+    if x.stride(1) != 1 or x.stride(0) < x.size(1):
+        x = x.contiguous()
+    return x
+
+
+def _ld(x: torch.Tensor) -> int:
+    return max(int(x.stride(0)), int(x.size(1)), 1)
+
+
+def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = False,
+              nodew: torch.Tensor | None = None, ew: torch.Tensor | None = None, heads: int = 1,
+              addend: torch.Tensor | None = None, bias: torch.Tensor | None = None,
+              relu: bool = False, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Raw call of gnn_aggregate_f32 (no autograd)."""
+    x = _as_f32_rows(x)
+    N, F = plan.num_nodes, x.size(1)
+    if x.size(0) != N:
+        raise ValueError(f"feature rows {x.size(0)} != plan nodes {N}")
+    if out is None:
+        out = torch.empty((N, F), dtype=torch.float32, device=x.device)
+    if addend is not None:
+        addend = _as_f32_rows(addend)
+    p = _lib.GnnAggParams(
+        mode, int(transpose), _lib.ptr(nodew), _lib.ptr(ew), int(heads),
+        _lib.ptr(addend), _ld(addend) if addend is not None else 0,
+        _lib.ptr(bias), int(relu),
+    )
+    if KernelTimer.active:
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+    _lib.call("gnn_aggregate_f32", plan.c_graph, p, x.data_ptr(), _ld(x), F, out.data_ptr(), _ld(out),
+              _lib.stream_handle(x.device))
+    if KernelTimer.active:
+        b.record()
+        KernelTimer.records.append(((int(mode), bool(transpose), int(F)), a, b,
+                                    agg_bytes(plan, F, mode, transpose, addend is not None)))
+    return out
+
+
+def agg_bytes(plan: GraphPlan, F: int, mode: int, transpose: bool, has_addend: bool) -> int:
+    """Algorithmic HBM bytes of one aggregation launch (fp32, int32 plan).
+
+    rowptr/colptr 4(N+1) + neighbour ids 4S + one F-row gather per slot 4·S·F + output
+    4·N·F, plus the per-node weights read (4N; per slot for MEAN_BWD/GCN) and the fused
+    root addend 4·N·F when present.  (SURVEY §8d per-edge model.)
+    """
+    N, S = plan.num_nodes, plan.num_slots
+    b = 4 * (N + 1) + 4 * S + 4 * S * F + 4 * N * F
+    if mode in (_lib.AGG_MEAN,):
+        b += 4 * N
+    elif mode in (_lib.AGG_MEAN_BWD, _lib.AGG_GCN):
+        b += 4 * S
+    if has_addend:
+        b += 4 * N * F
+    return b
+
+
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    """Deterministic column sum (bias gradients) via gnn_colsum_f32."""
+    x = _as_f32_rows(x)
+    rows, F = x.shape
+    out = torch.empty(F, dtype=torch.float32, device=x.device)
+    nb = _lib.c_size(0)
+    _lib.call("gnn_colsum_workspace_size", rows, F, nb)
+    ws = torch.empty(max(int(nb.value) // 4, 1), dtype=torch.float32, device=x.device)
+    _lib.call("gnn_colsum_f32", rows, F, x.data_ptr(), _ld(x), out.data_ptr(), ws.data_ptr(),
+              ws.numel() * 4, _lib.stream_handle(x.device))
+    return out
+
+
+# --------------------------------------------------------------------------- SAGE mean
+class _MeanAggregate(torch.autograd.Function):
+    @staticmethod
+    @_custom_fwd
+    def forward(ctx, x, plan: GraphPlan):
+        ctx.plan = plan
+        return aggregate(plan, x, _lib.AGG_MEAN, nodew=plan.deg)
+
+    @staticmethod
+    @_custom_bwd
+    def backward(ctx, dy):
+        plan = ctx.plan
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = aggregate(plan, dy, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg)
+        return dx, None
+
+
+def mean_aggregate(x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+    """PyG ``scatter(x[ei[0]], ei[1], reduce='mean')`` over x's N rows."""
+    plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
+    return _MeanAggregate.apply(x, plan)
+
+
+# --------------------------------------------------------------------------- GCN
+class _GCNAggregate(torch.autograd.Function):
+    @staticmethod
+    @_custom_fwd
+    def forward(ctx, y, plan: GraphPlan, bias):
+        ctx.plan = plan
+        ctx.has_bias = bias is not None
+        return aggregate(plan, y, _lib.AGG_GCN, nodew=plan.dinv, bias=bias)
+
+    @staticmethod
+    @_custom_bwd
+    def backward(ctx, dout):
+        plan = ctx.plan
+        dy = aggregate(plan, dout, _lib.AGG_GCN, transpose=True, nodew=plan.dinv) \
+            if ctx.needs_input_grad[0] else None
+        db = colsum(dout) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return dy, None, db
+
+
+def gcn_aggregate(y: torch.Tensor, edge_index: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """PyG GCNConv propagate (gcn_norm with self loops, 'add') of transformed features y, + bias."""
+    plan = get_plan(edge_index, y.size(0), _lib.LOOPS_REPLACE)
+    return _GCNAggregate.apply(y, plan, bias)
+
+
+# --------------------------------------------------------------------------- GAT
+class _GATAttention(torch.autograd.Function):
+    @staticmethod
+    @_custom_fwd
+    def forward(ctx, xh, att_src, att_dst, bias, plan: GraphPlan, heads: int, chans: int, concat: bool,
+                slope: float):
+        xh = _as_f32_rows(xh)
+        N = plan.num_nodes
+        dev = xh.device
+        att_src = att_src.contiguous().float()
+        att_dst = att_dst.contiguous().float()
+        stream = _lib.stream_handle(dev)
+        a_src = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        a_dst = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        _lib.call("gnn_gat_scores_f32", N, heads, chans, xh.data_ptr(), _ld(xh), att_src.data_ptr(),
+                  att_dst.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), stream)
+        alpha = torch.empty((max(plan.num_slots, 1), heads), dtype=torch.float32, device=dev)
+        fo = heads * chans if concat else chans
+        out = torch.empty((N, fo), dtype=torch.float32, device=dev)
+        b = bias.contiguous().float() if bias is not None else None
+        _lib.call("gnn_gat_fwd_f32", plan.c_graph, heads, chans, int(concat), float(slope), xh.data_ptr(),
+                  _ld(xh), a_src.data_ptr(), a_dst.data_ptr(), _lib.ptr(b), alpha.data_ptr(), out.data_ptr(),
+                  _ld(out), stream)
+        ctx.save_for_backward(xh, att_src, att_dst, a_src, a_dst, alpha)
+        ctx.meta = (plan, heads, chans, bool(concat), float(slope), bias is not None)
+        return out
+
+    @staticmethod
+    @_custom_bwd
+    def backward(ctx, dout):
+        xh, att_src, att_dst, a_src, a_dst, alpha = ctx.saved_tensors
+        plan, heads, chans, concat, slope, has_bias = ctx.meta
+        dout = _as_f32_rows(dout)
+        dev = xh.device
+        N = plan.num_nodes
+        F = heads * chans
+        dxh = torch.empty((N, F), dtype=torch.float32, device=dev)
+        datt_s = torch.empty(F, dtype=torch.float32, device=dev)
+        datt_d = torch.empty(F, dtype=torch.float32, device=dev)
+        nb = _lib.c_size(0)
+        _lib.call("gnn_gat_bwd_workspace_size", N, plan.num_slots, heads, chans, nb)
+        ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+        _lib.call("gnn_gat_bwd_f32", plan.c_graph, heads, chans, int(concat), slope, xh.data_ptr(), _ld(xh),
+                  a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
+                  dout.data_ptr(), _ld(dout), dxh.data_ptr(), _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(),
+                  ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+        db = colsum(dout) if has_bias and ctx.needs_input_grad[3] else None
+        return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db, None, None, None, None, None)
+
+
+def gat_attention(xh: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor, bias: torch.Tensor | None,
+                  edge_index: torch.Tensor, heads: int, chans: int, concat: bool = True,
+                  negative_slope: float = 0.2) -> torch.Tensor:
+    """PyG GATConv after ``lin``: scores, self-loop replacement, edge softmax, aggregation, bias."""
+    plan = get_plan(edge_index, xh.size(0), _lib.LOOPS_REPLACE)
+    return _GATAttention.apply(xh, att_src, att_dst, bias, plan, int(heads), int(chans), bool(concat),
+                               float(negative_slope))

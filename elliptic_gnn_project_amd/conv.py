@@ -1,0 +1,186 @@
+"""Drop-in replacements for ``torch_geometric.nn.{SAGEConv, GCNConv, GATConv}`` (PyG 2.5.3).
+
+The reference imports these at src/models/gnn.py:8 and constructs them at
+gnn.py:20-23 (GCN), :41-44 and :125-128 (SAGE), :64-67 (GAT).  Constructor arguments,
+parameter names (hence ``state_dict`` keys, a compatibility contract with
+best.ckpt consumers such as src/analysis/hub_ablation.py:88-98) and the
+``forward(x, edge_index)`` signature are PyG's; the neighbour aggregation runs in
+libgnnmp's HIP kernels and the dense transforms in MFMA GEMMs (hipBLASLt).
+
+Only PyG's defaults used by the reference are implemented (SAGE: aggr='mean',
+normalize=False, root_weight=True, project=False; GCN: improved=False,
+cached=False, add_self_loops=True, normalize=True; GAT: dropout=0, edge_dim=None,
+add_self_loops=True, fill_value='mean').  Anything else raises.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .aggregation import colsum, gat_attention, gcn_aggregate, mean_aggregate, aggregate
+from .graph import GraphPlan, get_plan
+
+__all__ = ["SAGEConv", "GCNConv", "GATConv"]
+
+
+def _glorot_(t: torch.Tensor) -> None:
+    # torch_geometric.nn.inits.glorot
+    stdv = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))
+    with torch.no_grad():
+        t.uniform_(-stdv, stdv)
+
+
+class _MeanAggRootBias(torch.autograd.Function):
+    """out = mean_{j->i} y[j, :Fo] + y[i, Fo:] + b  (K1 with the root term and bias fused in its epilogue).
+
+    ``y`` is the single GEMM output x·[W_l; W_r]ᵀ; its gradient is assembled in place
+    (transposed mean into the left half, dout into the right half) — no slice copies.
+    """
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, y, bias, plan: GraphPlan, fo: int):
+        ctx.plan = plan
+        ctx.fo = fo
+        ctx.has_bias = bias is not None
+        return aggregate(plan, y[:, :fo], _lib.AGG_MEAN, nodew=plan.deg, addend=y[:, fo:], bias=bias)
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dout):
+        plan, fo = ctx.plan, ctx.fo
+        dout = dout.contiguous()
+        dy = None
+        if ctx.needs_input_grad[0]:
+            dy = torch.empty((dout.size(0), 2 * fo), dtype=torch.float32, device=dout.device)
+            aggregate(plan, dout, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dy[:, :fo])
+            dy[:, fo:].copy_(dout)
+        db = colsum(dout) if ctx.has_bias and ctx.needs_input_grad[1] else None
+        return dy, db, None, None
+
+
+class SAGEConv(nn.Module):
+    """GraphSAGE ``out_i = W_l · mean_{j->i} x_j + b_l + W_r · x_i`` (PyG SAGEConv, aggr='mean').
+
+    ``order`` picks where ``lin_l`` runs relative to the (linear) mean:
+      'aggregate_first' — PyG's own order (aggregate width F_in);
+      'transform_first' — one GEMM x·[W_l;W_r]ᵀ, then the mean over F_out columns with
+                           the root term and bias fused into the aggregation epilogue;
+      'auto'            — transform first when out_channels < in_channels.
+    Both are the same linear map; results agree to fp32 rounding (tests: 1e-5).
+    """
+
+    def __init__(self, in_channels: int, out_channels: int, aggr: str = "mean", normalize: bool = False,
+                 root_weight: bool = True, project: bool = False, bias: bool = True, order: str = "auto",
+                 **kwargs):
+        super().__init__()
+        if aggr != "mean" or normalize or not root_weight or project or kwargs:
+            raise NotImplementedError("only SAGEConv(aggr='mean', normalize=False, root_weight=True, "
+                                      "project=False) — the configuration src/models/gnn.py uses")
+        if order not in ("auto", "aggregate_first", "transform_first"):
+            raise ValueError(f"unknown order {order!r}")
+        self.in_channels = int(in_channels)
+        self.out_channels = int(out_channels)
+        self.aggr = aggr
+        self.order = order
+        self.lin_l = nn.Linear(self.in_channels, self.out_channels, bias=bias)
+        self.lin_r = nn.Linear(self.in_channels, self.out_channels, bias=False)
+
+    def reset_parameters(self) -> None:
+        self.lin_l.reset_parameters()
+        self.lin_r.reset_parameters()
+
+    def _transform_first(self) -> bool:
+        if self.order == "auto":
+            return self.out_channels < self.in_channels
+        return self.order == "transform_first"
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        if self._transform_first():
+            fo = self.out_channels
+            w = torch.cat([self.lin_l.weight, self.lin_r.weight], dim=0)
+            y = F.linear(x, w)  # [N, 2*F_out]: MFMA GEMM
+            plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
+            return _MeanAggRootBias.apply(y, self.lin_l.bias, plan, fo)
+        agg = mean_aggregate(x, edge_index)
+        return self.lin_l(agg) + self.lin_r(x)
+
+    def __repr__(self) -> str:
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, aggr={self.aggr})"
+
+
+class GCNConv(nn.Module):
+    """GCN ``out_i = sum_{j->i, incl. self loop} dinv_j dinv_i (W x_j) + b`` (PyG GCNConv defaults)."""
+
+    def __init__(self, in_channels: int, out_channels: int, improved: bool = False, cached: bool = False,
+                 add_self_loops: bool = True, normalize: bool = True, bias: bool = True, **kwargs):
+        super().__init__()
+        if improved or not add_self_loops or not normalize or kwargs:
+            raise NotImplementedError("only GCNConv(improved=False, add_self_loops=True, normalize=True)")
+        self.in_channels = int(in_channels)
+        self.out_channels = int(out_channels)
+        self.cached = cached  # plans are cached per edge_index regardless
+        self.lin = nn.Linear(self.in_channels, self.out_channels, bias=False)
+        self.bias = nn.Parameter(torch.empty(self.out_channels)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        _glorot_(self.lin.weight)
+        if self.bias is not None:
+            nn.init.zeros_(self.bias)
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        y = self.lin(x)  # transform first (PyG order): aggregation width = out_channels
+        return gcn_aggregate(y, edge_index, self.bias)
+
+    def __repr__(self) -> str:
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"
+
+
+class GATConv(nn.Module):
+    """GAT (PyG GATConv, v1 attention) with ``heads`` heads of ``out_channels`` each."""
+
+    def __init__(self, in_channels: int, out_channels: int, heads: int = 1, concat: bool = True,
+                 negative_slope: float = 0.2, dropout: float = 0.0, add_self_loops: bool = True,
+                 edge_dim=None, fill_value="mean", bias: bool = True, **kwargs):
+        super().__init__()
+        if dropout != 0.0 or not add_self_loops or edge_dim is not None or kwargs:
+            raise NotImplementedError("only GATConv(dropout=0, add_self_loops=True, edge_dim=None)")
+        self.in_channels = int(in_channels)
+        self.out_channels = int(out_channels)
+        self.heads = int(heads)
+        self.concat = bool(concat)
+        self.negative_slope = float(negative_slope)
+        self.lin = nn.Linear(self.in_channels, self.heads * self.out_channels, bias=False)
+        self.att_src = nn.Parameter(torch.empty(1, self.heads, self.out_channels))
+        self.att_dst = nn.Parameter(torch.empty(1, self.heads, self.out_channels))
+        nb = self.heads * self.out_channels if self.concat else self.out_channels
+        self.bias = nn.Parameter(torch.empty(nb)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        _glorot_(self.lin.weight)
+        _glorot_(self.att_src)
+        _glorot_(self.att_dst)
+        if self.bias is not None:
+            nn.init.zeros_(self.bias)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        # PyG < 2.5 stored the shared projection as lin_src (== lin_dst): accept both spellings.
+        old = prefix + "lin_src.weight"
+        if old in state_dict and prefix + "lin.weight" not in state_dict:
+            state_dict[prefix + "lin.weight"] = state_dict.pop(old)
+            state_dict.pop(prefix + "lin_dst.weight", None)
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        xh = self.lin(x)  # [N, H*C]
+        return gat_attention(xh, self.att_src, self.att_dst, self.bias, edge_index, self.heads,
+                             self.out_channels, self.concat, self.negative_slope)
+
+    def __repr__(self) -> str:
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads})"

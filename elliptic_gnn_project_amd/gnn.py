@@ -1,0 +1,143 @@
+"""The four GNN families of the reference (src/models/gnn.py), on libgnnmp convs.
+
+Same constructor signatures, ``forward(x, edge_index, t_idx=None)``, attribute names
+(``convs``, ``bns``, ``res_projs``, ``time_emb``, ``time_embed_dim``) and hence the same
+``state_dict`` keys as the reference, so ``best.ckpt`` files and the reference's
+train/eval callers (src/train_gnn.py:67-104, src/analysis/*) work unchanged.
+
+  GCNNet        gnn.py:14-32   GCNConv stack, ReLU + dropout between layers
+  SAGENet       gnn.py:35-53   SAGEConv stack, ReLU + dropout between layers
+  GATNet        gnn.py:56-76   GATConv(heads, concat) stack, ELU + dropout; last layer 1 head, mean
+  SAGEResBNNet  gnn.py:82-194  time embedding + SAGEConv + BatchNorm + ReLU + dropout + residual
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .conv import GATConv, GCNConv, SAGEConv
+
+__all__ = ["GCNNet", "SAGENet", "GATNet", "SAGEResBNNet"]
+
+
+class _StackedConvNet(nn.Module):
+    """conv -> act -> dropout for every layer but the last; the last conv gives logits."""
+
+    act: Callable[[torch.Tensor], torch.Tensor] = staticmethod(F.relu)
+
+    def __init__(self, convs, dropout: float):
+        super().__init__()
+        if len(convs) < 2:
+            raise AssertionError("layers must be >= 2")  # reference: assert layers >= 2
+        self.dropout = dropout
+        self.convs = nn.ModuleList(convs)
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor, t_idx: Optional[torch.Tensor] = None):
+        *hidden, last = self.convs
+        h = x
+        for conv in hidden:
+            h = F.dropout(self.act(conv(h, edge_index)), p=self.dropout, training=self.training)
+        return last(h, edge_index)
+
+
+def _widths(in_dim: int, hidden_dim: int, layers: int, num_classes: int):
+    if layers < 2:
+        raise AssertionError("layers must be >= 2")
+    ins = [in_dim] + [hidden_dim] * (layers - 1)
+    outs = [hidden_dim] * (layers - 1) + [num_classes]
+    return list(zip(ins, outs))
+
+
+class GCNNet(_StackedConvNet):
+    def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2):
+        super().__init__([GCNConv(a, b) for a, b in _widths(in_dim, hidden_dim, layers, num_classes)], dropout)
+
+
+class SAGENet(_StackedConvNet):
+    def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2):
+        super().__init__([SAGEConv(a, b) for a, b in _widths(in_dim, hidden_dim, layers, num_classes)], dropout)
+
+
+class GATNet(_StackedConvNet):
+    act = staticmethod(F.elu)
+
+    def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2, heads=4):
+        per_head = hidden_dim // heads  # reference: hidden_dim // heads channels per head
+        convs = [GATConv(in_dim if i == 0 else hidden_dim, per_head, heads=heads) for i in range(layers - 1)]
+        convs.append(GATConv(hidden_dim, num_classes, heads=1, concat=False))
+        super().__init__(convs, dropout)
+
+
+class SAGEResBNNet(nn.Module):
+    """SAGE + BatchNorm + residual, optional timestep embedding concatenated to the input.
+
+    time_embed_type: 'learned' (nn.Embedding(max_timestep, dim)), 'sin' (fixed sin/cos of
+    2π·k·(t-1)/(T-1), k = 1..dim/2, zero-padded to dim), anything else / dim 0: none.
+    """
+
+    def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2, use_bn=True,
+                 residual=True, time_embed_dim=0, time_embed_type="learned", max_timestep=50):
+        super().__init__()
+        if layers < 2:
+            raise AssertionError("layers must be >= 2")
+        self.dropout = float(dropout)
+        self.use_bn = bool(use_bn)
+        self.residual = bool(residual)  # kept as an attribute; the reference always adds the residual
+        self.time_embed_dim = int(time_embed_dim)
+        self.time_embed_type = str(time_embed_type)
+        self.max_timestep = int(max_timestep)
+        self.time_emb = None
+        if self.time_embed_dim > 0 and self.time_embed_type in ("learned", "sin"):
+            if self.time_embed_type == "learned":
+                self.time_emb = nn.Embedding(self.max_timestep, self.time_embed_dim)
+            in_dim = in_dim + self.time_embed_dim
+        else:
+            self.time_embed_dim, self.time_embed_type = 0, "none"
+
+        dims = _widths(in_dim, hidden_dim, layers, num_classes)
+        self.convs = nn.ModuleList(SAGEConv(a, b) for a, b in dims)
+        self.bns = nn.ModuleList(nn.BatchNorm1d(hidden_dim) for _ in range(layers - 1)) if self.use_bn \
+            else nn.ModuleList()
+        self.res_projs = nn.ModuleList(
+            nn.Identity() if a == b else nn.Linear(a, b, bias=False) for a, b in dims[:-1]
+        )
+
+    def _sinusoid(self, t_idx: torch.Tensor) -> Optional[torch.Tensor]:
+        dim = self.time_embed_dim
+        if dim <= 0:
+            return None
+        t = (t_idx.long() - 1).clamp(0, self.max_timestep - 1).to(torch.float32)
+        t = t / max(float(self.max_timestep - 1), 1.0)
+        half = dim // 2
+        freqs = torch.arange(1, half + 1, device=t.device, dtype=t.dtype) * (2.0 * math.pi)
+        ang = t[:, None] * freqs[None, :]
+        feat = torch.cat([torch.sin(ang), torch.cos(ang)], dim=1)
+        if feat.size(1) < dim:
+            feat = F.pad(feat, (0, dim - feat.size(1)))
+        return feat
+
+    def _inject_time(self, x: torch.Tensor, t_idx: Optional[torch.Tensor]) -> torch.Tensor:
+        if self.time_embed_dim <= 0 or t_idx is None:
+            return x
+        if self.time_embed_type == "learned":
+            te = self.time_emb((t_idx.long() - 1).clamp(0, self.max_timestep - 1))
+        elif self.time_embed_type == "sin":
+            te = self._sinusoid(t_idx)
+        else:
+            return x
+        return torch.cat([x, te], dim=1)
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor, t_idx: Optional[torch.Tensor] = None):
+        h = self._inject_time(x, t_idx)
+        *hidden, last = self.convs
+        for li, conv in enumerate(hidden):
+            z = conv(h, edge_index)
+            if self.use_bn:
+                z = self.bns[li](z)
+            z = F.dropout(F.relu(z), p=self.dropout, training=self.training)
+            h = z + self.res_projs[li](h)
+        return last(h, edge_index)

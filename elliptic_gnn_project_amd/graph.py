@@ -1,0 +1,125 @@
+"""Graph plans: device CSR/CSC of one ``edge_index``, built once and cached on the tensor.
+
+The reference hands the same ``edge_index`` tensor to every conv call of every epoch
+(src/train_gnn.py:320-324 builds it, :387-390 pass it), but eval-time callers pass
+modified ones (hub ablation src/train_gnn.py:526-540, robustness.py:65-82).  A plan
+is therefore keyed on (tensor identity, in-place version, N, loop mode) and stored
+as an attribute of the edge_index tensor itself: it dies with the tensor and is
+rebuilt if the tensor is modified in place (``_version`` bump).
+
+HBM layout of a plan (int32 throughout, N+1 / S entries):
+    rowptr[N+1], col[S], csr_eid[S]       CSR by target (forward gathers)
+    colptr[N+1], row[S], csc2csr[S]       CSC by source (backward gathers)
+    deg[N] f32                             slots per target (mean count / GCN degree)
+    dinv[N] f32                            GCN deg^-1/2 (REPLACE plans only)
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_ATTR = "_gnnmp_plans"
+
+
+class GraphPlan:
+    """Stable CSR (by target) + CSC (by source) of ``edge_index`` on the HIP device."""
+
+    def __init__(self, edge_index: torch.Tensor, num_nodes: int, loops: int):
+        if edge_index.dim() != 2 or edge_index.size(0) != 2:
+            raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+        if edge_index.device.type != "cuda":
+            raise RuntimeError(
+                "elliptic_gnn_project_amd runs on the MI355X (HIP) device only; "
+                f"edge_index is on {edge_index.device}"
+            )
+        dev = edge_index.device
+        N = int(num_nodes)
+        E = int(edge_index.size(1))
+        self.num_nodes = N
+        self.num_edges = E
+        self.loops = loops
+        self.device = dev
+        ei = edge_index.to(torch.int64).contiguous()
+        smax = E + (N if loops == _lib.LOOPS_REPLACE else 0)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.rowptr = torch.empty(N + 1, **i32)
+        self.colptr = torch.empty(N + 1, **i32)
+        self.col = torch.empty(max(smax, 1), **i32)
+        self.csr_eid = torch.empty(max(smax, 1), **i32)
+        self.row = torch.empty(max(smax, 1), **i32)
+        self.csc2csr = torch.empty(max(smax, 1), **i32)
+        stats = torch.zeros(4, **i32)
+        lib = _lib.load()
+        ws_bytes = _lib.c_size(0)
+        _lib.check(lib.gnn_graph_workspace_size(N, E, ws_bytes), "gnn_graph_workspace_size")
+        ws = torch.empty(max(int(ws_bytes.value), 1), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            stream = _lib.stream_handle(dev)
+            _lib.check(
+                lib.gnn_graph_build(
+                    ei.data_ptr(), E, N, loops,
+                    self.rowptr.data_ptr(), self.col.data_ptr(), self.csr_eid.data_ptr(),
+                    self.colptr.data_ptr(), self.row.data_ptr(), self.csc2csr.data_ptr(),
+                    stats.data_ptr(), ws.data_ptr(), ws.numel(), stream,
+                ),
+                "gnn_graph_build",
+            )
+            st = stats.cpu()  # one host sync per plan build (never in the training loop)
+        del ws
+        if int(st[2]) > 0:
+            raise IndexError(
+                f"edge_index holds {int(st[2])} entries outside [0, {N}) "
+                "(PyG would raise in index_select)"
+            )
+        self.num_slots = int(st[0])
+        self.num_input_loops = int(st[1])
+        self.c_graph = _lib.GnnGraph(
+            N, self.num_slots,
+            self.rowptr.data_ptr(), self.col.data_ptr(),
+            self.colptr.data_ptr(), self.row.data_ptr(), self.csc2csr.data_ptr(),
+        )
+        self.deg = torch.empty(max(N, 1), dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            _lib.check(lib.gnn_in_degree_f32(self.c_graph, self.deg.data_ptr(), _lib.stream_handle(dev)),
+                       "gnn_in_degree_f32")
+        self._dinv = None
+
+    @property
+    def dinv(self) -> torch.Tensor:
+        """GCN normalisation deg^-1/2 (PyG gcn_norm); only meaningful on REPLACE plans."""
+        if self._dinv is None:
+            if self.loops != _lib.LOOPS_REPLACE:
+                raise RuntimeError("gcn norm needs a self-loop-replaced plan")
+            d = torch.empty(max(self.num_nodes, 1), dtype=torch.float32, device=self.device)
+            with torch.cuda.device(self.device):
+                _lib.call("gnn_gcn_norm_f32", self.c_graph, d.data_ptr(), _lib.stream_handle(self.device))
+            self._dinv = d
+        return self._dinv
+
+    def csr(self):
+        """(rowptr, col, csr_eid) trimmed to the used slots — for tests / inspection."""
+        S = self.num_slots
+        return self.rowptr, self.col[:S], self.csr_eid[:S]
+
+    def csc(self):
+        S = self.num_slots
+        return self.colptr, self.row[:S], self.csc2csr[:S]
+
+
+def get_plan(edge_index: torch.Tensor, num_nodes: int, loops: int = _lib.LOOPS_KEEP) -> GraphPlan:
+    """Cached plan for (edge_index, N, loop mode); rebuilt when edge_index changes in place."""
+    key = (int(num_nodes), int(loops))
+    version = edge_index._version
+    plans = getattr(edge_index, _ATTR, None)
+    if plans is None or plans.get("version") != version or plans.get("ptr") != edge_index.data_ptr():
+        plans = {"version": version, "ptr": edge_index.data_ptr()}
+        try:
+            setattr(edge_index, _ATTR, plans)
+        except (AttributeError, RuntimeError):  # e.g. inference tensors: no caching
+            pass
+    plan = plans.get(key)
+    if plan is None:
+        plan = GraphPlan(edge_index, num_nodes, loops)
+        plans[key] = plan
+    return plan

@@ -1,0 +1,172 @@
+/*
+ * gnnmp.h — C ABI of the MI355X (gfx950) GNN message-passing library `libgnnmp.so`.
+ *
+ * This is the drop-in boundary for the one hot path of elliptic-gnn-project:
+ * the neighbour aggregation that `torch_geometric.nn.{SAGEConv,GCNConv,GATConv}`
+ * perform inside `src/models/gnn.py` (imported at gnn.py:8, called at
+ * gnn.py:28,31,49,52,72,75,187,193).  PyG 2.5.3 (the CI pin,
+ * .github/workflows/ci.yml:17,39) is not vendored in the reference; every entry
+ * point below names the PyG operation it replaces.
+ *
+ * Conventions
+ *  - All buffers are device pointers owned by the caller.  The library never
+ *    allocates or frees device memory; scratch comes from a caller-provided
+ *    workspace whose size is queried first.
+ *  - Feature matrices are row-major [rows, F] with a leading dimension `ld`
+ *    (elements).  Outputs are fully overwritten (no zero-init contract).
+ *  - Graph arrays are int32 (N, E < 2^31).  `edge_index` is PyG's [2, E] int64
+ *    layout: row 0 = source j, row 1 = target i (flow source_to_target).
+ *  - Every launch goes on the caller's stream; no entry point synchronises the
+ *    host except gnn_graph_build's optional stats read (documented there).
+ *  - Errors: a gnn_status is returned; gnn_last_error() gives a thread-local
+ *    message.  Reductions are atomic-free: results are bitwise reproducible.
+ */
+#ifndef GNNMP_H_
+#define GNNMP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNNMP_ABI_VERSION 1
+
+typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
+
+typedef enum {
+  GNN_OK = 0,
+  GNN_ERR_INVALID_ARG = 1,
+  GNN_ERR_INDEX_OUT_OF_RANGE = 2, /* PyG: IndexError from index_select */
+  GNN_ERR_HIP = 3,
+  GNN_ERR_WORKSPACE = 4,
+  GNN_ERR_UNSUPPORTED = 5
+} gnn_status;
+
+/* Self-loop handling applied while building a graph plan. */
+typedef enum {
+  GNN_LOOPS_KEEP = 0,    /* SAGEConv: edges used exactly as given (duplicates and loops kept) */
+  GNN_LOOPS_REPLACE = 1  /* GCNConv add_remaining_self_loops / GATConv remove_self_loops +
+                            add_self_loops: drop every existing loop, then one loop per node,
+                            placed LAST in its CSR row and CSC column (PyG appends loops). */
+} gnn_loop_mode;
+
+/*
+ * A graph plan: CSR by destination (aggregation, forward) and CSC by source
+ * (transpose, backward), both stable in PyG edge order.
+ */
+typedef struct {
+  int64_t num_nodes;
+  int64_t num_slots;        /* stored edges (after loop handling) */
+  const int32_t* rowptr;    /* [N+1] CSR by target i */
+  const int32_t* col;       /* [S]   source j of each CSR slot */
+  const int32_t* colptr;    /* [N+1] CSC by source j */
+  const int32_t* row;       /* [S]   target i of each CSC slot */
+  const int32_t* csc2csr;   /* [S]   CSR slot holding the same edge as each CSC slot */
+} gnn_graph;
+
+int gnn_abi_version(void);
+const char* gnn_status_string(gnn_status s);
+const char* gnn_last_error(void);
+
+/* ------------------------------------------------------------------------ */
+/* K0  graph plan build  (replaces the implicit per-call index handling of
+ *     MessagePassing.propagate, and remove/add_(remaining_)self_loops)      */
+/* ------------------------------------------------------------------------ */
+gnn_status gnn_graph_workspace_size(int64_t num_nodes, int64_t num_edges, size_t* bytes);
+
+/*
+ * Build a plan from edge_index [2,E] int64 (contiguous).  Output arrays must
+ * hold S_max = E (KEEP) or E + N (REPLACE) slots; rowptr/colptr N+1.
+ * csr_eid[s] = PyG edge id of CSR slot s (original id; loop of node i = E + i).
+ * stats (device int32[4], zeroed by this call): {S, n_input_loops, n_bad_index, 0}.
+ * A non-zero n_bad_index means some index was outside [0, N): the plan is invalid
+ * (PyG raises IndexError); the caller reads stats after the stream completes.
+ */
+gnn_status gnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t num_nodes,
+                           gnn_loop_mode loops, int32_t* rowptr, int32_t* col, int32_t* csr_eid,
+                           int32_t* colptr, int32_t* row, int32_t* csc2csr, int32_t* stats,
+                           void* workspace, size_t workspace_bytes, gnn_stream_t stream);
+
+/* deg[i] = number of CSR slots of i as float (PyG `count` / `deg`, gnn.py:49 via SAGEConv mean). */
+gnn_status gnn_in_degree_f32(const gnn_graph* g, float* deg, gnn_stream_t stream);
+
+/* K3  gcn_norm (PyG torch_geometric.nn.conv.gcn_conv.gcn_norm, improved=False, add_self_loops=True):
+ *     dinv[i] = deg_i^-1/2 (inf -> 0) on a GNN_LOOPS_REPLACE plan.  Edge weight of (j -> i) is
+ *     dinv[j]*dinv[i], formed inside the aggregation kernels.  Replaces GCNConv.forward's norm. */
+gnn_status gnn_gcn_norm_f32(const gnn_graph* g, float* dinv, gnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* K1/K2/K4  segmented aggregation over a plan (atomic-free)                */
+/* ------------------------------------------------------------------------ */
+typedef enum {
+  GNN_AGG_SUM = 0,       /* y_r = sum_k x[nbr_k]                                          */
+  GNN_AGG_MEAN = 1,      /* y_r = (sum_k x[nbr_k]) / max(nodew[r],1)  — SAGEConv aggr='mean' fwd (K1) */
+  GNN_AGG_MEAN_BWD = 2,  /* y_r = sum_k x[nbr_k] / max(nodew[nbr_k],1) — mean backward over CSC (K2)  */
+  GNN_AGG_GCN = 3,       /* y_r = sum_k (nodew[nbr_k]*nodew[r]) * x[nbr_k] — GCNConv propagate (K4)    */
+  GNN_AGG_EDGE_W = 4     /* y_r = sum_k ew[slot_k, head(f)] * x[nbr_k, f] — GAT alpha-weighted (K5/K6) */
+} gnn_agg_mode;
+
+typedef struct {
+  gnn_agg_mode mode;
+  int32_t transpose;      /* 0: iterate CSR rows (targets gather sources); 1: CSC (sources gather targets) */
+  const float* nodew;     /* per-node weights (deg for MEAN*, dinv for GCN) */
+  const float* ew;        /* EDGE_W: per-CSR-slot weights [S, heads] */
+  int32_t heads;          /* EDGE_W: feature f uses head f / (F / heads) */
+  const float* addend;    /* optional [rows, F] added after the aggregation (ld_add) */
+  int64_t ld_add;
+  const float* bias;      /* optional [F] */
+  int32_t relu;           /* apply max(.,0) last */
+} gnn_agg_params;
+
+/* Generic fp32 aggregation: y[r, 0:F] for r in [0, N). */
+gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params* p, const float* x,
+                             int64_t ldx, int64_t F, float* y, int64_t ldy, gnn_stream_t stream);
+
+/* Named forms of the above (what an FFI binding of SAGEConv would call). */
+gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
+                                 int64_t F, float* out, int64_t ldo, gnn_stream_t stream);
+gnn_status gnn_sage_mean_bwd_f32(const gnn_graph* g, const float* deg, const float* dout,
+                                 int64_t ld_dout, int64_t F, float* dx, int64_t ld_dx,
+                                 gnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* K5/K6  GATConv edge softmax + aggregation (PyG GATConv.edge_update/message, utils.softmax) */
+/* ------------------------------------------------------------------------ */
+/* a_src[n,h] = <xh[n,h,:], att_src[h,:]>, a_dst likewise. xh is [N, H*C] (ld_xh). */
+gnn_status gnn_gat_scores_f32(int64_t N, int32_t H, int32_t C, const float* xh, int64_t ld_xh,
+                              const float* att_src, const float* att_dst, float* a_src,
+                              float* a_dst, gnn_stream_t stream);
+
+/* Fused forward over a GNN_LOOPS_REPLACE plan: e = leaky_relu(a_src[j]+a_dst[i], slope);
+ * alpha = exp(e - max_i) / (sum_i exp + 1e-16); out[i] = sum alpha * xh[j]
+ * (concat: [N,H*C]; else head-mean [N,C]) + bias.  alpha saved per CSR slot [S,H]. */
+gnn_status gnn_gat_fwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t concat, float slope,
+                           const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst,
+                           const float* bias, float* alpha, float* out, int64_t ldo,
+                           gnn_stream_t stream);
+
+/* Backward.  dout is [N,H*C] (concat) or [N,C].  Produces dxh [N,H*C] (includes the score
+ * paths through att_src/att_dst), d_att_src/d_att_dst [H*C].  workspace from
+ * gnn_gat_bwd_workspace_size. */
+gnn_status gnn_gat_bwd_workspace_size(int64_t N, int64_t S, int32_t H, int32_t C, size_t* bytes);
+gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t concat, float slope,
+                           const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst,
+                           const float* att_src, const float* att_dst, const float* alpha,
+                           const float* dout, int64_t ld_dout, float* dxh, int64_t ld_dxh,
+                           float* d_att_src, float* d_att_dst, void* workspace,
+                           size_t workspace_bytes, gnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Dense helpers used by the fused conv paths                               */
+/* ------------------------------------------------------------------------ */
+/* out[c] = sum_r x[r, c]  (bias gradients; deterministic two-stage column sum). */
+gnn_status gnn_colsum_workspace_size(int64_t rows, int64_t F, size_t* bytes);
+gnn_status gnn_colsum_f32(int64_t rows, int64_t F, const float* x, int64_t ldx, float* out,
+                          void* workspace, size_t workspace_bytes, gnn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNNMP_H_ */
