@@ -89,6 +89,41 @@ def cpu_baseline(data, state, cw, denom, budget_s: float):
     }
 
 
+MFMA_F32_PEAK_TFS = 157.3  # gfx950 dense fp32 MFMA (= vector fp32) peak, MI355X_MICROARCH.md
+
+
+def roofline(recs):
+    """Dominant libgnnmp kernel (by total HIP-event time) against its roofline.
+
+    Aggregations are HBM-bound: achieved = algorithmic bytes per launch / average duration.
+    MFMA GEMMs are priced in FLOPs against the fp32 MFMA peak.  Also reports every timed
+    kernel's share for the DESIGN.md breakdown.
+    """
+    names = {0: "sum", 1: "mean_fwd", 2: "mean_bwd", 3: "gcn", 4: "edge_w"}
+
+    def label(tag):
+        if tag[0] == "agg":
+            return f"agg[{names[tag[1]]},{'csc' if tag[2] else 'csr'},F={tag[3]}]"
+        return f"{tag[0]}[M={tag[1]},K={tag[2]},N={tag[3]}]"
+
+    tot = sum(r["ms"] for r in recs.values())
+    tag, r = max(recs.items(), key=lambda kv: kv[1]["ms"])
+    avg_ms = r["ms"] / r["launches"]
+    per = r["amount"] / r["launches"]
+    if tag[0] == "agg":
+        ach = per / (avg_ms * 1e-3) / 1e9
+        out = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
+    else:
+        ach = per / (avg_ms * 1e-3) / 1e12
+        out = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+               "frac": round(ach / MFMA_F32_PEAK_TFS, 4), "traffic": None}
+    out.update({"kernel": label(tag), "avg_us": round(avg_ms * 1e3, 2), "per_launch": int(per),
+                "timed_kernels": {label(t): {"us_per_launch": round(v["ms"] / v["launches"] * 1e3, 1),
+                                             "share": round(v["ms"] / tot, 3)} for t, v in recs.items()}})
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,17 +191,7 @@ def main():
         for _ in range(5):
             step()
         recs = KernelTimer.stop()
-        tag, r = max(recs.items(), key=lambda kv: kv[1]["ms"])
-        avg_ms = r["ms"] / r["launches"]
-        bpl = r["bytes"] / r["launches"]
-        achieved = bpl / (avg_ms * 1e-3) / 1e9
-        names = {0: "sum", 1: "mean_fwd", 2: "mean_bwd", 3: "gcn", 4: "edge_w"}
-        roof = {
-            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": f"agg_rowwave[{names[tag[0]]}, {'csc' if tag[1] else 'csr'}, F={tag[2]}]",
-            "avg_us": round(avg_ms * 1e3, 2), "bytes_per_launch": int(bpl),
-        }
+        roof = roofline(recs)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -70,6 +70,34 @@ class GnnAggParams(ctypes.Structure):
     ]
 
 
+class GnnGemmNTParams(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64),
+        ("a1", c_ptr), ("lda1", c_i64), ("k1", c_i64),
+        ("a2", c_ptr), ("lda2", c_i64), ("k2", c_i64),
+        ("bt", c_ptr), ("ldb", c_i64),
+        ("c", c_ptr), ("ldc", c_i64),
+        ("bias", c_ptr),
+        ("relu", c_i32),
+        ("dropout_p", ctypes.c_float),
+        ("seed", ctypes.c_uint64),
+        ("proj", c_ptr), ("nproj", c_i32), ("z", c_ptr), ("ldz", c_i64),
+    ]
+
+
+class GnnGemmTNParams(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i64), ("Nr", c_i64),
+        ("g", c_ptr), ("ldg", c_i64),
+        ("dz", c_ptr), ("lddz", c_i64),
+        ("proj", c_ptr), ("nproj", c_i32),
+        ("h", c_ptr), ("ldh", c_i64), ("hscale", ctypes.c_float),
+        ("gout", c_ptr), ("ldgout", c_i64),
+        ("a1", c_ptr), ("lda1", c_i64), ("k1", c_i64),
+        ("a2", c_ptr), ("lda2", c_i64), ("k2", c_i64),
+    ]
+
+
 # name -> (restype, argtypes).  Mirrors include/gnnmp.h one to one; the CPU test
 # suite checks that every function declared in the header appears here and is exported.
 SIGNATURES = {
@@ -110,6 +138,9 @@ SIGNATURES = {
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
          c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
+    "gnn_gemm_nt_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),
+    "gnn_gemm_tn_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32, ctypes.POINTER(c_size)]),
+    "gnn_gemm_tn_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams), c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_colsum_workspace_size": (ctypes.c_int, [c_i64, c_i64, ctypes.POINTER(c_size)]),
     "gnn_colsum_f32": (ctypes.c_int, [c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
 }

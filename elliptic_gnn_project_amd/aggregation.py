@@ -23,7 +23,8 @@ class KernelTimer:
 
     When ``KernelTimer.active`` is set, each aggregation launch records a pair of
     torch.cuda.Events on the stream it launches on (torch's current stream), tagged
-    (mode, transpose, F).  Off by default: zero overhead on the normal path.
+    ("agg", mode, transpose, F) with its algorithmic bytes, or ("gemm_nt"/"gemm_tn", M, K, N)
+    with its FLOPs.  Off by default: zero overhead on the normal path.
     """
 
     active = False
@@ -39,12 +40,12 @@ class KernelTimer:
         cls.active = False
         torch.cuda.synchronize()
         out = {}
-        for tag, a, b, nbytes in cls.records:
+        for tag, a, b, amount in cls.records:
             ms = a.elapsed_time(b)
-            d = out.setdefault(tag, {"launches": 0, "ms": 0.0, "bytes": 0})
+            d = out.setdefault(tag, {"launches": 0, "ms": 0.0, "amount": 0})
             d["launches"] += 1
             d["ms"] += ms
-            d["bytes"] += nbytes
+            d["amount"] += amount
         cls.records = []
         return out
 
@@ -92,7 +93,7 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
               _lib.stream_handle(x.device))
     if KernelTimer.active:
         b.record()
-        KernelTimer.records.append(((int(mode), bool(transpose), int(F)), a, b,
+        KernelTimer.records.append((("agg", int(mode), bool(transpose), int(F)), a, b,
                                     agg_bytes(plan, F, mode, transpose, addend is not None)))
     return out
 

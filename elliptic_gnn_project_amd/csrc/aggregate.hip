@@ -155,18 +155,21 @@ __global__ __launch_bounds__(256) void agg_rowwave_kernel(AggArgs a) {
   }
 }
 
-// One lane per row for narrow features (F <= 8).
+// Narrow rows (F <= 8, e.g. 2-class logits): a group of 8 lanes per row, lanes over the
+// row's slots (hubs are shared by 8 lanes), then a 3-step xor-shuffle reduction.
+constexpr int kGroup = 8;
 template <int MODE>
-__global__ __launch_bounds__(256) void agg_rowlane_kernel(AggArgs a) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < a.nrows;
-       r += (int64_t)gridDim.x * blockDim.x) {
+__global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
+  const int sub = threadIdx.x & (kGroup - 1);
+  for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kGroup; r < a.nrows;
+       r += (int64_t)gridDim.x * blockDim.x / kGroup) {
     const int32_t beg = a.ptr[r];
     const int32_t end = a.ptr[r + 1];
     float acc[8];
 #pragma unroll
     for (int f = 0; f < 8; ++f) acc[f] = 0.0f;
-    for (int32_t k = beg; k < end; ++k) {
-      int32_t n = a.nbr[k];
+    for (int32_t k = beg + sub; k < end; k += kGroup) {
+      const int32_t n = a.nbr[k];
       const float* xr = a.x + (int64_t)n * a.ldx;
 #pragma unroll
       for (int f = 0; f < 8; ++f) {
@@ -180,9 +183,18 @@ __global__ __launch_bounds__(256) void agg_rowlane_kernel(AggArgs a) {
 #pragma unroll
     for (int f = 0; f < 8; ++f) {
       if (f < a.F) {
-        float t[1] = {acc[f]};
-        finish<MODE, 1>(a, r, f, t);
-        a.y[r * a.ldy + f] = t[0];
+#pragma unroll
+        for (int off = kGroup / 2; off >= 1; off >>= 1) acc[f] += __shfl_xor(acc[f], off);
+      }
+    }
+    if (sub == 0) {
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        if (f < a.F) {
+          float t[1] = {acc[f]};
+          finish<MODE, 1>(a, r, f, t);
+          a.y[r * a.ldy + f] = t[0];
+        }
       }
     }
   }
@@ -194,9 +206,9 @@ template <int MODE>
 gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st) {
   if (a.nrows == 0 || a.F == 0) return GNN_OK;
   if (a.F <= 8) {
-    int64_t blocks = ceil_div(a.nrows, 256);
-    if (blocks > 65536) blocks = 65536;
-    agg_rowlane_kernel<MODE><<<(unsigned)blocks, 256, 0, st>>>(a);
+    int64_t blocks = ceil_div(a.nrows * kGroup, 256);
+    if (blocks > ((int64_t)1 << 20)) blocks = (int64_t)1 << 20;
+    agg_group_kernel<MODE><<<(unsigned)blocks, 256, 0, st>>>(a);
   } else {
     int64_t blocks = ceil_div(a.nrows, 4);
     if (blocks > (int64_t)1 << 20) blocks = (int64_t)1 << 20;
@@ -208,16 +220,31 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------ colsum
+// Stage 1: block b sums rows [b*rpb, (b+1)*rpb); threads form (row lanes x columns) so that
+// narrow F still uses the whole block; row-lane partials are combined in LDS in fixed order.
 __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t rows, int32_t F, const float* __restrict__ x,
                                                              int64_t ldx, int64_t rows_per_blk,
                                                              float* __restrict__ part) {
-  // block b sums rows [b*rows_per_blk, ...) for columns handled by threads (strided)
-  int64_t r0 = blockIdx.x * rows_per_blk;
-  int64_t r1 = r0 + rows_per_blk < rows ? r0 + rows_per_blk : rows;
-  for (int c = threadIdx.x; c < F; c += blockDim.x) {
+  __shared__ float red[256];
+  const int cols = F < 256 ? F : 256;
+  const int lanes = 256 / cols;  // row lanes per column
+  const int c_local = threadIdx.x % cols;
+  const int rl = threadIdx.x / cols;
+  const int64_t r0 = blockIdx.x * rows_per_blk;
+  const int64_t r1 = r0 + rows_per_blk < rows ? r0 + rows_per_blk : rows;
+  for (int cb = 0; cb < F; cb += cols) {
+    const int c = cb + c_local;
     float acc = 0.0f;
-    for (int64_t r = r0; r < r1; ++r) acc += x[r * ldx + c];
-    part[(int64_t)blockIdx.x * F + c] = acc;
+    if (rl < lanes && c < F)
+      for (int64_t r = r0 + rl; r < r1; r += lanes) acc += x[r * ldx + c];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x < cols && cb + (int)threadIdx.x < F) {
+      float s = 0.0f;
+      for (int l = 0; l < lanes; ++l) s += red[l * cols + threadIdx.x];
+      part[(int64_t)blockIdx.x * F + cb + threadIdx.x] = s;
+    }
+    __syncthreads();
   }
 }
 
@@ -230,7 +257,7 @@ __global__ void colsum_final_kernel(int32_t F, int32_t nblk, const float* __rest
   out[c] = acc;
 }
 
-constexpr int64_t kColsumBlocks = 1024;
+constexpr int64_t kColsumBlocks = 256;
 
 }  // namespace
 }  // namespace gnnmp
@@ -326,7 +353,7 @@ extern "C" gnn_status gnn_colsum_f32(int64_t rows, int64_t F, const float* x, in
   float* part = static_cast<float*>(workspace);
   colsum_partial_kernel<<<(unsigned)nblk, 256, 0, st>>>(rows, (int32_t)F, x, ldx, rpb, part);
   GNN_LAUNCH_CHECK();
-  colsum_final_kernel<<<(unsigned)ceil_div(F, 256), 256, 0, st>>>((int32_t)F, (int32_t)nblk, part, out);
+  colsum_final_kernel<<<(unsigned)ceil_div(F, 64), 64, 0, st>>>((int32_t)F, (int32_t)nblk, part, out);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }

@@ -1,0 +1,205 @@
+"""Fused SAGENet: the whole L-layer GraphSAGE forward/backward of src/models/gnn.py:35-53 as
+one autograd node over libgnnmp kernels (aggregate-first, PyG's own order).
+
+Forward, per hidden layer l (h_0 = x):
+    agg_l     = mean_{j->i} h_l[j]                                   K1  (CSR gather)
+    h_{l+1}   = dropout(relu([agg_l | h_l] · [W_l; W_r]ᵀ + b))      K7 NT (fused epilogue)
+  the last hidden layer's epilogue also projects onto the narrow output layer
+    z         = h_{L-1} · [W_l; W_r]_{L-1}ᵀ                          (registers -> [N, 2C])
+    logits    = mean_{j->i} z[j, :C] + z[i, C:] + b_{L-1}            K1 narrow (8 lanes/row)
+Backward:
+    dz        = [meanᵀ(dlogits) | dlogits]                           K2 narrow (CSC)
+    dW, db    = Gᵀ · [agg | h] with G = (dz · P) ⊙ relu'/dropout     K7 TN (G never stored)
+    (deeper layers: dh = meanᵀ(G·W_l) + G·W_r via K7 NT + K2, then TN again)
+Saved for backward: agg_l and h_l (the ReLU+dropout mask is h_{l+1} > 0), nothing else.
+
+The dropout mask is a counter hash of (seed, element index) — oracle/dropout_hash.py
+reproduces it bit for bit — so train-mode parity tests compare against the CPU oracle with
+the very same mask.  ``F.dropout`` semantics are kept: keep with probability 1-p, scale
+kept values by 1/(1-p).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from . import _lib
+from .aggregation import KernelTimer, aggregate, agg_bytes
+from .graph import GraphPlan, get_plan
+
+MAX_PROJ = 4  # nproj = 2 * num_classes <= 4
+
+
+def _ld(t: torch.Tensor) -> int:
+    return max(int(t.stride(0)), int(t.size(1)), 1)
+
+
+def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
+            out=None, want_c=True):
+    """C = epilogue([a1 | a2] · bt) on the MFMA NT kernel."""
+    M = a1.size(0)
+    if out is None and want_c:
+        out = torch.empty((M, n), dtype=torch.float32, device=a1.device)
+    p = _lib.GnnGemmNTParams(
+        M, n,
+        a1.data_ptr(), _ld(a1), a1.size(1),
+        _lib.ptr(a2), _ld(a2) if a2 is not None else 0, a2.size(1) if a2 is not None else 0,
+        bt.data_ptr(), _ld(bt),
+        _lib.ptr(out), _ld(out) if out is not None else 0,
+        _lib.ptr(bias), int(relu), float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF,
+        _lib.ptr(proj), proj.size(0) if proj is not None else 0, _lib.ptr(z), _ld(z) if z is not None else 0,
+    )
+    if KernelTimer.active:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("gnn_gemm_nt_f32", p, _lib.stream_handle(a1.device))
+    if KernelTimer.active:
+        e1.record()
+        k = a1.size(1) + (a2.size(1) if a2 is not None else 0)
+        KernelTimer.records.append((("gemm_nt", M, k, n), e0, e1, 2 * M * k * n))
+    return out
+
+
+def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gout=None):
+    """dW | db | dW2 | dzsum  (one flat fp32 buffer) = Gᵀ·[a1 | a2] on the MFMA TN kernel."""
+    M = a1.size(0)
+    k1 = a1.size(1)
+    k2 = a2.size(1) if a2 is not None else 0
+    nproj = proj.size(0) if dz is not None else 0
+    n_out = nr * (k1 + k2) + nr + nproj * nr + nproj
+    out = torch.empty(n_out, dtype=torch.float32, device=a1.device)
+    nb = _lib.c_size(0)
+    _lib.call("gnn_gemm_tn_workspace_size", M, nr, k1 + k2, nproj, nb)
+    ws = torch.empty(max(int(nb.value) // 4, 1), dtype=torch.float32, device=a1.device)
+    p = _lib.GnnGemmTNParams(
+        M, nr,
+        _lib.ptr(g), _ld(g) if g is not None else 0,
+        _lib.ptr(dz), _ld(dz) if dz is not None else 0,
+        _lib.ptr(proj), nproj,
+        _lib.ptr(h), _ld(h) if h is not None else 0, float(hscale),
+        _lib.ptr(gout), _ld(gout) if gout is not None else 0,
+        a1.data_ptr(), _ld(a1), k1,
+        _lib.ptr(a2), _ld(a2) if a2 is not None else 0, k2,
+    )
+    if KernelTimer.active:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+    _lib.call("gnn_gemm_tn_f32", p, out.data_ptr(), ws.data_ptr(), ws.numel() * 4, _lib.stream_handle(a1.device))
+    if KernelTimer.active:
+        e1.record()
+        KernelTimer.records.append((("gemm_tn", M, k1 + k2, nr), e0, e1, 2 * M * (k1 + k2) * nr))
+    o = 0
+    dW = out[o: o + nr * (k1 + k2)].view(nr, k1 + k2)
+    o += nr * (k1 + k2)
+    db = out[o: o + nr]
+    o += nr
+    dW2 = out[o: o + nproj * nr].view(nproj, nr) if nproj else None
+    o += nproj * nr
+    dzs = out[o: o + nproj] if nproj else None
+    return dW, db, dW2, dzs
+
+
+class _FusedSAGE(torch.autograd.Function):
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x, plan: GraphPlan, dropout_p: float, seeds: List[int], *params):
+        L = len(params) // 3
+        Wl = params[0::3]
+        bl = params[1::3]
+        Wr = params[2::3]
+        x = x.contiguous()
+        C = Wl[-1].size(0)
+        train_drop = dropout_p if dropout_p > 0 else 0.0
+        hs = [x]
+        aggs = []
+        P = torch.cat([Wl[-1], Wr[-1]], dim=0).contiguous()  # [2C, F_{L-1}]
+        z = None
+        for l in range(L - 1):
+            h = hs[-1]
+            agg = aggregate(plan, h, _lib.AGG_MEAN, nodew=plan.deg)
+            bt = torch.cat([Wl[l], Wr[l]], dim=1).t().contiguous()  # [2F_l, F_{l+1}]
+            last_hidden = l == L - 2
+            if last_hidden:
+                z = torch.empty((h.size(0), 2 * C), dtype=torch.float32, device=h.device)
+            hn = gemm_nt(agg, bt, Wl[l].size(0), a2=h, bias=bl[l], relu=True, dropout_p=train_drop,
+                         seed=seeds[l], proj=P if last_hidden else None, z=z if last_hidden else None)
+            aggs.append(agg)
+            hs.append(hn)
+        logits = aggregate(plan, z[:, :C], _lib.AGG_MEAN, nodew=plan.deg, addend=z[:, C:], bias=bl[-1])
+        ctx.plan = plan
+        ctx.meta = (L, C, float(dropout_p))
+        ctx.save_for_backward(*hs, *aggs, *params)
+        return logits
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dlogits):
+        plan = ctx.plan
+        L, C, p = ctx.meta
+        saved = ctx.saved_tensors
+        hs = saved[:L]
+        aggs = saved[L: 2 * L - 1]
+        params = saved[2 * L - 1:]
+        Wl, Wr = params[0::3], params[2::3]
+        hscale = 1.0 / (1.0 - p) if p > 0 else 1.0
+        dlogits = dlogits.contiguous()
+        N = dlogits.size(0)
+        dz = torch.empty((N, 2 * C), dtype=torch.float32, device=dlogits.device)
+        aggregate(plan, dlogits, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dz[:, :C])
+        dz[:, C:].copy_(dlogits)
+        P = torch.cat([Wl[-1], Wr[-1]], dim=0).contiguous()
+        grads = [None] * (3 * L)
+        need_x = ctx.needs_input_grad[0]
+        g = None
+        for l in range(L - 2, -1, -1):
+            fo, fi = Wl[l].shape
+            need_g = l > 0 or need_x
+            gout = torch.empty((N, fo), dtype=torch.float32, device=dz.device) if need_g else None
+            if l == L - 2:
+                dW, db, dW2, dzs = gemm_tn(fo, aggs[l], hs[l], dz=dz, proj=P, h=hs[l + 1], hscale=hscale,
+                                           gout=gout)
+                grads[3 * (L - 1) + 0] = dW2[:C]
+                grads[3 * (L - 1) + 1] = dzs[C:]
+                grads[3 * (L - 1) + 2] = dW2[C:]
+            else:
+                dW, db, _, _ = gemm_tn(fo, aggs[l], hs[l], g=g, h=hs[l + 1], hscale=hscale, gout=gout)
+            grads[3 * l + 0] = dW[:, :fi]
+            grads[3 * l + 1] = db
+            grads[3 * l + 2] = dW[:, fi:]
+            if need_g:
+                # dh_l = meanᵀ(G · W_l) + G · W_r   (G = dL/dpre_{l+1})
+                bt = torch.cat([Wl[l], Wr[l]], dim=1).contiguous()  # [fo, 2 fi]
+                dA = gemm_nt(gout, bt, 2 * fi)
+                dh = aggregate(plan, dA[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg,
+                               addend=dA[:, fi:])
+                g = dh  # next (lower) layer's upstream gradient w.r.t. h_l, masked inside TN
+        dx = g if need_x else None
+        return (dx, None, None, None, *grads)
+
+
+def fusable(model) -> bool:
+    """SAGENet with narrow output (2·classes <= 4), widths within the fused kernels' limits."""
+    convs = list(model.convs)
+    if len(convs) < 2:
+        return False
+    for c in convs:
+        if getattr(c, "aggr", None) != "mean" or c.lin_l.bias is None:
+            return False
+    for c in convs[:-1]:
+        if c.out_channels > 128 or 2 * c.in_channels > 384:
+            return False
+    return 2 * convs[-1].out_channels <= MAX_PROJ and convs[-1].in_channels <= 128
+
+
+def sage_forward(model, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+    plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
+    L = len(model.convs)
+    p = float(model.dropout) if model.training else 0.0
+    seeds = torch.randint(0, 2 ** 62, (L,), dtype=torch.int64).tolist() if p > 0 else [0] * L
+    params = []
+    for c in model.convs:
+        params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]
+    return _FusedSAGE.apply(x, plan, p, seeds, *params)

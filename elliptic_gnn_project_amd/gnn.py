@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import fused as _fused
 from .conv import GATConv, GCNConv, SAGEConv
 
 __all__ = ["GCNNet", "SAGENet", "GATNet", "SAGEResBNNet"]
@@ -58,8 +59,20 @@ class GCNNet(_StackedConvNet):
 
 
 class SAGENet(_StackedConvNet):
+    """When the shape allows (narrow 2-class output, widths within the kernels' limits) the whole
+    network runs as one fused autograd node (fused.py): aggregate-first SAGE layers on the MFMA
+    GEMM with bias/ReLU/dropout and the output layer's transform fused into its epilogue.
+    ``fused = False`` selects the per-conv path (same kernels, layer by layer)."""
+
+    fused = True
+
     def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2):
         super().__init__([SAGEConv(a, b) for a, b in _widths(in_dim, hidden_dim, layers, num_classes)], dropout)
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor, t_idx: Optional[torch.Tensor] = None):
+        if self.fused and x.is_cuda and _fused.fusable(self):
+            return _fused.sage_forward(self, x, edge_index)
+        return super().forward(x, edge_index, t_idx)
 
 
 class GATNet(_StackedConvNet):

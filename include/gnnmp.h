@@ -159,6 +159,46 @@ gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t con
                            size_t workspace_bytes, gnn_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* K7  fp32 MFMA GEMMs with the surrounding elementwise work fused in.      */
+/*     Replace PyG Linear lin_l/lin_r/lin (gnn.py:20-23,41-44,64-67) and the  */
+/*     F.relu + F.dropout between layers (gnn.py:29-30,50-51,73-74).          */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int64_t M, N;                          /* C is [M, N] */
+  const float* a1; int64_t lda1; int64_t k1;
+  const float* a2; int64_t lda2; int64_t k2;   /* optional 2nd K segment: A = [A1 | A2] (k2 = 0: none) */
+  const float* bt; int64_t ldb;          /* [k1+k2, N] row-major (Linear weight transposed) */
+  float* c; int64_t ldc;                 /* output (may be NULL when only z is wanted) */
+  const float* bias;                     /* [N] or NULL */
+  int32_t relu;                          /* max(., 0) after bias */
+  float dropout_p;                       /* after ReLU; 0 = off.  keep if hash(seed, row*N+col) < 1-p */
+  uint64_t seed;
+  const float* proj; int32_t nproj;      /* optional Z = C · projᵀ, proj [nproj, N], nproj <= 4, N <= 128 */
+  float* z; int64_t ldz;
+} gnn_gemm_nt_params;
+
+/* C = epilogue([A1|A2] · Bt). */
+gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream);
+
+typedef struct {
+  int64_t M, Nr;                         /* dW is [Nr, k1+k2], Nr <= 128, k1+k2 <= 384 */
+  const float* g; int64_t ldg;           /* G [M, Nr] ... */
+  const float* dz; int64_t lddz;         /* ... or G = dz · proj (dz [M, nproj], proj [nproj, Nr]) */
+  const float* proj; int32_t nproj;
+  const float* h; int64_t ldh; float hscale;   /* optional: G *= (h > 0 ? hscale : 0) — ReLU+dropout bwd */
+  float* gout; int64_t ldgout;           /* optional: store G */
+  const float* a1; int64_t lda1; int64_t k1;
+  const float* a2; int64_t lda2; int64_t k2;
+} gnn_gemm_tn_params;
+
+/* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).
+ * out (contiguous): dW [Nr, k1+k2] | db = Σ_m G [Nr] | (dz form) dW2 = dzᵀ·h [nproj, Nr] |
+ * dzsum = Σ_m dz [nproj]. */
+gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t Kc, int32_t nproj, size_t* bytes);
+gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* workspace, size_t workspace_bytes,
+                           gnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Dense helpers used by the fused conv paths                               */
 /* ------------------------------------------------------------------------ */
 /* out[c] = sum_r x[r, c]  (bias gradients; deterministic two-stage column sum). */

@@ -1,0 +1,166 @@
+"""GPU parity of the fp32 MFMA GEMM kernels (K7) and the fused SAGENet path.
+
+GEMMs are floating-point kernels: compared with a plain torch fp32 reference on the CPU
+(rtol=atol=1e-5 at these magnitudes).  The fused network is compared with the CPU oracle
+in eval mode and in train mode with dropout, using oracle/dropout_hash.py's bit-exact mask.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import pyg_ref
+from oracle.dropout_hash import keep_mask
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b, floor=1e-7):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), floor / 1e-5))
+
+
+@pytest.mark.parametrize("M,k1,k2,n", [(1000, 166, 166, 128), (257, 5, 0, 3), (4097, 128, 128, 128),
+                                       (300, 64, 64, 256), (129, 33, 17, 130), (64, 1, 0, 1)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "dropout", "proj"])
+def test_gemm_nt(device, M, k1, k2, n, epi):
+    from elliptic_gnn_project_amd.fused import gemm_nt
+
+    if epi == "proj" and n > 128:
+        pytest.skip("projection needs N <= 128")
+    g = torch.Generator().manual_seed(M + k1 + n)
+    a1 = torch.randn(M, k1, generator=g)
+    a2 = torch.randn(M, k2, generator=g) if k2 else None
+    bt = torch.randn(k1 + k2, n, generator=g) / (k1 + k2) ** 0.5
+    bias = torch.randn(n, generator=g)
+    proj = torch.randn(4, n, generator=g)
+    A = torch.cat([a1, a2], 1) if k2 else a1
+    ref = A @ bt
+    kw = {}
+    p = 0.0
+    if epi != "plain":
+        ref = torch.relu(ref + bias)
+        kw = dict(bias=bias.to(device), relu=True)
+    if epi == "dropout":
+        p = 0.3
+        m = torch.from_numpy(keep_mask(1234, M, n, p))
+        ref = ref * m / (1 - np.float32(p))
+        kw.update(dropout_p=p, seed=1234)
+    z = None
+    if epi == "proj":
+        z = torch.empty(M, 4, device=device)
+        kw.update(proj=proj.to(device), z=z)
+    c = gemm_nt(a1.to(device), bt.to(device), n, a2=a2.to(device) if a2 is not None else None, **kw)
+    torch.testing.assert_close(c.cpu(), ref, rtol=1e-5, atol=1e-5)
+    if epi == "proj":
+        torch.testing.assert_close(z.cpu(), ref @ proj.t(), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,nr,k1,k2", [(5000, 128, 166, 166), (777, 3, 20, 0), (64, 128, 128, 128),
+                                        (20000, 64, 167, 167), (33, 1, 1, 0)])
+@pytest.mark.parametrize("form", ["g", "g_mask", "dz_mask"])
+def test_gemm_tn(device, M, nr, k1, k2, form):
+    from elliptic_gnn_project_amd.fused import gemm_tn
+
+    g_ = torch.Generator().manual_seed(M + nr)
+    a1 = torch.randn(M, k1, generator=g_)
+    a2 = torch.randn(M, k2, generator=g_) if k2 else None
+    A = torch.cat([a1, a2], 1) if k2 else a1
+    h = torch.relu(torch.randn(M, nr, generator=g_))
+    dz = torch.randn(M, 4, generator=g_)
+    proj = torch.randn(4, nr, generator=g_)
+    G = torch.randn(M, nr, generator=g_)
+    kw = {}
+    if form == "dz_mask":
+        G = dz @ proj
+        kw = dict(dz=dz.to(device), proj=proj.to(device))
+    else:
+        kw = dict(g=G.to(device))
+    if form != "g":
+        G = torch.where(h > 0, G * 2.0, torch.zeros_like(G))
+        kw.update(h=h.to(device), hscale=2.0)
+    gout = torch.empty(M, nr, device=device)
+    dW, db, dW2, dzs = gemm_tn(nr, a1.to(device), a2.to(device) if a2 is not None else None, gout=gout, **kw)
+    torch.testing.assert_close(gout.cpu(), G, rtol=1e-5, atol=1e-5)
+    assert rel_l2(dW, G.t() @ A) < 1e-5
+    assert rel_l2(db, G.sum(0)) < 1e-5
+    if form == "dz_mask":
+        assert rel_l2(dW2, dz.t() @ h) < 1e-5
+        assert rel_l2(dzs, dz.sum(0)) < 1e-5
+
+
+def _graph(n, e, seed):
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+
+    return prepare_inputs(synthetic_elliptic(num_nodes=n, num_edges=e, seed=seed),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+
+
+@pytest.mark.parametrize("layers,hidden", [(2, 128), (3, 128), (3, 64), (4, 32)])
+@pytest.mark.parametrize("dropout", [0.0, 0.5])
+def test_fused_sage_train_step(device, layers, hidden, dropout):
+    """Fused SAGENet vs the oracle: logits and every parameter gradient, same dropout masks."""
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data = _graph(5000, 6000, seed=21)
+    N = data.x.size(0)
+    torch.manual_seed(5)
+    model = SAGENet(data.x.size(1), hidden, layers=layers, dropout=dropout).to(device)
+    params = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    model.train()
+    torch.manual_seed(77)
+    logits = model(data.x.to(device), data.edge_index.to(device))
+    torch.manual_seed(77)
+    seeds = torch.randint(0, 2 ** 62, (layers,), dtype=torch.int64).tolist()
+    masks = [torch.from_numpy(keep_mask(seeds[l], N, hidden, dropout)) for l in range(layers - 1)] \
+        if dropout > 0 else None
+    mask = data.train_mask
+    cw = pyg_ref.class_weight(data.y[mask])
+    loss = pyg_ref.ce_loss(logits[mask.to(device)], data.y[mask].to(device), cw.to(device))
+    loss.backward()
+    kw = dict(layers=layers, dropout=dropout, training=True, dropout_masks=masks)
+    ref = pyg_ref.model_forward("sage", params, data.x, data.edge_index, **kw)
+    torch.testing.assert_close(logits.detach().cpu(), ref, rtol=1e-5, atol=1e-5)
+    _, grads = pyg_ref.train_step_grads("sage", params, data.x, data.edge_index, data.y, mask, cw, **kw)
+    for k, v in model.named_parameters():
+        assert rel_l2(v.grad, grads[k]) < 1e-5, k
+
+
+def test_fused_matches_unfused_and_input_grad(device):
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data = _graph(3000, 4000, seed=3)
+    torch.manual_seed(1)
+    model = SAGENet(data.x.size(1), 64, layers=3, dropout=0.0).to(device)
+    x = data.x.to(device).requires_grad_(True)
+    ei = data.edge_index.to(device)
+    out_f = model(x, ei)
+    out_f.square().sum().backward()
+    gx_f = x.grad.clone()
+    gp_f = {k: v.grad.clone() for k, v in model.named_parameters()}
+    model.zero_grad()
+    x.grad = None
+    model.fused = False
+    out_u = model(x, ei)
+    out_u.square().sum().backward()
+    torch.testing.assert_close(out_f, out_u, rtol=1e-5, atol=1e-5)
+    assert rel_l2(gx_f, x.grad) < 1e-5
+    for k, v in model.named_parameters():
+        assert rel_l2(gp_f[k], v.grad) < 1e-5, k
+
+
+def test_fused_full_elliptic_eval_and_determinism(device):
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data = _graph(203_769, 234_355, seed=42)
+    torch.manual_seed(4)
+    model = SAGENet(166, 128, layers=2, dropout=0.5).to(device)
+    p = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    model.eval()
+    x, ei = data.x.to(device), data.edge_index.to(device)
+    with torch.no_grad():
+        a = model(x, ei)
+        b = model(x, ei)
+    assert torch.equal(a, b)
+    ref = pyg_ref.model_forward("sage", p, data.x, data.edge_index, layers=2)
+    torch.testing.assert_close(a.cpu(), ref, rtol=1e-5, atol=1e-5)
