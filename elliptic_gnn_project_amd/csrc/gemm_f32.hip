@@ -15,7 +15,7 @@
 // TN:  dW[Nr, k1+k2] = Σ_m G[m, Nr]ᵀ · [A1 | A2][m, :]   (split over M, slabs, ordered reduce)
 //      G = (G_src or dz·P) ⊙ (h > 0 ? scale : 0)   — ReLU+dropout backward computed on the fly
 //      side sums: db[n] = Σ G, dW2[q][n] = Σ dz[m,q]·h[m,n], dzsum[q] = Σ dz[m,q]
-//      Block = 8 waves: wave w owns dW rows (w&3)*32.. and k-tiles (w>>2)*6 .. +6.
+//      Block = 16 waves: wave w owns dW rows (w&3)*32.. and k-tiles (w>>2)*3 .. +3.
 // Both are atomic-free and deterministic.
 #include "common.hpp"
 
@@ -23,22 +23,23 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace gnnmp {
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
-// Dropout keep decision for element `idx` of a call seeded with `seed` (mirrored bit for
-// bit by oracle/dropout_hash.py so CPU parity can use the same masks).
-__device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t keep_thresh) {
-  return (uint32_t)(mix64(seed ^ (idx * 0xD1B54A32D192ED03ull)) >> 40) < keep_thresh;
+// Dropout keep decision for element `idx` of a call seeded with `seed`: murmur3's fmix32
+// over (idx * golden + seed_lo) ^ seed_hi, top 24 bits compared with (1-p)·2^24.  32-bit
+// arithmetic only (3 multiplies).  Mirrored bit for bit by oracle/dropout_hash.py.
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t idx, uint32_t keep_thresh) {
+  uint32_t h = idx * 0x9E3779B1u + (uint32_t)seed;
+  h ^= (uint32_t)(seed >> 32);
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (h >> 8) < keep_thresh;
 }
 
 namespace {
 
-constexpr int BM = 128, BN = 128, KC = 32, APITCH = KC + 1;
+constexpr int BN = 128;  // NT block columns (4 waves stacked by rows, each wave 4 x 32 columns)
 
 struct NTArgs {
   int64_t M;
@@ -53,179 +54,246 @@ struct NTArgs {
   const float* proj; int32_t nproj; float* z; int64_t ldz;
 };
 
-template <int AVEC>
-__device__ __forceinline__ void nt_load_a(const NTArgs& a, int c, int64_t m0, float (&ra)[16]) {
+// Tiling parameters: KC = K depth per LDS chunk, TM = 32-row tiles per wave (block rows
+// BM = 4 waves x 32·TM), UNR = fully unroll full chunks.
+template <int KC, int TM>
+struct NTShape {
+  static constexpr int BM = 128 * TM;
+  static constexpr int APITCH = KC + 1;  // odd pitch: conflict-free column reads of A
+  static constexpr int A_PER_THREAD = BM * KC / 256;
+  static constexpr int B_PER_THREAD = KC * BN / 256;
+};
+
+template <int KC>
+__device__ __forceinline__ void nt_chunk_range(const NTArgs& a, int c, const float*& A, int64_t& lda, int& k0,
+                                               int& kb0, int& klen) {
   const int nch1 = (a.k1 + KC - 1) / KC;
-  const float* A; int64_t lda; int k0, klen;
-  if (c < nch1) { A = a.a1; lda = a.lda1; k0 = c * KC; klen = min(KC, a.k1 - k0); }
-  else { A = a.a2; lda = a.lda2; k0 = (c - nch1) * KC; klen = min(KC, a.k2 - k0); }
-  constexpr int VPR = KC / AVEC;  // vectors per row
-#pragma unroll
-  for (int i = 0; i < 16 / AVEC; ++i) {
-    int v = threadIdx.x + 256 * i;
-    int r = v / VPR;
-    int k = (v % VPR) * AVEC;
-    int64_t row = m0 + r;
-    const float* p = A + row * lda + k0 + k;
-    if (row < a.M && k + AVEC <= klen) {
-      if constexpr (AVEC == 4) {
-        float4 t = *reinterpret_cast<const float4*>(p);
-        ra[i * 4 + 0] = t.x; ra[i * 4 + 1] = t.y; ra[i * 4 + 2] = t.z; ra[i * 4 + 3] = t.w;
-      } else if constexpr (AVEC == 2) {
-        float2 t = *reinterpret_cast<const float2*>(p);
-        ra[i * 2 + 0] = t.x; ra[i * 2 + 1] = t.y;
-      } else {
-        ra[i] = *p;
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < AVEC; ++q) ra[i * AVEC + q] = (row < a.M && k + q < klen) ? p[q] : 0.0f;
-    }
-  }
+  if (c < nch1) { A = a.a1; lda = a.lda1; k0 = c * KC; kb0 = k0; klen = min(KC, a.k1 - k0); }
+  else { A = a.a2; lda = a.lda2; k0 = (c - nch1) * KC; kb0 = a.k1 + k0; klen = min(KC, a.k2 - k0); }
 }
 
-template <int AVEC>
-__device__ __forceinline__ void nt_store_a(float* As, const float (&ra)[16]) {
+// Loads only (every address clamped into range, no data-dependent selects), so the
+// prefetch of chunk c+1 stays in flight across chunk c's MFMAs; masking happens in
+// nt_store, after them.  AVEC divides k1 and k2, so a vector never straddles K's end.
+template <int AVEC, int KC, int TM>
+__device__ __forceinline__ void nt_load(const NTArgs& a, int c, int64_t m0, int n0, bool bvec4,
+                                        float (&ra)[NTShape<KC, TM>::A_PER_THREAD],
+                                        float (&rb)[NTShape<KC, TM>::B_PER_THREAD]) {
+  using S = NTShape<KC, TM>;
+  const float* A; int64_t lda; int k0, kb0, klen;
+  nt_chunk_range<KC>(a, c, A, lda, k0, kb0, klen);
   constexpr int VPR = KC / AVEC;
 #pragma unroll
-  for (int i = 0; i < 16 / AVEC; ++i) {
-    int v = threadIdx.x + 256 * i;
-    int r = v / VPR;
-    int k = (v % VPR) * AVEC;
-#pragma unroll
-    for (int q = 0; q < AVEC; ++q) As[r * APITCH + k + q] = ra[i * AVEC + q];
-  }
-}
-
-__device__ __forceinline__ void nt_load_b(const NTArgs& a, int c, int n0, bool vec4, float (&rb)[16]) {
-  const int nch1 = (a.k1 + KC - 1) / KC;
-  int kb0, klen;
-  if (c < nch1) { kb0 = c * KC; klen = min(KC, a.k1 - c * KC); }
-  else { int cc = c - nch1; kb0 = a.k1 + cc * KC; klen = min(KC, a.k2 - cc * KC); }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int v = threadIdx.x + 256 * i;  // 1024 float4 slots = 32 rows x 32
-    int kk = v >> 5;
-    int n = (v & 31) * 4;
-    const float* p = a.bt + (int64_t)(kb0 + kk) * a.ldb + n0 + n;
-    if (vec4 && kk < klen && n0 + n + 4 <= a.Nc) {
+  for (int i = 0; i < S::A_PER_THREAD / AVEC; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int r = v / VPR;
+    const int k = (v % VPR) * AVEC;
+    int64_t row = m0 + r;
+    row = row < a.M ? row : a.M - 1;
+    const float* p = A + row * lda + k0 + (k < klen ? k : 0);
+    if constexpr (AVEC == 4) {
       float4 t = *reinterpret_cast<const float4*>(p);
+      ra[i * 4 + 0] = t.x; ra[i * 4 + 1] = t.y; ra[i * 4 + 2] = t.z; ra[i * 4 + 3] = t.w;
+    } else if constexpr (AVEC == 2) {
+      float2 t = *reinterpret_cast<const float2*>(p);
+      ra[i * 2 + 0] = t.x; ra[i * 2 + 1] = t.y;
+    } else {
+      ra[i] = *p;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < S::B_PER_THREAD / 4; ++i) {
+    const int v = threadIdx.x + 256 * i;  // float4 slots: KC rows x 32
+    const int kk = v >> 5;
+    const int n = (v & 31) * 4;
+    const float* p = a.bt + (int64_t)(kb0 + (kk < klen ? kk : 0)) * a.ldb;
+    if (bvec4) {  // Nc % 4 == 0: a float4 never straddles Nc
+      const int nn = n0 + n < a.Nc ? n0 + n : 0;
+      float4 t = *reinterpret_cast<const float4*>(p + nn);
       rb[i * 4 + 0] = t.x; rb[i * 4 + 1] = t.y; rb[i * 4 + 2] = t.z; rb[i * 4 + 3] = t.w;
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rb[i * 4 + q] = (kk < klen && n0 + n + q < a.Nc) ? p[q] : 0.0f;
+      for (int q = 0; q < 4; ++q) rb[i * 4 + q] = p[n0 + n + q < a.Nc ? n0 + n + q : 0];
     }
   }
 }
 
-__device__ __forceinline__ void nt_store_b(float* Bs, const float (&rb)[16]) {
+template <int AVEC, int KC, int TM>
+__device__ __forceinline__ void nt_store(const NTArgs& a, int c, int64_t m0, int n0, float* As, float* Bs,
+                                         const float (&ra)[NTShape<KC, TM>::A_PER_THREAD],
+                                         const float (&rb)[NTShape<KC, TM>::B_PER_THREAD]) {
+  using S = NTShape<KC, TM>;
+  const float* A; int64_t lda; int k0, kb0, klen;
+  nt_chunk_range<KC>(a, c, A, lda, k0, kb0, klen);
+  constexpr int VPR = KC / AVEC;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int v = threadIdx.x + 256 * i;
-    int kk = v >> 5;
-    int n = (v & 31) * 4;
-    *reinterpret_cast<float4*>(&Bs[kk * BN + n]) = make_float4(rb[i * 4], rb[i * 4 + 1], rb[i * 4 + 2], rb[i * 4 + 3]);
+  for (int i = 0; i < S::A_PER_THREAD / AVEC; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int r = v / VPR;
+    const int k = (v % VPR) * AVEC;
+    const bool ok = (m0 + r < a.M) && (k < klen);
+#pragma unroll
+    for (int q = 0; q < AVEC; ++q) As[r * S::APITCH + k + q] = ok ? ra[i * AVEC + q] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < S::B_PER_THREAD / 4; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int kk = v >> 5;
+    const int n = (v & 31) * 4;
+    float w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = (kk < klen && n0 + n + q < a.Nc) ? rb[i * 4 + q] : 0.0f;
+    *reinterpret_cast<float4*>(&Bs[kk * BN + n]) = make_float4(w[0], w[1], w[2], w[3]);
   }
 }
 
-__device__ __forceinline__ int chunk_ksteps(const NTArgs& a, int c) {
-  const int nch1 = (a.k1 + KC - 1) / KC;
-  int klen = (c < nch1) ? min(KC, a.k1 - c * KC) : min(KC, a.k2 - (c - nch1) * KC);
+template <int KC>
+__device__ __forceinline__ int nt_ksteps(const NTArgs& a, int c) {
+  const float* A; int64_t lda; int k0, kb0, klen;
+  nt_chunk_range<KC>(a, c, A, lda, k0, kb0, klen);
   return (klen + 1) >> 1;
 }
 
-template <int AVEC>
+template <int TM>
+__device__ __forceinline__ void nt_kstep(floatx16 (&acc)[TM][4], const float* Aw, const float* Bw, int s, int apitch) {
+  float af[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) af[tm] = Aw[tm * 32 * apitch + 2 * s];
+  const float* b = Bw + 2 * s * BN;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float bf = b[t * 32];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[tm], bf, acc[tm][t], 0, 0, 0);
+  }
+}
+
+template <int AVEC, int KC, int TM, bool UNR>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
-  __shared__ float As[2][BM * APITCH];
+  using S = NTShape<KC, TM>;
+  __shared__ float As[2][S::BM * S::APITCH];
   __shared__ __attribute__((aligned(16))) float Bs[2][KC * BN];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t m0 = (int64_t)blockIdx.x * S::BM;
   const int n0 = blockIdx.y * BN;
   const int nchunks = (a.k1 + KC - 1) / KC + (a.k2 + KC - 1) / KC;
-  const bool bvec4 = ((a.ldb & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.bt) & 15) == 0);
+  const bool bvec4 = ((a.ldb & 3) == 0) && ((a.Nc & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.bt) & 15) == 0);
 
-  floatx16 acc[4];
+  floatx16 acc[TM][4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tm][t][r] = 0.0f;
 
-  float ra[16], rb[16];
-  nt_load_a<AVEC>(a, 0, m0, ra);
-  nt_load_b(a, 0, n0, bvec4, rb);
-  nt_store_a<AVEC>(As[0], ra);
-  nt_store_b(Bs[0], rb);
+  float ra[S::A_PER_THREAD], rb[S::B_PER_THREAD];
+  nt_load<AVEC, KC, TM>(a, 0, m0, n0, bvec4, ra, rb);
+  nt_store<AVEC, KC, TM>(a, 0, m0, n0, As[0], Bs[0], ra, rb);
   __syncthreads();
 
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
-    if (c + 1 < nchunks) {
-      nt_load_a<AVEC>(a, c + 1, m0, ra);
-      nt_load_b(a, c + 1, n0, bvec4, rb);
-    }
-    const float* Aw = As[buf] + (wave * 32 + (lane & 31)) * APITCH + (lane >> 5);
+    if (c + 1 < nchunks) nt_load<AVEC, KC, TM>(a, c + 1, m0, n0, bvec4, ra, rb);
+    const float* Aw = As[buf] + (wave * 32 * TM + (lane & 31)) * S::APITCH + (lane >> 5);
     const float* Bw = Bs[buf] + (lane >> 5) * BN + (lane & 31);
-    const int ks = chunk_ksteps(a, c);
-    for (int s = 0; s < ks; ++s) {
-      const float af = Aw[2 * s];
-      const float* b = Bw + 2 * s * BN;
+    const int ks = nt_ksteps<KC>(a, c);
+    if (UNR && ks == KC / 2) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af, b[t * 32], acc[t], 0, 0, 0);
+      for (int s = 0; s < KC / 2; ++s) nt_kstep<TM>(acc, Aw, Bw, s, S::APITCH);
+    } else {
+      for (int s = 0; s < ks; ++s) nt_kstep<TM>(acc, Aw, Bw, s, S::APITCH);
     }
-    if (c + 1 < nchunks) {
-      nt_store_a<AVEC>(As[buf ^ 1], ra);
-      nt_store_b(Bs[buf ^ 1], rb);
-    }
+    if (c + 1 < nchunks) nt_store<AVEC, KC, TM>(a, c + 1, m0, n0, As[buf ^ 1], Bs[buf ^ 1], ra, rb);
     __syncthreads();
   }
 
   // ---------------- epilogue: bias, ReLU, dropout, store, optional projection
-  const int64_t rbase = m0 + wave * 32 + 4 * (lane >> 5);
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int col = n0 + t * 32 + (lane & 31);
-    const bool colok = col < a.Nc;
-    const float bv = (a.bias && colok) ? a.bias[col] : 0.0f;
+  for (int tm = 0; tm < TM; ++tm) {
+    const int64_t rbase = m0 + wave * 32 * TM + tm * 32 + 4 * (lane >> 5);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-      float v = acc[t][r] + bv;
-      if (a.relu) v = fmaxf(v, 0.0f);
-      if (a.dropout) v = keep_elem(a.seed, (uint64_t)row * (uint64_t)a.Nc + (uint64_t)col, a.keep_thresh) ? v * a.drop_scale : 0.0f;
-      if (!colok) v = 0.0f;
-      if (a.c && row < a.M && colok) a.c[row * a.ldc + col] = v;
-      acc[t][r] = v;
-    }
-  }
-  if (a.nproj > 0) {
-    for (int q = 0; q < a.nproj; ++q) {
-      float pw[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int col = n0 + t * 32 + (lane & 31);
-        pw[t] = col < a.Nc ? a.proj[(int64_t)q * a.Nc + col] : 0.0f;
-      }
+    for (int t = 0; t < 4; ++t) {
+      const int col = n0 + t * 32 + (lane & 31);
+      const bool colok = col < a.Nc;
+      const float bv = (a.bias && colok) ? a.bias[col] : 0.0f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float s = acc[0][r] * pw[0];
-        s = fmaf(acc[1][r], pw[1], s);
-        s = fmaf(acc[2][r], pw[2], s);
-        s = fmaf(acc[3][r], pw[3], s);
-#pragma unroll
-        for (int off = 16; off >= 1; off >>= 1) s += __shfl_xor(s, off);
         const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-        if ((lane & 31) == 0 && row < a.M) a.z[row * a.ldz + q] = s;
+        float v = acc[tm][t][r] + bv;
+        if (a.relu) v = fmaxf(v, 0.0f);
+        if (a.dropout)
+          v = keep_elem(a.seed, (uint32_t)row * (uint32_t)a.Nc + (uint32_t)col, a.keep_thresh) ? v * a.drop_scale : 0.0f;
+        if (!colok) v = 0.0f;
+        if (a.c && row < a.M && colok) a.c[row * a.ldc + col] = v;
+        acc[tm][t][r] = v;
+      }
+    }
+    if (a.nproj > 0) {
+      // z[row, q] = Σ_col h[row, col] · proj[q, col].  Each lane holds 4 columns of each of its
+      // 16 rows; the 4 projection sums are reduced over the 32 lanes of a half-wave with a
+      // reduce-and-split butterfly: xor 16 halves the q set, xor 8 halves it again, then
+      // xor 4/2/1 finish one value — 6 shuffles per row instead of 4 x 5.
+      float pw[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int col = n0 + t * 32 + (lane & 31);
+          pw[q][t] = (q < a.nproj && col < a.Nc) ? a.proj[(int64_t)q * a.Nc + col] : 0.0f;
+        }
+      const bool hi16 = lane & 16, hi8 = lane & 8;
+      const int qsel = (hi16 ? 2 : 0) + (hi8 ? 1 : 0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float ps[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float sum = acc[tm][0][r] * pw[q][0];
+          sum = fmaf(acc[tm][1][r], pw[q][1], sum);
+          sum = fmaf(acc[tm][2][r], pw[q][2], sum);
+          ps[q] = fmaf(acc[tm][3][r], pw[q][3], sum);
+        }
+        const float s0 = hi16 ? ps[0] : ps[2], s1 = hi16 ? ps[1] : ps[3];
+        const float k0 = (hi16 ? ps[2] : ps[0]) + __shfl_xor(s0, 16);
+        const float k1 = (hi16 ? ps[3] : ps[1]) + __shfl_xor(s1, 16);
+        float m = (hi8 ? k1 : k0) + __shfl_xor(hi8 ? k0 : k1, 8);
+        m += __shfl_xor(m, 4);
+        m += __shfl_xor(m, 2);
+        m += __shfl_xor(m, 1);
+        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
+        if ((lane & 7) == 0 && qsel < a.nproj && row < a.M) a.z[row * a.ldz + qsel] = m;
       }
     }
   }
 }
 
+template <int AVEC, int KC, int TM, bool UNR>
+void launch_nt(const NTArgs& a, hipStream_t st) {
+  dim3 grid((unsigned)ceil_div(a.M, NTShape<KC, TM>::BM), (unsigned)ceil_div(a.Nc, BN));
+  gemm_nt_kernel<AVEC, KC, TM, UNR><<<grid, 256, 0, st>>>(a);
+}
+
+// Variant table (tuning harness csrc/bench_gemm.hip); variant 0 is the production choice.
+template <int AVEC>
+void launch_nt_variant(const NTArgs& a, int variant, hipStream_t st) {
+  switch (variant) {
+    case 1: launch_nt<AVEC, 32, 1, false>(a, st); break;  // 32-deep chunks, 2 blocks/CU
+    case 2: launch_nt<AVEC, 32, 1, true>(a, st); break;
+    case 3: launch_nt<AVEC, 16, 1, true>(a, st); break;
+    case 4: launch_nt<AVEC, 16, 1, false>(a, st); break;
+    case 5: launch_nt<AVEC, 32, 2, false>(a, st); break;
+    case 6: launch_nt<AVEC, 16, 2, true>(a, st); break;
+    case 7: launch_nt<AVEC, 16, 2, false>(a, st); break;
+    default: launch_nt<AVEC, 16, 1, false>(a, st); break;  // production: measured fastest (r01 lab)
+  }
+}
+
 // ------------------------------------------------------------------------------------ TN
-constexpr int MC = 32;          // rows per chunk
-constexpr int TN_WAVES = 8;
-constexpr int KT_PER_WAVE = 6;  // k-tiles per wave -> Kc <= 2 * 6 * 32 = 384
-constexpr int KMAX = 2 * KT_PER_WAVE * 32;
+constexpr int TN_THREADS = 1024;  // 16 waves: wave w owns dW rows (w&3)*32.. and k-tiles (w>>2)*3 .. +3
+constexpr int KT_PER_WAVE = 3;
+constexpr int KMAX = 4 * KT_PER_WAVE * 32;  // Kc <= 384
 constexpr int TN_APITCH = KMAX;
 constexpr int MAXPROJ = 4;
 
@@ -244,10 +312,28 @@ struct TNArgs {
 };
 
 // slab layout: dW[Nr][Kc] | db[Nr] | dW2[nproj][Nr] | dzsum[nproj]
-__global__ __launch_bounds__(512) void gemm_tn_kernel(TNArgs a) {
-  __shared__ __attribute__((aligned(16))) float Gs[MC * 128];
-  __shared__ __attribute__((aligned(16))) float As[MC * TN_APITCH];
-  __shared__ float red[4 * 128 * (1 + MAXPROJ)];
+//
+// Structure (per 512-thread block, rows [mbeg, mend)): chunks of MC=32 rows, double-buffered
+// through LDS.  While the MFMAs of chunk c run, chunk c+1's operands are already in flight
+// into registers (every load unconditional on a clamped row: no branch-around-load waits);
+// they are transformed (G prologue) and stored after the MFMAs, then one barrier.
+template <int MC, int NTL>
+__device__ __forceinline__ void tn_mma(floatx16 (&acc)[KT_PER_WAVE], const float* gptr, const float* aptr, int kt0) {
+#pragma unroll 2
+  for (int s = 0; s < MC / 2; ++s) {
+    const float gf = gptr[2 * s * 128];
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) {
+      const float af = aptr[2 * s * TN_APITCH + (kt0 + t) * 32];
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(gf, af, acc[t], 0, 0, 0);
+    }
+  }
+}
+
+template <bool PROJ, bool MASK, int AVEC, int MC>
+__global__ __launch_bounds__(TN_THREADS) void gemm_tn_kernel(TNArgs a) {
+  __shared__ __attribute__((aligned(16))) float Gs[2][MC * 128];
+  __shared__ __attribute__((aligned(16))) float As[2][MC * TN_APITCH];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -255,6 +341,7 @@ __global__ __launch_bounds__(512) void gemm_tn_kernel(TNArgs a) {
   const int kt0 = (wave >> 2) * KT_PER_WAVE;
   const int Kc = a.k1 + a.k2;
   const int nkt = (Kc + 31) / 32;
+  const int ntl = max(0, min(KT_PER_WAVE, nkt - kt0));
   const int64_t mbeg = (int64_t)blockIdx.x * a.rows_per_block;
   const int64_t mend = min(a.M, mbeg + a.rows_per_block);
 
@@ -264,81 +351,129 @@ __global__ __launch_bounds__(512) void gemm_tn_kernel(TNArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
 
-  // prologue thread mapping: column n = tid & 127, rows rg*8 .. rg*8+7
-  const int pn = tid & 127;
+  const int pn = tid & 127;  // prologue: column pn, rows rg*GR .. rg*GR+GR-1
   const int rg = tid >> 7;
+  const bool colok = pn < a.Nr;
+  const int pnc = colok ? pn : 0;
   float db = 0.0f;
   float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
-  float dzs[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
-  float pcol[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
-  if (a.dz) {
+  float dzs = 0.f;  // column pn's dz sum (pn < MAXPROJ only)
+  __shared__ float Ps[MAXPROJ * 128];  // projection columns (kept in LDS: saves 4 VGPRs per thread)
+  if constexpr (PROJ) {
+    if (tid < 128) {
 #pragma unroll
-    for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (q < a.nproj && pn < a.Nr) ? a.proj[q * a.Nr + pn] : 0.0f;
+      for (int q = 0; q < MAXPROJ; ++q) Ps[q * 128 + tid] = (q < a.nproj && tid < a.Nr) ? a.proj[q * a.Nr + tid] : 0.0f;
+    }
+    __syncthreads();  // Ps is read by every thread's first store_chunk
   }
+  constexpr int NRG = TN_THREADS / 128;              // prologue row groups
+  constexpr int GR = MC / NRG;                       // prologue rows per thread
+  // A staging: 32 threads per chunk row; thread owns columns (tl*AVEC + 32*AVEC*j), j < AJ
+  constexpr int TPR = TN_THREADS / MC;               // threads per row (32)
+  constexpr int AJ = KMAX / (TPR * AVEC);            // vectors per thread per row
+  const int ar = tid / TPR;                          // this thread's chunk row
+  const int tl = tid - ar * TPR;
+  float rg_in[GR][PROJ ? MAXPROJ : 1];
+  float rh[GR];
+  float ra[AJ][AVEC];
 
-  for (int64_t m0 = mbeg; m0 < mend; m0 += MC) {
-    // ---- G chunk (prologue: recompute ReLU/dropout backward, side sums)
+  auto load_chunk = [&](int64_t m0) {
 #pragma unroll
-    for (int i = 0; i < MC / 4; ++i) {
-      const int r = rg * (MC / 4) + i;
-      const int64_t m = m0 + r;
-      float g = 0.0f;
-      if (m < mend && pn < a.Nr) {
-        float dzv[MAXPROJ];
-        if (a.dz) {
-#pragma unroll
-          for (int q = 0; q < MAXPROJ; ++q) dzv[q] = q < a.nproj ? a.dz[m * a.lddz + q] : 0.0f;
-          g = dzv[0] * pcol[0];
-#pragma unroll
-          for (int q = 1; q < MAXPROJ; ++q) g = fmaf(dzv[q], pcol[q], g);
+    for (int i = 0; i < GR; ++i) {
+      int64_t m = m0 + rg * GR + i;
+      m = m < mend ? m : mend - 1;  // clamped: always a valid row, masked in store_chunk
+      if constexpr (PROJ) {
+        if (a.nproj == 4 && (a.lddz & 3) == 0) {
+          float4 t = *reinterpret_cast<const float4*>(a.dz + m * a.lddz);
+          rg_in[i][0] = t.x; rg_in[i][1] = t.y; rg_in[i][2] = t.z; rg_in[i][3] = t.w;
         } else {
-          g = a.g[m * a.ldg + pn];
-        }
-        if (a.h) {
-          const float hv = a.h[m * a.ldh + pn];
-          g = hv > 0.0f ? g * a.hscale : 0.0f;
-          if (a.dz) {
 #pragma unroll
-            for (int q = 0; q < MAXPROJ; ++q) dw2[q] = fmaf(dzv[q], hv, dw2[q]);
-          }
+          for (int q = 0; q < MAXPROJ; ++q) rg_in[i][q] = a.dz[m * a.lddz + (q < a.nproj ? q : 0)];
         }
-        if (a.dz && pn == 0) {
+      } else {
+        rg_in[i][0] = a.g[m * a.ldg + pnc];
+      }
+      if constexpr (MASK) rh[i] = a.h[m * a.ldh + pnc];
+    }
+    int64_t m = m0 + ar;
+    m = m < mend ? m : mend - 1;
+    const float* b1 = a.a1 + m * a.lda1;
+    const float* b2 = a.a2 + m * a.lda2 - a.k1;
 #pragma unroll
-          for (int q = 0; q < MAXPROJ; ++q) dzs[q] += dzv[q];
+    for (int j = 0; j < AJ; ++j) {
+      const int k = tl * AVEC + TPR * AVEC * j;
+      const float* src = k < a.k1 ? b1 + k : (k < Kc ? b2 + k : b1);
+      if constexpr (AVEC == 2) {
+        float2 t = *reinterpret_cast<const float2*>(src);
+        ra[j][0] = t.x; ra[j][1] = t.y;
+      } else {
+        ra[j][0] = *src;
+      }
+    }
+  };
+
+  auto store_chunk = [&](int64_t m0, int buf) {
+#pragma unroll
+    for (int i = 0; i < GR; ++i) {
+      const int r = rg * GR + i;
+      const bool rok = m0 + r < mend;
+      const bool ok = rok && colok;
+      float g;
+      if constexpr (PROJ) {
+        g = rg_in[i][0] * Ps[pn];
+#pragma unroll
+        for (int q = 1; q < MAXPROJ; ++q) g = fmaf(rg_in[i][q], Ps[q * 128 + pn], g);
+      } else {
+        g = rg_in[i][0];
+      }
+      if constexpr (MASK) {
+        g = rh[i] > 0.0f ? g * a.hscale : 0.0f;
+        if constexpr (PROJ) {
+#pragma unroll
+          for (int q = 0; q < MAXPROJ; ++q) dw2[q] = fmaf(ok ? rg_in[i][q] : 0.0f, rh[i], dw2[q]);
         }
-        db += g;
-        if (a.gout) a.gout[m * a.ldgout + pn] = g;
       }
-      Gs[r * 128 + pn] = g;
-    }
-    // ---- A chunk: rows m0.., columns [0, Kc) of [A1 | A2], zero padded to nkt*32
-    const int kpad = nkt * 32;
-    for (int v = tid; v < MC * kpad; v += 512) {
-      const int r = v / kpad;
-      const int k = v - r * kpad;
-      const int64_t m = m0 + r;
-      float x = 0.0f;
-      if (m < mend) {
-        if (k < a.k1) x = a.a1[m * a.lda1 + k];
-        else if (k < Kc) x = a.a2[m * a.lda2 + (k - a.k1)];
+      if constexpr (PROJ) {
+        if (pn < MAXPROJ) dzs += rok ? rg_in[i][pn] : 0.0f;  // lanes 0..3 of each row group own one dz column
       }
-      As[r * TN_APITCH + k] = x;
+      g = ok ? g : 0.0f;
+      db += g;
+      if (a.gout && ok) a.gout[(m0 + r) * a.ldgout + pn] = g;
+      Gs[buf][r * 128 + pn] = g;
     }
+    const bool rok = m0 + ar < mend;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const int k = tl * AVEC + TPR * AVEC * j;
+      const bool ok = rok && k < Kc;
+      if constexpr (AVEC == 2) {
+        *reinterpret_cast<float2*>(&As[buf][ar * TN_APITCH + k]) = make_float2(ok ? ra[j][0] : 0.0f, ok ? ra[j][1] : 0.0f);
+      } else {
+        As[buf][ar * TN_APITCH + k] = ok ? ra[j][0] : 0.0f;
+      }
+    }
+  };
+
+  if (mbeg < mend) {
+    load_chunk(mbeg);
+    store_chunk(mbeg, 0);
     __syncthreads();
-    // ---- MFMA: dW[ntile rows][k tiles] += Gᵀ · A over these MC rows
-    const float* gptr = Gs + (lane >> 5) * 128 + ntile * 32 + (lane & 31);
-    const float* aptr = As + (lane >> 5) * TN_APITCH + (lane & 31);
-    for (int s = 0; s < MC / 2; ++s) {
-      const float gf = gptr[2 * s * 128];
-#pragma unroll
-      for (int t = 0; t < KT_PER_WAVE; ++t) {
-        if (kt0 + t < nkt) {
-          const float af = aptr[2 * s * TN_APITCH + (kt0 + t) * 32];
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(gf, af, acc[t], 0, 0, 0);
-        }
+    int buf = 0;
+    for (int64_t m0 = mbeg; m0 < mend; m0 += MC) {
+      const bool more = m0 + MC < mend;
+      if (more) load_chunk(m0 + MC);
+      const float* gptr = Gs[buf] + (lane >> 5) * 128 + ntile * 32 + (lane & 31);
+      const float* aptr = As[buf] + (lane >> 5) * TN_APITCH + (lane & 31);
+      switch (ntl) {
+        case 3: tn_mma<MC, 3>(acc, gptr, aptr, kt0); break;
+        case 2: tn_mma<MC, 2>(acc, gptr, aptr, kt0); break;
+        case 1: tn_mma<MC, 1>(acc, gptr, aptr, kt0); break;
+        default: break;
       }
+      if (more) store_chunk(m0 + MC, buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
     }
-    __syncthreads();
   }
 
   // ---- write this block's partial dW
@@ -354,49 +489,67 @@ __global__ __launch_bounds__(512) void gemm_tn_kernel(TNArgs a) {
       if (row < a.Nr && col < Kc) slab[(int64_t)row * Kc + col] = acc[t][r];
     }
   }
-  // ---- side sums: reduce the 4 row groups through LDS (fixed order)
-  const int ns = 1 + MAXPROJ;
+  // ---- side sums: reduce the 4 row groups through LDS (fixed order); reuse Gs as scratch
+  float* red = &As[0][0];  // 2*MC*KMAX >= NRG*128*(1+MAXPROJ) floats for MC >= 16
+  static_assert(2 * MC * TN_APITCH >= (TN_THREADS / 128) * 128 * (1 + MAXPROJ), "side-sum scratch");
+  constexpr int ns = 1 + MAXPROJ;
+  __syncthreads();
   red[(rg * 128 + pn) * ns + 0] = db;
 #pragma unroll
   for (int q = 0; q < MAXPROJ; ++q) red[(rg * 128 + pn) * ns + 1 + q] = dw2[q];
   __syncthreads();
-  if (tid < 128 && pn < a.Nr) {
+  if (tid < 128 && colok) {
     float* side = slab + (int64_t)a.Nr * Kc;
-    float s = 0.f;
-    for (int g2 = 0; g2 < 4; ++g2) s += red[(g2 * 128 + pn) * ns];
-    side[pn] = s;
+    float s2 = 0.f;
+    for (int g2 = 0; g2 < NRG; ++g2) s2 += red[(g2 * 128 + pn) * ns];
+    side[pn] = s2;
     for (int q = 0; q < a.nproj; ++q) {
       float w = 0.f;
-      for (int g2 = 0; g2 < 4; ++g2) w += red[(g2 * 128 + pn) * ns + 1 + q];
+      for (int g2 = 0; g2 < NRG; ++g2) w += red[(g2 * 128 + pn) * ns + 1 + q];
       side[a.Nr + q * a.Nr + pn] = w;
     }
   }
   __syncthreads();
-  // dzsum: only pn == 0 threads (one per row group) accumulated it
-  if (pn == 0) {
-#pragma unroll
-    for (int q = 0; q < MAXPROJ; ++q) red[rg * MAXPROJ + q] = dzs[q];
-  }
+  if (pn < MAXPROJ) red[rg * MAXPROJ + pn] = dzs;
   __syncthreads();
   if (tid < a.nproj) {
-    float s = 0.f;
-    for (int g2 = 0; g2 < 4; ++g2) s += red[g2 * MAXPROJ + tid];
-    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = s;
+    float s2 = 0.f;
+    for (int g2 = 0; g2 < NRG; ++g2) s2 += red[g2 * MAXPROJ + tid];
+    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = s2;
   }
 }
 
-// out[j] = Σ_b slab[b][j]   (fixed block order: deterministic)
+// out[j] = Σ_b slab[b][j]   (fixed block order: deterministic).  4 consecutive outputs per
+// thread (float4; slab stride is a multiple of 64 floats) and 4 independent slab streams in
+// flight, summed in block order.
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int64_t stride, int nblk,
                                                           float* __restrict__ out, int64_t n) {
-  int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
   if (j >= n) return;
-  float s = 0.0f;
-  for (int b = 0; b < nblk; ++b) s += slab[(int64_t)b * stride + j];
-  out[j] = s;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int b = 0;
+  for (; b + 4 <= nblk; b += 4) {
+    float4 v0 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 0) * stride + j);
+    float4 v1 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 1) * stride + j);
+    float4 v2 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 2) * stride + j);
+    float4 v3 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 3) * stride + j);
+    s.x = (((s.x + v0.x) + v1.x) + v2.x) + v3.x;
+    s.y = (((s.y + v0.y) + v1.y) + v2.y) + v3.y;
+    s.z = (((s.z + v0.z) + v1.z) + v2.z) + v3.z;
+    s.w = (((s.w + v0.w) + v1.w) + v2.w) + v3.w;
+  }
+  for (; b < nblk; ++b) {
+    float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)b * stride + j);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  if (j + 0 < n) out[j + 0] = s.x;
+  if (j + 1 < n) out[j + 1] = s.y;
+  if (j + 2 < n) out[j + 2] = s.z;
+  if (j + 3 < n) out[j + 3] = s.w;
 }
 
 int tn_blocks(int64_t M) {
-  int64_t chunks = ceil_div(M, MC);
+  int64_t chunks = ceil_div(M, 32);
   int64_t nb = chunks < 256 ? chunks : 256;
   return (int)(nb > 0 ? nb : 1);
 }
@@ -406,15 +559,15 @@ int tn_blocks(int64_t M) {
 
 using namespace gnnmp;
 
-extern "C" gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream) {
-  if (!p) return fail(GNN_ERR_INVALID_ARG, __func__, "null params");
+static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn_stream_t stream, const char* fn) {
+  if (!p) return fail(GNN_ERR_INVALID_ARG, fn, "null params");
   if (p->M < 0 || p->N < 1 || p->k1 < 1 || p->k2 < 0 || !p->a1 || !p->bt || (p->k2 > 0 && !p->a2))
-    return fail(GNN_ERR_INVALID_ARG, __func__, "bad shapes / null operands");
+    return fail(GNN_ERR_INVALID_ARG, fn, "bad shapes / null operands");
   if (p->lda1 < p->k1 || (p->k2 > 0 && p->lda2 < p->k2) || p->ldb < p->N || (p->c && p->ldc < p->N))
-    return fail(GNN_ERR_INVALID_ARG, __func__, "bad leading dimensions");
+    return fail(GNN_ERR_INVALID_ARG, fn, "bad leading dimensions");
   if (p->nproj < 0 || p->nproj > 4 || (p->nproj > 0 && (p->N > BN || !p->proj || !p->z || p->ldz < p->nproj)))
-    return fail(GNN_ERR_INVALID_ARG, __func__, "projection needs N <= 128, nproj <= 4, proj and z");
-  if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout p in [0,1)");
+    return fail(GNN_ERR_INVALID_ARG, fn, "projection needs N <= 128, nproj <= 4, proj and z");
+  if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, fn, "dropout p in [0,1)");
   if (p->M == 0) return GNN_OK;
   NTArgs a{};
   a.M = p->M; a.Nc = (int32_t)p->N;
@@ -431,13 +584,20 @@ extern "C" gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t 
             (a.k2 == 0 || ((a.k2 % 4 == 0) && (a.lda2 % 4 == 0) && al(a.a2, 16)));
   bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al(a.a1, 8) &&
             (a.k2 == 0 || ((a.k2 % 2 == 0) && (a.lda2 % 2 == 0) && al(a.a2, 8)));
-  dim3 grid((unsigned)ceil_div(p->M, BM), (unsigned)ceil_div(p->N, BN));
   hipStream_t st = (hipStream_t)stream;
-  if (v4) gemm_nt_kernel<4><<<grid, 256, 0, st>>>(a);
-  else if (v2) gemm_nt_kernel<2><<<grid, 256, 0, st>>>(a);
-  else gemm_nt_kernel<1><<<grid, 256, 0, st>>>(a);
-  GNN_LAUNCH_CHECK();
-  return GNN_OK;
+  if (v4) launch_nt_variant<4>(a, variant, st);
+  else if (v2) launch_nt_variant<2>(a, variant, st);
+  else launch_nt_variant<1>(a, variant, st);
+  return hip_check(hipGetLastError(), fn);
+}
+
+extern "C" gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream) {
+  return gemm_nt_dispatch(p, 0, stream, __func__);
+}
+
+// Tuning entry (not part of the public ABI): run NT tiling variant `variant`.
+extern "C" gnn_status gnnx_gemm_nt_variant_f32(const gnn_gemm_nt_params* p, int variant, gnn_stream_t stream) {
+  return gemm_nt_dispatch(p, variant, stream, __func__);
 }
 
 extern "C" gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t Kc, int32_t nproj, size_t* bytes) {
@@ -480,10 +640,20 @@ extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, v
   a.a1 = p->a1; a.lda1 = p->lda1; a.k1 = (int32_t)p->k1;
   a.a2 = p->a2; a.lda2 = p->lda2; a.k2 = (int32_t)p->k2;
   a.slab = static_cast<float*>(workspace); a.slab_stride = stride;
-  a.rows_per_block = ceil_div(ceil_div(p->M, MC), nblk) * MC;
-  gemm_tn_kernel<<<nblk, 512, 0, st>>>(a);
+  a.rows_per_block = ceil_div(ceil_div(p->M, 32), nblk) * 32;  // multiple of both chunk sizes
+  auto al8 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0; };
+  const bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al8(a.a1) &&
+                  (a.k2 == 0 || ((a.k2 % 2 == 0) && (a.lda2 % 2 == 0) && al8(a.a2)));
+  const bool proj = a.dz != nullptr, mask = a.h != nullptr;
+#define GNN_TN(P, MK, V, R) gemm_tn_kernel<P, MK, V, R><<<nblk, TN_THREADS, 0, st>>>(a)
+  // the dz·P + mask prologue holds twice the staging registers: 16-row chunks keep it spill-free
+  if (proj && mask) { if (v2) GNN_TN(true, true, 2, 16); else GNN_TN(true, true, 1, 16); }
+  else if (proj) { if (v2) GNN_TN(true, false, 2, 32); else GNN_TN(true, false, 1, 32); }
+  else if (mask) { if (v2) GNN_TN(false, true, 2, 32); else GNN_TN(false, true, 1, 32); }
+  else { if (v2) GNN_TN(false, false, 2, 32); else GNN_TN(false, false, 1, 32); }
+#undef GNN_TN
   GNN_LAUNCH_CHECK();
-  slab_reduce_kernel<<<(unsigned)ceil_div(n_out, 256), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+  slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), 256), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }
