@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
     return ap.parse_args()
 
 
@@ -149,22 +150,31 @@ def main():
     torch.manual_seed(42)  # identical initial weights on every rank
     model = SAGENet(data.x.size(1), hidden_dim=128, layers=2, dropout=0.5).to(dev)
     state0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4)
+    use_graph = not args.no_graph
+    opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4, capturable=use_graph)
     cw, denom = gdist.global_class_weight_and_count(data.y, data.train_mask, dist)
     loss_fn = _make_loss_fn({}, cw, model, 1, 34)
     bucket = gdist.GradBucket(model) if dist is not None else None
+    tidx = data.train_idx
+    ytr = data.y.index_select(0, tidx)
 
-    def step():
+    def eager_step():
         model.train()
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=bucket is None)
         logits = model(data.x, data.edge_index)
-        loss = loss_fn(logits[data.train_mask], data.y[data.train_mask], denom=denom)
+        loss = loss_fn(logits.index_select(0, tidx), ytr, denom=denom)
         loss.backward()
         if bucket is not None:
             bucket.allreduce_(dist)
         torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
         opt.step()
         return loss
+
+    if use_graph:
+        from elliptic_gnn_project_amd.train_gnn import CapturedStep
+        step = CapturedStep(eager_step)
+    else:
+        step = eager_step
 
     for _ in range(args.warmup):
         step()
@@ -189,7 +199,7 @@ def main():
     if not args.no_roofline:
         KernelTimer.start()
         for _ in range(5):
-            step()
+            eager_step()
         recs = KernelTimer.stop()
         roof = roofline(recs)
 
@@ -217,6 +227,7 @@ def main():
                             "full-batch train step (fwd+masked CE+bwd+clip+Adam)",
                 "nodes_per_gpu": data.x.size(0), "edges_per_gpu": E, "feats": data.x.size(1),
                 "parallelism": f"dp{world} timestep-partitioned" if world > 1 else "single",
+                "launch": "hip-graph replay of the whole step" if use_graph else "eager",
             },
             "roofline": roof,
             "cpu_baseline": cpu,

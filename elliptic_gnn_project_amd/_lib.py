@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # gnn_status
 GNN_OK = 0
@@ -81,6 +81,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("relu", c_i32),
         ("dropout_p", ctypes.c_float),
         ("seed", ctypes.c_uint64),
+        ("seed_ptr", c_ptr),
         ("proj", c_ptr), ("nproj", c_i32), ("z", c_ptr), ("ldz", c_i64),
     ]
 

@@ -7,13 +7,12 @@
 //   GCNConv:  message edge_weight * x_j, aggr='add', edge_weight = dinv[j]*dinv[i]  (gnn.py:28,31)
 //   GATConv:  message alpha * x_j per head (gnn.py:72,75)
 //
-// Mapping (CDNA4): one wave64 per destination row; the row's slot range and neighbour
-// ids are wave-uniform (scalar loads); lanes stride the F features with VEC-wide
-// (float2/float4) loads so each gathered row is read as contiguous 256-1024 B
-// wave-instructions.  Slots are summed in plan order (PyG edge order) with one
-// accumulator per feature: no atomics, bitwise reproducible.  Loads of up to 4
-// neighbours are issued before their adds to keep several rows in flight per wave.
-// Rows with F <= 8 (e.g. 2-class logits) use one lane per row instead.
+// Mapping (CDNA4): lanes stride the F features with VEC-wide (float2/float4) loads so each
+// gathered row is read as contiguous 256-1024 B wave-instructions; a lane group walks the
+// slots of several consecutive rows flat, keeping 4 neighbour rows in flight (see
+// agg_flat_kernel).  Slots are summed in plan order (PyG edge order) with one accumulator
+// per feature: no atomics, bitwise reproducible.  Rows with F <= 8 (2-class logits) use a
+// group of 8 lanes per row with lanes over slots instead.
 #include "common.hpp"
 
 namespace gnnmp {
@@ -112,47 +111,202 @@ __device__ __forceinline__ void finish(const AggArgs& a, int64_t r, int f0, floa
   }
 }
 
-// One wave per row; 4 waves per 256-thread block; grid-stride over rows.
-template <int MODE, int VEC>
-__global__ __launch_bounds__(256) void agg_rowwave_kernel(AggArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+// Wide rows (F > 8): flat-slot walk.  A group of LPS lanes (LPS = the power of two that
+// covers F/VEC chunks, or 64 with NCH chunks per lane) owns RPG consecutive rows and walks
+// their slots U at a time: U neighbour ids, then U·NCH row-chunk loads are all issued before
+// any add, regardless of where rows begin and end.  Row boundaries come from rowptrs held in
+// the group's lanes (no global load on the flush path); a row is flushed (mean divide,
+// root addend, bias, ReLU, store) when the walk passes its end, empty rows included.  Slots
+// are added in plan order: each output is the sequential edge-order sum PyG computes.
+constexpr int kU = 4;
+
+template <int MODE, int VEC, int LPS, int NCHMAX>
+__global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
+  const int gl = threadIdx.x & (LPS - 1);
+  const int gbase = (threadIdx.x & 63) & ~(LPS - 1);
+  const int64_t group = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPS;
+  const int64_t r0 = group * rpg;
+  if (r0 >= a.nrows) return;  // group-uniform
+  const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
   const int nchunk = a.F / VEC;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.nrows; r += (int64_t)gridDim.x * 4) {
-    const int32_t beg = __builtin_amdgcn_readfirstlane(a.ptr[r]);
-    const int32_t end = __builtin_amdgcn_readfirstlane(a.ptr[r + 1]);
-    for (int c = lane; c < nchunk; c += 64) {
-      const int f0 = c * VEC;
-      float acc[VEC];
+  const int nch = (nchunk + LPS - 1) / LPS;
+  const int32_t myptr = a.ptr[r0 + min(gl, nrow)];
+  float mydeg = 1.0f;
+  if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[r0 + min(gl, nrow - 1)];
+  auto ptr_at = [&](int j) { return __shfl(myptr, gbase + j); };
+
+  float acc[NCHMAX][VEC];
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) acc[q] = 0.0f;
-      int32_t k = beg;
-      for (; k + 4 <= end; k += 4) {
-        int32_t n0 = a.nbr[k], n1 = a.nbr[k + 1], n2 = a.nbr[k + 2], n3 = a.nbr[k + 3];
-        float v0[VEC], v1[VEC], v2[VEC], v3[VEC];
-        vload<VEC>(a.x + (int64_t)n0 * a.ldx + f0, v0);
-        vload<VEC>(a.x + (int64_t)n1 * a.ldx + f0, v1);
-        vload<VEC>(a.x + (int64_t)n2 * a.ldx + f0, v2);
-        vload<VEC>(a.x + (int64_t)n3 * a.ldx + f0, v3);
-        contrib<MODE, VEC>(a, n0, (int32_t)r, k, f0, v0);
-        contrib<MODE, VEC>(a, n1, (int32_t)r, k + 1, f0, v1);
-        contrib<MODE, VEC>(a, n2, (int32_t)r, k + 2, f0, v2);
-        contrib<MODE, VEC>(a, n3, (int32_t)r, k + 3, f0, v3);
+  for (int i = 0; i < NCHMAX; ++i)
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) acc[q] = (((acc[q] + v0[q]) + v1[q]) + v2[q]) + v3[q];
+    for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+
+  auto flush = [&](int j) {
+    const int64_t r = r0 + j;
+    float d = 1.0f;
+    if constexpr (MODE == GNN_AGG_MEAN) d = fmaxf(__shfl(mydeg, gbase + j), 1.0f);
+#pragma unroll
+    for (int i = 0; i < NCHMAX; ++i) {
+      const int c = gl + LPS * i;
+      if (i < nch && c < nchunk) {
+        const int f0 = c * VEC;
+        float t[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) t[q] = (MODE == GNN_AGG_MEAN) ? acc[i][q] / d : acc[i][q];
+        if (a.add) {
+          float ad[VEC];
+          vload<VEC>(a.add + r * a.ld_add + f0, ad);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += ad[q];
+        }
+        if (a.bias) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += a.bias[f0 + q];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] = fmaxf(t[q], 0.0f);
+        }
+        vstore<VEC>(a.y + r * a.ldy + f0, t);
       }
-      for (; k < end; ++k) {
-        int32_t n = a.nbr[k];
-        float v[VEC];
-        vload<VEC>(a.x + (int64_t)n * a.ldx + f0, v);
-        contrib<MODE, VEC>(a, n, (int32_t)r, k, f0, v);
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) acc[q] += v[q];
+      for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+    }
+  };
+
+  const int32_t send = ptr_at(nrow);
+  int j = 0;
+  int32_t cend = ptr_at(1);
+  for (int32_t s = ptr_at(0); s < send; s += kU) {
+    int32_t n[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) n[u] = a.nbr[s + u < send ? s + u : s];
+    float v[kU][NCHMAX][VEC];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int i = 0; i < NCHMAX; ++i)
+        if (i < nch) {
+          const int c = gl + LPS * i;
+          vload<VEC>(a.x + (int64_t)n[u] * a.ldx + (c < nchunk ? c : 0) * VEC, v[u][i]);
+        }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int32_t k = s + u;
+      if (k >= send) break;
+      while (k >= cend) {  // passing one or more row ends (empty rows flush zeros)
+        flush(j);
+        ++j;
+        cend = ptr_at(j + 1);
       }
-      finish<MODE, VEC>(a, r, f0, acc);
-      vstore<VEC>(a.y + r * a.ldy + f0, acc);
+#pragma unroll
+      for (int i = 0; i < NCHMAX; ++i)
+        if (i < nch) {
+          contrib<MODE, VEC>(a, n[u], (int32_t)(r0 + j), k, (gl + LPS * i) * VEC, v[u][i]);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];
+        }
     }
   }
+  for (; j < nrow; ++j) flush(j);  // the last open row and any trailing empty rows
+}
+
+// Wave-wide groups (LPS = 64, F/VEC > 32 chunks, e.g. the 166-wide layer-1 features):
+// every row boundary and neighbour id is wave-uniform, so they live in SGPRs (scalar loads,
+// v_readlane) and the next U neighbour ids are prefetched while the current U rows load.
+template <int MODE, int VEC, int NCH>
+__global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
+  constexpr int U = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t r0 = wave * rpg;
+  if (r0 >= a.nrows) return;
+  const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
+  const int nchunk = a.F / VEC;
+  const int32_t myptr = a.ptr[r0 + min(lane, nrow)];
+  float mydeg = 1.0f;
+  if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[r0 + min(lane, nrow - 1)];
+  int coff[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + 64 * i;
+    coff[i] = (c < nchunk ? c : 0) * VEC;
+  }
+  float acc[NCH][VEC];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+
+  auto flush = [&](int j) {
+    const int64_t r = r0 + j;
+    float d = 1.0f;
+    if constexpr (MODE == GNN_AGG_MEAN) d = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mydeg), j)), 1.0f);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nchunk) {
+        const int f0 = c * VEC;
+        float t[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) t[q] = (MODE == GNN_AGG_MEAN) ? acc[i][q] / d : acc[i][q];
+        if (a.add) {
+          float ad[VEC];
+          vload<VEC>(a.add + r * a.ld_add + f0, ad);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += ad[q];
+        }
+        if (a.bias) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += a.bias[f0 + q];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] = fmaxf(t[q], 0.0f);
+        }
+        vstore<VEC>(a.y + r * a.ldy + f0, t);
+      }
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+    }
+  };
+
+  const int32_t sbeg = __builtin_amdgcn_readlane(myptr, 0);
+  const int32_t send = __builtin_amdgcn_readlane(myptr, nrow);
+  int j = 0;
+  int32_t cend = __builtin_amdgcn_readlane(myptr, 1);
+  int32_t n[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) n[u] = __builtin_amdgcn_readfirstlane(a.nbr[min(sbeg + u, max(send - 1, sbeg))]);
+  for (int32_t s = sbeg; s < send; s += U) {
+    float v[U][NCH][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) vload<VEC>(a.x + (int64_t)n[u] * a.ldx + coff[i], v[u][i]);
+    int32_t nn[U];  // prefetch the next U neighbour ids behind this iteration's row loads
+#pragma unroll
+    for (int u = 0; u < U; ++u) nn[u] = __builtin_amdgcn_readfirstlane(a.nbr[min(s + U + u, send - 1)]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int32_t k = s + u;
+      if (k >= send) break;
+      while (k >= cend) {
+        flush(j);
+        ++j;
+        cend = __builtin_amdgcn_readlane(myptr, j + 1);
+      }
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        contrib<MODE, VEC>(a, n[u], (int32_t)(r0 + j), k, coff[i], v[u][i]);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) n[u] = nn[u];
+  }
+  for (; j < nrow; ++j) flush(j);
 }
 
 // Narrow rows (F <= 8, e.g. 2-class logits): a group of 8 lanes per row, lanes over the
@@ -210,11 +364,34 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st) {
     if (blocks > ((int64_t)1 << 20)) blocks = (int64_t)1 << 20;
     agg_group_kernel<MODE><<<(unsigned)blocks, 256, 0, st>>>(a);
   } else {
-    int64_t blocks = ceil_div(a.nrows, 4);
-    if (blocks > (int64_t)1 << 20) blocks = (int64_t)1 << 20;
-    if (vec == 4) agg_rowwave_kernel<MODE, 4><<<(unsigned)blocks, 256, 0, st>>>(a);
-    else if (vec == 2) agg_rowwave_kernel<MODE, 2><<<(unsigned)blocks, 256, 0, st>>>(a);
-    else agg_rowwave_kernel<MODE, 1><<<(unsigned)blocks, 256, 0, st>>>(a);
+    const int nchunk = a.F / vec;
+    int lps = 64;
+    if (nchunk <= 8) lps = 8;
+    else if (nchunk <= 16) lps = 16;
+    else if (nchunk <= 32) lps = 32;
+    if (nchunk > 64 * 4) return fail(GNN_ERR_UNSUPPORTED, "gnn_aggregate_f32", "F too wide for the gather kernel");
+    const int rpg = lps == 8 ? 7 : 8;
+    const int64_t groups = ceil_div(a.nrows, rpg);
+    const unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
+#define GNN_FLAT(V, L, NC) agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg)
+#define GNN_FLAT_V(V)                      \
+  do {                                     \
+    if (lps == 64) GNN_FLAT(V, 64, 4);     \
+    else if (lps == 32) GNN_FLAT(V, 32, 1); \
+    else if (lps == 16) GNN_FLAT(V, 16, 1); \
+    else GNN_FLAT(V, 8, 1);                \
+  } while (0)
+    if (lps == 64 && nchunk <= 128) {  // wave-uniform fast path (scalar row/neighbour handling)
+      const int rpw = 16;
+      const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
+      if (vec == 4) agg_wave_kernel<MODE, 4, 2><<<wblocks, 256, 0, st>>>(a, rpw);
+      else if (vec == 2) agg_wave_kernel<MODE, 2, 2><<<wblocks, 256, 0, st>>>(a, rpw);
+      else agg_wave_kernel<MODE, 1, 2><<<wblocks, 256, 0, st>>>(a, rpw);
+    } else if (vec == 4) GNN_FLAT_V(4);
+    else if (vec == 2) GNN_FLAT_V(2);
+    else GNN_FLAT_V(1);
+#undef GNN_FLAT_V
+#undef GNN_FLAT
   }
   return hip_check(hipGetLastError(), "gnn_aggregate_f32");
 }

@@ -50,7 +50,7 @@ struct NTArgs {
   float* c; int64_t ldc;
   const float* bias;
   int32_t relu;
-  int32_t dropout; uint32_t keep_thresh; float drop_scale; uint64_t seed;
+  int32_t dropout; uint32_t keep_thresh; float drop_scale; uint64_t seed; const uint64_t* seed_ptr;
   const float* proj; int32_t nproj; float* z; int64_t ldz;
 };
 
@@ -180,6 +180,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
   const int nchunks = (a.k1 + KC - 1) / KC + (a.k2 + KC - 1) / KC;
   const bool bvec4 = ((a.ldb & 3) == 0) && ((a.Nc & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.bt) & 15) == 0);
 
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
   floatx16 acc[TM][4];
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
         float v = acc[tm][t][r] + bv;
         if (a.relu) v = fmaxf(v, 0.0f);
         if (a.dropout)
-          v = keep_elem(a.seed, (uint32_t)row * (uint32_t)a.Nc + (uint32_t)col, a.keep_thresh) ? v * a.drop_scale : 0.0f;
+          v = keep_elem(seed, (uint32_t)row * (uint32_t)a.Nc + (uint32_t)col, a.keep_thresh) ? v * a.drop_scale : 0.0f;
         if (!colok) v = 0.0f;
         if (a.c && row < a.M && colok) a.c[row * a.ldc + col] = v;
         acc[tm][t][r] = v;
@@ -578,6 +579,7 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   a.keep_thresh = (uint32_t)((1.0 - (double)p->dropout_p) * 16777216.0);
   a.drop_scale = a.dropout ? (float)(1.0 / (1.0 - (double)p->dropout_p)) : 1.0f;
   a.seed = p->seed;
+  a.seed_ptr = p->seed_ptr;
   a.proj = p->proj; a.nproj = p->nproj; a.z = p->z; a.ldz = p->ldz;
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
   bool v4 = (a.k1 % 4 == 0) && (a.lda1 % 4 == 0) && al(a.a1, 16) &&

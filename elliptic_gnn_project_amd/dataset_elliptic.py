@@ -151,6 +151,18 @@ def prepare_inputs(data: GraphData, cfg: Dict, split: Optional[Dict] = None) -> 
         data.x = torch.cat([data.x, tnorm], dim=1)
     if cfg.get("symmetrize_edges", False):
         data.edge_index = torch.cat([data.edge_index, data.edge_index.flip(0)], dim=1)
+    index_masks(data)
+    return data
+
+
+def index_masks(data: GraphData) -> GraphData:
+    """Row indices of the split masks, computed once.  ``logits[mask]`` on a device needs a
+    nonzero() and a host sync every call; ``logits.index_select(0, idx)`` is the same rows in
+    the same order with neither (and its backward is a scatter, not a sort)."""
+    for name in ("train", "val", "test"):
+        m = getattr(data, f"{name}_mask", None)
+        if m is not None:
+            setattr(data, f"{name}_idx", torch.nonzero(m, as_tuple=False).flatten())
     return data
 
 

@@ -36,7 +36,7 @@ def _ld(t: torch.Tensor) -> int:
 
 
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
-            out=None, want_c=True):
+            out=None, want_c=True, seed_ptr=None):
     """C = epilogue([a1 | a2] · bt) on the MFMA NT kernel."""
     M = a1.size(0)
     if out is None and want_c:
@@ -47,7 +47,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.ptr(a2), _ld(a2) if a2 is not None else 0, a2.size(1) if a2 is not None else 0,
         bt.data_ptr(), _ld(bt),
         _lib.ptr(out), _ld(out) if out is not None else 0,
-        _lib.ptr(bias), int(relu), float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF,
+        _lib.ptr(bias), int(relu), float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ptr),
         _lib.ptr(proj), proj.size(0) if proj is not None else 0, _lib.ptr(z), _ld(z) if z is not None else 0,
     )
     if KernelTimer.active:
@@ -105,7 +105,7 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
 class _FusedSAGE(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, x, plan: GraphPlan, dropout_p: float, seeds: List[int], *params):
+    def forward(ctx, x, plan: GraphPlan, dropout_p: float, seeds: List[int], seed_ctr, *params):
         L = len(params) // 3
         Wl = params[0::3]
         bl = params[1::3]
@@ -125,7 +125,8 @@ class _FusedSAGE(torch.autograd.Function):
             if last_hidden:
                 z = torch.empty((h.size(0), 2 * C), dtype=torch.float32, device=h.device)
             hn = gemm_nt(agg, bt, Wl[l].size(0), a2=h, bias=bl[l], relu=True, dropout_p=train_drop,
-                         seed=seeds[l], proj=P if last_hidden else None, z=z if last_hidden else None)
+                         seed=seeds[l], proj=P if last_hidden else None, z=z if last_hidden else None,
+                         seed_ptr=seed_ctr)
             aggs.append(agg)
             hs.append(hn)
         logits = aggregate(plan, z[:, :C], _lib.AGG_MEAN, nodew=plan.deg, addend=z[:, C:], bias=bl[-1])
@@ -177,7 +178,7 @@ class _FusedSAGE(torch.autograd.Function):
                                addend=dA[:, fi:])
                 g = dh  # next (lower) layer's upstream gradient w.r.t. h_l, masked inside TN
         dx = g if need_x else None
-        return (dx, None, None, None, *grads)
+        return (dx, None, None, None, None, *grads)
 
 
 def fusable(model) -> bool:
@@ -194,12 +195,41 @@ def fusable(model) -> bool:
     return 2 * convs[-1].out_channels <= MAX_PROJ and convs[-1].in_channels <= 128
 
 
+_SEED_CTR = {}
+
+
+def _graph_seed_counter(device: torch.device) -> torch.Tensor:
+    """Per-device int64 dropout counter for HIP-graph capture.
+
+    Eager calls draw fresh seeds from torch's CPU generator (respects torch.manual_seed).  Under
+    stream capture a host-drawn seed would be frozen into the graph, so the forward instead
+    bumps this device counter (an add_ recorded in the graph) and the kernel derives the
+    seed from it on every replay.
+    """
+    c = _SEED_CTR.get(device)
+    if c is None:  # a fill kernel (capture-safe); start value from the seed without consuming the RNG
+        c = torch.full((1,), (torch.initial_seed() * 0x9E3779B97F4A7C15 + 1) % (2 ** 62), dtype=torch.int64,
+                       device=device)
+        _SEED_CTR[device] = c
+    return c
+
+
 def sage_forward(model, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
     plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
     L = len(model.convs)
     p = float(model.dropout) if model.training else 0.0
-    seeds = torch.randint(0, 2 ** 62, (L,), dtype=torch.int64).tolist() if p > 0 else [0] * L
+    ctr = None
+    if p > 0 and torch.cuda.is_current_stream_capturing():
+        ctr = _graph_seed_counter(x.device)
+        ctr.add_(1)
+        seeds = [l + 1 for l in range(L)]  # per-layer salts
+    elif p > 0:
+        if x.is_cuda:
+            _graph_seed_counter(x.device)  # create it outside any capture (a fill inside would replay)
+        seeds = torch.randint(0, 2 ** 62, (L,), dtype=torch.int64).tolist()
+    else:
+        seeds = [0] * L
     params = []
     for c in model.convs:
         params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]
-    return _FusedSAGE.apply(x, plan, p, seeds, *params)
+    return _FusedSAGE.apply(x, plan, p, seeds, ctr, *params)

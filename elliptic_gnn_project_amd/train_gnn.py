@@ -131,14 +131,20 @@ def _autocast(device, enabled: bool):
 
 
 # ----------------------------------------------------------------------------- loops
+def _rows(t: torch.Tensor, data, split: str) -> torch.Tensor:
+    """t[data.<split>_mask] via the precomputed index when available (no per-step host sync)."""
+    idx = getattr(data, f"{split}_idx", None)
+    return t.index_select(0, idx) if idx is not None else t[getattr(data, f"{split}_mask")]
+
+
 def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cfg, device, sync=True):
     """One full-batch step (src/train_gnn.py:187-209).  ``sync=False`` keeps the loss on device."""
     model.train()
     optimizer.zero_grad(set_to_none=True)
     with _autocast(device, use_amp):
         logits = model(data.x, edge_index, data.timestep if _model_uses_time_embed(model) else None)
-        t_idx = data.timestep[data.train_mask] if cfg.get("time_loss_weighting", "none") != "none" else None
-        loss = loss_fn(logits[data.train_mask], data.y[data.train_mask], t_idx)
+        t_idx = _rows(data.timestep, data, "train") if cfg.get("time_loss_weighting", "none") != "none" else None
+        loss = loss_fn(_rows(logits, data, "train"), _rows(data.y, data, "train"), t_idx)
     scaler.scale(loss).backward()
     if cfg.get("grad_clip", 0) and cfg["grad_clip"] > 0:
         scaler.unscale_(optimizer)
@@ -147,6 +153,31 @@ def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cf
     scaler.update()
     optimizer.zero_grad(set_to_none=True)
     return float(loss.item()) if sync else loss.detach()
+
+
+class CapturedStep:
+    """A training step captured once into a HIP graph and replayed (torch.cuda.CUDAGraph).
+
+    ``step_fn`` must be capture-safe: static input tensors, no host syncs, optimizer built
+    with ``capturable=True``.  The fused SAGE path switches its dropout seed to a device
+    counter under capture, so every replay draws a new mask.  Replaying removes the host's
+    per-kernel launch cost (≈40 launches per step) and the gaps between kernels.
+    """
+
+    def __init__(self, step_fn, warmup: int = 3):
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                step_fn()
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = step_fn()
+
+    def __call__(self):
+        self.graph.replay()
+        return self.out
 
 
 @torch.no_grad()

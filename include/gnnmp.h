@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 1
+#define GNNMP_ABI_VERSION 2
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -172,7 +172,9 @@ typedef struct {
   const float* bias;                     /* [N] or NULL */
   int32_t relu;                          /* max(., 0) after bias */
   float dropout_p;                       /* after ReLU; 0 = off.  keep if hash(seed, row*N+col) < 1-p */
-  uint64_t seed;
+  uint64_t seed;                         /* per-call salt (the seed itself when seed_ptr is NULL) */
+  const uint64_t* seed_ptr;              /* optional device counter: seed = *seed_ptr * golden + seed
+                                            (graph-replay safe: bump the counter inside the graph) */
   const float* proj; int32_t nproj;      /* optional Z = C · projᵀ, proj [nproj, N], nproj <= 4, N <= 128 */
   float* z; int64_t ldz;
 } gnn_gemm_nt_params;
