@@ -109,8 +109,6 @@ class _SyncBNFn(torch.autograd.Function):
         ctx.save_for_backward(xhat, invstd, weight)
         ctx.n = n
         ctx.dist = dist
-        ctx.unbiased = var * n / torch.clamp(n - 1, min=1)
-        ctx.mean = mean
         return xhat * weight + bias
 
     @staticmethod
@@ -137,11 +135,10 @@ class SyncBatchNorm1d(nn.BatchNorm1d):
         if not self.training or d is None:
             return super().forward(x)
         y = _SyncBNFn.apply(x, self.weight, self.bias, self.eps, d)
-        with torch.no_grad():  # running stats as BatchNorm1d (momentum, unbiased var)
+        with torch.no_grad():  # running stats as BatchNorm1d: momentum update, unbiased variance
             m = self.momentum if self.momentum is not None else 0.1
-            fn = torch.no_grad()
-            stats = torch.cat([x.sum(0), (x * x).sum(0), torch.tensor([float(x.size(0))], device=x.device,
-                                                                       dtype=x.dtype)])
+            n_local = torch.tensor([float(x.size(0))], device=x.device, dtype=x.dtype)
+            stats = torch.cat([x.sum(0), (x * x).sum(0), n_local])
             d.all_reduce(stats)
             C = x.size(1)
             n = stats[2 * C]
@@ -150,7 +147,6 @@ class SyncBatchNorm1d(nn.BatchNorm1d):
             self.running_mean.mul_(1 - m).add_(m * mean)
             self.running_var.mul_(1 - m).add_(m * var)
             self.num_batches_tracked += 1
-            del fn
         return y
 
 

@@ -292,3 +292,24 @@ def test_full_elliptic_sage_preset(device):
     with torch.no_grad():
         out2 = model(data.x.to(device), data.edge_index.to(device))
     assert torch.equal(out, out2)
+
+
+@pytest.mark.parametrize("arch", ["sage", "gcn", "gat"])
+def test_golden_fixture_through_hip(device, arch):
+    """The committed golden vectors (tests/golden) replayed through the HIP models."""
+    from pathlib import Path
+
+    from elliptic_gnn_project_amd.train_gnn import build_model
+
+    with np.load(Path(__file__).resolve().parent / "golden" / "elliptic600.npz") as z:
+        x = torch.from_numpy(z["x"])
+        ei = torch.from_numpy(z["edge_index"])
+        state = {k.split("/", 1)[1]: torch.from_numpy(z[k]).float() for k in z.files if k.startswith(arch + "/convs.")}
+        hidden = {"sage": 128, "gcn": 64, "gat": 64}[arch]
+        model = build_model(arch, x.size(1), dict(hidden_dim=hidden, layers=2, dropout=0.5, heads=4)).to(device)
+        model.load_state_dict(state)
+        model.eval()
+        with torch.no_grad():
+            out = model(x.to(device), ei.to(device)).cpu().numpy()
+        np.testing.assert_allclose(out, z[f"{arch}/logits_f32"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(out, z[f"{arch}/logits_f64"], rtol=1e-5, atol=1e-5)
