@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a HIP graph")
+    ap.add_argument("--graph", action="store_true", help="replay the step as one captured HIP graph")
     return ap.parse_args()
 
 
@@ -150,8 +150,8 @@ def main():
     torch.manual_seed(42)  # identical initial weights on every rank
     model = SAGENet(data.x.size(1), hidden_dim=128, layers=2, dropout=0.5).to(dev)
     state0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    use_graph = not args.no_graph
-    opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4, capturable=use_graph)
+    use_graph = args.graph
+    opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4, fused=True, capturable=use_graph)
     cw, denom = gdist.global_class_weight_and_count(data.y, data.train_mask, dist)
     loss_fn = _make_loss_fn({}, cw, model, 1, 34)
     bucket = gdist.GradBucket(model) if dist is not None else None

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # gnn_status
 GNN_OK = 0
@@ -76,6 +76,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("a1", c_ptr), ("lda1", c_i64), ("k1", c_i64),
         ("a2", c_ptr), ("lda2", c_i64), ("k2", c_i64),
         ("bt", c_ptr), ("ldb", c_i64),
+        ("w1", c_ptr), ("w2", c_ptr), ("ldw1", c_i64), ("ldw2", c_i64),
         ("c", c_ptr), ("ldc", c_i64),
         ("bias", c_ptr),
         ("relu", c_i32),

@@ -354,12 +354,74 @@ __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
   }
 }
 
+// Narrow rows, slot-parallel (F <= 4; MEAN / MEAN_BWD / SUM): a wave owns 64 consecutive rows
+// (one per lane).  Their slots are staged through LDS with lanes over SLOTS — neighbour ids
+// and the F-wide neighbour rows of 64 slots per instruction, all in flight together — and then
+// each lane adds its own row's slots from LDS in edge order (sequential, deterministic).
+constexpr int kNarrowCap = 256;  // slots staged per pass per wave
+template <int MODE>
+__global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
+  __shared__ float sv[4][kNarrowCap * 4];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + w) * 64;
+  if (r0 >= a.nrows) return;  // wave-uniform; no block barriers below
+  const int64_t r = r0 + lane;
+  const bool rok = r < a.nrows;
+  const int32_t pbeg = a.ptr[rok ? r : a.nrows];
+  const int32_t pend = a.ptr[rok ? r + 1 : a.nrows];
+  const int32_t base = __builtin_amdgcn_readfirstlane(a.ptr[r0]);
+  const int64_t rlast = min(r0 + 64, a.nrows);
+  const int32_t wend = __builtin_amdgcn_readfirstlane(a.ptr[rlast]);
+  const int F = a.F;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float* buf = sv[w];
+  for (int32_t pb = base; pb < wend; pb += kNarrowCap) {
+    const int32_t pe = min(pb + kNarrowCap, wend);
+#pragma unroll
+    for (int i = 0; i < kNarrowCap / 64; ++i) {
+      const int32_t k = pb + lane + 64 * i;
+      const int32_t kc = k < pe ? k : pb;
+      const int32_t n = a.nbr[kc];
+      const float* xr = a.x + (int64_t)n * a.ldx;
+      float d = 1.0f;
+      if constexpr (MODE == GNN_AGG_MEAN_BWD) d = fmaxf(a.nodew[n], 1.0f);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        float v = f < F ? xr[f] : 0.0f;
+        if constexpr (MODE == GNN_AGG_MEAN_BWD) v = v / d;
+        buf[f * kNarrowCap + lane + 64 * i] = v;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    const int32_t lo = max(pbeg, pb), hi = min(pend, pe);
+    for (int32_t k = lo; k < hi; ++k) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[f] += buf[f * kNarrowCap + (k - pb)];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (rok) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      if (f < F) {
+        float t[1] = {acc[f]};
+        finish<MODE, 1>(a, r, f, t);
+        a.y[r * a.ldy + f] = t[0];
+      }
+    }
+  }
+}
+
 bool aligned(const void* p, int bytes) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0; }
 
 template <int MODE>
 gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st) {
   if (a.nrows == 0 || a.F == 0) return GNN_OK;
-  if (a.F <= 8) {
+  if (a.F <= 4 && (MODE == GNN_AGG_MEAN || MODE == GNN_AGG_MEAN_BWD || MODE == GNN_AGG_SUM)) {
+    agg_narrow_lds_kernel<MODE><<<(unsigned)ceil_div(a.nrows, 256), 256, 0, st>>>(a);
+  } else if (a.F <= 8) {
     int64_t blocks = ceil_div(a.nrows * kGroup, 256);
     if (blocks > ((int64_t)1 << 20)) blocks = (int64_t)1 << 20;
     agg_group_kernel<MODE><<<(unsigned)blocks, 256, 0, st>>>(a);

@@ -109,6 +109,18 @@ int main(int argc, char** argv) {
     std::printf("NT variant %d: fused-epilogue %8.1f us (%6.1f TF)   plain %8.1f us (%6.1f TF)\n", v, a,
                 flops / a * 1e-6, b, flops / b * 1e-6);
   }
+  // B read in place from Linear weights W1/W2 [H, F] (the production forward form)
+  {
+    float* w = dev_rand(2 * F * H, 0.08f, 7);
+    gnn_gemm_nt_params pw = p;
+    pw.bt = nullptr; pw.w1 = w; pw.w2 = w + F * H; pw.ldw1 = F; pw.ldw2 = F;
+    for (int v : {0, 4, 1}) {
+      std::vector<float> tw;
+      for (int r = 0; r < rounds; ++r) tw.push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&pw, v, nullptr); }, 5));
+      float a = med(tw);
+      std::printf("NT variant %d w1/w2 form: fused-epilogue %8.1f us (%6.1f TF)\n", v, a, flops / a * 1e-6);
+    }
+  }
   // TN (dz form + mask), the backward weight-gradient shape
   gnn_gemm_tn_params q{};
   q.M = M; q.Nr = H; q.dz = dz; q.lddz = 4; q.proj = proj; q.nproj = 4; q.h = c; q.ldh = H; q.hscale = 2.f;

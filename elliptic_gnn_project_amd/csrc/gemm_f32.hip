@@ -40,6 +40,7 @@ __device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t idx, uint32_t 
 namespace {
 
 constexpr int BN = 128;  // NT block columns (4 waves stacked by rows, each wave 4 x 32 columns)
+constexpr int BNP = BN + 2;  // LDS pitch of the B tile: 2P = 4 mod 32 makes the transposed weight stores (8 lanes x float2 per row) conflict-free
 
 struct NTArgs {
   int64_t M;
@@ -47,6 +48,8 @@ struct NTArgs {
   const float* a1; int64_t lda1; int32_t k1;
   const float* a2; int64_t lda2; int32_t k2;
   const float* bt; int64_t ldb;
+  const float* w1; const float* w2; int64_t ldw1, ldw2;  // alternative B: W1 [Nc, k1], W2 [Nc, k2]
+  int32_t wvec2;                                          // W rows 8-byte aligned, k1/k2 even
   float* c; int64_t ldc;
   const float* bias;
   int32_t relu;
@@ -101,6 +104,29 @@ __device__ __forceinline__ void nt_load(const NTArgs& a, int c, int64_t m0, int 
       ra[i] = *p;
     }
   }
+  if (a.w1) {
+    // B from PyTorch Linear weights W [Nc, K] read in place (no transposed copy): 8 lanes cover
+    // KC consecutive k of one weight row with float2 loads (4·KC contiguous bytes).
+    const bool seg1 = c < (a.k1 + KC - 1) / KC;
+    const float* W = seg1 ? a.w1 : a.w2;
+    const int64_t ldw = seg1 ? a.ldw1 : a.ldw2;
+#pragma unroll
+    for (int i = 0; i < S::B_PER_THREAD / 2; ++i) {
+      const int v = threadIdx.x + 256 * i;  // float2 slots: 128 rows x KC/2
+      const int n = v / (KC / 2);
+      const int kk = (v % (KC / 2)) * 2;
+      const int nn = n0 + n < a.Nc ? n0 + n : 0;
+      const float* p = W + (int64_t)nn * ldw + k0 + (kk < klen ? kk : 0);
+      if (a.wvec2) {
+        float2 t = *reinterpret_cast<const float2*>(p);
+        rb[2 * i] = t.x; rb[2 * i + 1] = t.y;
+      } else {
+        rb[2 * i] = p[0];
+        rb[2 * i + 1] = p[kk + 1 < klen ? 1 : 0];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < S::B_PER_THREAD / 4; ++i) {
     const int v = threadIdx.x + 256 * i;  // float4 slots: KC rows x 32
@@ -135,15 +161,25 @@ __device__ __forceinline__ void nt_store(const NTArgs& a, int c, int64_t m0, int
 #pragma unroll
     for (int q = 0; q < AVEC; ++q) As[r * S::APITCH + k + q] = ok ? ra[i * AVEC + q] : 0.0f;
   }
+  if (a.w1) {
+#pragma unroll
+    for (int i = 0; i < S::B_PER_THREAD / 2; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      const int n = v / (KC / 2);
+      const int kk = (v % (KC / 2)) * 2;
+      const bool nok = n0 + n < a.Nc;
+      Bs[kk * BNP + n] = (nok && kk < klen) ? rb[2 * i] : 0.0f;
+      Bs[(kk + 1) * BNP + n] = (nok && kk + 1 < klen) ? rb[2 * i + 1] : 0.0f;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < S::B_PER_THREAD / 4; ++i) {
     const int v = threadIdx.x + 256 * i;
     const int kk = v >> 5;
     const int n = (v & 31) * 4;
-    float w[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) w[q] = (kk < klen && n0 + n + q < a.Nc) ? rb[i * 4 + q] : 0.0f;
-    *reinterpret_cast<float4*>(&Bs[kk * BN + n]) = make_float4(w[0], w[1], w[2], w[3]);
+    for (int q = 0; q < 4; ++q) Bs[kk * BNP + n + q] = (kk < klen && n0 + n + q < a.Nc) ? rb[i * 4 + q] : 0.0f;
   }
 }
 
@@ -159,7 +195,7 @@ __device__ __forceinline__ void nt_kstep(floatx16 (&acc)[TM][4], const float* Aw
   float af[TM];
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) af[tm] = Aw[tm * 32 * apitch + 2 * s];
-  const float* b = Bw + 2 * s * BN;
+  const float* b = Bw + 2 * s * BNP;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const float bf = b[t * 32];
@@ -172,7 +208,7 @@ template <int AVEC, int KC, int TM, bool UNR>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
   using S = NTShape<KC, TM>;
   __shared__ float As[2][S::BM * S::APITCH];
-  __shared__ __attribute__((aligned(16))) float Bs[2][KC * BN];
+  __shared__ float Bs[2][KC * BNP];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t m0 = (int64_t)blockIdx.x * S::BM;
@@ -198,7 +234,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
     const int buf = c & 1;
     if (c + 1 < nchunks) nt_load<AVEC, KC, TM>(a, c + 1, m0, n0, bvec4, ra, rb);
     const float* Aw = As[buf] + (wave * 32 * TM + (lane & 31)) * S::APITCH + (lane >> 5);
-    const float* Bw = Bs[buf] + (lane >> 5) * BN + (lane & 31);
+    const float* Bw = Bs[buf] + (lane >> 5) * BNP + (lane & 31);
     const int ks = nt_ksteps<KC>(a, c);
     if (UNR && ks == KC / 2) {
 #pragma unroll
@@ -487,7 +523,10 @@ __global__ __launch_bounds__(TN_THREADS) void gemm_tn_kernel(TNArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < a.Nr && col < Kc) slab[(int64_t)row * Kc + col] = acc[t][r];
+      // segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2], each contiguous
+      const int64_t idx = col < a.k1 ? (int64_t)row * a.k1 + col
+                                     : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (col - a.k1);
+      if (row < a.Nr && col < Kc) slab[idx] = acc[t][r];
     }
   }
   // ---- side sums: reduce the 4 row groups through LDS (fixed order); reuse Gs as scratch
@@ -520,33 +559,50 @@ __global__ __launch_bounds__(TN_THREADS) void gemm_tn_kernel(TNArgs a) {
   }
 }
 
-// out[j] = Σ_b slab[b][j]   (fixed block order: deterministic).  4 consecutive outputs per
-// thread (float4; slab stride is a multiple of 64 floats) and 4 independent slab streams in
-// flight, summed in block order.
+// out[j] = Σ_b slab[b][j], deterministic.  A 256-thread block owns 16 float4 outputs; its 16
+// thread rows each sum a fixed 1/16 of the slabs (4 independent loads in flight), and the 16
+// partials are combined through LDS in slab order.  ~700 blocks: the whole chip streams the
+// slabs instead of one thread per output walking all of them.
+constexpr int kRedOut = 16, kRedGrp = 16;
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int64_t stride, int nblk,
                                                           float* __restrict__ out, int64_t n) {
-  int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
-  if (j >= n) return;
+  __shared__ float4 part[kRedGrp][kRedOut];
+  const int o = threadIdx.x & (kRedOut - 1);
+  const int g = threadIdx.x / kRedOut;
+  const int64_t j = ((int64_t)blockIdx.x * kRedOut + o) * 4;
+  const int per = (nblk + kRedGrp - 1) / kRedGrp;
+  const int b0 = g * per, b1 = min(nblk, b0 + per);
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  int b = 0;
-  for (; b + 4 <= nblk; b += 4) {
-    float4 v0 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 0) * stride + j);
-    float4 v1 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 1) * stride + j);
-    float4 v2 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 2) * stride + j);
-    float4 v3 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 3) * stride + j);
-    s.x = (((s.x + v0.x) + v1.x) + v2.x) + v3.x;
-    s.y = (((s.y + v0.y) + v1.y) + v2.y) + v3.y;
-    s.z = (((s.z + v0.z) + v1.z) + v2.z) + v3.z;
-    s.w = (((s.w + v0.w) + v1.w) + v2.w) + v3.w;
+  if (j < n) {
+    int b = b0;
+    for (; b + 4 <= b1; b += 4) {
+      float4 v0 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 0) * stride + j);
+      float4 v1 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 1) * stride + j);
+      float4 v2 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 2) * stride + j);
+      float4 v3 = *reinterpret_cast<const float4*>(slab + (int64_t)(b + 3) * stride + j);
+      s.x = (((s.x + v0.x) + v1.x) + v2.x) + v3.x;
+      s.y = (((s.y + v0.y) + v1.y) + v2.y) + v3.y;
+      s.z = (((s.z + v0.z) + v1.z) + v2.z) + v3.z;
+      s.w = (((s.w + v0.w) + v1.w) + v2.w) + v3.w;
+    }
+    for (; b < b1; ++b) {
+      float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)b * stride + j);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
   }
-  for (; b < nblk; ++b) {
-    float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)b * stride + j);
-    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  part[g][o] = s;
+  __syncthreads();
+  if (g == 0 && j < n) {
+    float4 t = part[0][o];
+    for (int q = 1; q < kRedGrp; ++q) {
+      float4 v = part[q][o];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    if (j + 0 < n) out[j + 0] = t.x;
+    if (j + 1 < n) out[j + 1] = t.y;
+    if (j + 2 < n) out[j + 2] = t.z;
+    if (j + 3 < n) out[j + 3] = t.w;
   }
-  if (j + 0 < n) out[j + 0] = s.x;
-  if (j + 1 < n) out[j + 1] = s.y;
-  if (j + 2 < n) out[j + 2] = s.z;
-  if (j + 3 < n) out[j + 3] = s.w;
 }
 
 int tn_blocks(int64_t M) {
@@ -562,9 +618,13 @@ using namespace gnnmp;
 
 static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn_stream_t stream, const char* fn) {
   if (!p) return fail(GNN_ERR_INVALID_ARG, fn, "null params");
-  if (p->M < 0 || p->N < 1 || p->k1 < 1 || p->k2 < 0 || !p->a1 || !p->bt || (p->k2 > 0 && !p->a2))
+  if (p->M < 0 || p->N < 1 || p->k1 < 1 || p->k2 < 0 || !p->a1 || (p->k2 > 0 && !p->a2))
     return fail(GNN_ERR_INVALID_ARG, fn, "bad shapes / null operands");
-  if (p->lda1 < p->k1 || (p->k2 > 0 && p->lda2 < p->k2) || p->ldb < p->N || (p->c && p->ldc < p->N))
+  if (!p->bt && !(p->w1 && (p->k2 == 0 || p->w2)))
+    return fail(GNN_ERR_INVALID_ARG, fn, "need bt or w1 (and w2 when k2 > 0)");
+  if (p->w1 && (p->N > BN || p->ldw1 < p->k1 || (p->k2 > 0 && p->ldw2 < p->k2)))
+    return fail(GNN_ERR_INVALID_ARG, fn, "w1/w2 form needs N <= 128 and ldw >= k");
+  if (p->lda1 < p->k1 || (p->k2 > 0 && p->lda2 < p->k2) || (p->bt && p->ldb < p->N) || (p->c && p->ldc < p->N))
     return fail(GNN_ERR_INVALID_ARG, fn, "bad leading dimensions");
   if (p->nproj < 0 || p->nproj > 4 || (p->nproj > 0 && (p->N > BN || !p->proj || !p->z || p->ldz < p->nproj)))
     return fail(GNN_ERR_INVALID_ARG, fn, "projection needs N <= 128, nproj <= 4, proj and z");
@@ -574,7 +634,8 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   a.M = p->M; a.Nc = (int32_t)p->N;
   a.a1 = p->a1; a.lda1 = p->lda1; a.k1 = (int32_t)p->k1;
   a.a2 = p->a2; a.lda2 = p->lda2; a.k2 = (int32_t)p->k2;
-  a.bt = p->bt; a.ldb = p->ldb; a.c = p->c; a.ldc = p->ldc; a.bias = p->bias; a.relu = p->relu;
+  a.bt = p->bt; a.ldb = p->ldb; a.w1 = p->w1; a.w2 = p->w2; a.ldw1 = p->ldw1; a.ldw2 = p->ldw2; a.c = p->c;
+  a.ldc = p->ldc; a.bias = p->bias; a.relu = p->relu;
   a.dropout = p->dropout_p > 0.f;
   a.keep_thresh = (uint32_t)((1.0 - (double)p->dropout_p) * 16777216.0);
   a.drop_scale = a.dropout ? (float)(1.0 / (1.0 - (double)p->dropout_p)) : 1.0f;
@@ -582,6 +643,8 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   a.seed_ptr = p->seed_ptr;
   a.proj = p->proj; a.nproj = p->nproj; a.z = p->z; a.ldz = p->ldz;
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
+  a.wvec2 = a.w1 && (a.ldw1 % 2 == 0) && (a.k1 % 2 == 0) && al(a.w1, 8) &&
+            (a.k2 == 0 || ((a.ldw2 % 2 == 0) && (a.k2 % 2 == 0) && al(a.w2, 8)));
   bool v4 = (a.k1 % 4 == 0) && (a.lda1 % 4 == 0) && al(a.a1, 16) &&
             (a.k2 == 0 || ((a.k2 % 4 == 0) && (a.lda2 % 4 == 0) && al(a.a2, 16)));
   bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al(a.a1, 8) &&
@@ -655,7 +718,7 @@ extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, v
   else { if (v2) GNN_TN(false, false, 2, 32); else GNN_TN(false, false, 1, 32); }
 #undef GNN_TN
   GNN_LAUNCH_CHECK();
-  slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), 256), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+  slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }

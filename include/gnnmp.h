@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 2
+#define GNNMP_ABI_VERSION 3
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -167,7 +167,9 @@ typedef struct {
   int64_t M, N;                          /* C is [M, N] */
   const float* a1; int64_t lda1; int64_t k1;
   const float* a2; int64_t lda2; int64_t k2;   /* optional 2nd K segment: A = [A1 | A2] (k2 = 0: none) */
-  const float* bt; int64_t ldb;          /* [k1+k2, N] row-major (Linear weight transposed) */
+  const float* bt; int64_t ldb;          /* [k1+k2, N] row-major (Linear weight transposed), or NULL and: */
+  const float* w1; const float* w2;      /* ... B read in place from PyTorch Linear weights W1 [N, k1], */
+  int64_t ldw1, ldw2;                    /*     W2 [N, k2] (N <= 128): out = [A1|A2]·[W1|W2]ᵀ, no copy */
   float* c; int64_t ldc;                 /* output (may be NULL when only z is wanted) */
   const float* bias;                     /* [N] or NULL */
   int32_t relu;                          /* max(., 0) after bias */
@@ -194,8 +196,8 @@ typedef struct {
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).
- * out (contiguous): dW [Nr, k1+k2] | db = Σ_m G [Nr] | (dz form) dW2 = dzᵀ·h [nproj, Nr] |
- * dzsum = Σ_m dz [nproj]. */
+ * out (contiguous): dW1 = Gᵀ·A1 [Nr, k1] | dW2 = Gᵀ·A2 [Nr, k2] | db = Σ_m G [Nr] |
+ * (dz form) dWp = dzᵀ·h [nproj, Nr] | dzsum = Σ_m dz [nproj]. */
 gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t Kc, int32_t nproj, size_t* bytes);
 gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* workspace, size_t workspace_bytes,
                            gnn_stream_t stream);

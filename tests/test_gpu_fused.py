@@ -56,6 +56,25 @@ def test_gemm_nt(device, M, k1, k2, n, epi):
         torch.testing.assert_close(z.cpu(), ref @ proj.t(), rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("M,k1,k2,n", [(1000, 166, 166, 128), (300, 7, 9, 33), (4097, 128, 0, 64)])
+def test_gemm_nt_weight_layout(device, M, k1, k2, n):
+    """B read in place from PyTorch Linear weights (w1/w2) == B from the transposed copy."""
+    from elliptic_gnn_project_amd.fused import gemm_nt
+
+    g = torch.Generator().manual_seed(M + n)
+    a1 = torch.randn(M, k1, generator=g)
+    a2 = torch.randn(M, k2, generator=g) if k2 else None
+    w1 = torch.randn(n, k1, generator=g) / (k1 + k2) ** 0.5
+    w2 = torch.randn(n, k2, generator=g) / (k1 + k2) ** 0.5 if k2 else None
+    A = torch.cat([a1, a2], 1) if k2 else a1
+    W = torch.cat([w1, w2], 1) if k2 else w1
+    c = gemm_nt(a1.to(device), None, n, a2=a2.to(device) if k2 else None, w1=w1.to(device),
+                w2=w2.to(device) if k2 else None)
+    c2 = gemm_nt(a1.to(device), W.t().contiguous().to(device), n, a2=a2.to(device) if k2 else None)
+    assert torch.equal(c, c2)
+    torch.testing.assert_close(c.cpu(), A @ W.t(), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("M,nr,k1,k2", [(5000, 128, 166, 166), (777, 3, 20, 0), (64, 128, 128, 128),
                                         (20000, 64, 167, 167), (33, 1, 1, 0)])
 @pytest.mark.parametrize("form", ["g", "g_mask", "dz_mask"])
@@ -82,7 +101,9 @@ def test_gemm_tn(device, M, nr, k1, k2, form):
     gout = torch.empty(M, nr, device=device)
     dW, db, dW2, dzs = gemm_tn(nr, a1.to(device), a2.to(device) if a2 is not None else None, gout=gout, **kw)
     torch.testing.assert_close(gout.cpu(), G, rtol=1e-5, atol=1e-5)
-    assert rel_l2(dW, G.t() @ A) < 1e-5
+    dWfull = torch.cat([dW[0], dW[1]], 1) if dW[1] is not None else dW[0]
+    assert dW[0].is_contiguous()
+    assert rel_l2(dWfull, G.t() @ A) < 1e-5
     assert rel_l2(db, G.sum(0)) < 1e-5
     if form == "dz_mask":
         assert rel_l2(dW2, dz.t() @ h) < 1e-5

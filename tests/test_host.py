@@ -71,7 +71,8 @@ STRUCTS = {
     "gnn_graph": ("GnnGraph", ["num_nodes", "num_slots", "rowptr", "col", "colptr", "row", "csc2csr"]),
     "gnn_agg_params": ("GnnAggParams", ["mode", "transpose", "nodew", "ew", "heads", "addend", "ld_add", "bias",
                                         "relu"]),
-    "gnn_gemm_nt_params": ("GnnGemmNTParams", ["M", "N", "a1", "lda1", "k1", "a2", "lda2", "k2", "bt", "ldb", "c",
+    "gnn_gemm_nt_params": ("GnnGemmNTParams", ["M", "N", "a1", "lda1", "k1", "a2", "lda2", "k2", "bt", "ldb",
+                                               "w1", "w2", "ldw1", "ldw2", "c",
                                                "ldc", "bias", "relu", "dropout_p", "seed", "seed_ptr", "proj",
                                                "nproj", "z", "ldz"]),
     "gnn_gemm_tn_params": ("GnnGemmTNParams", ["M", "Nr", "g", "ldg", "dz", "lddz", "proj", "nproj", "h", "ldh",
