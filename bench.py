@@ -93,6 +93,31 @@ def cpu_baseline(data, state, cw, denom, budget_s: float):
 MFMA_F32_PEAK_TFS = 157.3  # gfx950 dense fp32 MFMA (= vector fp32) peak, MI355X_MICROARCH.md
 
 
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_latest.json")
+
+
+def measured_traffic(tag):
+    """HBM bytes per launch of the bench's dominant kernel from the committed PMC summary
+    (profiles/pmc_summary.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same
+    command, gfx950-corrected).  None when no summary matches the kernel and shape."""
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            rows = json.load(fh)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    if tag[0] == "gemm_nt":
+        M, N = tag[1], tag[3]
+        grid = -(-M // 128) * 256 * -(-N // 128)
+        cand = [r for r in rows if "gemm_nt_kernel" in r["kernel"] and r["grid_threads"] == grid]
+    elif tag[0] == "gemm_tn":
+        cand = [r for r in rows if "gemm_tn_kernel" in r["kernel"]]
+    else:
+        return None
+    if len(cand) != 1 or cand[0]["traffic_bytes"] is None:
+        return None
+    return int(cand[0]["traffic_bytes"])
+
+
 def roofline(recs):
     """Dominant libgnnmp kernel (by total HIP-event time) against its roofline.
 
@@ -119,9 +144,19 @@ def roofline(recs):
         ach = per / (avg_ms * 1e-3) / 1e12
         out = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                "frac": round(ach / MFMA_F32_PEAK_TFS, 4), "traffic": None}
+    out["traffic"] = measured_traffic(tag)
+    if out["traffic"] is not None:
+        out["traffic_source"] = os.path.relpath(TRAFFIC_FILE, ROOT)
+    timed = {}
+    for t, v in recs.items():
+        us = v["ms"] / v["launches"] * 1e3
+        e = {"us_per_launch": round(us, 1), "share": round(v["ms"] / tot, 3)}
+        if t[0] == "agg":  # HBM-bound: algorithmic bytes per launch / duration
+            gbs = v["amount"] / v["launches"] / (us * 1e-6) / 1e9
+            e.update({"hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)})
+        timed[label(t)] = e
     out.update({"kernel": label(tag), "avg_us": round(avg_ms * 1e3, 2), "per_launch": int(per),
-                "timed_kernels": {label(t): {"us_per_launch": round(v["ms"] / v["launches"] * 1e3, 1),
-                                             "share": round(v["ms"] / tot, 3)} for t, v in recs.items()}})
+                "timed_kernels": timed})
     return out
 
 

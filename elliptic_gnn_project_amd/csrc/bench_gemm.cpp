@@ -84,13 +84,13 @@ int main(int argc, char** argv) {
 
   const double flops = 2.0 * M * (2 * F) * H;
   Timer T;
-  const int nvar = 8;
+  const int nvar = 11;
   std::vector<std::vector<float>> t_epi(nvar), t_plain(nvar);
   // correctness: every variant must agree bitwise with variant 0 (same k-ordered fmaf chain)
   std::vector<float> ref(M * H), got(M * H);
   GK(gnnx_gemm_nt_variant_f32(&p, 0, nullptr));
   CK(hipMemcpy(ref.data(), c, M * H * 4, hipMemcpyDeviceToHost));
-  for (int v = 1; v < nvar; ++v) {
+  for (int v = 1; v < 8; ++v) {
     GK(gnnx_gemm_nt_variant_f32(&p, v, nullptr));
     CK(hipMemcpy(got.data(), c, M * H * 4, hipMemcpyDeviceToHost));
     size_t bad = 0;

@@ -204,7 +204,7 @@ __device__ __forceinline__ void nt_kstep(floatx16 (&acc)[TM][4], const float* Aw
   }
 }
 
-template <int AVEC, int KC, int TM, bool UNR>
+template <int AVEC, int KC, int TM, bool UNR, int EXP = 0>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
   using S = NTShape<KC, TM>;
   __shared__ float As[2][S::BM * S::APITCH];
@@ -232,17 +232,18 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
 
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
-    if (c + 1 < nchunks) nt_load<AVEC, KC, TM>(a, c + 1, m0, n0, bvec4, ra, rb);
+    if (EXP != 1 && EXP != 3 && c + 1 < nchunks) nt_load<AVEC, KC, TM>(a, c + 1, m0, n0, bvec4, ra, rb);
     const float* Aw = As[buf] + (wave * 32 * TM + (lane & 31)) * S::APITCH + (lane >> 5);
     const float* Bw = Bs[buf] + (lane >> 5) * BNP + (lane & 31);
     const int ks = nt_ksteps<KC>(a, c);
-    if (UNR && ks == KC / 2) {
+    if (EXP == 2) {
+    } else if (UNR && ks == KC / 2) {
 #pragma unroll
       for (int s = 0; s < KC / 2; ++s) nt_kstep<TM>(acc, Aw, Bw, s, S::APITCH);
     } else {
       for (int s = 0; s < ks; ++s) nt_kstep<TM>(acc, Aw, Bw, s, S::APITCH);
     }
-    if (c + 1 < nchunks) nt_store<AVEC, KC, TM>(a, c + 1, m0, n0, As[buf ^ 1], Bs[buf ^ 1], ra, rb);
+    if (EXP != 3 && c + 1 < nchunks) nt_store<AVEC, KC, TM>(a, c + 1, m0, n0, As[buf ^ 1], Bs[buf ^ 1], ra, rb);
     __syncthreads();
   }
 
@@ -306,10 +307,10 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
   }
 }
 
-template <int AVEC, int KC, int TM, bool UNR>
+template <int AVEC, int KC, int TM, bool UNR, int EXP = 0>
 void launch_nt(const NTArgs& a, hipStream_t st) {
   dim3 grid((unsigned)ceil_div(a.M, NTShape<KC, TM>::BM), (unsigned)ceil_div(a.Nc, BN));
-  gemm_nt_kernel<AVEC, KC, TM, UNR><<<grid, 256, 0, st>>>(a);
+  gemm_nt_kernel<AVEC, KC, TM, UNR, EXP><<<grid, 256, 0, st>>>(a);
 }
 
 // Variant table (tuning harness csrc/bench_gemm.hip); variant 0 is the production choice.
@@ -323,6 +324,9 @@ void launch_nt_variant(const NTArgs& a, int variant, hipStream_t st) {
     case 5: launch_nt<AVEC, 32, 2, false>(a, st); break;
     case 6: launch_nt<AVEC, 16, 2, true>(a, st); break;
     case 7: launch_nt<AVEC, 16, 2, false>(a, st); break;
+    case 8: launch_nt<AVEC, 16, 1, false, 1>(a, st); break;  // lab: no global loads in the loop
+    case 9: launch_nt<AVEC, 16, 1, false, 2>(a, st); break;  // lab: no MFMAs
+    case 10: launch_nt<AVEC, 16, 1, false, 3>(a, st); break;  // lab: MFMAs + barriers only
     default: launch_nt<AVEC, 16, 1, false>(a, st); break;  // production: measured fastest (r01 lab)
   }
 }
