@@ -32,6 +32,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "edges/s full-batch SAGE fwd+bwd, Elliptic 203k/234k/166-feat, 1→8 MI355X"
+
+# Workloads.  "sage" is the headline (BASELINE.json configs[1]); the others are the other
+# BASELINE configs, run through the same step for the DESIGN.md kernel table.
+PRESETS = {
+    "sage": dict(cfg=dict(arch="sage", hidden_dim=128, layers=2, dropout=0.5, symmetrize_edges=True,
+                          use_time_scalar=True, train_window_k=10),
+                 workload="configs/sage.yaml + symmetrize_edges=true: SAGE 2L 166->128->2, dropout 0.5"),
+    "gcn": dict(cfg=dict(arch="gcn", hidden_dim=64, layers=2, dropout=0.5, symmetrize_edges=False,
+                         use_time_scalar=True, train_window_k=10),
+                workload="BASELINE configs[0] preset on the GPU: GCN 2L 166->64->2, dropout 0.5, self loops"),
+    "gat": dict(cfg=dict(arch="gat", hidden_dim=64, layers=2, heads=4, dropout=0.5, symmetrize_edges=False,
+                         use_time_scalar=True, train_window_k=10),
+                workload="BASELINE configs[2] preset: GAT 2L 4 heads 166->4x16->2, dropout 0.5, self loops"),
+    "sage_resbn": dict(cfg=dict(arch="sage_resbn", hidden_dim=64, layers=3, dropout=0.2, symmetrize_edges=True,
+                                use_time_scalar=False, time_embed_dim=2, time_embed_type="sin",
+                                train_window_k=8, use_bn=True, residual=True),
+                       workload="configs/rec_k8.yaml: SAGE-ResBN 3L 167->64->64->2, BN, sin time embedding"),
+}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -45,28 +63,43 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the step as one captured HIP graph")
+    ap.add_argument("--arch", default="sage", choices=sorted(PRESETS), help="workload (sage = headline)")
     return ap.parse_args()
 
 
-def make_inputs(rank: int, degree: str):
+def make_inputs(rank: int, degree: str, cfg):
     from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
 
     data = synthetic_elliptic(degree=degree, seed=42 + rank)
-    cfg = dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10)
     return prepare_inputs(data, cfg)
 
 
-def cpu_baseline(data, state, cw, denom, budget_s: float):
+def _host_cpu() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(data, state, cw, denom, budget_s: float, cfg):
     """Oracle (PyG-2.5.3 ATen op sequence) train step on the host CPU, same step definition."""
     from oracle import pyg_ref
 
-    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in state.items()}
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in state.items()
+              if v.is_floating_point()}
     opt = torch.optim.Adam(params.values(), lr=0.003, weight_decay=1e-4)
     x, ei, y, m = data.x, data.edge_index, data.y, data.train_mask
+    kw = dict(layers=cfg["layers"], dropout=cfg["dropout"], training=True, heads=cfg.get("heads", 4),
+              time_embed_dim=cfg.get("time_embed_dim", 0), time_embed_type=cfg.get("time_embed_type", "none"),
+              t_idx=data.timestep)
 
     def step():
         opt.zero_grad(set_to_none=True)
-        logits = pyg_ref.model_forward("sage", params, x, ei, layers=2, dropout=0.5, training=True)
+        logits = pyg_ref.model_forward(cfg["arch"], params, x, ei, **kw)
         loss = torch.nn.functional.cross_entropy(logits[m], y[m], weight=cw, reduction="none").sum() / denom
         loss.backward()
         torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
@@ -86,6 +119,7 @@ def cpu_baseline(data, state, cw, denom, budget_s: float):
         "cores": torch.get_num_threads(),
         "kind": "port",
         "sample": f"{n} full-size steps (N={x.size(0)}, E={ei.size(1)}), {el:.1f}s, oracle/pyg_ref.py on CPU",
+        "host_cpu": _host_cpu(),
         "ms_per_step": 1e3 * el / n,
     }
 
@@ -130,13 +164,19 @@ def roofline(recs):
     def label(tag):
         if tag[0] == "agg":
             return f"agg[{names[tag[1]]},{'csc' if tag[2] else 'csr'},F={tag[3]}]"
+        if tag[0].startswith("gat"):
+            return f"{tag[0]}[H={tag[1]},C={tag[2]},out={tag[3]}]"
         return f"{tag[0]}[M={tag[1]},K={tag[2]},N={tag[3]}]"
+
+    if not recs:
+        return None
+    hbm = lambda t: t[0] == "agg" or t[0].startswith("gat")  # noqa: E731
 
     tot = sum(r["ms"] for r in recs.values())
     tag, r = max(recs.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = r["ms"] / r["launches"]
     per = r["amount"] / r["launches"]
-    if tag[0] == "agg":
+    if hbm(tag):
         ach = per / (avg_ms * 1e-3) / 1e9
         out = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
@@ -151,7 +191,7 @@ def roofline(recs):
     for t, v in recs.items():
         us = v["ms"] / v["launches"] * 1e3
         e = {"us_per_launch": round(us, 1), "share": round(v["ms"] / tot, 3)}
-        if t[0] == "agg":  # HBM-bound: algorithmic bytes per launch / duration
+        if hbm(t):  # HBM-bound: algorithmic bytes per launch / duration
             gbs = v["amount"] / v["launches"] / (us * 1e-6) / 1e9
             e.update({"hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)})
         timed[label(t)] = e
@@ -177,13 +217,16 @@ def main():
 
     from elliptic_gnn_project_amd import distributed as gdist
     from elliptic_gnn_project_amd.aggregation import KernelTimer
-    from elliptic_gnn_project_amd.gnn import SAGENet
-    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn
+    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn, build_model
 
-    data_cpu = make_inputs(rank, args.degree)
+    preset = PRESETS[args.arch]
+    cfg = preset["cfg"]
+    data_cpu = make_inputs(rank, args.degree, cfg)
     data = data_cpu.to(dev)
     torch.manual_seed(42)  # identical initial weights on every rank
-    model = SAGENet(data.x.size(1), hidden_dim=128, layers=2, dropout=0.5).to(dev)
+    model = build_model(cfg["arch"], data.x.size(1), cfg).to(dev)
+    if dist is not None:
+        gdist.convert_sync_batchnorm(model, dist)  # exact full-graph BN (SAGE-ResBN); no-op otherwise
     state0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     use_graph = args.graph
     opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4, fused=True, capturable=use_graph)
@@ -191,12 +234,13 @@ def main():
     loss_fn = _make_loss_fn({}, cw, model, 1, 34)
     bucket = gdist.GradBucket(model) if dist is not None else None
     tidx = data.train_idx
+    t_idx = data.timestep if cfg.get("time_embed_dim", 0) > 0 else None
     ytr = data.y.index_select(0, tidx)
 
     def eager_step():
         model.train()
         opt.zero_grad(set_to_none=bucket is None)
-        logits = model(data.x, data.edge_index)
+        logits = model(data.x, data.edge_index, t_idx)
         loss = loss_fn(logits.index_select(0, tidx), ytr, denom=denom)
         loss.backward()
         if bucket is not None:
@@ -240,12 +284,12 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(data_cpu, state0, cw, denom, args.cpu_seconds)
+        cpu = cpu_baseline(data_cpu, state0, cw.cpu(), denom, args.cpu_seconds, cfg)
         cpu["speedup_gpu_over_cpu"] = round(value / cpu["value"], 1)
 
     if rank == 0:
         print(json.dumps({
-            "metric": METRIC,
+            "metric": METRIC if args.arch == "sage" else METRIC.replace("SAGE", args.arch.upper()),
             "value": value,
             "unit": "edges/s",
             "n_gpus": world,
@@ -258,8 +302,7 @@ def main():
             "dtype": "f32",
             "data": f"synthetic Elliptic-shape ({args.degree} in-degree, seed 42+rank)",
             "config": {
-                "workload": "configs/sage.yaml + symmetrize_edges=true: SAGE 2L 166->128->2, dropout 0.5, "
-                            "full-batch train step (fwd+masked CE+bwd+clip+Adam)",
+                "workload": preset["workload"] + ", full-batch train step (fwd+masked CE+bwd+clip+Adam)",
                 "nodes_per_gpu": data.x.size(0), "edges_per_gpu": E, "feats": data.x.size(1),
                 "parallelism": f"dp{world} timestep-partitioned" if world > 1 else "single",
                 "launch": "hip-graph replay of the whole step" if use_graph else "eager",

@@ -36,6 +36,23 @@ class KernelTimer:
         cls.active = True
 
     @classmethod
+    def begin(cls):
+        """Event before a launch (None when inactive); pair with ``end``."""
+        if not cls.active:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    @classmethod
+    def end(cls, e0, tag, amount):
+        if e0 is None:
+            return
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        cls.records.append((tag, e0, e1, int(amount)))
+
+    @classmethod
     def stop(cls):
         cls.active = False
         torch.cuda.synchronize()
@@ -198,9 +215,14 @@ class _GATAttention(torch.autograd.Function):
         fo = heads * chans if concat else chans
         out = torch.empty((N, fo), dtype=torch.float32, device=dev)
         b = bias.contiguous().float() if bias is not None else None
+        t0 = KernelTimer.begin()
         _lib.call("gnn_gat_fwd_f32", plan.c_graph, heads, chans, int(concat), float(slope), xh.data_ptr(),
                   _ld(xh), a_src.data_ptr(), a_dst.data_ptr(), _lib.ptr(b), alpha.data_ptr(), out.data_ptr(),
                   _ld(out), stream)
+        S = plan.num_slots
+        # per slot: id 4 + a_src 4H + xh row 4HC + alpha 4H; per node: rowptr 4 + a_dst 4H + out 4·fo
+        KernelTimer.end(t0, ("gat_fwd", heads, chans, fo),
+                        S * (4 + 8 * heads + 4 * heads * chans) + N * (4 + 4 * heads + 4 * fo))
         ctx.save_for_backward(xh, att_src, att_dst, a_src, a_dst, alpha)
         ctx.meta = (plan, heads, chans, bool(concat), float(slope), bias is not None)
         return out
@@ -220,10 +242,17 @@ class _GATAttention(torch.autograd.Function):
         nb = _lib.c_size(0)
         _lib.call("gnn_gat_bwd_workspace_size", N, plan.num_slots, heads, chans, nb)
         ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+        t0 = KernelTimer.begin()
         _lib.call("gnn_gat_bwd_f32", plan.c_graph, heads, chans, int(concat), slope, xh.data_ptr(), _ld(xh),
                   a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
                   dout.data_ptr(), _ld(dout), dxh.data_ptr(), _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(),
                   ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+        S = plan.num_slots
+        fo = F if concat else chans
+        # rows pass (dα, de per slot): id 4 + alpha 4H + xh row 4HC + de 4H, dout row 4·fo per node;
+        # cols pass (CSC): id+map 8 + alpha/de 8H + dout row 4·fo per slot, dxh 4HC + scores 8H per node
+        KernelTimer.end(t0, ("gat_bwd", heads, chans, fo),
+                        S * (12 + 16 * heads + 4 * heads * chans + 4 * fo) + N * (8 + 16 * heads + 4 * F + 4 * fo))
         db = colsum(dout) if has_bias and ctx.needs_input_grad[3] else None
         return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db, None, None, None, None, None)
 
