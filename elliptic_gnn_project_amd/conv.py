@@ -23,6 +23,7 @@ import torch.nn.functional as F
 from . import _lib
 from .aggregation import colsum, gat_attention, gcn_aggregate, mean_aggregate, aggregate
 from .graph import GraphPlan, get_plan
+from .linear import Linear, linear, linear2
 
 __all__ = ["SAGEConv", "GCNConv", "GATConv"]
 
@@ -87,8 +88,8 @@ class SAGEConv(nn.Module):
         self.out_channels = int(out_channels)
         self.aggr = aggr
         self.order = order
-        self.lin_l = nn.Linear(self.in_channels, self.out_channels, bias=bias)
-        self.lin_r = nn.Linear(self.in_channels, self.out_channels, bias=False)
+        self.lin_l = Linear(self.in_channels, self.out_channels, bias=bias)
+        self.lin_r = Linear(self.in_channels, self.out_channels, bias=False)
 
     def reset_parameters(self) -> None:
         self.lin_l.reset_parameters()
@@ -103,11 +104,11 @@ class SAGEConv(nn.Module):
         if self._transform_first():
             fo = self.out_channels
             w = torch.cat([self.lin_l.weight, self.lin_r.weight], dim=0)
-            y = F.linear(x, w)  # [N, 2*F_out]: MFMA GEMM
+            y = linear(x, w)  # [N, 2*F_out]: MFMA GEMM (K7)
             plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
             return _MeanAggRootBias.apply(y, self.lin_l.bias, plan, fo)
         agg = mean_aggregate(x, edge_index)
-        return self.lin_l(agg) + self.lin_r(x)
+        return linear2(agg, x, self.lin_l.weight, self.lin_r.weight, self.lin_l.bias)  # one K7 GEMM
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, aggr={self.aggr})"
@@ -124,7 +125,7 @@ class GCNConv(nn.Module):
         self.in_channels = int(in_channels)
         self.out_channels = int(out_channels)
         self.cached = cached  # plans are cached per edge_index regardless
-        self.lin = nn.Linear(self.in_channels, self.out_channels, bias=False)
+        self.lin = Linear(self.in_channels, self.out_channels, bias=False)
         self.bias = nn.Parameter(torch.empty(self.out_channels)) if bias else None
         self.reset_parameters()
 
@@ -155,7 +156,7 @@ class GATConv(nn.Module):
         self.heads = int(heads)
         self.concat = bool(concat)
         self.negative_slope = float(negative_slope)
-        self.lin = nn.Linear(self.in_channels, self.heads * self.out_channels, bias=False)
+        self.lin = Linear(self.in_channels, self.heads * self.out_channels, bias=False)
         self.att_src = nn.Parameter(torch.empty(1, self.heads, self.out_channels))
         self.att_dst = nn.Parameter(torch.empty(1, self.heads, self.out_channels))
         nb = self.heads * self.out_channels if self.concat else self.out_channels

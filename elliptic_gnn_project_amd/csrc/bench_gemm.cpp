@@ -6,6 +6,9 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
+#include <cstdlib>
+#include <cmath>
 #include <cstdlib>
 #include <random>
 #include <string>
@@ -61,7 +64,7 @@ struct Timer {
 int main(int argc, char** argv) {
   const int64_t M = argc > 1 ? std::atoll(argv[1]) : 203769;
   const int rounds = argc > 2 ? std::atoi(argv[2]) : 7;
-  const int64_t F = 166, H = 128;
+  const int64_t F = std::getenv("LAB_F") ? std::atoll(std::getenv("LAB_F")) : 166, H = 128;
   float* agg = dev_rand(M * F, 1.f, 1);
   float* x = dev_rand(M * F, 1.f, 2);
   float* bt = dev_rand(2 * F * H, 0.08f, 3);
@@ -84,18 +87,37 @@ int main(int argc, char** argv) {
 
   const double flops = 2.0 * M * (2 * F) * H;
   Timer T;
-  const int nvar = 11;
+  const int nvar = 7;
   std::vector<std::vector<float>> t_epi(nvar), t_plain(nvar);
   // correctness: every variant must agree bitwise with variant 0 (same k-ordered fmaf chain)
   std::vector<float> ref(M * H), got(M * H);
   GK(gnnx_gemm_nt_variant_f32(&p, 0, nullptr));
   CK(hipMemcpy(ref.data(), c, M * H * 4, hipMemcpyDeviceToHost));
-  for (int v = 1; v < 8; ++v) {
+  for (int v = 1; v < nvar; ++v) {
+    if (v >= 4) continue;  // ablations: outputs are meaningless  // ablations: outputs are meaningless
     GK(gnnx_gemm_nt_variant_f32(&p, v, nullptr));
     CK(hipMemcpy(got.data(), c, M * H * 4, hipMemcpyDeviceToHost));
     size_t bad = 0;
-    for (size_t i = 0; i < got.size(); ++i) bad += got[i] != ref[i];
-    std::printf("variant %d mismatches vs 0: %zu\n", v, bad);
+    double maxd = 0.0;
+    for (size_t i = 0; i < got.size(); ++i) {
+      bad += got[i] != ref[i];
+      double d = std::fabs((double)got[i] - (double)ref[i]) / (1e-3 + std::fabs((double)ref[i]));
+      maxd = d > maxd ? d : maxd;
+    }
+    std::printf("variant %d mismatches vs 0: %zu  max rel diff %.2e\n", v, bad, maxd);
+  }
+  // LAB_ONLY=v[,wform]: time one variant only (for rocprofv3 --pmc passes); no other sections
+  if (const char* only = std::getenv("LAB_ONLY")) {
+    const int v = std::atoi(only);
+    gnn_gemm_nt_params q = p;
+    if (std::strchr(only, 'w')) {
+      float* w = dev_rand(2 * F * H, 0.08f, 7);
+      q.bt = nullptr; q.w1 = w; q.w2 = w + F * H; q.ldw1 = F; q.ldw2 = F;
+    }
+    for (int r = 0; r < rounds; ++r) GK(gnnx_gemm_nt_variant_f32(&q, v, nullptr));
+    CK(hipDeviceSynchronize());
+    std::printf("LAB_ONLY %s done\n", only);
+    return 0;
   }
   for (int r = 0; r < rounds; ++r) {
     for (int v = 0; v < nvar; ++v) {
@@ -114,7 +136,7 @@ int main(int argc, char** argv) {
     float* w = dev_rand(2 * F * H, 0.08f, 7);
     gnn_gemm_nt_params pw = p;
     pw.bt = nullptr; pw.w1 = w; pw.w2 = w + F * H; pw.ldw1 = F; pw.ldw2 = F;
-    for (int v : {0, 4, 1}) {
+    for (int v : {0, 1, 2, 3}) {
       std::vector<float> tw;
       for (int r = 0; r < rounds; ++r) tw.push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&pw, v, nullptr); }, 5));
       float a = med(tw);

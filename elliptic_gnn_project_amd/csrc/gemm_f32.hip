@@ -50,6 +50,7 @@ struct NTArgs {
   const float* bt; int64_t ldb;
   const float* w1; const float* w2; int64_t ldw1, ldw2;  // alternative B: W1 [Nc, k1], W2 [Nc, k2]
   int32_t wvec2;                                          // W rows 8-byte aligned, k1/k2 even
+  int32_t wvec;                                           // widest W row vector (1, 2, 4) for the nt2 staging
   float* c; int64_t ldc;
   const float* bias;
   int32_t relu;
@@ -204,50 +205,11 @@ __device__ __forceinline__ void nt_kstep(floatx16 (&acc)[TM][4], const float* Aw
   }
 }
 
-template <int AVEC, int KC, int TM, bool UNR, int EXP = 0>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
-  using S = NTShape<KC, TM>;
-  __shared__ float As[2][S::BM * S::APITCH];
-  __shared__ float Bs[2][KC * BNP];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * S::BM;
-  const int n0 = blockIdx.y * BN;
-  const int nchunks = (a.k1 + KC - 1) / KC + (a.k2 + KC - 1) / KC;
-  const bool bvec4 = ((a.ldb & 3) == 0) && ((a.Nc & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.bt) & 15) == 0);
-
-  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
-  floatx16 acc[TM][4];
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[tm][t][r] = 0.0f;
-
-  float ra[S::A_PER_THREAD], rb[S::B_PER_THREAD];
-  nt_load<AVEC, KC, TM>(a, 0, m0, n0, bvec4, ra, rb);
-  nt_store<AVEC, KC, TM>(a, 0, m0, n0, As[0], Bs[0], ra, rb);
-  __syncthreads();
-
-  for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1;
-    if (EXP != 1 && EXP != 3 && c + 1 < nchunks) nt_load<AVEC, KC, TM>(a, c + 1, m0, n0, bvec4, ra, rb);
-    const float* Aw = As[buf] + (wave * 32 * TM + (lane & 31)) * S::APITCH + (lane >> 5);
-    const float* Bw = Bs[buf] + (lane >> 5) * BNP + (lane & 31);
-    const int ks = nt_ksteps<KC>(a, c);
-    if (EXP == 2) {
-    } else if (UNR && ks == KC / 2) {
-#pragma unroll
-      for (int s = 0; s < KC / 2; ++s) nt_kstep<TM>(acc, Aw, Bw, s, S::APITCH);
-    } else {
-      for (int s = 0; s < ks; ++s) nt_kstep<TM>(acc, Aw, Bw, s, S::APITCH);
-    }
-    if (EXP != 3 && c + 1 < nchunks) nt_store<AVEC, KC, TM>(a, c + 1, m0, n0, As[buf ^ 1], Bs[buf ^ 1], ra, rb);
-    __syncthreads();
-  }
-
-  // ---------------- epilogue: bias, ReLU, dropout, store, optional projection
+// Epilogue shared by the NT kernels: bias, ReLU, dropout, store, optional projection.
+// acc[tm][t] is the 32x32 MFMA tile (rows wave·32·TM + tm·32 .., cols n0 + t·32 ..).
+template <int TM>
+__device__ __forceinline__ void nt_epilogue(const NTArgs& a, floatx16 (&acc)[TM][4], int64_t m0, int n0, int lane,
+                                            int wave, uint64_t seed) {
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     const int64_t rbase = m0 + wave * 32 * TM + tm * 32 + 4 * (lane >> 5);
@@ -308,26 +270,301 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
 }
 
 template <int AVEC, int KC, int TM, bool UNR, int EXP = 0>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
+  using S = NTShape<KC, TM>;
+  __shared__ float As[2][S::BM * S::APITCH];
+  __shared__ float Bs[2][KC * BNP];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * S::BM;
+  const int n0 = blockIdx.y * BN;
+  const int nchunks = (a.k1 + KC - 1) / KC + (a.k2 + KC - 1) / KC;
+  const bool bvec4 = ((a.ldb & 3) == 0) && ((a.Nc & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.bt) & 15) == 0);
+
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+  floatx16 acc[TM][4];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tm][t][r] = 0.0f;
+
+  float ra[S::A_PER_THREAD], rb[S::B_PER_THREAD];
+  nt_load<AVEC, KC, TM>(a, 0, m0, n0, bvec4, ra, rb);
+  nt_store<AVEC, KC, TM>(a, 0, m0, n0, As[0], Bs[0], ra, rb);
+  __syncthreads();
+
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    if (EXP != 1 && EXP != 3 && c + 1 < nchunks) nt_load<AVEC, KC, TM>(a, c + 1, m0, n0, bvec4, ra, rb);
+    const float* Aw = As[buf] + (wave * 32 * TM + (lane & 31)) * S::APITCH + (lane >> 5);
+    const float* Bw = Bs[buf] + (lane >> 5) * BNP + (lane & 31);
+    const int ks = nt_ksteps<KC>(a, c);
+    if (EXP == 2) {
+    } else if (UNR && ks == KC / 2) {
+#pragma unroll
+      for (int s = 0; s < KC / 2; ++s) nt_kstep<TM>(acc, Aw, Bw, s, S::APITCH);
+    } else {
+      for (int s = 0; s < ks; ++s) nt_kstep<TM>(acc, Aw, Bw, s, S::APITCH);
+    }
+    if (EXP != 3 && c + 1 < nchunks) nt_store<AVEC, KC, TM>(a, c + 1, m0, n0, As[buf ^ 1], Bs[buf ^ 1], ra, rb);
+    __syncthreads();
+  }
+
+  nt_epilogue<TM>(a, acc, m0, n0, lane, wave, seed);
+}
+
+template <int AVEC, int KC, int TM, bool UNR, int EXP = 0>
 void launch_nt(const NTArgs& a, hipStream_t st) {
   dim3 grid((unsigned)ceil_div(a.M, NTShape<KC, TM>::BM), (unsigned)ceil_div(a.Nc, BN));
   gemm_nt_kernel<AVEC, KC, TM, UNR, EXP><<<grid, 256, 0, st>>>(a);
+}
+
+// ------------------------------------------------------------ NT, k-permuted b128 fragments
+// Both LDS images are K-contiguous rows — A as [row][k], B as [n][k] (the PyTorch Linear weight
+// layout, so W is staged in place) — with a pitch of KC+4 floats.  MFMA k-step j of k-group g
+// pairs k = 8g+j (lanes 0-31) with k = 8g+4+j (lanes 32-63): each lane fetches the operands of
+// four k-steps with ONE ds_read_b128 (pitch ≡ 20 or 36 mod 64 dwords keeps the b128 lane groups
+// conflict-free), 5 LDS reads per 16 MFMAs instead of 20.  Every k is still summed exactly once
+// per output, in a fixed order, with zero-filled tails in both operands.
+template <int KC>
+struct NT2Shape {
+  static constexpr int BM = 128;
+  static constexpr int P = KC + 4;
+  static constexpr int A_PER_THREAD = BM * KC / 256;
+  static constexpr int B_PER_THREAD = BN * KC / 256;
+};
+
+// Stage rows [r0, r0+128) x [k0, k0+KC) of a K-contiguous row-major operand into registers.
+// Row and k are clamped (loads never depend on data: the prefetch stays in flight).
+template <int VEC, int KC>
+__device__ __forceinline__ void nt2_load_rows(const float* X, int64_t ldx, int64_t r0, int64_t rows, int k0,
+                                              int klen, float* reg) {
+  constexpr int VPR = KC / VEC;
+#pragma unroll
+  for (int i = 0; i < 128 * KC / 256 / VEC; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int r = v / VPR;
+    const int k = (v % VPR) * VEC;
+    int64_t row = r0 + r;
+    row = row < rows ? row : rows - 1;
+    const float* p = X + row * ldx + k0 + (k < klen ? k : 0);
+    if constexpr (VEC == 4) {
+      const float4 t = *reinterpret_cast<const float4*>(p);
+      reg[i * 4 + 0] = t.x; reg[i * 4 + 1] = t.y; reg[i * 4 + 2] = t.z; reg[i * 4 + 3] = t.w;
+    } else if constexpr (VEC == 2) {
+      const float2 t = *reinterpret_cast<const float2*>(p);
+      reg[i * 2 + 0] = t.x; reg[i * 2 + 1] = t.y;
+    } else {
+      reg[i] = *p;
+    }
+  }
+}
+
+template <int VEC, int KC>
+__device__ __forceinline__ void nt2_store_rows(float* L, int64_t r0, int64_t rows, int klen, bool full,
+                                               const float* reg) {
+  constexpr int VPR = KC / VEC;
+  constexpr int P = NT2Shape<KC>::P;
+#pragma unroll
+  for (int i = 0; i < 128 * KC / 256 / VEC; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int r = v / VPR;
+    const int k = (v % VPR) * VEC;
+    const bool ok = full || ((r0 + r < rows) && (k < klen));  // VEC divides klen: all-or-nothing
+    float* d = L + r * P + k;
+    if constexpr (VEC == 4) {
+      *reinterpret_cast<float4*>(d) = ok ? make_float4(reg[i * 4], reg[i * 4 + 1], reg[i * 4 + 2], reg[i * 4 + 3])
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if constexpr (VEC == 2) {
+      *reinterpret_cast<float2*>(d) = ok ? make_float2(reg[i * 2], reg[i * 2 + 1]) : make_float2(0.f, 0.f);
+    } else {
+      *d = ok ? reg[i] : 0.0f;
+    }
+  }
+}
+
+// B from the transposed copy Bt [K, Nc] (N-contiguous): lanes run along k so the transposed
+// scalar LDS stores spread over the banks; k and n are clamped.
+template <int KC>
+__device__ __forceinline__ void nt2_load_bt(const NTArgs& a, int kb0, int klen, int n0, bool bvec4, float* reg) {
+#pragma unroll
+  for (int i = 0; i < BN * KC / 256 / 4; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int kk = v % KC;
+    const int n = (v / KC) * 4;
+    const float* p = a.bt + (int64_t)(kb0 + (kk < klen ? kk : 0)) * a.ldb;
+    if (bvec4) {
+      const int nn = n0 + n < a.Nc ? n0 + n : 0;
+      const float4 t = *reinterpret_cast<const float4*>(p + nn);
+      reg[i * 4 + 0] = t.x; reg[i * 4 + 1] = t.y; reg[i * 4 + 2] = t.z; reg[i * 4 + 3] = t.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) reg[i * 4 + q] = p[n0 + n + q < a.Nc ? n0 + n + q : 0];
+    }
+  }
+}
+
+template <int KC>
+__device__ __forceinline__ void nt2_store_bt(const NTArgs& a, float* L, int klen, int n0, const float* reg) {
+  constexpr int P = NT2Shape<KC>::P;
+#pragma unroll
+  for (int i = 0; i < BN * KC / 256 / 4; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int kk = v % KC;
+    const int n = (v / KC) * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) L[(n + q) * P + kk] = (kk < klen && n0 + n + q < a.Nc) ? reg[i * 4 + q] : 0.0f;
+  }
+}
+
+template <int AVEC, int BVEC, int KC, bool WFORM>
+struct NT2Stage {
+  using S = NT2Shape<KC>;
+  float ra[S::A_PER_THREAD];
+  float rb[S::B_PER_THREAD];
+  __device__ __forceinline__ void load(const NTArgs& a, int c, int64_t m0, int n0, bool bvec4) {
+    const float* A; int64_t lda; int k0, kb0, klen;
+    nt_chunk_range<KC>(a, c, A, lda, k0, kb0, klen);
+    nt2_load_rows<AVEC, KC>(A, lda, m0, a.M, k0, klen, ra);
+    if constexpr (WFORM) {
+      const bool seg1 = c < (a.k1 + KC - 1) / KC;
+      nt2_load_rows<BVEC, KC>(seg1 ? a.w1 : a.w2, seg1 ? a.ldw1 : a.ldw2, n0, a.Nc, k0, klen, rb);
+    } else {
+      nt2_load_bt<KC>(a, kb0, klen, n0, bvec4, rb);
+    }
+  }
+  __device__ __forceinline__ void store(const NTArgs& a, int c, int64_t m0, int n0, float* As, float* Bs) {
+    const float* A; int64_t lda; int k0, kb0, klen;
+    nt_chunk_range<KC>(a, c, A, lda, k0, kb0, klen);
+    const bool kfull = klen == KC;
+    nt2_store_rows<AVEC, KC>(As, m0, a.M, klen, kfull && m0 + S::BM <= a.M, ra);
+    if constexpr (WFORM) nt2_store_rows<BVEC, KC>(Bs, n0, a.Nc, klen, kfull && n0 + BN <= a.Nc, rb);
+    else nt2_store_bt<KC>(a, Bs, klen, n0, rb);
+  }
+};
+
+template <int AVEC, int BVEC, int KC, bool WFORM, int EXP = 0, int DEPTH = 1>
+__global__ __launch_bounds__(256) void gemm_nt2_kernel(NTArgs a) {
+  using S = NT2Shape<KC>;
+  constexpr int P = S::P;
+  __shared__ __attribute__((aligned(16))) float As[2][S::BM * P];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * P];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * S::BM;
+  const int n0 = blockIdx.y * BN;
+  const int nch1 = (a.k1 + KC - 1) / KC;
+  const int nchunks = nch1 + (a.k2 + KC - 1) / KC;
+  const bool bvec4 = !WFORM && ((a.ldb & 3) == 0) && ((a.Nc & 3) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(a.bt) & 15) == 0);
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+
+  floatx16 acc[1][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][t][r] = 0.0f;
+
+  const int foff = (lane & 31) * P + 4 * (lane >> 5);
+  auto compute = [&](const float* Ab, const float* Bb, int c) {
+    const int klen = c < nch1 ? min(KC, a.k1 - c * KC) : min(KC, a.k2 - (c - nch1) * KC);
+    const int ng = (klen + 7) >> 3;
+    const float* Af = Ab + wave * 32 * P + foff;
+    const float* Bf = Bb + foff;
+#pragma unroll
+    for (int g = 0; g < KC / 8; ++g) {
+      if (g < ng) {
+        const float4 av = *reinterpret_cast<const float4*>(Af + 8 * g);
+        float4 bv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bv[t] = *reinterpret_cast<const float4*>(Bf + t * 32 * P + 8 * g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv[t].x, acc[0][t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv[t].y, acc[0][t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv[t].z, acc[0][t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[0][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv[t].w, acc[0][t], 0, 0, 0);
+      }
+    }
+  };
+
+  if constexpr (DEPTH == 1) {
+    NT2Stage<AVEC, BVEC, KC, WFORM> st;
+    st.load(a, 0, m0, n0, bvec4);
+    st.store(a, 0, m0, n0, As[0], Bs[0]);
+    __syncthreads();
+    for (int c = 0; c < nchunks; ++c) {
+      const int buf = EXP >= 4 ? 0 : (c & 1);
+      if ((EXP == 0 || EXP == 6) && c + 1 < nchunks) st.load(a, c + 1, m0, n0, bvec4);
+      compute(As[buf], Bs[buf], c);
+      if ((EXP == 0 || EXP == 7) && c + 1 < nchunks) st.store(a, c + 1, m0, n0, As[buf ^ 1], Bs[buf ^ 1]);
+      if (EXP == 6 && c + 1 < nchunks) {  // keep the loads alive without the LDS stores
+        float sink = 0.f;
+#pragma unroll
+        for (int i = 0; i < NT2Shape<KC>::A_PER_THREAD; ++i) sink += st.ra[i];
+#pragma unroll
+        for (int i = 0; i < NT2Shape<KC>::B_PER_THREAD; ++i) sink += st.rb[i];
+        if (sink == 12345.678f) As[buf][threadIdx.x] = sink;
+      }
+      if (EXP != 4) __syncthreads();
+    }
+  } else {
+    // Two register stages: while chunk c's MFMAs run, chunks c+1 and c+2 are in flight (one
+    // chunk of MFMAs, ≈0.85 µs, is shorter than a loaded HBM round trip).
+    NT2Stage<AVEC, BVEC, KC, WFORM> s0, s1;
+    s0.load(a, 0, m0, n0, bvec4);
+    s0.store(a, 0, m0, n0, As[0], Bs[0]);
+    __syncthreads();
+    if (1 < nchunks) s1.load(a, 1, m0, n0, bvec4);
+    if (2 < nchunks) s0.load(a, 2, m0, n0, bvec4);
+    for (int c = 0; c < nchunks; c += 2) {
+      compute(As[0], Bs[0], c);
+      if (c + 1 < nchunks) {
+        s1.store(a, c + 1, m0, n0, As[1], Bs[1]);
+        if (c + 3 < nchunks) s1.load(a, c + 3, m0, n0, bvec4);
+      }
+      __syncthreads();
+      if (c + 1 >= nchunks) break;
+      compute(As[1], Bs[1], c + 1);
+      if (c + 2 < nchunks) {
+        s0.store(a, c + 2, m0, n0, As[0], Bs[0]);
+        if (c + 4 < nchunks) s0.load(a, c + 4, m0, n0, bvec4);
+      }
+      __syncthreads();
+    }
+  }
+  nt_epilogue<1>(a, acc, m0, n0, lane, wave, seed);
+}
+
+template <int AVEC, int BVEC, int KC, bool WFORM, int EXP, int DEPTH>
+void launch_nt2(const NTArgs& a, hipStream_t st) {
+  dim3 grid((unsigned)ceil_div(a.M, NT2Shape<KC>::BM), (unsigned)ceil_div(a.Nc, BN));
+  gemm_nt2_kernel<AVEC, BVEC, KC, WFORM, EXP, DEPTH><<<grid, 256, 0, st>>>(a);
+}
+
+template <int AVEC, int KC, int EXP = 0, int DEPTH = 1>
+void launch_nt2_b(const NTArgs& a, hipStream_t st) {
+  if (!a.w1) launch_nt2<AVEC, 1, KC, false, EXP, DEPTH>(a, st);
+  else if (a.wvec == 4) launch_nt2<AVEC, 4, KC, true, EXP, DEPTH>(a, st);
+  else if (a.wvec == 2) launch_nt2<AVEC, 2, KC, true, EXP, DEPTH>(a, st);
+  else launch_nt2<AVEC, 1, KC, true, EXP, DEPTH>(a, st);
 }
 
 // Variant table (tuning harness csrc/bench_gemm.hip); variant 0 is the production choice.
 template <int AVEC>
 void launch_nt_variant(const NTArgs& a, int variant, hipStream_t st) {
   switch (variant) {
-    case 1: launch_nt<AVEC, 32, 1, false>(a, st); break;  // 32-deep chunks, 2 blocks/CU
-    case 2: launch_nt<AVEC, 32, 1, true>(a, st); break;
-    case 3: launch_nt<AVEC, 16, 1, true>(a, st); break;
-    case 4: launch_nt<AVEC, 16, 1, false>(a, st); break;
-    case 5: launch_nt<AVEC, 32, 2, false>(a, st); break;
-    case 6: launch_nt<AVEC, 16, 2, true>(a, st); break;
-    case 7: launch_nt<AVEC, 16, 2, false>(a, st); break;
-    case 8: launch_nt<AVEC, 16, 1, false, 1>(a, st); break;  // lab: no global loads in the loop
-    case 9: launch_nt<AVEC, 16, 1, false, 2>(a, st); break;  // lab: no MFMAs
-    case 10: launch_nt<AVEC, 16, 1, false, 3>(a, st); break;  // lab: MFMAs + barriers only
-    default: launch_nt<AVEC, 16, 1, false>(a, st); break;  // production: measured fastest (r01 lab)
+    case 1: launch_nt<AVEC, 16, 1, false>(a, st); break;     // r01 kernel: b32 fragment reads, [k][n] B image
+    case 2: launch_nt2_b<AVEC, 32>(a, st); break;            // 32-deep chunks (LDS: 2 blocks/CU)
+    case 3: launch_nt2_b<AVEC, 16, 0, 2>(a, st); break;      // two chunks of loads in flight
+    case 4: launch_nt2_b<AVEC, 16, 1>(a, st); break;         // ablation: no staging (MFMAs + LDS reads + barriers)
+    case 5: launch_nt2_b<AVEC, 16, 6>(a, st); break;         // ablation: global loads, no LDS stores
+    case 6: launch_nt2_b<AVEC, 16, 7>(a, st); break;         // ablation: LDS stores, no global loads
+    default: launch_nt2_b<AVEC, 16>(a, st); break;           // production (r01 lab: fastest)
   }
 }
 
@@ -649,6 +886,11 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
   a.wvec2 = a.w1 && (a.ldw1 % 2 == 0) && (a.k1 % 2 == 0) && al(a.w1, 8) &&
             (a.k2 == 0 || ((a.ldw2 % 2 == 0) && (a.k2 % 2 == 0) && al(a.w2, 8)));
+  auto wv = [&](int v) {
+    return a.w1 && (a.ldw1 % v == 0) && (a.k1 % v == 0) && al(a.w1, 4 * v) &&
+           (a.k2 == 0 || ((a.ldw2 % v == 0) && (a.k2 % v == 0) && al(a.w2, 4 * v)));
+  };
+  a.wvec = wv(4) ? 4 : (wv(2) ? 2 : 1);
   bool v4 = (a.k1 % 4 == 0) && (a.lda1 % 4 == 0) && al(a.a1, 16) &&
             (a.k2 == 0 || ((a.k2 % 4 == 0) && (a.lda2 % 4 == 0) && al(a.a2, 16)));
   bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al(a.a1, 8) &&

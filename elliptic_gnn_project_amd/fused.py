@@ -127,10 +127,9 @@ class _FusedSAGE(torch.autograd.Function):
             last_hidden = l == L - 2
             if last_hidden:
                 z = torch.empty((h.size(0), 2 * C), dtype=torch.float32, device=h.device)
-            # [W_l | W_r]ᵀ as one [2F, H] operand: a single cat kernel (≈3 µs) buys the fast
-            # row-major B path (the in-place w1/w2 form measures ≈30 µs slower per launch)
-            bt = torch.cat([Wl[l].t(), Wr[l].t()], dim=0)
-            hn = gemm_nt(agg, bt, Wl[l].size(0), a2=h, bias=bl[l], relu=True,
+            # B = [W_l | W_r]ᵀ read in place from the Linear weights (K-contiguous [n][k] rows are
+            # the NT kernel's LDS image): no transposed copy
+            hn = gemm_nt(agg, None, Wl[l].size(0), a2=h, w1=Wl[l], w2=Wr[l], bias=bl[l], relu=True,
                          dropout_p=train_drop, seed=seeds[l], proj=P if last_hidden else None,
                          z=z if last_hidden else None, seed_ptr=seed_ctr)
             aggs.append(agg)

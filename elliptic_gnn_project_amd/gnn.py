@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from . import fused as _fused
 from .conv import GATConv, GCNConv, SAGEConv
+from .linear import Linear
 
 __all__ = ["GCNNet", "SAGENet", "GATNet", "SAGEResBNNet"]
 
@@ -116,7 +117,7 @@ class SAGEResBNNet(nn.Module):
         self.bns = nn.ModuleList(nn.BatchNorm1d(hidden_dim) for _ in range(layers - 1)) if self.use_bn \
             else nn.ModuleList()
         self.res_projs = nn.ModuleList(
-            nn.Identity() if a == b else nn.Linear(a, b, bias=False) for a, b in dims[:-1]
+            nn.Identity() if a == b else Linear(a, b, bias=False) for a, b in dims[:-1]
         )
 
     def _sinusoid(self, t_idx: torch.Tensor) -> Optional[torch.Tensor]:

@@ -1,0 +1,86 @@
+"""Dense transforms of the convs on the MFMA GEMM kernels (K7) instead of torch's Linear.
+
+PyG's ``Linear`` inside SAGEConv (lin_l / lin_r, gnn.py:41-44), GCNConv (lin, gnn.py:20-23) and
+GATConv (lin, gnn.py:64-67), and SAGE-ResBN's ``res_projs`` (gnn.py:118-120), are tall-skinny
+fp32 GEMMs ([N≈2e5, ≤384] × [≤384, ≤128]).  Forward runs the NT kernel with the weight read in
+place ([out, in] is already the K-contiguous B image), bias fused; backward runs ONE TN kernel for
+dW (and db) and the NT kernel (B = W, row-major [K=out, N=in]) for the input gradient.
+
+``linear2`` is the two-segment form ``[a1 | a2] · [W1 | W2]ᵀ + b`` — SAGEConv's
+``lin_l(agg) + lin_r(x)`` as one GEMM with no concatenated copy of the operands.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .fused import gemm_nt, gemm_tn
+
+MAX_OUT = 128  # NT in-place weight form / TN dW rows
+MAX_IN = 384   # TN K extent
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    if x.stride(-1) != 1 or x.stride(0) < x.size(1):
+        x = x.contiguous()
+    return x
+
+
+def fits(in_total: int, out: int) -> bool:
+    return 1 <= out <= MAX_OUT and 1 <= in_total <= MAX_IN
+
+
+class _MfmaLinear(torch.autograd.Function):
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, a1, w1, bias, a2, w2):
+        a1 = _rows(a1)
+        a2 = _rows(a2) if a2 is not None else None
+        w1 = w1.contiguous()
+        w2 = w2.contiguous() if w2 is not None else None
+        y = gemm_nt(a1, None, w1.size(0), a2=a2, bias=bias, w1=w1, w2=w2)
+        ctx.save_for_backward(a1, w1, a2, w2)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        a1, w1, a2, w2 = ctx.saved_tensors
+        dy = dy.contiguous()
+        need = ctx.needs_input_grad
+        dW1 = db = dW2 = None
+        if need[1] or need[2] or need[4]:
+            (dW1, dW2), db, _, _ = gemm_tn(w1.size(0), a1, a2, g=dy)
+        da1 = gemm_nt(dy, w1, w1.size(1)) if need[0] else None
+        da2 = gemm_nt(dy, w2, w2.size(1)) if (a2 is not None and need[3]) else None
+        return (da1, dW1 if need[1] else None, db if (ctx.has_bias and need[2]) else None,
+                da2, dW2 if need[4] else None)
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """``F.linear`` on the MFMA kernels (HIP device, fp32 compute, 2-D input)."""
+    if not x.is_cuda:
+        raise RuntimeError("elliptic_gnn_project_amd.linear runs on the HIP device only")
+    if x.dim() != 2 or x.size(0) == 0 or not fits(weight.size(1), weight.size(0)):
+        return F.linear(x, weight, bias)  # outside the kernels' shape envelope: torch on the GPU
+    return _MfmaLinear.apply(x, weight, bias, None, None)
+
+
+def linear2(a1: torch.Tensor, a2: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor,
+            bias: torch.Tensor | None = None) -> torch.Tensor:
+    """``a1·W1ᵀ + a2·W2ᵀ + b`` as one GEMM over the two K segments."""
+    if not a1.is_cuda:
+        raise RuntimeError("elliptic_gnn_project_amd.linear2 runs on the HIP device only")
+    if a1.size(0) == 0 or not fits(w1.size(1) + w2.size(1), w1.size(0)):
+        return F.linear(a1, w1, bias) + F.linear(a2, w2)
+    return _MfmaLinear.apply(a1, w1, bias, a2, w2)
+
+
+class Linear(nn.Linear):
+    """``torch.nn.Linear`` (same parameters, init and state_dict keys) whose forward runs on
+    the MFMA kernels."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return linear(x, self.weight, self.bias)
