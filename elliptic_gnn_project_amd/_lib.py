@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # gnn_status
 GNN_OK = 0
@@ -44,6 +44,20 @@ c_ptr = ctypes.c_void_p
 c_size = ctypes.c_size_t
 
 
+class GnnSplit(ctypes.Structure):
+    _fields_ = [
+        ("seg_len", c_i32),
+        ("reserved", c_i32),
+        ("num_long", c_i64),
+        ("num_pieces", c_i64),
+        ("ptr", c_ptr),
+        ("nbr", c_ptr),
+        ("piece0", c_ptr),
+        ("piece_seg", c_ptr),
+        ("long_seg", c_ptr),
+    ]
+
+
 class GnnGraph(ctypes.Structure):
     _fields_ = [
         ("num_nodes", c_i64),
@@ -53,6 +67,8 @@ class GnnGraph(ctypes.Structure):
         ("colptr", c_ptr),
         ("row", c_ptr),
         ("csc2csr", c_ptr),
+        ("csr_split", ctypes.POINTER(GnnSplit)),
+        ("csc_split", ctypes.POINTER(GnnSplit)),
     ]
 
 
@@ -67,6 +83,8 @@ class GnnAggParams(ctypes.Structure):
         ("ld_add", c_i64),
         ("bias", c_ptr),
         ("relu", c_i32),
+        ("part", c_ptr),
+        ("part_bytes", c_size),
     ]
 
 
@@ -110,6 +128,12 @@ SIGNATURES = {
     "gnn_graph_build": (
         ctypes.c_int,
         [c_ptr, c_i64, c_i64, ctypes.c_int, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_split_workspace_size": (ctypes.c_int, [c_i64, ctypes.POINTER(c_size)]),
+    "gnn_split_count": (ctypes.c_int, [c_ptr, c_i64, c_i32, c_ptr, c_ptr]),
+    "gnn_split_build": (
+        ctypes.c_int,
+        [c_ptr, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
     "gnn_in_degree_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), c_ptr, c_ptr]),
     "gnn_gcn_norm_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), c_ptr, c_ptr]),

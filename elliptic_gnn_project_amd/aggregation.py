@@ -97,10 +97,13 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
         out = torch.empty((N, F), dtype=torch.float32, device=x.device)
     if addend is not None:
         addend = _as_f32_rows(addend)
+    # partial-sum rows for the long-segment split (used by the lane-group gather, 8 < F <= 128)
+    npieces = plan.split_pieces(transpose) if (mode != _lib.AGG_EDGE_W and 8 < F <= 128) else 0
+    part = torch.empty(npieces * F, dtype=torch.float32, device=x.device) if npieces else None
     p = _lib.GnnAggParams(
         mode, int(transpose), _lib.ptr(nodew), _lib.ptr(ew), int(heads),
         _lib.ptr(addend), _ld(addend) if addend is not None else 0,
-        _lib.ptr(bias), int(relu),
+        _lib.ptr(bias), int(relu), _lib.ptr(part), part.numel() * 4 if part is not None else 0,
     )
     if KernelTimer.active:
         a = torch.cuda.Event(enable_timing=True)

@@ -66,6 +66,13 @@ struct AggArgs {
   int32_t relu;
   int64_t nrows;
   int32_t F;
+  // long-segment split (gnn_split): main pass over truncated segments writes raw partials of
+  // long segments to part[piece0[r]]; pieces / combine passes read the full segments
+  const int32_t* piece0;   // null: no split
+  float* part;
+  const int32_t* fptr;
+  const int32_t* fnbr;
+  int32_t seg_len;
 };
 
 // Per-slot scaled contribution.
@@ -133,6 +140,7 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
   const int32_t myptr = a.ptr[r0 + min(gl, nrow)];
   float mydeg = 1.0f;
   if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[r0 + min(gl, nrow - 1)];
+  const int32_t mypiece = a.piece0 ? a.piece0[r0 + min(gl, nrow - 1)] : -1;
   auto ptr_at = [&](int j) { return __shfl(myptr, gbase + j); };
 
   float acc[NCHMAX][VEC];
@@ -145,10 +153,13 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
     const int64_t r = r0 + j;
     float d = 1.0f;
     if constexpr (MODE == GNN_AGG_MEAN) d = fmaxf(__shfl(mydeg, gbase + j), 1.0f);
+    const int32_t p0 = __shfl(mypiece, gbase + j);
 #pragma unroll
     for (int i = 0; i < NCHMAX; ++i) {
       const int c = gl + LPS * i;
-      if (i < nch && c < nchunk) {
+      if (i < nch && c < nchunk && p0 >= 0) {  // long row: raw partial of piece 0
+        vstore<VEC>(a.part + (int64_t)p0 * a.F + c * VEC, acc[i]);
+      } else if (i < nch && c < nchunk) {
         const int f0 = c * VEC;
         float t[VEC];
 #pragma unroll
@@ -226,6 +237,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   const int32_t myptr = a.ptr[r0 + min(lane, nrow)];
   float mydeg = 1.0f;
   if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[r0 + min(lane, nrow - 1)];
+  const int32_t mypiece = a.piece0 ? a.piece0[r0 + min(lane, nrow - 1)] : -1;
   int coff[NCH];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
@@ -242,10 +254,13 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
     const int64_t r = r0 + j;
     float d = 1.0f;
     if constexpr (MODE == GNN_AGG_MEAN) d = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mydeg), j)), 1.0f);
+    const int32_t p0 = __builtin_amdgcn_readlane(mypiece, j);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + 64 * i;
-      if (c < nchunk) {
+      if (c < nchunk && p0 >= 0) {  // long row: raw partial of piece 0
+        vstore<VEC>(a.part + (int64_t)p0 * a.F + c * VEC, acc[i]);
+      } else if (c < nchunk) {
         const int f0 = c * VEC;
         float t[VEC];
 #pragma unroll
@@ -342,12 +357,17 @@ __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
       }
     }
     if (sub == 0) {
+      const int32_t p0 = a.piece0 ? a.piece0[r] : -1;
 #pragma unroll
       for (int f = 0; f < 8; ++f) {
         if (f < a.F) {
           float t[1] = {acc[f]};
-          finish<MODE, 1>(a, r, f, t);
-          a.y[r * a.ldy + f] = t[0];
+          if (p0 >= 0) {
+            a.part[(int64_t)p0 * a.F + f] = t[0];
+          } else {
+            finish<MODE, 1>(a, r, f, t);
+            a.y[r * a.ldy + f] = t[0];
+          }
         }
       }
     }
@@ -396,29 +416,199 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
     const int32_t lo = max(pbeg, pb), hi = min(pend, pe);
-    for (int32_t k = lo; k < hi; ++k) {
+    // 4 interleaved partial sums: a hub lane's LDS reads pipeline instead of chaining
+    float q1[4] = {0.f, 0.f, 0.f, 0.f}, q2[4] = {0.f, 0.f, 0.f, 0.f}, q3[4] = {0.f, 0.f, 0.f, 0.f};
+    int32_t k = lo;
+    for (; k + 3 < hi; k += 4) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        acc[f] += buf[f * kNarrowCap + (k - pb)];
+        q1[f] += buf[f * kNarrowCap + (k + 1 - pb)];
+        q2[f] += buf[f * kNarrowCap + (k + 2 - pb)];
+        q3[f] += buf[f * kNarrowCap + (k + 3 - pb)];
+      }
+    }
+    for (; k < hi; ++k) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) acc[f] += buf[f * kNarrowCap + (k - pb)];
     }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[f] += (q1[f] + q2[f]) + q3[f];
     __builtin_amdgcn_wave_barrier();
   }
   if (rok) {
+    const int32_t p0 = a.piece0 ? a.piece0[r] : -1;
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
       if (f < F) {
         float t[1] = {acc[f]};
-        finish<MODE, 1>(a, r, f, t);
-        a.y[r * a.ldy + f] = t[0];
+        if (p0 >= 0) {
+          a.part[(int64_t)p0 * F + f] = t[0];
+        } else {
+          finish<MODE, 1>(a, r, f, t);
+          a.y[r * a.ldy + f] = t[0];
+        }
       }
     }
   }
 }
 
+// ---- long-segment split: pieces 1.. of every long segment, then the ordered combine.
+// Wide rows: one wave per piece, lanes over features, U neighbour rows in flight.
+template <int MODE, int VEC, int NCH>
+__global__ __launch_bounds__(256) void agg_piece_wide_kernel(AggArgs a, int64_t npieces, const int32_t* piece_seg) {
+  constexpr int U = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (p >= npieces) return;
+  const int32_t r = piece_seg[p];
+  const int32_t k = (int32_t)p - a.piece0[r];
+  if (k == 0) return;  // piece 0 belongs to the main pass
+  const int32_t beg = a.fptr[r] + k * a.seg_len;
+  const int32_t end = min(beg + a.seg_len, a.fptr[r + 1]);
+  const int nchunk = a.F / VEC;
+  float acc[NCH][VEC];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+  for (int32_t s = beg; s < end; s += U) {
+    int32_t n[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) n[u] = __builtin_amdgcn_readfirstlane(a.fnbr[min(s + u, end - 1)]);
+    float v[U][NCH][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int c = lane + 64 * i;
+        vload<VEC>(a.x + (int64_t)n[u] * a.ldx + (c < nchunk ? c : 0) * VEC, v[u][i]);
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (s + u >= end) break;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        contrib<MODE, VEC>(a, n[u], r, s + u, (lane + 64 * i) * VEC, v[u][i]);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nchunk) vstore<VEC>(a.part + p * a.F + c * VEC, acc[i]);
+  }
+}
+
+// Narrow rows (F <= 8): one wave per piece, lanes over its <= 64 slots, fixed xor tree.
+template <int MODE>
+__global__ __launch_bounds__(256) void agg_piece_narrow_kernel(AggArgs a, int64_t npieces, const int32_t* piece_seg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (p >= npieces) return;
+  const int32_t r = piece_seg[p];
+  const int32_t k = (int32_t)p - a.piece0[r];
+  if (k == 0) return;
+  const int32_t beg = a.fptr[r] + k * a.seg_len;
+  const int32_t end = min(beg + a.seg_len, a.fptr[r + 1]);
+  const int32_t slot = beg + lane;
+  const bool ok = slot < end;
+  const int32_t n = a.fnbr[ok ? slot : beg];
+  float acc[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) {
+    float v[1] = {(ok && f < a.F) ? a.x[(int64_t)n * a.ldx + f] : 0.0f};
+    if (ok && f < a.F) contrib<MODE, 1>(a, n, r, slot, f, v);
+    acc[f] = v[0];
+  }
+#pragma unroll
+  for (int f = 0; f < 8; ++f)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc[f] += __shfl_xor(acc[f], off);
+  if (lane == 0) {
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+      if (f < a.F) a.part[p * a.F + f] = acc[f];
+  }
+}
+
+// Combine: one wave per long segment, its pieces' partials added in piece order, then the
+// mode's finish (mean divide, root addend, bias, ReLU) and the store.
+template <int MODE, int VEC, int NCH>
+__global__ __launch_bounds__(256) void agg_combine_kernel(AggArgs a, int64_t nlong, const int32_t* long_seg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t l = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (l >= nlong) return;
+  const int32_t r = long_seg[l];
+  const int32_t p0 = a.piece0[r];
+  const int32_t deg = a.fptr[r + 1] - a.fptr[r];
+  const int32_t np = (deg + a.seg_len - 1) / a.seg_len;
+  const int nchunk = a.F / VEC;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + 64 * i;
+    if (c >= nchunk) continue;
+    float acc[VEC];
+    vload<VEC>(a.part + (int64_t)p0 * a.F + c * VEC, acc);
+    for (int32_t k = 1; k < np; ++k) {
+      float t[VEC];
+      vload<VEC>(a.part + (int64_t)(p0 + k) * a.F + c * VEC, t);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[q] += t[q];
+    }
+    finish<MODE, VEC>(a, r, c * VEC, acc);
+    vstore<VEC>(a.y + (int64_t)r * a.ldy + c * VEC, acc);
+  }
+}
+
 bool aligned(const void* p, int bytes) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0; }
 
+template <int MODE, int VEC, int NCH>
+void launch_split_passes(const AggArgs& a, const gnn_split* sp, hipStream_t st) {
+  if (sp->num_pieces > sp->num_long)
+    agg_piece_wide_kernel<MODE, VEC, NCH><<<(unsigned)ceil_div(sp->num_pieces * 64, 256), 256, 0, st>>>(
+        a, sp->num_pieces, sp->piece_seg);
+  agg_combine_kernel<MODE, VEC, NCH><<<(unsigned)ceil_div(sp->num_long * 64, 256), 256, 0, st>>>(
+      a, sp->num_long, sp->long_seg);
+}
+
+template <int MODE, int VEC>
+void launch_split_v(const AggArgs& a, const gnn_split* sp, hipStream_t st) {
+  const int nch = (int)ceil_div(a.F / VEC, 64);
+  if (nch <= 1) launch_split_passes<MODE, VEC, 1>(a, sp, st);
+  else if (nch <= 2) launch_split_passes<MODE, VEC, 2>(a, sp, st);
+  else launch_split_passes<MODE, VEC, 4>(a, sp, st);
+}
+
 template <int MODE>
-gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st) {
+gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp);
+
+template <int MODE>
+gnn_status launch_mode_split(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp) {
+  gnn_status s = launch_mode<MODE>(a, vec, st, nullptr);  // main pass over the truncated segments
+  if (s != GNN_OK || sp->num_long == 0) return s;
+  if (a.F <= 8) {
+    if (sp->num_pieces > sp->num_long)
+      agg_piece_narrow_kernel<MODE><<<(unsigned)ceil_div(sp->num_pieces * 64, 256), 256, 0, st>>>(
+          a, sp->num_pieces, sp->piece_seg);
+    agg_combine_kernel<MODE, 1, 1><<<(unsigned)ceil_div(sp->num_long * 64, 256), 256, 0, st>>>(
+        a, sp->num_long, sp->long_seg);
+  } else if (vec == 4) {
+    launch_split_v<MODE, 4>(a, sp, st);
+  } else if (vec == 2) {
+    launch_split_v<MODE, 2>(a, sp, st);
+  } else {
+    launch_split_v<MODE, 1>(a, sp, st);
+  }
+  return hip_check(hipGetLastError(), "gnn_aggregate_f32 (split passes)");
+}
+
+template <int MODE>
+gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp) {
   if (a.nrows == 0 || a.F == 0) return GNN_OK;
+  if (sp) return launch_mode_split<MODE>(a, vec, st, sp);
   if (a.F <= 4 && (MODE == GNN_AGG_MEAN || MODE == GNN_AGG_MEAN_BWD || MODE == GNN_AGG_SUM)) {
     agg_narrow_lds_kernel<MODE><<<(unsigned)ceil_div(a.nrows, 256), 256, 0, st>>>(a);
   } else if (a.F <= 8) {
@@ -460,7 +650,8 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st) {
 
 // ------------------------------------------------------------------ colsum
 // Stage 1: block b sums rows [b*rpb, (b+1)*rpb); threads form (row lanes x columns) so that
-// narrow F still uses the whole block; row-lane partials are combined in LDS in fixed order.
+// narrow F still uses the whole block; each thread keeps 4 independent accumulators (4 row
+// loads in flight), combined in a fixed order, then row-lane partials combine in LDS.
 __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t rows, int32_t F, const float* __restrict__ x,
                                                              int64_t ldx, int64_t rows_per_blk,
                                                              float* __restrict__ part) {
@@ -473,10 +664,18 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t rows, int32
   const int64_t r1 = r0 + rows_per_blk < rows ? r0 + rows_per_blk : rows;
   for (int cb = 0; cb < F; cb += cols) {
     const int c = cb + c_local;
-    float acc = 0.0f;
-    if (rl < lanes && c < F)
-      for (int64_t r = r0 + rl; r < r1; r += lanes) acc += x[r * ldx + c];
-    red[threadIdx.x] = acc;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (rl < lanes && c < F) {
+      int64_t r = r0 + rl;
+      for (; r + 3 * lanes < r1; r += 4 * lanes) {
+        a0 += x[r * ldx + c];
+        a1 += x[(r + lanes) * ldx + c];
+        a2 += x[(r + 2 * lanes) * ldx + c];
+        a3 += x[(r + 3 * lanes) * ldx + c];
+      }
+      for (; r < r1; r += lanes) a0 += x[r * ldx + c];
+    }
+    red[threadIdx.x] = (a0 + a1) + (a2 + a3);
     __syncthreads();
     if (threadIdx.x < cols && cb + (int)threadIdx.x < F) {
       float s = 0.0f;
@@ -487,16 +686,32 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(int64_t rows, int32
   }
 }
 
-__global__ void colsum_final_kernel(int32_t F, int32_t nblk, const float* __restrict__ part,
-                                    float* __restrict__ out) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= F) return;
-  float acc = 0.0f;
-  for (int b = 0; b < nblk; ++b) acc += part[(int64_t)b * F + c];
-  out[c] = acc;
+// Stage 2: one block per column; 256 threads stride the partials (4 loads in flight each),
+// then a fixed-shape LDS tree.  Deterministic.
+__global__ __launch_bounds__(256) void colsum_final_kernel(int32_t F, int32_t nblk, const float* __restrict__ part,
+                                                           float* __restrict__ out) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  const int t = threadIdx.x;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int b = t;
+  for (; b + 768 < nblk; b += 1024) {
+    a0 += part[(int64_t)b * F + c];
+    a1 += part[(int64_t)(b + 256) * F + c];
+    a2 += part[(int64_t)(b + 512) * F + c];
+    a3 += part[(int64_t)(b + 768) * F + c];
+  }
+  for (; b < nblk; b += 256) a0 += part[(int64_t)b * F + c];
+  red[t] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) red[t] += red[t + s];
+    __syncthreads();
+  }
+  if (t == 0) out[c] = red[0];
 }
 
-constexpr int64_t kColsumBlocks = 256;
+constexpr int64_t kColsumBlocks = 1024;
 
 }  // namespace
 }  // namespace gnnmp
@@ -539,14 +754,40 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
     int b = 4 * v;
     return aligned(x, b) && aligned(y, b) && aligned(p->addend, b);
   };
+  // Long-segment split (not for EDGE_W: its weights are indexed by the untruncated slot).
+  const gnn_split* sp = p->transpose ? g->csc_split : g->csr_split;
+  if (sp && (p->mode == GNN_AGG_EDGE_W || !p->part || sp->seg_len < 1 || sp->seg_len > 64 ||
+             p->part_bytes < (size_t)sp->num_pieces * (size_t)F * sizeof(float) ||
+             (sp->num_long > 0 && (!sp->ptr || !sp->nbr || !sp->piece0 || !sp->piece_seg || !sp->long_seg))))
+    sp = nullptr;  // unsplit fallback is always correct
+  if (sp) {
+    a.fptr = a.ptr;
+    a.fnbr = a.nbr;
+    a.ptr = sp->ptr;
+    a.nbr = sp->nbr;
+    a.piece0 = sp->piece0;
+    a.part = p->part;
+    a.seg_len = sp->seg_len;
+  }
   int vec = ok_vec(4) ? 4 : (ok_vec(2) ? 2 : 1);
+  while (sp && vec > 1 && !aligned(p->part, 4 * vec)) vec >>= 1;
+  // The split pays only for the lane-group gather (8..32 lanes per row, one row at a time per
+  // group): r01 measurements — F=64 GCN fwd 72 -> 37 µs; the wave-wide gather (F/vec > 32) and
+  // the narrow LDS/group kernels lose to the two extra launches.
+  if (sp && (F <= 8 || F / vec > 32)) sp = nullptr;
+  if (!sp) {
+    a.ptr = p->transpose ? g->colptr : g->rowptr;
+    a.nbr = p->transpose ? g->row : g->col;
+    a.piece0 = nullptr;
+    a.part = nullptr;
+  }
   hipStream_t st = (hipStream_t)stream;
   switch (p->mode) {
-    case GNN_AGG_SUM: return launch_mode<GNN_AGG_SUM>(a, vec, st);
-    case GNN_AGG_MEAN: return launch_mode<GNN_AGG_MEAN>(a, vec, st);
-    case GNN_AGG_MEAN_BWD: return launch_mode<GNN_AGG_MEAN_BWD>(a, vec, st);
-    case GNN_AGG_GCN: return launch_mode<GNN_AGG_GCN>(a, vec, st);
-    case GNN_AGG_EDGE_W: return launch_mode<GNN_AGG_EDGE_W>(a, vec, st);
+    case GNN_AGG_SUM: return launch_mode<GNN_AGG_SUM>(a, vec, st, sp);
+    case GNN_AGG_MEAN: return launch_mode<GNN_AGG_MEAN>(a, vec, st, sp);
+    case GNN_AGG_MEAN_BWD: return launch_mode<GNN_AGG_MEAN_BWD>(a, vec, st, sp);
+    case GNN_AGG_GCN: return launch_mode<GNN_AGG_GCN>(a, vec, st, sp);
+    case GNN_AGG_EDGE_W: return launch_mode<GNN_AGG_EDGE_W>(a, vec, st, nullptr);
   }
   return fail(GNN_ERR_INVALID_ARG, __func__, "unknown mode");
 }
@@ -592,7 +833,7 @@ extern "C" gnn_status gnn_colsum_f32(int64_t rows, int64_t F, const float* x, in
   float* part = static_cast<float*>(workspace);
   colsum_partial_kernel<<<(unsigned)nblk, 256, 0, st>>>(rows, (int32_t)F, x, ldx, rpb, part);
   GNN_LAUNCH_CHECK();
-  colsum_final_kernel<<<(unsigned)ceil_div(F, 64), 64, 0, st>>>((int32_t)F, (int32_t)nblk, part, out);
+  colsum_final_kernel<<<(unsigned)F, 256, 0, st>>>((int32_t)F, (int32_t)nblk, part, out);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }

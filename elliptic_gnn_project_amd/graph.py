@@ -11,15 +11,55 @@ HBM layout of a plan (int32 throughout, N+1 / S entries):
     rowptr[N+1], col[S], csr_eid[S]       CSR by target (forward gathers)
     colptr[N+1], row[S], csc2csr[S]       CSC by source (backward gathers)
     deg[N] f32                             slots per target (mean count / GCN degree)
+    split (per direction, when a segment has > SPLIT_LEN slots): truncated ptr/nbr,
+      piece0[N], piece_seg[pieces], long_seg[long]   (K0b, graph_split.hip)
     dinv[N] f32                            GCN deg^-1/2 (REPLACE plans only)
 """
 from __future__ import annotations
+
+import ctypes
+import os
 
 import torch
 
 from . import _lib
 
 _ATTR = "_gnnmp_plans"
+SPLIT_LEN = 32  # slots per piece of a long segment (K0b)
+
+
+def _split_enabled() -> bool:
+    return os.environ.get("GNNMP_SPLIT", "1") != "0"
+
+
+def _build_split(lib, ptr: torch.Tensor, nbr: torch.Tensor, n: int, T: int, dev):
+    """Long-segment split of one direction; None when no segment exceeds T slots."""
+    counts = torch.zeros(3, dtype=torch.int64, device=dev)
+    with torch.cuda.device(dev):
+        stream = _lib.stream_handle(dev)
+        _lib.check(lib.gnn_split_count(ptr.data_ptr(), n, T, counts.data_ptr(), stream), "gnn_split_count")
+        s_trunc, n_long, n_pieces = (int(v) for v in counts.cpu())  # one sync per plan build
+        if n_long == 0:
+            return None
+        i32 = dict(dtype=torch.int32, device=dev)
+        t = {
+            "ptr": torch.empty(n + 1, **i32),
+            "nbr": torch.empty(max(s_trunc, 1), **i32),
+            "piece0": torch.empty(max(n, 1), **i32),
+            "piece_seg": torch.empty(max(n_pieces, 1), **i32),
+            "long_seg": torch.empty(max(n_long, 1), **i32),
+        }
+        nb = _lib.c_size(0)
+        _lib.check(lib.gnn_split_workspace_size(n, nb), "gnn_split_workspace_size")
+        ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+        _lib.check(lib.gnn_split_build(ptr.data_ptr(), nbr.data_ptr(), n, T, t["ptr"].data_ptr(),
+                                       t["nbr"].data_ptr(), t["piece0"].data_ptr(), t["piece_seg"].data_ptr(),
+                                       t["long_seg"].data_ptr(), ws.data_ptr(), ws.numel(), stream),
+                   "gnn_split_build")
+        torch.cuda.current_stream(dev).synchronize()  # ws is freed below
+    t["c"] = _lib.GnnSplit(T, 0, n_long, n_pieces, t["ptr"].data_ptr(), t["nbr"].data_ptr(),
+                           t["piece0"].data_ptr(), t["piece_seg"].data_ptr(), t["long_seg"].data_ptr())
+    return t
 
 
 class GraphPlan:
@@ -79,6 +119,15 @@ class GraphPlan:
             self.rowptr.data_ptr(), self.col.data_ptr(),
             self.colptr.data_ptr(), self.row.data_ptr(), self.csc2csr.data_ptr(),
         )
+        # long-segment splits of both directions (K0b): hubs no longer set the gather's tail
+        self.split_len = SPLIT_LEN if _split_enabled() else 0
+        self._splits = {}
+        if self.split_len > 0 and self.num_slots > 0:
+            for name, ptr, nbr in (("csr", self.rowptr, self.col), ("csc", self.colptr, self.row)):
+                sp = _build_split(lib, ptr, nbr, N, self.split_len, dev)
+                if sp is not None:
+                    self._splits[name] = sp
+                    setattr(self.c_graph, f"{name}_split", ctypes.pointer(sp["c"]))
         self.deg = torch.empty(max(N, 1), dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
             _lib.check(lib.gnn_in_degree_f32(self.c_graph, self.deg.data_ptr(), _lib.stream_handle(dev)),
@@ -96,6 +145,11 @@ class GraphPlan:
                 _lib.call("gnn_gcn_norm_f32", self.c_graph, d.data_ptr(), _lib.stream_handle(self.device))
             self._dinv = d
         return self._dinv
+
+    def split_pieces(self, transpose: bool) -> int:
+        """Partial-sum rows an aggregation over this direction needs (0: unsplit)."""
+        sp = self._splits.get("csc" if transpose else "csr")
+        return int(sp["c"].num_pieces) if sp is not None else 0
 
     def csr(self):
         """(rowptr, col, csr_eid) trimmed to the used slots — for tests / inspection."""

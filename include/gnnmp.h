@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 3
+#define GNNMP_ABI_VERSION 4
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -56,6 +56,23 @@ typedef enum {
  * A graph plan: CSR by destination (aggregation, forward) and CSC by source
  * (transpose, backward), both stable in PyG edge order.
  */
+/*
+ * Long-segment split of one plan direction (see gnn_split_build).  Aggregations over a
+ * split direction run the truncated segments in the main pass, reduce the remaining pieces
+ * of long segments into a caller-provided partial buffer, and combine them in piece order.
+ */
+typedef struct {
+  int32_t seg_len;            /* T: slots per piece */
+  int32_t reserved;
+  int64_t num_long;           /* segments with more than T slots */
+  int64_t num_pieces;         /* pieces of the long segments (ceil(deg / T) each) */
+  const int32_t* ptr;         /* [N+1] segment pointer, every segment truncated to <= T slots */
+  const int32_t* nbr;         /* truncated segments' neighbours (PyG order kept) */
+  const int32_t* piece0;      /* [N] partial-sum row of piece 0 of a long segment, -1 if short */
+  const int32_t* piece_seg;   /* [num_pieces] segment of each piece */
+  const int32_t* long_seg;    /* [num_long] the long segments */
+} gnn_split;
+
 typedef struct {
   int64_t num_nodes;
   int64_t num_slots;        /* stored edges (after loop handling) */
@@ -64,6 +81,8 @@ typedef struct {
   const int32_t* colptr;    /* [N+1] CSC by source j */
   const int32_t* row;       /* [S]   target i of each CSC slot */
   const int32_t* csc2csr;   /* [S]   CSR slot holding the same edge as each CSC slot */
+  const gnn_split* csr_split; /* optional (NULL): long-row split of the CSR direction */
+  const gnn_split* csc_split; /* optional (NULL): long-column split of the CSC direction */
 } gnn_graph;
 
 int gnn_abi_version(void);
@@ -88,6 +107,19 @@ gnn_status gnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t
                            gnn_loop_mode loops, int32_t* rowptr, int32_t* col, int32_t* csr_eid,
                            int32_t* colptr, int32_t* row, int32_t* csc2csr, int32_t* stats,
                            void* workspace, size_t workspace_bytes, gnn_stream_t stream);
+
+/*
+ * K0b  long-segment split of one direction (ptr/nbr = rowptr/col or colptr/row).
+ * gnn_split_count writes {S_trunc, num_long, num_pieces} to device int64 counts[3] (the
+ * caller reads them after the stream completes and sizes the outputs: tptr N+1, tnbr S_trunc,
+ * piece0 N, piece_seg num_pieces, long_seg num_long).  gnn_split_build fills them.
+ */
+gnn_status gnn_split_workspace_size(int64_t num_segs, size_t* bytes);
+gnn_status gnn_split_count(const int32_t* ptr, int64_t num_segs, int32_t seg_len, int64_t* counts,
+                           gnn_stream_t stream);
+gnn_status gnn_split_build(const int32_t* ptr, const int32_t* nbr, int64_t num_segs, int32_t seg_len,
+                           int32_t* tptr, int32_t* tnbr, int32_t* piece0, int32_t* piece_seg,
+                           int32_t* long_seg, void* workspace, size_t workspace_bytes, gnn_stream_t stream);
 
 /* deg[i] = number of CSR slots of i as float (PyG `count` / `deg`, gnn.py:49 via SAGEConv mean). */
 gnn_status gnn_in_degree_f32(const gnn_graph* g, float* deg, gnn_stream_t stream);
@@ -118,6 +150,9 @@ typedef struct {
   int64_t ld_add;
   const float* bias;      /* optional [F] */
   int32_t relu;           /* apply max(.,0) last */
+  float* part;            /* partial sums for a split direction: >= num_pieces * F floats; NULL or
+                             too small -> the direction is aggregated unsplit */
+  size_t part_bytes;
 } gnn_agg_params;
 
 /* Generic fp32 aggregation: y[r, 0:F] for r in [0, N). */

@@ -313,3 +313,72 @@ def test_golden_fixture_through_hip(device, arch):
             out = model(x.to(device), ei.to(device)).cpu().numpy()
         np.testing.assert_allclose(out, z[f"{arch}/logits_f32"], rtol=1e-5, atol=1e-5)
         np.testing.assert_allclose(out, z[f"{arch}/logits_f64"], rtol=1e-5, atol=1e-5)
+
+
+def _split_graph():
+    """In-hub (1000 slots), out-hub (500), rows of exactly 32/33/64/65 slots, random rest."""
+    g = torch.Generator().manual_seed(11)
+    n = 600
+    parts = [rand_graph(n, 1500, seed=12)]
+    parts.append(torch.stack([torch.randint(0, n, (1000,), generator=g), torch.full((1000,), 5)]))
+    parts.append(torch.stack([torch.full((500,), 9), torch.randint(0, n, (500,), generator=g)]))
+    for node, d in ((20, 32), (21, 33), (22, 64), (23, 65)):
+        parts.append(torch.stack([torch.randint(0, n, (d,), generator=g), torch.full((d,), node)]))
+    ei = torch.cat(parts, 1)
+    perm = torch.randperm(ei.size(1), generator=g)
+    return ei[:, perm].contiguous(), n
+
+
+@pytest.mark.parametrize("F", [2, 3, 8, 16, 64, 128, 166])
+@pytest.mark.parametrize("mode", ["sum", "mean", "mean_bwd", "gcn"])
+def test_split_aggregation_modes(device, F, mode):
+    """Long-segment split (K0b) vs a float64 reference, every mode, both directions, with the
+    root addend / bias / ReLU epilogue; and split == unsplit within fp32 rounding."""
+    import os
+
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.aggregation import aggregate
+    from elliptic_gnn_project_amd.graph import GraphPlan
+
+    ei, n = _split_graph()
+    loops = _lib.LOOPS_REPLACE if mode == "gcn" else _lib.LOOPS_KEEP
+    plan = GraphPlan(ei.to(device), n, loops)
+    assert plan.split_pieces(False) > 0 and plan.split_pieces(True) > 0
+    os.environ["GNNMP_SPLIT"] = "0"
+    try:
+        plain = GraphPlan(ei.to(device), n, loops)
+    finally:
+        del os.environ["GNNMP_SPLIT"]
+    assert plain.split_pieces(False) == 0
+    gen = torch.Generator().manual_seed(F)
+    x = torch.randn(n, F, generator=gen, dtype=torch.float64)
+    add = torch.randn(n, F, generator=gen, dtype=torch.float64)
+    bias = torch.randn(F, generator=gen, dtype=torch.float64)
+    s, d = ei[0], ei[1]
+    if mode == "gcn":
+        keep = s != d
+        s = torch.cat([s[keep], torch.arange(n)])
+        d = torch.cat([d[keep], torch.arange(n)])
+    deg = torch.bincount(d, minlength=n).double()
+    if mode == "sum":
+        m, tr, nodew = _lib.AGG_SUM, False, None
+        ref = torch.zeros(n, F, dtype=torch.float64).index_add_(0, d, x[s])
+    elif mode == "mean":
+        m, tr, nodew = _lib.AGG_MEAN, False, plan.deg
+        ref = torch.zeros(n, F, dtype=torch.float64).index_add_(0, d, x[s]) / deg.clamp(min=1)[:, None]
+    elif mode == "mean_bwd":
+        m, tr, nodew = _lib.AGG_MEAN_BWD, True, plan.deg
+        ref = torch.zeros(n, F, dtype=torch.float64).index_add_(0, s, x[d] / deg.clamp(min=1)[d][:, None])
+    else:
+        m, tr, nodew = _lib.AGG_GCN, False, plan.dinv
+        dinv = deg.pow(-0.5)
+        ref = torch.zeros(n, F, dtype=torch.float64).index_add_(0, d, x[s] * (dinv[s] * dinv[d])[:, None])
+    ref = torch.relu(ref + add + bias)
+    xd, addd, bd = (t.float().to(device) for t in (x, add, bias))
+    out = aggregate(plan, xd, m, transpose=tr, nodew=nodew, addend=addd, bias=bd, relu=True)
+    torch.testing.assert_close(out.cpu().double(), ref, rtol=RTOL, atol=ATOL)
+    nodew_p = {None: None}.get(None) if nodew is None else (plain.dinv if mode == "gcn" else plain.deg)
+    out_p = aggregate(plain, xd, m, transpose=tr, nodew=nodew_p, addend=addd, bias=bd, relu=True)
+    torch.testing.assert_close(out, out_p, rtol=RTOL, atol=ATOL)
+    out2 = aggregate(plan, xd, m, transpose=tr, nodew=nodew, addend=addd, bias=bd, relu=True)
+    assert torch.equal(out, out2)  # deterministic

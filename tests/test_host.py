@@ -68,9 +68,12 @@ def test_host_side_argument_validation(lib):
 
 
 STRUCTS = {
-    "gnn_graph": ("GnnGraph", ["num_nodes", "num_slots", "rowptr", "col", "colptr", "row", "csc2csr"]),
+    "gnn_split": ("GnnSplit", ["seg_len", "reserved", "num_long", "num_pieces", "ptr", "nbr", "piece0",
+                               "piece_seg", "long_seg"]),
+    "gnn_graph": ("GnnGraph", ["num_nodes", "num_slots", "rowptr", "col", "colptr", "row", "csc2csr",
+                               "csr_split", "csc_split"]),
     "gnn_agg_params": ("GnnAggParams", ["mode", "transpose", "nodew", "ew", "heads", "addend", "ld_add", "bias",
-                                        "relu"]),
+                                        "relu", "part", "part_bytes"]),
     "gnn_gemm_nt_params": ("GnnGemmNTParams", ["M", "N", "a1", "lda1", "k1", "a2", "lda2", "k2", "bt", "ldb",
                                                "w1", "w2", "ldw1", "ldw2", "c",
                                                "ldc", "bias", "relu", "dropout_p", "seed", "seed_ptr", "proj",
