@@ -15,7 +15,11 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 4
+ABI_VERSION = 5
+
+# gnn_gemm_math
+MATH_SPLIT_BF16 = 0
+MATH_F32 = 1
 
 # gnn_status
 GNN_OK = 0
@@ -102,6 +106,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("seed_ptr", c_ptr),
         ("proj", c_ptr), ("nproj", c_i32), ("z", c_ptr), ("ldz", c_i64),
+        ("math", c_i32),
     ]
 
 
@@ -115,6 +120,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("gout", c_ptr), ("ldgout", c_i64),
         ("a1", c_ptr), ("lda1", c_i64), ("k1", c_i64),
         ("a2", c_ptr), ("lda2", c_i64), ("k2", c_i64),
+        ("math", c_i32),
     ]
 
 

@@ -1,15 +1,15 @@
-// Kernel lab: times libgnnmp kernels through the C ABI on the Elliptic SAGE-preset shapes
-// (hipEvent timing, all variants interleaved in one process, median of rounds).
+// Kernel lab: times libgnnmp GEMM kernels through the C ABI on the Elliptic SAGE-preset shapes
+// (hipEvent timing, variants interleaved in one process, median of rounds) and checks every
+// variant against a float64 host reference.
 //   ./bench_gemm [M] [rounds]
 // Not part of the library; built by `make lab`.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdio>
-#include <cstring>
-#include <cstdlib>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <string>
 #include <vector>
@@ -35,15 +35,23 @@ extern "C" gnn_status gnnx_gemm_nt_variant_f32(const gnn_gemm_nt_params* p, int 
     }                                                                          \
   } while (0)
 
-static float* dev_rand(size_t n, float scale, unsigned seed) {
+static std::vector<float> host_rand(size_t n, float scale, unsigned seed) {
   std::vector<float> h(n);
   std::mt19937 g(seed);
   std::normal_distribution<float> d(0.f, scale);
   for (auto& v : h) v = d(g);
+  return h;
+}
+static float* to_dev(const std::vector<float>& h) {
   float* p;
-  CK(hipMalloc(&p, n * sizeof(float)));
-  CK(hipMemcpy(p, h.data(), n * sizeof(float), hipMemcpyHostToDevice));
+  CK(hipMalloc(&p, h.size() * sizeof(float)));
+  CK(hipMemcpy(p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
   return p;
+}
+static std::vector<float> to_host(const float* d, size_t n) {
+  std::vector<float> h(n);
+  CK(hipMemcpy(h.data(), d, n * sizeof(float), hipMemcpyDeviceToHost));
+  return h;
 }
 
 struct Timer {
@@ -60,90 +68,81 @@ struct Timer {
     return ms * 1000.f / reps;
   }
 };
+static float med(std::vector<float> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; }
 
 int main(int argc, char** argv) {
   const int64_t M = argc > 1 ? std::atoll(argv[1]) : 203769;
   const int rounds = argc > 2 ? std::atoi(argv[2]) : 7;
   const int64_t F = std::getenv("LAB_F") ? std::atoll(std::getenv("LAB_F")) : 166, H = 128;
-  float* agg = dev_rand(M * F, 1.f, 1);
-  float* x = dev_rand(M * F, 1.f, 2);
-  float* bt = dev_rand(2 * F * H, 0.08f, 3);
-  float* bias = dev_rand(H, 0.1f, 4);
-  float* proj = dev_rand(4 * H, 0.1f, 5);
+  auto h_agg = host_rand(M * F, 1.f, 1), h_x = host_rand(M * F, 1.f, 2);
+  auto h_w = host_rand(2 * F * H, 0.08f, 7), h_bias = host_rand(H, 0.1f, 4), h_proj = host_rand(4 * H, 0.1f, 5);
+  auto h_dz = host_rand(M * 4, 1e-3f, 6);
+  float *agg = to_dev(h_agg), *x = to_dev(h_x), *w = to_dev(h_w), *bias = to_dev(h_bias), *proj = to_dev(h_proj);
+  float* dz = to_dev(h_dz);
   float *c, *z;
   CK(hipMalloc(&c, M * H * sizeof(float)));
   CK(hipMalloc(&z, M * 4 * sizeof(float)));
-  float* dz = dev_rand(M * 4, 1e-3f, 6);
 
   gnn_gemm_nt_params p{};
   p.M = M; p.N = H;
   p.a1 = agg; p.lda1 = F; p.k1 = F;
   p.a2 = x; p.lda2 = F; p.k2 = F;
-  p.bt = bt; p.ldb = H;
+  p.w1 = w; p.w2 = w + F * H; p.ldw1 = F; p.ldw2 = F;
   p.c = c; p.ldc = H; p.bias = bias; p.relu = 1; p.dropout_p = 0.5f; p.seed = 1234;
   p.proj = proj; p.nproj = 4; p.z = z; p.ldz = 4;
   gnn_gemm_nt_params plain = p;
   plain.bias = nullptr; plain.relu = 0; plain.dropout_p = 0.f; plain.proj = nullptr; plain.nproj = 0; plain.z = nullptr;
 
-  const double flops = 2.0 * M * (2 * F) * H;
-  Timer T;
-  const int nvar = 7;
-  std::vector<std::vector<float>> t_epi(nvar), t_plain(nvar);
-  // correctness: every variant must agree bitwise with variant 0 (same k-ordered fmaf chain)
-  std::vector<float> ref(M * H), got(M * H);
-  GK(gnnx_gemm_nt_variant_f32(&p, 0, nullptr));
-  CK(hipMemcpy(ref.data(), c, M * H * 4, hipMemcpyDeviceToHost));
-  for (int v = 1; v < nvar; ++v) {
-    if (v >= 4) continue;  // ablations: outputs are meaningless  // ablations: outputs are meaningless
-    GK(gnnx_gemm_nt_variant_f32(&p, v, nullptr));
-    CK(hipMemcpy(got.data(), c, M * H * 4, hipMemcpyDeviceToHost));
-    size_t bad = 0;
-    double maxd = 0.0;
-    for (size_t i = 0; i < got.size(); ++i) {
-      bad += got[i] != ref[i];
-      double d = std::fabs((double)got[i] - (double)ref[i]) / (1e-3 + std::fabs((double)ref[i]));
-      maxd = d > maxd ? d : maxd;
+  // ---- NT accuracy vs float64 on sampled rows (plain GEMM)
+  const std::vector<int> variants = {0, 1, 2, 3, 4, 5, 6, 16};  // <16: split-bf16 tilings; >=16: exact f32
+  std::vector<int64_t> rows;
+  for (int64_t r = 0; r < M; r += std::max<int64_t>(1, M / 3000)) rows.push_back(r);
+  rows.push_back(M - 1);
+  std::vector<double> ref(rows.size() * H);
+  double refmax = 0.0;
+  for (size_t i = 0; i < rows.size(); ++i)
+    for (int n = 0; n < H; ++n) {
+      double s = 0.0;
+      for (int k = 0; k < F; ++k) s += (double)h_agg[rows[i] * F + k] * h_w[n * F + k];
+      for (int k = 0; k < F; ++k) s += (double)h_x[rows[i] * F + k] * h_w[F * H + n * F + k];
+      ref[i * H + n] = s;
+      refmax = std::max(refmax, std::fabs(s));
     }
-    std::printf("variant %d mismatches vs 0: %zu  max rel diff %.2e\n", v, bad, maxd);
+  for (int v : variants) {
+    GK(gnnx_gemm_nt_variant_f32(&plain, v, nullptr));
+    auto got = to_host(c, M * H);
+    double maxabs = 0.0, maxrel = 0.0, se = 0.0, sr = 0.0;
+    for (size_t i = 0; i < rows.size(); ++i)
+      for (int n = 0; n < H; ++n) {
+        const double r = ref[i * H + n], d = std::fabs((double)got[rows[i] * H + n] - r);
+        maxabs = std::max(maxabs, d);
+        maxrel = std::max(maxrel, d / (1e-5 + std::fabs(r)));
+        se += d * d; sr += r * r;
+      }
+    std::printf("NT variant %2d vs f64: max|err| %.3e (max|ref| %.2f)  max rel(1e-5 floor) %.3e  relL2 %.3e\n", v, maxabs,
+                refmax, maxrel, std::sqrt(se / sr));
   }
-  // LAB_ONLY=v[,wform]: time one variant only (for rocprofv3 --pmc passes); no other sections
-  if (const char* only = std::getenv("LAB_ONLY")) {
+  if (const char* only = std::getenv("LAB_ONLY")) {  // one variant, for rocprofv3 --pmc passes
     const int v = std::atoi(only);
-    gnn_gemm_nt_params q = p;
-    if (std::strchr(only, 'w')) {
-      float* w = dev_rand(2 * F * H, 0.08f, 7);
-      q.bt = nullptr; q.w1 = w; q.w2 = w + F * H; q.ldw1 = F; q.ldw2 = F;
-    }
-    for (int r = 0; r < rounds; ++r) GK(gnnx_gemm_nt_variant_f32(&q, v, nullptr));
+    for (int r = 0; r < rounds; ++r) GK(gnnx_gemm_nt_variant_f32(&p, v, nullptr));
     CK(hipDeviceSynchronize());
     std::printf("LAB_ONLY %s done\n", only);
     return 0;
   }
-  for (int r = 0; r < rounds; ++r) {
-    for (int v = 0; v < nvar; ++v) {
-      t_epi[v].push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&p, v, nullptr); }, 5));
-      t_plain[v].push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&plain, v, nullptr); }, 5));
+  const double flops = 2.0 * M * (2 * F) * H;
+  Timer T;
+  for (int v : variants) {
+    std::vector<float> te, tp;
+    for (int r = 0; r < rounds; ++r) {
+      te.push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&p, v, nullptr); }, 5));
+      tp.push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&plain, v, nullptr); }, 5));
     }
+    std::printf("NT variant %2d: fused-epilogue %8.1f us (%6.1f TF)   plain %8.1f us (%6.1f TF)\n", v, med(te),
+                flops / med(te) * 1e-6, med(tp), flops / med(tp) * 1e-6);
   }
-  auto med = [](std::vector<float> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
-  for (int v = 0; v < nvar; ++v) {
-    float a = med(t_epi[v]), b = med(t_plain[v]);
-    std::printf("NT variant %d: fused-epilogue %8.1f us (%6.1f TF)   plain %8.1f us (%6.1f TF)\n", v, a,
-                flops / a * 1e-6, b, flops / b * 1e-6);
-  }
-  // B read in place from Linear weights W1/W2 [H, F] (the production forward form)
-  {
-    float* w = dev_rand(2 * F * H, 0.08f, 7);
-    gnn_gemm_nt_params pw = p;
-    pw.bt = nullptr; pw.w1 = w; pw.w2 = w + F * H; pw.ldw1 = F; pw.ldw2 = F;
-    for (int v : {0, 1, 2, 3}) {
-      std::vector<float> tw;
-      for (int r = 0; r < rounds; ++r) tw.push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&pw, v, nullptr); }, 5));
-      float a = med(tw);
-      std::printf("NT variant %d w1/w2 form: fused-epilogue %8.1f us (%6.1f TF)\n", v, a, flops / a * 1e-6);
-    }
-  }
-  // TN (dz form + mask), the backward weight-gradient shape
+
+  // ---- TN (dz form + mask), the backward weight-gradient shape.  h = NT output (fused epilogue).
+  GK(gnnx_gemm_nt_variant_f32(&p, 16, nullptr));
   gnn_gemm_tn_params q{};
   q.M = M; q.Nr = H; q.dz = dz; q.lddz = 4; q.proj = proj; q.nproj = 4; q.h = c; q.ldh = H; q.hscale = 2.f;
   q.a1 = agg; q.lda1 = F; q.k1 = F; q.a2 = x; q.lda2 = F; q.k2 = F;
@@ -151,11 +150,54 @@ int main(int argc, char** argv) {
   GK(gnn_gemm_tn_workspace_size(M, H, 2 * F, 4, &wsb));
   void* ws;
   CK(hipMalloc(&ws, wsb));
+  const int64_t nout = H * 2 * F + H + 4 * H + 4;
   float* out;
-  CK(hipMalloc(&out, (H * 2 * F + H + 4 * H + 4) * sizeof(float)));
-  std::vector<float> tt;
-  for (int r = 0; r < rounds; ++r) tt.push_back(T.run([&] { gnn_gemm_tn_f32(&q, out, ws, wsb, nullptr); }, 5));
-  float a = med(tt);
-  std::printf("TN dz+mask: %8.1f us (%6.1f TF)\n", a, flops / a * 1e-6);
+  CK(hipMalloc(&out, nout * sizeof(float)));
+  {  // accuracy on the first Mc rows (float64 host reference)
+    const int64_t Mc = std::min<int64_t>(M, 20000);
+    gnn_gemm_tn_params qc = q;
+    qc.M = Mc;
+    auto h_h = to_host(c, Mc * H);
+    std::vector<double> rdw(H * 2 * F, 0.0), rdb(H, 0.0);
+    std::vector<double> g(H);
+    for (int64_t m = 0; m < Mc; ++m) {
+      for (int n = 0; n < H; ++n) {
+        double s = 0.0;
+        for (int qq = 0; qq < 4; ++qq) s += (double)h_dz[m * 4 + qq] * h_proj[qq * H + n];
+        // the kernels form G in f32 (fmaf chain), so compare on the same f32 G
+        float gf = h_dz[m * 4 + 0] * h_proj[n];
+        for (int qq = 1; qq < 4; ++qq) gf = std::fma(h_dz[m * 4 + qq], h_proj[qq * H + n], gf);
+        gf = h_h[m * H + n] > 0.f ? gf * 2.f : 0.f;
+        g[n] = gf;
+        rdb[n] += gf;
+        (void)s;
+      }
+      for (int n = 0; n < H; ++n) {
+        if (g[n] == 0.0) continue;
+        for (int k = 0; k < F; ++k) rdw[n * F + k] += g[n] * h_agg[m * F + k];
+        for (int k = 0; k < F; ++k) rdw[H * F + n * F + k] += g[n] * h_x[m * F + k];
+      }
+    }
+    for (int math : {1, 0}) {
+      qc.math = math;
+      GK(gnn_gemm_tn_f32(&qc, out, ws, wsb, nullptr));
+      auto got = to_host(out, nout);
+      double se = 0, sr = 0, mx = 0, rmx = 0;
+      for (int64_t i = 0; i < H * 2 * F; ++i) {
+        const double d = std::fabs(got[i] - rdw[i]);
+        se += d * d; sr += rdw[i] * rdw[i]; mx = std::max(mx, d); rmx = std::max(rmx, std::fabs(rdw[i]));
+      }
+      double dbe = 0;
+      for (int n = 0; n < H; ++n) dbe = std::max(dbe, std::fabs(got[H * 2 * F + n] - rdb[n]));
+      std::printf("TN math=%d (M=%lld) vs f64: dW relL2 %.3e  max|err| %.3e (max|ref| %.3e)  db max|err| %.3e\n", math,
+                  (long long)Mc, std::sqrt(se / sr), mx, rmx, dbe);
+    }
+  }
+  for (int math : {1, 0}) {
+    q.math = math;
+    std::vector<float> tt;
+    for (int r = 0; r < rounds; ++r) tt.push_back(T.run([&] { gnn_gemm_tn_f32(&q, out, ws, wsb, nullptr); }, 5));
+    std::printf("TN dz+mask math=%d: %8.1f us (%6.1f TF)\n", math, med(tt), flops / med(tt) * 1e-6);
+  }
   return 0;
 }

@@ -19,44 +19,15 @@
 // Both are atomic-free and deterministic.
 #include "common.hpp"
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
+#include <algorithm>
+
+#include "gemm_common.hpp"
 
 namespace gnnmp {
-
-// Dropout keep decision for element `idx` of a call seeded with `seed`: murmur3's fmix32
-// over (idx * golden + seed_lo) ^ seed_hi, top 24 bits compared with (1-p)·2^24.  32-bit
-// arithmetic only (3 multiplies).  Mirrored bit for bit by oracle/dropout_hash.py.
-__device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t idx, uint32_t keep_thresh) {
-  uint32_t h = idx * 0x9E3779B1u + (uint32_t)seed;
-  h ^= (uint32_t)(seed >> 32);
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
-  return (h >> 8) < keep_thresh;
-}
-
 namespace {
 
-constexpr int BN = 128;  // NT block columns (4 waves stacked by rows, each wave 4 x 32 columns)
 constexpr int BNP = BN + 2;  // LDS pitch of the B tile: 2P = 4 mod 32 makes the transposed weight stores (8 lanes x float2 per row) conflict-free
 
-struct NTArgs {
-  int64_t M;
-  int32_t Nc;
-  const float* a1; int64_t lda1; int32_t k1;
-  const float* a2; int64_t lda2; int32_t k2;
-  const float* bt; int64_t ldb;
-  const float* w1; const float* w2; int64_t ldw1, ldw2;  // alternative B: W1 [Nc, k1], W2 [Nc, k2]
-  int32_t wvec2;                                          // W rows 8-byte aligned, k1/k2 even
-  int32_t wvec;                                           // widest W row vector (1, 2, 4) for the nt2 staging
-  float* c; int64_t ldc;
-  const float* bias;
-  int32_t relu;
-  int32_t dropout; uint32_t keep_thresh; float drop_scale; uint64_t seed; const uint64_t* seed_ptr;
-  const float* proj; int32_t nproj; float* z; int64_t ldz;
-};
 
 // Tiling parameters: KC = K depth per LDS chunk, TM = 32-row tiles per wave (block rows
 // BM = 4 waves x 32·TM), UNR = fully unroll full chunks.
@@ -205,69 +176,6 @@ __device__ __forceinline__ void nt_kstep(floatx16 (&acc)[TM][4], const float* Aw
   }
 }
 
-// Epilogue shared by the NT kernels: bias, ReLU, dropout, store, optional projection.
-// acc[tm][t] is the 32x32 MFMA tile (rows wave·32·TM + tm·32 .., cols n0 + t·32 ..).
-template <int TM>
-__device__ __forceinline__ void nt_epilogue(const NTArgs& a, floatx16 (&acc)[TM][4], int64_t m0, int n0, int lane,
-                                            int wave, uint64_t seed) {
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
-    const int64_t rbase = m0 + wave * 32 * TM + tm * 32 + 4 * (lane >> 5);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int col = n0 + t * 32 + (lane & 31);
-      const bool colok = col < a.Nc;
-      const float bv = (a.bias && colok) ? a.bias[col] : 0.0f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-        float v = acc[tm][t][r] + bv;
-        if (a.relu) v = fmaxf(v, 0.0f);
-        if (a.dropout)
-          v = keep_elem(seed, (uint32_t)row * (uint32_t)a.Nc + (uint32_t)col, a.keep_thresh) ? v * a.drop_scale : 0.0f;
-        if (!colok) v = 0.0f;
-        if (a.c && row < a.M && colok) a.c[row * a.ldc + col] = v;
-        acc[tm][t][r] = v;
-      }
-    }
-    if (a.nproj > 0) {
-      // z[row, q] = Σ_col h[row, col] · proj[q, col].  Each lane holds 4 columns of each of its
-      // 16 rows; the 4 projection sums are reduced over the 32 lanes of a half-wave with a
-      // reduce-and-split butterfly: xor 16 halves the q set, xor 8 halves it again, then
-      // xor 4/2/1 finish one value — 6 shuffles per row instead of 4 x 5.
-      float pw[4][4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int col = n0 + t * 32 + (lane & 31);
-          pw[q][t] = (q < a.nproj && col < a.Nc) ? a.proj[(int64_t)q * a.Nc + col] : 0.0f;
-        }
-      const bool hi16 = lane & 16, hi8 = lane & 8;
-      const int qsel = (hi16 ? 2 : 0) + (hi8 ? 1 : 0);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float ps[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float sum = acc[tm][0][r] * pw[q][0];
-          sum = fmaf(acc[tm][1][r], pw[q][1], sum);
-          sum = fmaf(acc[tm][2][r], pw[q][2], sum);
-          ps[q] = fmaf(acc[tm][3][r], pw[q][3], sum);
-        }
-        const float s0 = hi16 ? ps[0] : ps[2], s1 = hi16 ? ps[1] : ps[3];
-        const float k0 = (hi16 ? ps[2] : ps[0]) + __shfl_xor(s0, 16);
-        const float k1 = (hi16 ? ps[3] : ps[1]) + __shfl_xor(s1, 16);
-        float m = (hi8 ? k1 : k0) + __shfl_xor(hi8 ? k0 : k1, 8);
-        m += __shfl_xor(m, 4);
-        m += __shfl_xor(m, 2);
-        m += __shfl_xor(m, 1);
-        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-        if ((lane & 7) == 0 && qsel < a.nproj && row < a.M) a.z[row * a.ldz + qsel] = m;
-      }
-    }
-  }
-}
 
 template <int AVEC, int KC, int TM, bool UNR, int EXP = 0>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs a) {
@@ -569,25 +477,7 @@ void launch_nt_variant(const NTArgs& a, int variant, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------ TN
-constexpr int TN_THREADS = 1024;  // 16 waves: wave w owns dW rows (w&3)*32.. and k-tiles (w>>2)*3 .. +3
-constexpr int KT_PER_WAVE = 3;
-constexpr int KMAX = 4 * KT_PER_WAVE * 32;  // Kc <= 384
-constexpr int TN_APITCH = KMAX;
-constexpr int MAXPROJ = 4;
 
-struct TNArgs {
-  int64_t M;
-  int32_t Nr;
-  const float* g; int64_t ldg;
-  const float* dz; int64_t lddz; const float* proj; int32_t nproj;
-  const float* h; int64_t ldh; float hscale;
-  float* gout; int64_t ldgout;
-  const float* a1; int64_t lda1; int32_t k1;
-  const float* a2; int64_t lda2; int32_t k2;
-  float* slab; int64_t slab_stride;
-  int64_t rows_per_block;
-  int32_t want_db;
-};
 
 // slab layout: dW[Nr][Kc] | db[Nr] | dW2[nproj][Nr] | dzsum[nproj]
 //
@@ -870,6 +760,7 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   if (p->nproj < 0 || p->nproj > 4 || (p->nproj > 0 && (p->N > BN || !p->proj || !p->z || p->ldz < p->nproj)))
     return fail(GNN_ERR_INVALID_ARG, fn, "projection needs N <= 128, nproj <= 4, proj and z");
   if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, fn, "dropout p in [0,1)");
+  if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, fn, "bad math mode");
   if (p->M == 0) return GNN_OK;
   NTArgs a{};
   a.M = p->M; a.Nc = (int32_t)p->N;
@@ -896,6 +787,11 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al(a.a1, 8) &&
             (a.k2 == 0 || ((a.k2 % 2 == 0) && (a.lda2 % 2 == 0) && al(a.a2, 8)));
   hipStream_t st = (hipStream_t)stream;
+  if (p->math != GNN_MATH_F32 && a.w1 && a.Nc <= BN && variant < 16) {
+    launch_nt_x3(a, variant, st);  // split-bf16 MFMA (gemm_x3.hip)
+    return hip_check(hipGetLastError(), fn);
+  }
+  if (variant >= 16) variant -= 16;  // lab: exact-f32 kernel variants
   if (v4) launch_nt_variant<4>(a, variant, st);
   else if (v2) launch_nt_variant<2>(a, variant, st);
   else launch_nt_variant<1>(a, variant, st);
@@ -933,6 +829,7 @@ extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, v
     return fail(GNN_ERR_INVALID_ARG, __func__, "need g (or dz + proj)");
   }
   if (p->h && p->ldh < p->Nr) return fail(GNN_ERR_INVALID_ARG, __func__, "bad ldh");
+  if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, __func__, "bad math mode");
   if (p->gout && p->ldgout < p->Nr) return fail(GNN_ERR_INVALID_ARG, __func__, "bad ldgout");
   const int32_t nproj = p->dz ? p->nproj : 0;
   const int64_t Kc = p->k1 + p->k2;
@@ -956,6 +853,15 @@ extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, v
   const bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al8(a.a1) &&
                   (a.k2 == 0 || ((a.k2 % 2 == 0) && (a.lda2 % 2 == 0) && al8(a.a2)));
   const bool proj = a.dz != nullptr, mask = a.h != nullptr;
+  // the split kernel indexes rows with 32-bit element offsets
+  const int64_t ldmax = std::max({a.lda1, a.k2 > 0 ? a.lda2 : 0, a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
+  if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31)) {
+    launch_tn_x3(a, nblk, st);  // split-bf16 MFMA (gemm_x3.hip)
+    GNN_LAUNCH_CHECK();
+    slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+    GNN_LAUNCH_CHECK();
+    return GNN_OK;
+  }
 #define GNN_TN(P, MK, V, R) gemm_tn_kernel<P, MK, V, R><<<nblk, TN_THREADS, 0, st>>>(a)
   // the dz·P + mask prologue holds twice the staging registers: 16-row chunks keep it spill-free
   if (proj && mask) { if (v2) GNN_TN(true, true, 2, 16); else GNN_TN(true, true, 1, 16); }

@@ -1,0 +1,506 @@
+// K7x — fp32 GEMMs of K7 on the bf16 matrix cores by operand splitting ("x3").
+//
+// gfx950 runs v_mfma_f32_32x32x16_bf16 at 16x the FLOP rate of the exact-f32
+// v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md, Matrix cores).  Each f32 operand is split on the
+// fly into three bf16 terms, a = hi + mid + lo, by round-to-nearest conversions whose remainders
+// are exact in f32 (hi keeps 8 significant bits, mid the next 8, lo the rest: the sum is exact
+// for every normal f32).  The product keeps the six terms of magnitude >= 2^-16 relative,
+//     a·b ≈ hh + hm + mh + hl + lh + mm     (dropped: ml + lm + ll <= ~2^-23 |a·b|, unbiased)
+// accumulated in f32 by the MFMA, i.e. fp32-accurate results at 16/6 = 2.7x the exact-f32 MFMA
+// peak.  The splits happen while staging into LDS (VALU, hidden under the MFMAs); both operands
+// are K-contiguous bf16 planes read as ds_read_b128 fragments (pitch ≡ 12 or 20 dwords mod 64:
+// conflict-free b128 lane groups).
+//
+// NT (forward, replaces lin_l/lin_r + ReLU + dropout, gnn.py:41-44,49-51):
+//   C = epi([A1 | A2] · [W1 | W2]ᵀ), W read in place from the Linear weights; epilogue shared
+//   with the f32 kernels (gemm_common.hpp: bias, ReLU, counter-hash dropout, projection).
+// TN (backward weight gradients): dW = Gᵀ·[A1 | A2] over row chunks of 16 (one MFMA k-step),
+//   G formed on the fly from dz·P (or g) and the ReLU/dropout mask of h; per-block slabs reduced
+//   in a fixed order by gemm_f32.hip's slab_reduce_kernel.  Atomic-free and deterministic.
+#include "gemm_common.hpp"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+namespace gnnmp {
+namespace {
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {  // RNE, a in the low half
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
+}
+
+// (a, b) -> three packed bf16 pairs w[0] (hi), w[1] (mid), w[2] (lo); a = hi + mid + lo exactly.
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t (&w)[3]) {
+  w[0] = pk_bf16(a, b);
+  a -= __uint_as_float(w[0] << 16);
+  b -= __uint_as_float(w[0] & 0xffff0000u);
+  w[1] = pk_bf16(a, b);
+  a -= __uint_as_float(w[1] << 16);
+  b -= __uint_as_float(w[1] & 0xffff0000u);
+  w[2] = pk_bf16(a, b);
+}
+
+__device__ __forceinline__ floatx16 mfma6(const bf16x8 (&x)[3], const bf16x8 (&y)[3], floatx16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[1], y[1], c, 0, 0, 0);  // small terms first
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[2], y[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[1], y[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[0], c, 0, 0, 0);
+  return c;
+}
+
+__device__ __forceinline__ bf16x8 lds_frag(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// ------------------------------------------------------------------------------------- NT
+// Stage rows [r0, r0+ROWS) x [k0, k0+KC) of a K-contiguous f32 operand into registers, in units
+// of U = max(V, 2) consecutive k per thread.  Addresses are clamped (never data-dependent), so
+// the prefetch stays in flight across the MFMAs; masking happens at the split/store.
+template <int V, int KC, int ROWS>
+__device__ __forceinline__ void x3_load_rows(const float* X, int64_t ldx, int64_t r0, int64_t rows, int k0,
+                                             int klen, float* reg) {
+  constexpr int U = V < 2 ? 2 : V;
+  constexpr int UPR = KC / U;
+#pragma unroll
+  for (int i = 0; i < ROWS * KC / 256 / U; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int r = v / UPR;
+    const int k = (v % UPR) * U;
+    int64_t row = r0 + r;
+    row = row < rows ? row : rows - 1;
+    const float* p = X + row * ldx + k0 + (k < klen ? k : 0);
+    if constexpr (V == 4) {
+      const float4 t = *reinterpret_cast<const float4*>(p);
+      reg[i * 4 + 0] = t.x; reg[i * 4 + 1] = t.y; reg[i * 4 + 2] = t.z; reg[i * 4 + 3] = t.w;
+    } else if constexpr (V == 2) {
+      const float2 t = *reinterpret_cast<const float2*>(p);
+      reg[i * 2 + 0] = t.x; reg[i * 2 + 1] = t.y;
+    } else {
+      reg[i * 2 + 0] = p[0];
+      reg[i * 2 + 1] = p[k + 1 < klen ? 1 : 0];
+    }
+  }
+}
+
+// Split and store into three bf16 planes L[p * ROWS * PITCH + r * PITCH + k]; zero outside
+// (rows, klen).
+template <int V, int KC, int ROWS, int PITCH>
+__device__ __forceinline__ void x3_store_rows(uint16_t* L, int64_t r0, int64_t rows, int klen, const float* reg) {
+  constexpr int U = V < 2 ? 2 : V;
+  constexpr int UPR = KC / U;
+  constexpr int PL = ROWS * PITCH;
+#pragma unroll
+  for (int i = 0; i < ROWS * KC / 256 / U; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int r = v / UPR;
+    const int k = (v % UPR) * U;
+    const bool rok = r0 + r < rows;
+    uint32_t w[U / 2][3];
+#pragma unroll
+    for (int j = 0; j < U / 2; ++j) {
+      const int kk = k + 2 * j;
+      const float e0 = (rok && kk < klen) ? reg[i * U + 2 * j] : 0.0f;
+      const float e1 = (rok && kk + 1 < klen) ? reg[i * U + 2 * j + 1] : 0.0f;
+      split_pair(e0, e1, w[j]);
+    }
+    uint16_t* d = L + r * PITCH + k;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      if constexpr (U == 4) *reinterpret_cast<uint2*>(d + p * PL) = make_uint2(w[0][p], w[1][p]);
+      else *reinterpret_cast<uint32_t*>(d + p * PL) = w[0][p];
+    }
+  }
+}
+
+template <int KC>
+__device__ __forceinline__ void x3_chunk(const NTArgs& a, int c, int nch1, const float*& A, int64_t& lda,
+                                         const float*& W, int64_t& ldw, int& k0, int& klen) {
+  if (c < nch1) { A = a.a1; lda = a.lda1; W = a.w1; ldw = a.ldw1; k0 = c * KC; klen = min(KC, a.k1 - k0); }
+  else { A = a.a2; lda = a.lda2; W = a.w2; ldw = a.ldw2; k0 = (c - nch1) * KC; klen = min(KC, a.k2 - k0); }
+}
+
+// Block: 4 waves, wave w owns rows w·32·TM .. (+32·TM) x all 128 columns (the epilogue's
+// projection needs whole rows in one wave).  K in chunks of KC through double-buffered LDS,
+// fed by a ring of D register stages: chunk c's loads are issued D chunks ahead, so D chunks
+// of A (BM x KC f32) are in flight per block while the MFMAs run (the split MFMA work per chunk
+// is short; without depth the loop waits on HBM latency).  One barrier per chunk.
+template <int KC, int TM, int AV, int BV, int D>
+__global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a) {
+  constexpr int P = KC + 8;  // bf16 per LDS row: 24 or 40 (12 / 20 dwords)
+  constexpr int BM = 128 * TM;
+  constexpr int APL = BM * P, BPL = BN * P;
+  constexpr int AREG = BM * KC / 256, BREG = BN * KC / 256;
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][3 * APL];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * BPL];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int nch1 = (a.k1 + KC - 1) / KC;
+  const int nchunks = nch1 + (a.k2 + KC - 1) / KC;
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+
+  floatx16 acc[TM][4];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tm][t][r] = 0.0f;
+
+  float ra[D][AREG], rb[D][BREG];
+  auto load = [&](int c, float* rA, float* rB) {
+    const float *A, *W; int64_t lda, ldw; int k0, klen;
+    x3_chunk<KC>(a, c, nch1, A, lda, W, ldw, k0, klen);
+    x3_load_rows<AV, KC, BM>(A, lda, m0, a.M, k0, klen, rA);
+    x3_load_rows<BV, KC, BN>(W, ldw, n0, a.Nc, k0, klen, rB);
+  };
+  auto store = [&](int c, int buf, const float* rA, const float* rB) {
+    const float *A, *W; int64_t lda, ldw; int k0, klen;
+    x3_chunk<KC>(a, c, nch1, A, lda, W, ldw, k0, klen);
+    x3_store_rows<AV, KC, BM, P>(As[buf], m0, a.M, klen, rA);
+    x3_store_rows<BV, KC, BN, P>(Bs[buf], n0, a.Nc, klen, rB);
+  };
+  const int fr = (lane & 31) * P + 8 * (lane >> 5);
+  auto compute = [&](int buf, int c) {
+    const int klen = c < nch1 ? min(KC, a.k1 - c * KC) : min(KC, a.k2 - (c - nch1) * KC);
+    const uint16_t* Ab = As[buf] + wave * 32 * TM * P + fr;
+    const uint16_t* Bb = Bs[buf] + fr;
+#pragma unroll
+    for (int s = 0; s < KC / 16; ++s) {
+      if (16 * s < klen) {
+        bf16x8 af[TM][3], bf[4][3];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) af[tm][p] = lds_frag(Ab + p * APL + tm * 32 * P + 16 * s);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) bf[t][p] = lds_frag(Bb + p * BPL + t * 32 * P + 16 * s);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm) acc[tm][t] = mfma6(af[tm], bf[t], acc[tm][t]);
+      }
+    }
+  };
+
+  // Loads are unconditional (a clamped chunk index: the tail re-reads the last chunk) so the
+  // main loop is straight-line code and the compiler's vmcnt waits leave the other D-1 stages
+  // in flight; a branch around a load makes it drain every stage at the next store.
+#pragma unroll
+  for (int d = 0; d < D; ++d) load(min(d, nchunks - 1), ra[d], rb[d]);
+  int c0 = 0;
+  for (; c0 + D <= nchunks; c0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int c = c0 + d;
+      const int buf = c & 1;
+      store(c, buf, ra[d], rb[d]);  // buf was last read by compute(c - 2): behind barrier c - 1
+      __syncthreads();
+      load(min(c + D, nchunks - 1), ra[d], rb[d]);
+      compute(buf, c);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) {  // tail: the last nchunks mod D chunks, already loaded
+    const int c = c0 + d;
+    if (c < nchunks) {
+      store(c, c & 1, ra[d], rb[d]);
+      __syncthreads();
+      compute(c & 1, c);
+    }
+  }
+  nt_epilogue<TM>(a, acc, m0, n0, lane, wave, seed);
+}
+
+template <int KC, int TM, int AV, int D>
+void launch_nt_x3_b(const NTArgs& a, hipStream_t st) {
+  dim3 grid((unsigned)ceil_div(a.M, 128 * TM), (unsigned)ceil_div(a.Nc, BN));
+  if (a.wvec == 4) gemm_nt_x3_kernel<KC, TM, AV, 4, D><<<grid, 256, 0, st>>>(a);
+  else if (a.wvec == 2) gemm_nt_x3_kernel<KC, TM, AV, 2, D><<<grid, 256, 0, st>>>(a);
+  else gemm_nt_x3_kernel<KC, TM, AV, 1, D><<<grid, 256, 0, st>>>(a);
+}
+
+template <int KC, int TM, int D>
+void launch_nt_x3_a(const NTArgs& a, int av, hipStream_t st) {
+  if (av == 4) launch_nt_x3_b<KC, TM, 4, D>(a, st);
+  else if (av == 2) launch_nt_x3_b<KC, TM, 2, D>(a, st);
+  else launch_nt_x3_b<KC, TM, 1, D>(a, st);
+}
+
+// ------------------------------------------------------------------------------------- TN
+constexpr int TMC = 16;            // rows per chunk = one MFMA k-step
+constexpr int TP = TMC + 8;        // bf16 per transposed LDS row (12 dwords: conflict-free b128)
+constexpr int TGPL = 128 * TP;     // G plane: [n][m]
+constexpr int TAPL = KMAX * TP;    // A plane: [k][m]
+constexpr int TX_THREADS = 256;    // 4 waves, one per SIMD (512 registers each)
+constexpr int TX_AS = 3;           // A unit slots per thread (u = tid + 256·s < 768)
+
+// Staging: every thread owns TX_AS A slots and one G slot (plus a g slot for the g form with
+// MASK), each 8 consecutive rows of one column described by (base, ld, octet) and loaded by
+// the SAME straight-line code whatever the role, so the ring of D register stages keeps D-1
+// chunks of loads in flight across the store/barrier (a branch around a load would make the
+// compiler drain every stage).
+//   A slot s: u = tid + 256·s -> column k = u mod KP, rows 8·(u / KP) ..  if u < 2·KP, else idle
+//   G slot:   column n = tid mod 128, rows 8·(tid / 128) ..: h[:, n] (MASK) or g[:, n]
+// Idle slots load a fixed valid address.  dz (PROJ) is staged one chunk ahead into a 2-slot
+// LDS ring (16 rows x 4) by threads 0..63, so G(c) = (dz·P) ⊙ mask is formed at store(c)
+// from LDS instead of 32 registers of replicated dz rows per thread.
+template <bool PROJ, bool MASK, int D, int KT>
+__global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
+  constexpr int NS = TX_AS + ((!PROJ && MASK) ? 2 : 1);  // + G slot (+ g slot)
+  constexpr int GS = TX_AS;                              // the G slot index
+  __shared__ __attribute__((aligned(16))) uint16_t Gt[2][3 * TGPL];
+  __shared__ __attribute__((aligned(16))) uint16_t At[2][3 * TAPL];
+  __shared__ float Ps[MAXPROJ * 128];
+  __shared__ float dzL[2][TMC * MAXPROJ];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int ntile = wave;
+  const int Kc = a.k1 + a.k2;
+  const int nkt = (Kc + 31) / 32;
+  const int KP = nkt * 32;
+  const int64_t mbeg = (int64_t)blockIdx.x * a.rows_per_block;
+  const int64_t mend = min(a.M, mbeg + a.rows_per_block);
+  const int nch = mend > mbeg ? (int)((mend - mbeg + TMC - 1) / TMC) : 0;
+
+  floatx16 acc[KT];  // KT >= nkt k-tiles, computed unconditionally (tiles >= nkt are discarded)
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+
+  if constexpr (PROJ) {
+    if (tid < 128) {
+#pragma unroll
+      for (int q = 0; q < MAXPROJ; ++q) Ps[q * 128 + tid] = (q < a.nproj && tid < a.Nr) ? a.proj[q * a.Nr + tid] : 0.0f;
+    }
+  }
+
+  // ---- slot descriptors
+  const int gn = tid & 127, go = tid >> 7;
+  const bool gcol = gn < a.Nr;
+  const int gnc = gcol ? gn : 0;
+  const float* base[NS];
+  int ld32[NS];
+  int oct[NS];
+  int ak[TX_AS];
+  bool aon[TX_AS];
+#pragma unroll
+  for (int sl = 0; sl < TX_AS; ++sl) {
+    const int u = tid + TX_THREADS * sl;
+    aon[sl] = u < 2 * KP;
+    ak[sl] = u % KP;
+    oct[sl] = u / KP;
+    const int k = ak[sl];
+    if (aon[sl] && k < a.k1) { base[sl] = a.a1 + k; ld32[sl] = (int)a.lda1; }
+    else if (aon[sl] && k < Kc) { base[sl] = a.a2 + (k - a.k1); ld32[sl] = (int)a.lda2; }
+    else { base[sl] = a.a1; ld32[sl] = 0; oct[sl] = 0; }
+  }
+  if constexpr (MASK) { base[GS] = a.h + gnc; ld32[GS] = (int)a.ldh; }
+  else { base[GS] = a.g + gnc; ld32[GS] = (int)a.ldg; }
+  oct[GS] = go;
+  if constexpr (NS == GS + 2) { base[GS + 1] = a.g + gnc; ld32[GS + 1] = (int)a.ldg; oct[GS + 1] = go; }
+  // dz element of this thread (threads 0..63 keep theirs: row tid/4, column tid%4)
+  const int zr = (tid & 63) / MAXPROJ, zq = (tid & 63) % MAXPROJ;
+  const int zqc = PROJ ? min(zq, a.nproj - 1) : 0;
+
+  // 32-bit element offsets (the dispatcher guarantees M·ld < 2^31): rows clamped to mend - 1
+  const int mlast = (int)(mend - 1);
+  float rv[D][NS][8];
+  float rz[D];
+  auto load = [&](int d, int c) {
+    const int m0 = (int)mbeg + c * TMC;
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = min(m0 + 8 * oct[sl] + i, mlast);
+        rv[d][sl][i] = base[sl][(uint32_t)(m * ld32[sl])];
+      }
+    if constexpr (PROJ) {  // dz rows of chunk c + 1
+      const int m = min(m0 + TMC + zr, mlast);
+      rz[d] = a.dz[(uint32_t)(m * (int)a.lddz + zqc)];
+    }
+  };
+
+  float db = 0.f, dzs = 0.f;
+  float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
+  auto put8 = [](uint16_t* dst, int plane, const float (&e)[8]) {
+    uint32_t w[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_pair(e[2 * j], e[2 * j + 1], w[j]);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      *reinterpret_cast<uint4*>(dst + p * plane) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+  };
+  auto store = [&](int d, int c) {
+    const int buf = c & 1;
+    const int64_t m0 = mbeg + (int64_t)c * TMC;
+    if constexpr (PROJ) {
+      if (tid < TMC * MAXPROJ) {
+        const bool ok = zq < a.nproj && m0 + TMC + zr < mend;
+        dzL[(c + 1) & 1][tid] = ok ? rz[d] : 0.0f;  // slot read by G(c - 1), behind barrier c - 1
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < TX_AS; ++sl) {
+      if (aon[sl]) {
+        float e[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = (ak[sl] < Kc && m0 + 8 * oct[sl] + i < mend) ? rv[d][sl][i] : 0.0f;
+        put8(At[buf] + ak[sl] * TP + 8 * oct[sl], TAPL, e);
+      }
+    }
+    float e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 8 * go + i;
+      const bool rok = m0 + r < mend;
+      const bool ok = rok && gcol;
+      float g;
+      if constexpr (PROJ) {
+        const float* z = &dzL[buf][r * MAXPROJ];
+        g = z[0] * Ps[gn];
+#pragma unroll
+        for (int q = 1; q < MAXPROJ; ++q) g = fmaf(z[q], Ps[q * 128 + gn], g);
+        if constexpr (MASK) {
+#pragma unroll
+          for (int q = 0; q < MAXPROJ; ++q) dw2[q] = fmaf(ok ? z[q] : 0.0f, rv[d][GS][i], dw2[q]);
+        }
+        if (gn < MAXPROJ) dzs += rok ? z[gn] : 0.0f;
+      } else {
+        g = rv[d][NS - 1][i];
+      }
+      if constexpr (MASK) g = rv[d][GS][i] > 0.0f ? g * a.hscale : 0.0f;
+      g = ok ? g : 0.0f;
+      db += g;
+      if (a.gout && ok) a.gout[(m0 + r) * a.ldgout + gn] = g;
+      e[i] = g;
+    }
+    put8(Gt[buf] + gn * TP + 8 * go, TGPL, e);
+  };
+
+  const int fr = (lane & 31) * TP + 8 * (lane >> 5);
+  auto compute = [&](int c) {
+    const int buf = c & 1;
+    bf16x8 gf[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) gf[p] = lds_frag(Gt[buf] + p * TGPL + ntile * 32 * TP + fr);
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      bf16x8 af[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) af[p] = lds_frag(At[buf] + p * TAPL + t * 32 * TP + fr);
+      acc[t] = mfma6(gf, af, acc[t]);
+    }
+  };
+
+  if (nch > 0) {
+    if constexpr (PROJ) {  // dz of chunk 0
+      if (tid < TMC * MAXPROJ) {
+        const int64_t m = mbeg + zr;
+        dzL[0][tid] = (zq < a.nproj && m < mend) ? a.dz[m * a.lddz + zqc] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(d, min(d, nch - 1));
+    __syncthreads();  // Ps, dzL[0]
+    int c0 = 0;
+    for (; c0 + D <= nch; c0 += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int c = c0 + d;
+        store(d, c);  // buffers of chunk c - 2: last read before barrier c - 1
+        __syncthreads();
+        load(d, min(c + D, nch - 1));
+        compute(c);
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int c = c0 + d;
+      if (c < nch) {
+        store(d, c);
+        __syncthreads();
+        compute(c);
+      }
+    }
+  }
+
+  // ---- this block's partial dW (segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2])
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    if (t >= nkt) continue;
+    const int col = t * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int64_t idx = col < a.k1 ? (int64_t)row * a.k1 + col
+                                     : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (col - a.k1);
+      if (row < a.Nr && col < Kc) slab[idx] = acc[t][r];
+    }
+  }
+  // ---- side sums of the two row octets (G slots), combined in a fixed order via LDS
+  float* red = reinterpret_cast<float*>(&At[0][0]);
+  constexpr int ns = 2 + MAXPROJ;
+  __syncthreads();
+  red[(go * 128 + gn) * ns + 0] = db;
+  red[(go * 128 + gn) * ns + 1] = dzs;
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
+  __syncthreads();
+  if (tid < 128 && tid < a.Nr) {
+    float* side = slab + (int64_t)a.Nr * Kc;
+    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
+    for (int q = 0; q < a.nproj; ++q)
+      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+  }
+  if (PROJ && tid < a.nproj)
+    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+}
+
+}  // namespace
+
+// variant: 0 = production; others are lab tilings (bench_gemm.cpp).
+void launch_nt_x3(const NTArgs& a, int variant, hipStream_t st) {
+  auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
+  auto av_ok = [&](int v) {
+    return (a.k1 % v == 0) && (a.lda1 % v == 0) && al(a.a1, 4 * v) &&
+           (a.k2 == 0 || ((a.k2 % v == 0) && (a.lda2 % v == 0) && al(a.a2, 4 * v)));
+  };
+  const int av = av_ok(4) ? 4 : (av_ok(2) ? 2 : 1);
+  switch (variant) {  // lab (bench_gemm.cpp, r01 MI355X): D=2 fastest, D=1 latency-bound, TM=2 / KC=32 too little occupancy
+    case 1: launch_nt_x3_a<16, 1, 1>(a, av, st); break;
+    case 2: launch_nt_x3_a<16, 1, 3>(a, av, st); break;
+    case 3: launch_nt_x3_a<16, 1, 4>(a, av, st); break;
+    case 4: launch_nt_x3_a<32, 1, 2>(a, av, st); break;
+    case 5: launch_nt_x3_a<16, 2, 2>(a, av, st); break;
+    default: launch_nt_x3_a<16, 1, 2>(a, av, st); break;
+  }
+}
+
+template <int D, int KT>
+void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
+  const bool proj = a.dz != nullptr, mask = a.h != nullptr;
+  if (proj && mask) gemm_tn_x3_kernel<true, true, D, KT><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (proj) gemm_tn_x3_kernel<true, false, D, KT><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (mask) gemm_tn_x3_kernel<false, true, D, KT><<<nblk, TX_THREADS, 0, st>>>(a);
+  else gemm_tn_x3_kernel<false, false, D, KT><<<nblk, TX_THREADS, 0, st>>>(a);
+}
+
+void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st) {
+  const int nkt = (a.k1 + a.k2 + 31) / 32;
+  constexpr int D = 1;
+  if (nkt <= 6) launch_tn_x3_k<D, 6>(a, nblk, st);
+  else if (nkt <= 8) launch_tn_x3_k<D, 8>(a, nblk, st);
+  else if (nkt <= 11) launch_tn_x3_k<D, 11>(a, nblk, st);
+  else launch_tn_x3_k<D, 12>(a, nblk, st);
+}
+
+}  // namespace gnnmp

@@ -20,6 +20,7 @@ kept values by 1/(1-p).
 """
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
@@ -30,13 +31,25 @@ from .graph import GraphPlan, get_plan
 
 MAX_PROJ = 4  # nproj = 2 * num_classes <= 4
 
+# K7 GEMM arithmetic (include/gnnmp.h gnn_gemm_math): "split_bf16" (default) runs every f32 operand
+# as hi+mid+lo bf16 terms on the bf16 matrix cores (6 products, fp32-accurate); "f32" runs the exact
+# f32 MFMA.  GNNMP_GEMM_MATH overrides the default.
+GEMM_MATH = {"split_bf16": _lib.MATH_SPLIT_BF16, "f32": _lib.MATH_F32}
+_DEFAULT_MATH = GEMM_MATH[os.environ.get("GNNMP_GEMM_MATH", "split_bf16")]
+
+
+def _math(math) -> int:
+    if math is None:
+        return _DEFAULT_MATH
+    return GEMM_MATH[math] if isinstance(math, str) else int(math)
+
 
 def _ld(t: torch.Tensor) -> int:
     return max(int(t.stride(0)), int(t.size(1)), 1)
 
 
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
-            out=None, want_c=True, seed_ptr=None, w1=None, w2=None):
+            out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None):
     """C = epilogue([a1 | a2] · B) on the MFMA NT kernel; B = bt ([K, n] row-major) or, with bt None,
     [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2]."""
     M = a1.size(0)
@@ -51,6 +64,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.ptr(out), _ld(out) if out is not None else 0,
         _lib.ptr(bias), int(relu), float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ptr),
         _lib.ptr(proj), proj.size(0) if proj is not None else 0, _lib.ptr(z), _ld(z) if z is not None else 0,
+        _math(math),
     )
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
@@ -64,7 +78,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
     return out
 
 
-def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gout=None):
+def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gout=None, math=None):
     """((Gᵀ·a1, Gᵀ·a2), db, dzᵀ·h, dzsum) from one flat fp32 buffer — the MFMA TN kernel."""
     M = a1.size(0)
     k1 = a1.size(1)
@@ -84,6 +98,7 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         _lib.ptr(gout), _ld(gout) if gout is not None else 0,
         a1.data_ptr(), _ld(a1), k1,
         _lib.ptr(a2), _ld(a2) if a2 is not None else 0, k2,
+        _math(math),
     )
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)

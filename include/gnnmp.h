@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 4
+#define GNNMP_ABI_VERSION 5
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -198,6 +198,14 @@ gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t con
 /*     Replace PyG Linear lin_l/lin_r/lin (gnn.py:20-23,41-44,64-67) and the  */
 /*     F.relu + F.dropout between layers (gnn.py:29-30,50-51,73-74).          */
 /* ------------------------------------------------------------------------ */
+/* Arithmetic of the K7 GEMMs.  Both are fp32-accurate (inputs, outputs and accumulation f32). */
+typedef enum {
+  GNN_MATH_SPLIT_BF16 = 0, /* default: every f32 operand split into hi+mid+lo bf16 terms, 6 products on
+                              v_mfma_f32_32x32x16_bf16 (dropped terms <= ~2^-23 relative per product);
+                              used for the w1/w2 NT form and the TN kernel, else falls back to: */
+  GNN_MATH_F32 = 1         /* exact f32 MFMA (v_mfma_f32_32x32x2_f32, a k-ordered fmaf chain) */
+} gnn_gemm_math;
+
 typedef struct {
   int64_t M, N;                          /* C is [M, N] */
   const float* a1; int64_t lda1; int64_t k1;
@@ -214,6 +222,7 @@ typedef struct {
                                             (graph-replay safe: bump the counter inside the graph) */
   const float* proj; int32_t nproj;      /* optional Z = C · projᵀ, proj [nproj, N], nproj <= 4, N <= 128 */
   float* z; int64_t ldz;
+  int32_t math;                          /* gnn_gemm_math */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
@@ -228,6 +237,7 @@ typedef struct {
   float* gout; int64_t ldgout;           /* optional: store G */
   const float* a1; int64_t lda1; int64_t k1;
   const float* a2; int64_t lda2; int64_t k2;
+  int32_t math;                          /* gnn_gemm_math */
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).

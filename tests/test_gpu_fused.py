@@ -1,7 +1,8 @@
 """GPU parity of the fp32 MFMA GEMM kernels (K7) and the fused SAGENet path.
 
 GEMMs are floating-point kernels: compared with a plain torch fp32 reference on the CPU
-(rtol=atol=1e-5 at these magnitudes).  The fused network is compared with the CPU oracle
+(rtol=atol=1e-5 at these magnitudes), in both arithmetic modes: "split_bf16" (the default:
+hi+mid+lo bf16 terms on the bf16 matrix cores) and "f32" (exact f32 MFMA).  The fused network is compared with the CPU oracle
 in eval mode and in train mode with dropout, using oracle/dropout_hash.py's bit-exact mask.
 """
 import numpy as np
@@ -23,7 +24,8 @@ def rel_l2(a, b, floor=1e-7):
 @pytest.mark.parametrize("M,k1,k2,n", [(1000, 166, 166, 128), (257, 5, 0, 3), (4097, 128, 128, 128),
                                        (300, 64, 64, 256), (129, 33, 17, 130), (64, 1, 0, 1)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu", "dropout", "proj"])
-def test_gemm_nt(device, M, k1, k2, n, epi):
+@pytest.mark.parametrize("wform", [False, True])
+def test_gemm_nt(device, M, k1, k2, n, epi, wform):
     from elliptic_gnn_project_amd.fused import gemm_nt
 
     if epi == "proj" and n > 128:
@@ -50,15 +52,21 @@ def test_gemm_nt(device, M, k1, k2, n, epi):
     if epi == "proj":
         z = torch.empty(M, 4, device=device)
         kw.update(proj=proj.to(device), z=z)
-    c = gemm_nt(a1.to(device), bt.to(device), n, a2=a2.to(device) if a2 is not None else None, **kw)
+    if wform:  # B read in place from Linear weights W [n, k] (the split-bf16 path when n <= 128)
+        kw.update(w1=bt[:k1].t().contiguous().to(device), w2=bt[k1:].t().contiguous().to(device) if k2 else None)
+        if n > 128:
+            pytest.skip("w1/w2 form needs N <= 128")
+    c = gemm_nt(a1.to(device), None if wform else bt.to(device), n,
+                a2=a2.to(device) if a2 is not None else None, **kw)
     torch.testing.assert_close(c.cpu(), ref, rtol=1e-5, atol=1e-5)
     if epi == "proj":
         torch.testing.assert_close(z.cpu(), ref @ proj.t(), rtol=1e-5, atol=1e-4)
 
 
 @pytest.mark.parametrize("M,k1,k2,n", [(1000, 166, 166, 128), (300, 7, 9, 33), (4097, 128, 0, 64)])
-def test_gemm_nt_weight_layout(device, M, k1, k2, n):
-    """B read in place from PyTorch Linear weights (w1/w2) == B from the transposed copy."""
+@pytest.mark.parametrize("math", ["split_bf16", "f32"])
+def test_gemm_nt_weight_layout(device, M, k1, k2, n, math):
+    """B read in place from PyTorch Linear weights (w1/w2) vs B from the transposed copy."""
     from elliptic_gnn_project_amd.fused import gemm_nt
 
     g = torch.Generator().manual_seed(M + n)
@@ -69,16 +77,42 @@ def test_gemm_nt_weight_layout(device, M, k1, k2, n):
     A = torch.cat([a1, a2], 1) if k2 else a1
     W = torch.cat([w1, w2], 1) if k2 else w1
     c = gemm_nt(a1.to(device), None, n, a2=a2.to(device) if k2 else None, w1=w1.to(device),
-                w2=w2.to(device) if k2 else None)
-    c2 = gemm_nt(a1.to(device), W.t().contiguous().to(device), n, a2=a2.to(device) if k2 else None)
-    assert torch.equal(c, c2)
+                w2=w2.to(device) if k2 else None, math=math)
+    c2 = gemm_nt(a1.to(device), W.t().contiguous().to(device), n, a2=a2.to(device) if k2 else None, math=math)
+    if math == "f32":
+        assert torch.equal(c, c2)  # the same k-ordered fmaf chain
     torch.testing.assert_close(c.cpu(), A @ W.t(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(c2.cpu(), A @ W.t(), rtol=1e-5, atol=1e-5)
+
+
+def test_gemm_split_bf16_accuracy_vs_f64(device):
+    """The split-bf16 product keeps fp32 accuracy: error vs a float64 reference is no larger than
+    the exact-f32 MFMA's (Elliptic layer-1 shape, both K segments)."""
+    from elliptic_gnn_project_amd.fused import gemm_nt, gemm_tn
+
+    g = torch.Generator().manual_seed(7)
+    M, F, n = 20000, 166, 128
+    a1, a2 = torch.randn(M, F, generator=g), torch.randn(M, F, generator=g)
+    w1, w2 = torch.randn(n, F, generator=g) * 0.08, torch.randn(n, F, generator=g) * 0.08
+    ref = (torch.cat([a1, a2], 1).double() @ torch.cat([w1, w2], 1).double().t())
+    errs = {}
+    for math in ("split_bf16", "f32"):
+        c = gemm_nt(a1.to(device), None, n, a2=a2.to(device), w1=w1.to(device), w2=w2.to(device), math=math)
+        errs[math] = rel_l2(c, ref)
+    assert errs["split_bf16"] < 1e-6 and errs["split_bf16"] < 2 * errs["f32"], errs
+    G = torch.randn(M, n, generator=g) * 1e-3
+    refw = G.double().t() @ torch.cat([a1, a2], 1).double()
+    for math in ("split_bf16", "f32"):
+        dW, _, _, _ = gemm_tn(n, a1.to(device), a2.to(device), g=G.to(device), math=math)
+        errs["tn_" + math] = rel_l2(torch.cat([dW[0], dW[1]], 1), refw)
+    assert errs["tn_split_bf16"] < 1e-6 and errs["tn_split_bf16"] < 2 * errs["tn_f32"], errs
 
 
 @pytest.mark.parametrize("M,nr,k1,k2", [(5000, 128, 166, 166), (777, 3, 20, 0), (64, 128, 128, 128),
                                         (20000, 64, 167, 167), (33, 1, 1, 0)])
 @pytest.mark.parametrize("form", ["g", "g_mask", "dz_mask"])
-def test_gemm_tn(device, M, nr, k1, k2, form):
+@pytest.mark.parametrize("math", ["split_bf16", "f32"])
+def test_gemm_tn(device, M, nr, k1, k2, form, math):
     from elliptic_gnn_project_amd.fused import gemm_tn
 
     g_ = torch.Generator().manual_seed(M + nr)
@@ -99,7 +133,8 @@ def test_gemm_tn(device, M, nr, k1, k2, form):
         G = torch.where(h > 0, G * 2.0, torch.zeros_like(G))
         kw.update(h=h.to(device), hscale=2.0)
     gout = torch.empty(M, nr, device=device)
-    dW, db, dW2, dzs = gemm_tn(nr, a1.to(device), a2.to(device) if a2 is not None else None, gout=gout, **kw)
+    dW, db, dW2, dzs = gemm_tn(nr, a1.to(device), a2.to(device) if a2 is not None else None, gout=gout,
+                               math=math, **kw)
     torch.testing.assert_close(gout.cpu(), G, rtol=1e-5, atol=1e-5)
     dWfull = torch.cat([dW[0], dW[1]], 1) if dW[1] is not None else dW[0]
     assert dW[0].is_contiguous()

@@ -77,9 +77,10 @@ STRUCTS = {
     "gnn_gemm_nt_params": ("GnnGemmNTParams", ["M", "N", "a1", "lda1", "k1", "a2", "lda2", "k2", "bt", "ldb",
                                                "w1", "w2", "ldw1", "ldw2", "c",
                                                "ldc", "bias", "relu", "dropout_p", "seed", "seed_ptr", "proj",
-                                               "nproj", "z", "ldz"]),
+                                               "nproj", "z", "ldz", "math"]),
     "gnn_gemm_tn_params": ("GnnGemmTNParams", ["M", "Nr", "g", "ldg", "dz", "lddz", "proj", "nproj", "h", "ldh",
-                                               "hscale", "gout", "ldgout", "a1", "lda1", "k1", "a2", "lda2", "k2"]),
+                                               "hscale", "gout", "ldgout", "a1", "lda1", "k1", "a2", "lda2", "k2",
+                                               "math"]),
 }
 
 
