@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the step as one captured HIP graph")
     ap.add_argument("--arch", default="sage", choices=sorted(PRESETS), help="workload (sage = headline)")
+    ap.add_argument("--aten-step", action="store_true",
+                    help="loss/clip/Adam with the ATen ops instead of the fused libgnnmp step ops")
     return ap.parse_args()
 
 
@@ -229,7 +231,11 @@ def main():
         gdist.convert_sync_batchnorm(model, dist)  # exact full-graph BN (SAGE-ResBN); no-op otherwise
     state0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     use_graph = args.graph
-    opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4, fused=True, capturable=use_graph)
+    if args.aten_step:
+        opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4, fused=True, capturable=use_graph)
+    else:  # clip_grad_norm_(1.0) + Adam fused (train_ops.ClipAdam: 2 launches, device step counter)
+        from elliptic_gnn_project_amd.train_ops import ClipAdam
+        opt = ClipAdam(model.parameters(), lr=0.003, weight_decay=1e-4, max_norm=1.0)
     cw, denom = gdist.global_class_weight_and_count(data.y, data.train_mask, dist)
     loss_fn = _make_loss_fn({}, cw, model, 1, 34)
     bucket = gdist.GradBucket(model) if dist is not None else None
@@ -241,11 +247,15 @@ def main():
         model.train()
         opt.zero_grad(set_to_none=bucket is None)
         logits = model(data.x, data.edge_index, t_idx)
-        loss = loss_fn(logits.index_select(0, tidx), ytr, denom=denom)
+        if args.aten_step:
+            loss = loss_fn(logits.index_select(0, tidx), ytr, denom=denom)
+        else:  # the same masked weighted CE, one fused kernel (fwd + dlogits)
+            loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
         loss.backward()
         if bucket is not None:
             bucket.allreduce_(dist)
-        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        if args.aten_step:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
         opt.step()
         return loss
 

@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # gnn_gemm_math
 MATH_SPLIT_BF16 = 0
@@ -107,6 +107,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("seed_ptr", c_ptr),
         ("proj", c_ptr), ("nproj", c_i32), ("z", c_ptr), ("ldz", c_i64),
         ("math", c_i32),
+        ("workspace", c_ptr), ("workspace_bytes", c_size),
     ]
 
 
@@ -121,6 +122,22 @@ class GnnGemmTNParams(ctypes.Structure):
         ("a1", c_ptr), ("lda1", c_i64), ("k1", c_i64),
         ("a2", c_ptr), ("lda2", c_i64), ("k2", c_i64),
         ("math", c_i32),
+    ]
+
+
+ADAM_MAX_TENSORS = 24
+
+
+class GnnAdamTensor(ctypes.Structure):
+    _fields_ = [("param", c_ptr), ("grad", c_ptr), ("exp_avg", c_ptr), ("exp_avg_sq", c_ptr), ("numel", c_i64)]
+
+
+class GnnAdamGroup(ctypes.Structure):
+    _fields_ = [
+        ("num_tensors", c_i32),
+        ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
+        ("weight_decay", ctypes.c_double), ("max_norm", ctypes.c_double),
+        ("tensors", GnnAdamTensor * ADAM_MAX_TENSORS),
     ]
 
 
@@ -170,11 +187,19 @@ SIGNATURES = {
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
          c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
+    "gnn_gemm_nt_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_size)]),
     "gnn_gemm_nt_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),
     "gnn_gemm_tn_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32, ctypes.POINTER(c_size)]),
     "gnn_gemm_tn_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams), c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_colsum_workspace_size": (ctypes.c_int, [c_i64, c_i64, ctypes.POINTER(c_size)]),
     "gnn_colsum_f32": (ctypes.c_int, [c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
+    "gnn_masked_ce_workspace_size": (ctypes.c_int, [c_i64, ctypes.POINTER(c_size)]),
+    "gnn_masked_ce_f32": (
+        ctypes.c_int,
+        [c_i64, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_clip_adam_workspace_size": (ctypes.c_int, [ctypes.POINTER(c_size)]),
+    "gnn_clip_adam_f32": (ctypes.c_int, [ctypes.POINTER(GnnAdamGroup), c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
 }
 
 _LIB: ctypes.CDLL | None = None

@@ -90,11 +90,15 @@ int main(int argc, char** argv) {
   p.w1 = w; p.w2 = w + F * H; p.ldw1 = F; p.ldw2 = F;
   p.c = c; p.ldc = H; p.bias = bias; p.relu = 1; p.dropout_p = 0.5f; p.seed = 1234;
   p.proj = proj; p.nproj = 4; p.z = z; p.ldz = 4;
+  size_t ntws = 0;
+  GK(gnn_gemm_nt_workspace_size(H, F, F, &ntws));
+  CK(hipMalloc(&p.workspace, ntws));
+  p.workspace_bytes = ntws;
   gnn_gemm_nt_params plain = p;
   plain.bias = nullptr; plain.relu = 0; plain.dropout_p = 0.f; plain.proj = nullptr; plain.nproj = 0; plain.z = nullptr;
 
   // ---- NT accuracy vs float64 on sampled rows (plain GEMM)
-  const std::vector<int> variants = {0, 1, 2, 3, 4, 5, 6, 16};  // <16: split-bf16 tilings; >=16: exact f32
+  const std::vector<int> variants = {0, 1, 2, 3, 5, 16};  // <16: split-bf16 tilings; >=16: exact f32
   std::vector<int64_t> rows;
   for (int64_t r = 0; r < M; r += std::max<int64_t>(1, M / 3000)) rows.push_back(r);
   rows.push_back(M - 1);

@@ -126,7 +126,8 @@ struct TNArgs {
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,
 // defined in gemm_x3.hip.  Only the w1/w2 (in-place Linear weight) B form runs split.
-void launch_nt_x3(const NTArgs& a, int variant, hipStream_t st);
+void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipStream_t st);
+size_t nt_x3_workspace(int64_t k1, int64_t k2);
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st);
 
 }  // namespace gnnmp

@@ -788,7 +788,7 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
             (a.k2 == 0 || ((a.k2 % 2 == 0) && (a.lda2 % 2 == 0) && al(a.a2, 8)));
   hipStream_t st = (hipStream_t)stream;
   if (p->math != GNN_MATH_F32 && a.w1 && a.Nc <= BN && variant < 16) {
-    launch_nt_x3(a, variant, st);  // split-bf16 MFMA (gemm_x3.hip)
+    launch_nt_x3(a, variant, p->workspace, p->workspace_bytes, st);  // split-bf16 MFMA (gemm_x3.hip)
     return hip_check(hipGetLastError(), fn);
   }
   if (variant >= 16) variant -= 16;  // lab: exact-f32 kernel variants
@@ -796,6 +796,12 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   else if (v2) launch_nt_variant<2>(a, variant, st);
   else launch_nt_variant<1>(a, variant, st);
   return hip_check(hipGetLastError(), fn);
+}
+
+extern "C" gnn_status gnn_gemm_nt_workspace_size(int64_t N, int64_t k1, int64_t k2, size_t* bytes) {
+  if (!bytes || N < 1 || k1 < 1 || k2 < 0) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
+  *bytes = N <= BN ? nt_x3_workspace(k1, k2) : 0;
+  return GNN_OK;
 }
 
 extern "C" gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream) {

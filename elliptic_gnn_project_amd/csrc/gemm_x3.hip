@@ -55,12 +55,12 @@ __device__ __forceinline__ bf16x8 lds_frag(const uint16_t* p) { return *reinterp
 
 // ------------------------------------------------------------------------------------- NT
 // Stage rows [r0, r0+ROWS) x [k0, k0+KC) of a K-contiguous f32 operand into registers, in units
-// of U = max(V, 2) consecutive k per thread.  Addresses are clamped (never data-dependent), so
-// the prefetch stays in flight across the MFMAs; masking happens at the split/store.
-template <int V, int KC, int ROWS>
+// of U consecutive k per thread, each loaded as U/V vectors of V floats (V | k1, k2, ld).
+// Addresses are clamped (never data-dependent), so the prefetch stays in flight across the
+// MFMAs; masking happens at the split/store.
+template <int V, int U, int KC, int ROWS>
 __device__ __forceinline__ void x3_load_rows(const float* X, int64_t ldx, int64_t r0, int64_t rows, int k0,
                                              int klen, float* reg) {
-  constexpr int U = V < 2 ? 2 : V;
   constexpr int UPR = KC / U;
 #pragma unroll
   for (int i = 0; i < ROWS * KC / 256 / U; ++i) {
@@ -69,25 +69,27 @@ __device__ __forceinline__ void x3_load_rows(const float* X, int64_t ldx, int64_
     const int k = (v % UPR) * U;
     int64_t row = r0 + r;
     row = row < rows ? row : rows - 1;
-    const float* p = X + row * ldx + k0 + (k < klen ? k : 0);
-    if constexpr (V == 4) {
-      const float4 t = *reinterpret_cast<const float4*>(p);
-      reg[i * 4 + 0] = t.x; reg[i * 4 + 1] = t.y; reg[i * 4 + 2] = t.z; reg[i * 4 + 3] = t.w;
-    } else if constexpr (V == 2) {
-      const float2 t = *reinterpret_cast<const float2*>(p);
-      reg[i * 2 + 0] = t.x; reg[i * 2 + 1] = t.y;
-    } else {
-      reg[i * 2 + 0] = p[0];
-      reg[i * 2 + 1] = p[k + 1 < klen ? 1 : 0];
+    const float* p = X + row * ldx + k0;
+#pragma unroll
+    for (int j = 0; j < U; j += V) {
+      const int kk = k + j < klen ? k + j : 0;
+      if constexpr (V == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(p + kk);
+        reg[i * U + j] = t.x; reg[i * U + j + 1] = t.y; reg[i * U + j + 2] = t.z; reg[i * U + j + 3] = t.w;
+      } else if constexpr (V == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(p + kk);
+        reg[i * U + j] = t.x; reg[i * U + j + 1] = t.y;
+      } else {
+        reg[i * U + j] = p[kk];
+      }
     }
   }
 }
 
-// Split and store into three bf16 planes L[p * ROWS * PITCH + r * PITCH + k]; zero outside
-// (rows, klen).
-template <int V, int KC, int ROWS, int PITCH>
+// Split and store into three bf16 planes L[p * ROWS * PITCH + r * PITCH + k] (one b32 / b64 /
+// b128 store per plane for U = 2 / 4 / 8); zero outside (rows, klen).
+template <int U, int KC, int ROWS, int PITCH>
 __device__ __forceinline__ void x3_store_rows(uint16_t* L, int64_t r0, int64_t rows, int klen, const float* reg) {
-  constexpr int U = V < 2 ? 2 : V;
   constexpr int UPR = KC / U;
   constexpr int PL = ROWS * PITCH;
 #pragma unroll
@@ -107,10 +109,34 @@ __device__ __forceinline__ void x3_store_rows(uint16_t* L, int64_t r0, int64_t r
     uint16_t* d = L + r * PITCH + k;
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
-      if constexpr (U == 4) *reinterpret_cast<uint2*>(d + p * PL) = make_uint2(w[0][p], w[1][p]);
+      if constexpr (U == 8) *reinterpret_cast<uint4*>(d + p * PL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+      else if constexpr (U == 4) *reinterpret_cast<uint2*>(d + p * PL) = make_uint2(w[0][p], w[1][p]);
       else *reinterpret_cast<uint32_t*>(d + p * PL) = w[0][p];
     }
   }
+}
+
+// B pre-split once per call (BV == 0 kernels): per KC=16 chunk c, image [plane][n 128][16 k]
+// bf16 (12 KB, zero outside k < klen, n < Nc), copied to LDS as 3 b128 per thread per chunk.
+__global__ __launch_bounds__(256) void x3_presplit_b_kernel(NTArgs a, uint4* __restrict__ img, int nch1,
+                                                            int nchunks) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;  // (chunk, n, khalf)
+  if (idx >= nchunks * 256) return;
+  const int c = idx >> 8, n = (idx & 255) >> 1, kh = idx & 1;
+  const float* W; int64_t ldw; int k0, klen;
+  if (c < nch1) { W = a.w1; ldw = a.ldw1; k0 = c * 16; klen = min(16, a.k1 - k0); }
+  else { W = a.w2; ldw = a.ldw2; k0 = (c - nch1) * 16; klen = min(16, a.k2 - k0); }
+  float e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kh + j;
+    e[j] = (n < a.Nc && k < klen) ? W[(int64_t)n * ldw + k0 + k] : 0.0f;
+  }
+  uint32_t w[4][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) split_pair(e[2 * j], e[2 * j + 1], w[j]);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) img[((int64_t)c * 3 + p) * 256 + (idx & 255)] = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
 }
 
 template <int KC>
@@ -125,8 +151,8 @@ __device__ __forceinline__ void x3_chunk(const NTArgs& a, int c, int nch1, const
 // fed by a ring of D register stages: chunk c's loads are issued D chunks ahead, so D chunks
 // of A (BM x KC f32) are in flight per block while the MFMAs run (the split MFMA work per chunk
 // is short; without depth the loop waits on HBM latency).  One barrier per chunk.
-template <int KC, int TM, int AV, int BV, int D>
-__global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a) {
+template <int KC, int TM, int AV, int AU, int BV, int D>
+__global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* __restrict__ bimg) {
   constexpr int P = KC + 8;  // bf16 per LDS row: 24 or 40 (12 / 20 dwords)
   constexpr int BM = 128 * TM;
   constexpr int APL = BM * P, BPL = BN * P;
@@ -149,18 +175,40 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[tm][t][r] = 0.0f;
 
-  float ra[D][AREG], rb[D][BREG];
+  // BV > 0: B split on the fly from the f32 weights; BV == 0: B copied from the pre-split image
+  constexpr int BU = BV < 2 ? 2 : BV;
+  constexpr int RB = BV == 0 ? 12 : BREG;  // image: 3 planes x uint4 per thread (KC = 16)
+  static_assert(BV > 0 || KC == 16, "pre-split B image is cut in 16-deep chunks");
+  float ra[D][AREG], rb[D][RB];
   auto load = [&](int c, float* rA, float* rB) {
     const float *A, *W; int64_t lda, ldw; int k0, klen;
     x3_chunk<KC>(a, c, nch1, A, lda, W, ldw, k0, klen);
-    x3_load_rows<AV, KC, BM>(A, lda, m0, a.M, k0, klen, rA);
-    x3_load_rows<BV, KC, BN>(W, ldw, n0, a.Nc, k0, klen, rB);
+    x3_load_rows<AV, AU, KC, BM>(A, lda, m0, a.M, k0, klen, rA);
+    if constexpr (BV == 0) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const uint4 t = bimg[((int64_t)c * 3 + p) * 256 + threadIdx.x];
+        rB[4 * p] = __uint_as_float(t.x); rB[4 * p + 1] = __uint_as_float(t.y);
+        rB[4 * p + 2] = __uint_as_float(t.z); rB[4 * p + 3] = __uint_as_float(t.w);
+      }
+    } else {
+      x3_load_rows<BV, BU, KC, BN>(W, ldw, n0, a.Nc, k0, klen, rB);
+    }
   };
   auto store = [&](int c, int buf, const float* rA, const float* rB) {
     const float *A, *W; int64_t lda, ldw; int k0, klen;
     x3_chunk<KC>(a, c, nch1, A, lda, W, ldw, k0, klen);
-    x3_store_rows<AV, KC, BM, P>(As[buf], m0, a.M, klen, rA);
-    x3_store_rows<BV, KC, BN, P>(Bs[buf], n0, a.Nc, klen, rB);
+    x3_store_rows<AU, KC, BM, P>(As[buf], m0, a.M, klen, rA);
+    if constexpr (BV == 0) {
+      const int n = threadIdx.x >> 1, kh = threadIdx.x & 1;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint4*>(&Bs[buf][p * BPL + n * P + 8 * kh]) =
+            make_uint4(__float_as_uint(rB[4 * p]), __float_as_uint(rB[4 * p + 1]), __float_as_uint(rB[4 * p + 2]),
+                       __float_as_uint(rB[4 * p + 3]));
+    } else {
+      x3_store_rows<BU, KC, BN, P>(Bs[buf], n0, a.Nc, klen, rB);
+    }
   };
   const int fr = (lane & 31) * P + 8 * (lane >> 5);
   auto compute = [&](int buf, int c) {
@@ -216,19 +264,20 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a) {
   nt_epilogue<TM>(a, acc, m0, n0, lane, wave, seed);
 }
 
-template <int KC, int TM, int AV, int D>
-void launch_nt_x3_b(const NTArgs& a, hipStream_t st) {
+template <int KC, int TM, int AV, int AU, int D>
+void launch_nt_x3_b(const NTArgs& a, const uint4* bimg, hipStream_t st) {
   dim3 grid((unsigned)ceil_div(a.M, 128 * TM), (unsigned)ceil_div(a.Nc, BN));
-  if (a.wvec == 4) gemm_nt_x3_kernel<KC, TM, AV, 4, D><<<grid, 256, 0, st>>>(a);
-  else if (a.wvec == 2) gemm_nt_x3_kernel<KC, TM, AV, 2, D><<<grid, 256, 0, st>>>(a);
-  else gemm_nt_x3_kernel<KC, TM, AV, 1, D><<<grid, 256, 0, st>>>(a);
+  if (bimg) gemm_nt_x3_kernel<KC, TM, AV, AU, 0, D><<<grid, 256, 0, st>>>(a, bimg);
+  else if (a.wvec == 4) gemm_nt_x3_kernel<KC, TM, AV, AU, 4, D><<<grid, 256, 0, st>>>(a, nullptr);
+  else if (a.wvec == 2) gemm_nt_x3_kernel<KC, TM, AV, AU, 2, D><<<grid, 256, 0, st>>>(a, nullptr);
+  else gemm_nt_x3_kernel<KC, TM, AV, AU, 1, D><<<grid, 256, 0, st>>>(a, nullptr);
 }
 
-template <int KC, int TM, int D>
-void launch_nt_x3_a(const NTArgs& a, int av, hipStream_t st) {
-  if (av == 4) launch_nt_x3_b<KC, TM, 4, D>(a, st);
-  else if (av == 2) launch_nt_x3_b<KC, TM, 2, D>(a, st);
-  else launch_nt_x3_b<KC, TM, 1, D>(a, st);
+template <int KC, int TM, int D, int AU>
+void launch_nt_x3_a(const NTArgs& a, int av, const uint4* bimg, hipStream_t st) {
+  if (av == 4) launch_nt_x3_b<KC, TM, 4, (AU < 4 ? 4 : AU), D>(a, bimg, st);
+  else if (av == 2) launch_nt_x3_b<KC, TM, 2, AU, D>(a, bimg, st);
+  else launch_nt_x3_b<KC, TM, 1, AU, D>(a, bimg, st);
 }
 
 // ------------------------------------------------------------------------------------- TN
@@ -468,20 +517,34 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 }  // namespace
 
 // variant: 0 = production; others are lab tilings (bench_gemm.cpp).
-void launch_nt_x3(const NTArgs& a, int variant, hipStream_t st) {
+size_t nt_x3_workspace(int64_t k1, int64_t k2) {  // pre-split B image, 12 KB per 16-deep chunk
+  return (size_t)((k1 + 15) / 16 + (k2 + 15) / 16) * 3 * 256 * sizeof(uint4);
+}
+
+// variant: 0 = production; others are lab tilings (bench_gemm.cpp).
+void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipStream_t st) {
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
   auto av_ok = [&](int v) {
     return (a.k1 % v == 0) && (a.lda1 % v == 0) && al(a.a1, 4 * v) &&
            (a.k2 == 0 || ((a.k2 % v == 0) && (a.lda2 % v == 0) && al(a.a2, 4 * v)));
   };
   const int av = av_ok(4) ? 4 : (av_ok(2) ? 2 : 1);
-  switch (variant) {  // lab (bench_gemm.cpp, r01 MI355X): D=2 fastest, D=1 latency-bound, TM=2 / KC=32 too little occupancy
-    case 1: launch_nt_x3_a<16, 1, 1>(a, av, st); break;
-    case 2: launch_nt_x3_a<16, 1, 3>(a, av, st); break;
-    case 3: launch_nt_x3_a<16, 1, 4>(a, av, st); break;
-    case 4: launch_nt_x3_a<32, 1, 2>(a, av, st); break;
-    case 5: launch_nt_x3_a<16, 2, 2>(a, av, st); break;
-    default: launch_nt_x3_a<16, 1, 2>(a, av, st); break;
+  const uint4* bimg = nullptr;
+  const bool pre = ws && ws_bytes >= nt_x3_workspace(a.k1, a.k2) && a.Nc <= BN;
+  if (pre) {
+    const int nch1 = (a.k1 + 15) / 16, nch = nch1 + (a.k2 + 15) / 16;
+    x3_presplit_b_kernel<<<nch, 256, 0, st>>>(a, static_cast<uint4*>(ws), nch1, nch);
+    bimg = static_cast<const uint4*>(ws);
+  }
+  // lab (bench_gemm.cpp, MI355X, Elliptic layer-1 shape, fused epilogue): pre-split B with b32 A
+  // stores and D = 2 184 us; B split in-kernel 195-200 us; D = 1 228 us; D = 3 188 us.
+  switch (variant) {
+    case 1: launch_nt_x3_a<16, 1, 1, 2>(a, av, bimg, st); break;
+    case 2: launch_nt_x3_a<16, 1, 3, 4>(a, av, bimg, st); break;
+    case 3: launch_nt_x3_a<16, 1, 2, 2>(a, av, nullptr, st); break;
+    case 4: launch_nt_x3_a<16, 1, 2, 4>(a, av, nullptr, st); break;
+    case 5: launch_nt_x3_a<16, 1, 2, 8>(a, av, bimg, st); break;
+    default: launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st); break;
   }
 }
 

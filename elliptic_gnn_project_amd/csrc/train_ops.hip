@@ -1,0 +1,229 @@
+// The small per-step work around the hot path, fused: the masked class-weighted cross entropy
+// of src/train_gnn.py:136-183 (loss + dlogits in one pass over the N rows) and
+// clip_grad_norm_ + Adam (src/train_gnn.py:203-206) over every parameter in two launches.
+// Both replace chains of 6-12 small ATen kernels (index_select, log_softmax, nll_loss, their
+// backward passes and zero fills; per-tensor norms, stack, clamp, mul, multi-tensor Adam).
+// Reductions are fixed-order (block partials summed in index order): bitwise reproducible.
+#include <algorithm>
+#include <cmath>
+
+#include "common.hpp"
+
+namespace gnnmp {
+namespace {
+
+constexpr int kCeThreads = 256;
+constexpr int kMaxClasses = 16;
+
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  // wave64 butterfly, then the 4 wave sums in order
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+  return t;  // valid in thread 0
+}
+
+// loss_i = -w[y_i] · log_softmax(x_i)[y_i] on rows with mask_i (F.cross_entropy(weight=w,
+// reduction='none')); dx_i = w[y_i] · (softmax(x_i) - onehot(y_i)) · inv_denom there, 0 elsewhere.
+// partial[b] = Σ loss over block b's rows.
+template <int CT>  // CT > 0: compile-time class count (registers); CT == 0: runtime C <= kMaxClasses
+__global__ __launch_bounds__(kCeThreads) void masked_ce_kernel(int64_t N, int Crt, const float* __restrict__ x,
+                                                               int64_t ldx, const int64_t* __restrict__ y,
+                                                               const uint8_t* __restrict__ mask,
+                                                               const float* __restrict__ w, float inv_denom,
+                                                               float* __restrict__ dx, int64_t ldd,
+                                                               float* __restrict__ partial) {
+  constexpr int CM = CT > 0 ? CT : kMaxClasses;
+  const int C = CT > 0 ? CT : Crt;
+  __shared__ float sh[kCeThreads / 64];
+  const int64_t row = (int64_t)blockIdx.x * kCeThreads + threadIdx.x;
+  float l = 0.f;
+  if (row < N) {
+    const int64_t t = y[row];
+    const bool on = mask[row] != 0 && t >= 0 && t < C;
+    float v[CM];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) {
+        v[c] = x[row * ldx + c];
+        mx = fmaxf(mx, v[c]);
+      }
+    float s = 0.f, xt = 0.f;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) {
+        if (c == t) xt = v[c];
+        v[c] = expf(v[c] - mx);
+        s += v[c];
+      }
+    const float wt = on ? w[t] : 0.f;
+    if (on) l = -wt * (xt - mx - logf(s));
+    const float g = wt * inv_denom, rs = 1.0f / s;
+#pragma unroll
+    for (int c = 0; c < CM; ++c)
+      if (c < C) dx[row * ldd + c] = on ? g * (v[c] * rs - (c == t ? 1.f : 0.f)) : 0.f;
+  }
+  const float t = block_sum(l, sh);
+  if (threadIdx.x == 0) partial[blockIdx.x] = t;
+}
+
+// out[0] = scale · Σ_i partial[i], summed in a fixed order by one block.
+__global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restrict__ partial, int n, float scale,
+                                                           float* __restrict__ out) {
+  __shared__ float sh[4];
+  float v = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) v += partial[i];
+  const float t = block_sum(v, sh);
+  if (threadIdx.x == 0) out[0] = t * scale;
+}
+
+// ---------------------------------------------------------------------------- clip + Adam
+constexpr int kAdamThreads = 256;
+constexpr int kAdamBlocks = 64;
+
+struct AdamTable {
+  int32_t n;
+  float* p[GNN_ADAM_MAX_TENSORS];
+  float* g[GNN_ADAM_MAX_TENSORS];
+  float* m[GNN_ADAM_MAX_TENSORS];
+  float* v[GNN_ADAM_MAX_TENSORS];
+  int64_t off[GNN_ADAM_MAX_TENSORS + 1];  // element offsets of the flattened parameter list
+};
+
+// Σ g² over this block's slice of the flattened gradients; block 0 also advances the step.
+__global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, float* __restrict__ partial,
+                                                                float* __restrict__ step) {
+  __shared__ float sh[kAdamThreads / 64];
+  const int64_t total = tb.off[tb.n];
+  const int64_t per = (total + gridDim.x - 1) / gridDim.x;
+  const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(total, e0 + per);
+  float s = 0.f;
+  int j = 0;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamThreads) {
+    while (e >= tb.off[j + 1]) ++j;
+    const float g = tb.g[j][e - tb.off[j]];
+    s = fmaf(g, g, s);
+  }
+  const float t = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = t;
+    if (blockIdx.x == 0) step[0] += 1.0f;
+  }
+}
+
+// Mirrors torch.optim.Adam's default (foreach, non-capturable) update: bias corrections and
+// 1 - beta in double, as the Python scalars are; m.lerp_(g, 1 - b1); v = v·b2 + (1 - b2)·g·g;
+// p += -lr/bc1 · m / (sqrt(v)/sqrt(bc2) + eps).
+__global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, const float* __restrict__ partial,
+                                                                  int nblk, const float* __restrict__ step,
+                                                                  double max_norm, double lr, double beta1,
+                                                                  double beta2, double eps, double wd,
+                                                                  float* __restrict__ norm_out) {
+  __shared__ float coef_sh;
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int i = 0; i < nblk; ++i) tot += partial[i];  // same fixed order in every block
+    const float norm = sqrtf(tot);
+    float coef = 1.0f;
+    if (max_norm > 0.0) coef = fminf((float)max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
+    coef_sh = coef;
+    if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+  }
+  __syncthreads();
+  const float coef = coef_sh;
+  const double t = (double)step[0];
+  const double bc1 = 1.0 - pow(beta1, t), bc2 = 1.0 - pow(beta2, t);
+  const float neg_step = (float)(-lr / bc1), bc2s = (float)sqrt(bc2);
+  const float b2 = (float)beta2, omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
+  const float epsf = (float)eps, wdf = (float)wd;
+  const int64_t total = tb.off[tb.n];
+  const int64_t per = (total + gridDim.x - 1) / gridDim.x;
+  const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(total, e0 + per);
+  int j = 0;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamThreads) {
+    while (e >= tb.off[j + 1]) ++j;
+    const int64_t i = e - tb.off[j];
+    float g = tb.g[j][i] * coef;
+    tb.g[j][i] = g;  // clip_grad_norm_ scales .grad in place
+    const float p = tb.p[j][i];
+    if (wdf != 0.f) g = g + wdf * p;  // Adam (not AdamW) weight decay: grad.add(param, alpha=wd)
+    const float m0 = tb.m[j][i];
+    const float m = fmaf(omb1, g - m0, m0);  // exp_avg.lerp_(grad, 1 - beta1)
+    const float v = tb.v[j][i] * b2 + omb2 * g * g;
+    tb.m[j][i] = m;
+    tb.v[j][i] = v;
+    tb.p[j][i] = p + neg_step * (m / (sqrtf(v) / bc2s + epsf));
+  }
+}
+
+}  // namespace
+}  // namespace gnnmp
+
+using namespace gnnmp;
+
+extern "C" gnn_status gnn_masked_ce_workspace_size(int64_t N, size_t* bytes) {
+  if (!bytes || N < 0) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
+  *bytes = (size_t)std::max<int64_t>(1, ceil_div(N, kCeThreads)) * sizeof(float);
+  return GNN_OK;
+}
+
+extern "C" gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logits, int64_t ldx, const int64_t* y,
+                                        const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
+                                        int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,
+                                        gnn_stream_t stream) {
+  if (N < 0 || C < 1 || C > kMaxClasses || ldx < C || ld_d < C || !loss || (N > 0 && (!logits || !y || !mask ||
+                                                                                        !class_w || !dlogits)))
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad args (1 <= C <= 16)");
+  const int nblk = (int)std::max<int64_t>(1, ceil_div(N, kCeThreads));
+  if (!workspace || workspace_bytes < nblk * sizeof(float)) return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* partial = static_cast<float*>(workspace);
+  if (N == 0) return hip_check(hipMemsetAsync(loss, 0, sizeof(float), st), __func__);
+  if (C == 2)
+    masked_ce_kernel<2><<<nblk, kCeThreads, 0, st>>>(N, C, logits, ldx, y, mask, class_w, inv_denom, dlogits, ld_d,
+                                                     partial);
+  else
+    masked_ce_kernel<0><<<nblk, kCeThreads, 0, st>>>(N, C, logits, ldx, y, mask, class_w, inv_denom, dlogits, ld_d,
+                                                     partial);
+  GNN_LAUNCH_CHECK();
+  sum_partials_kernel<<<1, 256, 0, st>>>(partial, nblk, inv_denom, loss);
+  GNN_LAUNCH_CHECK();
+  return GNN_OK;
+}
+
+extern "C" gnn_status gnn_clip_adam_workspace_size(size_t* bytes) {
+  if (!bytes) return fail(GNN_ERR_INVALID_ARG, __func__, "null");
+  *bytes = kAdamBlocks * sizeof(float);
+  return GNN_OK;
+}
+
+extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, float* norm_out, void* workspace,
+                                        size_t workspace_bytes, gnn_stream_t stream) {
+  if (!grp || !step || grp->num_tensors < 0 || grp->num_tensors > GNN_ADAM_MAX_TENSORS)
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad group");
+  if (!workspace || workspace_bytes < kAdamBlocks * sizeof(float))
+    return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
+  AdamTable tb{};
+  tb.n = grp->num_tensors;
+  tb.off[0] = 0;
+  for (int j = 0; j < tb.n; ++j) {
+    const gnn_adam_tensor& t = grp->tensors[j];
+    if (t.numel < 0 || (t.numel > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq)))
+      return fail(GNN_ERR_INVALID_ARG, __func__, "bad tensor");
+    tb.p[j] = t.param; tb.g[j] = t.grad; tb.m[j] = t.exp_avg; tb.v[j] = t.exp_avg_sq;
+    tb.off[j + 1] = tb.off[j] + t.numel;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  float* partial = static_cast<float*>(workspace);
+  grad_sq_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, step);
+  GNN_LAUNCH_CHECK();
+  clip_adam_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, kAdamBlocks, step, grp->max_norm, grp->lr,
+                                                         grp->beta1, grp->beta2, grp->eps, grp->weight_decay, norm_out);
+  GNN_LAUNCH_CHECK();
+  return GNN_OK;
+}

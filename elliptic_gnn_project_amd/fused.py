@@ -20,6 +20,7 @@ kept values by 1/(1-p).
 """
 from __future__ import annotations
 
+import functools
 import os
 from typing import List
 
@@ -48,6 +49,24 @@ def _ld(t: torch.Tensor) -> int:
     return max(int(t.stride(0)), int(t.size(1)), 1)
 
 
+@functools.lru_cache(maxsize=256)
+def _nt_ws_bytes(n, k1, k2) -> int:
+    nb = _lib.c_size(0)
+    _lib.call("gnn_gemm_nt_workspace_size", n, k1, k2, nb)
+    return int(nb.value)
+
+
+@functools.lru_cache(maxsize=256)
+def _tn_ws_bytes(M, nr, kc, nproj) -> int:
+    nb = _lib.c_size(0)
+    _lib.call("gnn_gemm_tn_workspace_size", M, nr, kc, nproj, nb)
+    return int(nb.value)
+
+
+def _nt_workspace(device, n, k1, k2):
+    return torch.empty(max(_nt_ws_bytes(n, k1, k2) // 4, 1), dtype=torch.float32, device=device)
+
+
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
             out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None):
     """C = epilogue([a1 | a2] · B) on the MFMA NT kernel; B = bt ([K, n] row-major) or, with bt None,
@@ -55,6 +74,10 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
     M = a1.size(0)
     if out is None and want_c:
         out = torch.empty((M, n), dtype=torch.float32, device=a1.device)
+    ws = None
+    if w1 is not None:  # B pre-split image for the streaming split-bf16 kernel (≈24 KB per 32 of K)
+        k2_ = a2.size(1) if a2 is not None else 0
+        ws = _nt_workspace(a1.device, n, a1.size(1), k2_)
     p = _lib.GnnGemmNTParams(
         M, n,
         a1.data_ptr(), _ld(a1), a1.size(1),
@@ -65,6 +88,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.ptr(bias), int(relu), float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ptr),
         _lib.ptr(proj), proj.size(0) if proj is not None else 0, _lib.ptr(z), _ld(z) if z is not None else 0,
         _math(math),
+        _lib.ptr(ws), ws.numel() * 4 if ws is not None else 0,
     )
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
@@ -86,9 +110,7 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     nproj = proj.size(0) if dz is not None else 0
     n_out = nr * (k1 + k2) + nr + nproj * nr + nproj
     out = torch.empty(n_out, dtype=torch.float32, device=a1.device)
-    nb = _lib.c_size(0)
-    _lib.call("gnn_gemm_tn_workspace_size", M, nr, k1 + k2, nproj, nb)
-    ws = torch.empty(max(int(nb.value) // 4, 1), dtype=torch.float32, device=a1.device)
+    ws = torch.empty(max(_tn_ws_bytes(M, nr, k1 + k2, nproj) // 4, 1), dtype=torch.float32, device=a1.device)
     p = _lib.GnnGemmTNParams(
         M, nr,
         _lib.ptr(g), _ld(g) if g is not None else 0,

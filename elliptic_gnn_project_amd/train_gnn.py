@@ -123,6 +123,21 @@ def _make_loss_fn(cfg: Dict, cw: torch.Tensor, model, t_min: int, t_max: int):
             loss = loss + embed_l2 * model.time_emb.weight.pow(2).mean()
         return loss
 
+    def full(logits, y_all, mask, denom=None, t_idx_all=None):
+        """The same loss from the full logits and the row mask: on the GPU in the default
+        configuration one fused kernel (train_ops.masked_cross_entropy); else loss_fn on the rows."""
+        if loss_fn.plain and logits.is_cuda and logits.dtype == torch.float32:
+            from .train_ops import masked_cross_entropy
+            w = cw_dev.get(logits.device)
+            if w is None:
+                w = cw_dev[logits.device] = cw.to(logits.device)
+            return masked_cross_entropy(logits, y_all, mask, w, denom=denom)
+        idx = mask.nonzero().squeeze(1)
+        t_sel = t_idx_all.index_select(0, idx) if t_idx_all is not None else None
+        return loss_fn(logits.index_select(0, idx), y_all.index_select(0, idx), t_sel, denom=denom)
+
+    loss_fn.plain = not focal and scheme == "none" and embed_l2 == 0.0
+    loss_fn.full = full
     return loss_fn
 
 
@@ -137,6 +152,22 @@ def _rows(t: torch.Tensor, data, split: str) -> torch.Tensor:
     return t.index_select(0, idx) if idx is not None else t[getattr(data, f"{split}_mask")]
 
 
+def _clips_itself(optimizer) -> bool:
+    from .train_ops import ClipAdam
+    return isinstance(optimizer, ClipAdam) and bool(optimizer.max_norm)
+
+
+def make_optimizer(model, cfg: Dict, device, use_amp: bool):
+    """Adam(lr, weight_decay) (src/train_gnn.py:357).  On the GPU without AMP: ClipAdam, the
+    fused clip_grad_norm_(grad_clip) + Adam step (train_ops.py); otherwise torch.optim.Adam."""
+    if device.type == "cuda" and not use_amp:
+        from .train_ops import ClipAdam
+        clip = cfg.get("grad_clip", 0)
+        return ClipAdam(model.parameters(), lr=cfg["lr"], weight_decay=cfg["weight_decay"],
+                        max_norm=float(clip) if clip and clip > 0 else None)
+    return torch.optim.Adam(model.parameters(), lr=cfg["lr"], weight_decay=cfg["weight_decay"])
+
+
 def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cfg, device, sync=True):
     """One full-batch step (src/train_gnn.py:187-209).  ``sync=False`` keeps the loss on device."""
     model.train()
@@ -144,9 +175,12 @@ def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cf
     with _autocast(device, use_amp):
         logits = model(data.x, edge_index, data.timestep if _model_uses_time_embed(model) else None)
         t_idx = _rows(data.timestep, data, "train") if cfg.get("time_loss_weighting", "none") != "none" else None
-        loss = loss_fn(_rows(logits, data, "train"), _rows(data.y, data, "train"), t_idx)
+        if getattr(loss_fn, "plain", False) and logits.is_cuda and not use_amp:
+            loss = loss_fn.full(logits, data.y, data.train_mask, denom=getattr(data, "n_train", None))
+        else:
+            loss = loss_fn(_rows(logits, data, "train"), _rows(data.y, data, "train"), t_idx)
     scaler.scale(loss).backward()
-    if cfg.get("grad_clip", 0) and cfg["grad_clip"] > 0:
+    if cfg.get("grad_clip", 0) and cfg["grad_clip"] > 0 and not _clips_itself(optimizer):
         scaler.unscale_(optimizer)
         torch.nn.utils.clip_grad_norm_(model.parameters(), cfg["grad_clip"])
     scaler.step(optimizer)
@@ -253,7 +287,7 @@ def main(cfg: Dict) -> Dict:
     data = data.to(device)
     ei = data.edge_index
     model = build_model(cfg["arch"], data.x.size(1), cfg).to(device)
-    opt = torch.optim.Adam(model.parameters(), lr=cfg["lr"], weight_decay=cfg["weight_decay"])
+    opt = make_optimizer(model, cfg, device, use_amp)
     cw = class_weight(data.y[data.train_mask].cpu()) if cfg.get("class_weight_pos", "auto") == "auto" \
         else torch.tensor([1.0, float(cfg["class_weight_pos"])], dtype=torch.float32)
     t_train = data.timestep[data.train_mask]

@@ -1,0 +1,137 @@
+"""Fused step ops around the hot path: masked weighted cross entropy and clip + Adam.
+
+``masked_cross_entropy`` is the loss of ``_make_loss_fn`` (src/train_gnn.py:136-183) in its
+default configuration — ``F.cross_entropy(logits[train_mask], y[train_mask], weight=cw,
+reduction='none').mean()`` (:159-175) — computed over the full logits with the row mask applied
+inside one kernel that also writes d(loss)/d(logits) (gnn_masked_ce_f32).  ``ClipAdam`` is
+``clip_grad_norm_(params, max_norm)`` (:203-205) followed by ``torch.optim.Adam.step()`` (:206)
+in two launches over every parameter (gnn_clip_adam_f32), graph-replay safe (device step count).
+Both run on the GPU only; the CPU path keeps the ATen ops.
+"""
+from __future__ import annotations
+
+import functools
+from typing import Iterable
+
+import torch
+
+from . import _lib
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=device)
+
+
+@functools.lru_cache(maxsize=64)
+def _ce_ws_bytes(N: int) -> int:
+    nb = _lib.c_size(0)
+    _lib.call("gnn_masked_ce_workspace_size", N, nb)
+    return int(nb.value)
+
+
+class _MaskedCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, y, mask_u8, class_w, inv_denom: float):
+        logits = logits.contiguous()
+        N, C = logits.shape
+        dl = torch.empty_like(logits)
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        ws = _ws(_ce_ws_bytes(N), logits.device)
+        _lib.call("gnn_masked_ce_f32", N, C, logits.data_ptr(), C, y.data_ptr(), mask_u8.data_ptr(),
+                  class_w.data_ptr(), float(inv_denom), dl.data_ptr(), C, loss.data_ptr(), ws.data_ptr(),
+                  ws.numel() * 4, _lib.stream_handle(logits.device))
+        ctx.save_for_backward(dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return dl * g, None, None, None, None
+
+
+def masked_cross_entropy(logits: torch.Tensor, y: torch.Tensor, mask: torch.Tensor, class_w: torch.Tensor,
+                         denom: float | None = None) -> torch.Tensor:
+    """Σ_{i: mask_i} CE_w(logits_i, y_i) / denom (denom defaults to mask.sum(): the reference's .mean()).
+
+    ``mask`` is a bool/uint8 [N] tensor, ``y`` int64 [N] (labels of unmasked rows are ignored).
+    """
+    if not logits.is_cuda:
+        raise RuntimeError("masked_cross_entropy runs on the GPU (libgnnmp); use the ATen loss on CPU")
+    if logits.dtype != torch.float32:
+        logits = logits.float()
+    if denom is None:
+        denom = float(mask.sum())  # host sync; pass denom to avoid it
+    m8 = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)  # bool: no copy
+    w = class_w.to(device=logits.device, dtype=torch.float32).contiguous()
+    return _MaskedCE.apply(logits, y.contiguous(), m8.contiguous(), w, 1.0 / float(denom))
+
+
+class ClipAdam(torch.optim.Optimizer):
+    """``clip_grad_norm_(max_norm)`` + ``Adam`` (L2 weight decay, amsgrad off) in two kernels.
+
+    Same update as ``torch.optim.Adam(lr, betas, eps, weight_decay)`` preceded by
+    ``torch.nn.utils.clip_grad_norm_(params, max_norm)`` (grads scaled in place by
+    min(1, max_norm / (‖g‖ + 1e-6))); ``max_norm=None`` skips clipping.  The step counter lives on
+    the device, so a captured HIP graph replays it.  ``last_norm`` holds the pre-clip total norm.
+    """
+
+    def __init__(self, params: Iterable, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 max_norm: float | None = 1.0):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        if max_norm and len(self.param_groups) > 1:
+            raise ValueError("ClipAdam clips over one parameter group (as clip_grad_norm_ over model.parameters())")
+        self.max_norm = max_norm
+        self._ws = None
+        self._groups = {}
+        self.last_norm = None
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        for gi, group in enumerate(self.param_groups):
+            ps = [p for p in group["params"] if p.grad is not None]
+            if not ps:
+                continue
+            dev = ps[0].device
+            if self._ws is None:
+                if not ps[0].is_cuda:
+                    raise RuntimeError("ClipAdam runs on the GPU (libgnnmp)")
+                nb = _lib.c_size(0)
+                _lib.call("gnn_clip_adam_workspace_size", nb)
+                self._ws = _ws(int(nb.value), dev)
+                self.last_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+            if "step_t" not in group:  # device step counter of this group (advanced by the kernel)
+                group["step_t"] = torch.zeros(1, dtype=torch.float32, device=dev)
+            # the ctypes argument block is rebuilt only when a pointer or a hyper-parameter changed
+            # (the caching allocator usually hands every step's grads the same addresses)
+            key = (tuple(p.grad.data_ptr() for p in ps), tuple(p.data_ptr() for p in ps), group["lr"],
+                   group["betas"], group["eps"], group["weight_decay"], self.max_norm)
+            cached = self._groups.get(gi)
+            if cached is None or cached[0] != key:
+                cached = (key, self._build(group, ps))
+                self._groups[gi] = cached
+            _lib.call("gnn_clip_adam_f32", cached[1], group["step_t"].data_ptr(), self.last_norm.data_ptr(),
+                      self._ws.data_ptr(), self._ws.numel() * 4, _lib.stream_handle(dev))
+        return loss
+
+    def _build(self, group, ps):
+        if len(ps) > _lib.ADAM_MAX_TENSORS:
+            raise ValueError(f"ClipAdam: at most {_lib.ADAM_MAX_TENSORS} tensors per group")
+        grp = _lib.GnnAdamGroup()
+        grp.num_tensors = len(ps)
+        grp.lr, (grp.beta1, grp.beta2) = group["lr"], group["betas"]
+        grp.eps, grp.weight_decay = group["eps"], group["weight_decay"]
+        grp.max_norm = float(self.max_norm) if self.max_norm else 0.0
+        for j, p in enumerate(ps):
+            st = self.state[p]
+            if not st:
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                st["step"] = group["step_t"]
+            if not (p.is_contiguous() and p.grad.is_contiguous() and p.dtype == torch.float32):
+                raise ValueError("ClipAdam needs contiguous fp32 params and grads")
+            t = grp.tensors[j]
+            t.param, t.grad = p.data_ptr(), p.grad.data_ptr()
+            t.exp_avg, t.exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+            t.numel = p.numel()
+        return grp

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 5
+#define GNNMP_ABI_VERSION 6
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -223,9 +223,12 @@ typedef struct {
   const float* proj; int32_t nproj;      /* optional Z = C · projᵀ, proj [nproj, N], nproj <= 4, N <= 128 */
   float* z; int64_t ldz;
   int32_t math;                          /* gnn_gemm_math */
+  void* workspace; size_t workspace_bytes; /* optional: the split-bf16 w1/w2 form pre-splits B here
+                                            (gnn_gemm_nt_workspace_size) and streams A without LDS */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
+gnn_status gnn_gemm_nt_workspace_size(int64_t N, int64_t k1, int64_t k2, size_t* bytes);
 gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream);
 
 typedef struct {
@@ -254,6 +257,37 @@ gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* worksp
 gnn_status gnn_colsum_workspace_size(int64_t rows, int64_t F, size_t* bytes);
 gnn_status gnn_colsum_f32(int64_t rows, int64_t F, const float* x, int64_t ldx, float* out,
                           void* workspace, size_t workspace_bytes, gnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Step ops around the hot path (src/train_gnn.py:136-183, 201-206)          */
+/* ------------------------------------------------------------------------ */
+/* Masked class-weighted cross entropy over all N rows, forward and backward in one pass:
+ * rows with mask[i] != 0 and 0 <= y[i] < C contribute loss_i = -w[y_i]·log_softmax(x_i)[y_i]
+ * (F.cross_entropy(weight=w, reduction='none')); *loss = Σ loss_i · inv_denom (the reference's
+ * loss_vec.mean() with inv_denom = 1 / n_train, src/train_gnn.py:175); dlogits = d(*loss)/dx
+ * (zero on every other row).  C <= 16.  Deterministic fixed-order reduction. */
+gnn_status gnn_masked_ce_workspace_size(int64_t N, size_t* bytes);
+gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logits, int64_t ldx, const int64_t* y,
+                             const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
+                             int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,
+                             gnn_stream_t stream);
+
+/* clip_grad_norm_(max_norm) + torch.optim.Adam.step() (weight_decay as L2 on the gradient) over
+ * up to GNN_ADAM_MAX_TENSORS parameters (src/train_gnn.py:203-206).  `step` is a device float
+ * incremented by the call (graph-replay safe); norm_out (optional, device) gets the pre-clip
+ * total norm.  max_norm <= 0 disables clipping.  Grads are scaled in place, as torch does. */
+#define GNN_ADAM_MAX_TENSORS 24
+typedef struct {
+  float* param; float* grad; float* exp_avg; float* exp_avg_sq; int64_t numel;
+} gnn_adam_tensor;
+typedef struct {
+  int32_t num_tensors;
+  double lr, beta1, beta2, eps, weight_decay, max_norm;  /* double, as torch's Python scalars */
+  gnn_adam_tensor tensors[GNN_ADAM_MAX_TENSORS];
+} gnn_adam_group;
+gnn_status gnn_clip_adam_workspace_size(size_t* bytes);
+gnn_status gnn_clip_adam_f32(const gnn_adam_group* group, float* step, float* norm_out, void* workspace,
+                             size_t workspace_bytes, gnn_stream_t stream);
 
 #ifdef __cplusplus
 }
