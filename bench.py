@@ -45,6 +45,12 @@ PRESETS = {
     "gat": dict(cfg=dict(arch="gat", hidden_dim=64, layers=2, heads=4, dropout=0.5, symmetrize_edges=False,
                          use_time_scalar=True, train_window_k=10),
                 workload="BASELINE configs[2] preset: GAT 2L 4 heads 166->4x16->2, dropout 0.5, self loops"),
+    "sage_scaled": dict(cfg=dict(arch="sage", hidden_dim=128, layers=3, dropout=0.5, symmetrize_edges=True,
+                                 use_time_scalar=True, train_window_k=10),
+                        gen=dict(num_nodes=2_000_000, num_edges=4_000_000), dtype="bf16",
+                        metric="edges/s full-batch SAGE fwd+bwd, scaled Elliptic 2M/4M/166-feat bf16, 1→8 MI355X",
+                        workload="BASELINE configs[4]: synthetic scaled Elliptic 2M nodes / 4M edges (8M "
+                                 "symmetrized) / 166 feats, SAGE 3L 166->128->128->2, bf16 storage, f32 accumulate"),
     "sage_resbn": dict(cfg=dict(arch="sage_resbn", hidden_dim=64, layers=3, dropout=0.2, symmetrize_edges=True,
                                 use_time_scalar=False, time_embed_dim=2, time_embed_type="sin",
                                 train_window_k=8, use_bn=True, residual=True),
@@ -69,10 +75,10 @@ def parse():
     return ap.parse_args()
 
 
-def make_inputs(rank: int, degree: str, cfg):
+def make_inputs(rank: int, degree: str, cfg, gen=None):
     from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
 
-    data = synthetic_elliptic(degree=degree, seed=42 + rank)
+    data = synthetic_elliptic(degree=degree, seed=42 + rank, **(gen or {}))
     return prepare_inputs(data, cfg)
 
 
@@ -144,9 +150,9 @@ def measured_traffic(tag):
     if tag[0] == "gemm_nt":
         M, N = tag[1], tag[3]
         grid = -(-M // 128) * 256 * -(-N // 128)
-        cand = [r for r in rows if "gemm_nt_kernel" in r["kernel"] and r["grid_threads"] == grid]
+        cand = [r for r in rows if "gemm_nt" in r["kernel"] and r["grid_threads"] == grid]
     elif tag[0] == "gemm_tn":
-        cand = [r for r in rows if "gemm_tn_kernel" in r["kernel"]]
+        cand = [r for r in rows if "gemm_tn" in r["kernel"]]
     else:
         return None
     if len(cand) != 1 or cand[0]["traffic_bytes"] is None:
@@ -154,25 +160,43 @@ def measured_traffic(tag):
     return int(cand[0]["traffic_bytes"])
 
 
+BF16_MFMA_PEAK_TFS = 2500.0  # gfx950 dense bf16 MFMA peak (MI355X_MICROARCH.md)
+
+
+def gemm_floor(tag):
+    """(bytes, time at the HBM roofline, time at the MFMA roofline, MFMA peak) of one GEMM launch.
+
+    Algorithmic bytes: NT reads A [M, K] and writes C [M, N]; TN reads A [M, K] and h [M, N]
+    (weights, slabs and the 4-wide dz are < 1 %).  MFMA time: 2·M·K·N FLOPs at the peak of the
+    arithmetic used — split-bf16 (6 bf16 products per f32 product: 2.5 PF / 6), bf16 storage
+    (one product: 2.5 PF) or exact f32 (157.3 TF)."""
+    kind, M, K, N, ea, ec, prod = tag
+    byts = M * K * ea + M * N * ec
+    peak = MFMA_F32_PEAK_TFS if prod == 0 else BF16_MFMA_PEAK_TFS / prod
+    return byts, byts / (HBM_PEAK_GBS * 1e9), 2.0 * M * K * N / (peak * 1e12), peak
+
+
 def roofline(recs):
     """Dominant libgnnmp kernel (by total HIP-event time) against its roofline.
 
     Aggregations are HBM-bound: achieved = algorithmic bytes per launch / average duration.
-    MFMA GEMMs are priced in FLOPs against the fp32 MFMA peak.  Also reports every timed
-    kernel's share for the DESIGN.md breakdown.
+    GEMMs are priced against whichever roofline bounds them (the larger of the HBM time of their
+    algorithmic bytes and the MFMA time of their FLOPs at the peak of the arithmetic they use).
+    Also reports every timed kernel's share and rooflines for the DESIGN.md breakdown.
     """
     names = {0: "sum", 1: "mean_fwd", 2: "mean_bwd", 3: "gcn", 4: "edge_w"}
 
     def label(tag):
-        if tag[0] == "agg":
-            return f"agg[{names[tag[1]]},{'csc' if tag[2] else 'csr'},F={tag[3]}]"
+        if tag[0].startswith("agg"):
+            return f"{tag[0]}[{names[tag[1]]},{'csc' if tag[2] else 'csr'},F={tag[3]}]"
         if tag[0].startswith("gat"):
             return f"{tag[0]}[H={tag[1]},C={tag[2]},out={tag[3]}]"
-        return f"{tag[0]}[M={tag[1]},K={tag[2]},N={tag[3]}]"
+        math = {0: "f32", 1: "bf16", 6: "split-bf16"}[tag[6]]
+        return f"{tag[0]}[M={tag[1]},K={tag[2]},N={tag[3]},{math}]"
 
     if not recs:
         return None
-    hbm = lambda t: t[0] == "agg" or t[0].startswith("gat")  # noqa: E731
+    hbm = lambda t: t[0].startswith("agg") or t[0].startswith("gat")  # noqa: E731
 
     tot = sum(r["ms"] for r in recs.values())
     tag, r = max(recs.items(), key=lambda kv: kv[1]["ms"])
@@ -183,9 +207,15 @@ def roofline(recs):
         out = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None}
     else:
-        ach = per / (avg_ms * 1e-3) / 1e12
-        out = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-               "frac": round(ach / MFMA_F32_PEAK_TFS, 4), "traffic": None}
+        byts, t_hbm, t_mfma, peak = gemm_floor(tag)
+        if t_hbm >= t_mfma:
+            ach = byts / (avg_ms * 1e-3) / 1e9
+            out = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "algorithmic_bytes": int(byts)}
+        else:
+            ach = per / (avg_ms * 1e-3) / 1e12
+            out = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                   "frac": round(ach / peak, 4), "traffic": None}
     out["traffic"] = measured_traffic(tag)
     if out["traffic"] is not None:
         out["traffic_source"] = os.path.relpath(TRAFFIC_FILE, ROOT)
@@ -196,6 +226,10 @@ def roofline(recs):
         if hbm(t):  # HBM-bound: algorithmic bytes per launch / duration
             gbs = v["amount"] / v["launches"] / (us * 1e-6) / 1e9
             e.update({"hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)})
+        else:
+            byts, t_hbm, t_mfma, peak = gemm_floor(t)
+            e.update({"hbm_frac": round(t_hbm / (us * 1e-6), 4), "mfma_frac": round(t_mfma / (us * 1e-6), 4),
+                      "floor_us": round(max(t_hbm, t_mfma) * 1e6, 1)})
         timed[label(t)] = e
     out.update({"kernel": label(tag), "avg_us": round(avg_ms * 1e3, 2), "per_launch": int(per),
                 "timed_kernels": timed})
@@ -223,8 +257,11 @@ def main():
 
     preset = PRESETS[args.arch]
     cfg = preset["cfg"]
-    data_cpu = make_inputs(rank, args.degree, cfg)
+    data_cpu = make_inputs(rank, args.degree, cfg, preset.get("gen"))
     data = data_cpu.to(dev)
+    bf16 = preset.get("dtype") == "bf16"
+    if bf16:  # bf16 storage of the node features (and, through the fused path, every activation)
+        data.x = data.x.to(torch.bfloat16)
     torch.manual_seed(42)  # identical initial weights on every rank
     model = build_model(cfg["arch"], data.x.size(1), cfg).to(dev)
     if dist is not None:
@@ -299,7 +336,7 @@ def main():
 
     if rank == 0:
         print(json.dumps({
-            "metric": METRIC if args.arch == "sage" else METRIC.replace("SAGE", args.arch.upper()),
+            "metric": preset.get("metric") or (METRIC if args.arch == "sage" else METRIC.replace("SAGE", args.arch.upper())),
             "value": value,
             "unit": "edges/s",
             "n_gpus": world,
@@ -309,7 +346,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "bf16" if bf16 else "f32",
             "data": f"synthetic Elliptic-shape ({args.degree} in-degree, seed 42+rank)",
             "config": {
                 "workload": preset["workload"] + ", full-batch train step (fwd+masked CE+bwd+clip+Adam)",

@@ -15,7 +15,11 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 6
+ABI_VERSION = 7
+
+# gnn_dtype
+DTYPE_F32 = 0
+DTYPE_BF16 = 1
 
 # gnn_gemm_math
 MATH_SPLIT_BF16 = 0
@@ -108,6 +112,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("proj", c_ptr), ("nproj", c_i32), ("z", c_ptr), ("ldz", c_i64),
         ("math", c_i32),
         ("workspace", c_ptr), ("workspace_bytes", c_size),
+        ("a_dtype", c_i32), ("c_dtype", c_i32),
     ]
 
 
@@ -122,6 +127,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("a1", c_ptr), ("lda1", c_i64), ("k1", c_i64),
         ("a2", c_ptr), ("lda2", c_i64), ("k2", c_i64),
         ("math", c_i32),
+        ("a_dtype", c_i32), ("h_dtype", c_i32),
     ]
 
 
@@ -161,6 +167,10 @@ SIGNATURES = {
     "gnn_in_degree_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), c_ptr, c_ptr]),
     "gnn_gcn_norm_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), c_ptr, c_ptr]),
     "gnn_aggregate_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), ctypes.POINTER(GnnAggParams), c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_aggregate_bf16": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), ctypes.POINTER(GnnAggParams), c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
     ),

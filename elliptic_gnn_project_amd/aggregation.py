@@ -88,7 +88,9 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
               nodew: torch.Tensor | None = None, ew: torch.Tensor | None = None, heads: int = 1,
               addend: torch.Tensor | None = None, bias: torch.Tensor | None = None,
               relu: bool = False, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Raw call of gnn_aggregate_f32 (no autograd)."""
+    """Raw call of gnn_aggregate_f32 (no autograd); bf16 rows go to gnn_aggregate_bf16 (bf16 out)."""
+    if x.dtype == torch.bfloat16:
+        return _aggregate_bf16(plan, x, mode, transpose, nodew, addend, bias, relu, out)
     x = _as_f32_rows(x)
     N, F = plan.num_nodes, x.size(1)
     if x.size(0) != N:
@@ -118,7 +120,37 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
     return out
 
 
-def agg_bytes(plan: GraphPlan, F: int, mode: int, transpose: bool, has_addend: bool) -> int:
+def _aggregate_bf16(plan, x, mode, transpose, nodew, addend, bias, relu, out):
+    if x.dim() != 2 or x.stride(1) != 1:
+        x = x.contiguous()
+    N, F = plan.num_nodes, x.size(1)
+    if x.size(0) != N:
+        raise ValueError(f"feature rows {x.size(0)} != plan nodes {N}")
+    if out is None:
+        out = torch.empty((N, F), dtype=torch.bfloat16, device=x.device)
+    if out.dtype != torch.bfloat16:
+        raise TypeError("bf16 aggregation writes bf16")
+    if addend is not None:
+        addend = _as_f32_rows(addend)
+    p = _lib.GnnAggParams(
+        mode, int(transpose), _lib.ptr(nodew), None, 1,
+        _lib.ptr(addend), _ld(addend) if addend is not None else 0,
+        _lib.ptr(bias), int(relu), None, 0,
+    )
+    if KernelTimer.active:
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+    _lib.call("gnn_aggregate_bf16", plan.c_graph, p, x.data_ptr(), _ld(x), F, out.data_ptr(), _ld(out),
+              _lib.stream_handle(x.device))
+    if KernelTimer.active:
+        b.record()
+        KernelTimer.records.append((("agg_bf16", int(mode), bool(transpose), int(F)), a, b,
+                                    agg_bytes(plan, F, mode, transpose, addend is not None, elem=2)))
+    return out
+
+
+def agg_bytes(plan: GraphPlan, F: int, mode: int, transpose: bool, has_addend: bool, elem: int = 4) -> int:
     """Algorithmic HBM bytes of one aggregation launch (fp32, int32 plan).
 
     rowptr/colptr 4(N+1) + neighbour ids 4S + one F-row gather per slot 4·S·F + output
@@ -126,7 +158,7 @@ def agg_bytes(plan: GraphPlan, F: int, mode: int, transpose: bool, has_addend: b
     root addend 4·N·F when present.  (SURVEY §8d per-edge model.)
     """
     N, S = plan.num_nodes, plan.num_slots
-    b = 4 * (N + 1) + 4 * S + 4 * S * F + 4 * N * F
+    b = 4 * (N + 1) + 4 * S + elem * S * F + elem * N * F
     if mode in (_lib.AGG_MEAN,):
         b += 4 * N
     elif mode in (_lib.AGG_MEAN_BWD, _lib.AGG_GCN):

@@ -51,6 +51,35 @@ __device__ __forceinline__ void vstore(float* p, const float (&v)[VEC]) {
   }
 }
 
+// bf16 rows (bf16-storage path): VEC bf16 per lane-chunk widened to f32 / rounded back (RNE).
+template <int VEC>
+__device__ __forceinline__ void vload_bf(const uint16_t* p, float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    const uint2 t = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+    v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+  } else if constexpr (VEC == 2) {
+    const uint32_t t = *reinterpret_cast<const uint32_t*>(p);
+    v[0] = __uint_as_float(t << 16); v[1] = __uint_as_float(t & 0xffff0000u);
+  } else {
+    v[0] = __uint_as_float((uint32_t)p[0] << 16);
+  }
+}
+
+__device__ __forceinline__ uint16_t to_bf16(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+template <int VEC>
+__device__ __forceinline__ void vstore_bf(uint16_t* p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)to_bf16(v[0]) | ((uint32_t)to_bf16(v[1]) << 16),
+                                              (uint32_t)to_bf16(v[2]) | ((uint32_t)to_bf16(v[3]) << 16));
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<uint32_t*>(p) = (uint32_t)to_bf16(v[0]) | ((uint32_t)to_bf16(v[1]) << 16);
+  } else {
+    p[0] = to_bf16(v[0]);
+  }
+}
+
 struct AggArgs {
   const int32_t* ptr;    // segment pointer (rowptr or colptr)
   const int32_t* nbr;    // neighbour per slot (col or row)
@@ -225,7 +254,7 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 // Wave-wide groups (LPS = 64, F/VEC > 32 chunks, e.g. the 166-wide layer-1 features):
 // every row boundary and neighbour id is wave-uniform, so they live in SGPRs (scalar loads,
 // v_readlane) and the next U neighbour ids are prefetched while the current U rows load.
-template <int MODE, int VEC, int NCH>
+template <int MODE, int VEC, int NCH, bool BF = false>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   constexpr int U = 8;
   const int lane = threadIdx.x & 63;
@@ -258,7 +287,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + 64 * i;
-      if (c < nchunk && p0 >= 0) {  // long row: raw partial of piece 0
+      if (!BF && c < nchunk && p0 >= 0) {  // long row: raw partial of piece 0
         vstore<VEC>(a.part + (int64_t)p0 * a.F + c * VEC, acc[i]);
       } else if (c < nchunk) {
         const int f0 = c * VEC;
@@ -279,7 +308,8 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
           for (int q = 0; q < VEC; ++q) t[q] = fmaxf(t[q], 0.0f);
         }
-        vstore<VEC>(a.y + r * a.ldy + f0, t);
+        if constexpr (BF) vstore_bf<VEC>(reinterpret_cast<uint16_t*>(a.y) + r * a.ldy + f0, t);
+        else vstore<VEC>(a.y + r * a.ldy + f0, t);
       }
 #pragma unroll
       for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
@@ -298,7 +328,10 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) vload<VEC>(a.x + (int64_t)n[u] * a.ldx + coff[i], v[u][i]);
+      for (int i = 0; i < NCH; ++i) {
+        if constexpr (BF) vload_bf<VEC>(reinterpret_cast<const uint16_t*>(a.x) + (int64_t)n[u] * a.ldx + coff[i], v[u][i]);
+        else vload<VEC>(a.x + (int64_t)n[u] * a.ldx + coff[i], v[u][i]);
+      }
     int32_t nn[U];  // prefetch the next U neighbour ids behind this iteration's row loads
 #pragma unroll
     for (int u = 0; u < U; ++u) nn[u] = __builtin_amdgcn_readfirstlane(a.nbr[min(s + U + u, send - 1)]);
@@ -790,6 +823,70 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
     case GNN_AGG_EDGE_W: return launch_mode<GNN_AGG_EDGE_W>(a, vec, st, nullptr);
   }
   return fail(GNN_ERR_INVALID_ARG, __func__, "unknown mode");
+}
+
+// bf16-storage aggregation: x and y bf16 ([rows, F], ld in elements), f32 accumulation in plan
+// order, y rounded once (RNE).  Modes SUM / MEAN / MEAN_BWD / GCN; addend (f32), bias, ReLU as
+// in gnn_aggregate_f32; no long-segment split.  F <= 512.
+namespace gnnmp {
+namespace {
+template <int MODE>
+gnn_status launch_bf16(const AggArgs& a, int vec, hipStream_t st) {
+  if (a.nrows == 0 || a.F == 0) return GNN_OK;
+  const int rpw = 16;
+  const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
+  const int nchunk = a.F / vec;
+  if (nchunk <= 64) {
+    if (vec == 4) agg_wave_kernel<MODE, 4, 1, true><<<wblocks, 256, 0, st>>>(a, rpw);
+    else if (vec == 2) agg_wave_kernel<MODE, 2, 1, true><<<wblocks, 256, 0, st>>>(a, rpw);
+    else agg_wave_kernel<MODE, 1, 1, true><<<wblocks, 256, 0, st>>>(a, rpw);
+  } else {
+    if (vec == 4) agg_wave_kernel<MODE, 4, 2, true><<<wblocks, 256, 0, st>>>(a, rpw);
+    else if (vec == 2) agg_wave_kernel<MODE, 2, 2, true><<<wblocks, 256, 0, st>>>(a, rpw);
+    else agg_wave_kernel<MODE, 1, 2, true><<<wblocks, 256, 0, st>>>(a, rpw);
+  }
+  return hip_check(hipGetLastError(), "gnn_aggregate_bf16");
+}
+
+}  // namespace
+}  // namespace gnnmp
+
+extern "C" gnn_status gnn_aggregate_bf16(const gnn_graph* g, const gnn_agg_params* p, const void* x, int64_t ldx,
+                                         int64_t F, void* y, int64_t ldy, gnn_stream_t stream) {
+  if (!g || !p) return fail(GNN_ERR_INVALID_ARG, __func__, "null graph or params");
+  if (F < 0 || ldx < F || ldy < F) return fail(GNN_ERR_INVALID_ARG, __func__, "bad F / leading dimensions");
+  if (p->mode == GNN_AGG_EDGE_W) return fail(GNN_ERR_UNSUPPORTED, __func__, "EDGE_W has no bf16 form");
+  if ((p->mode == GNN_AGG_MEAN || p->mode == GNN_AGG_MEAN_BWD || p->mode == GNN_AGG_GCN) && !p->nodew)
+    return fail(GNN_ERR_INVALID_ARG, __func__, "mode needs nodew");
+  if (g->num_nodes > 0 && F > 0 && (!x || !y)) return fail(GNN_ERR_INVALID_ARG, __func__, "null x/y");
+  if (p->addend && p->ld_add < F) return fail(GNN_ERR_INVALID_ARG, __func__, "bad ld_add");
+  AggArgs a{};
+  a.ptr = p->transpose ? g->colptr : g->rowptr;
+  a.nbr = p->transpose ? g->row : g->col;
+  if (!a.ptr || (g->num_slots > 0 && !a.nbr)) return fail(GNN_ERR_INVALID_ARG, __func__, "plan arrays null");
+  a.nodew = p->nodew;
+  a.heads = 1;
+  a.chan = (int32_t)(F > 0 ? F : 1);
+  a.x = static_cast<const float*>(x); a.ldx = ldx;
+  a.y = static_cast<float*>(y); a.ldy = ldy;
+  a.add = p->addend; a.ld_add = p->ld_add;
+  a.bias = p->bias; a.relu = p->relu;
+  a.nrows = g->num_nodes;
+  a.F = (int32_t)F;
+  auto ok_vec = [&](int v) {
+    if (F % v || ldx % v || ldy % v || (p->addend && p->ld_add % v)) return false;
+    return aligned(x, 2 * v) && aligned(y, 2 * v) && aligned(p->addend, 4 * v);
+  };
+  const int vec = ok_vec(4) ? 4 : (ok_vec(2) ? 2 : 1);
+  if (F / vec > 128) return fail(GNN_ERR_UNSUPPORTED, __func__, "F too wide for the bf16 gather");
+  hipStream_t st = (hipStream_t)stream;
+  switch (p->mode) {
+    case GNN_AGG_SUM: return launch_bf16<GNN_AGG_SUM>(a, vec, st);
+    case GNN_AGG_MEAN: return launch_bf16<GNN_AGG_MEAN>(a, vec, st);
+    case GNN_AGG_MEAN_BWD: return launch_bf16<GNN_AGG_MEAN_BWD>(a, vec, st);
+    case GNN_AGG_GCN: return launch_bf16<GNN_AGG_GCN>(a, vec, st);
+    default: return fail(GNN_ERR_INVALID_ARG, __func__, "unknown mode");
+  }
 }
 
 extern "C" gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg, const float* x,

@@ -38,11 +38,18 @@ struct NTArgs {
   int32_t relu;
   int32_t dropout; uint32_t keep_thresh; float drop_scale; uint64_t seed; const uint64_t* seed_ptr;
   const float* proj; int32_t nproj; float* z; int64_t ldz;
+  int32_t a_bf16;  // A1/A2 hold bf16 (the float pointers are reinterpreted; ld in elements)
+  int32_t c_bf16;  // C is stored as bf16 (RNE), and the projection reads the rounded values
 };
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {  // RNE (v_cvt_pk_bf16_f32), NaN stays NaN
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+}
 
 // Epilogue shared by the NT kernels: bias, ReLU, dropout, store, optional projection.
 // acc[tm][t] is the 32x32 MFMA tile (rows wave·32·TM + tm·32 .., cols n0 + t·32 ..).
-template <int TM>
+template <int TM, bool CBF = false>
 __device__ __forceinline__ void nt_epilogue(const NTArgs& a, floatx16 (&acc)[TM][4], int64_t m0, int n0, int lane,
                                             int wave, uint64_t seed) {
 #pragma unroll
@@ -61,7 +68,13 @@ __device__ __forceinline__ void nt_epilogue(const NTArgs& a, floatx16 (&acc)[TM]
         if (a.dropout)
           v = keep_elem(seed, (uint32_t)row * (uint32_t)a.Nc + (uint32_t)col, a.keep_thresh) ? v * a.drop_scale : 0.0f;
         if (!colok) v = 0.0f;
-        if (a.c && row < a.M && colok) a.c[row * a.ldc + col] = v;
+        if constexpr (CBF) {
+          const uint16_t b = f32_to_bf16(v);
+          v = bf16_to_f32(b);
+          if (a.c && row < a.M && colok) reinterpret_cast<uint16_t*>(a.c)[row * a.ldc + col] = b;
+        } else {
+          if (a.c && row < a.M && colok) a.c[row * a.ldc + col] = v;
+        }
         acc[tm][t][r] = v;
       }
     }
@@ -122,12 +135,14 @@ struct TNArgs {
   float* slab; int64_t slab_stride;
   int64_t rows_per_block;
   int32_t want_db;
+  int32_t a_bf16;  // A1/A2 hold bf16
+  int32_t h_bf16;  // h holds bf16
 };
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,
 // defined in gemm_x3.hip.  Only the w1/w2 (in-place Linear weight) B form runs split.
 void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipStream_t st);
 size_t nt_x3_workspace(int64_t k1, int64_t k2);
-void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st);
+void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st);  // NPL = 3, or 1 when a_bf16
 
 }  // namespace gnnmp

@@ -761,6 +761,8 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
     return fail(GNN_ERR_INVALID_ARG, fn, "projection needs N <= 128, nproj <= 4, proj and z");
   if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, fn, "dropout p in [0,1)");
   if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, fn, "bad math mode");
+  if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->c_dtype != GNN_DTYPE_F32 && p->c_dtype != GNN_DTYPE_BF16))
+    return fail(GNN_ERR_INVALID_ARG, fn, "bad dtype");
   if (p->M == 0) return GNN_OK;
   NTArgs a{};
   a.M = p->M; a.Nc = (int32_t)p->N;
@@ -787,6 +789,14 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al(a.a1, 8) &&
             (a.k2 == 0 || ((a.k2 % 2 == 0) && (a.lda2 % 2 == 0) && al(a.a2, 8)));
   hipStream_t st = (hipStream_t)stream;
+  a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16;
+  a.c_bf16 = p->c_dtype == GNN_DTYPE_BF16;
+  if (a.a_bf16 || a.c_bf16) {
+    if (!a.a_bf16 || !a.w1 || a.Nc > BN || p->math == GNN_MATH_F32)
+      return fail(GNN_ERR_UNSUPPORTED, fn, "bf16 NT needs bf16 A, the w1/w2 form, N <= 128 and split math");
+    launch_nt_x3(a, 0, p->workspace, p->workspace_bytes, st);
+    return hip_check(hipGetLastError(), fn);
+  }
   if (p->math != GNN_MATH_F32 && a.w1 && a.Nc <= BN && variant < 16) {
     launch_nt_x3(a, variant, p->workspace, p->workspace_bytes, st);  // split-bf16 MFMA (gemm_x3.hip)
     return hip_check(hipGetLastError(), fn);
@@ -859,8 +869,15 @@ extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, v
   const bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al8(a.a1) &&
                   (a.k2 == 0 || ((a.k2 % 2 == 0) && (a.lda2 % 2 == 0) && al8(a.a2)));
   const bool proj = a.dz != nullptr, mask = a.h != nullptr;
+  a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16;
+  a.h_bf16 = p->h_dtype == GNN_DTYPE_BF16;
+  if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->h_dtype != GNN_DTYPE_F32 && p->h_dtype != GNN_DTYPE_BF16))
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad dtype");
+  if (a.h_bf16 && !a.a_bf16) return fail(GNN_ERR_UNSUPPORTED, __func__, "bf16 h needs bf16 A");
   // the split kernel indexes rows with 32-bit element offsets
   const int64_t ldmax = std::max({a.lda1, a.k2 > 0 ? a.lda2 : 0, a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
+  if (a.a_bf16 && (p->math == GNN_MATH_F32 || (a.M + 32) * ldmax >= ((int64_t)1 << 31)))
+    return fail(GNN_ERR_UNSUPPORTED, __func__, "bf16 TN needs split math and M*ld < 2^31");
   if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31)) {
     launch_tn_x3(a, nblk, st);  // split-bf16 MFMA (gemm_x3.hip)
     GNN_LAUNCH_CHECK();

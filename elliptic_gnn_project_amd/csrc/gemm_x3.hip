@@ -51,16 +51,57 @@ __device__ __forceinline__ floatx16 mfma6(const bf16x8 (&x)[3], const bf16x8 (&y
   return c;
 }
 
+template <int NPL>
+__device__ __forceinline__ floatx16 mfma_planes(const bf16x8 (&x)[NPL], const bf16x8 (&y)[NPL], floatx16 c) {
+  if constexpr (NPL == 3) return mfma6(x, y, c);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[0], c, 0, 0, 0);
+}
+
 __device__ __forceinline__ bf16x8 lds_frag(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// p + e elements of a buffer that holds f32 or (BF) bf16
+template <bool BF>
+__device__ __forceinline__ const float* elem_ptr(const float* p, int64_t e) {
+  if constexpr (BF) return reinterpret_cast<const float*>(reinterpret_cast<const uint16_t*>(p) + e);
+  else return p + e;
+}
 
 // ------------------------------------------------------------------------------------- NT
 // Stage rows [r0, r0+ROWS) x [k0, k0+KC) of a K-contiguous f32 operand into registers, in units
 // of U consecutive k per thread, each loaded as U/V vectors of V floats (V | k1, k2, ld).
 // Addresses are clamped (never data-dependent), so the prefetch stays in flight across the
 // MFMAs; masking happens at the split/store.
-template <int V, int U, int KC, int ROWS>
+template <int V, int U, int KC, int ROWS, bool BF = false>
 __device__ __forceinline__ void x3_load_rows(const float* X, int64_t ldx, int64_t r0, int64_t rows, int k0,
                                              int klen, float* reg) {
+  if constexpr (BF) {  // bf16 rows (ld in elements): V bf16 per load, widened to f32 (exact)
+    const uint16_t* X16 = reinterpret_cast<const uint16_t*>(X);
+    constexpr int UPR = KC / U;
+#pragma unroll
+    for (int i = 0; i < ROWS * KC / 256 / U; ++i) {
+      const int v = threadIdx.x + 256 * i;
+      const int r = v / UPR;
+      const int k = (v % UPR) * U;
+      int64_t row = r0 + r;
+      row = row < rows ? row : rows - 1;
+      const uint16_t* p = X16 + row * ldx + k0;
+#pragma unroll
+      for (int j = 0; j < U; j += V) {
+        const int kk = k + j < klen ? k + j : 0;
+        if constexpr (V == 4) {
+          const uint2 t = *reinterpret_cast<const uint2*>(p + kk);
+          reg[i * U + j] = __uint_as_float(t.x << 16); reg[i * U + j + 1] = __uint_as_float(t.x & 0xffff0000u);
+          reg[i * U + j + 2] = __uint_as_float(t.y << 16); reg[i * U + j + 3] = __uint_as_float(t.y & 0xffff0000u);
+        } else if constexpr (V == 2) {
+          const uint32_t t = *reinterpret_cast<const uint32_t*>(p + kk);
+          reg[i * U + j] = __uint_as_float(t << 16); reg[i * U + j + 1] = __uint_as_float(t & 0xffff0000u);
+        } else {
+          reg[i * U + j] = bf16_to_f32(p[kk]);
+        }
+      }
+    }
+    return;
+  }
   constexpr int UPR = KC / U;
 #pragma unroll
   for (int i = 0; i < ROWS * KC / 256 / U; ++i) {
@@ -88,7 +129,7 @@ __device__ __forceinline__ void x3_load_rows(const float* X, int64_t ldx, int64_
 
 // Split and store into three bf16 planes L[p * ROWS * PITCH + r * PITCH + k] (one b32 / b64 /
 // b128 store per plane for U = 2 / 4 / 8); zero outside (rows, klen).
-template <int U, int KC, int ROWS, int PITCH>
+template <int U, int KC, int ROWS, int PITCH, int NPL = 3>
 __device__ __forceinline__ void x3_store_rows(uint16_t* L, int64_t r0, int64_t rows, int klen, const float* reg) {
   constexpr int UPR = KC / U;
   constexpr int PL = ROWS * PITCH;
@@ -108,7 +149,7 @@ __device__ __forceinline__ void x3_store_rows(uint16_t* L, int64_t r0, int64_t r
     }
     uint16_t* d = L + r * PITCH + k;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < NPL; ++p) {
       if constexpr (U == 8) *reinterpret_cast<uint4*>(d + p * PL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
       else if constexpr (U == 4) *reinterpret_cast<uint2*>(d + p * PL) = make_uint2(w[0][p], w[1][p]);
       else *reinterpret_cast<uint32_t*>(d + p * PL) = w[0][p];
@@ -151,14 +192,16 @@ __device__ __forceinline__ void x3_chunk(const NTArgs& a, int c, int nch1, const
 // fed by a ring of D register stages: chunk c's loads are issued D chunks ahead, so D chunks
 // of A (BM x KC f32) are in flight per block while the MFMAs run (the split MFMA work per chunk
 // is short; without depth the loop waits on HBM latency).  One barrier per chunk.
-template <int KC, int TM, int AV, int AU, int BV, int D>
+// NPL = 3: f32 operands split (6 products); NPL = 1 with ABF: bf16 operands as stored, B rounded
+// to bf16 (the image's hi plane), one product (the bf16-storage path); CBF: C stored as bf16.
+template <int KC, int TM, int AV, int AU, int BV, int D, int NPL = 3, bool ABF = false, bool CBF = false>
 __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* __restrict__ bimg) {
   constexpr int P = KC + 8;  // bf16 per LDS row: 24 or 40 (12 / 20 dwords)
   constexpr int BM = 128 * TM;
   constexpr int APL = BM * P, BPL = BN * P;
   constexpr int AREG = BM * KC / 256, BREG = BN * KC / 256;
-  __shared__ __attribute__((aligned(16))) uint16_t As[2][3 * APL];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * BPL];
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][NPL * APL];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][NPL * BPL];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t m0 = (int64_t)blockIdx.x * BM;
@@ -183,10 +226,10 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   auto load = [&](int c, float* rA, float* rB) {
     const float *A, *W; int64_t lda, ldw; int k0, klen;
     x3_chunk<KC>(a, c, nch1, A, lda, W, ldw, k0, klen);
-    x3_load_rows<AV, AU, KC, BM>(A, lda, m0, a.M, k0, klen, rA);
+    x3_load_rows<AV, AU, KC, BM, ABF>(A, lda, m0, a.M, k0, klen, rA);
     if constexpr (BV == 0) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NPL; ++p) {
         const uint4 t = bimg[((int64_t)c * 3 + p) * 256 + threadIdx.x];
         rB[4 * p] = __uint_as_float(t.x); rB[4 * p + 1] = __uint_as_float(t.y);
         rB[4 * p + 2] = __uint_as_float(t.z); rB[4 * p + 3] = __uint_as_float(t.w);
@@ -198,16 +241,16 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   auto store = [&](int c, int buf, const float* rA, const float* rB) {
     const float *A, *W; int64_t lda, ldw; int k0, klen;
     x3_chunk<KC>(a, c, nch1, A, lda, W, ldw, k0, klen);
-    x3_store_rows<AU, KC, BM, P>(As[buf], m0, a.M, klen, rA);
+    x3_store_rows<AU, KC, BM, P, NPL>(As[buf], m0, a.M, klen, rA);
     if constexpr (BV == 0) {
       const int n = threadIdx.x >> 1, kh = threadIdx.x & 1;
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < NPL; ++p)
         *reinterpret_cast<uint4*>(&Bs[buf][p * BPL + n * P + 8 * kh]) =
             make_uint4(__float_as_uint(rB[4 * p]), __float_as_uint(rB[4 * p + 1]), __float_as_uint(rB[4 * p + 2]),
                        __float_as_uint(rB[4 * p + 3]));
     } else {
-      x3_store_rows<BU, KC, BN, P>(Bs[buf], n0, a.Nc, klen, rB);
+      x3_store_rows<BU, KC, BN, P, NPL>(Bs[buf], n0, a.Nc, klen, rB);
     }
   };
   const int fr = (lane & 31) * P + 8 * (lane >> 5);
@@ -218,19 +261,19 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
 #pragma unroll
     for (int s = 0; s < KC / 16; ++s) {
       if (16 * s < klen) {
-        bf16x8 af[TM][3], bf[4][3];
+        bf16x8 af[TM][NPL], bf[4][NPL];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
-          for (int p = 0; p < 3; ++p) af[tm][p] = lds_frag(Ab + p * APL + tm * 32 * P + 16 * s);
+          for (int p = 0; p < NPL; ++p) af[tm][p] = lds_frag(Ab + p * APL + tm * 32 * P + 16 * s);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int p = 0; p < 3; ++p) bf[t][p] = lds_frag(Bb + p * BPL + t * 32 * P + 16 * s);
+          for (int p = 0; p < NPL; ++p) bf[t][p] = lds_frag(Bb + p * BPL + t * 32 * P + 16 * s);
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int tm = 0; tm < TM; ++tm) acc[tm][t] = mfma6(af[tm], bf[t], acc[tm][t]);
+          for (int tm = 0; tm < TM; ++tm) acc[tm][t] = mfma_planes<NPL>(af[tm], bf[t], acc[tm][t]);
       }
     }
   };
@@ -261,7 +304,7 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
       compute(c & 1, c);
     }
   }
-  nt_epilogue<TM>(a, acc, m0, n0, lane, wave, seed);
+  nt_epilogue<TM, CBF>(a, acc, m0, n0, lane, wave, seed);
 }
 
 template <int KC, int TM, int AV, int AU, int D>
@@ -298,12 +341,14 @@ constexpr int TX_AS = 3;           // A unit slots per thread (u = tid + 256·s 
 // Idle slots load a fixed valid address.  dz (PROJ) is staged one chunk ahead into a 2-slot
 // LDS ring (16 rows x 4) by threads 0..63, so G(c) = (dz·P) ⊙ mask is formed at store(c)
 // from LDS instead of 32 registers of replicated dz rows per thread.
-template <bool PROJ, bool MASK, int D, int KT>
+// NPL = 3: f32 operands split (6 products).  NPL = 1: the bf16-storage path — A (ABF) and h
+// (HBF) are read as bf16, G is rounded to bf16, one product per MFMA.
+template <bool PROJ, bool MASK, int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false>
 __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   constexpr int NS = TX_AS + ((!PROJ && MASK) ? 2 : 1);  // + G slot (+ g slot)
   constexpr int GS = TX_AS;                              // the G slot index
-  __shared__ __attribute__((aligned(16))) uint16_t Gt[2][3 * TGPL];
-  __shared__ __attribute__((aligned(16))) uint16_t At[2][3 * TAPL];
+  __shared__ __attribute__((aligned(16))) uint16_t Gt[2][NPL * TGPL];
+  __shared__ __attribute__((aligned(16))) uint16_t At[2][NPL * TAPL];
   __shared__ float Ps[MAXPROJ * 128];
   __shared__ float dzL[2][TMC * MAXPROJ];
   const int tid = threadIdx.x;
@@ -346,11 +391,11 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
     ak[sl] = u % KP;
     oct[sl] = u / KP;
     const int k = ak[sl];
-    if (aon[sl] && k < a.k1) { base[sl] = a.a1 + k; ld32[sl] = (int)a.lda1; }
-    else if (aon[sl] && k < Kc) { base[sl] = a.a2 + (k - a.k1); ld32[sl] = (int)a.lda2; }
+    if (aon[sl] && k < a.k1) { base[sl] = elem_ptr<ABF>(a.a1, k); ld32[sl] = (int)a.lda1; }
+    else if (aon[sl] && k < Kc) { base[sl] = elem_ptr<ABF>(a.a2, k - a.k1); ld32[sl] = (int)a.lda2; }
     else { base[sl] = a.a1; ld32[sl] = 0; oct[sl] = 0; }
   }
-  if constexpr (MASK) { base[GS] = a.h + gnc; ld32[GS] = (int)a.ldh; }
+  if constexpr (MASK) { base[GS] = elem_ptr<HBF>(a.h, gnc); ld32[GS] = (int)a.ldh; }
   else { base[GS] = a.g + gnc; ld32[GS] = (int)a.ldg; }
   oct[GS] = go;
   if constexpr (NS == GS + 2) { base[GS + 1] = a.g + gnc; ld32[GS + 1] = (int)a.ldg; oct[GS + 1] = go; }
@@ -369,7 +414,9 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int m = min(m0 + 8 * oct[sl] + i, mlast);
-        rv[d][sl][i] = base[sl][(uint32_t)(m * ld32[sl])];
+        const uint32_t off = (uint32_t)(m * ld32[sl]);
+        const bool bf = sl < TX_AS ? ABF : (sl == GS && MASK ? HBF : false);  // compile-time per slot
+        rv[d][sl][i] = bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(base[sl])[off]) : base[sl][off];
       }
     if constexpr (PROJ) {  // dz rows of chunk c + 1
       const int m = min(m0 + TMC + zr, mlast);
@@ -384,7 +431,7 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) split_pair(e[2 * j], e[2 * j + 1], w[j]);
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < NPL; ++p)
       *reinterpret_cast<uint4*>(dst + p * plane) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
   };
   auto store = [&](int d, int c) {
@@ -437,15 +484,15 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   const int fr = (lane & 31) * TP + 8 * (lane >> 5);
   auto compute = [&](int c) {
     const int buf = c & 1;
-    bf16x8 gf[3];
+    bf16x8 gf[NPL];
 #pragma unroll
-    for (int p = 0; p < 3; ++p) gf[p] = lds_frag(Gt[buf] + p * TGPL + ntile * 32 * TP + fr);
+    for (int p = 0; p < NPL; ++p) gf[p] = lds_frag(Gt[buf] + p * TGPL + ntile * 32 * TP + fr);
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      bf16x8 af[3];
+      bf16x8 af[NPL];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) af[p] = lds_frag(At[buf] + p * TAPL + t * 32 * TP + fr);
-      acc[t] = mfma6(gf, af, acc[t]);
+      for (int p = 0; p < NPL; ++p) af[p] = lds_frag(At[buf] + p * TAPL + t * 32 * TP + fr);
+      acc[t] = mfma_planes<NPL>(gf, af, acc[t]);
     }
   };
 
@@ -528,8 +575,30 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
     return (a.k1 % v == 0) && (a.lda1 % v == 0) && al(a.a1, 4 * v) &&
            (a.k2 == 0 || ((a.k2 % v == 0) && (a.lda2 % v == 0) && al(a.a2, 4 * v)));
   };
-  const int av = av_ok(4) ? 4 : (av_ok(2) ? 2 : 1);
   const uint4* bimg = nullptr;
+  if (a.a_bf16) {  // bf16 storage: one product per MFMA on bf16 operands (B rounded to bf16)
+    auto bv_ok = [&](int v) {
+      return (a.k1 % v == 0) && (a.lda1 % v == 0) && al(a.a1, 2 * v) &&
+             (a.k2 == 0 || ((a.k2 % v == 0) && (a.lda2 % v == 0) && al(a.a2, 2 * v)));
+    };
+    const bool pre = ws && ws_bytes >= nt_x3_workspace(a.k1, a.k2) && a.Nc <= BN;
+    if (pre) {
+      const int nch1 = (a.k1 + 15) / 16, nch = nch1 + (a.k2 + 15) / 16;
+      x3_presplit_b_kernel<<<nch, 256, 0, st>>>(a, static_cast<uint4*>(ws), nch1, nch);
+      bimg = static_cast<const uint4*>(ws);
+    }
+    dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)ceil_div(a.Nc, BN));
+#define GNN_NTB(AVV, BVV, C) gemm_nt_x3_kernel<16, 1, AVV, 2, BVV, 2, 1, true, C><<<grid, 256, 0, st>>>(a, bimg)
+#define GNN_NTB_C(AVV, BVV) do { if (a.c_bf16) GNN_NTB(AVV, BVV, true); else GNN_NTB(AVV, BVV, false); } while (0)
+    const bool v2 = bv_ok(2);
+    if (bimg) { if (v2) GNN_NTB_C(2, 0); else GNN_NTB_C(1, 0); }
+    else if (a.wvec >= 2) { if (v2) GNN_NTB_C(2, 2); else GNN_NTB_C(1, 2); }
+    else { if (v2) GNN_NTB_C(2, 1); else GNN_NTB_C(1, 1); }
+#undef GNN_NTB_C
+#undef GNN_NTB
+    return;
+  }
+  const int av = av_ok(4) ? 4 : (av_ok(2) ? 2 : 1);
   const bool pre = ws && ws_bytes >= nt_x3_workspace(a.k1, a.k2) && a.Nc <= BN;
   if (pre) {
     const int nch1 = (a.k1 + 15) / 16, nch = nch1 + (a.k2 + 15) / 16;
@@ -548,18 +617,23 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
   }
 }
 
-template <int D, int KT>
+template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false>
 void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
   const bool proj = a.dz != nullptr, mask = a.h != nullptr;
-  if (proj && mask) gemm_tn_x3_kernel<true, true, D, KT><<<nblk, TX_THREADS, 0, st>>>(a);
-  else if (proj) gemm_tn_x3_kernel<true, false, D, KT><<<nblk, TX_THREADS, 0, st>>>(a);
-  else if (mask) gemm_tn_x3_kernel<false, true, D, KT><<<nblk, TX_THREADS, 0, st>>>(a);
-  else gemm_tn_x3_kernel<false, false, D, KT><<<nblk, TX_THREADS, 0, st>>>(a);
+  if (proj && mask) gemm_tn_x3_kernel<true, true, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (proj) gemm_tn_x3_kernel<true, false, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (mask) gemm_tn_x3_kernel<false, true, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
+  else gemm_tn_x3_kernel<false, false, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
 }
 
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
   constexpr int D = 1;
+  if (a.a_bf16) {  // bf16 storage (A and h bf16; G rounded to bf16): one product per MFMA
+    if (nkt <= 8) { if (a.h_bf16) launch_tn_x3_k<D, 8, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 8, 1, true, false>(a, nblk, st); }
+    else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false>(a, nblk, st); }
+    return;
+  }
   if (nkt <= 6) launch_tn_x3_k<D, 6>(a, nblk, st);
   else if (nkt <= 8) launch_tn_x3_k<D, 8>(a, nblk, st);
   else if (nkt <= 11) launch_tn_x3_k<D, 11>(a, nblk, st);

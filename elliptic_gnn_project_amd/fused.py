@@ -69,11 +69,13 @@ def _nt_workspace(device, n, k1, k2):
 
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
             out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None):
+    """bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too."""
     """C = epilogue([a1 | a2] · B) on the MFMA NT kernel; B = bt ([K, n] row-major) or, with bt None,
     [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2]."""
     M = a1.size(0)
+    bf = a1.dtype == torch.bfloat16
     if out is None and want_c:
-        out = torch.empty((M, n), dtype=torch.float32, device=a1.device)
+        out = torch.empty((M, n), dtype=torch.bfloat16 if bf else torch.float32, device=a1.device)
     ws = None
     if w1 is not None:  # B pre-split image for the streaming split-bf16 kernel (≈24 KB per 32 of K)
         k2_ = a2.size(1) if a2 is not None else 0
@@ -89,6 +91,8 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.ptr(proj), proj.size(0) if proj is not None else 0, _lib.ptr(z), _ld(z) if z is not None else 0,
         _math(math),
         _lib.ptr(ws), ws.numel() * 4 if ws is not None else 0,
+        _lib.DTYPE_BF16 if bf else _lib.DTYPE_F32,
+        _lib.DTYPE_BF16 if (out is not None and out.dtype == torch.bfloat16) else _lib.DTYPE_F32,
     )
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
@@ -98,7 +102,12 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
     if KernelTimer.active:
         e1.record()
         k = a1.size(1) + (a2.size(1) if a2 is not None else 0)
-        KernelTimer.records.append((("gemm_nt", M, k, n), e0, e1, 2 * M * k * n))
+        # tag: kind, M, K, N, A element bytes, C element bytes, MFMA products per bf16 term
+        # (6 split-bf16, 1 bf16 storage, 0 exact f32)
+        ea = a1.element_size()
+        prod = 0 if (_math(math) == _lib.MATH_F32 or w1 is None) else (1 if ea == 2 else 6)
+        KernelTimer.records.append((("gemm_nt", M, k, n, ea, out.element_size() if out is not None else 0, prod),
+                                    e0, e1, 2 * M * k * n))
     return out
 
 
@@ -121,6 +130,8 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         a1.data_ptr(), _ld(a1), k1,
         _lib.ptr(a2), _ld(a2) if a2 is not None else 0, k2,
         _math(math),
+        _lib.DTYPE_BF16 if a1.dtype == torch.bfloat16 else _lib.DTYPE_F32,
+        _lib.DTYPE_BF16 if (h is not None and h.dtype == torch.bfloat16) else _lib.DTYPE_F32,
     )
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
@@ -129,7 +140,10 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     _lib.call("gnn_gemm_tn_f32", p, out.data_ptr(), ws.data_ptr(), ws.numel() * 4, _lib.stream_handle(a1.device))
     if KernelTimer.active:
         e1.record()
-        KernelTimer.records.append((("gemm_tn", M, k1 + k2, nr), e0, e1, 2 * M * (k1 + k2) * nr))
+        ea = a1.element_size()
+        prod = 0 if _math(math) == _lib.MATH_F32 else (1 if ea == 2 else 6)
+        KernelTimer.records.append((("gemm_tn", M, k1 + k2, nr, ea, h.element_size() if h is not None else 4, prod),
+                                    e0, e1, 2 * M * (k1 + k2) * nr))
     o = 0
     dW1 = out[o: o + nr * k1].view(nr, k1)  # contiguous per segment: autograd adopts them, no clone
     o += nr * k1
@@ -147,6 +161,8 @@ class _FusedSAGE(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, x, plan: GraphPlan, dropout_p: float, seeds: List[int], seed_ctr, *params):
+        # x bf16 selects the bf16-storage path: agg_l and h_l stored bf16, GEMMs on bf16 operands
+        # (weights rounded to bf16) with f32 accumulation; z, logits and all gradients stay f32.
         L = len(params) // 3
         Wl = params[0::3]
         bl = params[1::3]
@@ -221,7 +237,7 @@ class _FusedSAGE(torch.autograd.Function):
                 dh = aggregate(plan, dA[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg,
                                addend=dA[:, fi:])
                 g = dh  # next (lower) layer's upstream gradient w.r.t. h_l, masked inside TN
-        dx = g if need_x else None
+        dx = g.to(hs[0].dtype) if need_x else None
         return (dx, None, None, None, None, *grads)
 
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 6
+#define GNNMP_ABI_VERSION 7
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -159,6 +159,11 @@ typedef struct {
 gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params* p, const float* x,
                              int64_t ldx, int64_t F, float* y, int64_t ldy, gnn_stream_t stream);
 
+/* bf16-storage form: x and y hold bf16 ([rows, F], ld in elements), f32 accumulation in plan
+ * order, y rounded once (RNE).  Modes SUM / MEAN / MEAN_BWD / GCN (no EDGE_W); addend f32. */
+gnn_status gnn_aggregate_bf16(const gnn_graph* g, const gnn_agg_params* p, const void* x, int64_t ldx,
+                              int64_t F, void* y, int64_t ldy, gnn_stream_t stream);
+
 /* Named forms of the above (what an FFI binding of SAGEConv would call). */
 gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
                                  int64_t F, float* out, int64_t ldo, gnn_stream_t stream);
@@ -198,6 +203,9 @@ gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t con
 /*     Replace PyG Linear lin_l/lin_r/lin (gnn.py:20-23,41-44,64-67) and the  */
 /*     F.relu + F.dropout between layers (gnn.py:29-30,50-51,73-74).          */
 /* ------------------------------------------------------------------------ */
+/* Element type of a feature buffer. */
+typedef enum { GNN_DTYPE_F32 = 0, GNN_DTYPE_BF16 = 1 } gnn_dtype;
+
 /* Arithmetic of the K7 GEMMs.  Both are fp32-accurate (inputs, outputs and accumulation f32). */
 typedef enum {
   GNN_MATH_SPLIT_BF16 = 0, /* default: every f32 operand split into hi+mid+lo bf16 terms, 6 products on
@@ -224,7 +232,10 @@ typedef struct {
   float* z; int64_t ldz;
   int32_t math;                          /* gnn_gemm_math */
   void* workspace; size_t workspace_bytes; /* optional: the split-bf16 w1/w2 form pre-splits B here
-                                            (gnn_gemm_nt_workspace_size) and streams A without LDS */
+                                            (gnn_gemm_nt_workspace_size) */
+  int32_t a_dtype;                       /* gnn_dtype of A1/A2 (BF16: w1/w2 form; B rounded to bf16,
+                                            one bf16 product, f32 accumulate — the bf16-storage path) */
+  int32_t c_dtype;                       /* gnn_dtype of C (BF16 needs a_dtype BF16); z stays f32 */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
@@ -241,6 +252,8 @@ typedef struct {
   const float* a1; int64_t lda1; int64_t k1;
   const float* a2; int64_t lda2; int64_t k2;
   int32_t math;                          /* gnn_gemm_math */
+  int32_t a_dtype;                       /* gnn_dtype of A1/A2 (BF16: G rounded to bf16, one product) */
+  int32_t h_dtype;                       /* gnn_dtype of h */
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).

@@ -1,0 +1,141 @@
+"""bf16-storage path (BASELINE configs[4]: the scaled 2M-node 3-layer SAGE in bf16): node
+features, aggregates and hidden activations stored bf16, every GEMM on bf16 operands (weights
+rounded to bf16) with f32 accumulation; z, logits and gradients f32.
+
+The reference is the same computation in float64 on the CPU with the same rounding points
+(inputs, aggregates and hidden activations rounded to bf16 where the kernels store them).  The
+kernels sum in a different order than the reference, so a stored bf16 value may land one bf16
+ulp (2^-8 relative) away; tolerances are stated per test in those terms."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+BF_ULP = 2.0 ** -8
+
+
+def rb(t):  # round to bf16 (RNE), back to the computing dtype
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def rel_l2(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("F", [166, 128, 7])
+def test_aggregate_bf16_mean(device, F):
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.aggregation import aggregate
+    from elliptic_gnn_project_amd.graph import get_plan
+    from oracle import pyg_ref
+
+    g = torch.Generator().manual_seed(F)
+    N, E = 3000, 9000
+    ei = torch.randint(0, N, (2, E), generator=g)
+    x = torch.randn(N, F, generator=g).to(torch.bfloat16)
+    ref = pyg_ref.scatter(x.double()[ei[0]], ei[1], N, "mean")
+    plan = get_plan(ei.to(device), N, _lib.LOOPS_KEEP)
+    y = aggregate(plan, x.to(device), _lib.AGG_MEAN, nodew=plan.deg)
+    assert y.dtype == torch.bfloat16
+    d = (y.double().cpu() - ref).abs()
+    assert float((d <= BF_ULP * ref.abs() + 1e-30).double().mean()) == 1.0, float(d.max())
+
+
+@pytest.mark.parametrize("M,k1,k2,n", [(3000, 166, 166, 128), (777, 128, 128, 64), (129, 30, 0, 2)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu_proj"])
+def test_gemm_nt_bf16(device, M, k1, k2, n, epi):
+    from elliptic_gnn_project_amd.fused import gemm_nt
+
+    g = torch.Generator().manual_seed(M + n)
+    a1 = torch.randn(M, k1, generator=g).to(torch.bfloat16)
+    a2 = torch.randn(M, k2, generator=g).to(torch.bfloat16) if k2 else None
+    w1 = torch.randn(n, k1, generator=g) * 0.1
+    w2 = torch.randn(n, k2, generator=g) * 0.1 if k2 else None
+    bias = torch.randn(n, generator=g)
+    proj = torch.randn(4, n, generator=g)
+    A = torch.cat([a1, a2], 1) if k2 else a1
+    W = torch.cat([w1, w2], 1) if k2 else w1
+    ref = A.double() @ rb(W).double().t()
+    kw = {}
+    z = None
+    if epi != "plain":
+        ref = torch.relu(ref + bias.double())
+        z = torch.empty(M, 4, device=device)
+        kw = dict(bias=bias.to(device), relu=True, proj=proj.to(device), z=z)
+    c = gemm_nt(a1.to(device), None, n, a2=a2.to(device) if k2 else None, w1=w1.to(device),
+                w2=w2.to(device) if k2 else None, **kw)
+    assert c.dtype == torch.bfloat16
+    d = (c.double().cpu() - ref).abs()
+    assert float(d.max()) <= float((BF_ULP * ref.abs() + 1e-5).max()), float(d.max())
+    assert rel_l2(c, ref) < 3e-3
+    if z is not None:  # projection of the stored (bf16-rounded) h
+        assert rel_l2(z, c.double().cpu() @ proj.double().t()) < 1e-5
+
+
+@pytest.mark.parametrize("form", ["dz_mask", "g_mask"])
+def test_gemm_tn_bf16(device, form):
+    from elliptic_gnn_project_amd.fused import gemm_tn
+
+    g_ = torch.Generator().manual_seed(5)
+    M, nr, k1, k2 = 5000, 128, 166, 166
+    a1 = torch.randn(M, k1, generator=g_).to(torch.bfloat16)
+    a2 = torch.randn(M, k2, generator=g_).to(torch.bfloat16)
+    h = torch.relu(torch.randn(M, nr, generator=g_)).to(torch.bfloat16)
+    dz = torch.randn(M, 4, generator=g_) * 1e-3
+    proj = torch.randn(4, nr, generator=g_)
+    G = dz @ proj if form == "dz_mask" else torch.randn(M, nr, generator=g_) * 1e-3
+    kw = dict(dz=dz.to(device), proj=proj.to(device)) if form == "dz_mask" else dict(g=G.to(device))
+    Gm = torch.where(h.float() > 0, G * 2.0, torch.zeros_like(G))
+    gout = torch.empty(M, nr, device=device)
+    dW, db, dW2, _ = gemm_tn(nr, a1.to(device), a2.to(device), h=h.to(device), hscale=2.0, gout=gout, **kw)
+    torch.testing.assert_close(gout.cpu(), Gm, rtol=1e-5, atol=1e-8)  # G itself stays f32
+    A = torch.cat([a1, a2], 1).double()
+    ref = rb(Gm).double().t() @ A  # the MFMA operand is G rounded to bf16
+    assert rel_l2(torch.cat([dW[0], dW[1]], 1), ref) < 1e-5
+    assert rel_l2(db, Gm.sum(0)) < 1e-5
+    if form == "dz_mask":
+        assert rel_l2(dW2, dz.t().double() @ h.double()) < 1e-5
+
+
+def _ref_sage_bf16(params, x_bf, ei, N, layers):
+    """float64 SAGE forward with the bf16-storage rounding points, autograd for the grads."""
+    from oracle import pyg_ref
+
+    P = {k: v.double().requires_grad_(True) for k, v in params.items()}
+    h = x_bf.double()
+    for l in range(layers - 1):
+        agg = rb(pyg_ref.scatter(h[ei[0]], ei[1], N, "mean"))
+        pre = agg @ rb(P[f"convs.{l}.lin_l.weight"]).t() + P[f"convs.{l}.lin_l.bias"] + \
+            h @ rb(P[f"convs.{l}.lin_r.weight"]).t()
+        h = rb(torch.relu(pre))
+    l = layers - 1
+    z_l = h @ P[f"convs.{l}.lin_l.weight"].t()
+    z_r = h @ P[f"convs.{l}.lin_r.weight"].t()
+    logits = pyg_ref.scatter(z_l[ei[0]], ei[1], N, "mean") + z_r + P[f"convs.{l}.lin_l.bias"]
+    return logits, P
+
+
+def test_fused_sage_bf16_train_step(device):
+    """3-layer SAGE on bf16 features: logits within 2e-3 and parameter gradients within 2e-2
+    (relative L2) of the float64 reference with the same rounding points (gradient operands are
+    rounded to bf16 inside the kernels, the reference keeps them exact)."""
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=6000, num_edges=9000, seed=4),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+    N = data.x.size(0)
+    torch.manual_seed(3)
+    model = SAGENet(data.x.size(1), 128, layers=3, dropout=0.0).to(device)
+    params = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    x_bf = data.x.to(torch.bfloat16)
+    logits = model(x_bf.to(device), data.edge_index.to(device))
+    assert logits.dtype == torch.float32
+    w = torch.randn(N, 2, generator=torch.Generator().manual_seed(1))
+    (logits * w.to(device)).sum().backward()
+    ref, P = _ref_sage_bf16(params, x_bf, data.edge_index, N, 3)
+    assert rel_l2(logits, ref) < 2e-3
+    (ref * w.double()).sum().backward()
+    for k, v in model.named_parameters():
+        assert rel_l2(v.grad, P[k].grad) < 2e-2, k
