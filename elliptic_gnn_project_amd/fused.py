@@ -228,15 +228,22 @@ class _FusedSAGE(torch.autograd.Function):
             grads[3 * l + 0] = dW[0]
             grads[3 * l + 1] = db
             grads[3 * l + 2] = dW[1]
-            if need_g:
-                # dh_l = meanᵀ(G · W_l) + G · W_r   (G = dL/dpre_{l+1}); W [fo, fi] is already the
-                # row-major [K, N] operand of the NT kernel: no copies
+            if need_g and fi <= 128:
+                # dh_l = meanᵀ(G · W_l) + G · W_r = [meanᵀ(G) | G] · [W_l; W_r]  (G = dL/dpre_{l+1}):
+                # reassociated so one transposed aggregation of G (width fo) and ONE GEMM
+                # (K = 2·fo, split-bf16, W read as the [fi, fo] transposes) replace two GEMMs
+                # and the [N, 2·fi] intermediate
+                aggG = aggregate(plan, gout, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg)
+                g = gemm_nt(aggG, None, fi, a2=gout, w1=Wl[l].t().contiguous(), w2=Wr[l].t().contiguous())
+            elif need_g:
+                # fi > 128 (the input layer's dx): W [fo, fi] is already the row-major [K, N]
+                # operand of the NT kernel (exact f32 form)
                 dA = torch.empty((N, 2 * fi), dtype=torch.float32, device=dz.device)
                 gemm_nt(gout, Wl[l], fi, out=dA[:, :fi])
                 gemm_nt(gout, Wr[l], fi, out=dA[:, fi:])
-                dh = aggregate(plan, dA[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg,
-                               addend=dA[:, fi:])
-                g = dh  # next (lower) layer's upstream gradient w.r.t. h_l, masked inside TN
+                g = aggregate(plan, dA[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg,
+                              addend=dA[:, fi:])
+            # g: next (lower) layer's upstream gradient w.r.t. h_l, masked inside its TN
         dx = g.to(hs[0].dtype) if need_x else None
         return (dx, None, None, None, None, *grads)
 
