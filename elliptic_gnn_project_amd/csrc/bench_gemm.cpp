@@ -17,6 +17,8 @@
 #include "../../include/gnnmp.h"
 
 extern "C" gnn_status gnnx_gemm_nt_variant_f32(const gnn_gemm_nt_params* p, int variant, gnn_stream_t stream);
+extern "C" gnn_status gnnx_gemm_tn_variant_f32(const gnn_gemm_tn_params* p, float* out, void* workspace,
+                                               size_t workspace_bytes, int variant, gnn_stream_t stream);
 
 #define CK(x)                                                                 \
   do {                                                                        \
@@ -97,8 +99,24 @@ int main(int argc, char** argv) {
   gnn_gemm_nt_params plain = p;
   plain.bias = nullptr; plain.relu = 0; plain.dropout_p = 0.f; plain.proj = nullptr; plain.nproj = 0; plain.z = nullptr;
 
+  if (const char* tn = std::getenv("LAB_TN_ONLY")) {  // one TN variant only (PMC passes): 0 = x3, 1 = x3b
+    GK(gnnx_gemm_nt_variant_f32(&p, 16, nullptr));
+    gnn_gemm_tn_params q{};
+    q.M = M; q.Nr = H; q.dz = dz; q.lddz = 4; q.proj = proj; q.nproj = 4; q.h = c; q.ldh = H; q.hscale = 2.f;
+    q.a1 = agg; q.lda1 = F; q.k1 = F; q.a2 = x; q.lda2 = F; q.k2 = F;
+    size_t wsb = 0;
+    GK(gnn_gemm_tn_workspace_size(M, H, 2 * F, 4, &wsb));
+    void* ws;
+    CK(hipMalloc(&ws, wsb));
+    float* out;
+    CK(hipMalloc(&out, (H * 2 * F + H + 4 * H + 4) * sizeof(float)));
+    for (int r = 0; r < rounds; ++r) GK(gnnx_gemm_tn_variant_f32(&q, out, ws, wsb, std::atoi(tn), nullptr));
+    CK(hipDeviceSynchronize());
+    std::printf("LAB_TN_ONLY %s done\n", tn);
+    return 0;
+  }
   // ---- NT accuracy vs float64 on sampled rows (plain GEMM)
-  const std::vector<int> variants = {0, 1, 2, 3, 5, 16};  // <16: split-bf16 tilings; >=16: exact f32
+  const std::vector<int> variants = {0, 16};  // <16: split-bf16 tilings; >=16: exact f32
   std::vector<int64_t> rows;
   for (int64_t r = 0; r < M; r += std::max<int64_t>(1, M / 3000)) rows.push_back(r);
   rows.push_back(M - 1);
@@ -182,9 +200,9 @@ int main(int argc, char** argv) {
         for (int k = 0; k < F; ++k) rdw[H * F + n * F + k] += g[n] * h_x[m * F + k];
       }
     }
-    for (int math : {1, 0}) {
-      qc.math = math;
-      GK(gnn_gemm_tn_f32(&qc, out, ws, wsb, nullptr));
+    for (int math : {1, 0, 2}) {  // 2: split-bf16 with the 32-row-chunk kernel (variant 1)
+      qc.math = math == 2 ? 0 : math;
+      GK(gnnx_gemm_tn_variant_f32(&qc, out, ws, wsb, math == 2 ? 1 : 0, nullptr));
       auto got = to_host(out, nout);
       double se = 0, sr = 0, mx = 0, rmx = 0;
       for (int64_t i = 0; i < H * 2 * F; ++i) {
@@ -197,10 +215,11 @@ int main(int argc, char** argv) {
                   (long long)Mc, std::sqrt(se / sr), mx, rmx, dbe);
     }
   }
-  for (int math : {1, 0}) {
-    q.math = math;
+  for (int math : {1, 0, 2}) {
+    q.math = math == 2 ? 0 : math;
     std::vector<float> tt;
-    for (int r = 0; r < rounds; ++r) tt.push_back(T.run([&] { gnn_gemm_tn_f32(&q, out, ws, wsb, nullptr); }, 5));
+    for (int r = 0; r < rounds; ++r)
+      tt.push_back(T.run([&] { gnnx_gemm_tn_variant_f32(&q, out, ws, wsb, math == 2 ? 1 : 0, nullptr); }, 5));
     std::printf("TN dz+mask math=%d: %8.1f us (%6.1f TF)\n", math, med(tt), flops / med(tt) * 1e-6);
   }
   return 0;

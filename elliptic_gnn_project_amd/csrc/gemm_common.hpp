@@ -143,6 +143,6 @@ struct TNArgs {
 // defined in gemm_x3.hip.  Only the w1/w2 (in-place Linear weight) B form runs split.
 void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipStream_t st);
 size_t nt_x3_workspace(int64_t k1, int64_t k2);
-void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st);  // NPL = 3, or 1 when a_bf16
+void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant = 0);  // NPL = 3, or 1 when a_bf16
 
 }  // namespace gnnmp

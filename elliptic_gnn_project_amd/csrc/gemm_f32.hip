@@ -831,31 +831,46 @@ extern "C" gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t 
   return GNN_OK;
 }
 
+static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void* workspace,
+                                   size_t workspace_bytes, gnn_stream_t stream, int variant);
+
 extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* workspace,
                                       size_t workspace_bytes, gnn_stream_t stream) {
-  if (!p || !out) return fail(GNN_ERR_INVALID_ARG, __func__, "null params/out");
+  return gemm_tn_dispatch(p, out, workspace, workspace_bytes, stream, 0);
+}
+
+// Tuning entry (not part of the public ABI): split-bf16 TN tiling `variant` (gemm_x3.hip).
+extern "C" gnn_status gnnx_gemm_tn_variant_f32(const gnn_gemm_tn_params* p, float* out, void* workspace,
+                                               size_t workspace_bytes, int variant, gnn_stream_t stream) {
+  return gemm_tn_dispatch(p, out, workspace, workspace_bytes, stream, variant);
+}
+
+static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void* workspace,
+                                   size_t workspace_bytes, gnn_stream_t stream, int variant) {
+  const char* __fn = "gnn_gemm_tn_f32";
+  if (!p || !out) return fail(GNN_ERR_INVALID_ARG, __fn, "null params/out");
   if (p->M < 0 || p->Nr < 1 || p->Nr > 128 || p->k1 < 1 || p->k2 < 0 || p->k1 + p->k2 > KMAX)
-    return fail(GNN_ERR_UNSUPPORTED, __func__, "needs 1 <= Nr <= 128 and k1 + k2 <= 384");
+    return fail(GNN_ERR_UNSUPPORTED, __fn, "needs 1 <= Nr <= 128 and k1 + k2 <= 384");
   if (!p->a1 || (p->k2 > 0 && !p->a2) || p->lda1 < p->k1 || (p->k2 > 0 && p->lda2 < p->k2))
-    return fail(GNN_ERR_INVALID_ARG, __func__, "bad A operands");
+    return fail(GNN_ERR_INVALID_ARG, __fn, "bad A operands");
   if (p->dz) {
     if (p->nproj < 1 || p->nproj > MAXPROJ || !p->proj || p->lddz < p->nproj)
-      return fail(GNN_ERR_INVALID_ARG, __func__, "dz form needs 1 <= nproj <= 4 and proj");
+      return fail(GNN_ERR_INVALID_ARG, __fn, "dz form needs 1 <= nproj <= 4 and proj");
   } else if (!p->g || p->ldg < p->Nr) {
-    return fail(GNN_ERR_INVALID_ARG, __func__, "need g (or dz + proj)");
+    return fail(GNN_ERR_INVALID_ARG, __fn, "need g (or dz + proj)");
   }
-  if (p->h && p->ldh < p->Nr) return fail(GNN_ERR_INVALID_ARG, __func__, "bad ldh");
-  if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, __func__, "bad math mode");
-  if (p->gout && p->ldgout < p->Nr) return fail(GNN_ERR_INVALID_ARG, __func__, "bad ldgout");
+  if (p->h && p->ldh < p->Nr) return fail(GNN_ERR_INVALID_ARG, __fn, "bad ldh");
+  if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, __fn, "bad math mode");
+  if (p->gout && p->ldgout < p->Nr) return fail(GNN_ERR_INVALID_ARG, __fn, "bad ldgout");
   const int32_t nproj = p->dz ? p->nproj : 0;
   const int64_t Kc = p->k1 + p->k2;
   const int64_t n_out = p->Nr * Kc + p->Nr + (int64_t)nproj * p->Nr + nproj;
   int64_t stride = (n_out + 63) / 64 * 64;
   const int nblk = tn_blocks(p->M);
   if (!workspace || workspace_bytes < (size_t)nblk * stride * sizeof(float))
-    return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
+    return fail(GNN_ERR_WORKSPACE, __fn, "workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  if (p->M == 0) return hip_check(hipMemsetAsync(out, 0, n_out * sizeof(float), st), __func__);
+  if (p->M == 0) return hip_check(hipMemsetAsync(out, 0, n_out * sizeof(float), st), __fn);
   TNArgs a{};
   a.M = p->M; a.Nr = (int32_t)p->Nr;
   a.g = p->g; a.ldg = p->ldg; a.dz = p->dz; a.lddz = p->lddz; a.proj = p->proj; a.nproj = nproj;
@@ -872,14 +887,14 @@ extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, v
   a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16;
   a.h_bf16 = p->h_dtype == GNN_DTYPE_BF16;
   if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->h_dtype != GNN_DTYPE_F32 && p->h_dtype != GNN_DTYPE_BF16))
-    return fail(GNN_ERR_INVALID_ARG, __func__, "bad dtype");
-  if (a.h_bf16 && !a.a_bf16) return fail(GNN_ERR_UNSUPPORTED, __func__, "bf16 h needs bf16 A");
+    return fail(GNN_ERR_INVALID_ARG, __fn, "bad dtype");
+  if (a.h_bf16 && !a.a_bf16) return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 h needs bf16 A");
   // the split kernel indexes rows with 32-bit element offsets
   const int64_t ldmax = std::max({a.lda1, a.k2 > 0 ? a.lda2 : 0, a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
   if (a.a_bf16 && (p->math == GNN_MATH_F32 || (a.M + 32) * ldmax >= ((int64_t)1 << 31)))
-    return fail(GNN_ERR_UNSUPPORTED, __func__, "bf16 TN needs split math and M*ld < 2^31");
+    return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 TN needs split math and M*ld < 2^31");
   if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31)) {
-    launch_tn_x3(a, nblk, st);  // split-bf16 MFMA (gemm_x3.hip)
+    launch_tn_x3(a, nblk, st, variant);  // split-bf16 MFMA (gemm_x3.hip)
     GNN_LAUNCH_CHECK();
     slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
     GNN_LAUNCH_CHECK();

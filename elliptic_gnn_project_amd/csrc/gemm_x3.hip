@@ -484,15 +484,20 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   const int fr = (lane & 31) * TP + 8 * (lane >> 5);
   auto compute = [&](int c) {
     const int buf = c & 1;
-    bf16x8 gf[NPL];
+    // software-pipelined: tile t+1's fragments are read before tile t's MFMAs issue, so with one
+    // wave per SIMD the LDS latency hides behind the MFMAs instead of stalling every tile
+    bf16x8 gf[NPL], af[2][NPL];
 #pragma unroll
     for (int p = 0; p < NPL; ++p) gf[p] = lds_frag(Gt[buf] + p * TGPL + ntile * 32 * TP + fr);
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      bf16x8 af[NPL];
+    for (int p = 0; p < NPL; ++p) af[0][p] = lds_frag(At[buf] + p * TAPL + fr);
 #pragma unroll
-      for (int p = 0; p < NPL; ++p) af[p] = lds_frag(At[buf] + p * TAPL + t * 32 * TP + fr);
-      acc[t] = mfma_planes<NPL>(gf, af, acc[t]);
+    for (int t = 0; t < KT; ++t) {
+      if (t + 1 < KT) {
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) af[(t + 1) & 1][p] = lds_frag(At[buf] + p * TAPL + (t + 1) * 32 * TP + fr);
+      }
+      acc[t] = mfma_planes<NPL>(gf, af[t & 1], acc[t]);
     }
   };
 
@@ -561,9 +566,236 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
     slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
 }
 
+// ----------------------------------------------------------------- TN, 32-row chunks ("x3b")
+// Same roles and split as gemm_tn_x3_kernel, but 32 rows (two MFMA k-steps) per chunk through a
+// single LDS image with two barriers per chunk: the next chunk's loads (one register stage) have
+// a whole chunk of MFMAs (2 x KT x 6 per wave) to land, instead of the 16-row kernel's single
+// k-step — the 16-row kernel waits on HBM latency every chunk.  Slots: 6 A units (u = tid +
+// 256·s < 4·KP: column u mod KP, rows 8·(u / KP) ..) and 2 G units (column tid mod 128, rows
+// 8·(tid / 128 + 2s) ..) per thread.  dz staged one chunk ahead into a 2-slot LDS ring.
+constexpr int TB_MC = 32;
+constexpr int TB_P = TB_MC + 8;     // 20 dwords: conflict-free b128 reads and writes
+constexpr int TB_GPL = 128 * TB_P;
+constexpr int TB_APL = KMAX * TB_P;
+constexpr int TB_AS = 6;
+constexpr int TB_GS = 2;
+
+template <bool PROJ, bool MASK, int KT, int NPL = 3, bool ABF = false, bool HBF = false>
+__global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3b_kernel(TNArgs a) {
+  constexpr bool GX = !PROJ && MASK;         // g form with mask: an extra g slot per G unit
+  constexpr int NS = TB_AS + TB_GS * (GX ? 2 : 1);
+  __shared__ __attribute__((aligned(16))) uint16_t Gt[NPL * TB_GPL];
+  __shared__ __attribute__((aligned(16))) uint16_t At[NPL * TB_APL];
+  __shared__ float Ps[MAXPROJ * 128];
+  __shared__ float dzL[2][TB_MC * MAXPROJ];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int ntile = tid >> 6;
+  const int Kc = a.k1 + a.k2;
+  const int nkt = (Kc + 31) / 32;
+  const int KP = nkt * 32;
+  const int64_t mbeg = (int64_t)blockIdx.x * a.rows_per_block;
+  const int64_t mend = min(a.M, mbeg + a.rows_per_block);
+  const int nch = mend > mbeg ? (int)((mend - mbeg + TB_MC - 1) / TB_MC) : 0;
+
+  floatx16 acc[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+
+  if constexpr (PROJ) {
+    if (tid < 128) {
+#pragma unroll
+      for (int q = 0; q < MAXPROJ; ++q) Ps[q * 128 + tid] = (q < a.nproj && tid < a.Nr) ? a.proj[q * a.Nr + tid] : 0.0f;
+    }
+  }
+
+  const int gn = tid & 127;
+  const bool gcol = gn < a.Nr;
+  const int gnc = gcol ? gn : 0;
+  const float* base[NS];
+  int ld32[NS];
+  int oct[NS];
+  int ak[TB_AS];
+  bool aon[TB_AS];
+#pragma unroll
+  for (int sl = 0; sl < TB_AS; ++sl) {
+    const int u = tid + TX_THREADS * sl;
+    aon[sl] = u < 4 * KP;
+    ak[sl] = u % KP;
+    oct[sl] = u / KP;
+    const int k = ak[sl];
+    if (aon[sl] && k < a.k1) { base[sl] = elem_ptr<ABF>(a.a1, k); ld32[sl] = (int)a.lda1; }
+    else if (aon[sl] && k < Kc) { base[sl] = elem_ptr<ABF>(a.a2, k - a.k1); ld32[sl] = (int)a.lda2; }
+    else { base[sl] = a.a1; ld32[sl] = 0; oct[sl] = 0; }
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < TB_GS; ++s2) {
+    const int sl = TB_AS + s2;
+    if constexpr (MASK) { base[sl] = elem_ptr<HBF>(a.h, gnc); ld32[sl] = (int)a.ldh; }
+    else { base[sl] = a.g + gnc; ld32[sl] = (int)a.ldg; }
+    oct[sl] = (tid >> 7) + 2 * s2;
+    if constexpr (GX) { base[sl + TB_GS] = a.g + gnc; ld32[sl + TB_GS] = (int)a.ldg; oct[sl + TB_GS] = oct[sl]; }
+  }
+  const int zr = (tid & 127) / MAXPROJ, zq = (tid & 127) % MAXPROJ;  // dz element (threads 0..127)
+  const int zqc = PROJ ? min(zq, a.nproj - 1) : 0;
+  const int mlast = (int)(mend - 1);
+
+  float rv[NS][8];
+  float rz = 0.f;
+  auto load = [&](int c) {
+    const int m0 = (int)mbeg + c * TB_MC;
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = min(m0 + 8 * oct[sl] + i, mlast);
+        const uint32_t off = (uint32_t)(m * ld32[sl]);
+        const bool bf = sl < TB_AS ? ABF : (sl < TB_AS + TB_GS && MASK ? HBF : false);
+        rv[sl][i] = bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(base[sl])[off]) : base[sl][off];
+      }
+    if constexpr (PROJ) {  // dz rows of chunk c + 1
+      const int m = min(m0 + TB_MC + zr, mlast);
+      rz = a.dz[(uint32_t)(m * (int)a.lddz + zqc)];
+    }
+  };
+
+  float db = 0.f, dzs = 0.f;
+  float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
+  auto put8 = [](uint16_t* dst, int plane, const float (&e)[8]) {
+    uint32_t w[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_pair(e[2 * j], e[2 * j + 1], w[j]);
+#pragma unroll
+    for (int p = 0; p < NPL; ++p)
+      *reinterpret_cast<uint4*>(dst + p * plane) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+  };
+  auto store = [&](int c) {
+    const int64_t m0 = mbeg + (int64_t)c * TB_MC;
+    if constexpr (PROJ) {
+      if (tid < TB_MC * MAXPROJ) {
+        const bool ok = zq < a.nproj && m0 + TB_MC + zr < mend;
+        dzL[(c + 1) & 1][tid] = ok ? rz : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < TB_AS; ++sl) {
+      if (aon[sl]) {
+        float e[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = (ak[sl] < Kc && m0 + 8 * oct[sl] + i < mend) ? rv[sl][i] : 0.0f;
+        put8(At + ak[sl] * TB_P + 8 * oct[sl], TB_APL, e);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < TB_GS; ++s2) {
+      const int sl = TB_AS + s2;
+      float e[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = 8 * oct[sl] + i;
+        const bool rok = m0 + r < mend;
+        const bool ok = rok && gcol;
+        float g;
+        if constexpr (PROJ) {
+          const float* z = &dzL[c & 1][r * MAXPROJ];
+          g = z[0] * Ps[gn];
+#pragma unroll
+          for (int q = 1; q < MAXPROJ; ++q) g = fmaf(z[q], Ps[q * 128 + gn], g);
+          if constexpr (MASK) {
+#pragma unroll
+            for (int q = 0; q < MAXPROJ; ++q) dw2[q] = fmaf(ok ? z[q] : 0.0f, rv[sl][i], dw2[q]);
+          }
+          if (gn < MAXPROJ) dzs += rok ? z[gn] : 0.0f;
+        } else {
+          g = GX ? rv[sl + TB_GS][i] : rv[sl][i];
+        }
+        if constexpr (MASK) g = rv[sl][i] > 0.0f ? g * a.hscale : 0.0f;
+        g = ok ? g : 0.0f;
+        db += g;
+        if (a.gout && ok) a.gout[(m0 + r) * a.ldgout + gn] = g;
+        e[i] = g;
+      }
+      put8(Gt + gn * TB_P + 8 * oct[sl], TB_GPL, e);
+    }
+  };
+
+  const int fr = (lane & 31) * TB_P + 8 * (lane >> 5);
+  auto compute = [&]() {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {  // software-pipelined as in gemm_tn_x3_kernel
+      bf16x8 gf[NPL], af[2][NPL];
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) gf[p] = lds_frag(Gt + p * TB_GPL + ntile * 32 * TB_P + fr + 16 * s);
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) af[0][p] = lds_frag(At + p * TB_APL + fr + 16 * s);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        if (t + 1 < KT) {
+#pragma unroll
+          for (int p = 0; p < NPL; ++p)
+            af[(t + 1) & 1][p] = lds_frag(At + p * TB_APL + (t + 1) * 32 * TB_P + fr + 16 * s);
+        }
+        acc[t] = mfma_planes<NPL>(gf, af[t & 1], acc[t]);
+      }
+    }
+  };
+
+  if (nch > 0) {
+    if constexpr (PROJ) {
+      if (tid < TB_MC * MAXPROJ) {
+        const int64_t m = mbeg + zr;
+        dzL[0][tid] = (zq < a.nproj && m < mend) ? a.dz[m * a.lddz + zqc] : 0.0f;
+      }
+    }
+    load(0);
+    __syncthreads();  // Ps, dzL[0]
+    store(0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      load(min(c + 1, nch - 1));  // unconditional: in flight across this chunk's MFMAs
+      compute();
+      __syncthreads();            // every wave is done with the image
+      if (c + 1 < nch) store(c + 1);
+      __syncthreads();
+    }
+  }
+
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    if (t >= nkt) continue;
+    const int col = t * 32 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int64_t idx = col < a.k1 ? (int64_t)row * a.k1 + col
+                                     : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (col - a.k1);
+      if (row < a.Nr && col < Kc) slab[idx] = acc[t][r];
+    }
+  }
+  float* red = reinterpret_cast<float*>(At);
+  constexpr int ns = 2 + MAXPROJ;
+  const int go = tid >> 7;
+  __syncthreads();
+  red[(go * 128 + gn) * ns + 0] = db;
+  red[(go * 128 + gn) * ns + 1] = dzs;
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
+  __syncthreads();
+  if (tid < 128 && tid < a.Nr) {
+    float* side = slab + (int64_t)a.Nr * Kc;
+    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
+    for (int q = 0; q < a.nproj; ++q)
+      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+  }
+  if (PROJ && tid < a.nproj)
+    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+}
+
 }  // namespace
 
-// variant: 0 = production; others are lab tilings (bench_gemm.cpp).
 size_t nt_x3_workspace(int64_t k1, int64_t k2) {  // pre-split B image, 12 KB per 16-deep chunk
   return (size_t)((k1 + 15) / 16 + (k2 + 15) / 16) * 3 * 256 * sizeof(uint4);
 }
@@ -626,18 +858,42 @@ void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
   else gemm_tn_x3_kernel<false, false, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
 }
 
-void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st) {
+template <int KT, int NPL = 3, bool ABF = false, bool HBF = false>
+void launch_tn_x3b_k(const TNArgs& a, int nblk, hipStream_t st) {
+  const bool proj = a.dz != nullptr, mask = a.h != nullptr;
+  if (proj && mask) gemm_tn_x3b_kernel<true, true, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (proj) gemm_tn_x3b_kernel<true, false, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (mask) gemm_tn_x3b_kernel<false, true, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
+  else gemm_tn_x3b_kernel<false, false, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
+}
+
+// variant 0: 16-row chunks (x3, production); 1: 32-row chunks (x3b).  Lab (MI355X, Elliptic layer-1
+// TN): x3 206-212 us, x3b 224-227 us; both VALU-bound in the staging (PMC: ~10 VALU per MFMA,
+// MFMA busy 25 %), see DESIGN.md §4.
+void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
   constexpr int D = 1;
-  if (a.a_bf16) {  // bf16 storage (A and h bf16; G rounded to bf16): one product per MFMA
-    if (nkt <= 8) { if (a.h_bf16) launch_tn_x3_k<D, 8, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 8, 1, true, false>(a, nblk, st); }
-    else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false>(a, nblk, st); }
+  if (variant == 0) {
+    if (a.a_bf16) {
+      if (nkt <= 8) { if (a.h_bf16) launch_tn_x3_k<D, 8, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 8, 1, true, false>(a, nblk, st); }
+      else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false>(a, nblk, st); }
+      return;
+    }
+    if (nkt <= 6) launch_tn_x3_k<D, 6>(a, nblk, st);
+    else if (nkt <= 8) launch_tn_x3_k<D, 8>(a, nblk, st);
+    else if (nkt <= 11) launch_tn_x3_k<D, 11>(a, nblk, st);
+    else launch_tn_x3_k<D, 12>(a, nblk, st);
     return;
   }
-  if (nkt <= 6) launch_tn_x3_k<D, 6>(a, nblk, st);
-  else if (nkt <= 8) launch_tn_x3_k<D, 8>(a, nblk, st);
-  else if (nkt <= 11) launch_tn_x3_k<D, 11>(a, nblk, st);
-  else launch_tn_x3_k<D, 12>(a, nblk, st);
+  if (a.a_bf16) {
+    if (nkt <= 8) { if (a.h_bf16) launch_tn_x3b_k<8, 1, true, true>(a, nblk, st); else launch_tn_x3b_k<8, 1, true, false>(a, nblk, st); }
+    else { if (a.h_bf16) launch_tn_x3b_k<12, 1, true, true>(a, nblk, st); else launch_tn_x3b_k<12, 1, true, false>(a, nblk, st); }
+    return;
+  }
+  if (nkt <= 6) launch_tn_x3b_k<6>(a, nblk, st);
+  else if (nkt <= 8) launch_tn_x3b_k<8>(a, nblk, st);
+  else if (nkt <= 11) launch_tn_x3b_k<11>(a, nblk, st);
+  else launch_tn_x3b_k<12>(a, nblk, st);
 }
 
 }  // namespace gnnmp

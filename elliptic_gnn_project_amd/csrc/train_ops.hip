@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const float* __restri
 
 // ---------------------------------------------------------------------------- clip + Adam
 constexpr int kAdamThreads = 256;
-constexpr int kAdamBlocks = 64;
+constexpr int kAdamBlocks = 64;  // <= 64: clip_adam_kernel reduces the partials with one wave
 
 struct AdamTable {
   int32_t n;
@@ -125,14 +125,16 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
                                                                   double beta2, double eps, double wd,
                                                                   float* __restrict__ norm_out) {
   __shared__ float coef_sh;
-  if (threadIdx.x == 0) {
-    float tot = 0.f;
-    for (int i = 0; i < nblk; ++i) tot += partial[i];  // same fixed order in every block
+  if (threadIdx.x < 64) {  // the nblk <= 64 partials: one per lane, fixed butterfly (same in every block)
+    float tot = threadIdx.x < nblk ? partial[threadIdx.x] : 0.f;
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
     const float norm = sqrtf(tot);
     float coef = 1.0f;
     if (max_norm > 0.0) coef = fminf((float)max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
-    coef_sh = coef;
-    if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+    if (threadIdx.x == 0) {
+      coef_sh = coef;
+      if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+    }
   }
   __syncthreads();
   const float coef = coef_sh;

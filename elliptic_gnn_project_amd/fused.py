@@ -190,6 +190,7 @@ class _FusedSAGE(torch.autograd.Function):
         logits = aggregate(plan, z[:, :C], _lib.AGG_MEAN, nodew=plan.deg, addend=z[:, C:], bias=bl[-1])
         ctx.plan = plan
         ctx.meta = (L, C, float(dropout_p))
+        ctx.P = P  # the output layer's stacked weights, reused by the backward (no second cat)
         ctx.save_for_backward(*hs, *aggs, *params)
         return logits
 
@@ -209,7 +210,7 @@ class _FusedSAGE(torch.autograd.Function):
         dz = torch.empty((N, 2 * C), dtype=torch.float32, device=dlogits.device)
         aggregate(plan, dlogits, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dz[:, :C])
         dz[:, C:].copy_(dlogits)
-        P = torch.cat([Wl[-1], Wr[-1]], dim=0).contiguous()
+        P = ctx.P
         grads = [None] * (3 * L)
         need_x = ctx.needs_input_grad[0]
         g = None
