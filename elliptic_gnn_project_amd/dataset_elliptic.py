@@ -174,3 +174,109 @@ def save_graph(path: str, data: GraphData) -> None:
 def load_graph(path: str) -> GraphData:
     with np.load(path, allow_pickle=False) as z:
         return GraphData(**{k: torch.from_numpy(z[k]) for k in z.files})
+
+
+# ----------------------------------------------------------------------------- CSV ingest
+_LABELS = {"class1": 1, "1": 1, "illicit": 1, "class2": 0, "2": 0, "licit": 0, "unknown": -1, "-1": -1}
+
+
+def _label(v) -> int:
+    """Elliptic class string/number -> 1 illicit, 0 licit, -1 unknown (dataset_elliptic.py:12-29)."""
+    return _LABELS.get(str(v).strip().lower(), -1)
+
+
+def _is_timestep_column(col) -> bool:
+    """Integers in [1, 49] (>95 % integral): the Elliptic time index (dataset_elliptic.py:32-46)."""
+    import pandas as pd
+
+    v = pd.to_numeric(col, errors="coerce").dropna().astype(float)
+    return (not v.empty) and v.min() >= 1 and v.max() <= 49 and bool((v.round() == v).mean() > 0.95)
+
+
+def load_elliptic_csv(data_dir: str, features_csv: str = "elliptic_txs_features.csv",
+                      classes_csv: str = "elliptic_txs_classes.csv",
+                      edgelist_csv: str = "elliptic_txs_edgelist.csv") -> GraphData:
+    """Elliptic CSVs -> GraphData(x, edge_index, y, timestep): the reference's
+    load_elliptic_as_graph (src/data/dataset_elliptic.py:49-265), without PyG.
+
+    Nodes in features-CSV row order (a left join keeps it, :163); features = every column after
+    txId, minus column 1 when it looks like the timestep (:113-140); timestep from classes.csv
+    ('time_step' / 'timestep') when present, else from features column 1 (:142-156); labels via
+    the class map, -1 when missing (:182-186); edges from 'txId1,txId2' or a headerless list, in
+    file order, endpoints mapped to rows, unknown txIds dropped, and only same-timestep edges
+    kept (:201-245).  Vectorised (pandas / numpy) instead of per-edge dict lookups.
+    """
+    import os
+
+    import pandas as pd
+
+    cls = pd.read_csv(os.path.join(data_dir, classes_csv))
+    cls.columns = [c.strip() for c in cls.columns]
+    if "txId" not in cls.columns:
+        tx = next((c for c in cls.columns if c.lower().startswith("tx")), None)
+        if tx is not None:
+            cls = cls.rename(columns={tx: "txId"})
+    if "time_step" in cls.columns:
+        cls = cls.rename(columns={"time_step": "timestep"})
+    cls_ts = "timestep" in cls.columns
+    if "class" not in cls.columns:
+        cc = next((c for c in cls.columns if c.lower().startswith("class")), None)
+        if cc is not None:
+            cls = cls.rename(columns={cc: "class"})
+    cls["txId"] = pd.to_numeric(cls["txId"], errors="raise").astype(np.int64)
+    cls["label"] = cls["class"].map(_label).astype(np.int64)
+    keep = ["txId", "label"] + (["timestep"] if cls_ts else [])
+    cls = cls[keep]
+    if cls_ts:
+        cls["timestep"] = pd.to_numeric(cls["timestep"], errors="raise").astype(np.int64)
+
+    feat = pd.read_csv(os.path.join(data_dir, features_csv), header=None)
+    if feat.shape[1] < 2:
+        raise ValueError("features CSV appears malformed (needs at least txId + 1 column).")
+    tx_ids = pd.to_numeric(feat.iloc[:, 0], errors="raise").astype(np.int64).to_numpy()
+    feat_ts = _is_timestep_column(feat.iloc[:, 1])
+    x = feat.iloc[:, 2:] if feat_ts else feat.iloc[:, 1:]
+    x = torch.tensor(x.to_numpy(dtype=np.float32))
+
+    nodes = pd.DataFrame({"txId": tx_ids})
+    if feat_ts:
+        nodes["ts_feat"] = pd.to_numeric(feat.iloc[:, 1], errors="raise").astype(np.int64).to_numpy()
+    nodes = nodes.merge(cls, on="txId", how="left")  # left join: features row order
+    if cls_ts:
+        ts = nodes["timestep"]
+    elif feat_ts:
+        ts = nodes["ts_feat"]
+    else:
+        raise ValueError("No timestep column found in classes and features did not contain a valid timestep "
+                         "column (expected classes 'time_step'/'timestep' or features column 2 in 1..49).")
+    if ts.isna().any():
+        raise ValueError("timestep missing for some nodes")
+    y = torch.tensor(nodes["label"].fillna(-1).astype(np.int64).to_numpy())
+    timestep = torch.tensor(ts.astype(np.int64).to_numpy())
+
+    epath = os.path.join(data_dir, edgelist_csv)
+    sniff = pd.read_csv(epath, nrows=5)
+    header = sniff.shape[1] >= 2 and not np.issubdtype(sniff.dtypes.iloc[0], np.number)
+    edges = pd.read_csv(epath, header=0 if header else None)
+    if {"txId1", "txId2"}.issubset(edges.columns):
+        edges = edges[["txId1", "txId2"]]
+    edges = edges.iloc[:, :2].apply(pd.to_numeric, errors="coerce").dropna().astype(np.int64).to_numpy()
+    # txId -> row (the last occurrence, as the reference's dict comprehension), unknown ids dropped,
+    # same-timestep edges only, file order kept
+    order = np.argsort(tx_ids, kind="stable")
+    sorted_ids = tx_ids[order]
+
+    def rows_of(ids):
+        pos = np.searchsorted(sorted_ids, ids, side="right") - 1
+        pos_c = np.maximum(pos, 0)
+        ok = (pos >= 0) & (sorted_ids[pos_c] == ids) if len(sorted_ids) else np.zeros(len(ids), bool)
+        return order[pos_c], ok
+
+    src, ok_s = rows_of(edges[:, 0]) if len(edges) else (np.zeros(0, np.int64), np.zeros(0, bool))
+    dst, ok_d = rows_of(edges[:, 1]) if len(edges) else (np.zeros(0, np.int64), np.zeros(0, bool))
+    keep_e = ok_s & ok_d
+    src, dst = src[keep_e], dst[keep_e]
+    tnp = timestep.numpy()
+    same = tnp[src] == tnp[dst]
+    edge_index = torch.tensor(np.stack([src[same], dst[same]]).astype(np.int64))
+    return GraphData(x=x, edge_index=edge_index, y=y, timestep=timestep)

@@ -225,40 +225,35 @@ def eval_split(model, data, edge_index, mask):
 
 
 # ----------------------------------------------------------------------------- metrics (src/utils/metrics.py)
-def pr_auc_illicit(y_true, y_score) -> float:
-    from sklearn.metrics import average_precision_score
-    return float(average_precision_score(y_true, y_score))
+from .metrics import pr_auc_illicit  # noqa: E402  (src/utils/metrics.py restated)
 
 
 def _metrics(y_bin, p, thr, cfg) -> Dict:
-    from sklearn.metrics import f1_score, precision_recall_curve, roc_auc_score
+    """Test-split metrics of main (src/train_gnn.py:466-519) via metrics.py."""
+    from . import metrics as M
 
-    prec, rec, _ = precision_recall_curve(y_bin, p)
-    tp = cfg.get("precision_target", 0.90)
-    m = prec >= tp
     k = cfg.get("topk", 100)
-    idx = np.argsort(-p)[:k]
+    two = len(np.unique(y_bin)) > 1
     return dict(
-        pr_auc_illicit=pr_auc_illicit(y_bin, p),
-        roc_auc=float(roc_auc_score(y_bin, p)) if len(np.unique(y_bin)) > 1 else float("nan"),
-        f1_illicit_at_thr=float(f1_score(y_bin, (p >= thr).astype(int))),
+        pr_auc_illicit=M.pr_auc_illicit(y_bin, p),
+        roc_auc=M.roc_auc_illicit(y_bin, p) if two else float("nan"),
+        f1_illicit_at_thr=M.f1_at_threshold(y_bin, p, thr),
         threshold=float(thr),
-        precision_at_k=float(np.mean(y_bin[idx])) if len(idx) else 0.0,
-        recall_at_precision=float(np.max(rec[m])) if np.any(m) else 0.0,
+        precision_at_k=M.precision_at_k(y_bin, p, k) if len(p) else 0.0,
+        recall_at_precision=M.recall_at_precision(y_bin, p, cfg.get("precision_target", 0.90)),
+        ece=M.expected_calibration_error(y_bin, p),
         n_test=int(len(y_bin)),
     )
 
 
 def _threshold(y_bin, p, cfg) -> float:
-    from sklearn.metrics import precision_recall_curve
+    """Decision threshold (src/train_gnn.py:466-483): precision target if set, else max F1."""
+    from . import metrics as M
 
-    prec, rec, thr = precision_recall_curve(y_bin, p)
-    thr = np.append(thr, 1.0)
     target = cfg.get("precision_target", 0.0)
-    if target and target > 0 and np.any(prec >= target):
-        return float(thr[np.argmax(prec >= target)])
-    f1 = 2 * prec * rec / (prec + rec + 1e-12)
-    return float(thr[np.nanargmax(f1)])
+    if target and target > 0:
+        return M.pick_threshold_for_precision(y_bin, p, target)
+    return M.pick_threshold_max_f1(y_bin, p)[0]
 
 
 # ----------------------------------------------------------------------------- data
