@@ -99,7 +99,7 @@ int main(int argc, char** argv) {
   gnn_gemm_nt_params plain = p;
   plain.bias = nullptr; plain.relu = 0; plain.dropout_p = 0.f; plain.proj = nullptr; plain.nproj = 0; plain.z = nullptr;
 
-  if (const char* tn = std::getenv("LAB_TN_ONLY")) {  // one TN variant only (PMC passes): 0 = x3, 1 = x3b
+  if (const char* tn = std::getenv("LAB_TN_ONLY")) {  // one TN variant only (PMC passes): 0 = x3, 2 = x3b
     GK(gnnx_gemm_nt_variant_f32(&p, 16, nullptr));
     gnn_gemm_tn_params q{};
     q.M = M; q.Nr = H; q.dz = dz; q.lddz = 4; q.proj = proj; q.nproj = 4; q.h = c; q.ldh = H; q.hscale = 2.f;
@@ -202,7 +202,7 @@ int main(int argc, char** argv) {
     }
     for (int math : {1, 0, 2}) {  // 2: split-bf16 with the 32-row-chunk kernel (variant 1)
       qc.math = math == 2 ? 0 : math;
-      GK(gnnx_gemm_tn_variant_f32(&qc, out, ws, wsb, math == 2 ? 1 : 0, nullptr));
+      GK(gnnx_gemm_tn_variant_f32(&qc, out, ws, wsb, math == 2 ? 2 : 0, nullptr));
       auto got = to_host(out, nout);
       double se = 0, sr = 0, mx = 0, rmx = 0;
       for (int64_t i = 0; i < H * 2 * F; ++i) {
@@ -219,7 +219,7 @@ int main(int argc, char** argv) {
     q.math = math == 2 ? 0 : math;
     std::vector<float> tt;
     for (int r = 0; r < rounds; ++r)
-      tt.push_back(T.run([&] { gnnx_gemm_tn_variant_f32(&q, out, ws, wsb, math == 2 ? 1 : 0, nullptr); }, 5));
+      tt.push_back(T.run([&] { gnnx_gemm_tn_variant_f32(&q, out, ws, wsb, math == 2 ? 2 : 0, nullptr); }, 5));
     std::printf("TN dz+mask math=%d: %8.1f us (%6.1f TF)\n", math, med(tt), flops / med(tt) * 1e-6);
   }
   return 0;

@@ -867,13 +867,14 @@ void launch_tn_x3b_k(const TNArgs& a, int nblk, hipStream_t st) {
   else gemm_tn_x3b_kernel<false, false, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
 }
 
-// variant 0: 16-row chunks (x3, production); 1: 32-row chunks (x3b).  Lab (MI355X, Elliptic layer-1
-// TN): x3 206-212 us, x3b 224-227 us; both VALU-bound in the staging (PMC: ~10 VALU per MFMA,
-// MFMA busy 25 %), see DESIGN.md §4.
+// variant 0 / 1: 16-row chunks (x3, production); 2: 32-row chunks (x3b).  Lab (MI355X, Elliptic
+// layer-1 TN): x3 206-212 us, x3b 224-227 us — both VALU-bound in a staging phase separate from
+// the MFMAs (PMC: ~10 VALU per MFMA, MFMA busy 25 %).  A two-register-set form that interleaves
+// the staging with the MFMAs spilled (the compiler keeps both sets' addresses live), see DESIGN.md.
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
   constexpr int D = 1;
-  if (variant == 0) {
+  if (variant <= 1) {
     if (a.a_bf16) {
       if (nkt <= 8) { if (a.h_bf16) launch_tn_x3_k<D, 8, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 8, 1, true, false>(a, nblk, st); }
       else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false>(a, nblk, st); }
@@ -885,15 +886,18 @@ void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
     else launch_tn_x3_k<D, 12>(a, nblk, st);
     return;
   }
-  if (a.a_bf16) {
-    if (nkt <= 8) { if (a.h_bf16) launch_tn_x3b_k<8, 1, true, true>(a, nblk, st); else launch_tn_x3b_k<8, 1, true, false>(a, nblk, st); }
-    else { if (a.h_bf16) launch_tn_x3b_k<12, 1, true, true>(a, nblk, st); else launch_tn_x3b_k<12, 1, true, false>(a, nblk, st); }
+  if (variant == 2) {
+    if (a.a_bf16) {
+      if (nkt <= 8) { if (a.h_bf16) launch_tn_x3b_k<8, 1, true, true>(a, nblk, st); else launch_tn_x3b_k<8, 1, true, false>(a, nblk, st); }
+      else { if (a.h_bf16) launch_tn_x3b_k<12, 1, true, true>(a, nblk, st); else launch_tn_x3b_k<12, 1, true, false>(a, nblk, st); }
+      return;
+    }
+    if (nkt <= 6) launch_tn_x3b_k<6>(a, nblk, st);
+    else if (nkt <= 8) launch_tn_x3b_k<8>(a, nblk, st);
+    else if (nkt <= 11) launch_tn_x3b_k<11>(a, nblk, st);
+    else launch_tn_x3b_k<12>(a, nblk, st);
     return;
   }
-  if (nkt <= 6) launch_tn_x3b_k<6>(a, nblk, st);
-  else if (nkt <= 8) launch_tn_x3b_k<8>(a, nblk, st);
-  else if (nkt <= 11) launch_tn_x3b_k<11>(a, nblk, st);
-  else launch_tn_x3b_k<12>(a, nblk, st);
 }
 
 }  // namespace gnnmp
