@@ -172,7 +172,7 @@ def gemm_floor(tag):
     (one product: 2.5 PF) or exact f32 (157.3 TF)."""
     kind, M, K, N, ea, ec, prod = tag
     byts = M * K * ea + M * N * ec
-    peak = MFMA_F32_PEAK_TFS if prod == 0 else BF16_MFMA_PEAK_TFS / prod
+    peak = MFMA_F32_PEAK_TFS if prod <= 0 else BF16_MFMA_PEAK_TFS / prod  # VALU f32 peak = MFMA f32
     return byts, byts / (HBM_PEAK_GBS * 1e9), 2.0 * M * K * N / (peak * 1e12), peak
 
 
@@ -191,7 +191,7 @@ def roofline(recs):
             return f"{tag[0]}[{names[tag[1]]},{'csc' if tag[2] else 'csr'},F={tag[3]}]"
         if tag[0].startswith("gat"):
             return f"{tag[0]}[H={tag[1]},C={tag[2]},out={tag[3]}]"
-        math = {0: "f32", 1: "bf16", 6: "split-bf16"}[tag[6]]
+        math = {-1: "valu-f32", 0: "f32", 1: "bf16", 6: "split-bf16"}[tag[6]]
         return f"{tag[0]}[M={tag[1]},K={tag[2]},N={tag[3]},{math}]"
 
     if not recs:

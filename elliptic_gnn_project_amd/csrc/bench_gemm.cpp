@@ -96,6 +96,8 @@ int main(int argc, char** argv) {
   GK(gnn_gemm_nt_workspace_size(H, F, F, &ntws));
   CK(hipMalloc(&p.workspace, ntws));
   p.workspace_bytes = ntws;
+  if (std::getenv("LAB_NOPROJ")) { p.proj = nullptr; p.nproj = 0; p.z = nullptr; }
+  if (std::getenv("LAB_NODROP")) p.dropout_p = 0.f;
   gnn_gemm_nt_params plain = p;
   plain.bias = nullptr; plain.relu = 0; plain.dropout_p = 0.f; plain.proj = nullptr; plain.nproj = 0; plain.z = nullptr;
 
@@ -116,7 +118,15 @@ int main(int argc, char** argv) {
     return 0;
   }
   // ---- NT accuracy vs float64 on sampled rows (plain GEMM)
-  const std::vector<int> variants = {0, 16};  // <16: split-bf16 tilings; >=16: exact f32
+  std::vector<int> variants = {0, 1, 2, 16};  // 0 production, 1/2 pipelined orders, >=16: exact f32
+  if (const char* vs = std::getenv("LAB_NT_VARIANTS")) {  // e.g. "0,6,7,8,9"
+    variants.clear();
+    for (const char* q = vs; *q;) {
+      variants.push_back(std::atoi(q));
+      while (*q && *q != ',') ++q;
+      if (*q == ',') ++q;
+    }
+  }
   std::vector<int64_t> rows;
   for (int64_t r = 0; r < M; r += std::max<int64_t>(1, M / 3000)) rows.push_back(r);
   rows.push_back(M - 1);
@@ -153,15 +163,21 @@ int main(int argc, char** argv) {
   }
   const double flops = 2.0 * M * (2 * F) * H;
   Timer T;
+  // rounds interleave the variants (after one untimed warm-up pass), so clock ramp and thermal
+  // drift do not favour whichever variant is measured last
+  std::vector<std::vector<float>> te(variants.size()), tp(variants.size());
   for (int v : variants) {
-    std::vector<float> te, tp;
-    for (int r = 0; r < rounds; ++r) {
-      te.push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&p, v, nullptr); }, 5));
-      tp.push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&plain, v, nullptr); }, 5));
-    }
-    std::printf("NT variant %2d: fused-epilogue %8.1f us (%6.1f TF)   plain %8.1f us (%6.1f TF)\n", v, med(te),
-                flops / med(te) * 1e-6, med(tp), flops / med(tp) * 1e-6);
+    T.run([&] { gnnx_gemm_nt_variant_f32(&p, v, nullptr); }, 5);
+    T.run([&] { gnnx_gemm_nt_variant_f32(&plain, v, nullptr); }, 5);
   }
+  for (int r = 0; r < rounds; ++r)
+    for (size_t i = 0; i < variants.size(); ++i) {
+      te[i].push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&p, variants[i], nullptr); }, 5));
+      tp[i].push_back(T.run([&] { gnnx_gemm_nt_variant_f32(&plain, variants[i], nullptr); }, 5));
+    }
+  for (size_t i = 0; i < variants.size(); ++i)
+    std::printf("NT variant %2d: fused-epilogue %8.1f us (%6.1f TF)   plain %8.1f us (%6.1f TF)\n", variants[i],
+                med(te[i]), flops / med(te[i]) * 1e-6, med(tp[i]), flops / med(tp[i]) * 1e-6);
 
   // ---- TN (dz form + mask), the backward weight-gradient shape.  h = NT output (fused epilogue).
   GK(gnnx_gemm_nt_variant_f32(&p, 16, nullptr));
@@ -200,9 +216,9 @@ int main(int argc, char** argv) {
         for (int k = 0; k < F; ++k) rdw[H * F + n * F + k] += g[n] * h_x[m * F + k];
       }
     }
-    for (int math : {1, 0, 2}) {  // 2: split-bf16 with the 32-row-chunk kernel (variant 1)
-      qc.math = math == 2 ? 0 : math;
-      GK(gnnx_gemm_tn_variant_f32(&qc, out, ws, wsb, math == 2 ? 2 : 0, nullptr));
+    for (int math : {1, 0, 3}) {  // 1: exact f32; 0: split-bf16 (production); 3: split-bf16, classic order
+      qc.math = math >= 2 ? 0 : math;
+      GK(gnnx_gemm_tn_variant_f32(&qc, out, ws, wsb, math >= 2 ? math : 0, nullptr));
       auto got = to_host(out, nout);
       double se = 0, sr = 0, mx = 0, rmx = 0;
       for (int64_t i = 0; i < H * 2 * F; ++i) {
@@ -215,12 +231,16 @@ int main(int argc, char** argv) {
                   (long long)Mc, std::sqrt(se / sr), mx, rmx, dbe);
     }
   }
-  for (int math : {1, 0, 2}) {
-    q.math = math == 2 ? 0 : math;
-    std::vector<float> tt;
-    for (int r = 0; r < rounds; ++r)
-      tt.push_back(T.run([&] { gnnx_gemm_tn_variant_f32(&q, out, ws, wsb, math == 2 ? 2 : 0, nullptr); }, 5));
-    std::printf("TN dz+mask math=%d: %8.1f us (%6.1f TF)\n", math, med(tt), flops / med(tt) * 1e-6);
-  }
+  const int tmaths[3] = {1, 0, 3};
+  std::vector<float> tt[3];
+  auto tn_run = [&](int math) {
+    q.math = math >= 2 ? 0 : math;
+    return T.run([&] { gnnx_gemm_tn_variant_f32(&q, out, ws, wsb, math >= 2 ? math : 0, nullptr); }, 5);
+  };
+  for (int m : tmaths) tn_run(m);  // warm-up
+  for (int r = 0; r < rounds; ++r)
+    for (int i = 0; i < 3; ++i) tt[i].push_back(tn_run(tmaths[i]));
+  for (int i = 0; i < 3; ++i)
+    std::printf("TN dz+mask math=%d: %8.1f us (%6.1f TF)\n", tmaths[i], med(tt[i]), flops / med(tt[i]) * 1e-6);
   return 0;
 }

@@ -12,6 +12,10 @@
 // (lane & (H-1), H a power of two <= 64), so per-head max / sum / dot reductions are
 // xor-shuffles over lane offsets >= H — no LDS, no atomics.  Attention weights are
 // recomputed (bit-identically) in the feature pass instead of being re-read.
+#include <algorithm>
+#include <initializer_list>
+#include <utility>
+
 #include "common.hpp"
 
 namespace gnnmp {
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(256) void gat_bwd_cols_kernel(GatArgs a) {
 }
 
 // d att[f] = sum_n dscore[n, h(f)] * xh[n, f]  (two-stage, deterministic)
-constexpr int kAttBlocks = 512;
+constexpr int kAttBlocks = 512;  // generic path partials
 __global__ __launch_bounds__(256) void gat_att_partial_kernel(GatArgs a, int64_t rows_per_blk, float* part) {
   const int F = a.H * a.C;
   int64_t r0 = blockIdx.x * rows_per_blk;
@@ -259,6 +263,335 @@ __global__ void gat_att_final_kernel(int F, int nblk, const float* part, float* 
   d_att_d[f] = sd;
 }
 
+
+// ================================================================ lane-group kernels (fast path)
+// A destination row (forward, rows pass) or source column (cols pass) is owned by a group of
+// G lanes (G a power of two, 4..64), so a wave64 serves 64/G rows at once instead of idling
+// most lanes on Elliptic's ~2-slot rows.  Two lane views of the same group:
+//   pair view:  lane lig walks (slot, head) pairs idx = lig + t*G with head lig & (H-1) fixed
+//               (G % H == 0), so per-head max / sum are xor-shuffles over offsets H..G/2;
+//   slot view:  lane lig owns VEC consecutive features fl*VEC.. (fl = lig & (FLp-1), all of one
+//               head) and walks the slots k = beg + ep, step EP = G/FLp; partial sums over the
+//               EP edge phases are xor-shuffles over offsets FLp..G/2.
+// The softmax statistics of head h live in lane h of the group after the pair-view
+// reduction and reach the slot view through one __shfl (the whole wave participates).
+struct GatGeom {
+  int G, lgG;    // lanes per row/column (slot view and forward pair view)
+  int Gb, lgGb;  // lanes per row in the backward rows pass (pair view only)
+  int lgH;
+  int FL, FLp, lgFLp;  // feature slots of VEC floats, its power-of-two ceiling
+  int L;               // slots per head (C / VEC)
+};
+
+template <int VEC>
+struct VecF { float v[VEC]; };
+
+template <int VEC>
+__device__ __forceinline__ VecF<VEC> ldv(const float* p) {
+  VecF<VEC> r;
+  if constexpr (VEC == 4) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+  } else if constexpr (VEC == 2) {
+    float2 t = *reinterpret_cast<const float2*>(p);
+    r.v[0] = t.x; r.v[1] = t.y;
+  } else {
+    r.v[0] = *p;
+  }
+  return r;
+}
+
+template <int VEC>
+__device__ __forceinline__ void stv(float* p, const VecF<VEC>& r) {
+  if constexpr (VEC == 4) *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+  else if constexpr (VEC == 2) *reinterpret_cast<float2*>(p) = make_float2(r.v[0], r.v[1]);
+  else *p = r.v[0];
+}
+
+// Forward: per-head max and sum of exp in the pair view (the first pair's score kept in a
+// register), alpha written in pair order (contiguous: alpha[beg*H + idx]), then the
+// alpha-weighted gather in the slot view with alpha recomputed bit-identically.
+template <int VEC>
+__global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int H = a.H, C = a.C, G = g.G;
+  const int lig = lane & (G - 1);
+  const int gbase = lane - lig;
+  const int rpw = 64 >> g.lgG;
+  const int hl = lig & (H - 1);
+  const int fl = lig & (g.FLp - 1);
+  const int ep = lig >> g.lgFLp;
+  const int EP = G >> g.lgFLp;
+  const bool slot_ok = fl < g.FL;
+  const int f0 = fl * VEC;
+  const int hs = slot_ok ? f0 / C : 0;
+  const int c0 = f0 - hs * C;
+  const int64_t rpb = 4 * (int64_t)rpw;
+  for (int64_t base = (int64_t)blockIdx.x * rpb; base < a.N; base += (int64_t)gridDim.x * rpb) {
+    const int64_t r = base + wave * rpw + (lane >> g.lgG);
+    const bool valid = r < a.N;
+    int32_t beg = 0, end = 0;
+    if (valid) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
+    const int32_t npair = (end - beg) << g.lgH;
+    const float adr = valid ? a.a_d[r * H + hl] : 0.0f;
+    float e0 = -INFINITY;
+    if (lig < npair) e0 = leaky(a.a_s[(int64_t)a.col[beg + (lig >> g.lgH)] * H + hl] + adr, a.slope);
+    float m = e0;
+    for (int32_t idx = lig + G; idx < npair; idx += G)
+      m = fmaxf(m, leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope));
+    for (int off = G >> 1; off >= H; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    float s = lig < npair ? expf(e0 - m) : 0.0f;
+    for (int32_t idx = lig + G; idx < npair; idx += G)
+      s += expf(leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope) - m);
+    for (int off = G >> 1; off >= H; off >>= 1) s += __shfl_xor(s, off);
+    const float denom = s + 1e-16f;
+    float* alpha_r = a.alpha + (int64_t)beg * H;
+    if (lig < npair) alpha_r[lig] = expf(e0 - m) / denom;
+    for (int32_t idx = lig + G; idx < npair; idx += G)
+      alpha_r[idx] = expf(leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope) - m) / denom;
+    // slot view
+    const float ms = __shfl(m, gbase + hs);
+    const float dn = __shfl(denom, gbase + hs);
+    const float ads = valid ? a.a_d[r * H + hs] : 0.0f;
+    VecF<VEC> acc;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc.v[i] = 0.0f;
+    if (slot_ok) {
+      for (int32_t k = beg + ep; k < end; k += EP) {
+        const int32_t j = a.col[k];
+        const float al = expf(leaky(a.a_s[(int64_t)j * H + hs] + ads, a.slope) - ms) / dn;
+        const VecF<VEC> x = ldv<VEC>(a.xh + (int64_t)j * a.ld_xh + f0);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc.v[i] += al * x.v[i];
+      }
+    }
+    for (int off = G >> 1; off >= g.FLp; off >>= 1) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc.v[i] += __shfl_xor(acc.v[i], off);
+    }
+    if (!a.concat) {  // mean over heads: same channel sits L slots apart (L, H powers of two)
+      for (int off = g.FLp >> 1; off >= g.L; off >>= 1) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc.v[i] += __shfl_xor(acc.v[i], off);
+      }
+    }
+    if (valid && slot_ok && ep == 0) {
+      if (a.concat) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc.v[i] += a.bias ? a.bias[f0 + i] : 0.0f;
+        stv<VEC>(a.out + r * a.ldo + f0, acc);
+      } else if (hs == 0) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc.v[i] = acc.v[i] / (float)H + (a.bias ? a.bias[c0 + i] : 0.0f);
+        stv<VEC>(a.out + r * a.ldo + c0, acc);
+      }
+    }
+  }
+}
+
+// Backward rows pass (pair view, Gb lanes per row): d alpha per (slot, head) as a C-long dot
+// of the row's upstream gradient with the neighbour's features, kept in dz between the two
+// sweeps; then the softmax and leaky-relu backward and d a_dst = sum over the row.
+template <int VEC>
+__global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatGeom g) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int H = a.H, C = a.C, G = g.Gb;
+  const int lig = lane & (G - 1);
+  const int rpw = 64 >> g.lgGb;
+  const int hl = lig & (H - 1);
+  const float inv_h = a.concat ? 1.0f : 1.0f / (float)H;
+  const int64_t rpb = 4 * (int64_t)rpw;
+  for (int64_t base = (int64_t)blockIdx.x * rpb; base < a.N; base += (int64_t)gridDim.x * rpb) {
+    const int64_t r = base + wave * rpw + (lane >> g.lgGb);
+    const bool valid = r < a.N;
+    int32_t beg = 0, end = 0;
+    if (valid) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
+    const int32_t npair = (end - beg) << g.lgH;
+    const float adr = valid ? a.a_d[r * H + hl] : 0.0f;
+    const float* dor = a.dout + r * a.ld_dout + (a.concat ? (int64_t)hl * C : 0);
+    const float* alpha_r = a.alpha + (int64_t)beg * H;
+    float* dz_r = a.dz + (int64_t)beg * H;
+    float t = 0.0f;
+    for (int32_t idx = lig; idx < npair; idx += G) {
+      const int32_t j = a.col[beg + (idx >> g.lgH)];
+      const float* xr = a.xh + (int64_t)j * a.ld_xh + (int64_t)hl * C;
+      float da = 0.0f;
+      for (int c = 0; c < C; c += VEC) {
+        const VecF<VEC> d = ldv<VEC>(dor + c), x = ldv<VEC>(xr + c);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) da += d.v[i] * x.v[i];
+      }
+      da *= inv_h;
+      dz_r[idx] = da;
+      t += alpha_r[idx] * da;
+    }
+    for (int off = G >> 1; off >= H; off >>= 1) t += __shfl_xor(t, off);
+    float sdz = 0.0f;
+    for (int32_t idx = lig; idx < npair; idx += G) {
+      const int32_t j = a.col[beg + (idx >> g.lgH)];
+      const float de = alpha_r[idx] * (dz_r[idx] - t);
+      const float z = a.a_s[(int64_t)j * H + hl] + adr;
+      const float dzv = z > 0.0f ? de : de * a.slope;
+      dz_r[idx] = dzv;
+      sdz += dzv;
+    }
+    for (int off = G >> 1; off >= H; off >>= 1) sdz += __shfl_xor(sdz, off);
+    if (valid && lig < H) a.dad[r * H + lig] = sdz;
+  }
+}
+
+// Backward cols pass (CSC, G lanes per source column): d a_src as the pair-view sum of dz,
+// the transposed alpha-weighted gather of upstream rows in the slot view, the score-path
+// terms, and the attention-vector gradients accumulated in registers across the columns a
+// lane visits (one partial per block; gat_att_reduce_kernel finishes them).
+template <int VEC>
+__global__ __launch_bounds__(256) void gat_bwd_cols_group_kernel(GatArgs a, GatGeom g, float* __restrict__ part) {
+  __shared__ float red[2][4][256];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int H = a.H, C = a.C, G = g.G;
+  const int F = H * C;
+  const int lig = lane & (G - 1);
+  const int gbase = lane - lig;
+  const int rpw = 64 >> g.lgG;
+  const int hl = lig & (H - 1);
+  const int fl = lig & (g.FLp - 1);
+  const int ep = lig >> g.lgFLp;
+  const int EP = G >> g.lgFLp;
+  const bool slot_ok = fl < g.FL;
+  const int f0 = fl * VEC;
+  const int hs = slot_ok ? f0 / C : 0;
+  const int c0 = f0 - hs * C;
+  const float inv_h = a.concat ? 1.0f : 1.0f / (float)H;
+  const int dcol = a.concat ? f0 : c0;
+  VecF<VEC> ps, pd, as, ad;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { ps.v[i] = 0.0f; pd.v[i] = 0.0f; }
+  if (slot_ok) { as = ldv<VEC>(a.att_s + f0); ad = ldv<VEC>(a.att_d + f0); }
+  const int64_t rpb = 4 * (int64_t)rpw;
+  for (int64_t base = (int64_t)blockIdx.x * rpb; base < a.N; base += (int64_t)gridDim.x * rpb) {
+    const int64_t j = base + wave * rpw + (lane >> g.lgG);
+    const bool valid = j < a.N;
+    int32_t beg = 0, end = 0;
+    if (valid) { beg = a.colptr[j]; end = a.colptr[j + 1]; }
+    const int32_t npair = (end - beg) << g.lgH;
+    float s = 0.0f;
+    for (int32_t idx = lig; idx < npair; idx += G)
+      s += a.dz[(int64_t)a.csc2csr[beg + (idx >> g.lgH)] * H + hl];
+    for (int off = G >> 1; off >= H; off >>= 1) s += __shfl_xor(s, off);
+    const float dash = __shfl(s, gbase + hs);
+    VecF<VEC> acc;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc.v[i] = 0.0f;
+    if (slot_ok) {
+      for (int32_t k = beg + ep; k < end; k += EP) {
+        const int32_t i_ = a.row[k];
+        const float al = a.alpha[(int64_t)a.csc2csr[k] * H + hs];
+        const VecF<VEC> d = ldv<VEC>(a.dout + (int64_t)i_ * a.ld_dout + dcol);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc.v[i] += al * d.v[i];
+      }
+    }
+    for (int off = G >> 1; off >= g.FLp; off >>= 1) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc.v[i] += __shfl_xor(acc.v[i], off);
+    }
+    if (valid && slot_ok && ep == 0) {
+      const float dadh = a.dad[j * H + hs];
+      const VecF<VEC> x = ldv<VEC>(a.xh + j * a.ld_xh + f0);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        acc.v[i] = acc.v[i] * inv_h + dash * as.v[i] + dadh * ad.v[i];
+        ps.v[i] += dash * x.v[i];
+        pd.v[i] += dadh * x.v[i];
+      }
+      stv<VEC>(a.dxh + j * a.ld_dxh + f0, acc);
+    }
+  }
+  // block partial of d att_src / d att_dst: groups of a wave, then the 4 waves through LDS
+  for (int off = 32; off >= G; off >>= 1) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      ps.v[i] += __shfl_xor(ps.v[i], off);
+      pd.v[i] += __shfl_xor(pd.v[i], off);
+    }
+  }
+  if (lane < G && ep == 0 && slot_ok) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) { red[0][wave][f0 + i] = ps.v[i]; red[1][wave][f0 + i] = pd.v[i]; }
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < 2 * F; f += blockDim.x) {
+    const int w = f >= F;
+    const int ff = f - w * F;
+    part[((int64_t)blockIdx.x * 2 + w) * F + ff] =
+        ((red[w][0][ff] + red[w][1][ff]) + red[w][2][ff]) + red[w][3][ff];
+  }
+}
+
+// d att (2F outputs) = sum over the cols pass's block partials: one block per output.
+__global__ __launch_bounds__(256) void gat_att_reduce_kernel(int F, int nblk, const float* __restrict__ part,
+                                                             float* __restrict__ d_att_s, float* __restrict__ d_att_d) {
+  __shared__ float wsum[4];
+  const int w = blockIdx.x >= (unsigned)F;
+  const int f = blockIdx.x - w * F;
+  float s = 0.0f;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) s += part[((int64_t)b * 2 + w) * F + f];
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+    (w ? d_att_d : d_att_s)[f] = t;
+  }
+}
+
+int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
+int pow2ceil(int v) { return 1 << ilog2(v); }
+
+bool vec_ok(const void* p, int64_t ld, int v) {
+  return ((uintptr_t)p % (uintptr_t)(4 * v)) == 0 && ld % v == 0;
+}
+
+// Fast-path geometry, or false when the generic one-wave-per-row kernels must run
+// (more than 64 slots of VEC floats, or a head mean whose slots per head are not a power of two).
+bool gat_geom(int H, int C, int concat, std::initializer_list<std::pair<const void*, int64_t>> ops, GatGeom* g,
+              int* vec) {
+  const int F = H * C;
+  int v = 4;
+  for (; v > 1; v >>= 1) {
+    if (C % v) continue;
+    bool ok = true;
+    for (auto& o : ops) ok = ok && (o.first == nullptr || vec_ok(o.first, o.second, v));
+    if (ok) break;
+  }
+  const int FL = F / v, L = C / v;
+  if (FL > 64) return false;
+  if (!concat && (L & (L - 1))) return false;
+  g->FL = FL;
+  g->FLp = pow2ceil(FL);
+  g->lgFLp = ilog2(g->FLp);
+  g->L = L;
+  g->lgH = ilog2(H);
+  g->G = std::max(std::max(g->FLp, H), 4);
+  g->lgG = ilog2(g->G);
+  g->Gb = std::min(64, std::max(4, 2 * H));
+  g->lgGb = ilog2(g->Gb);
+  *vec = v;
+  return true;
+}
+
+unsigned group_blocks(int64_t N, int G, int64_t cap) {
+  int64_t rpb = 4 * (64 / G);
+  int64_t b = ceil_div(N, rpb);
+  if (b > cap) b = cap;
+  return (unsigned)(b > 0 ? b : 1);
+}
+
+constexpr int64_t kColsBlocks = 2048;  // cols-pass grid cap = number of d att partials
+
 bool pow2_heads(int H) { return H >= 1 && H <= 64 && (H & (H - 1)) == 0; }
 
 unsigned row_blocks(int64_t N) {
@@ -272,7 +605,7 @@ void carve_bwd(C& c, int64_t N, int64_t S, int H, int C_, float** dz, float** da
   auto p0 = c.template take<float>((size_t)(S > 0 ? S : 1) * H);
   auto p1 = c.template take<float>((size_t)(N > 0 ? N : 1) * H);
   auto p2 = c.template take<float>((size_t)(N > 0 ? N : 1) * H);
-  auto p3 = c.template take<float>((size_t)kAttBlocks * 2 * H * C_);
+  auto p3 = c.template take<float>((size_t)2048 * 2 * H * C_);  // max(kAttBlocks, kColsBlocks)
   if (dz) { *dz = (float*)p0; *dad = (float*)p1; *das = (float*)p2; *part = (float*)p3; }
 }
 
@@ -318,7 +651,16 @@ extern "C" gnn_status gnn_gat_fwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
   a.xh = xh; a.ld_xh = ld_xh; a.a_s = a_src; a.a_d = a_dst; a.bias = bias;
   a.alpha = alpha; a.out = out; a.ldo = ldo;
   hipStream_t st = (hipStream_t)stream;
-  gat_fwd_kernel<<<row_blocks(a.N), 256, 0, st>>>(a);
+  GatGeom gg;
+  int vec = 1;
+  if (gat_geom(H, C, concat, {{xh, ld_xh}, {out, ldo}}, &gg, &vec)) {
+    const unsigned nb = group_blocks(a.N, gg.G, (int64_t)1 << 20);
+    if (vec == 4) gat_fwd_group_kernel<4><<<nb, 256, 0, st>>>(a, gg);
+    else if (vec == 2) gat_fwd_group_kernel<2><<<nb, 256, 0, st>>>(a, gg);
+    else gat_fwd_group_kernel<1><<<nb, 256, 0, st>>>(a, gg);
+  } else {
+    gat_fwd_kernel<<<row_blocks(a.N), 256, 0, st>>>(a);
+  }
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }
@@ -361,6 +703,29 @@ extern "C" gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
   a.xh = xh; a.ld_xh = ld_xh; a.a_s = a_src; a.a_d = a_dst;
   a.att_s = att_src; a.att_d = att_dst; a.alpha = const_cast<float*>(alpha);
   a.dout = dout; a.ld_dout = ld_dout; a.dxh = dxh; a.ld_dxh = ld_dxh;
+  GatGeom gg;
+  int vec = 1;
+  if (gat_geom(H, C, concat, {{xh, ld_xh}, {dout, ld_dout}, {dxh, ld_dxh}, {att_src, 0}, {att_dst, 0}}, &gg,
+               &vec)) {
+    const unsigned nbr = group_blocks(a.N, gg.Gb, (int64_t)1 << 20);
+    const unsigned nbc = group_blocks(a.N, gg.G, kColsBlocks);
+    switch (vec) {
+#define GNN_GAT_BWD(V)                                                            \
+  case V:                                                                         \
+    gat_bwd_rows_group_kernel<V><<<nbr, 256, 0, st>>>(a, gg);                     \
+    GNN_LAUNCH_CHECK();                                                           \
+    gat_bwd_cols_group_kernel<V><<<nbc, 256, 0, st>>>(a, gg, part);               \
+    break;
+      GNN_GAT_BWD(4)
+      GNN_GAT_BWD(2)
+      default: GNN_GAT_BWD(1)
+#undef GNN_GAT_BWD
+    }
+    GNN_LAUNCH_CHECK();
+    gat_att_reduce_kernel<<<(unsigned)(2 * F), 256, 0, st>>>((int)F, (int)nbc, part, d_att_src, d_att_dst);
+    GNN_LAUNCH_CHECK();
+    return GNN_OK;
+  }
   gat_bwd_rows_kernel<<<row_blocks(a.N), 256, 0, st>>>(a);
   GNN_LAUNCH_CHECK();
   gat_bwd_cols_kernel<<<row_blocks(a.N), 256, 0, st>>>(a);

@@ -145,4 +145,11 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
 size_t nt_x3_workspace(int64_t k1, int64_t k2);
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant = 0);  // NPL = 3, or 1 when a_bf16
 
+// VALU kernels for the narrow output-layer shapes (gemm_skinny.hip).  launch_nt_skinny returns
+// false (launching nothing) when the shape/epilogue is outside its envelope.
+bool launch_nt_skinny(const NTArgs& a, hipStream_t st);
+int tn_skinny_blocks(int64_t M);
+bool tn_skinny_ok(const TNArgs& a);
+void launch_tn_skinny(const TNArgs& a, int nblk, hipStream_t st);
+
 }  // namespace gnnmp

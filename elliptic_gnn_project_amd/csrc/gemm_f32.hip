@@ -791,6 +791,7 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   hipStream_t st = (hipStream_t)stream;
   a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16;
   a.c_bf16 = p->c_dtype == GNN_DTYPE_BF16;
+  if (variant == 0 && launch_nt_skinny(a, st)) return hip_check(hipGetLastError(), fn);  // Nc <= 8 or K <= 8
   if (a.a_bf16 || a.c_bf16) {
     if (!a.a_bf16 || !a.w1 || a.Nc > BN || p->math == GNN_MATH_F32)
       return fail(GNN_ERR_UNSUPPORTED, fn, "bf16 NT needs bf16 A, the w1/w2 form, N <= 128 and split math");
@@ -827,7 +828,9 @@ extern "C" gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t 
   if (!bytes || M < 0 || Nr < 1 || Kc < 1 || nproj < 0) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
   int64_t stride = Nr * Kc + Nr + (int64_t)nproj * Nr + nproj;
   stride = (stride + 63) / 64 * 64;
-  *bytes = (size_t)tn_blocks(M) * stride * sizeof(float);
+  int64_t nb = tn_blocks(M);
+  if (Nr <= 8 && nproj == 0) nb = std::max<int64_t>(nb, tn_skinny_blocks(M));  // gemm_skinny.hip
+  *bytes = (size_t)nb * stride * sizeof(float);
   return GNN_OK;
 }
 
@@ -866,7 +869,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   const int64_t Kc = p->k1 + p->k2;
   const int64_t n_out = p->Nr * Kc + p->Nr + (int64_t)nproj * p->Nr + nproj;
   int64_t stride = (n_out + 63) / 64 * 64;
-  const int nblk = tn_blocks(p->M);
+  int nblk = tn_blocks(p->M);
   if (!workspace || workspace_bytes < (size_t)nblk * stride * sizeof(float))
     return fail(GNN_ERR_WORKSPACE, __fn, "workspace too small");
   hipStream_t st = (hipStream_t)stream;
@@ -891,6 +894,16 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   if (a.h_bf16 && !a.a_bf16) return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 h needs bf16 A");
   // the split kernel indexes rows with 32-bit element offsets
   const int64_t ldmax = std::max({a.lda1, a.k2 > 0 ? a.lda2 : 0, a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
+  if (variant == 0 && tn_skinny_ok(a)) {  // Nr <= 8 plain g form: VALU stream (gemm_skinny.hip)
+    nblk = tn_skinny_blocks(a.M);
+    if (workspace_bytes < (size_t)nblk * stride * sizeof(float))
+      return fail(GNN_ERR_WORKSPACE, __fn, "workspace too small");
+    launch_tn_skinny(a, nblk, st);
+    GNN_LAUNCH_CHECK();
+    slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+    GNN_LAUNCH_CHECK();
+    return GNN_OK;
+  }
   if (a.a_bf16 && (p->math == GNN_MATH_F32 || (a.M + 32) * ldmax >= ((int64_t)1 << 31)))
     return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 TN needs split math and M*ld < 2^31");
   if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31)) {

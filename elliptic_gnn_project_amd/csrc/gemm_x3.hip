@@ -194,7 +194,9 @@ __device__ __forceinline__ void x3_chunk(const NTArgs& a, int c, int nch1, const
 // is short; without depth the loop waits on HBM latency).  One barrier per chunk.
 // NPL = 3: f32 operands split (6 products); NPL = 1 with ABF: bf16 operands as stored, B rounded
 // to bf16 (the image's hi plane), one product (the bf16-storage path); CBF: C stored as bf16.
-template <int KC, int TM, int AV, int AU, int BV, int D, int NPL = 3, bool ABF = false, bool CBF = false>
+constexpr int NT_PIPE = 32, NT_HINTS = 64;  // gemm_nt_x3_kernel LAB flags (bits 1-16: lab ablations)
+
+template <int KC, int TM, int AV, int AU, int BV, int D, int NPL = 3, bool ABF = false, bool CBF = false, int LAB = 0>
 __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* __restrict__ bimg) {
   constexpr int P = KC + 8;  // bf16 per LDS row: 24 or 40 (12 / 20 dwords)
   constexpr int BM = 128 * TM;
@@ -241,8 +243,9 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   auto store = [&](int c, int buf, const float* rA, const float* rB) {
     const float *A, *W; int64_t lda, ldw; int k0, klen;
     x3_chunk<KC>(a, c, nch1, A, lda, W, ldw, k0, klen);
-    x3_store_rows<AU, KC, BM, P, NPL>(As[buf], m0, a.M, klen, rA);
-    if constexpr (BV == 0) {
+    if constexpr (!(LAB & 8)) x3_store_rows<AU, KC, BM, P, NPL>(As[buf], m0, a.M, klen, rA);
+    if constexpr (LAB & 16) {
+    } else if constexpr (BV == 0) {
       const int n = threadIdx.x >> 1, kh = threadIdx.x & 1;
 #pragma unroll
       for (int p = 0; p < NPL; ++p)
@@ -260,7 +263,7 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
     const uint16_t* Bb = Bs[buf] + fr;
 #pragma unroll
     for (int s = 0; s < KC / 16; ++s) {
-      if (16 * s < klen) {
+      if (KC == 16 || 16 * s < klen) {  // KC == 16: every chunk has klen >= 1 (no branch)
         bf16x8 af[TM][NPL], bf[4][NPL];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
@@ -283,16 +286,56 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   // in flight; a branch around a load makes it drain every stage at the next store.
 #pragma unroll
   for (int d = 0; d < D; ++d) load(min(d, nchunks - 1), ra[d], rb[d]);
+  if constexpr ((LAB & NT_PIPE) != 0) {
+    // software-pipelined order: between two barriers, stage chunk c+1 into the other buffer
+    // while the MFMAs of chunk c run, so VALU splits / LDS writes interleave with the MFMAs
+    store(0, 0, ra[0], rb[0]);
+    load(min(D, nchunks - 1), ra[0], rb[0]);
+    int c = 0;
+    for (; c + D < nchunks; c += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int cc = c + d;  // cc + 1 < nchunks for all d here
+        const int d1 = (d + 1) % D;
+        __syncthreads();
+        store(cc + 1, (cc + 1) & 1, ra[d1], rb[d1]);
+        load(min(cc + 1 + D, nchunks - 1), ra[d1], rb[d1]);
+        compute(cc & 1, cc);
+        if constexpr ((LAB & NT_HINTS) != 0) {  // interleave: per MFMA, a few VALU / DS ops
+#pragma unroll
+          for (int i = 0; i < 4 * TM * (NPL == 3 ? 6 : 1) * (KC / 16); ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int cc = c + d;
+      if (cc < nchunks) {
+        const int d1 = (d + 1) % D;
+        __syncthreads();
+        if (cc + 1 < nchunks) store(cc + 1, (cc + 1) & 1, ra[d1], rb[d1]);
+        compute(cc & 1, cc);
+      }
+    }
+    nt_epilogue<TM, CBF>(a, acc, m0, n0, lane, wave, seed);
+    return;
+  }
   int c0 = 0;
   for (; c0 + D <= nchunks; c0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const int c = c0 + d;
       const int buf = c & 1;
-      store(c, buf, ra[d], rb[d]);  // buf was last read by compute(c - 2): behind barrier c - 1
+      if constexpr (!(LAB & 4)) store(c, buf, ra[d], rb[d]);  // buf last read by compute(c - 2): behind barrier c - 1
       __syncthreads();
-      load(min(c + D, nchunks - 1), ra[d], rb[d]);
-      compute(buf, c);
+      if constexpr (!(LAB & 2)) load(min(c + D, nchunks - 1), ra[d], rb[d]);
+      if constexpr (!(LAB & 1)) compute(buf, c);
     }
   }
 #pragma unroll
@@ -307,10 +350,10 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   nt_epilogue<TM, CBF>(a, acc, m0, n0, lane, wave, seed);
 }
 
-template <int KC, int TM, int AV, int AU, int D>
+template <int KC, int TM, int AV, int AU, int D, int LAB = 0>
 void launch_nt_x3_b(const NTArgs& a, const uint4* bimg, hipStream_t st) {
   dim3 grid((unsigned)ceil_div(a.M, 128 * TM), (unsigned)ceil_div(a.Nc, BN));
-  if (bimg) gemm_nt_x3_kernel<KC, TM, AV, AU, 0, D><<<grid, 256, 0, st>>>(a, bimg);
+  if (bimg) gemm_nt_x3_kernel<KC, TM, AV, AU, 0, D, 3, false, false, LAB><<<grid, 256, 0, st>>>(a, bimg);
   else if (a.wvec == 4) gemm_nt_x3_kernel<KC, TM, AV, AU, 4, D><<<grid, 256, 0, st>>>(a, nullptr);
   else if (a.wvec == 2) gemm_nt_x3_kernel<KC, TM, AV, AU, 2, D><<<grid, 256, 0, st>>>(a, nullptr);
   else gemm_nt_x3_kernel<KC, TM, AV, AU, 1, D><<<grid, 256, 0, st>>>(a, nullptr);
@@ -343,14 +386,15 @@ constexpr int TX_AS = 3;           // A unit slots per thread (u = tid + 256·s 
 // from LDS instead of 32 registers of replicated dz rows per thread.
 // NPL = 3: f32 operands split (6 products).  NPL = 1: the bf16-storage path — A (ABF) and h
 // (HBF) are read as bf16, G is rounded to bf16, one product per MFMA.
-template <bool PROJ, bool MASK, int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false>
+template <bool PROJ, bool MASK, int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0,
+          bool GOUT = true>
 __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   constexpr int NS = TX_AS + ((!PROJ && MASK) ? 2 : 1);  // + G slot (+ g slot)
   constexpr int GS = TX_AS;                              // the G slot index
   __shared__ __attribute__((aligned(16))) uint16_t Gt[2][NPL * TGPL];
   __shared__ __attribute__((aligned(16))) uint16_t At[2][NPL * TAPL];
   __shared__ float Ps[MAXPROJ * 128];
-  __shared__ float dzL[2][TMC * MAXPROJ];
+  __shared__ float dzL[2][TX_THREADS];  // rows 0..63 used; all threads write (branch-free staging)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -388,12 +432,13 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   for (int sl = 0; sl < TX_AS; ++sl) {
     const int u = tid + TX_THREADS * sl;
     aon[sl] = u < 2 * KP;
-    ak[sl] = u % KP;
-    oct[sl] = u / KP;
+    // idle slots stage into column KMAX - 1: only read by a tile t >= nkt, whose dW is discarded
+    ak[sl] = aon[sl] ? u % KP : KMAX - 1;
+    oct[sl] = aon[sl] ? u / KP : 0;
     const int k = ak[sl];
     if (aon[sl] && k < a.k1) { base[sl] = elem_ptr<ABF>(a.a1, k); ld32[sl] = (int)a.lda1; }
     else if (aon[sl] && k < Kc) { base[sl] = elem_ptr<ABF>(a.a2, k - a.k1); ld32[sl] = (int)a.lda2; }
-    else { base[sl] = a.a1; ld32[sl] = 0; oct[sl] = 0; }
+    else { base[sl] = a.a1; ld32[sl] = 0; }
   }
   if constexpr (MASK) { base[GS] = elem_ptr<HBF>(a.h, gnc); ld32[GS] = (int)a.ldh; }
   else { base[GS] = a.g + gnc; ld32[GS] = (int)a.ldg; }
@@ -405,19 +450,24 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 
   // 32-bit element offsets (the dispatcher guarantees M·ld < 2^31): rows clamped to mend - 1
   const int mlast = (int)(mend - 1);
+  uint32_t olast[NS];  // offset of the block's last row: clamping offsets = clamping rows (ld >= 0)
+#pragma unroll
+  for (int sl = 0; sl < NS; ++sl) olast[sl] = (uint32_t)(mlast * ld32[sl]);
   float rv[D][NS][8];
   float rz[D];
   auto load = [&](int d, int c) {
     const int m0 = (int)mbeg + c * TMC;
 #pragma unroll
-    for (int sl = 0; sl < NS; ++sl)
+    for (int sl = 0; sl < NS; ++sl) {
+      uint32_t o = (uint32_t)((m0 + 8 * oct[sl]) * ld32[sl]);  // one multiply per slot (rows by adds)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const int m = min(m0 + 8 * oct[sl] + i, mlast);
-        const uint32_t off = (uint32_t)(m * ld32[sl]);
+        const uint32_t off = min(o, olast[sl]);
+        o += (uint32_t)ld32[sl];
         const bool bf = sl < TX_AS ? ABF : (sl == GS && MASK ? HBF : false);  // compile-time per slot
         rv[d][sl][i] = bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(base[sl])[off]) : base[sl][off];
       }
+    }
     if constexpr (PROJ) {  // dz rows of chunk c + 1
       const int m = min(m0 + TMC + zr, mlast);
       rz[d] = a.dz[(uint32_t)(m * (int)a.lddz + zqc)];
@@ -437,20 +487,16 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   auto store = [&](int d, int c) {
     const int buf = c & 1;
     const int64_t m0 = mbeg + (int64_t)c * TMC;
-    if constexpr (PROJ) {
-      if (tid < TMC * MAXPROJ) {
-        const bool ok = zq < a.nproj && m0 + TMC + zr < mend;
-        dzL[(c + 1) & 1][tid] = ok ? rz[d] : 0.0f;  // slot read by G(c - 1), behind barrier c - 1
-      }
+    if constexpr (PROJ) {  // slot read by G(c - 1), behind barrier c - 1 (threads >= 64: unused)
+      const bool ok = tid < TMC * MAXPROJ && zq < a.nproj && m0 + TMC + zr < mend;
+      dzL[(c + 1) & 1][tid] = ok ? rz[d] : 0.0f;
     }
 #pragma unroll
-    for (int sl = 0; sl < TX_AS; ++sl) {
-      if (aon[sl]) {
-        float e[8];
+    for (int sl = 0; sl < TX_AS; ++sl) {  // unconditional (idle slots: column KMAX - 1, zeros)
+      float e[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = (ak[sl] < Kc && m0 + 8 * oct[sl] + i < mend) ? rv[d][sl][i] : 0.0f;
-        put8(At[buf] + ak[sl] * TP + 8 * oct[sl], TAPL, e);
-      }
+      for (int i = 0; i < 8; ++i) e[i] = (ak[sl] < Kc && m0 + 8 * oct[sl] + i < mend) ? rv[d][sl][i] : 0.0f;
+      put8(At[buf] + ak[sl] * TP + 8 * oct[sl], TAPL, e);
     }
     float e[8];
 #pragma unroll
@@ -468,14 +514,16 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 #pragma unroll
           for (int q = 0; q < MAXPROJ; ++q) dw2[q] = fmaf(ok ? z[q] : 0.0f, rv[d][GS][i], dw2[q]);
         }
-        if (gn < MAXPROJ) dzs += rok ? z[gn] : 0.0f;
+        dzs += (gn < MAXPROJ && rok) ? z[gn & (MAXPROJ - 1)] : 0.0f;
       } else {
         g = rv[d][NS - 1][i];
       }
       if constexpr (MASK) g = rv[d][GS][i] > 0.0f ? g * a.hscale : 0.0f;
       g = ok ? g : 0.0f;
       db += g;
-      if (a.gout && ok) a.gout[(m0 + r) * a.ldgout + gn] = g;
+      if constexpr (GOUT) {
+        if (a.gout && ok) a.gout[(m0 + r) * a.ldgout + gn] = g;
+      }
       e[i] = g;
     }
     put8(Gt[buf] + gn * TP + 8 * go, TGPL, e);
@@ -503,14 +551,49 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 
   if (nch > 0) {
     if constexpr (PROJ) {  // dz of chunk 0
-      if (tid < TMC * MAXPROJ) {
-        const int64_t m = mbeg + zr;
-        dzL[0][tid] = (zq < a.nproj && m < mend) ? a.dz[m * a.lddz + zqc] : 0.0f;
-      }
+      const int64_t m = mbeg + zr;
+      dzL[0][tid] = (tid < TMC * MAXPROJ && zq < a.nproj && m < mend) ? a.dz[m * a.lddz + zqc] : 0.0f;
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) load(d, min(d, nch - 1));
     __syncthreads();  // Ps, dzL[0]
+    if constexpr (PIPE != 0) {
+      // software-pipelined order: between two barriers, chunk c+1 is staged into the other
+      // buffers while chunk c's MFMAs run (PIPE == 2 adds interleave hints for the scheduler)
+      store(0, 0);
+      load(0, min(D, nch - 1));
+      int c = 0;
+      for (; c + D < nch; c += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+          const int cc = c + d;
+          const int d1 = (d + 1) % D;
+          __syncthreads();
+          store(d1, cc + 1);
+          load(d1, min(cc + 1 + D, nch - 1));
+          compute(cc);
+          if constexpr (PIPE == 2) {
+#pragma unroll
+            for (int i = 0; i < KT * (NPL == 3 ? 6 : 1); ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+              __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+              __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+              __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        const int cc = c + d;
+        if (cc < nch) {
+          __syncthreads();
+          if (cc + 1 < nch) store((d + 1) % D, cc + 1);
+          compute(cc);
+        }
+      }
+    } else {
     int c0 = 0;
     for (; c0 + D <= nch; c0 += D) {
 #pragma unroll
@@ -531,6 +614,7 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
         compute(c);
       }
     }
+    }
   }
 
   // ---- this block's partial dW (segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2])
@@ -550,234 +634,6 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   // ---- side sums of the two row octets (G slots), combined in a fixed order via LDS
   float* red = reinterpret_cast<float*>(&At[0][0]);
   constexpr int ns = 2 + MAXPROJ;
-  __syncthreads();
-  red[(go * 128 + gn) * ns + 0] = db;
-  red[(go * 128 + gn) * ns + 1] = dzs;
-#pragma unroll
-  for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
-  __syncthreads();
-  if (tid < 128 && tid < a.Nr) {
-    float* side = slab + (int64_t)a.Nr * Kc;
-    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
-    for (int q = 0; q < a.nproj; ++q)
-      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
-  }
-  if (PROJ && tid < a.nproj)
-    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
-}
-
-// ----------------------------------------------------------------- TN, 32-row chunks ("x3b")
-// Same roles and split as gemm_tn_x3_kernel, but 32 rows (two MFMA k-steps) per chunk through a
-// single LDS image with two barriers per chunk: the next chunk's loads (one register stage) have
-// a whole chunk of MFMAs (2 x KT x 6 per wave) to land, instead of the 16-row kernel's single
-// k-step — the 16-row kernel waits on HBM latency every chunk.  Slots: 6 A units (u = tid +
-// 256·s < 4·KP: column u mod KP, rows 8·(u / KP) ..) and 2 G units (column tid mod 128, rows
-// 8·(tid / 128 + 2s) ..) per thread.  dz staged one chunk ahead into a 2-slot LDS ring.
-constexpr int TB_MC = 32;
-constexpr int TB_P = TB_MC + 8;     // 20 dwords: conflict-free b128 reads and writes
-constexpr int TB_GPL = 128 * TB_P;
-constexpr int TB_APL = KMAX * TB_P;
-constexpr int TB_AS = 6;
-constexpr int TB_GS = 2;
-
-template <bool PROJ, bool MASK, int KT, int NPL = 3, bool ABF = false, bool HBF = false>
-__global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3b_kernel(TNArgs a) {
-  constexpr bool GX = !PROJ && MASK;         // g form with mask: an extra g slot per G unit
-  constexpr int NS = TB_AS + TB_GS * (GX ? 2 : 1);
-  __shared__ __attribute__((aligned(16))) uint16_t Gt[NPL * TB_GPL];
-  __shared__ __attribute__((aligned(16))) uint16_t At[NPL * TB_APL];
-  __shared__ float Ps[MAXPROJ * 128];
-  __shared__ float dzL[2][TB_MC * MAXPROJ];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int ntile = tid >> 6;
-  const int Kc = a.k1 + a.k2;
-  const int nkt = (Kc + 31) / 32;
-  const int KP = nkt * 32;
-  const int64_t mbeg = (int64_t)blockIdx.x * a.rows_per_block;
-  const int64_t mend = min(a.M, mbeg + a.rows_per_block);
-  const int nch = mend > mbeg ? (int)((mend - mbeg + TB_MC - 1) / TB_MC) : 0;
-
-  floatx16 acc[KT];
-#pragma unroll
-  for (int t = 0; t < KT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-
-  if constexpr (PROJ) {
-    if (tid < 128) {
-#pragma unroll
-      for (int q = 0; q < MAXPROJ; ++q) Ps[q * 128 + tid] = (q < a.nproj && tid < a.Nr) ? a.proj[q * a.Nr + tid] : 0.0f;
-    }
-  }
-
-  const int gn = tid & 127;
-  const bool gcol = gn < a.Nr;
-  const int gnc = gcol ? gn : 0;
-  const float* base[NS];
-  int ld32[NS];
-  int oct[NS];
-  int ak[TB_AS];
-  bool aon[TB_AS];
-#pragma unroll
-  for (int sl = 0; sl < TB_AS; ++sl) {
-    const int u = tid + TX_THREADS * sl;
-    aon[sl] = u < 4 * KP;
-    ak[sl] = u % KP;
-    oct[sl] = u / KP;
-    const int k = ak[sl];
-    if (aon[sl] && k < a.k1) { base[sl] = elem_ptr<ABF>(a.a1, k); ld32[sl] = (int)a.lda1; }
-    else if (aon[sl] && k < Kc) { base[sl] = elem_ptr<ABF>(a.a2, k - a.k1); ld32[sl] = (int)a.lda2; }
-    else { base[sl] = a.a1; ld32[sl] = 0; oct[sl] = 0; }
-  }
-#pragma unroll
-  for (int s2 = 0; s2 < TB_GS; ++s2) {
-    const int sl = TB_AS + s2;
-    if constexpr (MASK) { base[sl] = elem_ptr<HBF>(a.h, gnc); ld32[sl] = (int)a.ldh; }
-    else { base[sl] = a.g + gnc; ld32[sl] = (int)a.ldg; }
-    oct[sl] = (tid >> 7) + 2 * s2;
-    if constexpr (GX) { base[sl + TB_GS] = a.g + gnc; ld32[sl + TB_GS] = (int)a.ldg; oct[sl + TB_GS] = oct[sl]; }
-  }
-  const int zr = (tid & 127) / MAXPROJ, zq = (tid & 127) % MAXPROJ;  // dz element (threads 0..127)
-  const int zqc = PROJ ? min(zq, a.nproj - 1) : 0;
-  const int mlast = (int)(mend - 1);
-
-  float rv[NS][8];
-  float rz = 0.f;
-  auto load = [&](int c) {
-    const int m0 = (int)mbeg + c * TB_MC;
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = min(m0 + 8 * oct[sl] + i, mlast);
-        const uint32_t off = (uint32_t)(m * ld32[sl]);
-        const bool bf = sl < TB_AS ? ABF : (sl < TB_AS + TB_GS && MASK ? HBF : false);
-        rv[sl][i] = bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(base[sl])[off]) : base[sl][off];
-      }
-    if constexpr (PROJ) {  // dz rows of chunk c + 1
-      const int m = min(m0 + TB_MC + zr, mlast);
-      rz = a.dz[(uint32_t)(m * (int)a.lddz + zqc)];
-    }
-  };
-
-  float db = 0.f, dzs = 0.f;
-  float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
-  auto put8 = [](uint16_t* dst, int plane, const float (&e)[8]) {
-    uint32_t w[4][3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) split_pair(e[2 * j], e[2 * j + 1], w[j]);
-#pragma unroll
-    for (int p = 0; p < NPL; ++p)
-      *reinterpret_cast<uint4*>(dst + p * plane) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
-  };
-  auto store = [&](int c) {
-    const int64_t m0 = mbeg + (int64_t)c * TB_MC;
-    if constexpr (PROJ) {
-      if (tid < TB_MC * MAXPROJ) {
-        const bool ok = zq < a.nproj && m0 + TB_MC + zr < mend;
-        dzL[(c + 1) & 1][tid] = ok ? rz : 0.0f;
-      }
-    }
-#pragma unroll
-    for (int sl = 0; sl < TB_AS; ++sl) {
-      if (aon[sl]) {
-        float e[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = (ak[sl] < Kc && m0 + 8 * oct[sl] + i < mend) ? rv[sl][i] : 0.0f;
-        put8(At + ak[sl] * TB_P + 8 * oct[sl], TB_APL, e);
-      }
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < TB_GS; ++s2) {
-      const int sl = TB_AS + s2;
-      float e[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = 8 * oct[sl] + i;
-        const bool rok = m0 + r < mend;
-        const bool ok = rok && gcol;
-        float g;
-        if constexpr (PROJ) {
-          const float* z = &dzL[c & 1][r * MAXPROJ];
-          g = z[0] * Ps[gn];
-#pragma unroll
-          for (int q = 1; q < MAXPROJ; ++q) g = fmaf(z[q], Ps[q * 128 + gn], g);
-          if constexpr (MASK) {
-#pragma unroll
-            for (int q = 0; q < MAXPROJ; ++q) dw2[q] = fmaf(ok ? z[q] : 0.0f, rv[sl][i], dw2[q]);
-          }
-          if (gn < MAXPROJ) dzs += rok ? z[gn] : 0.0f;
-        } else {
-          g = GX ? rv[sl + TB_GS][i] : rv[sl][i];
-        }
-        if constexpr (MASK) g = rv[sl][i] > 0.0f ? g * a.hscale : 0.0f;
-        g = ok ? g : 0.0f;
-        db += g;
-        if (a.gout && ok) a.gout[(m0 + r) * a.ldgout + gn] = g;
-        e[i] = g;
-      }
-      put8(Gt + gn * TB_P + 8 * oct[sl], TB_GPL, e);
-    }
-  };
-
-  const int fr = (lane & 31) * TB_P + 8 * (lane >> 5);
-  auto compute = [&]() {
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {  // software-pipelined as in gemm_tn_x3_kernel
-      bf16x8 gf[NPL], af[2][NPL];
-#pragma unroll
-      for (int p = 0; p < NPL; ++p) gf[p] = lds_frag(Gt + p * TB_GPL + ntile * 32 * TB_P + fr + 16 * s);
-#pragma unroll
-      for (int p = 0; p < NPL; ++p) af[0][p] = lds_frag(At + p * TB_APL + fr + 16 * s);
-#pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        if (t + 1 < KT) {
-#pragma unroll
-          for (int p = 0; p < NPL; ++p)
-            af[(t + 1) & 1][p] = lds_frag(At + p * TB_APL + (t + 1) * 32 * TB_P + fr + 16 * s);
-        }
-        acc[t] = mfma_planes<NPL>(gf, af[t & 1], acc[t]);
-      }
-    }
-  };
-
-  if (nch > 0) {
-    if constexpr (PROJ) {
-      if (tid < TB_MC * MAXPROJ) {
-        const int64_t m = mbeg + zr;
-        dzL[0][tid] = (zq < a.nproj && m < mend) ? a.dz[m * a.lddz + zqc] : 0.0f;
-      }
-    }
-    load(0);
-    __syncthreads();  // Ps, dzL[0]
-    store(0);
-    __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-      load(min(c + 1, nch - 1));  // unconditional: in flight across this chunk's MFMAs
-      compute();
-      __syncthreads();            // every wave is done with the image
-      if (c + 1 < nch) store(c + 1);
-      __syncthreads();
-    }
-  }
-
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    if (t >= nkt) continue;
-    const int col = t * 32 + (lane & 31);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int64_t idx = col < a.k1 ? (int64_t)row * a.k1 + col
-                                     : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (col - a.k1);
-      if (row < a.Nr && col < Kc) slab[idx] = acc[t][r];
-    }
-  }
-  float* red = reinterpret_cast<float*>(At);
-  constexpr int ns = 2 + MAXPROJ;
-  const int go = tid >> 7;
   __syncthreads();
   red[(go * 128 + gn) * ns + 0] = db;
   red[(go * 128 + gn) * ns + 1] = dzs;
@@ -820,7 +676,7 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
       bimg = static_cast<const uint4*>(ws);
     }
     dim3 grid((unsigned)ceil_div(a.M, 128), (unsigned)ceil_div(a.Nc, BN));
-#define GNN_NTB(AVV, BVV, C) gemm_nt_x3_kernel<16, 1, AVV, 2, BVV, 2, 1, true, C><<<grid, 256, 0, st>>>(a, bimg)
+#define GNN_NTB(AVV, BVV, C) gemm_nt_x3_kernel<16, 1, AVV, 2, BVV, 2, 1, true, C, BVV == 0 ? NT_PIPE | NT_HINTS : 0><<<grid, 256, 0, st>>>(a, bimg)
 #define GNN_NTB_C(AVV, BVV) do { if (a.c_bf16) GNN_NTB(AVV, BVV, true); else GNN_NTB(AVV, BVV, false); } while (0)
     const bool v2 = bv_ok(2);
     if (bimg) { if (v2) GNN_NTB_C(2, 0); else GNN_NTB_C(1, 0); }
@@ -837,67 +693,71 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
     x3_presplit_b_kernel<<<nch, 256, 0, st>>>(a, static_cast<uint4*>(ws), nch1, nch);
     bimg = static_cast<const uint4*>(ws);
   }
-  // lab (bench_gemm.cpp, MI355X, Elliptic layer-1 shape, fused epilogue): pre-split B with b32 A
-  // stores and D = 2 184 us; B split in-kernel 195-200 us; D = 1 228 us; D = 3 188 us.
+  // Lab (bench_gemm.cpp, MI355X, Elliptic layer-1 shape, same process, plain / fused epilogue):
+  //   classic order (stage c; barrier; MFMAs of c)            171-182 / 202-228 us
+  //   pipelined order (barrier; stage c+1 with MFMAs of c)    164-169 / 189-194 us
+  //   pipelined + sched_group_barrier interleave (production) 155-159 / 182-185 us
+  // Ablations of the classic instance (what bounds it): no MFMA phase 122, no global loads 127,
+  // MFMA phase + barriers only 103, LDS staging only 70 (A 49, B 49), barriers + epilogue 30;
+  // D = 1 228, D = 3 188; A fragments loaded straight to registers (no A through LDS) 291
+  // (fragment-shaped loads touch 32 rows per instruction).
+  if (!bimg) {  // no workspace: B split in-kernel
+    launch_nt_x3_a<16, 1, 2, 2>(a, av, nullptr, st);
+    return;
+  }
   switch (variant) {
-    case 1: launch_nt_x3_a<16, 1, 1, 2>(a, av, bimg, st); break;
-    case 2: launch_nt_x3_a<16, 1, 3, 4>(a, av, bimg, st); break;
-    case 3: launch_nt_x3_a<16, 1, 2, 2>(a, av, nullptr, st); break;
-    case 4: launch_nt_x3_a<16, 1, 2, 4>(a, av, nullptr, st); break;
-    case 5: launch_nt_x3_a<16, 1, 2, 8>(a, av, bimg, st); break;
-    default: launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st); break;
+    case 1: launch_nt_x3_b<16, 1, 2, 2, 2, NT_PIPE | NT_HINTS>(a, bimg, st); break;  // pipelined + hints
+    case 2: launch_nt_x3_b<16, 1, 2, 2, 2, NT_PIPE>(a, bimg, st); break;             // pipelined
+    case 6: launch_nt_x3_b<16, 1, 2, 2, 2, 1>(a, bimg, st); break;  // ablation: no MFMA phase
+    case 7: launch_nt_x3_b<16, 1, 2, 2, 2, 2>(a, bimg, st); break;  // ablation: no global loads in the loop
+    case 8: launch_nt_x3_b<16, 1, 2, 2, 2, 6>(a, bimg, st); break;  // ablation: MFMA phase + barriers only
+    case 9: launch_nt_x3_b<16, 1, 2, 2, 2, 3>(a, bimg, st); break;  // ablation: LDS staging + barriers only
+    default:  // production: classic order (branch-free MFMA phase)
+      launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
+      break;
   }
 }
 
-template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false>
+template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0, bool GO = false>
+void launch_tn_x3_kg(const TNArgs& a, int nblk, hipStream_t st) {
+  const bool proj = a.dz != nullptr, mask = a.h != nullptr;
+  if (proj && mask) gemm_tn_x3_kernel<true, true, D, KT, NPL, ABF, HBF, PIPE, GO><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (proj) gemm_tn_x3_kernel<true, false, D, KT, NPL, ABF, HBF, PIPE, GO><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (mask) gemm_tn_x3_kernel<false, true, D, KT, NPL, ABF, HBF, PIPE, GO><<<nblk, TX_THREADS, 0, st>>>(a);
+  else gemm_tn_x3_kernel<false, false, D, KT, NPL, ABF, HBF, PIPE, GO><<<nblk, TX_THREADS, 0, st>>>(a);
+}
+
+// the G write-out (gout, needed only when a further layer's dh follows) is a compile-time branch
+template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0>
 void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
-  const bool proj = a.dz != nullptr, mask = a.h != nullptr;
-  if (proj && mask) gemm_tn_x3_kernel<true, true, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
-  else if (proj) gemm_tn_x3_kernel<true, false, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
-  else if (mask) gemm_tn_x3_kernel<false, true, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
-  else gemm_tn_x3_kernel<false, false, D, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
+  if (a.gout) launch_tn_x3_kg<D, KT, NPL, ABF, HBF, PIPE, true>(a, nblk, st);
+  else launch_tn_x3_kg<D, KT, NPL, ABF, HBF, PIPE, false>(a, nblk, st);
 }
 
-template <int KT, int NPL = 3, bool ABF = false, bool HBF = false>
-void launch_tn_x3b_k(const TNArgs& a, int nblk, hipStream_t st) {
-  const bool proj = a.dz != nullptr, mask = a.h != nullptr;
-  if (proj && mask) gemm_tn_x3b_kernel<true, true, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
-  else if (proj) gemm_tn_x3b_kernel<true, false, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
-  else if (mask) gemm_tn_x3b_kernel<false, true, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
-  else gemm_tn_x3b_kernel<false, false, KT, NPL, ABF, HBF><<<nblk, TX_THREADS, 0, st>>>(a);
-}
 
-// variant 0 / 1: 16-row chunks (x3, production); 2: 32-row chunks (x3b).  Lab (MI355X, Elliptic
-// layer-1 TN): x3 206-212 us, x3b 224-227 us — both VALU-bound in a staging phase separate from
-// the MFMAs (PMC: ~10 VALU per MFMA, MFMA busy 25 %).  A two-register-set form that interleaves
-// the staging with the MFMAs spilled (the compiler keeps both sets' addresses live), see DESIGN.md.
+// Lab (MI355X, Elliptic layer-1 TN, dz form + mask, same process): classic order 205-215 us,
+// pipelined 200-210, pipelined + interleave hints (production) 192.  A 32-row-chunk variant
+// (single LDS image, 2 barriers per chunk) measured 217-227 us and was removed.
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
   constexpr int D = 1;
-  if (variant <= 1) {
-    if (a.a_bf16) {
-      if (nkt <= 8) { if (a.h_bf16) launch_tn_x3_k<D, 8, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 8, 1, true, false>(a, nblk, st); }
-      else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false>(a, nblk, st); }
-      return;
-    }
-    if (nkt <= 6) launch_tn_x3_k<D, 6>(a, nblk, st);
-    else if (nkt <= 8) launch_tn_x3_k<D, 8>(a, nblk, st);
-    else if (nkt <= 11) launch_tn_x3_k<D, 11>(a, nblk, st);
-    else launch_tn_x3_k<D, 12>(a, nblk, st);
+  if (a.a_bf16) {
+    if (nkt <= 8) { if (a.h_bf16) launch_tn_x3_k<D, 8, 1, true, true, 2>(a, nblk, st); else launch_tn_x3_k<D, 8, 1, true, false, 2>(a, nblk, st); }
+    else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true, 2>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false, 2>(a, nblk, st); }
     return;
   }
-  if (variant == 2) {
-    if (a.a_bf16) {
-      if (nkt <= 8) { if (a.h_bf16) launch_tn_x3b_k<8, 1, true, true>(a, nblk, st); else launch_tn_x3b_k<8, 1, true, false>(a, nblk, st); }
-      else { if (a.h_bf16) launch_tn_x3b_k<12, 1, true, true>(a, nblk, st); else launch_tn_x3b_k<12, 1, true, false>(a, nblk, st); }
-      return;
-    }
-    if (nkt <= 6) launch_tn_x3b_k<6>(a, nblk, st);
-    else if (nkt <= 8) launch_tn_x3b_k<8>(a, nblk, st);
-    else if (nkt <= 11) launch_tn_x3b_k<11>(a, nblk, st);
-    else launch_tn_x3b_k<12>(a, nblk, st);
+  if (variant == 3) {  // lab: classic order (stage c; barrier; MFMAs of c)
+    if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 0>(a, nblk, st);
+    else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 0>(a, nblk, st);
+    else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 0>(a, nblk, st);
+    else launch_tn_x3_k<D, 12, 3, false, false, 0>(a, nblk, st);
     return;
   }
+  // production: pipelined order + interleave hints
+  if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 2>(a, nblk, st);
+  else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 2>(a, nblk, st);
+  else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 2>(a, nblk, st);
+  else launch_tn_x3_k<D, 12, 3, false, false, 2>(a, nblk, st);
 }
 
 }  // namespace gnnmp

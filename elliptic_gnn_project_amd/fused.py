@@ -69,9 +69,9 @@ def _nt_workspace(device, n, k1, k2):
 
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
             out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None):
-    """bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too."""
-    """C = epilogue([a1 | a2] · B) on the MFMA NT kernel; B = bt ([K, n] row-major) or, with bt None,
-    [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2]."""
+    """C = epilogue([a1 | a2] · B) on the NT kernels; B = bt ([K, n] row-major) or, with bt None,
+    [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2].
+    bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too."""
     M = a1.size(0)
     bf = a1.dtype == torch.bfloat16
     if out is None and want_c:
@@ -103,9 +103,11 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         e1.record()
         k = a1.size(1) + (a2.size(1) if a2 is not None else 0)
         # tag: kind, M, K, N, A element bytes, C element bytes, MFMA products per bf16 term
-        # (6 split-bf16, 1 bf16 storage, 0 exact f32)
+        # (6 split-bf16, 1 bf16 storage, 0 exact f32, -1 the VALU kernels of the skinny shapes)
         ea = a1.element_size()
         prod = 0 if (_math(math) == _lib.MATH_F32 or w1 is None) else (1 if ea == 2 else 6)
+        if ea == 4 and proj is None and (n <= 8 or (k <= 8 and a2 is None)):
+            prod = -1
         KernelTimer.records.append((("gemm_nt", M, k, n, ea, out.element_size() if out is not None else 0, prod),
                                     e0, e1, 2 * M * k * n))
     return out
@@ -142,6 +144,8 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         e1.record()
         ea = a1.element_size()
         prod = 0 if _math(math) == _lib.MATH_F32 else (1 if ea == 2 else 6)
+        if ea == 4 and nr <= 8 and dz is None and h is None and gout is None:
+            prod = -1
         KernelTimer.records.append((("gemm_tn", M, k1 + k2, nr, ea, h.element_size() if h is not None else 4, prod),
                                     e0, e1, 2 * M * (k1 + k2) * nr))
     o = 0

@@ -145,6 +145,61 @@ def test_gemm_tn(device, M, nr, k1, k2, form, math):
         assert rel_l2(dzs, dz.sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("M,k1,k2,n", [(50000, 64, 0, 2), (3001, 166, 166, 2), (1000, 7, 9, 5), (777, 384, 0, 8),
+                                       (4097, 2, 0, 64), (1000, 3, 0, 33), (513, 8, 0, 256), (100, 1, 0, 1)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu", "dropout"])
+@pytest.mark.parametrize("wform", [False, True])
+def test_gemm_nt_skinny(device, M, k1, k2, n, epi, wform):
+    """Narrow output-layer shapes (N <= 8, or K <= 8) on the VALU kernels (gemm_skinny.hip):
+    full f32 arithmetic, the NT epilogue (bias, ReLU, counter-hash dropout) unchanged."""
+    from elliptic_gnn_project_amd.fused import gemm_nt
+
+    if wform and n > 128:
+        pytest.skip("w1/w2 form needs N <= 128")
+    g = torch.Generator().manual_seed(M + k1 + 3 * n)
+    a1 = torch.randn(M, k1, generator=g)
+    a2 = torch.randn(M, k2, generator=g) if k2 else None
+    bt = torch.randn(k1 + k2, n, generator=g) / (k1 + k2) ** 0.5
+    bias = torch.randn(n, generator=g)
+    A = torch.cat([a1, a2], 1) if k2 else a1
+    ref = (A.double() @ bt.double()).float()
+    kw = {}
+    if epi != "plain":
+        ref = torch.relu(ref + bias)
+        kw = dict(bias=bias.to(device), relu=True)
+    if epi == "dropout":
+        p = 0.4
+        m = torch.from_numpy(keep_mask(99, M, n, p))
+        ref = ref * m / (1 - np.float32(p))
+        kw.update(dropout_p=p, seed=99)
+    if wform:
+        kw.update(w1=bt[:k1].t().contiguous().to(device), w2=bt[k1:].t().contiguous().to(device) if k2 else None)
+    for math in ("split_bf16", "f32"):
+        c = gemm_nt(a1.to(device), None if wform else bt.to(device), n,
+                    a2=a2.to(device) if a2 is not None else None, math=math, **kw)
+        torch.testing.assert_close(c.cpu(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,nr,k1,k2", [(50000, 2, 64, 0), (3001, 2, 166, 166), (1000, 5, 7, 9), (777, 8, 384, 0),
+                                        (1000, 1, 3, 0), (203769, 2, 64, 0)])
+def test_gemm_tn_skinny(device, M, nr, k1, k2):
+    """dW = Gᵀ·A and db = Σ G for Nr <= 8 (plain g form) on the VALU kernel; deterministic."""
+    from elliptic_gnn_project_amd.fused import gemm_tn
+
+    g_ = torch.Generator().manual_seed(M + 7 * nr)
+    a1 = torch.randn(M, k1, generator=g_)
+    a2 = torch.randn(M, k2, generator=g_) if k2 else None
+    A = torch.cat([a1, a2], 1) if k2 else a1
+    G = torch.randn(M, nr, generator=g_)
+    a1d, a2d = a1.to(device), a2.to(device) if a2 is not None else None
+    dW, db, _, _ = gemm_tn(nr, a1d, a2d, g=G.to(device))
+    dWfull = torch.cat([dW[0], dW[1]], 1) if dW[1] is not None else dW[0]
+    assert rel_l2(dWfull, G.double().t() @ A.double()) < 1e-6
+    assert rel_l2(db, G.double().sum(0)) < 1e-6
+    dW2, db2, _, _ = gemm_tn(nr, a1d, a2d, g=G.to(device))
+    assert torch.equal(dW2[0], dW[0]) and torch.equal(db2, db)
+
+
 def _graph(n, e, seed):
     from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
 

@@ -194,7 +194,8 @@ def test_gcn_conv(device, dims):
 
 
 @pytest.mark.parametrize("cfg", [(166, 8, 4, True), (166, 16, 4, True), (32, 2, 1, False), (24, 3, 2, False),
-                                 (40, 5, 8, True)])
+                                 (40, 5, 8, True), (32, 64, 4, True), (16, 72, 4, True), (20, 4, 2, False),
+                                 (12, 6, 2, True)])
 def test_gat_conv(device, cfg):
     from elliptic_gnn_project_amd.conv import GATConv
 
