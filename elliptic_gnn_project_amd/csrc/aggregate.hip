@@ -254,9 +254,8 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 // Wave-wide groups (LPS = 64, F/VEC > 32 chunks, e.g. the 166-wide layer-1 features):
 // every row boundary and neighbour id is wave-uniform, so they live in SGPRs (scalar loads,
 // v_readlane) and the next U neighbour ids are prefetched while the current U rows load.
-template <int MODE, int VEC, int NCH, bool BF = false>  // BF: x and y hold bf16 (no split partials)
+template <int MODE, int VEC, int NCH, bool BF = false, int U = 8>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
-  constexpr int U = 8;
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t r0 = wave * rpg;
@@ -669,9 +668,9 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     if (lps == 64 && nchunk <= 128) {  // wave-uniform fast path (scalar row/neighbour handling)
       const int rpw = 16;
       const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
-      if (vec == 4) agg_wave_kernel<MODE, 4, 2><<<wblocks, 256, 0, st>>>(a, rpw);
-      else if (vec == 2) agg_wave_kernel<MODE, 2, 2><<<wblocks, 256, 0, st>>>(a, rpw);
-      else agg_wave_kernel<MODE, 1, 2><<<wblocks, 256, 0, st>>>(a, rpw);
+      if (vec == 4) agg_wave_kernel<MODE, 4, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
+      else if (vec == 2) agg_wave_kernel<MODE, 2, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
+      else agg_wave_kernel<MODE, 1, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
     } else if (vec == 4) GNN_FLAT_V(4);
     else if (vec == 2) GNN_FLAT_V(2);
     else GNN_FLAT_V(1);

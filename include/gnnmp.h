@@ -213,6 +213,9 @@ typedef enum {
                               used for the w1/w2 NT form and the TN kernel, else falls back to: */
   GNN_MATH_F32 = 1         /* exact f32 MFMA (v_mfma_f32_32x32x2_f32, a k-ordered fmaf chain) */
 } gnn_gemm_math;
+/* Skinny shapes run full-f32 VALU kernels whatever `math` says (the 2-class output layers,
+ * gnn.py:23,66,124): NT with N <= 8 (K <= 384) or with K <= 8 (one A segment), f32 A/C and no
+ * projection; TN with Nr <= 8 in the plain g form (no dz/proj, h or gout) and f32 A. */
 
 typedef struct {
   int64_t M, N;                          /* C is [M, N] */
