@@ -99,7 +99,8 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
         out = torch.empty((N, F), dtype=torch.float32, device=x.device)
     if addend is not None:
         addend = _as_f32_rows(addend)
-    # partial-sum rows for the long-segment split (used by the lane-group gather, 8 < F <= 128)
+    # partial-sum rows for the long-segment split (used by the lane-group gather, 8 < F <= 128;
+    # the narrow F <= 4 kernels measured no faster with it on the bench graph)
     npieces = plan.split_pieces(transpose) if (mode != _lib.AGG_EDGE_W and 8 < F <= 128) else 0
     part = torch.empty(npieces * F, dtype=torch.float32, device=x.device) if npieces else None
     p = _lib.GnnAggParams(

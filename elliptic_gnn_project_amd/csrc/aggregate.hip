@@ -426,6 +426,20 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   const int64_t rlast = min(r0 + 64, a.nrows);
   const int32_t wend = __builtin_amdgcn_readfirstlane(a.ptr[rlast]);
   const int F = a.F;
+  // the row's epilogue operands (1/deg, root addend, bias) are loaded up front, in flight with
+  // the gather instead of one more dependent round trip after it
+  float pdeg = 1.0f, padd[4] = {0.f, 0.f, 0.f, 0.f}, pbias[4] = {0.f, 0.f, 0.f, 0.f};
+  if (rok) {
+    if constexpr (MODE == GNN_AGG_MEAN) pdeg = fmaxf(a.nodew[r], 1.0f);
+    if (a.add) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) padd[f] = f < F ? a.add[r * a.ld_add + f] : 0.0f;
+    }
+  }
+  if (a.bias) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) pbias[f] = f < F ? a.bias[f] : 0.0f;
+  }
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float* buf = sv[w];
   for (int32_t pb = base; pb < wend; pb += kNarrowCap) {
@@ -476,8 +490,11 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
         float t[1] = {acc[f]};
         if (p0 >= 0) {
           a.part[(int64_t)p0 * F + f] = t[0];
-        } else {
-          finish<MODE, 1>(a, r, f, t);
+        } else {  // finish<MODE, 1> with the preloaded operands (same operation order)
+          if constexpr (MODE == GNN_AGG_MEAN) t[0] = t[0] / pdeg;
+          if (a.add) t[0] += padd[f];
+          if (a.bias) t[0] += pbias[f];
+          if (a.relu) t[0] = fmaxf(t[0], 0.0f);
           a.y[r * a.ldy + f] = t[0];
         }
       }

@@ -487,22 +487,21 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   auto store = [&](int d, int c) {
     const int buf = c & 1;
     const int64_t m0 = mbeg + (int64_t)c * TMC;
+    const int nrow = (int)min((int64_t)TMC, mend - m0);  // valid rows of this chunk (32-bit compares)
     if constexpr (PROJ) {  // slot read by G(c - 1), behind barrier c - 1 (threads >= 64: unused)
       const bool ok = tid < TMC * MAXPROJ && zq < a.nproj && m0 + TMC + zr < mend;
       dzL[(c + 1) & 1][tid] = ok ? rz[d] : 0.0f;
     }
+    // A is stored unmasked: rows past mend were loaded clamped (finite copies of the last row)
+    // and meet G = 0 there; columns >= Kc (padding, idle slots at KMAX - 1) only feed dW
+    // columns that are never written out
 #pragma unroll
-    for (int sl = 0; sl < TX_AS; ++sl) {  // unconditional (idle slots: column KMAX - 1, zeros)
-      float e[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) e[i] = (ak[sl] < Kc && m0 + 8 * oct[sl] + i < mend) ? rv[d][sl][i] : 0.0f;
-      put8(At[buf] + ak[sl] * TP + 8 * oct[sl], TAPL, e);
-    }
+    for (int sl = 0; sl < TX_AS; ++sl) put8(At[buf] + ak[sl] * TP + 8 * oct[sl], TAPL, rv[d][sl]);
     float e[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = 8 * go + i;
-      const bool rok = m0 + r < mend;
+      const bool rok = r < nrow;
       const bool ok = rok && gcol;
       float g;
       if constexpr (PROJ) {
