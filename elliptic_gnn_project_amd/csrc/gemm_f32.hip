@@ -892,7 +892,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->h_dtype != GNN_DTYPE_F32 && p->h_dtype != GNN_DTYPE_BF16))
     return fail(GNN_ERR_INVALID_ARG, __fn, "bad dtype");
   if (a.h_bf16 && !a.a_bf16) return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 h needs bf16 A");
-  // the split kernel indexes rows with 32-bit element offsets
+  // widest row pitch of any operand (the split kernel uses 32-bit element offsets)
   const int64_t ldmax = std::max({a.lda1, a.k2 > 0 ? a.lda2 : 0, a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
   if (variant == 0 && tn_skinny_ok(a)) {  // Nr <= 8 plain g form: VALU stream (gemm_skinny.hip)
     nblk = tn_skinny_blocks(a.M);
@@ -904,9 +904,10 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
     GNN_LAUNCH_CHECK();
     return GNN_OK;
   }
-  if (a.a_bf16 && (p->math == GNN_MATH_F32 || (a.M + 32) * ldmax >= ((int64_t)1 << 31)))
-    return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 TN needs split math and M*ld < 2^31");
-  if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31)) {
+  // the split kernel indexes rows with 32-bit element offsets and loads whole 16-row chunks
+  if (a.a_bf16 && (p->math == GNN_MATH_F32 || (a.M + 32) * ldmax >= ((int64_t)1 << 31) || a.M < 16))
+    return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 TN needs split math, M >= 16 and M*ld < 2^31");
+  if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31) && a.M >= 16) {
     launch_tn_x3(a, nblk, st, variant);  // split-bf16 MFMA (gemm_x3.hip)
     GNN_LAUNCH_CHECK();
     slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);

@@ -449,28 +449,29 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   const int zqc = PROJ ? min(zq, a.nproj - 1) : 0;
 
   // 32-bit element offsets (the dispatcher guarantees M·ld < 2^31): rows clamped to mend - 1
-  const int mlast = (int)(mend - 1);
-  uint32_t olast[NS];  // offset of the block's last row: clamping offsets = clamping rows (ld >= 0)
-#pragma unroll
-  for (int sl = 0; sl < NS; ++sl) olast[sl] = (uint32_t)(mlast * ld32[sl]);
+  // Chunk c covers rows [mbeg + 16c, +16) but is LOADED from row ldbase(c) = min(that, M - 16)
+  // (the dispatcher guarantees M >= 16): every load is in bounds with no per-element clamp,
+  // rows past mend belong to the next block or repeat earlier rows, and the G mask (rows
+  // [lo, hi) of the loaded chunk) zeroes them.
+  const int Mi = (int)a.M;
+  auto ldbase = [&](int c) { return min((int)mbeg + c * TMC, Mi - TMC); };
   float rv[D][NS][8];
   float rz[D];
   auto load = [&](int d, int c) {
-    const int m0 = (int)mbeg + c * TMC;
+    const int mb = ldbase(c);
 #pragma unroll
     for (int sl = 0; sl < NS; ++sl) {
-      uint32_t o = (uint32_t)((m0 + 8 * oct[sl]) * ld32[sl]);  // one multiply per slot (rows by adds)
+      uint32_t o = (uint32_t)((mb + 8 * oct[sl]) * ld32[sl]);  // one multiply per slot (rows by adds)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const uint32_t off = min(o, olast[sl]);
+        const uint32_t off = o;
         o += (uint32_t)ld32[sl];
         const bool bf = sl < TX_AS ? ABF : (sl == GS && MASK ? HBF : false);  // compile-time per slot
         rv[d][sl][i] = bf ? bf16_to_f32(reinterpret_cast<const uint16_t*>(base[sl])[off]) : base[sl][off];
       }
     }
     if constexpr (PROJ) {  // dz rows of chunk c + 1
-      const int m = min(m0 + TMC + zr, mlast);
-      rz[d] = a.dz[(uint32_t)(m * (int)a.lddz + zqc)];
+      rz[d] = a.dz[(uint32_t)((ldbase(c + 1) + zr) * (int)a.lddz + zqc)];
     }
   };
 
@@ -486,10 +487,13 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   };
   auto store = [&](int d, int c) {
     const int buf = c & 1;
-    const int64_t m0 = mbeg + (int64_t)c * TMC;
-    const int nrow = (int)min((int64_t)TMC, mend - m0);  // valid rows of this chunk (32-bit compares)
+    const int mb = ldbase(c);
+    const int rlo = (int)mbeg + c * TMC - mb;  // valid loaded rows: [rlo, rhi)
+    const int rhi = (int)mend - mb;
     if constexpr (PROJ) {  // slot read by G(c - 1), behind barrier c - 1 (threads >= 64: unused)
-      const bool ok = tid < TMC * MAXPROJ && zq < a.nproj && m0 + TMC + zr < mend;
+      const int mb1 = ldbase(c + 1);
+      const bool ok = tid < TMC * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + (c + 1) * TMC - mb1 &&
+                      zr < (int)mend - mb1;
       dzL[(c + 1) & 1][tid] = ok ? rz[d] : 0.0f;
     }
     // A is stored unmasked: rows past mend were loaded clamped (finite copies of the last row)
@@ -501,7 +505,7 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int r = 8 * go + i;
-      const bool rok = r < nrow;
+      const bool rok = r >= rlo && r < rhi;
       const bool ok = rok && gcol;
       float g;
       if constexpr (PROJ) {
@@ -521,7 +525,7 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
       g = ok ? g : 0.0f;
       db += g;
       if constexpr (GOUT) {
-        if (a.gout && ok) a.gout[(m0 + r) * a.ldgout + gn] = g;
+        if (a.gout && ok) a.gout[(int64_t)(mb + r) * a.ldgout + gn] = g;
       }
       e[i] = g;
     }
@@ -550,8 +554,9 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 
   if (nch > 0) {
     if constexpr (PROJ) {  // dz of chunk 0
-      const int64_t m = mbeg + zr;
-      dzL[0][tid] = (tid < TMC * MAXPROJ && zq < a.nproj && m < mend) ? a.dz[m * a.lddz + zqc] : 0.0f;
+      const int mb0 = ldbase(0);
+      const bool ok0 = tid < TMC * MAXPROJ && zq < a.nproj && zr >= (int)mbeg - mb0 && zr < (int)mend - mb0;
+      dzL[0][tid] = ok0 ? a.dz[(int64_t)(mb0 + zr) * a.lddz + zqc] : 0.0f;
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) load(d, min(d, nch - 1));

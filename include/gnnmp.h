@@ -255,7 +255,8 @@ typedef struct {
   const float* a1; int64_t lda1; int64_t k1;
   const float* a2; int64_t lda2; int64_t k2;
   int32_t math;                          /* gnn_gemm_math */
-  int32_t a_dtype;                       /* gnn_dtype of A1/A2 (BF16: G rounded to bf16, one product) */
+  int32_t a_dtype;                       /* gnn_dtype of A1/A2 (BF16: G rounded to bf16, one product;
+                                            needs M >= 16) */
   int32_t h_dtype;                       /* gnn_dtype of h */
 } gnn_gemm_tn_params;
 
