@@ -76,10 +76,18 @@ int main(int argc, char** argv) {
   const int64_t M = argc > 1 ? std::atoll(argv[1]) : 203769;
   const int rounds = argc > 2 ? std::atoi(argv[2]) : 7;
   const int64_t F = std::getenv("LAB_F") ? std::atoll(std::getenv("LAB_F")) : 166, H = 128;
+  // LAB_PAD: rows stored with a 16-byte pitch (ld = F rounded up to 4), pad columns NaN (must be ignored)
+  const int64_t LD = std::getenv("LAB_PAD") ? (F + 3) / 4 * 4 : F;
   auto h_agg = host_rand(M * F, 1.f, 1), h_x = host_rand(M * F, 1.f, 2);
   auto h_w = host_rand(2 * F * H, 0.08f, 7), h_bias = host_rand(H, 0.1f, 4), h_proj = host_rand(4 * H, 0.1f, 5);
   auto h_dz = host_rand(M * 4, 1e-3f, 6);
-  float *agg = to_dev(h_agg), *x = to_dev(h_x), *w = to_dev(h_w), *bias = to_dev(h_bias), *proj = to_dev(h_proj);
+  auto pad = [&](const std::vector<float>& v) {
+    std::vector<float> o(M * LD, std::nanf(""));
+    for (int64_t r = 0; r < M; ++r) std::copy(v.begin() + r * F, v.begin() + (r + 1) * F, o.begin() + r * LD);
+    return o;
+  };
+  float *agg = to_dev(LD == F ? h_agg : pad(h_agg)), *x = to_dev(LD == F ? h_x : pad(h_x));
+  float *w = to_dev(h_w), *bias = to_dev(h_bias), *proj = to_dev(h_proj);
   float* dz = to_dev(h_dz);
   float *c, *z;
   CK(hipMalloc(&c, M * H * sizeof(float)));
@@ -87,8 +95,8 @@ int main(int argc, char** argv) {
 
   gnn_gemm_nt_params p{};
   p.M = M; p.N = H;
-  p.a1 = agg; p.lda1 = F; p.k1 = F;
-  p.a2 = x; p.lda2 = F; p.k2 = F;
+  p.a1 = agg; p.lda1 = LD; p.k1 = F;
+  p.a2 = x; p.lda2 = LD; p.k2 = F;
   p.w1 = w; p.w2 = w + F * H; p.ldw1 = F; p.ldw2 = F;
   p.c = c; p.ldc = H; p.bias = bias; p.relu = 1; p.dropout_p = 0.5f; p.seed = 1234;
   p.proj = proj; p.nproj = 4; p.z = z; p.ldz = 4;
@@ -105,7 +113,7 @@ int main(int argc, char** argv) {
     GK(gnnx_gemm_nt_variant_f32(&p, 16, nullptr));
     gnn_gemm_tn_params q{};
     q.M = M; q.Nr = H; q.dz = dz; q.lddz = 4; q.proj = proj; q.nproj = 4; q.h = c; q.ldh = H; q.hscale = 2.f;
-    q.a1 = agg; q.lda1 = F; q.k1 = F; q.a2 = x; q.lda2 = F; q.k2 = F;
+    q.a1 = agg; q.lda1 = LD; q.k1 = F; q.a2 = x; q.lda2 = LD; q.k2 = F;
     size_t wsb = 0;
     GK(gnn_gemm_tn_workspace_size(M, H, 2 * F, 4, &wsb));
     void* ws;
@@ -183,7 +191,7 @@ int main(int argc, char** argv) {
   GK(gnnx_gemm_nt_variant_f32(&p, 16, nullptr));
   gnn_gemm_tn_params q{};
   q.M = M; q.Nr = H; q.dz = dz; q.lddz = 4; q.proj = proj; q.nproj = 4; q.h = c; q.ldh = H; q.hscale = 2.f;
-  q.a1 = agg; q.lda1 = F; q.k1 = F; q.a2 = x; q.lda2 = F; q.k2 = F;
+  q.a1 = agg; q.lda1 = LD; q.k1 = F; q.a2 = x; q.lda2 = LD; q.k2 = F;
   size_t wsb = 0;
   GK(gnn_gemm_tn_workspace_size(M, H, 2 * F, 4, &wsb));
   void* ws;

@@ -11,8 +11,20 @@ namespace gnnmp {
 // Dropout keep decision for element `idx` of a call seeded with `seed`: murmur3's fmix32
 // over (idx * golden + seed_lo) ^ seed_hi, top 24 bits compared with (1-p)·2^24.  32-bit
 // arithmetic only (3 multiplies).  Mirrored bit for bit by oracle/dropout_hash.py.
+constexpr uint32_t kDropGolden = 0x9E3779B1u;
+// keep_elem from the premixed first term h0 = idx * kDropGolden + (uint32_t)seed, which a tile
+// epilogue forms by additions (the map idx -> h0 is linear mod 2^32): two multiplies per element.
+__device__ __forceinline__ bool keep_premixed(uint32_t h, uint64_t seed, uint32_t keep_thresh) {
+  h ^= (uint32_t)(seed >> 32);
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return (h >> 8) < keep_thresh;
+}
 __device__ __forceinline__ bool keep_elem(uint64_t seed, uint32_t idx, uint32_t keep_thresh) {
-  uint32_t h = idx * 0x9E3779B1u + (uint32_t)seed;
+  uint32_t h = idx * kDropGolden + (uint32_t)seed;
   h ^= (uint32_t)(seed >> 32);
   h ^= h >> 16;
   h *= 0x85EBCA6Bu;
@@ -55,18 +67,21 @@ __device__ __forceinline__ void nt_epilogue(const NTArgs& a, floatx16 (&acc)[TM]
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     const int64_t rbase = m0 + wave * 32 * TM + tm * 32 + 4 * (lane >> 5);
+    const uint32_t hstep = (uint32_t)a.Nc * kDropGolden;  // premixed hash step per row
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int col = n0 + t * 32 + (lane & 31);
       const bool colok = col < a.Nc;
       const float bv = (a.bias && colok) ? a.bias[col] : 0.0f;
+      const uint32_t h0 = ((uint32_t)rbase * (uint32_t)a.Nc + (uint32_t)col) * kDropGolden + (uint32_t)seed;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
         float v = acc[tm][t][r] + bv;
         if (a.relu) v = fmaxf(v, 0.0f);
-        if (a.dropout)
-          v = keep_elem(seed, (uint32_t)row * (uint32_t)a.Nc + (uint32_t)col, a.keep_thresh) ? v * a.drop_scale : 0.0f;
+        if (a.dropout)  // == keep_elem(seed, row * Nc + col, thresh), bit for bit
+          v = keep_premixed(h0 + (uint32_t)((r & 3) + 8 * (r >> 2)) * hstep, seed, a.keep_thresh) ? v * a.drop_scale
+                                                                                                 : 0.0f;
         if (!colok) v = 0.0f;
         if constexpr (CBF) {
           const uint16_t b = f32_to_bf16(v);
