@@ -359,7 +359,6 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
 // (dwordx4 DMA of the swizzled image, lane-linear).  A 3-stage ring keeps two chunks in flight
 // behind a counted vmcnt and a raw s_barrier (one per chunk); each lane splits its own A
 // fragment after reading it (2 ds_read_b128) and feeds the MFMAs directly.
-constexpr int XG_S = 3;                        // LDS stages
 constexpr int XG_A = 128 * 16 * 4;             // raw f32 A tile per stage (8 KB)
 constexpr int XG_B = 3 * 128 * 16 * 2;         // pre-split B image per stage (12 KB)
 constexpr int XG_ST = XG_A + XG_B;
@@ -500,6 +499,143 @@ __global__ __launch_bounds__(256) void gemm_nt_x3g_kernel(NTArgs a, const uint4*
   }
   if (c < nchunks) step(L0, L2, c);
   if (c + 1 < nchunks) step(L1, L0, c + 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  nt_epilogue<1, false>(a, acc, m0, n0, lane, wave, seed);
+}
+
+// 32-deep chunks ("x3h"): with 16-byte A rows, every A DMA instruction moves 8 full 128-byte
+// row lines (4 per wave per chunk) and each barrier covers 48 MFMAs.  B: two 16-deep image
+// chunks per stage.  S = 2 or 3 LDS stages of 40 KB.
+constexpr int XH_A = 128 * 32 * 4;  // 16 KB raw f32 A
+constexpr int XH_B = 2 * XG_B;      // 24 KB pre-split B
+constexpr int XH_ST = XH_A + XH_B;
+
+template <int S>
+__global__ __launch_bounds__(256) void gemm_nt_x3h_kernel(NTArgs a, const uint4* __restrict__ bimg,
+                                                          const float* __restrict__ zeros) {
+  __shared__ __attribute__((aligned(16))) char L0[XH_ST];
+  __shared__ __attribute__((aligned(16))) char L1[XH_ST];
+  __shared__ __attribute__((aligned(16))) char L2[S == 3 ? XH_ST : 16];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * 128;
+  const int n0 = blockIdx.y * BN;
+  const int nch1 = (a.k1 + 31) / 32;
+  const int nchunks = nch1 + (a.k2 + 31) / 32;
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+
+  floatx16 acc[1][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][t][r] = 0.0f;
+
+  // A DMA: instruction j of wave w fills rows 8(4w + j) .. +8 (1 KB); lane l -> row + (l >> 3),
+  // physical quad l & 7 holding logical quad (l & 7) ^ ((row >> 1) & 7)
+  int64_t arow[4];
+  int akq[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t r = m0 + 8 * (4 * wave + j) + (lane >> 3);
+    arow[j] = r < a.M ? r : a.M - 1;
+    akq[j] = 4 * ((lane & 7) ^ ((4 * (j & 1) + (lane >> 4)) & 7));
+  }
+  auto issue = [&](char* st, int c) {
+    const float* A; int64_t lda; int k0, klen;
+    if (c < nch1) { A = a.a1; lda = a.lda1; k0 = c * 32; klen = min(32, a.k1 - k0); }
+    else { A = a.a2; lda = a.lda2; k0 = (c - nch1) * 32; klen = min(32, a.k2 - k0); }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* src = akq[j] < klen ? A + arow[j] * lda + k0 + akq[j] : zeros;
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + (4 * wave + j) * 1024), 16, 0, 0);
+    }
+    const char* bsrc = reinterpret_cast<const char*>(bimg) + (int64_t)c * XH_B;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int b = 6 * wave + j;
+      __builtin_amdgcn_global_load_lds(bsrc + (b * 64 + lane) * 16, (lds_ptr_t)(st + XH_A + b * 1024), 16, 0, 0);
+    }
+  };
+  const int frow = wave * 32 + (lane & 31);
+  const int kh = lane >> 5;
+  const int fsw = (frow >> 1) & 7;
+  uint32_t aoff[2][2];
+#pragma unroll
+  for (int sc = 0; sc < 2; ++sc)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) aoff[sc][h] = frow * 128 + 16 * ((4 * sc + 2 * kh + h) ^ fsw);
+  const uint32_t boff = XH_A + ((lane & 31) * 16 + 8 * (kh ^ (((lane & 31) >> 3) & 1))) * 2;
+  auto compute = [&](const char* st, int c) {
+    const int klen = c < nch1 ? min(32, a.k1 - c * 32) : min(32, a.k2 - (c - nch1) * 32);
+    const uint32_t sb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)st;
+#pragma unroll
+    for (int sc = 0; sc < 2; ++sc) {  // two 16-deep sub-chunks; <= 14 LDS reads in flight (lgkmcnt <= 15)
+      u32x4 lo, hi, b[4][3];
+      asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(sb + aoff[sc][0]));
+      asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(sb + aoff[sc][1]));
+      const uint32_t ba = sb + boff + sc * XG_B;
+#define GNN_XH_RB(T, P) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(b[T][P]) : "v"(ba), "i"((P * 128 + T * 32) * 32))
+      GNN_XH_RB(0, 0); GNN_XH_RB(0, 1); GNN_XH_RB(0, 2);
+      GNN_XH_RB(1, 0); GNN_XH_RB(1, 1); GNN_XH_RB(1, 2);
+      GNN_XH_RB(2, 0); GNN_XH_RB(2, 1); GNN_XH_RB(2, 2);
+      GNN_XH_RB(3, 0); GNN_XH_RB(3, 1); GNN_XH_RB(3, 2);
+#undef GNN_XH_RB
+      asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(lo), "+v"(hi), "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]));
+      const int kb = 16 * sc + 8 * kh;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lo[i] = kb + i < klen ? lo[i] : 0u;
+        hi[i] = kb + 4 + i < klen ? hi[i] : 0u;
+      }
+      uint32_t w[4][3];
+      split_pair(__uint_as_float(lo[0]), __uint_as_float(lo[1]), w[0]);
+      split_pair(__uint_as_float(lo[2]), __uint_as_float(lo[3]), w[1]);
+      split_pair(__uint_as_float(hi[0]), __uint_as_float(hi[1]), w[2]);
+      split_pair(__uint_as_float(hi[2]), __uint_as_float(hi[3]), w[3]);
+      bf16x8 af[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) af[p] = __builtin_bit_cast(bf16x8, make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]));
+      auto mm = [&](int t) {
+        const bf16x8 bf[3] = {__builtin_bit_cast(bf16x8, b[t][0]), __builtin_bit_cast(bf16x8, b[t][1]),
+                              __builtin_bit_cast(bf16x8, b[t][2])};
+        acc[0][t] = mfma6(af, bf, acc[0][t]);
+      };
+      mm(0);
+      asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2]));
+      mm(1);
+      asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[2][2]));
+      mm(2);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[3][0]), "+v"(b[3][1]), "+v"(b[3][2]));
+      mm(3);
+    }
+  };
+  auto step = [&](char* cur, char* nxt, int c) {
+    if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");  // 4 A + 6 B per chunk
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(nxt, min(c + S - 1, nchunks - 1));  // clamped: the tail refills stages never read again
+    compute(cur, c);
+  };
+
+  issue(L0, 0);
+  int c = 0;
+  if constexpr (S == 3) {
+    issue(L1, min(1, nchunks - 1));
+    for (; c + 3 <= nchunks; c += 3) {
+      step(L0, L2, c);
+      step(L1, L0, c + 1);
+      step(L2, L1, c + 2);
+    }
+    if (c < nchunks) step(L0, L2, c);
+    if (c + 1 < nchunks) step(L1, L0, c + 1);
+  } else {
+    for (; c + 2 <= nchunks; c += 2) {
+      step(L0, L1, c);
+      step(L1, L0, c + 1);
+    }
+    if (c < nchunks) step(L0, L1, c);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   nt_epilogue<1, false>(a, acc, m0, n0, lane, wave, seed);
 }
@@ -810,8 +946,9 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 
 }  // namespace
 
-size_t nt_x3_workspace(int64_t k1, int64_t k2) {  // pre-split B image, 12 KB per 16-deep chunk,
-  return (size_t)((k1 + 15) / 16 + (k2 + 15) / 16) * 3 * 256 * sizeof(uint4) + 64;  // + 64 B of zeros
+size_t nt_x3_workspace(int64_t k1, int64_t k2) {  // pre-split B image, 12 KB per 16-deep chunk
+  // (segments padded to 32-deep chunks for the x3h form), + 64 B of zeros
+  return (size_t)(2 * ((k1 + 31) / 32) + 2 * ((k2 + 31) / 32)) * 3 * 256 * sizeof(uint4) + 64;
 }
 
 // variant: 0 = production; others are lab tilings (bench_gemm.cpp).
@@ -861,7 +998,9 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
   // (fragment-shaped loads touch 32 rows per instruction).  LDS-DMA form (gemm_nt_x3g_kernel,
   // 3-stage ring, counted vmcnt, asm fragment reads): 167 with dword A DMA, 151 with dwordx4 A
   // DMA on 16-byte rows, 102 with the A DMA removed — the A tile's 64-byte row pieces, not the
-  // MFMA phase, bound it; classic 145-154 in the same runs.
+  // MFMA phase, bound it; classic 145-154 in the same runs.  32-deep DMA chunks (x3h: full
+  // 128-byte row lines, 48 MFMAs per barrier, 2 or 3 stages of 40 KB) 143-149 = classic.
+  // TM = 2 (a wave owns 64 rows, 128 AGPRs, one wave per SIMD) 216-233.
   if (!bimg) {  // no workspace: B split in-kernel
     launch_nt_x3_a<16, 1, 2, 2>(a, av, nullptr, st);
     return;
@@ -880,6 +1019,16 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
       const dim3 g((unsigned)ceil_div(a.M, 128), (unsigned)ceil_div(a.Nc, BN));
       if (variant == 11 && av == 4) gemm_nt_x3g_kernel<true><<<g, 256, 0, st>>>(a, bimg, zeros);
       else gemm_nt_x3g_kernel<false><<<g, 256, 0, st>>>(a, bimg, zeros);
+      break;
+    }
+    case 12: case 13: {  // lab: 32-deep LDS-DMA form (16-byte A rows only); 12: 3 stages, 13: 2 stages
+      if (av != 4) { launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st); break; }
+      const int nch1 = 2 * ((a.k1 + 31) / 32), nch = nch1 + 2 * ((a.k2 + 31) / 32);
+      x3_presplit_b_kernel<<<nch, 256, 0, st>>>(a, static_cast<uint4*>(ws), nch1, nch, 1);
+      const float* zeros = reinterpret_cast<const float*>(static_cast<const char*>(ws) + (size_t)nch * XG_B);
+      const dim3 g((unsigned)ceil_div(a.M, 128), (unsigned)ceil_div(a.Nc, BN));
+      if (variant == 12) gemm_nt_x3h_kernel<3><<<g, 256, 0, st>>>(a, bimg, zeros);
+      else gemm_nt_x3h_kernel<2><<<g, 256, 0, st>>>(a, bimg, zeros);
       break;
     }
     default:  // production: classic order (branch-free MFMA phase)
