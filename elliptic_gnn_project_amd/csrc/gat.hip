@@ -338,16 +338,19 @@ __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g
     float e0 = -INFINITY;
     if (lig < npair) e0 = leaky(a.a_s[(int64_t)a.col[beg + (lig >> g.lgH)] * H + hl] + adr, a.slope);
     float m = e0;
+#pragma unroll 1
     for (int32_t idx = lig + G; idx < npair; idx += G)
       m = fmaxf(m, leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope));
     for (int off = G >> 1; off >= H; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
     float s = lig < npair ? expf(e0 - m) : 0.0f;
+#pragma unroll 1
     for (int32_t idx = lig + G; idx < npair; idx += G)
       s += expf(leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope) - m);
     for (int off = G >> 1; off >= H; off >>= 1) s += __shfl_xor(s, off);
     const float denom = s + 1e-16f;
     float* alpha_r = a.alpha + (int64_t)beg * H;
     if (lig < npair) alpha_r[lig] = expf(e0 - m) / denom;
+#pragma unroll 1
     for (int32_t idx = lig + G; idx < npair; idx += G)
       alpha_r[idx] = expf(leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope) - m) / denom;
     // slot view
@@ -358,6 +361,7 @@ __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc.v[i] = 0.0f;
     if (slot_ok) {
+#pragma unroll 2
       for (int32_t k = beg + ep; k < end; k += EP) {
         const int32_t j = a.col[k];
         const float al = expf(leaky(a.a_s[(int64_t)j * H + hs] + ads, a.slope) - ms) / dn;
