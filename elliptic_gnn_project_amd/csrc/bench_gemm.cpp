@@ -224,7 +224,7 @@ int main(int argc, char** argv) {
         for (int k = 0; k < F; ++k) rdw[H * F + n * F + k] += g[n] * h_x[m * F + k];
       }
     }
-    for (int math : {1, 0, 3}) {  // 1: exact f32; 0: split-bf16 (production); 3: split-bf16, classic order
+    for (int math : {1, 0, 3}) {  // 1: exact f32; 0: split-bf16 (production); 3: pipelined order
       qc.math = math >= 2 ? 0 : math;
       GK(gnnx_gemm_tn_variant_f32(&qc, out, ws, wsb, math >= 2 ? math : 0, nullptr));
       auto got = to_host(out, nout);
@@ -239,16 +239,16 @@ int main(int argc, char** argv) {
                   (long long)Mc, std::sqrt(se / sr), mx, rmx, dbe);
     }
   }
-  const int tmaths[3] = {1, 0, 3};
-  std::vector<float> tt[3];
+  const int tmaths[4] = {1, 0, 3, 4};
+  std::vector<float> tt[4];
   auto tn_run = [&](int math) {
     q.math = math >= 2 ? 0 : math;
     return T.run([&] { gnnx_gemm_tn_variant_f32(&q, out, ws, wsb, math >= 2 ? math : 0, nullptr); }, 5);
   };
   for (int m : tmaths) tn_run(m);  // warm-up
   for (int r = 0; r < rounds; ++r)
-    for (int i = 0; i < 3; ++i) tt[i].push_back(tn_run(tmaths[i]));
-  for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 4; ++i) tt[i].push_back(tn_run(tmaths[i]));
+  for (int i = 0; i < 4; ++i)
     std::printf("TN dz+mask math=%d: %8.1f us (%6.1f TF)\n", tmaths[i], med(tt[i]), flops / med(tt[i]) * 1e-6);
   return 0;
 }

@@ -803,16 +803,18 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
         g = z[0] * Ps[gn];
 #pragma unroll
         for (int q = 1; q < MAXPROJ; ++q) g = fmaf(z[q], Ps[q * 128 + gn], g);
+        // the staged dz rows are zero outside [rlo, rhi) (and P columns >= Nr are zero), so G,
+        // dzᵀh and Σdz need no per-row masks here (h of those rows is finite: our activations)
         if constexpr (MASK) {
 #pragma unroll
-          for (int q = 0; q < MAXPROJ; ++q) dw2[q] = fmaf(ok ? z[q] : 0.0f, rv[d][GS][i], dw2[q]);
+          for (int q = 0; q < MAXPROJ; ++q) dw2[q] = fmaf(z[q], rv[d][GS][i], dw2[q]);
         }
-        dzs += (gn < MAXPROJ && rok) ? z[gn & (MAXPROJ - 1)] : 0.0f;
+        if (gn < MAXPROJ) dzs += z[gn & (MAXPROJ - 1)];
       } else {
         g = rv[d][NS - 1][i];
       }
       if constexpr (MASK) g = rv[d][GS][i] > 0.0f ? g * a.hscale : 0.0f;
-      g = ok ? g : 0.0f;
+      if constexpr (!PROJ) g = ok ? g : 0.0f;
       db += g;
       if constexpr (GOUT) {
         if (a.gout && ok) a.gout[(int64_t)(mb + r) * a.ldgout + gn] = g;
@@ -1054,29 +1056,38 @@ void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
 }
 
 
-// Lab (MI355X, Elliptic layer-1 TN, dz form + mask, same process): classic order 205-215 us,
-// pipelined 200-210, pipelined + interleave hints (production) 192.  A 32-row-chunk variant
-// (single LDS image, 2 barriers per chunk) measured 217-227 us and was removed.
+// Lab (MI355X, Elliptic layer-1 TN, dz form + mask, variants interleaved in one process): with the
+// staging VALU cut from ~530 to ~325 per chunk (unmasked A, row offsets by adds, no per-row masks
+// in the dz form) the classic order runs 156 us and the pipelined order with interleave hints
+// 183 (before the cuts: 207 vs 196).  A 32-row-chunk variant measured 217-227 and was removed.
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
   constexpr int D = 1;
   if (a.a_bf16) {
-    if (nkt <= 8) { if (a.h_bf16) launch_tn_x3_k<D, 8, 1, true, true, 2>(a, nblk, st); else launch_tn_x3_k<D, 8, 1, true, false, 2>(a, nblk, st); }
-    else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true, 2>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false, 2>(a, nblk, st); }
+    if (nkt <= 8) { if (a.h_bf16) launch_tn_x3_k<D, 8, 1, true, true, 0>(a, nblk, st); else launch_tn_x3_k<D, 8, 1, true, false, 0>(a, nblk, st); }
+    else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true, 0>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false, 0>(a, nblk, st); }
     return;
   }
-  if (variant == 3) {  // lab: classic order (stage c; barrier; MFMAs of c)
-    if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 0>(a, nblk, st);
-    else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 0>(a, nblk, st);
-    else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 0>(a, nblk, st);
-    else launch_tn_x3_k<D, 12, 3, false, false, 0>(a, nblk, st);
+  if (variant == 3 || variant == 4) {  // lab: pipelined order (3: + interleave hints, 4: without)
+    const int pp = variant == 3 ? 2 : 1;
+    if (pp == 2) {
+      if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 2>(a, nblk, st);
+      else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 2>(a, nblk, st);
+      else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 2>(a, nblk, st);
+      else launch_tn_x3_k<D, 12, 3, false, false, 2>(a, nblk, st);
+    } else {
+      if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 1>(a, nblk, st);
+      else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 1>(a, nblk, st);
+      else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 1>(a, nblk, st);
+      else launch_tn_x3_k<D, 12, 3, false, false, 1>(a, nblk, st);
+    }
     return;
   }
-  // production: pipelined order + interleave hints
-  if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 2>(a, nblk, st);
-  else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 2>(a, nblk, st);
-  else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 2>(a, nblk, st);
-  else launch_tn_x3_k<D, 12, 3, false, false, 2>(a, nblk, st);
+  // production: classic order (stage c; barrier; MFMAs of c)
+  if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 0>(a, nblk, st);
+  else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 0>(a, nblk, st);
+  else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 0>(a, nblk, st);
+  else launch_tn_x3_k<D, 12, 3, false, false, 0>(a, nblk, st);
 }
 
 }  // namespace gnnmp
