@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -181,6 +181,10 @@ SIGNATURES = {
     "gnn_sage_mean_bwd_f32": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_edge_dot_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_ptr],
     ),
     "gnn_gat_scores_f32": (
         ctypes.c_int,

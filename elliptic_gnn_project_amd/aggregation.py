@@ -15,7 +15,7 @@ import torch
 from . import _lib
 from .graph import GraphPlan, get_plan
 
-__all__ = ["mean_aggregate", "gcn_aggregate", "gat_attention", "aggregate", "colsum", "KernelTimer"]
+__all__ = ["mean_aggregate", "masked_mean_aggregate", "edge_dot", "gcn_aggregate", "gat_attention", "aggregate", "colsum", "KernelTimer"]
 
 
 class KernelTimer:
@@ -204,6 +204,59 @@ def mean_aggregate(x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
     """PyG ``scatter(x[ei[0]], ei[1], reduce='mean')`` over x's N rows."""
     plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
     return _MeanAggregate.apply(x, plan)
+
+
+# --------------------------------------------------------------------------- explain mode
+def edge_dot(plan: GraphPlan, a: torch.Tensor, b: torch.Tensor, nodew: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-edge <a[i], b[j]> / max(nodew[i], 1) in PyG edge order [E] (gnn_edge_dot_f32)."""
+    a, b = _as_f32_rows(a), _as_f32_rows(b)
+    N, F = plan.num_nodes, a.size(1)
+    if a.size(0) != N or b.size(0) != N or b.size(1) != F:
+        raise ValueError(f"edge_dot operands {tuple(a.shape)} / {tuple(b.shape)} vs plan nodes {N}")
+    if plan.loops != _lib.LOOPS_KEEP:
+        raise NotImplementedError("edge_dot: plans with replaced self loops")
+    out = torch.empty(plan.num_edges, dtype=torch.float32, device=a.device)
+    _lib.call("gnn_edge_dot_f32", plan.c_graph, plan.csr_eid.data_ptr(), _lib.ptr(nodew), a.data_ptr(), _ld(a),
+              b.data_ptr(), _ld(b), F, out.data_ptr(), _lib.stream_handle(a.device))
+    return out
+
+
+class _MaskedMeanAggregate(torch.autograd.Function):
+    """PyG explain-mode SAGE mean: out_i = (sum_e m_e x_j) / max(deg_i, 1).
+
+    PyG 2.5.3 MessagePassing.propagate multiplies each message by the (sigmoided) edge mask
+    before ``aggr='mean'`` (the count stays the plain in-degree).  Forward and dx run the
+    EDGE_W aggregation with m in CSR slot order; dm is gnn_edge_dot_f32 (SDDMM).
+    """
+
+    @staticmethod
+    @_custom_fwd
+    def forward(ctx, x, m, plan: GraphPlan):
+        S = plan.num_slots
+        ew = m.detach().float()[plan.csr_eid[:S].long()].contiguous()
+        deg = plan.deg[: plan.num_nodes].clamp_min(1.0).unsqueeze(1)
+        out = aggregate(plan, x, _lib.AGG_EDGE_W, ew=ew).div_(deg)
+        ctx.plan = plan
+        ctx.save_for_backward(x, ew)
+        return out
+
+    @staticmethod
+    @_custom_bwd
+    def backward(ctx, dout):
+        plan = ctx.plan
+        x, ew = ctx.saved_tensors
+        dy = _as_f32_rows(dout) / plan.deg[: plan.num_nodes].clamp_min(1.0).unsqueeze(1)
+        dx = aggregate(plan, dy, _lib.AGG_EDGE_W, transpose=True, ew=ew) if ctx.needs_input_grad[0] else None
+        dm = edge_dot(plan, dy, x) if ctx.needs_input_grad[1] else None
+        return dx, dm, None
+
+
+def masked_mean_aggregate(x: torch.Tensor, edge_index: torch.Tensor, edge_mask: torch.Tensor) -> torch.Tensor:
+    """Explain-mode ``scatter(x[ei[0]] * edge_mask[:, None], ei[1], reduce='mean')``."""
+    if edge_mask.dim() != 1 or edge_mask.numel() != edge_index.size(1):
+        raise ValueError(f"edge_mask must be [E={edge_index.size(1)}], got {tuple(edge_mask.shape)}")
+    plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
+    return _MaskedMeanAggregate.apply(x, edge_mask, plan)
 
 
 # --------------------------------------------------------------------------- GCN

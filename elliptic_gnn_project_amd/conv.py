@@ -21,7 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .aggregation import colsum, gat_attention, gcn_aggregate, mean_aggregate, aggregate
+from .aggregation import colsum, gat_attention, gcn_aggregate, masked_mean_aggregate, mean_aggregate, aggregate
 from .graph import GraphPlan, get_plan
 from .linear import Linear, linear, linear2
 
@@ -101,6 +101,11 @@ class SAGEConv(nn.Module):
         return self.order == "transform_first"
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        if getattr(self, "explain", False) and getattr(self, "_edge_mask", None) is not None:
+            # PyG explain mode (set_masks): messages x_j scaled by the (sigmoided) edge mask
+            m = self._edge_mask.sigmoid() if getattr(self, "_apply_sigmoid", True) else self._edge_mask
+            agg = masked_mean_aggregate(x, edge_index, m)
+            return linear2(agg, x, self.lin_l.weight, self.lin_r.weight, self.lin_l.bias)
         if self._transform_first():
             fo = self.out_channels
             w = torch.cat([self.lin_l.weight, self.lin_r.weight], dim=0)
@@ -135,6 +140,8 @@ class GCNConv(nn.Module):
             nn.init.zeros_(self.bias)
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        if getattr(self, "explain", False):
+            raise NotImplementedError("explain-mode edge masks are implemented for SAGEConv only")
         y = self.lin(x)  # transform first (PyG order): aggregation width = out_channels
         return gcn_aggregate(y, edge_index, self.bias)
 
@@ -179,9 +186,35 @@ class GATConv(nn.Module):
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        if getattr(self, "explain", False):
+            raise NotImplementedError("explain-mode edge masks are implemented for SAGEConv only")
         xh = self.lin(x)  # [N, H*C]
         return gat_attention(xh, self.att_src, self.att_dst, self.bias, edge_index, self.heads,
                              self.out_channels, self.concat, self.negative_slope)
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads})"
+
+
+def set_masks(model: nn.Module, mask: torch.Tensor, edge_index: torch.Tensor, apply_sigmoid: bool = True) -> None:
+    """PyG ``torch_geometric.explain.algorithm.utils.set_masks``: put every conv of ``model`` in
+    explain mode with the per-edge message multiplier ``mask`` [E] (GNNExplainer's hook,
+    src/analysis/explain.py:593-672)."""
+    loop_mask = edge_index[0] != edge_index[1]
+    for module in model.modules():
+        if isinstance(module, (SAGEConv, GCNConv, GATConv)):
+            module.explain = True
+            module._edge_mask = mask
+            module._loop_mask = loop_mask
+            module._apply_sigmoid = apply_sigmoid
+
+
+def clear_masks(model: nn.Module) -> nn.Module:
+    """PyG ``clear_masks``: leave explain mode."""
+    for module in model.modules():
+        if isinstance(module, (SAGEConv, GCNConv, GATConv)):
+            module.explain = False
+            module._edge_mask = None
+            module._loop_mask = None
+            module._apply_sigmoid = True
+    return model

@@ -259,6 +259,8 @@ def fusable(model) -> bool:
     if len(convs) < 2:
         return False
     for c in convs:
+        if getattr(c, "explain", False):  # explain mode: per-conv path with the edge mask
+            return False
         if getattr(c, "aggr", None) != "mean" or c.lin_l.bias is None:
             return False
     for c in convs[:-1]:

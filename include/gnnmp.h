@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 7
+#define GNNMP_ABI_VERSION 8
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -170,6 +170,15 @@ gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg, const flo
 gnn_status gnn_sage_mean_bwd_f32(const gnn_graph* g, const float* deg, const float* dout,
                                  int64_t ld_dout, int64_t F, float* dx, int64_t ld_dx,
                                  gnn_stream_t stream);
+
+/* Explain mode (PyG MessagePassing.propagate with `explain` on: every message multiplied by
+ * edge_mask[e] before aggregation; driven by GNNExplainer, src/analysis/explain.py:593-672).
+ * Forward and x-gradient run as GNN_AGG_EDGE_W with the mask as slot weight; this entry point
+ * gives the mask gradient: out[eid ? eid[s] : s] = <a[r], b[col[s]]> / max(nodew[r], 1)
+ * (nodew NULL: / 1) for every CSR slot s of row r — for SAGEConv's mean a = dOut, b = x. */
+gnn_status gnn_edge_dot_f32(const gnn_graph* g, const int32_t* eid, const float* nodew, const float* a,
+                            int64_t lda, const float* b, int64_t ldb, int64_t F, float* out,
+                            gnn_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* K5/K6  GATConv edge softmax + aggregation (PyG GATConv.edge_update/message, utils.softmax) */

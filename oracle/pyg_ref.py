@@ -96,6 +96,18 @@ def sage_conv(x: Tensor, edge_index: Tensor, lin_l_w: Tensor, lin_l_b: Optional[
     return F.linear(agg, lin_l_w, lin_l_b) + F.linear(x, lin_r_w)
 
 
+def sage_conv_explain(x: Tensor, edge_index: Tensor, edge_mask: Tensor, lin_l_w: Tensor,
+                      lin_l_b: Optional[Tensor], lin_r_w: Tensor, apply_sigmoid: bool = True) -> Tensor:
+    """SAGEConv in explain mode [PyG 2.5.3 MessagePassing.propagate, `if self._explain`]:
+    the message x_j is multiplied by edge_mask (sigmoided when `_apply_sigmoid`) before the
+    'mean' aggregation; the count stays the in-degree.  Set by `explain.algorithm.utils.set_masks`
+    (GNNExplainer, src/analysis/explain.py:593-672)."""
+    m = edge_mask.sigmoid() if apply_sigmoid else edge_mask
+    x_j = x.index_select(0, edge_index[0]) * m.view(-1, 1)
+    agg = scatter(x_j, edge_index[1], x.size(0), reduce="mean")
+    return F.linear(agg, lin_l_w, lin_l_b) + F.linear(x, lin_r_w)
+
+
 def gcn_norm(edge_index: Tensor, num_nodes: int, dtype=torch.float32):
     ei = add_remaining_self_loops(edge_index, num_nodes)
     w = torch.ones(ei.size(1), dtype=dtype, device=ei.device)
