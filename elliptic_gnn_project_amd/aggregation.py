@@ -15,7 +15,7 @@ import torch
 from . import _lib
 from .graph import GraphPlan, get_plan
 
-__all__ = ["mean_aggregate", "masked_mean_aggregate", "edge_dot", "gcn_aggregate", "gat_attention", "aggregate", "colsum", "KernelTimer"]
+__all__ = ["mean_aggregate", "masked_mean_aggregate", "masked_gcn_aggregate", "edge_dot", "gcn_aggregate", "gat_attention", "aggregate", "colsum", "KernelTimer"]
 
 
 class KernelTimer:
@@ -208,14 +208,14 @@ def mean_aggregate(x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
 
 # --------------------------------------------------------------------------- explain mode
 def edge_dot(plan: GraphPlan, a: torch.Tensor, b: torch.Tensor, nodew: torch.Tensor | None = None) -> torch.Tensor:
-    """Per-edge <a[i], b[j]> / max(nodew[i], 1) in PyG edge order [E] (gnn_edge_dot_f32)."""
+    """Per-edge <a[i], b[j]> / max(nodew[i], 1) in PyG edge order [E] (+N loops on REPLACE plans)."""
     a, b = _as_f32_rows(a), _as_f32_rows(b)
     N, F = plan.num_nodes, a.size(1)
     if a.size(0) != N or b.size(0) != N or b.size(1) != F:
         raise ValueError(f"edge_dot operands {tuple(a.shape)} / {tuple(b.shape)} vs plan nodes {N}")
-    if plan.loops != _lib.LOOPS_KEEP:
-        raise NotImplementedError("edge_dot: plans with replaced self loops")
-    out = torch.empty(plan.num_edges, dtype=torch.float32, device=a.device)
+    # REPLACE plans: appended loop of node i has id E + i, dropped input loops stay 0
+    n_out = plan.num_edges + (N if plan.loops == _lib.LOOPS_REPLACE else 0)
+    out = torch.zeros(n_out, dtype=torch.float32, device=a.device)
     _lib.call("gnn_edge_dot_f32", plan.c_graph, plan.csr_eid.data_ptr(), _lib.ptr(nodew), a.data_ptr(), _ld(a),
               b.data_ptr(), _ld(b), F, out.data_ptr(), _lib.stream_handle(a.device))
     return out
@@ -257,6 +257,51 @@ def masked_mean_aggregate(x: torch.Tensor, edge_index: torch.Tensor, edge_mask: 
         raise ValueError(f"edge_mask must be [E={edge_index.size(1)}], got {tuple(edge_mask.shape)}")
     plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
     return _MaskedMeanAggregate.apply(x, edge_mask, plan)
+
+
+class _MaskedGCNAggregate(torch.autograd.Function):
+    """PyG explain-mode GCNConv propagate: message (dinv_j dinv_i) y_j times the edge mask, where
+    PyG keeps the mask of non-loop edges (``edge_mask[_loop_mask]``) and gives the N appended
+    self loops mask 1.  Runs EDGE_W with w_slot = m_ext[eid] * dinv_j * dinv_i; dm by K10."""
+
+    @staticmethod
+    @_custom_fwd
+    def forward(ctx, y, m, plan: GraphPlan, bias):
+        S, N = plan.num_slots, plan.num_nodes
+        eid = plan.csr_eid[:S].long()
+        seg = torch.repeat_interleave(torch.arange(N, device=y.device), plan.rowptr.diff().long(), output_size=S)
+        dinv = plan.dinv
+        norm = dinv[plan.col[:S].long()] * dinv[seg]
+        m_ext = torch.cat([m.detach().float(), torch.ones(N, dtype=torch.float32, device=y.device)])
+        ew = (m_ext[eid] * norm).contiguous()
+        norm_e = torch.zeros(plan.num_edges + N, dtype=torch.float32, device=y.device)
+        norm_e[eid] = norm
+        ctx.plan = plan
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(y, ew, norm_e)
+        return aggregate(plan, y, _lib.AGG_EDGE_W, ew=ew, bias=bias)
+
+    @staticmethod
+    @_custom_bwd
+    def backward(ctx, dout):
+        plan = ctx.plan
+        y, ew, norm_e = ctx.saved_tensors
+        dout = _as_f32_rows(dout)
+        dy = aggregate(plan, dout, _lib.AGG_EDGE_W, transpose=True, ew=ew) if ctx.needs_input_grad[0] else None
+        dm = None
+        if ctx.needs_input_grad[1]:
+            dm = (edge_dot(plan, dout, y) * norm_e)[: plan.num_edges]
+        db = colsum(dout) if ctx.has_bias and ctx.needs_input_grad[3] else None
+        return dy, dm, None, db
+
+
+def masked_gcn_aggregate(y: torch.Tensor, edge_index: torch.Tensor, edge_mask: torch.Tensor,
+                         bias: torch.Tensor | None = None) -> torch.Tensor:
+    """Explain-mode GCNConv propagate of transformed features y (+ bias)."""
+    if edge_mask.dim() != 1 or edge_mask.numel() != edge_index.size(1):
+        raise ValueError(f"edge_mask must be [E={edge_index.size(1)}], got {tuple(edge_mask.shape)}")
+    plan = get_plan(edge_index, y.size(0), _lib.LOOPS_REPLACE)
+    return _MaskedGCNAggregate.apply(y, edge_mask, plan, bias)
 
 
 # --------------------------------------------------------------------------- GCN

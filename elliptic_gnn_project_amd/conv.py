@@ -21,7 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .aggregation import colsum, gat_attention, gcn_aggregate, masked_mean_aggregate, mean_aggregate, aggregate
+from .aggregation import colsum, gat_attention, gcn_aggregate, masked_gcn_aggregate, masked_mean_aggregate, mean_aggregate, aggregate
 from .graph import GraphPlan, get_plan
 from .linear import Linear, linear, linear2
 
@@ -140,8 +140,9 @@ class GCNConv(nn.Module):
             nn.init.zeros_(self.bias)
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
-        if getattr(self, "explain", False):
-            raise NotImplementedError("explain-mode edge masks are implemented for SAGEConv only")
+        if getattr(self, "explain", False) and getattr(self, "_edge_mask", None) is not None:
+            m = self._edge_mask.sigmoid() if getattr(self, "_apply_sigmoid", True) else self._edge_mask
+            return masked_gcn_aggregate(self.lin(x), edge_index, m, self.bias)
         y = self.lin(x)  # transform first (PyG order): aggregation width = out_channels
         return gcn_aggregate(y, edge_index, self.bias)
 
@@ -187,7 +188,7 @@ class GATConv(nn.Module):
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
         if getattr(self, "explain", False):
-            raise NotImplementedError("explain-mode edge masks are implemented for SAGEConv only")
+            raise NotImplementedError("explain-mode edge masks are implemented for SAGEConv and GCNConv")
         xh = self.lin(x)  # [N, H*C]
         return gat_attention(xh, self.att_src, self.att_dst, self.bias, edge_index, self.heads,
                              self.out_channels, self.concat, self.negative_slope)

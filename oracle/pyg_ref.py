@@ -125,6 +125,19 @@ def gcn_conv(x: Tensor, edge_index: Tensor, lin_w: Tensor, bias: Optional[Tensor
     return out + bias if bias is not None else out
 
 
+def gcn_conv_explain(x: Tensor, edge_index: Tensor, edge_mask: Tensor, lin_w: Tensor, bias: Optional[Tensor],
+                     apply_sigmoid: bool = True) -> Tensor:
+    """GCNConv in explain mode [PyG 2.5.3 propagate]: messages w_e * h_j times the mask; the mask of
+    the non-loop input edges is kept (`edge_mask[self._loop_mask]`) and the appended loops get 1."""
+    m = edge_mask.sigmoid() if apply_sigmoid else edge_mask
+    keep = edge_index[0] != edge_index[1]
+    m = torch.cat([m[keep], m.new_ones(x.size(0))])
+    ei, w = gcn_norm(edge_index, x.size(0), x.dtype)
+    h = F.linear(x, lin_w)
+    out = scatter((w.view(-1, 1) * h.index_select(0, ei[0])) * m.view(-1, 1), ei[1], x.size(0), reduce="sum")
+    return out + bias if bias is not None else out
+
+
 def gat_conv(x: Tensor, edge_index: Tensor, lin_w: Tensor, att_src: Tensor, att_dst: Tensor,
              bias: Optional[Tensor], heads: int, chans: int, concat: bool = True,
              negative_slope: float = 0.2, return_alpha: bool = False):
