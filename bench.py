@@ -6,17 +6,22 @@ SAGE 166->128->2, dropout 0.5, fp32, N=203,769 nodes, E=468,710 symmetrized edge
 the reference's train_epoch (src/train_gnn.py:187-209): forward + masked weighted CE +
 backward + clip_grad_norm_(1.0) + Adam; the loss stays on device (no per-step .item()).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--arch A] [--scale weak|strong]
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): weak scaling.  Each rank owns
-a full Elliptic-shaped timestep partition of an N-times larger graph (no cross-timestep
-edges, so no halo exchange); gradients are summed with one flat RCCL all-reduce per step
-and the loss is normalised by the global train count.  value = edges of all ranks / max
-rank time.
+N > 1 (launched by torch.distributed.run, one rank per GPU): ONE global graph is partitioned
+by whole timesteps over the ranks (distributed.shard_graph: LPT bin-packing, no cross-timestep
+edges, so no halo exchange); gradients are summed with one flat RCCL all-reduce per step, the
+loss is normalised by the global train count and BatchNorm (SAGE-ResBN) is SyncBN.
+  --scale weak   (default) the global graph is N Elliptic-shaped blocks (seeds 42..42+N-1,
+                 49 timesteps each), partitioned by (block, timestep): per-GPU work fixed.
+  --scale strong the global graph is the ONE 203,769-node Elliptic graph split N ways
+                 (BASELINE configs[3], rec_k8: --arch sage_resbn --scale strong).
+value = edges of the global graph x steps / max-over-ranks wall time.
 
 Extra fields: ``roofline`` (dominant libgnnmp kernel: algorithmic bytes per launch / its
 HIP-event-timed average duration, on the launch stream) and ``cpu_baseline`` (the oracle —
-the PyG-2.5.3 ATen op sequence — timed on this host's cores, rank 0 only, bounded sample).
+the PyG-2.5.3 ATen op sequence — timed on this host's cores, rank 0 at N=1 only, bounded
+sample; all usable physical cores and a 1-thread figure, with the host's model/sockets/cores).
 """
 from __future__ import annotations
 
@@ -72,63 +77,131 @@ def parse():
     ap.add_argument("--arch", default="sage", choices=sorted(PRESETS), help="workload (sage = headline)")
     ap.add_argument("--aten-step", action="store_true",
                     help="loss/clip/Adam with the ATen ops instead of the fused libgnnmp step ops")
+    ap.add_argument("--scale", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak = one Elliptic block per rank; strong = the one Elliptic graph split N ways")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo only for multi-rank tests on one device")
+    ap.add_argument("--cpu-1t-seconds", type=float, default=8.0, help="1-thread CPU baseline sample budget")
     return ap.parse_args()
 
 
-def make_inputs(rank: int, degree: str, cfg, gen=None):
-    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+def make_global_graph(world: int, scale: str, degree: str, cfg, gen=None):
+    """The bench's global graph (prepared as train_gnn.main prepares it) and its partition key.
 
-    data = synthetic_elliptic(degree=degree, seed=42 + rank, **(gen or {}))
-    return prepare_inputs(data, cfg)
+    world 1 / strong: the seeded Elliptic-shaped graph (seed 42).  weak: world such blocks
+    (seeds 42 + b) as one disjoint union, partitioned by (block, timestep)."""
+    from elliptic_gnn_project_amd.dataset_elliptic import concat_graphs, prepare_inputs, synthetic_elliptic
+
+    nblk = world if (scale == "weak" and world > 1) else 1
+    blocks = [prepare_inputs(synthetic_elliptic(degree=degree, seed=42 + b, **(gen or {})), cfg) for b in range(nblk)]
+    if nblk == 1:
+        return blocks[0], blocks[0].timestep
+    g = concat_graphs(blocks)
+    return g, g.part_key
 
 
-def _host_cpu() -> str:
+def host_cpu_info():
+    """(model, sockets, physical cores, usable threads) of this host: /proc/cpuinfo topology and
+    the CPU share this process may use (affinity and the cgroup quota)."""
+    import os as _os
+
+    model, phys, sockets = "unknown", set(), set()
     try:
+        cur = {}
         with open("/proc/cpuinfo") as fh:
-            for line in fh:
-                if line.startswith("model name"):
-                    return line.split(":", 1)[1].strip()
+            for line in list(fh) + ["\n"]:
+                if not line.strip():
+                    if "core id" in cur or "physical id" in cur:
+                        phys.add((cur.get("physical id", "0"), cur.get("core id", cur.get("processor"))))
+                        sockets.add(cur.get("physical id", "0"))
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                cur[k.strip()] = v.strip()
+                if k.strip() == "model name":
+                    model = v.strip()
     except OSError:
         pass
-    return "unknown"
+    ncpu = _os.cpu_count() or 1
+    cores = len(phys) or ncpu
+    usable = len(_os.sched_getaffinity(0)) if hasattr(_os, "sched_getaffinity") else ncpu
+    try:  # cgroup v2 quota, e.g. "1600000 100000" -> 16 CPUs
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            usable = min(usable, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return model, max(1, len(sockets)), cores, max(1, min(cores, usable))
 
 
-def cpu_baseline(data, state, cw, denom, budget_s: float, cfg):
-    """Oracle (PyG-2.5.3 ATen op sequence) train step on the host CPU, same step definition."""
+def cpu_baseline(data, state, cw, denom, cfg, budget_s: float, budget_1t: float):
+    """Oracle (PyG-2.5.3 ATen op sequence) train step on the host CPU, same step definition
+    (fwd + masked weighted CE + bwd + clip + Adam), SURVEY §8(d): all usable physical cores
+    (torch.set_num_threads) and one thread, each on a bounded sample: the full graph when a
+    step fits the budget, else a prefix of whole timesteps (edges/s is per-edge work)."""
+    from elliptic_gnn_project_amd.distributed import local_subgraph
     from oracle import pyg_ref
 
-    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in state.items()
-              if v.is_floating_point()}
-    opt = torch.optim.Adam(params.values(), lr=0.003, weight_decay=1e-4)
-    x, ei, y, m = data.x, data.edge_index, data.y, data.train_mask
+    model, sockets, cores, threads = host_cpu_info()
     kw = dict(layers=cfg["layers"], dropout=cfg["dropout"], training=True, heads=cfg.get("heads", 4),
-              time_embed_dim=cfg.get("time_embed_dim", 0), time_embed_type=cfg.get("time_embed_type", "none"),
-              t_idx=data.timestep)
+              time_embed_dim=cfg.get("time_embed_dim", 0), time_embed_type=cfg.get("time_embed_type", "none"))
 
-    def step():
-        opt.zero_grad(set_to_none=True)
-        logits = pyg_ref.model_forward(cfg["arch"], params, x, ei, **kw)
-        loss = torch.nn.functional.cross_entropy(logits[m], y[m], weight=cw, reduction="none").sum() / denom
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
-        opt.step()
+    def sample(max_edges):
+        if data.edge_index.size(1) <= max_edges:
+            return data.x, data.edge_index, data.y, data.train_mask, data.timestep, "full graph"
+        ts = sorted(torch.unique(data.timestep).tolist())
+        e_t = torch.bincount(data.timestep[data.edge_index[1]], minlength=max(ts) + 1)
+        keep, acc = [], 0
+        for t in ts:
+            if keep and acc + int(e_t[t]) > max_edges:
+                break
+            keep.append(t)
+            acc += int(e_t[t])
+        nodes, ei = local_subgraph(data.timestep, data.edge_index, keep)
+        return (data.x[nodes], ei, data.y[nodes], data.train_mask[nodes], data.timestep[nodes],
+                f"timesteps {keep[0]}..{keep[-1]} ({len(keep)} of {len(ts)})")
 
-    step()  # warm-up (allocator, thread pool)
-    n, t0 = 0, time.perf_counter()
-    while True:
-        step()
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s or n >= 50:
-            break
+    def run(nthreads, budget, max_edges):
+        torch.set_num_threads(nthreads)
+        x, ei, y, m, t_idx, what = sample(max_edges)
+        params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in state.items()
+                  if v.is_floating_point()}
+        opt = torch.optim.Adam(params.values(), lr=0.003, weight_decay=1e-4)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            logits = pyg_ref.model_forward(cfg["arch"], params, x, ei, t_idx=t_idx, **kw)
+            loss = torch.nn.functional.cross_entropy(logits[m], y[m], weight=cw, reduction="none").sum() / denom
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(params.values(), 1.0)
+            opt.step()
+
+        step()  # warm-up (allocator, thread pool)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            step()
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= budget or n >= 50:
+                break
+        return ei.size(1) * n / el, 1e3 * el / n, f"{n} steps on {what} (N={x.size(0)}, E={ei.size(1)}), {el:.1f}s"
+
+    t0 = torch.get_num_threads()
+    try:
+        v, ms, smp = run(threads, budget_s, 2_000_000)
+        v1, ms1, smp1 = run(1, budget_1t, 480_000)
+    finally:
+        torch.set_num_threads(t0)
     return {
-        "value": ei.size(1) * n / el,
+        "value": v,
         "unit": "edges/s",
-        "cores": torch.get_num_threads(),
+        "cores": threads,
         "kind": "port",
-        "sample": f"{n} full-size steps (N={x.size(0)}, E={ei.size(1)}), {el:.1f}s, oracle/pyg_ref.py on CPU",
-        "host_cpu": _host_cpu(),
-        "ms_per_step": 1e3 * el / n,
+        "sample": f"{smp}; oracle/pyg_ref.py (PyG 2.5.3 ATen op sequence) on CPU, {threads} threads",
+        "ms_per_step": ms,
+        "one_thread": {"value": v1, "ms_per_step": ms1, "sample": smp1},
+        "host_cpu": model, "sockets": sockets, "physical_cores": cores,
+        "threads_note": "threads = min(physical cores, this process's CPU share: affinity / cgroup quota)",
     }
 
 
@@ -244,12 +317,16 @@ def main():
     if world != args.gpus:
         if not (world == 1 and args.gpus == 1):
             raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torch.distributed.run")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(local % max(ndev, 1))
+    dev = torch.device("cuda", local % max(ndev, 1))
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from elliptic_gnn_project_amd import distributed as gdist
     from elliptic_gnn_project_amd.aggregation import KernelTimer
@@ -257,7 +334,9 @@ def main():
 
     preset = PRESETS[args.arch]
     cfg = preset["cfg"]
-    data_cpu = make_inputs(rank, args.degree, cfg, preset.get("gen"))
+    full, key = make_global_graph(world, args.scale, args.degree, cfg, preset.get("gen"))
+    E_global = full.edge_index.size(1)
+    data_cpu = gdist.shard_graph(full, world, rank, key=key) if world > 1 else full
     data = data_cpu.to(dev)
     bf16 = preset.get("dtype") == "bf16"
     if bf16:  # bf16 storage of the node features (and, through the fused path, every activation)
@@ -273,7 +352,8 @@ def main():
     else:  # clip_grad_norm_(1.0) + Adam fused (train_ops.ClipAdam: 2 launches, device step counter)
         from elliptic_gnn_project_amd.train_ops import ClipAdam
         opt = ClipAdam(model.parameters(), lr=0.003, weight_decay=1e-4, max_norm=1.0)
-    cw, denom = gdist.global_class_weight_and_count(data.y, data.train_mask, dist)
+    # class weights and the loss divisor from the GLOBAL train labels (src/train_gnn.py:175,362-365)
+    cw, denom = gdist.global_class_weight_and_count(full.y, full.train_mask, None)
     loss_fn = _make_loss_fn({}, cw, model, 1, 34)
     bucket = gdist.GradBucket(model) if dist is not None else None
     tidx = data.train_idx
@@ -314,12 +394,15 @@ def main():
     if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t0
+    n_local = torch.tensor([float(data.x.size(0)), float(data.edge_index.size(1))], dtype=torch.float64)
     if dist is not None:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
-    E = data.edge_index.size(1)
-    value = E * world * args.steps / el
+        nl = n_local.to(t.device)
+        dist.all_reduce(nl, op=dist.ReduceOp.MAX)
+        n_local = nl.cpu()
+    value = E_global * args.steps / el
 
     roof = None
     if not args.no_roofline:
@@ -331,10 +414,11 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(data_cpu, state0, cw.cpu(), denom, args.cpu_seconds, cfg)
+        cpu = cpu_baseline(data_cpu, state0, cw.cpu(), denom, cfg, args.cpu_seconds, args.cpu_1t_seconds)
         cpu["speedup_gpu_over_cpu"] = round(value / cpu["value"], 1)
 
     if rank == 0:
+        scaling = "weak" if (world == 1 or args.scale == "weak") else "strong"
         print(json.dumps({
             "metric": preset.get("metric") or (METRIC if args.arch == "sage" else METRIC.replace("SAGE", args.arch.upper())),
             "value": value,
@@ -344,14 +428,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * el / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "bf16" if bf16 else "f32",
-            "data": f"synthetic Elliptic-shape ({args.degree} in-degree, seed 42+rank)",
+            "data": f"synthetic Elliptic-shape ({args.degree} in-degree, seeded)",
             "config": {
                 "workload": preset["workload"] + ", full-batch train step (fwd+masked CE+bwd+clip+Adam)",
-                "nodes_per_gpu": data.x.size(0), "edges_per_gpu": E, "feats": data.x.size(1),
-                "parallelism": f"dp{world} timestep-partitioned" if world > 1 else "single",
+                "global_nodes": full.num_nodes, "global_edges": E_global, "feats": data.x.size(1),
+                "max_nodes_per_gpu": int(n_local[0]), "max_edges_per_gpu": int(n_local[1]),
+                "parallelism": f"dp{world} timestep-partitioned ({args.scale})" if world > 1 else "single",
+                "collective": f"{args.dist_backend} all-reduce of one flat fp32 gradient bucket per step" if world > 1 else None,
                 "launch": "hip-graph replay of the whole step" if use_graph else "eager",
             },
             "roofline": roof,

@@ -5,7 +5,7 @@ gnn.py:20-23 (GCN), :41-44 and :125-128 (SAGE), :64-67 (GAT).  Constructor argum
 parameter names (hence ``state_dict`` keys, a compatibility contract with
 best.ckpt consumers such as src/analysis/hub_ablation.py:88-98) and the
 ``forward(x, edge_index)`` signature are PyG's; the neighbour aggregation runs in
-libgnnmp's HIP kernels and the dense transforms in MFMA GEMMs (hipBLASLt).
+libgnnmp's HIP kernels and the dense transforms in libgnnmp's MFMA GEMMs (K7, csrc/gemm_*.hip).
 
 Only PyG's defaults used by the reference are implemented (SAGE: aggr='mean',
 normalize=False, root_weight=True, project=False; GCN: improved=False,

@@ -162,8 +162,29 @@ def index_masks(data: GraphData) -> GraphData:
     for name in ("train", "val", "test"):
         m = getattr(data, f"{name}_mask", None)
         if m is not None:
-            setattr(data, f"{name}_idx", torch.nonzero(m, as_tuple=False).flatten())
+            idx = torch.nonzero(m, as_tuple=False).flatten()
+            setattr(data, f"{name}_idx", idx)
+            setattr(data, f"n_{name}", int(idx.numel()))  # host ints: the loss divisor needs no sync
     return data
+
+
+def concat_graphs(blocks) -> GraphData:
+    """Disjoint union of prepared graphs (node rows stacked, edges offset, order kept), with
+    ``part_key`` = timestep + T_max·block so that whole (block, timestep) units can be
+    partitioned (bench.py's weak-scaling graph: one Elliptic-shaped block per rank)."""
+    keys = [k for k in blocks[0].keys() if not k.endswith("_idx")]
+    out, off, tmax = {}, 0, max(int(b.timestep.max()) for b in blocks)
+    eis, pk = [], []
+    for bi, b in enumerate(blocks):
+        eis.append(b.edge_index + off)
+        pk.append(b.timestep + tmax * bi)
+        off += b.num_nodes
+    for k in keys:
+        if k != "edge_index":
+            out[k] = torch.cat([getattr(b, k) for b in blocks], dim=0)
+    out["edge_index"] = torch.cat(eis, dim=1)
+    out["part_key"] = torch.cat(pk)
+    return index_masks(GraphData(**out))
 
 
 def save_graph(path: str, data: GraphData) -> None:

@@ -6,6 +6,8 @@ timesteps and any depth of message passing on a subset of whole timesteps needs 
 
   partition_timesteps   greedy LPT bin-packing of timesteps (cost a·N_t + b·E_t) onto ranks
   local_subgraph        a rank's node rows + its edges relabelled to local ids
+  shard_graph           a prepared graph's rows / edges / masks for one rank (host side)
+  gather_rows           every rank's per-node outputs back into one [N, ...] tensor (eval)
   global_class_weight_and_count
                         class weights from the GLOBAL train labels (src/train_gnn.py:362-365)
                         and the global train count, so sum-over-ranks of the per-rank
@@ -56,6 +58,63 @@ def local_subgraph(timestep: torch.Tensor, edge_index: torch.Tensor, steps: Sequ
     return nodes, local[edge_index[:, keep]]
 
 
+def shard_graph(data, world: int, rank: int, parts: Optional[List[List[int]]] = None,
+                key: Optional[torch.Tensor] = None):
+    """This rank's whole-timestep shard of a prepared graph (prepare_inputs output, on the host).
+
+    Returns a GraphData with the local rows of every node tensor (x, y, timestep, the split
+    masks and their indices), the relabelled local ``edge_index`` (PyG edge order kept) and
+    ``nodes`` (global row ids, ascending), plus ``parts`` (the timesteps of every rank).
+    ``key`` (default ``data.timestep``) is the per-node partition unit: bench.py's weak-scaling
+    graph of several Elliptic blocks partitions by (block, timestep)."""
+    from .dataset_elliptic import GraphData, index_masks
+
+    key = data.timestep if key is None else key
+    if parts is None:
+        parts = partition_timesteps(key, data.edge_index, world)
+    nodes, ei = local_subgraph(key, data.edge_index, parts[rank])
+    local = {"edge_index": ei, "nodes": nodes}
+    n = data.timestep.numel()
+    for k in data.keys():
+        v = getattr(data, k)
+        if k in ("edge_index",) or k.endswith("_idx"):
+            continue
+        if v.dim() >= 1 and v.size(0) == n:
+            local[k] = v.index_select(0, nodes)
+    out = GraphData(**local)
+    out.parts = parts
+    return index_masks(out)
+
+
+def gather_rows(values: torch.Tensor, nodes: torch.Tensor, num_nodes: int, dist) -> torch.Tensor:
+    """Scatter every rank's per-node ``values`` (rows of its local ``nodes``) into one [num_nodes,
+    ...] tensor on every rank (all_gather of zero-padded blocks; the shards are disjoint)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        out = values.new_zeros((num_nodes,) + tuple(values.shape[1:]))
+        out[nodes.to(values.device)] = values
+        return out
+    world = dist.get_world_size()
+    if values.is_cuda and dist.get_backend() == "gloo":  # gloo gathers host tensors
+        return gather_rows(values.cpu(), nodes.cpu(), num_nodes, dist).to(values.device)
+    cnt = torch.tensor([values.size(0)], dtype=torch.int64, device=values.device)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt)
+    mx = int(max(int(c) for c in cnts))
+    pad_v = values.new_zeros((mx,) + tuple(values.shape[1:]))
+    pad_v[: values.size(0)] = values
+    pad_n = torch.full((mx,), -1, dtype=torch.int64, device=values.device)
+    pad_n[: values.size(0)] = nodes.to(values.device)
+    vs = [torch.empty_like(pad_v) for _ in range(world)]
+    ns = [torch.empty_like(pad_n) for _ in range(world)]
+    dist.all_gather(vs, pad_v)
+    dist.all_gather(ns, pad_n)
+    out = values.new_zeros((num_nodes,) + tuple(values.shape[1:]))
+    for v, nn_, c in zip(vs, ns, cnts):
+        c = int(c)
+        out[nn_[:c]] = v[:c]
+    return out
+
+
 def global_class_weight_and_count(y: torch.Tensor, train_mask: torch.Tensor, dist=None
                                   ) -> Tuple[torch.Tensor, int]:
     yt = y[train_mask]
@@ -92,23 +151,43 @@ class GradBucket:
         dist.all_reduce(self.flat)
 
 
+def global_batch_stats(x: torch.Tensor, dist) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """(mean, biased var, n) of the rows of ``x`` over every rank, with ONE all-reduce.
+
+    Each rank contributes its centred statistics (Chan's parallel merge, all-reduce-only form):
+    n_r, n_r·m_r, n_r·m_r² and M2_r = Σ(x − m_r)² (local, fp32 two-pass), summed in float64:
+        mean = Σ n_r m_r / n,   var = (Σ M2_r + Σ n_r m_r² − n·mean²) / n
+    so features with a large mean and a small spread keep their precision (no E[x²] − mean²
+    over raw fp32 sums), and the variance is never negative."""
+    C = x.size(1)
+    n_r = x.size(0)
+    if n_r > 0:
+        m_r = x.mean(0)
+        m2_r = (x - m_r).pow(2).sum(0)
+    else:
+        m_r = x.new_zeros(C)
+        m2_r = x.new_zeros(C)
+    m_d = m_r.double()
+    stats = torch.cat([m_d * n_r, m_d * m_d * n_r, m2_r.double(),
+                       torch.full((1,), float(n_r), dtype=torch.float64, device=x.device)])
+    if dist is not None:
+        dist.all_reduce(stats)
+    n = stats[3 * C]
+    mean = stats[:C] / n
+    var = ((stats[2 * C: 3 * C] + stats[C: 2 * C] - n * mean * mean) / n).clamp_(min=0.0)
+    return mean.to(x.dtype), var.to(x.dtype), n
+
+
 class _SyncBNFn(torch.autograd.Function):
+    """y = (x − mean)·invstd·w + b with (mean, invstd) over all ranks' rows (computed by the
+    caller, so the running statistics reuse them: one collective forward, one backward)."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias, eps, group_dist):
-        dist = group_dist
-        n_local = torch.tensor([float(x.size(0))], dtype=x.dtype, device=x.device)
-        stats = torch.cat([x.sum(0), (x * x).sum(0), n_local])
-        if dist is not None:
-            dist.all_reduce(stats)
-        C = x.size(1)
-        n = stats[2 * C]
-        mean = stats[:C] / n
-        var = stats[C: 2 * C] / n - mean * mean  # biased, as BatchNorm normalises with
-        invstd = torch.rsqrt(var + eps)
+    def forward(ctx, x, weight, bias, mean, invstd, n, group_dist):
         xhat = (x - mean) * invstd
         ctx.save_for_backward(xhat, invstd, weight)
         ctx.n = n
-        ctx.dist = dist
+        ctx.dist = group_dist
         return xhat * weight + bias
 
     @staticmethod
@@ -119,14 +198,18 @@ class _SyncBNFn(torch.autograd.Function):
         dbias_w = red.clone()
         if ctx.dist is not None:
             ctx.dist.all_reduce(red)
+        n = ctx.n.to(dy.dtype)
         sdy, sdyx = red[:C], red[C:]
-        dx = (weight * invstd) * (dy - sdy / ctx.n - xhat * sdyx / ctx.n)
+        dx = (weight * invstd) * (dy - sdy / n - xhat * sdyx / n)
         # parameter grads are LOCAL sums; the gradient all-reduce adds the other ranks'
-        return dx, dbias_w[C:], dbias_w[:C], None, None
+        return dx, dbias_w[C:], dbias_w[:C], None, None, None, None
 
 
 class SyncBatchNorm1d(nn.BatchNorm1d):
-    """BatchNorm1d whose training-mode statistics span every rank's nodes (exact full-graph BN)."""
+    """BatchNorm1d whose training-mode statistics span every rank's nodes (exact full-graph BN).
+
+    Training mode: one all-reduce of the merged (mean, M2, n) statistics forward (shared by the
+    normalisation and the running-stat update), one of (Σdy, Σdy·x̂) backward."""
 
     dist = None  # set to torch.distributed once the process group is up
 
@@ -134,20 +217,19 @@ class SyncBatchNorm1d(nn.BatchNorm1d):
         d = self.dist if (self.dist is not None and self.dist.is_initialized()) else None
         if not self.training or d is None:
             return super().forward(x)
-        y = _SyncBNFn.apply(x, self.weight, self.bias, self.eps, d)
-        with torch.no_grad():  # running stats as BatchNorm1d: momentum update, unbiased variance
-            m = self.momentum if self.momentum is not None else 0.1
-            n_local = torch.tensor([float(x.size(0))], device=x.device, dtype=x.dtype)
-            stats = torch.cat([x.sum(0), (x * x).sum(0), n_local])
-            d.all_reduce(stats)
-            C = x.size(1)
-            n = stats[2 * C]
-            mean = stats[:C] / n
-            var = (stats[C: 2 * C] / n - mean * mean) * n / torch.clamp(n - 1, min=1)
-            self.running_mean.mul_(1 - m).add_(m * mean)
-            self.running_var.mul_(1 - m).add_(m * var)
-            self.num_batches_tracked += 1
-        return y
+        with torch.no_grad():
+            mean, var, n = global_batch_stats(x.detach(), d)
+            invstd = torch.rsqrt(var + self.eps)
+            if self.track_running_stats:  # as BatchNorm1d: momentum update, unbiased variance
+                self.num_batches_tracked += 1
+                # momentum None: cumulative average, as nn.BatchNorm1d
+                m = self.momentum if self.momentum is not None else 1.0 / float(self.num_batches_tracked)
+                unbiased = var * (n / torch.clamp(n - 1, min=1)).to(var.dtype)
+                self.running_mean.mul_(1 - m).add_(m * mean)
+                self.running_var.mul_(1 - m).add_(m * unbiased)
+        w = self.weight if self.affine else torch.ones_like(mean)
+        b = self.bias if self.affine else torch.zeros_like(mean)
+        return _SyncBNFn.apply(x, w, b, mean, invstd, n, d)
 
 
 def convert_sync_batchnorm(model: nn.Module, dist) -> nn.Module:

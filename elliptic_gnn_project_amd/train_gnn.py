@@ -29,6 +29,7 @@ import torch.nn.functional as F
 import yaml
 
 from .dataset_elliptic import GraphData, load_graph, prepare_inputs, synthetic_elliptic
+from .distributed import GradBucket, convert_sync_batchnorm, gather_rows, shard_graph
 from .gnn import GATNet, GCNNet, SAGENet, SAGEResBNNet
 
 
@@ -92,7 +93,10 @@ def _norm_train_time(t_vec, t_min, t_max):
     return (t_vec.float() - float(t_min)) / max(float(t_max - t_min), 1.0)
 
 
-def _make_loss_fn(cfg: Dict, cw: torch.Tensor, model, t_min: int, t_max: int):
+def _make_loss_fn(cfg: Dict, cw: torch.Tensor, model, t_min: int, t_max: int, world: int = 1):
+    """src/train_gnn.py:136-183.  ``world`` > 1 (timestep-partitioned ranks): the embedding L2
+    term is added once per rank, so each rank adds 1/world of it (the all-reduced gradient and
+    loss then carry it once)."""
     scheme = str(cfg.get("time_loss_weighting", "none"))
     embed_l2 = float(cfg.get("time_embed_l2", 0.0))
     focal = bool(cfg.get("focal_loss", False))
@@ -120,7 +124,7 @@ def _make_loss_fn(cfg: Dict, cw: torch.Tensor, model, t_min: int, t_max: int):
         # sum over ranks equals the single-device .mean() (src/train_gnn.py:175).
         loss = loss_vec.mean() if denom is None else loss_vec.sum() / float(denom)
         if embed_l2 > 0.0 and getattr(model, "time_emb", None) is not None:
-            loss = loss + embed_l2 * model.time_emb.weight.pow(2).mean()
+            loss = loss + (embed_l2 / world) * model.time_emb.weight.pow(2).mean()
         return loss
 
     def full(logits, y_all, mask, denom=None, t_idx_all=None):
@@ -159,33 +163,50 @@ def _clips_itself(optimizer) -> bool:
 
 def make_optimizer(model, cfg: Dict, device, use_amp: bool):
     """Adam(lr, weight_decay) (src/train_gnn.py:357).  On the GPU without AMP: ClipAdam, the
-    fused clip_grad_norm_(grad_clip) + Adam step (train_ops.py); otherwise torch.optim.Adam."""
+    fused clip_grad_norm_(grad_clip) + Adam step (train_ops.py), when one launch pair covers the
+    parameters (≤ ADAM_MAX_TENSORS tensors); otherwise torch.optim.Adam (train_epoch then clips
+    with clip_grad_norm_ as the reference does)."""
     if device.type == "cuda" and not use_amp:
         from .train_ops import ClipAdam
-        clip = cfg.get("grad_clip", 0)
-        return ClipAdam(model.parameters(), lr=cfg["lr"], weight_decay=cfg["weight_decay"],
-                        max_norm=float(clip) if clip and clip > 0 else None)
+        if ClipAdam.supports(model.parameters()):
+            clip = cfg.get("grad_clip", 0)
+            return ClipAdam(model.parameters(), lr=cfg["lr"], weight_decay=cfg["weight_decay"],
+                            max_norm=float(clip) if clip and clip > 0 else None)
     return torch.optim.Adam(model.parameters(), lr=cfg["lr"], weight_decay=cfg["weight_decay"])
 
 
-def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cfg, device, sync=True):
-    """One full-batch step (src/train_gnn.py:187-209).  ``sync=False`` keeps the loss on device."""
+def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cfg, device, sync=True,
+                denom=None, bucket=None, dist=None):
+    """One full-batch step (src/train_gnn.py:187-209).  ``sync=False`` keeps the loss on device.
+
+    Timestep-partitioned data parallelism: ``denom`` is the GLOBAL train count (the per-rank
+    loss is sum/denom, so the ranks' losses and gradients add up to the single-device .mean(),
+    :175) and ``bucket`` (distributed.GradBucket) all-reduces every gradient in one collective
+    before the clip and the optimizer step, so every rank applies the same update."""
     model.train()
-    optimizer.zero_grad(set_to_none=True)
+    optimizer.zero_grad(set_to_none=bucket is None)
+    if denom is None:
+        denom = getattr(data, "n_train", None)
     with _autocast(device, use_amp):
         logits = model(data.x, edge_index, data.timestep if _model_uses_time_embed(model) else None)
         t_idx = _rows(data.timestep, data, "train") if cfg.get("time_loss_weighting", "none") != "none" else None
         if getattr(loss_fn, "plain", False) and logits.is_cuda and not use_amp:
-            loss = loss_fn.full(logits, data.y, data.train_mask, denom=getattr(data, "n_train", None))
+            loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
         else:
-            loss = loss_fn(_rows(logits, data, "train"), _rows(data.y, data, "train"), t_idx)
+            loss = loss_fn(_rows(logits, data, "train"), _rows(data.y, data, "train"), t_idx,
+                           denom=denom if bucket is not None else None)
     scaler.scale(loss).backward()
+    if bucket is not None:
+        bucket.allreduce_(dist)
     if cfg.get("grad_clip", 0) and cfg["grad_clip"] > 0 and not _clips_itself(optimizer):
         scaler.unscale_(optimizer)
         torch.nn.utils.clip_grad_norm_(model.parameters(), cfg["grad_clip"])
     scaler.step(optimizer)
     scaler.update()
-    optimizer.zero_grad(set_to_none=True)
+    optimizer.zero_grad(set_to_none=bucket is None)
+    if bucket is not None:
+        loss = loss.detach().clone()
+        dist.all_reduce(loss)  # the global loss (sum of the ranks' partial means)
     return float(loss.item()) if sync else loss.detach()
 
 
@@ -215,13 +236,51 @@ class CapturedStep:
 
 
 @torch.no_grad()
-def eval_split(model, data, edge_index, mask):
+def eval_split(model, data, edge_index, mask, dist=None, num_nodes=None):
+    """src/train_gnn.py:248-257.  Partitioned (``dist`` given, ``data`` a shard): every rank runs
+    its own timesteps and the probabilities / labels are gathered over the global node order
+    (``num_nodes`` rows); ``mask`` is then the GLOBAL mask (host or device)."""
     model.eval()
     logits = model(data.x, edge_index, data.timestep if _model_uses_time_embed(model) else None)
+    if dist is not None:
+        logits = gather_rows(logits.float(), data.nodes, num_nodes, dist)
+        y = gather_rows(data.y, data.nodes, num_nodes, dist)
+    else:
+        y = data.y
     probs = torch.softmax(logits, dim=1)[:, 1].detach().cpu().numpy()
-    y = data.y.detach().cpu().numpy()
+    y = y.detach().cpu().numpy()
     m = mask.detach().cpu().numpy()
     return y[m], probs[m], logits
+
+
+class RunLogger:
+    """``training_log.csv`` (epoch, train_loss, val_pr_auc) as src/utils/logger.py:5-27 writes it,
+    plus the TensorBoard scalars when tensorboard is importable (it is optional here)."""
+
+    def __init__(self, outdir: str):
+        os.makedirs(outdir, exist_ok=True)
+        self.csv_path = os.path.join(outdir, "training_log.csv")
+        if not os.path.exists(self.csv_path):
+            with open(self.csv_path, "w", newline="") as f:
+                csv.writer(f).writerow(["epoch", "train_loss", "val_pr_auc"])
+        self.tb = None
+        try:
+            from torch.utils.tensorboard import SummaryWriter
+            self.tb = SummaryWriter(log_dir=os.path.join(outdir, "tb"))
+        except Exception:  # tensorboard absent: CSV only
+            self.tb = None
+
+    def log_epoch(self, epoch: int, train_loss: float, val_pr_auc: float) -> None:
+        with open(self.csv_path, "a", newline="") as f:
+            csv.writer(f).writerow([epoch, f"{train_loss:.6f}", f"{val_pr_auc:.6f}"])
+        if self.tb is not None:
+            self.tb.add_scalar("loss/train", train_loss, epoch)
+            self.tb.add_scalar("val/pr_auc_illicit", val_pr_auc, epoch)
+
+    def close(self) -> None:
+        if self.tb is not None:
+            self.tb.flush()
+            self.tb.close()
 
 
 # ----------------------------------------------------------------------------- metrics (src/utils/metrics.py)
@@ -256,6 +315,13 @@ def _threshold(y_bin, p, cfg) -> float:
     return M.pick_threshold_max_f1(y_bin, p)[0]
 
 
+def _max_f1_threshold(y_bin, p) -> float:
+    """use_val_for_thresholds false: max-F1 threshold on the test split (src/train_gnn.py:473-474)."""
+    from . import metrics as M
+
+    return M.pick_threshold_max_f1(y_bin, p)[0]
+
+
 # ----------------------------------------------------------------------------- data
 def load_data(cfg: Dict) -> GraphData:
     path = cfg.get("graph_file") or os.path.join(cfg.get("processed_dir", "data/processed"), "graph.npz")
@@ -270,54 +336,133 @@ def load_data(cfg: Dict) -> GraphData:
     return synthetic_elliptic(**(syn if isinstance(syn, dict) else {}))
 
 
+def _init_distributed(cfg: Dict):
+    """One process per GPU under torch.distributed.run (WORLD_SIZE/RANK/LOCAL_RANK from the env).
+
+    New optional keys: ``world_size`` (must equal WORLD_SIZE when given),
+    ``partition`` ('timestep': whole timesteps per rank — exact, the graph is block-diagonal in
+    time, src/data/dataset_elliptic.py:235-243) and ``dist_backend`` ('nccl' = RCCL, default;
+    'gloo' for tests).  Returns (dist or None, world, rank)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    want = int(cfg.get("world_size", world) or 1)
+    if want != world:
+        raise RuntimeError(f"world_size={want} but WORLD_SIZE={world}: launch with "
+                           f"python -m torch.distributed.run --nproc-per-node {want} ...")
+    if world == 1:
+        return None, 1, 0
+    if cfg.get("partition", "timestep") != "timestep":
+        raise ValueError(f"partition={cfg.get('partition')!r}: only 'timestep' partitioning is exact")
+    import torch.distributed as dist
+
+    rank = int(os.environ["RANK"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local % torch.cuda.device_count())
+    if not dist.is_initialized():
+        backend = cfg.get("dist_backend", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
+        else:
+            dist.init_process_group(backend)
+    return dist, world, rank
+
+
+def per_timestep_pr_auc(y_te: np.ndarray, p_te: np.ndarray, test_ts: np.ndarray) -> Dict:
+    """``test_pr_auc_by_time`` and ``pr_auc_last{1,3,5}`` of metrics.json (src/train_gnn.py:497-519):
+    PR-AUC of each test timestep in chronological order, and the means of the last 1/3/5."""
+    out: Dict = {}
+    if test_ts.size == 0:
+        return out
+    pr_by_t = []
+    for t in sorted(set(int(v) for v in test_ts.tolist())):
+        idx = test_ts == t
+        pr_by_t.append(float("nan") if idx.sum() == 0 else pr_auc_illicit((y_te[idx] == 1).astype(int), p_te[idx]))
+    out["test_pr_auc_by_time"] = pr_by_t
+    if pr_by_t:
+        out["pr_auc_last1"] = float(pr_by_t[-1])
+        if len(pr_by_t) >= 3:
+            out["pr_auc_last3"] = float(sum(pr_by_t[-3:]) / 3)
+        if len(pr_by_t) >= 5:
+            out["pr_auc_last5"] = float(sum(pr_by_t[-5:]) / 5)
+    return out
+
+
+def hub_edge_mask(edge_index: torch.Tensor, num_nodes: int, frac: float):
+    """Edges kept by the hub ablation of main (src/train_gnn.py:526-539): the int(frac·N) nodes of
+    highest in+out degree (torch.topk, as the reference) lose every incident edge.
+    Returns (hub flags [N] bool, kept-edge mask [E] bool, number of hubs); host tensors."""
+    ei = edge_index.detach().cpu()
+    num_hubs = int(frac * float(num_nodes))
+    deg = torch.bincount(ei[0], minlength=num_nodes) + torch.bincount(ei[1], minlength=num_nodes)
+    hubs = torch.zeros(num_nodes, dtype=torch.bool)
+    if num_hubs > 0:
+        hubs[torch.topk(deg, num_hubs).indices] = True
+    return hubs, ~(hubs[ei[0]] | hubs[ei[1]]), num_hubs
+
+
 def main(cfg: Dict) -> Dict:
-    set_seed(cfg.get("seed", 42))
+    """src/train_gnn.py:282-564 on libgnnmp, single GPU or timestep-partitioned over ranks."""
+    dist, world, rank = _init_distributed(cfg)
+    set_seed(cfg.get("seed", 42))  # same seed on every rank: identical initial weights
+    is_main = rank == 0
     outdir = os.path.join(cfg.get("output_root", "outputs"), "gnn", cfg["run_name"])
-    os.makedirs(outdir, exist_ok=True)
+    logger = RunLogger(outdir) if is_main else None
     device = get_device(cfg)
+    if bool(cfg.get("mini_batch", False)):
+        raise NotImplementedError("mini_batch: NeighborLoader sampling is not implemented yet (SURVEY §8f #3)")
     use_amp = bool(cfg.get("amp", True))
     scaler = torch.amp.GradScaler(device=device.type, enabled=use_amp)
 
-    data = prepare_inputs(load_data(cfg), cfg)
-    data = data.to(device)
+    full = prepare_inputs(load_data(cfg), cfg)  # host: masks window, time scalar, symmetrize
+    N = full.num_nodes
+    n_train = int(full.n_train)
+    local = shard_graph(full, world, rank) if dist is not None else full
+    data = local.to(device)
     ei = data.edge_index
     model = build_model(cfg["arch"], data.x.size(1), cfg).to(device)
+    bucket = None
+    if dist is not None:
+        convert_sync_batchnorm(model, dist)  # BatchNorm over all N nodes (gnn.py:188-189)
+        bucket = GradBucket(model)
     opt = make_optimizer(model, cfg, device, use_amp)
-    cw = class_weight(data.y[data.train_mask].cpu()) if cfg.get("class_weight_pos", "auto") == "auto" \
+    cw = class_weight(full.y[full.train_mask]) if cfg.get("class_weight_pos", "auto") == "auto" \
         else torch.tensor([1.0, float(cfg["class_weight_pos"])], dtype=torch.float32)
-    t_train = data.timestep[data.train_mask]
-    loss_fn = _make_loss_fn(cfg, cw, model, int(t_train.min()), int(t_train.max()))
+    t_train = full.timestep[full.train_mask]
+    loss_fn = _make_loss_fn(cfg, cw, model, int(t_train.min()), int(t_train.max()), world)
+    gmask = (lambda name: getattr(full, name)) if dist is not None else (lambda name: getattr(data, name))
+    ev = dict(dist=dist, num_nodes=N) if dist is not None else {}
 
     best_val, best_state, bad = -1.0, None, 0
     patience = cfg.get("patience", 20)
-    log_path = os.path.join(outdir, "training_log.csv")
-    with open(log_path, "w", newline="") as f:
-        csv.writer(f).writerow(["epoch", "train_loss", "val_pr_auc"])
     for epoch in range(1, cfg["max_epochs"] + 1):
-        loss = train_epoch(model, data, ei, opt, loss_fn, scaler, use_amp, cfg, device)
-        y_val, p_val, _ = eval_split(model, data, ei, data.val_mask)
+        loss = train_epoch(model, data, ei, opt, loss_fn, scaler, use_amp, cfg, device, denom=n_train,
+                           bucket=bucket, dist=dist)
+        y_val, p_val, _ = eval_split(model, data, ei, gmask("val_mask"), **ev)
         pr_val = 0.0 if y_val.size == 0 else pr_auc_illicit((y_val == 1).astype(int), p_val)
-        with open(log_path, "a", newline="") as f:
-            csv.writer(f).writerow([epoch, f"{loss:.6f}", f"{pr_val:.6f}"])
+        if logger is not None:
+            logger.log_epoch(epoch, loss, pr_val)
         if pr_val > best_val:
             best_val, bad = pr_val, 0
             best_state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
         else:
             bad += 1
-        if epoch % 10 == 0 or epoch == 1:
+        if is_main and (epoch % 10 == 0 or epoch == 1):
             print(f"Epoch {epoch:4d} | loss {loss:.4f} | val PR-AUC(illicit) {pr_val:.4f} (best {best_val:.4f})")
         if bad >= patience:
-            print("Early stopping.")
+            if is_main:
+                print("Early stopping.")
             break
     if best_state is not None:
         model.load_state_dict({k: v.to(device) for k, v in best_state.items()})
 
     T = None
-    if bool(cfg.get("calibrate_temperature", True)):
-        _, _, lv = eval_split(model, data, ei, data.val_mask)
+    if bool(cfg.get("calibrate_temperature", True)):  # TemperatureScaler.fit (src/utils/calibrate.py:8-30)
+        _, _, lv = eval_split(model, data, ei, gmask("val_mask"), **ev)
+        vm_dev = gmask("val_mask").to(lv.device)
+        yv = (gather_rows(data.y, data.nodes, N, dist) if dist is not None else data.y)[vm_dev]
         Tp = torch.ones(1, device=device, requires_grad=True)
         lbfgs = torch.optim.LBFGS([Tp], lr=0.1, max_iter=1000)
-        lv, yv = lv[data.val_mask].detach(), data.y[data.val_mask]
+        lv = lv[vm_dev].detach()
 
         def closure():
             lbfgs.zero_grad()
@@ -327,35 +472,62 @@ def main(cfg: Dict) -> Dict:
 
         lbfgs.step(closure)
         T = Tp.detach()
+        if dist is not None:
+            dist.broadcast(T, 0)  # one temperature for every rank
 
     def get_probs(edge_index_eval):
         model.eval()
         with torch.no_grad():
             lg = model(data.x, edge_index_eval, data.timestep if _model_uses_time_embed(model) else None)
+            if dist is not None:
+                lg = gather_rows(lg.float(), data.nodes, N, dist)
             if T is not None:
                 lg = lg / T
             return torch.softmax(lg, dim=1)[:, 1].cpu().numpy()
 
     probs = get_probs(ei)
-    y_np = data.y.cpu().numpy()
-    vm, tm = data.val_mask.cpu().numpy(), data.test_mask.cpu().numpy()
-    ts = data.timestep.cpu().numpy()
-    for split, m in (("val", vm), ("test", tm)):
-        np.save(os.path.join(outdir, f"scores_{split}.npy"), probs[m])
-        np.save(os.path.join(outdir, f"y_{split}.npy"), y_np[m])
-        np.save(os.path.join(outdir, f"node_idx_{split}.npy"), np.where(m)[0])
-        np.save(os.path.join(outdir, f"timestep_{split}.npy"), ts[m])
+    y_np = full.y.numpy() if dist is not None else data.y.cpu().numpy()
+    vm, tm = gmask("val_mask").cpu().numpy(), gmask("test_mask").cpu().numpy()
+    ts = full.timestep.numpy() if dist is not None else data.timestep.cpu().numpy()
     y_val, p_val = (y_np[vm] == 1).astype(int), probs[vm]
     y_te, p_te = (y_np[tm] == 1).astype(int), probs[tm]
-    thr = _threshold(y_val, p_val, cfg) if cfg.get("use_val_for_thresholds", True) else _threshold(y_te, p_te, cfg)
+    thr = _threshold(y_val, p_val, cfg) if cfg.get("use_val_for_thresholds", True) \
+        else _max_f1_threshold(y_te, p_te)
     metrics = _metrics(y_te, p_te, thr, cfg) if y_te.size else {}
     metrics["best_val_pr_auc"] = best_val
-    torch.save(model.state_dict(), os.path.join(outdir, "best.ckpt"))
-    with open(os.path.join(outdir, "metrics.json"), "w") as f:
-        json.dump(metrics, f, indent=2)
-    with open(os.path.join(outdir, "config_used.yaml"), "w") as f:
-        yaml.safe_dump(cfg, f)
-    print(json.dumps(metrics, indent=2))
+    metrics.update(per_timestep_pr_auc(y_np[tm], p_te, ts[tm]))
+
+    frac = float(cfg.get("ablate_hubs_frac", 0.0))
+    metrics_hub = None
+    if frac > 0:  # src/train_gnn.py:525-558: forward again without the hubs' edges
+        hubs, keep, num_hubs = hub_edge_mask(full.edge_index, N, frac)
+        if dist is not None:  # this rank's edges, through its nodes' global ids
+            nodes = local.nodes
+            lei = local.edge_index
+            keep_l = ~(hubs[nodes[lei[0]]] | hubs[nodes[lei[1]]])
+            ei_abl = lei[:, keep_l].to(device)
+        else:
+            ei_abl = full.edge_index[:, keep].to(device)
+        p_abl = get_probs(ei_abl)[tm]
+        metrics_hub = _metrics(y_te, p_abl, thr, cfg) if y_te.size else {}
+        metrics_hub.update(n_hubs=int(num_hubs), hub_fraction=frac, n_edges_remaining=int(keep.sum()))
+
+    if is_main:
+        for split, m in (("val", vm), ("test", tm)):
+            np.save(os.path.join(outdir, f"scores_{split}.npy"), probs[m])
+            np.save(os.path.join(outdir, f"y_{split}.npy"), y_np[m])
+            np.save(os.path.join(outdir, f"node_idx_{split}.npy"), np.where(m)[0])
+            np.save(os.path.join(outdir, f"timestep_{split}.npy"), ts[m])
+        torch.save(model.state_dict(), os.path.join(outdir, "best.ckpt"))
+        with open(os.path.join(outdir, "metrics.json"), "w") as f:
+            json.dump(metrics, f, indent=2)
+        if metrics_hub is not None:
+            with open(os.path.join(outdir, "metrics_hub_removed.json"), "w") as f:
+                json.dump(metrics_hub, f, indent=2)
+        with open(os.path.join(outdir, "config_used.yaml"), "w") as f:
+            yaml.safe_dump(cfg, f)
+        logger.close()
+        print(json.dumps(metrics, indent=2))
     return metrics
 
 

@@ -61,6 +61,9 @@ def masked_cross_entropy(logits: torch.Tensor, y: torch.Tensor, mask: torch.Tens
         logits = logits.float()
     if denom is None:
         denom = float(mask.sum())  # host sync; pass denom to avoid it
+    if float(denom) == 0.0:
+        # empty selection: the reference's loss_vec.mean() is NaN and its gradient is zero
+        return logits.sum() * 0.0 + float("nan")
     m8 = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)  # bool: no copy
     w = class_w.to(device=logits.device, dtype=torch.float32).contiguous()
     return _MaskedCE.apply(logits, y.contiguous(), m8.contiguous(), w, 1.0 / float(denom))
@@ -114,9 +117,17 @@ class ClipAdam(torch.optim.Optimizer):
                       self._ws.data_ptr(), self._ws.numel() * 4, _lib.stream_handle(dev))
         return loss
 
+    @staticmethod
+    def supports(params) -> bool:
+        """True when one ClipAdam launch pair covers ``params`` (≤ ADAM_MAX_TENSORS fp32 tensors);
+        make_optimizer falls back to torch.optim.Adam + clip_grad_norm_ otherwise."""
+        ps = list(params)
+        return 0 < len(ps) <= _lib.ADAM_MAX_TENSORS and all(p.dtype == torch.float32 for p in ps)
+
     def _build(self, group, ps):
         if len(ps) > _lib.ADAM_MAX_TENSORS:
-            raise ValueError(f"ClipAdam: at most {_lib.ADAM_MAX_TENSORS} tensors per group")
+            raise ValueError(f"ClipAdam: at most {_lib.ADAM_MAX_TENSORS} tensors per group "
+                             "(use torch.optim.Adam + clip_grad_norm_; make_optimizer does so)")
         grp = _lib.GnnAdamGroup()
         grp.num_tensors = len(ps)
         grp.lr, (grp.beta1, grp.beta2) = group["lr"], group["betas"]
