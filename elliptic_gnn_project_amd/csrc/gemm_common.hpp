@@ -160,6 +160,13 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
 size_t nt_x3_workspace(int64_t k1, int64_t k2);
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant = 0);  // NPL = 3, or 1 when a_bf16
 
+// weight-stationary persistent split-bf16 NT (gemm_ws.hip): B fragments resident in registers,
+// one block per CU sweeping 32-row tiles.  nt_ws_ok: the shapes/epilogues it takes.  `img`: at
+// least nt_x3_workspace(k1, k2) bytes of workspace for its pre-split B image (concatenated K).
+bool nt_ws_ok(const NTArgs& a);
+size_t nt_ws_tail_offset(int64_t k1, int64_t k2);
+void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks = 0);
+
 // VALU kernels for the narrow output-layer shapes (gemm_skinny.hip).  launch_nt_skinny returns
 // false (launching nothing) when the shape/epilogue is outside its envelope.
 bool launch_nt_skinny(const NTArgs& a, hipStream_t st);

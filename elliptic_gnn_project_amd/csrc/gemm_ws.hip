@@ -1,0 +1,532 @@
+// K7a-ws — weight-stationary persistent NT GEMM for the SAGE forward (split-bf16, fp32-accurate).
+//
+//   C = epi([A1 | A2] · [W1 | W2]ᵀ)      A1 = agg [M, k1], A2 = h [M, k2], W = the Linear weights
+//
+// Shape of the hot call (SAGE preset layer 1): M = 203,769, K = 166 + 166, N = 128.  The B
+// operand (3 bf16 planes × 128 × 352 pre-split = 264 KB) is far too small to be worth streaming
+// through LDS per row tile — the tiled form re-stages it in each of 1,592 blocks (≈ 400 MB of
+// L2→LDS per launch, more than the 270 MB A stream).  Here it is STATIONARY IN REGISTERS:
+//   * one persistent 512-thread block per CU (8 waves, 2 per SIMD).  Wave w owns output columns
+//     32·(w&3) .. +32 and HALF of the k-steps (w < 4: the first ceil(NKS/2), w >= 4: the rest);
+//     its B fragments (≤ 11 k-steps × 3 planes × 4 VGPRs) stay in registers for the launch;
+//   * the block sweeps 32-row tiles of A (t = blockIdx.x, += gridDim.x).  Each tile is loaded as
+//     flat dwordx4 quads (A segments contiguous: lda == k), split into hi/mid/lo bf16 (RNE,
+//     exact remainders) ONCE per element by the thread that loaded it, and written to one of two
+//     static LDS buffers in the MFMA fragment layout [plane][k-step][row 32][16 k] (8-row XOR
+//     swizzle of the 16-byte halves: conflict-free ds_read_b128).  Tile t+1's loads are issued
+//     before tile t's MFMAs and staged between them (sched_barrier fences keep the order);
+//   * the two waves of a column group sum their K-half accumulators through LDS (each keeps
+//     16 of the 32 rows), then run the epilogue on their rows: bias, ReLU, counter-hash dropout
+//     (bit-identical to keep_elem) and the output layer's projection z = h·Pᵀ (per-wave partial
+//     sums over 32 columns, added across the 4 column groups in a fixed order).
+// Two waves per SIMD hide each other's LDS / HBM / barrier latency under the MFMAs; HBM traffic
+// is the algorithmic minimum: A once (270 MB), C once (104 MB).
+#include "gemm_common.hpp"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+namespace gnnmp {
+namespace {
+
+constexpr int WS_ROWS = 32;            // rows per tile (the MFMA M)
+constexpr int WS_KSB = 32 * 32 + 32;   // bytes per k-step block of one plane: [row 32][32 B] + 32 B pad
+
+__device__ __forceinline__ uint32_t ws_pk(float a, float b) {  // RNE, a in the low half
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2v{a, b}, bf16x2v));
+}
+
+__device__ __forceinline__ void ws_split(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  h = ws_pk(a, b);
+  a -= __uint_as_float(h << 16);
+  b -= __uint_as_float(h & 0xffff0000u);
+  m = ws_pk(a, b);
+  a -= __uint_as_float(m << 16);
+  b -= __uint_as_float(m & 0xffff0000u);
+  l = ws_pk(a, b);
+}
+
+// The MFMA as an asm statement so its B operand (the stationary weights) can be read straight
+// from the accumulator file: hipcc keeps MFMA sources in VGPRs and, with 264 registers of B,
+// would copy every fragment back from AGPRs (4 v_accvgpr_read per MFMA — as many VALU
+// instructions as the whole epilogue).  Hazards hipcc does not pad for an asm statement
+// (cdna_hip_programming.md §5.7): the chain's first MFMA takes the literal 0 as C (no VALU write
+// of the accumulator before it), chained MFMAs read C back to back (0 states), and ws_mfma_end
+// pads 24 states before any other instruction touches the result.  The B registers are written
+// once, by the global loads of the prologue.
+template <bool FIRST>
+__device__ __forceinline__ void ws_mfma(floatx16& acc, const bf16x8& x, const bf16x8& b) {
+  if constexpr (FIRST) asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(acc) : "v"(x), "a"(b));
+  else asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(x), "a"(b));
+}
+__device__ __forceinline__ void ws_mfma_end(floatx16& acc) { asm volatile("s_nop 15\n\ts_nop 7" : "+v"(acc)); }
+
+// byte offset of bf16 element (row, kk) inside one plane of an A buffer
+__device__ __forceinline__ uint32_t ws_off(int row, int kk) {
+  return (uint32_t)((kk >> 4) * WS_KSB + row * 32 + ((((kk >> 3) & 1) ^ ((row >> 3) & 1)) << 4) + ((kk & 7) << 1));
+}
+
+// Flags of the fused epilogue (compile-time: the interleaved loop must stay one basic block).
+constexpr int WS_BIAS = 1, WS_RELU = 2, WS_DROP = 4, WS_PROJ = 8;
+
+// KS = 1: 4 waves (one per SIMD), every wave holds all NKS k-steps of its columns (≤ 264 VGPRs
+//         of B; 512-register waves).  KS = 2: 8 waves (two per SIMD), each holds half the
+//         k-steps; the pair's partial sums meet through LDS.
+// LAB (timing ablations only, bench_gemm variants 10-14): bit 1 no A loads / staging, bit 2 no
+// epilogue, bit 4 no MFMAs, bit 8 every tile's A re-read from the block's first tile (L2-hot).
+template <int NKS, int EPI, int KS, int LAB = 0>
+__global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const uint4* __restrict__ bimg, int ntiles,
+                                                             const float* __restrict__ tail) {
+  constexpr int WS_THREADS = 256 * KS;
+  constexpr int PLB = NKS * WS_KSB;        // bytes per plane
+  constexpr int BUF = 3 * PLB;             // bytes per A buffer
+  constexpr int KH0 = (NKS + KS - 1) / KS; // k-steps of the first K part (waves 0-3)
+  constexpr int KH = KH0;                  // register slots per wave (the second part has <= KH0)
+  constexpr int QN = (128 * NKS + WS_THREADS - 1) / WS_THREADS;  // staged quads per thread per tile
+  constexpr int RV = 16 / KS;              // accumulator rows (r-slots) a wave finishes
+  // LDS: two A buffers, the C tile of the epilogue ([32 rows][128] f32: coalesced C stores and
+  // the projection read it), the K-half exchange (KS 2: aliased onto the C tile when the A
+  // buffers leave no room — one more barrier per tile) and the projection weights.
+  constexpr int CT_BYTES = WS_ROWS * BN * 4;
+  constexpr int XCH_BYTES = KS == 2 ? 2 * 4 * 8 * 64 * 4 : 0;
+  constexpr bool XALIAS = KS == 2 && 2 * BUF + CT_BYTES + XCH_BYTES + MAXPROJ * (BN + 16) * 4 > 163840;
+  __shared__ __attribute__((aligned(16))) char A0[BUF];
+  __shared__ __attribute__((aligned(16))) char A1[BUF];
+  __shared__ __attribute__((aligned(16))) char CT[CT_BYTES + (XALIAS ? 0 : XCH_BYTES)];
+  constexpr int PLP = BN + 16;  // PL row pitch: the 4 q rows x 4 part chunks of a read hit distinct banks
+  __shared__ __attribute__((aligned(16))) float PL[MAXPROJ * PLP];  // projection weights [q][col]
+  float* const ctile = reinterpret_cast<float*>(CT);
+  float* const xbase = reinterpret_cast<float*>(CT + (XALIAS ? 0 : CT_BYTES));  // [2][4 groups][8][64]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int grp = wave & 3;        // column group
+  const int half = KS == 2 ? wave >> 2 : 0;  // K part (and, in the epilogue, row half)
+  // kernel arguments into registers once (a per-lane select of a struct field would compile to
+  // a vector load of the kernarg segment)
+  const float* const pa1 = a.a1;
+  const float* const pa2 = a.a2 ? a.a2 : a.a1;
+  const int k1 = a.k1, k2 = a.k2;
+  const int64_t M = a.M;
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+
+  // ---- stationary B: columns 32·grp .. +32, k-steps of this wave's half, 3 planes
+  //      (bimg: [chunk][plane][2n + kh], zero for n >= Nc and k >= k_g)
+  const int s0 = half ? KH0 : 0;
+  const int ns = half ? NKS - KH0 : KH0;
+  bf16x8 bw[KH][3];
+  {
+    const int slot = 2 * (32 * grp + (lane & 31)) + (lane >> 5);
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+      const int c = min(s0 + s, NKS - 1);  // the second half may have one k-step less: its last
+#pragma unroll                              // slot is loaded but never used
+      for (int p = 0; p < 3; ++p) bw[s][p] = __builtin_bit_cast(bf16x8, bimg[(c * 3 + p) * 256 + slot]);
+    }
+  }
+
+  // ---- zero the pad columns of both buffers once (k in [k1 + k2, 16·NKS): the staging never
+  //      writes them; B is zero there but LDS garbage could be NaN)
+  {
+    const int npad = NKS * 16 - k1 - k2;
+    for (int i = tid; i < 2 * 3 * WS_ROWS * npad; i += WS_THREADS) {
+      const int c = i % npad, rest = i / npad;
+      const int row = rest % WS_ROWS, bp = rest / WS_ROWS;  // bp = buffer * 3 + plane
+      const int kk = k1 + k2 + c;
+      char* base = (bp / 3 == 0 ? A0 : A1) + (bp % 3) * PLB;
+      *reinterpret_cast<uint16_t*>(base + ws_off(row, kk)) = 0;
+    }
+  }
+
+  // ---- per-thread staging map (tile-invariant): quad i -> flat element f = 4q of segment g.
+  //      Idle quads (q >= nq) stage zeros into the pad bytes of k-step 0 (never read).
+  uint32_t qoff[QN];               // LDS byte offsets of the quad's two pairs (pair 2 << 16 | pair 1)
+  int32_t qf[QN];                  // flat element offset inside the tile's segment
+  uint32_t qseg2 = 0, qidle = 0;   // bit i: quad i in segment 2 / idle
+  const int nq1 = 8 * k1, nq = nq1 + 8 * k2;  // quads per tile (32 rows · k / 4)
+#pragma unroll
+  for (int i = 0; i < QN; ++i) {
+    const int q = tid + WS_THREADS * i;
+    const bool seg2 = q >= nq1;
+    const int kg = seg2 ? k2 : k1;
+    const int f = 4 * (seg2 ? q - nq1 : q);
+    const int row = f / max(kg, 1), col = f - row * kg;
+    const int so = seg2 ? k1 : 0;  // K concatenated: segment 2 starts at k1 (even: pairs stay in a k-step)
+    const bool ok = q < nq;
+    const uint32_t o0 = ok ? ws_off(row, so + col) : 1024u;
+    const uint32_t o1 = ok ? (col + 2 < kg ? ws_off(row, so + col + 2) : ws_off(row + 1, so)) : 1028u;
+    qoff[i] = (o1 << 16) | o0;  // PLB < 64 KB
+    qf[i] = ok ? f : 0;
+    qseg2 |= (ok && seg2) ? (1u << i) : 0u;
+    qidle |= ok ? 0u : (1u << i);
+  }
+
+  // Staging registers, two sets: the quads of tile t+G are staged from one set during tile t's
+  // k-loop, and each quad's registers are refilled with tile t+3G right after (prefetch depth 2:
+  // every load has two tiles of MFMAs to land).
+  float4 st[2][QN];
+  // quad i of tile t into set `sb`: one unconditional 16-byte load (tile starts are 16-byte
+  // aligned: 32·k·4 bytes).  The last tile is read from `tail`, a zero-padded copy of its rows
+  // made by ws_tail_kernel, and tiles past the end re-read it (never staged into a used
+  // buffer), so the loads carry no branches: hipcc's vmcnt bookkeeping then waits for exactly
+  // the quad being staged instead of draining every prefetch in flight.
+  const float* const tail1 = tail;
+  const float* const tail2 = tail + WS_ROWS * k1;
+  auto load_quad = [&](int sb, int i, int t) {
+    const bool s2 = (qseg2 >> i) & 1u;
+    const int tc = (LAB & 8) ? blockIdx.x : min(t, ntiles - 1);  // LAB 8: re-read an L2-hot tile
+    const bool last = tc == ntiles - 1;
+    const float* b1 = last ? tail1 : pa1 + (int64_t)tc * WS_ROWS * k1;
+    const float* b2 = last ? tail2 : pa2 + (int64_t)tc * WS_ROWS * k2;
+    st[sb][i] = *reinterpret_cast<const float4*>((s2 ? b2 : b1) + qf[i]);
+    if ((qidle >> i) & 1u) st[sb][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  // stage one pair (half a quad: elements 2h, 2h+1) of quad i: split + 3 plane writes
+  auto stage_pair = [&](char* buf, int sb, int i, int h) {
+    uint32_t hi, mi, lo;
+    if (h == 0) ws_split(st[sb][i].x, st[sb][i].y, hi, mi, lo);
+    else ws_split(st[sb][i].z, st[sb][i].w, hi, mi, lo);
+    const uint32_t o = h == 0 ? (qoff[i] & 0xffffu) : (qoff[i] >> 16);
+    *reinterpret_cast<uint32_t*>(buf + o) = hi;
+    *reinterpret_cast<uint32_t*>(buf + PLB + o) = mi;
+    *reinterpret_cast<uint32_t*>(buf + 2 * PLB + o) = lo;
+  };
+  auto stage_quad = [&](char* buf, int sb, int i) {
+    stage_pair(buf, sb, i, 0);
+    stage_pair(buf, sb, i, 1);
+  };
+
+  const int frow = lane & 31;
+  const uint32_t foff = (uint32_t)(frow * 32 + (((lane >> 5) ^ ((frow >> 3) & 1)) << 4)) + s0 * WS_KSB;
+  const int col = 32 * grp + (lane & 31);
+  const bool colok = col < a.Nc;
+  const int Nc = a.Nc;
+  const uint32_t hstep = (uint32_t)Nc * kDropGolden;
+  if constexpr ((EPI & WS_PROJ) != 0) {
+    for (int i = tid; i < MAXPROJ * BN; i += WS_THREADS) {
+      const int q = i / BN, c = i % BN;
+      PL[q * PLP + c] = (q < a.nproj && c < Nc) ? a.proj[(int64_t)q * Nc + c] : 0.f;
+    }
+  }
+  float* const cptr = a.c;
+  const int64_t ldc = a.ldc;
+  // C stores as dwordx4 from the LDS tile when rows are 16-byte aligned (else one dword per lane)
+  const bool cvec = cptr && (ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(cptr) & 15) == 0);
+
+  // MFMAs of this wave's K half from `cur`; the next tile's quads split into `nxt` in between
+  auto kloop = [&](const char* cur, char* nxt, int sb, int tload) {
+    floatx16 acc;
+    constexpr int SQ0 = KH - QN > 0 ? KH - QN : 0;  // k-steps SQ0.. stage one quad each
+    // one fragment set, each plane re-read for step s+1 right after its last use in step s:
+    // plane 2 after MFMA 1, plane 1 after MFMA 3, plane 0 after MFMA 6 — each read has 3-5
+    // MFMAs (x2 waves per SIMD) to land before its next use
+    bf16x8 x[3];
+    auto frag = [&](int s, int p) { return *reinterpret_cast<const bf16x8*>(cur + p * PLB + s * WS_KSB + foff); };
+#pragma unroll
+    for (int p = 0; p < 3; ++p) x[p] = frag(0, p);
+    // Program order pinned by sched_barrier fences: between two dependent MFMAs (32 cycles) the
+    // wave issues the independent work of one slot — the next step's fragment reads, half a
+    // staged quad (split + 3 plane writes), the refill load — so it hides under the MFMA chain.
+#define WS_FENCE __builtin_amdgcn_sched_barrier(0)
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+      const int sn = s + 1 < KH ? s + 1 : s;
+      const bool stg = (LAB & 1) == 0 && s >= SQ0 && s - SQ0 < QN;  // compile-time (unrolled)
+      const int qi = s - SQ0;
+      const bool mm = (LAB & 4) == 0 && (KS == 1 || NKS % 2 == 0 || s < ns);  // odd NKS, KS 2: the
+      if (mm) {                                                               // second part is 1 shorter
+        if (s == 0) ws_mfma<true>(acc, x[2], bw[s][0]);  // small terms first
+        else ws_mfma<false>(acc, x[2], bw[s][0]);
+      }
+      WS_FENCE;
+      if (s + 1 < KH) x[2] = frag(sn, 2);
+      if (stg) stage_pair(nxt, sb, qi, 0);
+      WS_FENCE;
+      if (mm) ws_mfma<false>(acc, x[1], bw[s][1]);
+      WS_FENCE;
+      if (stg) stage_pair(nxt, sb, qi, 1);
+      WS_FENCE;
+      if (mm) ws_mfma<false>(acc, x[1], bw[s][0]);
+      WS_FENCE;
+      if (s + 1 < KH) x[1] = frag(sn, 1);
+      if (stg) load_quad(sb, qi, tload);
+      WS_FENCE;
+      if (mm) {
+        ws_mfma<false>(acc, x[0], bw[s][2]);
+        ws_mfma<false>(acc, x[0], bw[s][1]);
+        ws_mfma<false>(acc, x[0], bw[s][0]);
+      }
+      WS_FENCE;
+      if (s + 1 < KH) x[0] = frag(sn, 0);
+      WS_FENCE;
+    }
+#undef WS_FENCE
+    if constexpr (KH < QN && (LAB & 1) == 0) {
+#pragma unroll
+      for (int i = KH; i < QN; ++i) {
+        stage_quad(nxt, sb, i);
+        load_quad(sb, i, tload);
+      }
+    }
+    if constexpr ((LAB & 4) != 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = x[0][r & 7];
+    }
+    ws_mfma_end(acc);
+    return acc;
+  };
+
+  // K-half exchange of tile t.  acc holds this wave's K-half partial sums; the wave keeps
+  // r-slots [8·half, 8·half + 8) (rows 16·half .. +16) and sends the other 8 to its partner.
+  auto exchange_send = [&](const floatx16& acc) {
+    if constexpr (KS == 2) {
+      float* xo = xbase + ((half * 4 + grp) * 8) * 64;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xo[j * 64 + lane] = acc[(1 - half) * 8 + j];
+    }
+  };
+  auto exchange_recv = [&](const floatx16& acc, float (&v)[RV]) {
+    if constexpr (KS == 2) {
+      const float* xi = xbase + (((1 - half) * 4 + grp) * 8) * 64;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float o = xi[j * 64 + lane];
+        const float m = acc[half * 8 + j];
+        v[j] = half ? o + m : m + o;  // K-half 0 + K-half 1, same order on both waves
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RV; ++j) v[j] = acc[j];
+    }
+  };
+  // E1: this wave's rows of tile t -> bias, ReLU, dropout (element row·Nc + col, bit-identical to
+  // keep_elem) -> the LDS C tile.
+  auto epi_tile = [&](const float (&v)[RV], int t) {
+    const int64_t rbase = (int64_t)t * WS_ROWS + 4 * (lane >> 5);
+    const uint32_t h0 = ((uint32_t)rbase * (uint32_t)Nc + (uint32_t)col) * kDropGolden + (uint32_t)seed;
+    float bv = 0.f;
+    if constexpr ((EPI & WS_BIAS) != 0) bv = colok ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int j = 0; j < RV; ++j) {
+      const int r = half * RV + j;
+      const int rl = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      float x = v[j] + bv;
+      if constexpr ((EPI & WS_RELU) != 0) x = fmaxf(x, 0.f);
+      if constexpr ((EPI & WS_DROP) != 0)
+        x = keep_premixed(h0 + (uint32_t)(rl - 4 * (lane >> 5)) * hstep, seed, a.keep_thresh) ? x * a.drop_scale : 0.f;
+      ctile[rl * BN + col] = colok ? x : 0.f;
+    }
+  };
+  // E2 (after a barrier): coalesced C stores of tile t and the projection z = h·Pᵀ from the tile:
+  // thread -> (row, q, part) computes a 128/NP-long dot product; the NP parts (adjacent lanes)
+  // are summed in a fixed order.
+  auto epi_store = [&](int t) {
+    const int64_t r0 = (int64_t)t * WS_ROWS;
+    if (cptr) {
+      constexpr int NQ4 = WS_ROWS * BN / 4 / WS_THREADS;  // float4 chunks per thread
+#pragma unroll
+      for (int i = 0; i < NQ4; ++i) {
+        const int u = tid + WS_THREADS * i;
+        const int rl = u / (BN / 4), c4 = (u % (BN / 4)) * 4;
+        const int64_t row = r0 + rl;
+        const float4 x = *reinterpret_cast<const float4*>(ctile + rl * BN + c4);
+        if (row < M) {
+          if (cvec && c4 + 3 < Nc) {
+            *reinterpret_cast<float4*>(cptr + row * ldc + c4) = x;
+          } else {
+            float* d = cptr + row * ldc + c4;
+            if (c4 < Nc) d[0] = x.x;
+            if (c4 + 1 < Nc) d[1] = x.y;
+            if (c4 + 2 < Nc) d[2] = x.z;
+            if (c4 + 3 < Nc) d[3] = x.w;
+          }
+        }
+      }
+    }
+    if constexpr ((EPI & WS_PROJ) != 0) {
+      // part p takes the float4 chunks j ≡ p (mod NP): a 16-lane read group touches 4 q rows ×
+      // 4 adjacent chunks = 64 distinct banks
+      constexpr int NP = WS_THREADS / (WS_ROWS * MAXPROJ);  // parts per dot product: 2 or 4
+      const int part = tid % NP, q = (tid / NP) % MAXPROJ, rl = tid / (NP * MAXPROJ);
+      const float4* hrow = reinterpret_cast<const float4*>(ctile + rl * BN);
+      const float4* prow = reinterpret_cast<const float4*>(PL + q * PLP);
+      float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll 2
+      for (int j = part; j < BN / 4; j += 2 * NP) {  // 2 trips unrolled: bounded LDS loads in flight
+        const float4 h0_ = hrow[j], p0 = prow[j];
+        const float4 h1_ = hrow[j + NP], p1 = prow[j + NP];
+        acc0 = fmaf(h0_.x, p0.x, acc0); acc0 = fmaf(h0_.y, p0.y, acc0);
+        acc0 = fmaf(h0_.z, p0.z, acc0); acc0 = fmaf(h0_.w, p0.w, acc0);
+        acc1 = fmaf(h1_.x, p1.x, acc1); acc1 = fmaf(h1_.y, p1.y, acc1);
+        acc1 = fmaf(h1_.z, p1.z, acc1); acc1 = fmaf(h1_.w, p1.w, acc1);
+      }
+      float zsum = acc0 + acc1;
+      zsum += __shfl_xor(zsum, 1);
+      if constexpr (NP == 4) zsum += __shfl_xor(zsum, 2);
+      const int64_t row = r0 + rl;
+      if (part == 0 && q < a.nproj && row < M) a.z[row * a.ldz + q] = zsum;
+    }
+  };
+
+  // Per tile:  kloop(t) [stages t+1 from st] | loads(t+2) into st | exchange send | BARRIER 1 |
+  //            exchange recv [| BARRIER 1b when the exchange aliases the C tile] | E1: C tile |
+  //            BARRIER 2 | E2: C stores + projection.
+  // Tile t+2's loads are issued before tile t's C stores, so the staging waits of kloop(t+1)
+  // (in-order vmcnt) never wait for those stores.  Barrier 1 publishes A(t+1) and the exchange
+  // and retires every read of A(t) and of the C tile of t-1; barrier 2 publishes the C tile.
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  const int G = gridDim.x;
+#pragma unroll
+  for (int i = 0; i < QN; ++i) load_quad(0, i, t);
+#pragma unroll
+  for (int i = 0; i < QN; ++i) stage_quad(A0, 0, i);
+#pragma unroll
+  for (int i = 0; i < QN; ++i) {
+    load_quad(1, i, t + G);       // tile t + G: staged during tile t
+    load_quad(0, i, t + 2 * G);   // tile t + 2G: staged during tile t + G
+  }
+  __syncthreads();
+  float v[RV];
+  auto finish = [&](const floatx16& acc) {
+    exchange_send(acc);
+    __syncthreads();
+    exchange_recv(acc, v);
+    if constexpr (XALIAS) __syncthreads();
+    if constexpr ((LAB & 2) == 0) {
+      epi_tile(v, t);
+      __syncthreads();
+      epi_store(t);
+    } else {
+      if (v[0] == 123.f) cptr[tid] = v[RV - 1];  // keep the accumulators live
+    }
+  };
+  // two tiles per trip: static A buffers (A0 -> A1 -> A0) and register sets (1, 0), so the
+  // compiler sees staging writes and fragment reads as disjoint.  Past the end the staging
+  // rewrites the spare buffer with stale quads (never read) and load_quad loads nothing.
+  while (true) {
+    finish(kloop(A0, A1, 1, t + 3 * G));  // stages t + G from set 1, refills it with t + 3G
+    t += G;
+    if (t >= ntiles) break;
+    finish(kloop(A1, A0, 0, t + 3 * G));  // stages t + G from set 0
+    t += G;
+    if (t >= ntiles) break;
+  }
+}
+
+int ws_num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// The last (partial) row tile, zero-padded to 32 rows: [32][k1] then [32][k2] f32.
+__global__ __launch_bounds__(256) void ws_tail_kernel(NTArgs a, float* __restrict__ tail, int64_t r0) {
+  const int n1 = WS_ROWS * a.k1, n = n1 + WS_ROWS * a.k2;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const bool s2 = i >= n1;
+    const int kg = s2 ? a.k2 : a.k1;
+    const int j = s2 ? i - n1 : i;
+    const int r = j / kg, c = j - r * kg;
+    const int64_t row = r0 + r;
+    tail[i] = row < a.M ? (s2 ? a.a2[row * a.lda2 + c] : a.a1[row * a.lda1 + c]) : 0.f;
+  }
+}
+
+// B image over the CONCATENATED K (k < k1: W1, else W2 at k - k1): per 16-deep chunk c,
+// [plane hi/mid/lo][2n + khalf] uint4 (8 bf16), zero for n >= Nc and k >= k1 + k2.
+__global__ __launch_bounds__(256) void ws_presplit_b_kernel(NTArgs a, uint4* __restrict__ img, int nchunks) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;  // (chunk, n, khalf)
+  if (idx >= nchunks * 256) return;
+  const int c = idx >> 8, n = (idx & 255) >> 1, kh = idx & 1;
+  float e[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * c + 8 * kh + j;
+    float v = 0.f;
+    if (n < a.Nc && k < a.k1) v = a.w1[(int64_t)n * a.ldw1 + k];
+    else if (n < a.Nc && k < a.k1 + a.k2) v = a.w2[(int64_t)n * a.ldw2 + (k - a.k1)];
+    e[j] = v;
+  }
+  uint32_t w[4][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ws_split(e[2 * j], e[2 * j + 1], w[j][0], w[j][1], w[j][2]);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) img[((int64_t)c * 3 + p) * 256 + (idx & 255)] = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+}
+
+template <int NKS, int KS, int LAB = 0>
+void launch_ws_k(const NTArgs& a, const uint4* bimg, const float* tail, hipStream_t st) {
+  const int ntiles = (int)ceil_div(a.M, WS_ROWS);
+  const int grid = std::min(ntiles, ws_num_cus());
+  const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
+#define GNN_WS(E) gemm_nt_ws_kernel<NKS, E, KS, LAB><<<grid, 256 * KS, 0, st>>>(a, bimg, ntiles, tail)
+  if (proj && drop) GNN_WS(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
+  else if (proj) GNN_WS(WS_BIAS | WS_RELU | WS_PROJ);
+  else if (drop) GNN_WS(WS_BIAS | WS_RELU | WS_DROP);
+  else if (relu) GNN_WS(WS_BIAS | WS_RELU);
+  else if (bias) GNN_WS(WS_BIAS);
+  else GNN_WS(0);
+#undef GNN_WS
+}
+
+}  // namespace
+
+// Shapes the weight-stationary form takes: f32 A and C, contiguous A segments (lda == k, even k,
+// 16-byte aligned), 1 <= N <= 128, M >= 32, ceil((k1 + k2) / 16) k-steps in {8, 11, 16, 21}, and
+// an epilogue among plain | bias | bias+ReLU | bias+ReLU+dropout, each + projection when ReLU.
+bool nt_ws_ok(const NTArgs& a) {
+  if (a.a_bf16 || a.c_bf16 || !a.w1 || a.Nc > BN || a.Nc < 1) return false;
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (a.lda1 != a.k1 || (a.k1 & 1) || !al(a.a1)) return false;
+  if (a.k2 > 0 && (a.lda2 != a.k2 || (a.k2 & 1) || !al(a.a2))) return false;
+  const int nks = (a.k1 + a.k2 + 15) / 16;
+  if (nks != 8 && nks != 11 && nks != 16 && nks != 21) return false;
+  if (a.M < WS_ROWS || a.M * (int64_t)std::max(a.k1, a.k2) >= ((int64_t)1 << 40)) return false;
+  const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
+  if ((drop || proj || relu) && !(relu && bias)) return false;
+  return true;
+}
+
+// ks: K parts per column group (0 = the default: 2 when the half-K B fragments and the rest fit
+// a 256-register wave without spills, i.e. NKS <= 16; 1 for NKS = 21: 252 AGPRs of B).
+size_t nt_ws_tail_offset(int64_t k1, int64_t k2) {  // the B image (<= 24 chunks x 12 KB), then the tail tile
+  return (size_t)((k1 + k2 + 15) / 16) * 3 * 256 * sizeof(uint4);
+}
+
+void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks) {
+  const int nks = (a.k1 + a.k2 + 15) / 16;
+  float* tail = reinterpret_cast<float*>(reinterpret_cast<char*>(img) + nt_ws_tail_offset(a.k1, a.k2));
+  ws_presplit_b_kernel<<<nks, 256, 0, st>>>(a, img, nks);
+  ws_tail_kernel<<<16, 256, 0, st>>>(a, tail, (ceil_div(a.M, WS_ROWS) - 1) * WS_ROWS);
+#define GNN_WSL(N, K, L) launch_ws_k<N, K, L>(a, img, tail, st)
+  if (ks < 0) {  // lab ablations of the production NKS = 21 instance (KS 1)
+    if (nks != 21) ks = 0;
+    else {
+      switch (-ks) {
+        case 1: GNN_WSL(21, 1, 1); break;
+        case 2: GNN_WSL(21, 1, 2); break;
+        case 3: GNN_WSL(21, 1, 3); break;
+        case 4: GNN_WSL(21, 1, 4); break;
+        default: GNN_WSL(21, 1, 8); break;
+      }
+      return;
+    }
+  }
+  if (ks == 0) ks = nks <= 16 ? 2 : 1;
+  switch (nks) {
+    case 8: if (ks == 2) GNN_WSL(8, 2, 0); else GNN_WSL(8, 1, 0); break;
+    case 11: if (ks == 2) GNN_WSL(11, 2, 0); else GNN_WSL(11, 1, 0); break;
+    case 16: if (ks == 2) GNN_WSL(16, 2, 0); else GNN_WSL(16, 1, 0); break;
+    default: if (ks == 2) GNN_WSL(21, 2, 0); else GNN_WSL(21, 1, 0); break;
+  }
+#undef GNN_WSL
+}
+
+}  // namespace gnnmp

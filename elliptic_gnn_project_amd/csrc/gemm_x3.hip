@@ -354,292 +354,6 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   nt_epilogue<TM, CBF>(a, acc, m0, n0, lane, wave, seed);
 }
 
-// NT through LDS-DMA ("x3g").  Both operands reach LDS by global_load_lds with no VGPR staging:
-// the raw f32 A tile (128 rows x 16 k, dword DMA, quad-swizzled rows) and the pre-split B image
-// (dwordx4 DMA of the swizzled image, lane-linear).  A 3-stage ring keeps two chunks in flight
-// behind a counted vmcnt and a raw s_barrier (one per chunk); each lane splits its own A
-// fragment after reading it (2 ds_read_b128) and feeds the MFMAs directly.
-constexpr int XG_A = 128 * 16 * 4;             // raw f32 A tile per stage (8 KB)
-constexpr int XG_B = 3 * 128 * 16 * 2;         // pre-split B image per stage (12 KB)
-constexpr int XG_ST = XG_A + XG_B;
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// AQ: A rows 16-byte aligned (lda % 4 == 0): the A tile moves as dwordx4 DMA (2 per wave per
-// chunk) instead of dword DMA (8), which alone bounded the dword form (lab: 136 of 167 us).
-template <bool AQ>
-__global__ __launch_bounds__(256) void gemm_nt_x3g_kernel(NTArgs a, const uint4* __restrict__ bimg,
-                                                          const float* __restrict__ zeros) {
-  // one __shared__ object per stage and a loop unrolled by the stage count: every LDS access has
-  // a static stage, so the compiler's LDS-DMA alias tracking waits only for that stage's DMA
-  __shared__ __attribute__((aligned(16))) char L0[XG_ST];
-  __shared__ __attribute__((aligned(16))) char L1[XG_ST];
-  __shared__ __attribute__((aligned(16))) char L2[XG_ST];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * 128;
-  const int n0 = blockIdx.y * BN;
-  const int nch1 = (a.k1 + 15) / 16;
-  const int nchunks = nch1 + (a.k2 + 15) / 16;
-  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
-
-  floatx16 acc[1][4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][t][r] = 0.0f;
-
-  // A DMA: wave w, instruction j fills LDS rows 4(8w + j) .. +4 (256 B); lane l -> row + (l >> 4),
-  // physical quad (l >> 2) & 3 holding logical quad pq ^ ((row >> 2) & 3) = pq ^ (j & 3).
-  // Columns k >= klen are DMA'd from a zero buffer, so the fragment needs no masking.
-  constexpr int NA = AQ ? 2 : 8;  // A DMA instructions per wave per chunk
-  int64_t arow[NA];
-  int akq[NA];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) {
-    if constexpr (AQ) {  // instruction j: rows 16(2w + j) .. +16, lane -> row + l/4, physical quad l & 3
-      const int64_t r = m0 + 16 * (2 * wave + j) + (lane >> 2);
-      arow[j] = r < a.M ? r : a.M - 1;
-      akq[j] = 4 * ((lane & 3) ^ ((lane >> 4) & 3));
-    } else {
-      const int64_t r = m0 + 4 * (8 * wave + j) + (lane >> 4);
-      arow[j] = r < a.M ? r : a.M - 1;
-      akq[j] = 4 * (((lane >> 2) & 3) ^ (j & 3)) + (lane & 3);
-    }
-  }
-  auto issue = [&](char* st, int c) {
-    const float* A; int64_t lda; int k0, klen;
-    if (c < nch1) { A = a.a1; lda = a.lda1; k0 = c * 16; klen = min(16, a.k1 - k0); }
-    else { A = a.a2; lda = a.lda2; k0 = (c - nch1) * 16; klen = min(16, a.k2 - k0); }
-#pragma unroll
-    for (int j = 0; j < NA; ++j) {
-      const float* src = akq[j] < klen ? A + arow[j] * lda + k0 + akq[j] : zeros;
-      if constexpr (AQ) __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + (2 * wave + j) * 1024), 16, 0, 0);
-      else __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + (8 * wave + j) * 256), 4, 0, 0);
-    }
-    const char* bsrc = reinterpret_cast<const char*>(bimg) + (int64_t)c * XG_B;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int b = 3 * wave + j;
-      __builtin_amdgcn_global_load_lds(bsrc + (b * 64 + lane) * 16, (lds_ptr_t)(st + XG_A + b * 1024), 16, 0, 0);
-    }
-  };
-  // Fragment reads are inline-asm ds_read_b128 with counted lgkmcnt waits tied to their
-  // results: hipcc would otherwise wait vmcnt(0) (every DMA in flight, including the ones just
-  // issued for later chunks) before an LDS read it cannot prove disjoint from them.
-  const int frow = wave * 32 + (lane & 31);
-  const int kh = lane >> 5;
-  const int fsw = (frow >> 2) & 3;
-  const uint32_t aoff0 = (frow * 16 + 4 * ((2 * kh) ^ fsw)) * 4, aoff1 = (frow * 16 + 4 * ((2 * kh + 1) ^ fsw)) * 4;
-  // B fragment of tile t, plane p: row n = 32t + (lane & 31), half kh ^ bit 3 of n (t-independent)
-  const uint32_t boff = XG_A + ((lane & 31) * 16 + 8 * (kh ^ (((lane & 31) >> 3) & 1))) * 2;
-  auto compute = [&](const char* st, int c) {
-    const int klen = c < nch1 ? min(16, a.k1 - c * 16) : min(16, a.k2 - (c - nch1) * 16);
-    (void)klen;
-    const uint32_t sb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)st;
-    const uint32_t aa0 = sb + aoff0, aa1 = sb + aoff1, ba = sb + boff;
-    u32x4 lo, hi, b[4][3];
-    asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(aa0));
-    asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(aa1));
-#define GNN_XG_RB(T, P) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(b[T][P]) : "v"(ba), "i"((P * 128 + T * 32) * 32))
-    GNN_XG_RB(0, 0); GNN_XG_RB(0, 1); GNN_XG_RB(0, 2);
-    GNN_XG_RB(1, 0); GNN_XG_RB(1, 1); GNN_XG_RB(1, 2);
-    GNN_XG_RB(2, 0); GNN_XG_RB(2, 1); GNN_XG_RB(2, 2);
-    GNN_XG_RB(3, 0); GNN_XG_RB(3, 1); GNN_XG_RB(3, 2);
-#undef GNN_XG_RB
-    asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(lo), "+v"(hi), "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]));
-    if constexpr (AQ) {  // a DMA'd quad may straddle klen (pad columns, next segment): zero k >= klen
-      const int k0v = 8 * kh;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        lo[i] = k0v + i < klen ? lo[i] : 0u;
-        hi[i] = k0v + 4 + i < klen ? hi[i] : 0u;
-      }
-    }
-    uint32_t w[4][3];
-    split_pair(__uint_as_float(lo[0]), __uint_as_float(lo[1]), w[0]);
-    split_pair(__uint_as_float(lo[2]), __uint_as_float(lo[3]), w[1]);
-    split_pair(__uint_as_float(hi[0]), __uint_as_float(hi[1]), w[2]);
-    split_pair(__uint_as_float(hi[2]), __uint_as_float(hi[3]), w[3]);
-    bf16x8 af[3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) af[p] = __builtin_bit_cast(bf16x8, make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]));
-    auto mm = [&](int t) {
-      const bf16x8 bf[3] = {__builtin_bit_cast(bf16x8, b[t][0]), __builtin_bit_cast(bf16x8, b[t][1]),
-                            __builtin_bit_cast(bf16x8, b[t][2])};
-      acc[0][t] = mfma6(af, bf, acc[0][t]);
-    };
-    mm(0);
-    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2]));
-    mm(1);
-    asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[2][2]));
-    mm(2);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[3][0]), "+v"(b[3][1]), "+v"(b[3][2]));
-    mm(3);
-  };
-  // step: chunk c (in stage cur) has landed for this wave once chunk c+1's DMAs are the only
-  // ones left; the barrier makes every wave's part visible and retires every read of `nxt`
-  // (chunk c-1), which then receives chunk c+2 (clamped: the tail refills stages never read again)
-  auto step = [&](char* cur, char* nxt, int c) {
-    if constexpr (AQ) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");   // 2 A + 3 B per chunk
-    else asm volatile("s_waitcnt vmcnt(11) lgkmcnt(0)" ::: "memory");                   // 8 A + 3 B per chunk
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue(nxt, min(c + 2, nchunks - 1));
-    compute(cur, c);
-  };
-
-  issue(L0, 0);
-  issue(L1, min(1, nchunks - 1));
-  int c = 0;
-  for (; c + 3 <= nchunks; c += 3) {
-    step(L0, L2, c);
-    step(L1, L0, c + 1);
-    step(L2, L1, c + 2);
-  }
-  if (c < nchunks) step(L0, L2, c);
-  if (c + 1 < nchunks) step(L1, L0, c + 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  nt_epilogue<1, false>(a, acc, m0, n0, lane, wave, seed);
-}
-
-// 32-deep chunks ("x3h"): with 16-byte A rows, every A DMA instruction moves 8 full 128-byte
-// row lines (4 per wave per chunk) and each barrier covers 48 MFMAs.  B: two 16-deep image
-// chunks per stage.  S = 2 or 3 LDS stages of 40 KB.
-constexpr int XH_A = 128 * 32 * 4;  // 16 KB raw f32 A
-constexpr int XH_B = 2 * XG_B;      // 24 KB pre-split B
-constexpr int XH_ST = XH_A + XH_B;
-
-template <int S>
-__global__ __launch_bounds__(256) void gemm_nt_x3h_kernel(NTArgs a, const uint4* __restrict__ bimg,
-                                                          const float* __restrict__ zeros) {
-  __shared__ __attribute__((aligned(16))) char L0[XH_ST];
-  __shared__ __attribute__((aligned(16))) char L1[XH_ST];
-  __shared__ __attribute__((aligned(16))) char L2[S == 3 ? XH_ST : 16];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * 128;
-  const int n0 = blockIdx.y * BN;
-  const int nch1 = (a.k1 + 31) / 32;
-  const int nchunks = nch1 + (a.k2 + 31) / 32;
-  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
-
-  floatx16 acc[1][4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][t][r] = 0.0f;
-
-  // A DMA: instruction j of wave w fills rows 8(4w + j) .. +8 (1 KB); lane l -> row + (l >> 3),
-  // physical quad l & 7 holding logical quad (l & 7) ^ ((row >> 1) & 7)
-  int64_t arow[4];
-  int akq[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t r = m0 + 8 * (4 * wave + j) + (lane >> 3);
-    arow[j] = r < a.M ? r : a.M - 1;
-    akq[j] = 4 * ((lane & 7) ^ ((4 * (j & 1) + (lane >> 4)) & 7));
-  }
-  auto issue = [&](char* st, int c) {
-    const float* A; int64_t lda; int k0, klen;
-    if (c < nch1) { A = a.a1; lda = a.lda1; k0 = c * 32; klen = min(32, a.k1 - k0); }
-    else { A = a.a2; lda = a.lda2; k0 = (c - nch1) * 32; klen = min(32, a.k2 - k0); }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float* src = akq[j] < klen ? A + arow[j] * lda + k0 + akq[j] : zeros;
-      __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)(st + (4 * wave + j) * 1024), 16, 0, 0);
-    }
-    const char* bsrc = reinterpret_cast<const char*>(bimg) + (int64_t)c * XH_B;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int b = 6 * wave + j;
-      __builtin_amdgcn_global_load_lds(bsrc + (b * 64 + lane) * 16, (lds_ptr_t)(st + XH_A + b * 1024), 16, 0, 0);
-    }
-  };
-  const int frow = wave * 32 + (lane & 31);
-  const int kh = lane >> 5;
-  const int fsw = (frow >> 1) & 7;
-  uint32_t aoff[2][2];
-#pragma unroll
-  for (int sc = 0; sc < 2; ++sc)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) aoff[sc][h] = frow * 128 + 16 * ((4 * sc + 2 * kh + h) ^ fsw);
-  const uint32_t boff = XH_A + ((lane & 31) * 16 + 8 * (kh ^ (((lane & 31) >> 3) & 1))) * 2;
-  auto compute = [&](const char* st, int c) {
-    const int klen = c < nch1 ? min(32, a.k1 - c * 32) : min(32, a.k2 - (c - nch1) * 32);
-    const uint32_t sb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)st;
-#pragma unroll
-    for (int sc = 0; sc < 2; ++sc) {  // two 16-deep sub-chunks; <= 14 LDS reads in flight (lgkmcnt <= 15)
-      u32x4 lo, hi, b[4][3];
-      asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(sb + aoff[sc][0]));
-      asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(sb + aoff[sc][1]));
-      const uint32_t ba = sb + boff + sc * XG_B;
-#define GNN_XH_RB(T, P) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(b[T][P]) : "v"(ba), "i"((P * 128 + T * 32) * 32))
-      GNN_XH_RB(0, 0); GNN_XH_RB(0, 1); GNN_XH_RB(0, 2);
-      GNN_XH_RB(1, 0); GNN_XH_RB(1, 1); GNN_XH_RB(1, 2);
-      GNN_XH_RB(2, 0); GNN_XH_RB(2, 1); GNN_XH_RB(2, 2);
-      GNN_XH_RB(3, 0); GNN_XH_RB(3, 1); GNN_XH_RB(3, 2);
-#undef GNN_XH_RB
-      asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(lo), "+v"(hi), "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]));
-      const int kb = 16 * sc + 8 * kh;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        lo[i] = kb + i < klen ? lo[i] : 0u;
-        hi[i] = kb + 4 + i < klen ? hi[i] : 0u;
-      }
-      uint32_t w[4][3];
-      split_pair(__uint_as_float(lo[0]), __uint_as_float(lo[1]), w[0]);
-      split_pair(__uint_as_float(lo[2]), __uint_as_float(lo[3]), w[1]);
-      split_pair(__uint_as_float(hi[0]), __uint_as_float(hi[1]), w[2]);
-      split_pair(__uint_as_float(hi[2]), __uint_as_float(hi[3]), w[3]);
-      bf16x8 af[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) af[p] = __builtin_bit_cast(bf16x8, make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]));
-      auto mm = [&](int t) {
-        const bf16x8 bf[3] = {__builtin_bit_cast(bf16x8, b[t][0]), __builtin_bit_cast(bf16x8, b[t][1]),
-                              __builtin_bit_cast(bf16x8, b[t][2])};
-        acc[0][t] = mfma6(af, bf, acc[0][t]);
-      };
-      mm(0);
-      asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[1][2]));
-      mm(1);
-      asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[2][2]));
-      mm(2);
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[3][0]), "+v"(b[3][1]), "+v"(b[3][2]));
-      mm(3);
-    }
-  };
-  auto step = [&](char* cur, char* nxt, int c) {
-    if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");  // 4 A + 6 B per chunk
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue(nxt, min(c + S - 1, nchunks - 1));  // clamped: the tail refills stages never read again
-    compute(cur, c);
-  };
-
-  issue(L0, 0);
-  int c = 0;
-  if constexpr (S == 3) {
-    issue(L1, min(1, nchunks - 1));
-    for (; c + 3 <= nchunks; c += 3) {
-      step(L0, L2, c);
-      step(L1, L0, c + 1);
-      step(L2, L1, c + 2);
-    }
-    if (c < nchunks) step(L0, L2, c);
-    if (c + 1 < nchunks) step(L1, L0, c + 1);
-  } else {
-    for (; c + 2 <= nchunks; c += 2) {
-      step(L0, L1, c);
-      step(L1, L0, c + 1);
-    }
-    if (c < nchunks) step(L0, L1, c);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  nt_epilogue<1, false>(a, acc, m0, n0, lane, wave, seed);
-}
-
 template <int KC, int TM, int AV, int AU, int D, int LAB = 0>
 void launch_nt_x3_b(const NTArgs& a, const uint4* bimg, hipStream_t st) {
   dim3 grid((unsigned)ceil_div(a.M, 128 * TM), (unsigned)ceil_div(a.Nc, BN));
@@ -949,8 +663,11 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 }  // namespace
 
 size_t nt_x3_workspace(int64_t k1, int64_t k2) {  // pre-split B image, 12 KB per 16-deep chunk
-  // (segments padded to 32-deep chunks for the x3h form), + 64 B of zeros
-  return (size_t)(2 * ((k1 + 31) / 32) + 2 * ((k2 + 31) / 32)) * 3 * 256 * sizeof(uint4) + 64;
+  // (segments padded to 32-deep chunks), + 64 B of zeros; the weight-stationary form also keeps
+  // its zero-padded tail tile here ([32][k1 + k2] f32 after its B image)
+  const size_t x3 = (size_t)(2 * ((k1 + 31) / 32) + 2 * ((k2 + 31) / 32)) * 3 * 256 * sizeof(uint4) + 64;
+  const size_t ws = nt_ws_tail_offset(k1, k2) + (size_t)32 * (k1 + k2) * sizeof(float);
+  return x3 > ws ? x3 : ws;
 }
 
 // variant: 0 = production; others are lab tilings (bench_gemm.cpp).
@@ -985,6 +702,12 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
   }
   const int av = av_ok(4) ? 4 : (av_ok(2) ? 2 : 1);
   const bool pre = ws && ws_bytes >= nt_x3_workspace(a.k1, a.k2) && a.Nc <= BN;
+  if (pre && (variant == 0 || variant == 3 || variant == 4) && nt_ws_ok(a)) {
+    // production: weight-stationary persistent form (gemm_ws.hip, its own B image in `ws`);
+    // lab 3 / 4 force 1 / 2 K parts
+    launch_nt_ws(a, static_cast<uint4*>(ws), st, variant == 0 ? 0 : variant - 2);
+    return;
+  }
   if (pre) {
     const int nch1 = (a.k1 + 15) / 16, nch = nch1 + (a.k2 + 15) / 16;
     x3_presplit_b_kernel<<<nch, 256, 0, st>>>(a, static_cast<uint4*>(ws), nch1, nch);
@@ -1014,26 +737,11 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
     case 7: launch_nt_x3_b<16, 1, 2, 2, 2, 2>(a, bimg, st); break;  // ablation: no global loads in the loop
     case 8: launch_nt_x3_b<16, 1, 2, 2, 2, 6>(a, bimg, st); break;  // ablation: MFMA phase + barriers only
     case 9: launch_nt_x3_b<16, 1, 2, 2, 2, 3>(a, bimg, st); break;  // ablation: LDS staging + barriers only
-    case 10: case 11: {  // lab: LDS-DMA form (10: dword A DMA, 11: dwordx4 A DMA when lda % 4 == 0)
-      const int nch1 = (a.k1 + 15) / 16, nch = nch1 + (a.k2 + 15) / 16;
-      x3_presplit_b_kernel<<<nch, 256, 0, st>>>(a, static_cast<uint4*>(ws), nch1, nch, 1);
-      const float* zeros = reinterpret_cast<const float*>(static_cast<const char*>(ws) + (size_t)nch * XG_B);
-      const dim3 g((unsigned)ceil_div(a.M, 128), (unsigned)ceil_div(a.Nc, BN));
-      if (variant == 11 && av == 4) gemm_nt_x3g_kernel<true><<<g, 256, 0, st>>>(a, bimg, zeros);
-      else gemm_nt_x3g_kernel<false><<<g, 256, 0, st>>>(a, bimg, zeros);
+    case 10: case 11: case 12: case 13: case 14:  // lab: weight-stationary ablations (gemm_ws.hip)
+      if (nt_ws_ok(a)) launch_nt_ws(a, const_cast<uint4*>(bimg), st, -(variant - 9));
+      else launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
       break;
-    }
-    case 12: case 13: {  // lab: 32-deep LDS-DMA form (16-byte A rows only); 12: 3 stages, 13: 2 stages
-      if (av != 4) { launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st); break; }
-      const int nch1 = 2 * ((a.k1 + 31) / 32), nch = nch1 + 2 * ((a.k2 + 31) / 32);
-      x3_presplit_b_kernel<<<nch, 256, 0, st>>>(a, static_cast<uint4*>(ws), nch1, nch, 1);
-      const float* zeros = reinterpret_cast<const float*>(static_cast<const char*>(ws) + (size_t)nch * XG_B);
-      const dim3 g((unsigned)ceil_div(a.M, 128), (unsigned)ceil_div(a.Nc, BN));
-      if (variant == 12) gemm_nt_x3h_kernel<3><<<g, 256, 0, st>>>(a, bimg, zeros);
-      else gemm_nt_x3h_kernel<2><<<g, 256, 0, st>>>(a, bimg, zeros);
-      break;
-    }
-    default:  // production: classic order (branch-free MFMA phase)
+    default:  // classic order (branch-free MFMA phase): shapes outside nt_ws_ok; lab variant 20
       launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
       break;
   }

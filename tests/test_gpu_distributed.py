@@ -29,10 +29,12 @@ CFG = dict(arch="sage_resbn", hidden_dim=64, layers=3, dropout=0.0, use_bn=True,
            time_embed_dim=2, time_embed_type="sin", use_time_scalar=False, symmetrize_edges=True, train_window_k=8)
 
 
-def rel_l2(a, b):
+def rel_l2(a, b, floor=1e-7):
+    """Relative L2 with an absolute floor (as test_gpu_parity): a conv bias feeding BatchNorm has
+    an exactly-zero gradient, so both sides are rounding noise at the 1e-9 level there."""
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()
-    return float((a - b).norm() / max(float(b.norm()), 1e-12))
+    return float((a - b).norm() / max(float(b.norm()), floor / 1e-5))
 
 
 def _data(n=6000, e=9000, seed=31):
