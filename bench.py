@@ -223,7 +223,9 @@ def measured_traffic(tag):
     if tag[0] == "gemm_nt":
         M, N = tag[1], tag[3]
         grid = -(-M // 128) * 256 * -(-N // 128)
-        cand = [r for r in rows if "gemm_nt" in r["kernel"] and r["grid_threads"] == grid]
+        cand = [r for r in rows if "gemm_nt_ws" in r["kernel"]]  # the weight-stationary form
+        if len(cand) != 1:
+            cand = [r for r in rows if "gemm_nt" in r["kernel"] and r["grid_threads"] == grid]
     elif tag[0] == "gemm_tn":
         cand = [r for r in rows if "gemm_tn" in r["kernel"]]
     else:

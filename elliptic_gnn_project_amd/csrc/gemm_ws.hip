@@ -429,7 +429,9 @@ int ws_num_cus() {
 // The last (partial) row tile, zero-padded to 32 rows: [32][k1] then [32][k2] f32.
 __global__ __launch_bounds__(256) void ws_tail_kernel(NTArgs a, float* __restrict__ tail, int64_t r0) {
   const int n1 = WS_ROWS * a.k1, n = n1 + WS_ROWS * a.k2;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+  {
+    const int i = blockIdx.x * 256 + threadIdx.x;  // one element per thread
+    if (i >= n) return;
     const bool s2 = i >= n1;
     const int kg = s2 ? a.k2 : a.k1;
     const int j = s2 ? i - n1 : i;
@@ -504,7 +506,8 @@ void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks) {
   const int nks = (a.k1 + a.k2 + 15) / 16;
   float* tail = reinterpret_cast<float*>(reinterpret_cast<char*>(img) + nt_ws_tail_offset(a.k1, a.k2));
   ws_presplit_b_kernel<<<nks, 256, 0, st>>>(a, img, nks);
-  ws_tail_kernel<<<16, 256, 0, st>>>(a, tail, (ceil_div(a.M, WS_ROWS) - 1) * WS_ROWS);
+  ws_tail_kernel<<<(unsigned)ceil_div(WS_ROWS * (a.k1 + a.k2), 256), 256, 0, st>>>(a, tail,
+                                                                              (ceil_div(a.M, WS_ROWS) - 1) * WS_ROWS);
 #define GNN_WSL(N, K, L) launch_ws_k<N, K, L>(a, img, tail, st)
   if (ks < 0) {  // lab ablations of the production NKS = 21 instance (KS 1)
     if (nks != 21) ks = 0;
