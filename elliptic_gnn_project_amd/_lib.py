@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -131,6 +131,27 @@ class GnnGemmTNParams(ctypes.Structure):
     ]
 
 
+# gnn_act
+ACT_NONE = 0
+ACT_ELU = 1
+
+
+class GnnGatFwdParams(ctypes.Structure):
+    _fields_ = [
+        ("heads", c_i32), ("chans", c_i32), ("concat", c_i32),
+        ("slope", ctypes.c_float),
+        ("xh", c_ptr), ("ld_xh", c_i64),
+        ("att_src", c_ptr), ("att_dst", c_ptr),
+        ("bias", c_ptr),
+        ("act", ctypes.c_int),
+        ("dropout_p", ctypes.c_float),
+        ("seed", ctypes.c_uint64), ("seed_ptr", c_ptr),
+        ("a_src", c_ptr), ("a_dst", c_ptr),
+        ("alpha", c_ptr),
+        ("out", c_ptr), ("ldo", c_i64),
+    ]
+
+
 ADAM_MAX_TENSORS = 24
 
 
@@ -194,6 +215,12 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr,
          c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_gat_fwd_fused_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), ctypes.POINTER(GnnGatFwdParams), c_ptr]),
+    "gnn_gat_act_bwd_f32": (
+        ctypes.c_int,
+        [c_i64, c_i64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr,
+         c_i64, c_ptr],
     ),
     "gnn_gat_bwd_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, ctypes.POINTER(c_size)]),
     "gnn_gat_bwd_f32": (

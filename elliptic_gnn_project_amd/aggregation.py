@@ -331,10 +331,14 @@ def gcn_aggregate(y: torch.Tensor, edge_index: torch.Tensor, bias: torch.Tensor 
 
 # --------------------------------------------------------------------------- GAT
 class _GATAttention(torch.autograd.Function):
+    """K5/K6 with the scores formed in-kernel (gnn_gat_fwd_fused_f32) and, for GATNet's hidden
+    layers, ELU + counter-hash dropout on the store; the backward undoes them in one elementwise
+    pass (gnn_gat_act_bwd_f32) before the softmax / aggregation backward."""
+
     @staticmethod
     @_custom_fwd
     def forward(ctx, xh, att_src, att_dst, bias, plan: GraphPlan, heads: int, chans: int, concat: bool,
-                slope: float):
+                slope: float, act: int, dropout_p: float, seed: int, seed_ctr):
         xh = _as_f32_rows(xh)
         N = plan.num_nodes
         dev = xh.device
@@ -343,33 +347,43 @@ class _GATAttention(torch.autograd.Function):
         stream = _lib.stream_handle(dev)
         a_src = torch.empty((N, heads), dtype=torch.float32, device=dev)
         a_dst = torch.empty((N, heads), dtype=torch.float32, device=dev)
-        _lib.call("gnn_gat_scores_f32", N, heads, chans, xh.data_ptr(), _ld(xh), att_src.data_ptr(),
-                  att_dst.data_ptr(), a_src.data_ptr(), a_dst.data_ptr(), stream)
         alpha = torch.empty((max(plan.num_slots, 1), heads), dtype=torch.float32, device=dev)
         fo = heads * chans if concat else chans
         out = torch.empty((N, fo), dtype=torch.float32, device=dev)
         b = bias.contiguous().float() if bias is not None else None
+        p = _lib.GnnGatFwdParams(
+            heads, chans, int(concat), float(slope), xh.data_ptr(), _ld(xh), att_src.data_ptr(), att_dst.data_ptr(),
+            _lib.ptr(b), int(act), float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ctr),
+            a_src.data_ptr(), a_dst.data_ptr(), alpha.data_ptr(), out.data_ptr(), _ld(out),
+        )
         t0 = KernelTimer.begin()
-        _lib.call("gnn_gat_fwd_f32", plan.c_graph, heads, chans, int(concat), float(slope), xh.data_ptr(),
-                  _ld(xh), a_src.data_ptr(), a_dst.data_ptr(), _lib.ptr(b), alpha.data_ptr(), out.data_ptr(),
-                  _ld(out), stream)
+        _lib.call("gnn_gat_fwd_fused_f32", plan.c_graph, p, stream)
         S = plan.num_slots
-        # per slot: id 4 + a_src 4H + xh row 4HC + alpha 4H; per node: rowptr 4 + a_dst 4H + out 4·fo
+        # per slot: id 4 + xh row 4HC + alpha 8H (raw score, then normalised); per node: rowptr 4,
+        # own xh row 4HC, a_src + a_dst 8H, out 4·fo
         KernelTimer.end(t0, ("gat_fwd", heads, chans, fo),
-                        S * (4 + 8 * heads + 4 * heads * chans) + N * (4 + 4 * heads + 4 * fo))
-        ctx.save_for_backward(xh, att_src, att_dst, a_src, a_dst, alpha)
-        ctx.meta = (plan, heads, chans, bool(concat), float(slope), bias is not None)
+                        S * (4 + 8 * heads + 4 * heads * chans) + N * (4 + 8 * heads + 4 * heads * chans + 4 * fo))
+        post = act != _lib.ACT_NONE or dropout_p > 0
+        ctx.save_for_backward(xh, att_src, att_dst, a_src, a_dst, alpha, seed_ctr, out if post else None)
+        ctx.meta = (plan, heads, chans, bool(concat), float(slope), bias is not None, int(act), float(dropout_p),
+                    int(seed))
         return out
 
     @staticmethod
     @_custom_bwd
     def backward(ctx, dout):
-        xh, att_src, att_dst, a_src, a_dst, alpha = ctx.saved_tensors
-        plan, heads, chans, concat, slope, has_bias = ctx.meta
+        xh, att_src, att_dst, a_src, a_dst, alpha, seed_ctr, out = ctx.saved_tensors
+        plan, heads, chans, concat, slope, has_bias, act, dropout_p, seed = ctx.meta
         dout = _as_f32_rows(dout)
         dev = xh.device
         N = plan.num_nodes
         F = heads * chans
+        if out is not None:  # through dropout(act(.)) first: d pre
+            dpre = torch.empty_like(out)
+            _lib.call("gnn_gat_act_bwd_f32", N, out.size(1), act, dropout_p, seed & 0xFFFFFFFFFFFFFFFF,
+                      _lib.ptr(seed_ctr), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout), dpre.data_ptr(),
+                      _ld(dpre), _lib.stream_handle(dev))
+            dout = dpre
         dxh = torch.empty((N, F), dtype=torch.float32, device=dev)
         datt_s = torch.empty(F, dtype=torch.float32, device=dev)
         datt_d = torch.empty(F, dtype=torch.float32, device=dev)
@@ -388,13 +402,15 @@ class _GATAttention(torch.autograd.Function):
         KernelTimer.end(t0, ("gat_bwd", heads, chans, fo),
                         S * (12 + 16 * heads + 4 * heads * chans + 4 * fo) + N * (8 + 16 * heads + 4 * F + 4 * fo))
         db = colsum(dout) if has_bias and ctx.needs_input_grad[3] else None
-        return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db, None, None, None, None, None)
+        return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db) + (None,) * 9
 
 
 def gat_attention(xh: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor, bias: torch.Tensor | None,
                   edge_index: torch.Tensor, heads: int, chans: int, concat: bool = True,
-                  negative_slope: float = 0.2) -> torch.Tensor:
-    """PyG GATConv after ``lin``: scores, self-loop replacement, edge softmax, aggregation, bias."""
+                  negative_slope: float = 0.2, act: int = _lib.ACT_NONE, dropout_p: float = 0.0, seed: int = 0,
+                  seed_ctr: torch.Tensor | None = None) -> torch.Tensor:
+    """PyG GATConv after ``lin``: scores, self-loop replacement, edge softmax, aggregation, bias;
+    optionally ``dropout(act(.))`` of GATNet's hidden layers on the store (counter-hash dropout)."""
     plan = get_plan(edge_index, xh.size(0), _lib.LOOPS_REPLACE)
     return _GATAttention.apply(xh, att_src, att_dst, bias, plan, int(heads), int(chans), bool(concat),
-                               float(negative_slope))
+                               float(negative_slope), int(act), float(dropout_p), int(seed), seed_ctr)

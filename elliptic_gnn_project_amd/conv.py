@@ -186,12 +186,15 @@ class GATConv(nn.Module):
             state_dict.pop(prefix + "lin_dst.weight", None)
         super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
 
-    def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor, *, _post=None) -> torch.Tensor:
+        """``_post`` = (act, dropout_p, seed, seed_ctr): GATNet's ``dropout(elu(.))`` applied on the
+        kernel's store (gnn.py:72-74) — internal to GATNet.forward, not part of PyG's API."""
         if getattr(self, "explain", False):
             raise NotImplementedError("explain-mode edge masks are implemented for SAGEConv and GCNConv")
         xh = self.lin(x)  # [N, H*C]
+        act, p, seed, ctr = _post if _post is not None else (_lib.ACT_NONE, 0.0, 0, None)
         return gat_attention(xh, self.att_src, self.att_dst, self.bias, edge_index, self.heads,
-                             self.out_channels, self.concat, self.negative_slope)
+                             self.out_channels, self.concat, self.negative_slope, act, p, seed, ctr)
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads})"

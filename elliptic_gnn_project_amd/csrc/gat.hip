@@ -16,7 +16,7 @@
 #include <initializer_list>
 #include <utility>
 
-#include "common.hpp"
+#include "gemm_common.hpp"  // keep_elem (the counter-hash dropout shared with the NT epilogue)
 
 namespace gnnmp {
 namespace {
@@ -308,97 +308,398 @@ __device__ __forceinline__ void stv(float* p, const VecF<VEC>& r) {
   else *p = r.v[0];
 }
 
-// Forward: per-head max and sum of exp in the pair view (the first pair's score kept in a
-// register), alpha written in pair order (contiguous: alpha[beg*H + idx]), then the
-// alpha-weighted gather in the slot view with alpha recomputed bit-identically.
+// Long rows: the plan's K0b csr_split lists the rows with more than T slots (Elliptic's hubs).
+// A group of G lanes would walk such a row in one dependent loop and set the kernel's tail,
+// so each long row gets a whole 256-thread block, and those blocks are dispatched ahead of
+// the short-row blocks (blockIdx < n): their chains overlap the bulk instead of trailing it.
+// The short-row path skips rows with more than T slots.
+struct GatLong {
+  const int32_t* rows;
+  int32_t n;
+  int32_t T;
+};
+
+// Store-side operands of the forward: GATNet's hidden-layer activation and dropout
+// (gnn.py:73-74) and, for the in-kernel score form, the attention vectors and score outputs.
+struct GatEpi {
+  int act;              // gnn_act
+  int dropout;
+  uint32_t keep_thresh;
+  float drop_scale;
+  uint64_t seed;        // as NTArgs: *seed_ptr * golden + seed when seed_ptr is set
+  const uint64_t* seed_ptr;
+  float* as_out;        // XS: a_src / a_dst written [N, H]
+  float* ad_out;
+};
+
+__device__ __forceinline__ uint64_t gat_seed(const GatEpi& e) {
+  return e.seed_ptr ? (*e.seed_ptr) * 0x9E3779B97F4A7C15ull + e.seed : e.seed;
+}
+
+__device__ __forceinline__ float gat_store_val(const GatEpi& e, uint64_t seed, float v, int64_t r, int col, int Fo) {
+  if (e.act == GNN_ACT_ELU) v = v > 0.0f ? v : expm1f(v);
+  if (e.dropout)
+    v = keep_elem(seed, (uint32_t)r * (uint32_t)Fo + (uint32_t)col, e.keep_thresh) ? v * e.drop_scale : 0.0f;
+  return v;
+}
+
+// Sum of a per-lane partial over the L slot-view lanes of one head (contiguous, starting at
+// lane h0 of the wave).  L a power of two: xor butterfly (commutative pairs: every lane gets the
+// bit-identical sum); otherwise a fixed-order gather.  All lanes of the head must be active.
+__device__ __forceinline__ float head_sum(float v, int L, int h0) {
+  if ((L & (L - 1)) == 0) {
+    for (int off = 1; off < L; off <<= 1) v += __shfl_xor(v, off);
+    return v;
+  }
+  float s = 0.0f;
+  for (int i = 0; i < L; ++i) s += __shfl(v, h0 + i);
+  return s;
+}
+
 template <int VEC>
-__global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int H = a.H, C = a.C, G = g.G;
-  const int lig = lane & (G - 1);
-  const int gbase = lane - lig;
-  const int rpw = 64 >> g.lgG;
-  const int hl = lig & (H - 1);
-  const int fl = lig & (g.FLp - 1);
-  const int ep = lig >> g.lgFLp;
-  const int EP = G >> g.lgFLp;
-  const bool slot_ok = fl < g.FL;
-  const int f0 = fl * VEC;
-  const int hs = slot_ok ? f0 / C : 0;
-  const int c0 = f0 - hs * C;
-  const int64_t rpb = 4 * (int64_t)rpw;
-  for (int64_t base = (int64_t)blockIdx.x * rpb; base < a.N; base += (int64_t)gridDim.x * rpb) {
-    const int64_t r = base + wave * rpw + (lane >> g.lgG);
-    const bool valid = r < a.N;
-    int32_t beg = 0, end = 0;
-    if (valid) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
-    const int32_t npair = (end - beg) << g.lgH;
-    const float adr = valid ? a.a_d[r * H + hl] : 0.0f;
-    float e0 = -INFINITY;
-    if (lig < npair) e0 = leaky(a.a_s[(int64_t)a.col[beg + (lig >> g.lgH)] * H + hl] + adr, a.slope);
-    float m = e0;
-#pragma unroll 1
-    for (int32_t idx = lig + G; idx < npair; idx += G)
-      m = fmaxf(m, leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope));
-    for (int off = G >> 1; off >= H; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    float s = lig < npair ? expf(e0 - m) : 0.0f;
-#pragma unroll 1
-    for (int32_t idx = lig + G; idx < npair; idx += G)
-      s += expf(leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope) - m);
-    for (int off = G >> 1; off >= H; off >>= 1) s += __shfl_xor(s, off);
-    const float denom = s + 1e-16f;
-    float* alpha_r = a.alpha + (int64_t)beg * H;
-    if (lig < npair) alpha_r[lig] = expf(e0 - m) / denom;
-#pragma unroll 1
-    for (int32_t idx = lig + G; idx < npair; idx += G)
-      alpha_r[idx] = expf(leaky(a.a_s[(int64_t)a.col[beg + (idx >> g.lgH)] * H + hl] + adr, a.slope) - m) / denom;
-    // slot view
-    const float ms = __shfl(m, gbase + hs);
-    const float dn = __shfl(denom, gbase + hs);
-    const float ads = valid ? a.a_d[r * H + hs] : 0.0f;
-    VecF<VEC> acc;
+__device__ __forceinline__ float vdot(const VecF<VEC>& x, const VecF<VEC>& w) {
+  float s = x.v[0] * w.v[0];
+#pragma unroll
+  for (int i = 1; i < VEC; ++i) s = fmaf(x.v[i], w.v[i], s);
+  return s;
+}
+
+// Online softmax state of one slot-view lane: running max m, sum s and accumulator (both
+// scaled by exp(-m)).  merge() combines two states; it is symmetric, so the two lanes of an
+// xor exchange end with bit-identical results.
+template <int VEC>
+struct Online {
+  float m, s;
+  VecF<VEC> acc;
+  __device__ __forceinline__ void init() {
+    m = -INFINITY;
+    s = 0.0f;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc.v[i] = 0.0f;
-    if (slot_ok) {
-#pragma unroll 2
-      for (int32_t k = beg + ep; k < end; k += EP) {
-        const int32_t j = a.col[k];
-        const float al = expf(leaky(a.a_s[(int64_t)j * H + hs] + ads, a.slope) - ms) / dn;
-        const VecF<VEC> x = ldv<VEC>(a.xh + (int64_t)j * a.ld_xh + f0);
+  }
+  __device__ __forceinline__ void add(float e, const VecF<VEC>& x) {
+    const float mn = fmaxf(m, e);
+    const float sc = expf(m - mn);
+    const float p = expf(e - mn);
+    s = s * sc + p;
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) acc.v[i] += al * x.v[i];
+    for (int i = 0; i < VEC; ++i) acc.v[i] = acc.v[i] * sc + p * x.v[i];
+    m = mn;
+  }
+  __device__ __forceinline__ void merge(float m2, float s2, const VecF<VEC>& acc2) {
+    const float mn = fmaxf(m, m2);
+    const float c1 = m == -INFINITY ? 0.0f : expf(m - mn);
+    const float c2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
+    s = s * c1 + s2 * c2;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc.v[i] = acc.v[i] * c1 + acc2.v[i] * c2;
+    m = mn;
+  }
+};
+
+// Per-lane geometry of the slot view (lanes over VEC-float feature slots x slot phases).
+struct SlotLane {
+  int fl, ep, EP, f0, hs, c0, L, hfirst;  // hfirst: first lane (wave index) of this lane's head
+  bool ok;
+};
+
+__device__ __forceinline__ SlotLane slot_lane(const GatGeom& g, int lig, int width, int wave_lane, int VEC, int C) {
+  SlotLane s;
+  s.fl = lig & (g.FLp - 1);
+  s.ep = lig >> g.lgFLp;
+  s.EP = width >> g.lgFLp;
+  s.ok = s.fl < g.FL;
+  s.f0 = s.fl * VEC;
+  s.hs = s.ok ? s.f0 / C : 0;
+  s.c0 = s.f0 - s.hs * C;
+  s.L = g.L;
+  s.hfirst = (wave_lane - s.fl) + s.hs * s.L;
+  return s;
+}
+
+// The slot pass of one lane: slots beg + ep, += EP, two per trip (both neighbour rows in flight;
+// the lanes of a head share their trip count, so the head_sum exchanges stay converged).
+template <int VEC, bool XS>
+__device__ __forceinline__ void slot_pass(const GatArgs& a, const SlotLane& sl, int32_t beg, int32_t end, float adr,
+                                          const VecF<VEC>& as_v, bool writer, Online<VEC>& st) {
+  const int H = a.H;
+  for (int32_t k = beg + sl.ep; k < end; k += 2 * sl.EP) {
+    const bool two = k + sl.EP < end;
+    const int32_t j0 = a.col[k];
+    const int32_t j1 = two ? a.col[k + sl.EP] : j0;
+    const VecF<VEC> x0 = ldv<VEC>(a.xh + (int64_t)j0 * a.ld_xh + sl.f0);
+    const VecF<VEC> x1 = ldv<VEC>(a.xh + (int64_t)j1 * a.ld_xh + sl.f0);
+    float s0, s1;
+    if constexpr (XS) {
+      s0 = head_sum(vdot<VEC>(x0, as_v), sl.L, sl.hfirst);
+      s1 = head_sum(vdot<VEC>(x1, as_v), sl.L, sl.hfirst);
+    } else {
+      s0 = a.a_s[(int64_t)j0 * H + sl.hs];
+      s1 = a.a_s[(int64_t)j1 * H + sl.hs];
+    }
+    const float e0 = leaky(s0 + adr, a.slope);
+    if (writer) a.alpha[(int64_t)k * H + sl.hs] = e0;
+    st.add(e0, x0);
+    if (two) {
+      const float e1 = leaky(s1 + adr, a.slope);
+      if (writer) a.alpha[(int64_t)(k + sl.EP) * H + sl.hs] = e1;
+      st.add(e1, x1);
+    }
+  }
+}
+
+constexpr int kLongLds = 4 * 64 * 2 + 4 * 256 + 256;  // wave m/s [4][64] x 2, partials [4][256], final [256]
+
+// One block, one long row (more than T slots): 256/FLp slot phases, each lane an online
+// softmax over its slots; phases merged in the wave by xor exchanges, waves through LDS in a
+// fixed order.  XS: scores from the gathered xh rows (and the row's own a_src / a_dst written).
+template <int VEC, bool XS>
+__device__ void gat_fwd_long_row(const GatArgs& a, const GatGeom& g, const GatEpi& ep_, uint64_t seed,
+                                 const VecF<VEC>& as_v, const VecF<VEC>& ad_v, int64_t r, float* sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, C = a.C, F = H * C;
+  const int Fo = a.concat ? F : C;
+  const SlotLane sl = slot_lane(g, tid, 256, lane, VEC, C);
+  const int32_t beg = a.rowptr[r], end = a.rowptr[r + 1];
+  float* sm = sh;
+  float* ss = sh + 256;
+  float* red = sh + 512;
+  float* fin = sh + 512 + 1024;
+  float adr;
+  if constexpr (XS) {
+    VecF<VEC> xr;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) xr.v[i] = 0.0f;
+    if (sl.ok) xr = ldv<VEC>(a.xh + r * a.ld_xh + sl.f0);
+    const float ps = head_sum(vdot<VEC>(xr, as_v), sl.L, sl.hfirst);
+    adr = head_sum(vdot<VEC>(xr, ad_v), sl.L, sl.hfirst);
+    if (sl.ok && sl.ep == 0 && sl.fl == sl.hs * sl.L) {
+      ep_.as_out[r * H + sl.hs] = ps;
+      ep_.ad_out[r * H + sl.hs] = adr;
+    }
+  } else {
+    adr = a.a_d[r * H + sl.hs];
+  }
+  const bool writer = sl.ok && sl.fl == sl.hs * sl.L;  // one lane per (head, phase) keeps the raw scores
+  Online<VEC> st;
+  st.init();
+  if (sl.ok) slot_pass<VEC, XS>(a, sl, beg, end, adr, as_v, writer, st);
+  for (int off = 32; off >= g.FLp; off >>= 1) {
+    VecF<VEC> a2;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) a2.v[i] = __shfl_xor(st.acc.v[i], off);
+    st.merge(__shfl_xor(st.m, off), __shfl_xor(st.s, off), a2);
+  }
+  if (lane < g.FLp) {
+    sm[wave * 64 + sl.fl] = st.m;
+    ss[wave * 64 + sl.fl] = st.s;
+    if (sl.ok) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) red[wave * 256 + sl.f0 + i] = st.acc.v[i];
+    }
+  }
+  __syncthreads();
+  Online<VEC> tot;
+  tot.init();
+  if (sl.ok) {
+    for (int w = 0; w < 4; ++w) {
+      VecF<VEC> a2;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) a2.v[i] = red[w * 256 + sl.f0 + i];
+      tot.merge(sm[w * 64 + sl.fl], ss[w * 64 + sl.fl], a2);
+    }
+  }
+  const float denom = tot.s + 1e-16f;
+  if (a.concat) {
+    if (sl.ok && sl.ep == 0) {
+      VecF<VEC> o;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const int f = sl.f0 + i;
+        o.v[i] = gat_store_val(ep_, seed, tot.acc.v[i] / denom + (a.bias ? a.bias[f] : 0.0f), r, f, Fo);
       }
+      stv<VEC>(a.out + r * a.ldo + sl.f0, o);
     }
-    for (int off = G >> 1; off >= g.FLp; off >>= 1) {
+  } else {
+    if (sl.ok && sl.ep == 0) {
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) acc.v[i] += __shfl_xor(acc.v[i], off);
+      for (int i = 0; i < VEC; ++i) fin[sl.f0 + i] = tot.acc.v[i] / denom;
     }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+      float t = 0.0f;
+      for (int h = 0; h < H; ++h) t += fin[h * C + c];
+      a.out[r * a.ldo + c] = gat_store_val(ep_, seed, t / (float)H + (a.bias ? a.bias[c] : 0.0f), r, c, Fo);
+    }
+  }
+  if (writer) {  // the lane's own raw scores, normalised in place
+#pragma unroll 1
+    for (int32_t k = beg + sl.ep; k < end; k += sl.EP) {
+      float* p = a.alpha + (int64_t)k * H + sl.hs;
+      *p = expf(*p - tot.m) / denom;
+    }
+  }
+}
+
+// Forward, short rows (<= T slots): G lanes per row in the slot view, one pass with an online
+// softmax per lane, merged across the EP slot phases by xor exchanges; out = acc / (s + 1e-16)
+// (+ bias, activation, dropout).  The lane that owns a (head, phase) writes each slot's raw
+// score e into alpha during the pass and normalises it afterwards (its own writes, re-read).
+// XS: the scores come from the gathered xh rows themselves (a_src[j] = <xh[j,h,:], att_src[h]>,
+// reduced over the head's lanes), so the only dependent loads per row are rowptr -> col -> xh.
+template <int VEC, bool XS>
+__global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g, GatLong lg, GatEpi ep_) {
+  __shared__ float sh[kLongLds];
+  const int lane = threadIdx.x & 63;
+  const int H = a.H, C = a.C, F = H * C;
+  const int Fo = a.concat ? F : C;
+  const uint64_t seed = ep_.dropout ? gat_seed(ep_) : 0;
+  // attention vectors of this lane's feature slot (XS)
+  VecF<VEC> as_v, ad_v;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) { as_v.v[i] = 0.0f; ad_v.v[i] = 0.0f; }
+  if ((int)blockIdx.x < lg.n) {
+    const SlotLane sl = slot_lane(g, threadIdx.x, 256, lane, VEC, C);
+    if (XS && sl.ok) { as_v = ldv<VEC>(a.att_s + sl.f0); ad_v = ldv<VEC>(a.att_d + sl.f0); }
+    gat_fwd_long_row<VEC, XS>(a, g, ep_, seed, as_v, ad_v, lg.rows[blockIdx.x], sh);
+    return;
+  }
+  const int64_t bid = blockIdx.x - lg.n, nblk = gridDim.x - lg.n;
+  const int wave = threadIdx.x >> 6;
+  const int G = g.G;
+  const int lig = lane & (G - 1);
+  const int rpw = 64 >> g.lgG;
+  const SlotLane sl = slot_lane(g, lig, G, lane, VEC, C);
+  if (XS && sl.ok) { as_v = ldv<VEC>(a.att_s + sl.f0); ad_v = ldv<VEC>(a.att_d + sl.f0); }
+  const bool writer = sl.ok && sl.fl == sl.hs * sl.L;
+  const int64_t rpb = 4 * (int64_t)rpw;
+  for (int64_t base = bid * rpb; base < a.N; base += nblk * rpb) {
+    const int64_t r = base + wave * rpw + (lane >> g.lgG);
+    int32_t beg = 0, end = 0;
+    if (r < a.N) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
+    const bool own = r < a.N && end - beg <= lg.T;
+    if (!own) end = beg;
+    float adr;
+    if constexpr (XS) {
+      VecF<VEC> xr;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) xr.v[i] = 0.0f;
+      if (own && sl.ok) xr = ldv<VEC>(a.xh + r * a.ld_xh + sl.f0);
+      const float ps = head_sum(vdot<VEC>(xr, as_v), sl.L, sl.hfirst);
+      adr = head_sum(vdot<VEC>(xr, ad_v), sl.L, sl.hfirst);
+      if (own && sl.ep == 0 && writer) {
+        ep_.as_out[r * H + sl.hs] = ps;
+        ep_.ad_out[r * H + sl.hs] = adr;
+      }
+    } else {
+      adr = own ? a.a_d[r * H + sl.hs] : 0.0f;
+    }
+    Online<VEC> st;
+    st.init();
+    if (sl.ok) slot_pass<VEC, XS>(a, sl, beg, end, adr, as_v, writer, st);
+    for (int off = G >> 1; off >= g.FLp; off >>= 1) {
+      VecF<VEC> a2;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) a2.v[i] = __shfl_xor(st.acc.v[i], off);
+      st.merge(__shfl_xor(st.m, off), __shfl_xor(st.s, off), a2);
+    }
+    const float denom = st.s + 1e-16f;
+    VecF<VEC> o;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) o.v[i] = st.acc.v[i] / denom;
     if (!a.concat) {  // mean over heads: same channel sits L slots apart (L, H powers of two)
       for (int off = g.FLp >> 1; off >= g.L; off >>= 1) {
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) acc.v[i] += __shfl_xor(acc.v[i], off);
+        for (int i = 0; i < VEC; ++i) o.v[i] += __shfl_xor(o.v[i], off);
       }
     }
-    if (valid && slot_ok && ep == 0) {
+    if (own && sl.ok && sl.ep == 0) {
       if (a.concat) {
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) acc.v[i] += a.bias ? a.bias[f0 + i] : 0.0f;
-        stv<VEC>(a.out + r * a.ldo + f0, acc);
-      } else if (hs == 0) {
+        for (int i = 0; i < VEC; ++i) {
+          const int f = sl.f0 + i;
+          o.v[i] = gat_store_val(ep_, seed, o.v[i] + (a.bias ? a.bias[f] : 0.0f), r, f, Fo);
+        }
+        stv<VEC>(a.out + r * a.ldo + sl.f0, o);
+      } else if (sl.hs == 0) {
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) acc.v[i] = acc.v[i] / (float)H + (a.bias ? a.bias[c0 + i] : 0.0f);
-        stv<VEC>(a.out + r * a.ldo + c0, acc);
+        for (int i = 0; i < VEC; ++i) {
+          const int c = sl.c0 + i;
+          o.v[i] = gat_store_val(ep_, seed, o.v[i] / (float)H + (a.bias ? a.bias[c] : 0.0f), r, c, Fo);
+        }
+        stv<VEC>(a.out + r * a.ldo + sl.c0, o);
+      }
+    }
+    if (writer) {
+#pragma unroll 1
+      for (int32_t k = beg + sl.ep; k < end; k += sl.EP) {
+        float* p = a.alpha + (int64_t)k * H + sl.hs;
+        *p = expf(*p - st.m) / denom;
       }
     }
   }
 }
 
+// Backward rows pass, one long row per block: the same two sweeps as the group kernel below
+// with 256 pair lanes and the per-head sums t / d a_dst taken across the waves through LDS.
+template <int VEC>
+__device__ void gat_bwd_long_row(const GatArgs& a, const GatGeom& g, int64_t r, float* sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, C = a.C;
+  const int32_t beg = a.rowptr[r], end = a.rowptr[r + 1];
+  const int32_t npair = (end - beg) << g.lgH;
+  const int hl = tid & (H - 1);
+  const float adr = a.a_d[r * H + hl];
+  const float inv_h = a.concat ? 1.0f : 1.0f / (float)H;
+  const float* dor = a.dout + r * a.ld_dout + (a.concat ? (int64_t)hl * C : 0);
+  const float* alpha_r = a.alpha + (int64_t)beg * H;
+  float* dz_r = a.dz + (int64_t)beg * H;
+  float t = 0.0f;
+  for (int32_t idx = tid; idx < npair; idx += 256) {
+    const int32_t j = a.col[beg + (idx >> g.lgH)];
+    const float* xr = a.xh + (int64_t)j * a.ld_xh + (int64_t)hl * C;
+    float da = 0.0f;
+    for (int c = 0; c < C; c += VEC) {
+      const VecF<VEC> d = ldv<VEC>(dor + c), x = ldv<VEC>(xr + c);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) da += d.v[i] * x.v[i];
+    }
+    da *= inv_h;
+    dz_r[idx] = da;
+    t += alpha_r[idx] * da;
+  }
+  for (int off = 32; off >= H; off >>= 1) t += __shfl_xor(t, off);
+  if (lane < H) sh[wave * 64 + lane] = t;
+  __syncthreads();
+  t = ((sh[hl] + sh[64 + hl]) + sh[128 + hl]) + sh[192 + hl];
+  float sdz = 0.0f;
+  for (int32_t idx = tid; idx < npair; idx += 256) {
+    const int32_t j = a.col[beg + (idx >> g.lgH)];
+    const float de = alpha_r[idx] * (dz_r[idx] - t);
+    const float z = a.a_s[(int64_t)j * H + hl] + adr;
+    const float dzv = z > 0.0f ? de : de * a.slope;
+    dz_r[idx] = dzv;
+    sdz += dzv;
+  }
+  for (int off = 32; off >= H; off >>= 1) sdz += __shfl_xor(sdz, off);
+  if (lane < H) sh[256 + wave * 64 + lane] = sdz;
+  __syncthreads();
+  if (tid < H) a.dad[r * H + tid] = ((sh[256 + tid] + sh[320 + tid]) + sh[384 + tid]) + sh[448 + tid];
+}
+
 // Backward rows pass (pair view, Gb lanes per row): d alpha per (slot, head) as a C-long dot
 // of the row's upstream gradient with the neighbour's features, kept in dz between the two
-// sweeps; then the softmax and leaky-relu backward and d a_dst = sum over the row.
+// sweeps; then the softmax and leaky-relu backward and d a_dst = sum over the row.  The first
+// pair of each lane keeps its d alpha, alpha and score sign in registers, so a short row's
+// second sweep re-reads nothing.
 template <int VEC>
-__global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatGeom g) {
+__global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatGeom g, GatLong lg) {
+  __shared__ float sh[512];
+  if ((int)blockIdx.x < lg.n) {
+    gat_bwd_long_row<VEC>(a, g, lg.rows[blockIdx.x], sh);
+    return;
+  }
+  const int64_t bid = blockIdx.x - lg.n, nblk = gridDim.x - lg.n;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int H = a.H, C = a.C, G = g.Gb;
@@ -407,17 +708,19 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatG
   const int hl = lig & (H - 1);
   const float inv_h = a.concat ? 1.0f : 1.0f / (float)H;
   const int64_t rpb = 4 * (int64_t)rpw;
-  for (int64_t base = (int64_t)blockIdx.x * rpb; base < a.N; base += (int64_t)gridDim.x * rpb) {
+  for (int64_t base = bid * rpb; base < a.N; base += nblk * rpb) {
     const int64_t r = base + wave * rpw + (lane >> g.lgGb);
-    const bool valid = r < a.N;
     int32_t beg = 0, end = 0;
-    if (valid) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
+    if (r < a.N) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
+    const bool own = r < a.N && end - beg <= lg.T;
+    if (!own) end = beg;
     const int32_t npair = (end - beg) << g.lgH;
-    const float adr = valid ? a.a_d[r * H + hl] : 0.0f;
-    const float* dor = a.dout + r * a.ld_dout + (a.concat ? (int64_t)hl * C : 0);
+    const float adr = own ? a.a_d[r * H + hl] : 0.0f;
+    const float* dor = a.dout + (own ? r : 0) * a.ld_dout + (a.concat ? (int64_t)hl * C : 0);
     const float* alpha_r = a.alpha + (int64_t)beg * H;
     float* dz_r = a.dz + (int64_t)beg * H;
-    float t = 0.0f;
+    float t = 0.0f, da0 = 0.0f, al0 = 0.0f;
+    bool pos0 = false;
     for (int32_t idx = lig; idx < npair; idx += G) {
       const int32_t j = a.col[beg + (idx >> g.lgH)];
       const float* xr = a.xh + (int64_t)j * a.ld_xh + (int64_t)hl * C;
@@ -428,12 +731,25 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatG
         for (int i = 0; i < VEC; ++i) da += d.v[i] * x.v[i];
       }
       da *= inv_h;
-      dz_r[idx] = da;
-      t += alpha_r[idx] * da;
+      const float al = alpha_r[idx];
+      if (idx == lig) {
+        da0 = da;
+        al0 = al;
+        pos0 = a.a_s[(int64_t)j * H + hl] + adr > 0.0f;
+      } else {
+        dz_r[idx] = da;
+      }
+      t += al * da;
     }
     for (int off = G >> 1; off >= H; off >>= 1) t += __shfl_xor(t, off);
     float sdz = 0.0f;
-    for (int32_t idx = lig; idx < npair; idx += G) {
+    if (lig < npair) {
+      const float de = al0 * (da0 - t);
+      const float dzv = pos0 ? de : de * a.slope;
+      dz_r[lig] = dzv;
+      sdz = dzv;
+    }
+    for (int32_t idx = lig + G; idx < npair; idx += G) {
       const int32_t j = a.col[beg + (idx >> g.lgH)];
       const float de = alpha_r[idx] * (dz_r[idx] - t);
       const float z = a.a_s[(int64_t)j * H + hl] + adr;
@@ -442,7 +758,7 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatG
       sdz += dzv;
     }
     for (int off = G >> 1; off >= H; off >>= 1) sdz += __shfl_xor(sdz, off);
-    if (valid && lig < H) a.dad[r * H + lig] = sdz;
+    if (own && lig < H) a.dad[r * H + lig] = sdz;
   }
 }
 
@@ -552,6 +868,55 @@ __global__ __launch_bounds__(256) void gat_att_reduce_kernel(int F, int nblk, co
   }
 }
 
+// Store-side activation / dropout as one in-place pass (the fused forward's fallback for shapes
+// outside the lane-group geometry).
+__global__ __launch_bounds__(256) void gat_act_fwd_kernel(int64_t N, int32_t Fo, float* __restrict__ out, int64_t ldo,
+                                                          GatEpi e) {
+  const uint64_t seed = e.dropout ? gat_seed(e) : 0;
+  const int64_t total = N * Fo;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / Fo;
+    const int c = (int)(t - r * Fo);
+    float* q = out + r * ldo + c;
+    *q = gat_store_val(e, seed, *q, r, c, Fo);
+  }
+}
+
+// d pre = dy * keep / (1-p) * act'(pre), from the stored y = dropout(act(pre)):
+// ELU' = 1 for y > 0, else exp(pre) = elu(pre) + 1 with elu(pre) = y * (1-p) for a kept element.
+__global__ __launch_bounds__(256) void gat_act_bwd_kernel(int64_t N, int32_t F, GatEpi e, float keep_p,
+                                                          const float* __restrict__ y, int64_t ldy,
+                                                          const float* dy, int64_t lddy, float* dp, int64_t ldp) {
+  const uint64_t seed = e.dropout ? gat_seed(e) : 0;
+  const int64_t total = N * F;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / F;
+    const int c = (int)(t - r * F);
+    float g = dy[r * lddy + c];
+    const float yv = y[r * ldy + c];
+    if (e.dropout) g = keep_elem(seed, (uint32_t)r * (uint32_t)F + (uint32_t)c, e.keep_thresh) ? g * e.drop_scale : 0.0f;
+    if (e.act == GNN_ACT_ELU && !(yv > 0.0f)) g = g * ((e.dropout ? yv * keep_p : yv) + 1.0f);
+    dp[r * ldp + c] = g;
+  }
+}
+
+GatEpi make_epi(int act, float dropout_p, uint64_t seed, const uint64_t* seed_ptr) {
+  GatEpi e{};
+  e.act = act;
+  e.dropout = dropout_p > 0.0f;
+  e.keep_thresh = (uint32_t)((1.0 - (double)dropout_p) * 16777216.0);  // as the NT epilogue (gemm_f32.hip)
+  e.drop_scale = e.dropout ? (float)(1.0 / (1.0 - (double)dropout_p)) : 1.0f;
+  e.seed = seed;
+  e.seed_ptr = seed_ptr;
+  return e;
+}
+
+unsigned elem_blocks(int64_t n) {
+  int64_t b = ceil_div(n, 256);
+  if (b > 16384) b = 16384;
+  return (unsigned)(b > 0 ? b : 1);
+}
+
 int ilog2(int v) { int l = 0; while ((1 << l) < v) ++l; return l; }
 int pow2ceil(int v) { return 1 << ilog2(v); }
 
@@ -592,6 +957,14 @@ unsigned group_blocks(int64_t N, int G, int64_t cap) {
   int64_t b = ceil_div(N, rpb);
   if (b > cap) b = cap;
   return (unsigned)(b > 0 ? b : 1);
+}
+
+// Long-row list of the plan's CSR split (K0b); none when the plan has no split.
+GatLong long_rows(const gnn_graph* g) {
+  const gnn_split* sp = g->csr_split;
+  if (sp && sp->num_long > 0 && sp->long_seg && sp->num_long < (int64_t)1 << 20)
+    return GatLong{sp->long_seg, (int32_t)sp->num_long, sp->seg_len};
+  return GatLong{nullptr, 0, INT32_MAX};
 }
 
 constexpr int64_t kColsBlocks = 2048;  // cols-pass grid cap = number of d att partials
@@ -658,13 +1031,78 @@ extern "C" gnn_status gnn_gat_fwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
   GatGeom gg;
   int vec = 1;
   if (gat_geom(H, C, concat, {{xh, ld_xh}, {out, ldo}}, &gg, &vec)) {
-    const unsigned nb = group_blocks(a.N, gg.G, (int64_t)1 << 20);
-    if (vec == 4) gat_fwd_group_kernel<4><<<nb, 256, 0, st>>>(a, gg);
-    else if (vec == 2) gat_fwd_group_kernel<2><<<nb, 256, 0, st>>>(a, gg);
-    else gat_fwd_group_kernel<1><<<nb, 256, 0, st>>>(a, gg);
+    const GatLong lg = long_rows(g);
+    const unsigned nb = group_blocks(a.N, gg.G, (int64_t)1 << 20) + (unsigned)lg.n;
+    const GatEpi ep{};
+    if (vec == 4) gat_fwd_group_kernel<4, false><<<nb, 256, 0, st>>>(a, gg, lg, ep);
+    else if (vec == 2) gat_fwd_group_kernel<2, false><<<nb, 256, 0, st>>>(a, gg, lg, ep);
+    else gat_fwd_group_kernel<1, false><<<nb, 256, 0, st>>>(a, gg, lg, ep);
   } else {
     gat_fwd_kernel<<<row_blocks(a.N), 256, 0, st>>>(a);
   }
+  GNN_LAUNCH_CHECK();
+  return GNN_OK;
+}
+
+extern "C" gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fwd_params* p, gnn_stream_t stream) {
+  if (!g || !p) return fail(GNN_ERR_INVALID_ARG, __func__, "null graph or params");
+  const int32_t H = p->heads, C = p->chans, concat = p->concat;
+  if (!pow2_heads(H)) return fail(GNN_ERR_UNSUPPORTED, __func__, "heads must be a power of two <= 64");
+  if (C < 1 || p->ld_xh < (int64_t)H * C || p->ldo < (concat ? (int64_t)H * C : C))
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad sizes");
+  if (p->act != GNN_ACT_NONE && p->act != GNN_ACT_ELU) return fail(GNN_ERR_INVALID_ARG, __func__, "unknown act");
+  if (!(p->dropout_p >= 0.0f && p->dropout_p < 1.0f)) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout_p not in [0, 1)");
+  if (g->num_nodes == 0) return GNN_OK;
+  if (!p->xh || !p->att_src || !p->att_dst || !p->a_src || !p->a_dst || !p->alpha || !p->out || !g->rowptr || !g->col)
+    return fail(GNN_ERR_INVALID_ARG, __func__, "null");
+  GatArgs a{};
+  a.rowptr = g->rowptr; a.col = g->col; a.N = g->num_nodes;
+  a.H = H; a.C = C; a.concat = concat; a.slope = p->slope;
+  a.xh = p->xh; a.ld_xh = p->ld_xh; a.a_s = p->a_src; a.a_d = p->a_dst; a.bias = p->bias;
+  a.att_s = p->att_src; a.att_d = p->att_dst;
+  a.alpha = p->alpha; a.out = p->out; a.ldo = p->ldo;
+  GatEpi ep = make_epi(p->act, p->dropout_p, p->seed, p->seed_ptr);
+  ep.as_out = p->a_src;
+  ep.ad_out = p->a_dst;
+  hipStream_t st = (hipStream_t)stream;
+  GatGeom gg;
+  int vec = 1;
+  if (gat_geom(H, C, concat, {{p->xh, p->ld_xh}, {p->out, p->ldo}, {p->att_src, 0}, {p->att_dst, 0}}, &gg, &vec)) {
+    const GatLong lg = long_rows(g);
+    const unsigned nb = group_blocks(a.N, gg.G, (int64_t)1 << 20) + (unsigned)lg.n;
+    if (vec == 4) gat_fwd_group_kernel<4, true><<<nb, 256, 0, st>>>(a, gg, lg, ep);
+    else if (vec == 2) gat_fwd_group_kernel<2, true><<<nb, 256, 0, st>>>(a, gg, lg, ep);
+    else gat_fwd_group_kernel<1, true><<<nb, 256, 0, st>>>(a, gg, lg, ep);
+    GNN_LAUNCH_CHECK();
+    return GNN_OK;
+  }
+  // generic geometry: scores pass, one wave per row, then the activation / dropout pass
+  gat_scores_kernel<<<(unsigned)ceil_div(a.N * H, 256), 256, 0, st>>>(a.N, H, C, p->xh, p->ld_xh, p->att_src,
+                                                                      p->att_dst, p->a_src, p->a_dst);
+  GNN_LAUNCH_CHECK();
+  gat_fwd_kernel<<<row_blocks(a.N), 256, 0, st>>>(a);
+  GNN_LAUNCH_CHECK();
+  if (ep.act != GNN_ACT_NONE || ep.dropout) {
+    const int32_t Fo = concat ? H * C : C;
+    gat_act_fwd_kernel<<<elem_blocks(a.N * Fo), 256, 0, st>>>(a.N, Fo, p->out, p->ldo, ep);
+    GNN_LAUNCH_CHECK();
+  }
+  return GNN_OK;
+}
+
+extern "C" gnn_status gnn_gat_act_bwd_f32(int64_t N, int64_t F, gnn_act act, float dropout_p, uint64_t seed,
+                                          const uint64_t* seed_ptr, const float* y, int64_t ldy, const float* dy,
+                                          int64_t lddy, float* dpre, int64_t ld_dpre, gnn_stream_t stream) {
+  if (N < 0 || F < 1 || F > INT32_MAX || ldy < F || lddy < F || ld_dpre < F)
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad sizes");
+  if (act != GNN_ACT_NONE && act != GNN_ACT_ELU) return fail(GNN_ERR_INVALID_ARG, __func__, "unknown act");
+  if (!(dropout_p >= 0.0f && dropout_p < 1.0f)) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout_p not in [0, 1)");
+  if (N == 0) return GNN_OK;
+  if (!y || !dy || !dpre) return fail(GNN_ERR_INVALID_ARG, __func__, "null");
+  const GatEpi ep = make_epi(act, dropout_p, seed, seed_ptr);
+  const float keep_p = (float)(1.0 - (double)dropout_p);
+  gat_act_bwd_kernel<<<elem_blocks(N * F), 256, 0, (hipStream_t)stream>>>(N, (int32_t)F, ep, keep_p, y, ldy, dy,
+                                                                         lddy, dpre, ld_dpre);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }
@@ -711,12 +1149,13 @@ extern "C" gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
   int vec = 1;
   if (gat_geom(H, C, concat, {{xh, ld_xh}, {dout, ld_dout}, {dxh, ld_dxh}, {att_src, 0}, {att_dst, 0}}, &gg,
                &vec)) {
-    const unsigned nbr = group_blocks(a.N, gg.Gb, (int64_t)1 << 20);
+    const GatLong lg = long_rows(g);
+    const unsigned nbr = group_blocks(a.N, gg.Gb, (int64_t)1 << 20) + (unsigned)lg.n;
     const unsigned nbc = group_blocks(a.N, gg.G, kColsBlocks);
     switch (vec) {
 #define GNN_GAT_BWD(V)                                                            \
   case V:                                                                         \
-    gat_bwd_rows_group_kernel<V><<<nbr, 256, 0, st>>>(a, gg);                     \
+    gat_bwd_rows_group_kernel<V><<<nbr, 256, 0, st>>>(a, gg, lg);                 \
     GNN_LAUNCH_CHECK();                                                           \
     gat_bwd_cols_group_kernel<V><<<nbc, 256, 0, st>>>(a, gg, part);               \
     break;

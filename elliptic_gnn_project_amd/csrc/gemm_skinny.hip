@@ -56,10 +56,11 @@ template <int VEC, int NC>
 __global__ __launch_bounds__(256) void nt_skinny_n_kernel(NTArgs a, int lg_tpr) {
   __shared__ float ws[SK_MAXN * SK_KMAX];
   const int K = a.k1 + a.k2;
-  for (int i = threadIdx.x; i < a.Nc * K; i += 256) {
+  for (int i = threadIdx.x; i < NC * K; i += 256) {  // rows Nc..NC-1 zero (their dots are discarded)
     const int n = i / K, k = i - n * K;
     float w;
-    if (a.bt) w = a.bt[(int64_t)k * a.ldb + n];
+    if (n >= a.Nc) w = 0.0f;
+    else if (a.bt) w = a.bt[(int64_t)k * a.ldb + n];
     else w = k < a.k1 ? a.w1[(int64_t)n * a.ldw1 + k] : a.w2[(int64_t)n * a.ldw2 + (k - a.k1)];
     ws[i] = w;
   }
@@ -227,7 +228,9 @@ bool launch_nt_skinny(const NTArgs& a, hipStream_t st) {
              (a.k2 == 0 || (a.k2 % v == 0 && a.lda2 % v == 0 && al(a.a2, 4 * v)));
     };
     const int VEC = v_ok(4) ? 4 : (v_ok(2) ? 2 : 1);
-    const int lg = std::min(6, lg2ceil(K / VEC));
+    // TPR lanes per row: enough for K/VEC chunks (capped at a wave) and at least Nc, since lane
+    // n of the row writes column n
+    const int lg = std::max(lg2ceil(a.Nc), std::min(6, lg2ceil(K / VEC)));
     const unsigned nb = grid_for(a.M, 256 >> lg, 8192);
     const int NC = a.Nc <= 1 ? 1 : a.Nc <= 2 ? 2 : a.Nc <= 4 ? 4 : 8;
 #define GNN_SKN(V, N) nt_skinny_n_kernel<V, N><<<nb, 256, 0, st>>>(a, lg)

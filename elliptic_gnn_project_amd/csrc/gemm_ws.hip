@@ -481,7 +481,7 @@ void launch_ws_k(const NTArgs& a, const uint4* bimg, const float* tail, hipStrea
 }  // namespace
 
 // Shapes the weight-stationary form takes: f32 A and C, contiguous A segments (lda == k, even k,
-// 16-byte aligned), 1 <= N <= 128, M >= 32, ceil((k1 + k2) / 16) k-steps in {8, 11, 16, 21}, and
+// 16-byte aligned), 64 < N <= 128, M >= 32, ceil((k1 + k2) / 16) k-steps in {8, 11, 16, 21}, and
 // an epilogue among plain | bias | bias+ReLU | bias+ReLU+dropout, each + projection when ReLU.
 bool nt_ws_ok(const NTArgs& a) {
   if (a.a_bf16 || a.c_bf16 || !a.w1 || a.Nc > BN || a.Nc < 1) return false;
@@ -491,6 +491,9 @@ bool nt_ws_ok(const NTArgs& a) {
   const int nks = (a.k1 + a.k2 + 15) / 16;
   if (nks != 8 && nks != 11 && nks != 16 && nks != 21) return false;
   if (a.M < WS_ROWS || a.M * (int64_t)std::max(a.k1, a.k2) >= ((int64_t)1 << 40)) return false;
+  // the block always computes 128 columns: at N <= 64 half its MFMAs are wasted and the tiled
+  // x3 kernel wins (r07: GAT/GCN layer 1, K = 166, N = 64: 104 vs 80 us)
+  if (a.Nc <= 64) return false;
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
   if ((drop || proj || relu) && !(relu && bias)) return false;
   return true;

@@ -288,21 +288,26 @@ def _graph_seed_counter(device: torch.device) -> torch.Tensor:
     return c
 
 
+def dropout_seeds(L: int, p: float, x: torch.Tensor):
+    """(per-layer seeds, device counter or None) for the counter-hash dropout of one forward:
+    L seeds from torch's CPU generator when eager; per-layer salts plus the bumped device
+    counter under HIP-graph capture (see _graph_seed_counter)."""
+    if p > 0 and torch.cuda.is_current_stream_capturing():
+        ctr = _graph_seed_counter(x.device)
+        ctr.add_(1)
+        return [l + 1 for l in range(L)], ctr
+    if p > 0:
+        if x.is_cuda:
+            _graph_seed_counter(x.device)  # create it outside any capture (a fill inside would replay)
+        return torch.randint(0, 2 ** 62, (L,), dtype=torch.int64).tolist(), None
+    return [0] * L, None
+
+
 def sage_forward(model, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
     plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
     L = len(model.convs)
     p = float(model.dropout) if model.training else 0.0
-    ctr = None
-    if p > 0 and torch.cuda.is_current_stream_capturing():
-        ctr = _graph_seed_counter(x.device)
-        ctr.add_(1)
-        seeds = [l + 1 for l in range(L)]  # per-layer salts
-    elif p > 0:
-        if x.is_cuda:
-            _graph_seed_counter(x.device)  # create it outside any capture (a fill inside would replay)
-        seeds = torch.randint(0, 2 ** 62, (L,), dtype=torch.int64).tolist()
-    else:
-        seeds = [0] * L
+    seeds, ctr = dropout_seeds(L, p, x)
     params = []
     for c in model.convs:
         params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]

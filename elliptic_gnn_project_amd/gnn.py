@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _lib
 from . import fused as _fused
 from .conv import GATConv, GCNConv, SAGEConv
 from .linear import Linear
@@ -77,6 +78,10 @@ class SAGENet(_StackedConvNet):
 
 
 class GATNet(_StackedConvNet):
+    """The hidden layers' ``dropout(elu(conv(h)))`` (gnn.py:72-74) runs on the attention kernel's
+    store (ELU, then the same counter-hash dropout as the fused SAGE path, oracle/dropout_hash.py);
+    explain mode falls back to F.elu / F.dropout around each conv."""
+
     act = staticmethod(F.elu)
 
     def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2, heads=4):
@@ -84,6 +89,17 @@ class GATNet(_StackedConvNet):
         convs = [GATConv(in_dim if i == 0 else hidden_dim, per_head, heads=heads) for i in range(layers - 1)]
         convs.append(GATConv(hidden_dim, num_classes, heads=1, concat=False))
         super().__init__(convs, dropout)
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor, t_idx: Optional[torch.Tensor] = None):
+        if not x.is_cuda or any(getattr(c, "explain", False) for c in self.convs):
+            return super().forward(x, edge_index, t_idx)
+        *hidden, last = self.convs
+        p = float(self.dropout) if self.training else 0.0
+        seeds, ctr = _fused.dropout_seeds(len(self.convs), p, x)
+        h = x
+        for i, conv in enumerate(hidden):
+            h = conv(h, edge_index, _post=(_lib.ACT_ELU, p, seeds[i], ctr))
+        return last(h, edge_index)
 
 
 class SAGEResBNNet(nn.Module):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 8
+#define GNNMP_ABI_VERSION 9
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -195,6 +195,35 @@ gnn_status gnn_gat_fwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t con
                            const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst,
                            const float* bias, float* alpha, float* out, int64_t ldo,
                            gnn_stream_t stream);
+
+/* Fused forward, scores in-kernel: a_src / a_dst are formed from the gathered xh rows and the
+ * attention vectors (no gnn_gat_scores_f32 pass; both are written out for the backward), and
+ * GATNet's hidden-layer activation is applied on the store (src/models/gnn.py:72-74):
+ *   out = dropout(act(sum_j alpha_ij xh[j] + bias))   act = GNN_ACT_NONE | GNN_ACT_ELU (alpha 1)
+ * dropout as in gnn_gemm_nt_params: keep iff hash(seed, row*F_out + col) < 1-p, kept / (1-p).
+ * Same softmax as gnn_gat_fwd_f32 (one-pass online max / sum, merged in a fixed order). */
+typedef enum { GNN_ACT_NONE = 0, GNN_ACT_ELU = 1 } gnn_act;
+typedef struct {
+  int32_t heads, chans, concat;
+  float slope;
+  const float* xh; int64_t ld_xh;         /* [N, H*C] */
+  const float* att_src; const float* att_dst;  /* [H*C] */
+  const float* bias;                      /* optional [F_out] */
+  gnn_act act;
+  float dropout_p;                        /* 0 = off */
+  uint64_t seed; const uint64_t* seed_ptr; /* as gnn_gemm_nt_params */
+  float* a_src; float* a_dst;             /* out [N, H] */
+  float* alpha;                           /* out [S, H] */
+  float* out; int64_t ldo;                /* out [N, F_out] */
+} gnn_gat_fwd_params;
+gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fwd_params* p, gnn_stream_t stream);
+
+/* Gradient through y = dropout(act(pre)) from y itself (F.elu / F.dropout backward, gnn.py:73-74):
+ * dpre = dy * keep * 1/(1-p) * act'(pre), ELU' = 1 for y > 0 else exp(pre) = y*(1-p) + 1.
+ * [N, F]; dpre may alias dy. */
+gnn_status gnn_gat_act_bwd_f32(int64_t N, int64_t F, gnn_act act, float dropout_p, uint64_t seed,
+                               const uint64_t* seed_ptr, const float* y, int64_t ldy, const float* dy,
+                               int64_t lddy, float* dpre, int64_t ld_dpre, gnn_stream_t stream);
 
 /* Backward.  dout is [N,H*C] (concat) or [N,C].  Produces dxh [N,H*C] (includes the score
  * paths through att_src/att_dst), d_att_src/d_att_dst [H*C].  workspace from

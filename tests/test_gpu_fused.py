@@ -146,7 +146,9 @@ def test_gemm_tn(device, M, nr, k1, k2, form, math):
 
 
 @pytest.mark.parametrize("M,k1,k2,n", [(50000, 64, 0, 2), (3001, 166, 166, 2), (1000, 7, 9, 5), (777, 384, 0, 8),
-                                       (4097, 2, 0, 64), (1000, 3, 0, 33), (513, 8, 0, 256), (100, 1, 0, 1)])
+                                       (4097, 2, 0, 64), (1000, 3, 0, 33), (513, 8, 0, 256), (100, 1, 0, 1),
+                                       # fewer K chunks than output columns (lanes per row >= N)
+                                       (1000, 12, 0, 6), (999, 8, 0, 8), (640, 4, 4, 5)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu", "dropout"])
 @pytest.mark.parametrize("wform", [False, True])
 def test_gemm_nt_skinny(device, M, k1, k2, n, epi, wform):

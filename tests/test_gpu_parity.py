@@ -225,6 +225,117 @@ def test_gat_conv(device, cfg):
             assert rel_l2(v.grad, leaf[k].grad) < 1e-5, (name, k)
 
 
+@pytest.mark.parametrize("cfg", [(24, 16, 4, True), (16, 2, 1, False), (20, 4, 2, False), (12, 3, 2, True)])
+def test_gat_long_rows(device, cfg):
+    """GAT over the K0b split graph (hub of 1000 in-slots, rows of 32/33/64/65 slots): the long
+    rows run one block each ahead of the short rows; matches PyG and the unsplit plan."""
+    import os
+
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.conv import GATConv
+    from elliptic_gnn_project_amd.graph import get_plan
+
+    fin, C, H, concat = cfg
+    ei, n = _split_graph()
+    torch.manual_seed(6)
+    conv = GATConv(fin, C, heads=H, concat=concat).to(device)
+    with torch.no_grad():
+        conv.bias.normal_()
+    p = _params(conv)
+    x = torch.randn(n, fin)
+    xg = x.to(device).requires_grad_(True)
+    eid = ei.to(device)
+    out = conv(xg, eid)
+    assert get_plan(eid, n, _lib.LOOPS_REPLACE).split_pieces(False) > 0  # the split (its long-row list) is used
+    xr = x.clone().requires_grad_(True)
+    leaf = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    ref = pyg_ref.gat_conv(xr, ei, leaf["lin.weight"], leaf["att_src"], leaf["att_dst"], leaf["bias"],
+                           H, C, concat=concat)
+    torch.testing.assert_close(out.detach().cpu(), ref.detach(), rtol=RTOL, atol=ATOL)
+    dy = torch.randn_like(ref)
+    out.backward(dy.to(device))
+    ref.backward(dy)
+    assert rel_l2(xg.grad, xr.grad) < 1e-5
+    for k, v in conv.named_parameters():
+        assert rel_l2(v.grad, leaf[k].grad) < 1e-5, k
+    os.environ["GNNMP_SPLIT"] = "0"
+    try:
+        eid2 = ei.clone().to(device)
+        out_p = conv(x.to(device), eid2)
+        assert get_plan(eid2, n, _lib.LOOPS_REPLACE).split_pieces(False) == 0
+    finally:
+        del os.environ["GNNMP_SPLIT"]
+    torch.testing.assert_close(out.detach(), out_p, rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.parametrize("cfg", [(24, 16, 4, True), (20, 3, 2, True), (10, 130, 1, True), (12, 4, 2, False)])
+@pytest.mark.parametrize("p", [0.0, 0.5])
+def test_gat_fused_post(device, cfg, p):
+    """gnn_gat_fwd_fused_f32 with ELU + counter-hash dropout on the store (GATNet's hidden-layer
+    dropout(elu(.))) and its backward, vs PyG + the same mask; (10, 130, 1) takes the generic
+    one-wave-per-row geometry (F/VEC > 64) and its separate activation pass."""
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.conv import GATConv
+    from oracle.dropout_hash import keep_mask
+
+    fin, C, H, concat = cfg
+    ei, n = _split_graph()
+    torch.manual_seed(8)
+    conv = GATConv(fin, C, heads=H, concat=concat).to(device)
+    with torch.no_grad():
+        conv.bias.normal_()
+    prm = _params(conv)
+    x = torch.randn(n, fin)
+    xg = x.to(device).requires_grad_(True)
+    seed = 0x1234_5678_9ABC
+    out = conv(xg, ei.to(device), _post=(_lib.ACT_ELU, p, seed, None))
+    xr = x.clone().requires_grad_(True)
+    leaf = {k: v.clone().requires_grad_(True) for k, v in prm.items()}
+    ref = torch.nn.functional.elu(pyg_ref.gat_conv(xr, ei, leaf["lin.weight"], leaf["att_src"], leaf["att_dst"],
+                                                   leaf["bias"], H, C, concat=concat))
+    if p > 0:
+        ref = ref * (torch.from_numpy(keep_mask(seed, n, ref.size(1), p)).float() / (1.0 - p))
+    torch.testing.assert_close(out.detach().cpu(), ref.detach(), rtol=RTOL, atol=ATOL)
+    dy = torch.randn_like(ref)
+    out.backward(dy.to(device))
+    ref.backward(dy)
+    assert rel_l2(xg.grad, xr.grad) < 1e-5
+    for k, v in conv.named_parameters():
+        assert rel_l2(v.grad, leaf[k].grad) < 1e-5, k
+
+
+@pytest.mark.parametrize("layers,hidden", [(2, 64), (3, 32)])
+def test_gat_net_train_dropout(device, layers, hidden):
+    """GATNet train step with dropout 0.5: logits and every gradient vs the oracle under the
+    same counter-hash masks (one per hidden layer, seeds drawn from torch's generator)."""
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.gnn import GATNet
+    from oracle.dropout_hash import keep_mask
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=5000, num_edges=6000, seed=31),
+                          dict(use_time_scalar=True, symmetrize_edges=False, train_window_k=10))
+    N = data.x.size(0)
+    torch.manual_seed(5)
+    model = GATNet(data.x.size(1), hidden, layers=layers, dropout=0.5, heads=4).to(device)
+    prm = _params(model)
+    model.train()
+    torch.manual_seed(77)
+    logits = model(data.x.to(device), data.edge_index.to(device))
+    torch.manual_seed(77)
+    seeds = torch.randint(0, 2 ** 62, (layers,), dtype=torch.int64).tolist()
+    masks = [torch.from_numpy(keep_mask(seeds[l], N, hidden, 0.5)) for l in range(layers - 1)]
+    mask = data.train_mask
+    cw = pyg_ref.class_weight(data.y[mask])
+    loss = pyg_ref.ce_loss(logits[mask.to(device)], data.y[mask].to(device), cw.to(device))
+    loss.backward()
+    kw = dict(layers=layers, heads=4, dropout=0.5, training=True, dropout_masks=masks)
+    ref = pyg_ref.model_forward("gat", prm, data.x, data.edge_index, **kw)
+    torch.testing.assert_close(logits.detach().cpu(), ref, rtol=RTOL, atol=ATOL)
+    _, grads = pyg_ref.train_step_grads("gat", prm, data.x, data.edge_index, data.y, mask, cw, **kw)
+    for k, v in model.named_parameters():
+        assert rel_l2(v.grad, grads[k]) < 1e-5, k
+
+
 MODELS = [
     ("sage", dict(hidden_dim=128, layers=2)),
     ("sage", dict(hidden_dim=128, layers=3)),
