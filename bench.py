@@ -73,7 +73,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--graph", action="store_true", help="replay the step as one captured HIP graph")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every kernel from Python each step (default: replay the step as captured "
+                         "HIP graphs; N>1: forward+backward graph, eager all-reduce, optimizer graph)")
+    ap.add_argument("--graph", action="store_true", help=argparse.SUPPRESS)  # the default; kept for old scripts
     ap.add_argument("--arch", default="sage", choices=sorted(PRESETS), help="workload (sage = headline)")
     ap.add_argument("--aten-step", action="store_true",
                     help="loss/clip/Adam with the ATen ops instead of the fused libgnnmp step ops")
@@ -348,7 +351,11 @@ def main():
     if dist is not None:
         gdist.convert_sync_batchnorm(model, dist)  # exact full-graph BN (SAGE-ResBN); no-op otherwise
     state0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    use_graph = args.graph
+    # HIP-graph replay of the step (the MI355X stand-in for a tracing compiler): one graph at N=1;
+    # at N>1 the gradient all-reduce stays eager between a forward+backward graph and an optimizer
+    # graph.  SyncBatchNorm's in-forward collective (SAGE-ResBN at N>1) keeps that case eager.
+    has_sync_bn = any(isinstance(m, gdist.SyncBatchNorm1d) for m in model.modules())
+    use_graph = not args.eager and not (dist is not None and has_sync_bn)
     if args.aten_step:
         opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4, fused=True, capturable=use_graph)
     else:  # clip_grad_norm_(1.0) + Adam fused (train_ops.ClipAdam: 2 launches, device step counter)
@@ -362,7 +369,7 @@ def main():
     t_idx = data.timestep if cfg.get("time_embed_dim", 0) > 0 else None
     ytr = data.y.index_select(0, tidx)
 
-    def eager_step():
+    def fwd_bwd():
         model.train()
         opt.zero_grad(set_to_none=bucket is None)
         logits = model(data.x, data.edge_index, t_idx)
@@ -371,16 +378,29 @@ def main():
         else:  # the same masked weighted CE, one fused kernel (fwd + dlogits)
             loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
         loss.backward()
-        if bucket is not None:
-            bucket.allreduce_(dist)
+        return loss
+
+    def allreduce():
+        bucket.allreduce_(dist)
+
+    def opt_step():
         if args.aten_step:
             torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
         opt.step()
+
+    def eager_step():
+        loss = fwd_bwd()
+        if bucket is not None:
+            allreduce()
+        opt_step()
         return loss
 
     if use_graph:
         from elliptic_gnn_project_amd.train_gnn import CapturedStep
-        step = CapturedStep(eager_step)
+        if bucket is None:
+            step = CapturedStep(eager_step)
+        else:
+            step = CapturedStep(fwd_bwd, mid=allreduce, tail=opt_step)
     else:
         step = eager_step
 
@@ -440,7 +460,8 @@ def main():
                 "max_nodes_per_gpu": int(n_local[0]), "max_edges_per_gpu": int(n_local[1]),
                 "parallelism": f"dp{world} timestep-partitioned ({args.scale})" if world > 1 else "single",
                 "collective": f"{args.dist_backend} all-reduce of one flat fp32 gradient bucket per step" if world > 1 else None,
-                "launch": "hip-graph replay of the whole step" if use_graph else "eager",
+                "launch": ("eager" if not use_graph else "hip-graph replay of the whole step" if bucket is None
+                           else "hip-graph replay of fwd+bwd and of the optimizer, eager all-reduce between"),
             },
             "roofline": roof,
             "cpu_baseline": cpu,

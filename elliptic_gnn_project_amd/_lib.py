@@ -149,6 +149,7 @@ class GnnGatFwdParams(ctypes.Structure):
         ("a_src", c_ptr), ("a_dst", c_ptr),
         ("alpha", c_ptr),
         ("out", c_ptr), ("ldo", c_i64),
+        ("edge_w", c_ptr),
     ]
 
 
@@ -227,6 +228,11 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
          c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_gat_bwd_ew_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
+         c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
     "gnn_gemm_nt_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_size)]),
     "gnn_gemm_nt_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),

@@ -414,3 +414,74 @@ def gat_attention(xh: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor
     plan = get_plan(edge_index, xh.size(0), _lib.LOOPS_REPLACE)
     return _GATAttention.apply(xh, att_src, att_dst, bias, plan, int(heads), int(chans), bool(concat),
                                float(negative_slope), int(act), float(dropout_p), int(seed), seed_ctr)
+
+
+class _GATAttentionMasked(torch.autograd.Function):
+    """Explain-mode GATConv propagate: every message alpha * xh[j] scaled by the per-slot mask
+    value w (generic one-wave-per-row kernels; d w from gnn_gat_bwd_ew_f32)."""
+
+    @staticmethod
+    @_custom_fwd
+    def forward(ctx, xh, att_src, att_dst, bias, w_slot, plan: GraphPlan, heads: int, chans: int, concat: bool,
+                slope: float):
+        xh = _as_f32_rows(xh)
+        N = plan.num_nodes
+        dev = xh.device
+        att_src = att_src.contiguous().float()
+        att_dst = att_dst.contiguous().float()
+        w_slot = w_slot.contiguous().float()
+        a_src = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        a_dst = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        alpha = torch.empty((max(plan.num_slots, 1), heads), dtype=torch.float32, device=dev)
+        fo = heads * chans if concat else chans
+        out = torch.empty((N, fo), dtype=torch.float32, device=dev)
+        b = bias.contiguous().float() if bias is not None else None
+        p = _lib.GnnGatFwdParams(
+            heads, chans, int(concat), float(slope), xh.data_ptr(), _ld(xh), att_src.data_ptr(), att_dst.data_ptr(),
+            _lib.ptr(b), _lib.ACT_NONE, 0.0, 0, None, a_src.data_ptr(), a_dst.data_ptr(), alpha.data_ptr(),
+            out.data_ptr(), _ld(out), w_slot.data_ptr(),
+        )
+        _lib.call("gnn_gat_fwd_fused_f32", plan.c_graph, p, _lib.stream_handle(dev))
+        ctx.save_for_backward(xh, att_src, att_dst, a_src, a_dst, alpha, w_slot)
+        ctx.meta = (plan, heads, chans, bool(concat), float(slope), bias is not None)
+        return out
+
+    @staticmethod
+    @_custom_bwd
+    def backward(ctx, dout):
+        xh, att_src, att_dst, a_src, a_dst, alpha, w_slot = ctx.saved_tensors
+        plan, heads, chans, concat, slope, has_bias = ctx.meta
+        dout = _as_f32_rows(dout)
+        dev = xh.device
+        N = plan.num_nodes
+        F = heads * chans
+        dxh = torch.empty((N, F), dtype=torch.float32, device=dev)
+        datt_s = torch.empty(F, dtype=torch.float32, device=dev)
+        datt_d = torch.empty(F, dtype=torch.float32, device=dev)
+        dw = torch.empty_like(w_slot)
+        nb = _lib.c_size(0)
+        _lib.call("gnn_gat_bwd_workspace_size", N, plan.num_slots, heads, chans, nb)
+        ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+        _lib.call("gnn_gat_bwd_ew_f32", plan.c_graph, heads, chans, int(concat), slope, xh.data_ptr(), _ld(xh),
+                  a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
+                  dout.data_ptr(), _ld(dout), dxh.data_ptr(), _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(),
+                  w_slot.data_ptr(), dw.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+        db = colsum(dout) if has_bias and ctx.needs_input_grad[3] else None
+        return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db, dw) + (None,) * 5
+
+
+def masked_gat_attention(xh: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor, bias: torch.Tensor | None,
+                         edge_index: torch.Tensor, edge_mask: torch.Tensor, heads: int, chans: int,
+                         concat: bool = True, negative_slope: float = 0.2) -> torch.Tensor:
+    """Explain-mode GATConv after ``lin``: ``edge_mask`` [E] (already sigmoided if so configured)
+    scales each input edge's message; input self loops are replaced (their mask unused) and the
+    appended loops carry 1, as PyG's ``edge_mask[self._loop_mask]`` + ones."""
+    if edge_mask.dim() != 1 or edge_mask.numel() != edge_index.size(1):
+        raise ValueError(f"edge_mask must be [E={edge_index.size(1)}], got {tuple(edge_mask.shape)}")
+    plan = get_plan(edge_index, xh.size(0), _lib.LOOPS_REPLACE)
+    S = plan.num_slots
+    eid = plan.csr_eid[:S].long()  # original edge id per CSR slot (appended loop of i: E + i)
+    m_ext = torch.cat([edge_mask.float(), edge_mask.new_ones(plan.num_nodes, dtype=torch.float32)])
+    w_slot = m_ext.index_select(0, eid)
+    return _GATAttentionMasked.apply(xh, att_src, att_dst, bias, w_slot, plan, int(heads), int(chans),
+                                     bool(concat), float(negative_slope))

@@ -21,7 +21,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .aggregation import colsum, gat_attention, gcn_aggregate, masked_gcn_aggregate, masked_mean_aggregate, mean_aggregate, aggregate
+from .aggregation import (aggregate, colsum, gat_attention, gcn_aggregate, masked_gat_attention, masked_gcn_aggregate,
+                          masked_mean_aggregate, mean_aggregate)
 from .graph import GraphPlan, get_plan
 from .linear import Linear, linear, linear2
 
@@ -189,8 +190,11 @@ class GATConv(nn.Module):
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor, *, _post=None) -> torch.Tensor:
         """``_post`` = (act, dropout_p, seed, seed_ctr): GATNet's ``dropout(elu(.))`` applied on the
         kernel's store (gnn.py:72-74) — internal to GATNet.forward, not part of PyG's API."""
-        if getattr(self, "explain", False):
-            raise NotImplementedError("explain-mode edge masks are implemented for SAGEConv and GCNConv")
+        if getattr(self, "explain", False) and getattr(self, "_edge_mask", None) is not None:
+            # PyG explain mode: each message alpha * xh_j scaled by the (sigmoided) edge mask
+            m = self._edge_mask.sigmoid() if getattr(self, "_apply_sigmoid", True) else self._edge_mask
+            return masked_gat_attention(self.lin(x), self.att_src, self.att_dst, self.bias, edge_index, m,
+                                        self.heads, self.out_channels, self.concat, self.negative_slope)
         xh = self.lin(x)  # [N, H*C]
         act, p, seed, ctr = _post if _post is not None else (_lib.ACT_NONE, 0.0, 0, None)
         return gat_attention(xh, self.att_src, self.att_dst, self.bias, edge_index, self.heads,

@@ -23,6 +23,14 @@ namespace {
 
 __device__ __forceinline__ float leaky(float z, float slope) { return z > 0.0f ? z : z * slope; }
 
+// Fast-path arithmetic (lane-group kernels): exp as one v_exp_f32 of x*log2(e) (exp(-inf) = 0,
+// relative error ~|x| * 2^-24: the softmax arguments are <= 0 and large |x| carry negligible
+// weight), 1/x as one v_rcp_f32 (1 ulp).  Both well inside the 1e-5 parity bound.
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// 24-bit row offsets (the host routes graphs with N or a row pitch >= 2^24 to the generic kernels)
+__device__ __forceinline__ uint32_t roff(int32_t row, int64_t ld) { return __umul24((uint32_t)row, (uint32_t)ld); }
+
 __device__ __forceinline__ float wave_max_over_heads(float v, int H) {
   for (int off = 32; off >= H; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
   return v;
@@ -72,6 +80,9 @@ struct GatArgs {
   float* dad;     // [N, H]
   float* das;     // [N, H]
   float* dxh; int64_t ld_dxh;
+  // explain mode (generic kernels only): per-CSR-slot message multiplier and its gradient
+  const float* ew;  // [S] or null
+  float* dew;       // [S] or null
 };
 
 // ---------------------------------------------------------------- forward (K5)
@@ -121,6 +132,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(GatArgs a) {
           int32_t j = a.col[k];
           float e = leaky(a.a_s[(int64_t)j * H + h] + adh, a.slope);
           float al = expf(e - mh) / dh;
+          if (a.ew) al *= a.ew[k];
           acc += al * a.xh[(int64_t)j * a.ld_xh + f];
         }
         if (a.bias) acc += a.bias[f];
@@ -138,6 +150,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(GatArgs a) {
             int32_t j = a.col[k];
             float e = leaky(a.a_s[(int64_t)j * H + h] + adh, a.slope);
             float al = expf(e - mh) / dh;
+            if (a.ew) al *= a.ew[k];
             acc += al * a.xh[(int64_t)j * a.ld_xh + h * C + c];
           }
           tot += acc;
@@ -175,6 +188,7 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_kernel(GatArgs a) {
       const float* xr = a.xh + (int64_t)j * a.ld_xh + (int64_t)hl * C;
       float da = 0.0f;
       for (int c = 0; c < C; ++c) da += dO(a, r, hl, c) * xr[c];
+      if (a.ew) da *= a.ew[k];
       t += a.alpha[(int64_t)k * H + hl] * da;
     }
     t = wave_sum_over_heads(t, H);
@@ -186,6 +200,12 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_kernel(GatArgs a) {
       float da = 0.0f;
       for (int c = 0; c < C; ++c) da += dO(a, r, hl, c) * xr[c];
       float al = a.alpha[(int64_t)k * H + hl];
+      if (a.dew) {  // d ew[k] = sum over heads of alpha * <dO, xh[j]>: the H lanes of slot k are adjacent
+        float v = al * da;
+        for (int off = 1; off < H; off <<= 1) v += __shfl_xor(v, off);
+        if (hl == 0) a.dew[k] = v;
+      }
+      if (a.ew) da *= a.ew[k];
       float de = al * (da - t);
       float z = a.a_s[(int64_t)j * H + hl] + adr;
       float dzv = z > 0.0f ? de : de * a.slope;
@@ -221,7 +241,9 @@ __global__ __launch_bounds__(256) void gat_bwd_cols_kernel(GatArgs a) {
       float acc = 0.0f;
       for (int32_t k = beg; k < end; ++k) {
         int32_t i = a.row[k];
-        float al = a.alpha[(int64_t)a.csc2csr[k] * H + h];
+        const int32_t ks = a.csc2csr[k];
+        float al = a.alpha[(int64_t)ks * H + h];
+        if (a.ew) al *= a.ew[ks];
         acc += al * dO(a, i, h, c);
       }
       const float dash = __shfl(s, h);
@@ -337,7 +359,7 @@ __device__ __forceinline__ uint64_t gat_seed(const GatEpi& e) {
 }
 
 __device__ __forceinline__ float gat_store_val(const GatEpi& e, uint64_t seed, float v, int64_t r, int col, int Fo) {
-  if (e.act == GNN_ACT_ELU) v = v > 0.0f ? v : expm1f(v);
+  if (e.act == GNN_ACT_ELU) v = v > 0.0f ? v : fexp(v) - 1.0f;
   if (e.dropout)
     v = keep_elem(seed, (uint32_t)r * (uint32_t)Fo + (uint32_t)col, e.keep_thresh) ? v * e.drop_scale : 0.0f;
   return v;
@@ -377,19 +399,22 @@ struct Online {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc.v[i] = 0.0f;
   }
-  __device__ __forceinline__ void add(float e, const VecF<VEC>& x) {
-    const float mn = fmaxf(m, e);
-    const float sc = expf(m - mn);
-    const float p = expf(e - mn);
-    s = s * sc + p;
+  // two slots at once (e1 = -inf: absent): 3 exps per pair; returns their unnormalised weights
+  __device__ __forceinline__ void add2(float e0, const VecF<VEC>& x0, float e1, const VecF<VEC>& x1, float& p0,
+                                       float& p1) {
+    const float mn = fmaxf(m, fmaxf(e0, e1));
+    const float sc = fexp(m - mn);  // 0 while m = -inf
+    p0 = fexp(e0 - mn);
+    p1 = fexp(e1 - mn);
+    s = (s * sc + p0) + p1;
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) acc.v[i] = acc.v[i] * sc + p * x.v[i];
+    for (int i = 0; i < VEC; ++i) acc.v[i] = (acc.v[i] * sc + p0 * x0.v[i]) + p1 * x1.v[i];
     m = mn;
   }
   __device__ __forceinline__ void merge(float m2, float s2, const VecF<VEC>& acc2) {
     const float mn = fmaxf(m, m2);
-    const float c1 = m == -INFINITY ? 0.0f : expf(m - mn);
-    const float c2 = m2 == -INFINITY ? 0.0f : expf(m2 - mn);
+    const float c1 = m == -INFINITY ? 0.0f : fexp(m - mn);
+    const float c2 = m2 == -INFINITY ? 0.0f : fexp(m2 - mn);
     s = s * c1 + s2 * c2;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) acc.v[i] = acc.v[i] * c1 + acc2.v[i] * c2;
@@ -418,33 +443,59 @@ __device__ __forceinline__ SlotLane slot_lane(const GatGeom& g, int lig, int wid
 }
 
 // The slot pass of one lane: slots beg + ep, += EP, two per trip (both neighbour rows in flight;
-// the lanes of a head share their trip count, so the head_sum exchanges stay converged).
+// the lanes of a head share their trip count, so the head_sum exchanges stay converged).  The
+// first trip's weights stay in registers (p0f, p1f with the running max m1 they refer to: most
+// rows end there); later trips park their raw scores in alpha (writer lane) for normalise_alpha.
 template <int VEC, bool XS>
 __device__ __forceinline__ void slot_pass(const GatArgs& a, const SlotLane& sl, int32_t beg, int32_t end, float adr,
-                                          const VecF<VEC>& as_v, bool writer, Online<VEC>& st) {
+                                          const VecF<VEC>& as_v, bool writer, Online<VEC>& st, float& p0f,
+                                          float& p1f, float& m1) {
   const int H = a.H;
-  for (int32_t k = beg + sl.ep; k < end; k += 2 * sl.EP) {
+  const int32_t k0 = beg + sl.ep;
+  for (int32_t k = k0; k < end; k += 2 * sl.EP) {
     const bool two = k + sl.EP < end;
     const int32_t j0 = a.col[k];
     const int32_t j1 = two ? a.col[k + sl.EP] : j0;
-    const VecF<VEC> x0 = ldv<VEC>(a.xh + (int64_t)j0 * a.ld_xh + sl.f0);
-    const VecF<VEC> x1 = ldv<VEC>(a.xh + (int64_t)j1 * a.ld_xh + sl.f0);
+    const VecF<VEC> x0 = ldv<VEC>(a.xh + roff(j0, a.ld_xh) + sl.f0);
+    const VecF<VEC> x1 = ldv<VEC>(a.xh + roff(j1, a.ld_xh) + sl.f0);
     float s0, s1;
     if constexpr (XS) {
       s0 = head_sum(vdot<VEC>(x0, as_v), sl.L, sl.hfirst);
       s1 = head_sum(vdot<VEC>(x1, as_v), sl.L, sl.hfirst);
     } else {
-      s0 = a.a_s[(int64_t)j0 * H + sl.hs];
-      s1 = a.a_s[(int64_t)j1 * H + sl.hs];
+      s0 = a.a_s[roff(j0, H) + sl.hs];
+      s1 = a.a_s[roff(j1, H) + sl.hs];
     }
     const float e0 = leaky(s0 + adr, a.slope);
-    if (writer) a.alpha[(int64_t)k * H + sl.hs] = e0;
-    st.add(e0, x0);
-    if (two) {
-      const float e1 = leaky(s1 + adr, a.slope);
-      if (writer) a.alpha[(int64_t)(k + sl.EP) * H + sl.hs] = e1;
-      st.add(e1, x1);
+    const float e1 = two ? leaky(s1 + adr, a.slope) : -INFINITY;
+    float p0, p1;
+    st.add2(e0, x0, e1, x1, p0, p1);
+    if (k == k0) {
+      p0f = p0;
+      p1f = p1;
+      m1 = st.m;
+    } else if (writer) {
+      a.alpha[roff(k, H) + sl.hs] = e0;
+      if (two) a.alpha[roff(k + sl.EP, H) + sl.hs] = e1;
     }
+  }
+}
+
+// alpha = exp(e - m) / denom for the writer lane's slots (rinv = 1 / denom): the first trip as
+// its kept weights rescaled to the final max, later trips from their parked raw scores.
+__device__ __forceinline__ void normalise_alpha(const GatArgs& a, const SlotLane& sl, int32_t beg, int32_t end,
+                                                float p0f, float p1f, float m1, float m, float rinv) {
+  const int H = a.H;
+  const int32_t k0 = beg + sl.ep;
+  if (k0 < end) {
+    const float sc = fexp(m1 - m) * rinv;
+    a.alpha[roff(k0, H) + sl.hs] = p0f * sc;
+    if (k0 + sl.EP < end) a.alpha[roff(k0 + sl.EP, H) + sl.hs] = p1f * sc;
+  }
+#pragma unroll 1
+  for (int32_t k = k0 + 2 * sl.EP; k < end; k += sl.EP) {
+    float* p = a.alpha + roff(k, H) + sl.hs;
+    *p = fexp(*p - m) * rinv;
   }
 }
 
@@ -470,7 +521,7 @@ __device__ void gat_fwd_long_row(const GatArgs& a, const GatGeom& g, const GatEp
     VecF<VEC> xr;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) xr.v[i] = 0.0f;
-    if (sl.ok) xr = ldv<VEC>(a.xh + r * a.ld_xh + sl.f0);
+    if (sl.ok) xr = ldv<VEC>(a.xh + roff((int32_t)r, a.ld_xh) + sl.f0);
     const float ps = head_sum(vdot<VEC>(xr, as_v), sl.L, sl.hfirst);
     adr = head_sum(vdot<VEC>(xr, ad_v), sl.L, sl.hfirst);
     if (sl.ok && sl.ep == 0 && sl.fl == sl.hs * sl.L) {
@@ -483,7 +534,8 @@ __device__ void gat_fwd_long_row(const GatArgs& a, const GatGeom& g, const GatEp
   const bool writer = sl.ok && sl.fl == sl.hs * sl.L;  // one lane per (head, phase) keeps the raw scores
   Online<VEC> st;
   st.init();
-  if (sl.ok) slot_pass<VEC, XS>(a, sl, beg, end, adr, as_v, writer, st);
+  float p0f = 0.0f, p1f = 0.0f, m1 = 0.0f;
+  if (sl.ok) slot_pass<VEC, XS>(a, sl, beg, end, adr, as_v, writer, st, p0f, p1f, m1);
   for (int off = 32; off >= g.FLp; off >>= 1) {
     VecF<VEC> a2;
 #pragma unroll
@@ -509,21 +561,21 @@ __device__ void gat_fwd_long_row(const GatArgs& a, const GatGeom& g, const GatEp
       tot.merge(sm[w * 64 + sl.fl], ss[w * 64 + sl.fl], a2);
     }
   }
-  const float denom = tot.s + 1e-16f;
+  const float rinv = frcp(tot.s + 1e-16f);
   if (a.concat) {
     if (sl.ok && sl.ep == 0) {
       VecF<VEC> o;
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         const int f = sl.f0 + i;
-        o.v[i] = gat_store_val(ep_, seed, tot.acc.v[i] / denom + (a.bias ? a.bias[f] : 0.0f), r, f, Fo);
+        o.v[i] = gat_store_val(ep_, seed, tot.acc.v[i] * rinv + (a.bias ? a.bias[f] : 0.0f), r, f, Fo);
       }
       stv<VEC>(a.out + r * a.ldo + sl.f0, o);
     }
   } else {
     if (sl.ok && sl.ep == 0) {
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) fin[sl.f0 + i] = tot.acc.v[i] / denom;
+      for (int i = 0; i < VEC; ++i) fin[sl.f0 + i] = tot.acc.v[i] * rinv;
     }
     __syncthreads();
     for (int c = tid; c < C; c += 256) {
@@ -532,19 +584,13 @@ __device__ void gat_fwd_long_row(const GatArgs& a, const GatGeom& g, const GatEp
       a.out[r * a.ldo + c] = gat_store_val(ep_, seed, t / (float)H + (a.bias ? a.bias[c] : 0.0f), r, c, Fo);
     }
   }
-  if (writer) {  // the lane's own raw scores, normalised in place
-#pragma unroll 1
-    for (int32_t k = beg + sl.ep; k < end; k += sl.EP) {
-      float* p = a.alpha + (int64_t)k * H + sl.hs;
-      *p = expf(*p - tot.m) / denom;
-    }
-  }
+  if (writer) normalise_alpha(a, sl, beg, end, p0f, p1f, m1, tot.m, rinv);
 }
 
 // Forward, short rows (<= T slots): G lanes per row in the slot view, one pass with an online
 // softmax per lane, merged across the EP slot phases by xor exchanges; out = acc / (s + 1e-16)
-// (+ bias, activation, dropout).  The lane that owns a (head, phase) writes each slot's raw
-// score e into alpha during the pass and normalises it afterwards (its own writes, re-read).
+// (+ bias, activation, dropout).  The lane that owns a (head, phase) normalises each slot's raw
+// score into alpha afterwards (the first trip's from registers, later ones re-read from alpha).
 // XS: the scores come from the gathered xh rows themselves (a_src[j] = <xh[j,h,:], att_src[h]>,
 // reduced over the head's lanes), so the only dependent loads per row are rowptr -> col -> xh.
 template <int VEC, bool XS>
@@ -584,7 +630,7 @@ __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g
       VecF<VEC> xr;
 #pragma unroll
       for (int i = 0; i < VEC; ++i) xr.v[i] = 0.0f;
-      if (own && sl.ok) xr = ldv<VEC>(a.xh + r * a.ld_xh + sl.f0);
+      if (r < a.N && sl.ok) xr = ldv<VEC>(a.xh + roff((int32_t)r, a.ld_xh) + sl.f0);  // beside the rowptr loads
       const float ps = head_sum(vdot<VEC>(xr, as_v), sl.L, sl.hfirst);
       adr = head_sum(vdot<VEC>(xr, ad_v), sl.L, sl.hfirst);
       if (own && sl.ep == 0 && writer) {
@@ -596,17 +642,18 @@ __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g
     }
     Online<VEC> st;
     st.init();
-    if (sl.ok) slot_pass<VEC, XS>(a, sl, beg, end, adr, as_v, writer, st);
+    float p0f = 0.0f, p1f = 0.0f, m1 = 0.0f;
+    if (sl.ok) slot_pass<VEC, XS>(a, sl, beg, end, adr, as_v, writer, st, p0f, p1f, m1);
     for (int off = G >> 1; off >= g.FLp; off >>= 1) {
       VecF<VEC> a2;
 #pragma unroll
       for (int i = 0; i < VEC; ++i) a2.v[i] = __shfl_xor(st.acc.v[i], off);
       st.merge(__shfl_xor(st.m, off), __shfl_xor(st.s, off), a2);
     }
-    const float denom = st.s + 1e-16f;
+    const float rinv = frcp(st.s + 1e-16f);
     VecF<VEC> o;
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) o.v[i] = st.acc.v[i] / denom;
+    for (int i = 0; i < VEC; ++i) o.v[i] = st.acc.v[i] * rinv;
     if (!a.concat) {  // mean over heads: same channel sits L slots apart (L, H powers of two)
       for (int off = g.FLp >> 1; off >= g.L; off >>= 1) {
 #pragma unroll
@@ -630,68 +677,117 @@ __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g
         stv<VEC>(a.out + r * a.ldo + sl.c0, o);
       }
     }
-    if (writer) {
-#pragma unroll 1
-      for (int32_t k = beg + sl.ep; k < end; k += sl.EP) {
-        float* p = a.alpha + (int64_t)k * H + sl.hs;
-        *p = expf(*p - st.m) / denom;
-      }
-    }
+    if (writer) normalise_alpha(a, sl, beg, end, p0f, p1f, m1, st.m, rinv);
   }
 }
 
-// Backward rows pass, one long row per block: the same two sweeps as the group kernel below
-// with 256 pair lanes and the per-head sums t / d a_dst taken across the waves through LDS.
+// Backward rows pass in the slot view (the forward's lanes): for slot k of row r and head h,
+// d alpha = <dO[r,h,:], xh[j,h,:]> (a VEC-wide dot per lane, summed over the head's lanes),
+// t_h = sum_k alpha d alpha (merged over the EP phases), then d e = alpha (d alpha - t), the
+// leaky-relu backward into dz[k,h] and d a_dst[r,h] = sum_k dz.  The first trip's
+// (d alpha, alpha, score sign) stay in registers; later trips park d alpha in dz (writer lane).
+struct BwdSlot {
+  float da, al;
+  bool pos;
+};
+
+template <int VEC>
+__device__ __forceinline__ float bwd_pass1(const GatArgs& a, const SlotLane& sl, int32_t beg, int32_t end, float adr,
+                                           const VecF<VEC>& dO, float inv_h, bool writer, BwdSlot& q0, BwdSlot& q1) {
+  const int H = a.H;
+  const int32_t k0 = beg + sl.ep;
+  float t = 0.0f;
+  for (int32_t k = k0; k < end; k += 2 * sl.EP) {
+    const bool two = k + sl.EP < end;
+    const int32_t j0 = a.col[k];
+    const int32_t j1 = two ? a.col[k + sl.EP] : j0;
+    const VecF<VEC> x0 = ldv<VEC>(a.xh + roff(j0, a.ld_xh) + sl.f0);
+    const VecF<VEC> x1 = ldv<VEC>(a.xh + roff(j1, a.ld_xh) + sl.f0);
+    const float al0 = a.alpha[roff(k, H) + sl.hs];
+    const float al1 = two ? a.alpha[roff(k + sl.EP, H) + sl.hs] : 0.0f;
+    const float z0 = a.a_s[roff(j0, H) + sl.hs] + adr;
+    const float z1 = a.a_s[roff(j1, H) + sl.hs] + adr;
+    const float da0 = head_sum(vdot<VEC>(x0, dO), sl.L, sl.hfirst) * inv_h;
+    const float da1 = head_sum(vdot<VEC>(x1, dO), sl.L, sl.hfirst) * inv_h;
+    if (k == k0) {
+      q0 = BwdSlot{da0, al0, z0 > 0.0f};
+      q1 = BwdSlot{da1, al1, z1 > 0.0f};
+    } else if (writer) {
+      a.dz[roff(k, H) + sl.hs] = da0;
+      if (two) a.dz[roff(k + sl.EP, H) + sl.hs] = da1;
+    }
+    t += al0 * da0;
+    if (two) t += al1 * da1;
+  }
+  return t;
+}
+
+// Writer lanes only: dz = leaky'(z) * alpha * (d alpha - t) per slot, returns their sum.
+__device__ __forceinline__ float bwd_pass2(const GatArgs& a, const SlotLane& sl, int32_t beg, int32_t end, float adr,
+                                           float t, const BwdSlot& q0, const BwdSlot& q1) {
+  const int H = a.H;
+  const int32_t k0 = beg + sl.ep;
+  float sdz = 0.0f;
+  if (k0 < end) {
+    const float de = q0.al * (q0.da - t);
+    const float v = q0.pos ? de : de * a.slope;
+    a.dz[roff(k0, H) + sl.hs] = v;
+    sdz += v;
+  }
+  if (k0 + sl.EP < end) {
+    const float de = q1.al * (q1.da - t);
+    const float v = q1.pos ? de : de * a.slope;
+    a.dz[roff(k0 + sl.EP, H) + sl.hs] = v;
+    sdz += v;
+  }
+#pragma unroll 1
+  for (int32_t k = k0 + 2 * sl.EP; k < end; k += sl.EP) {
+    const int32_t j = a.col[k];
+    float* p = a.dz + roff(k, H) + sl.hs;
+    const float de = a.alpha[roff(k, H) + sl.hs] * (*p - t);
+    const float v = a.a_s[roff(j, H) + sl.hs] + adr > 0.0f ? de : de * a.slope;
+    *p = v;
+    sdz += v;
+  }
+  return sdz;
+}
+
+// the lane's slice of the row's upstream gradient (concat: its features; mean: its channels)
+template <int VEC>
+__device__ __forceinline__ VecF<VEC> load_dO(const GatArgs& a, const SlotLane& sl, int64_t r, bool ok) {
+  VecF<VEC> d;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) d.v[i] = 0.0f;
+  if (ok && sl.ok) d = ldv<VEC>(a.dout + r * a.ld_dout + (a.concat ? sl.f0 : sl.c0));
+  return d;
+}
+
+// One block, one long row: 256/FLp slot phases; t and d a_dst merged in the wave by xor
+// exchanges and across the waves through LDS in a fixed order.
 template <int VEC>
 __device__ void gat_bwd_long_row(const GatArgs& a, const GatGeom& g, int64_t r, float* sh) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.H, C = a.C;
+  const SlotLane sl = slot_lane(g, tid, 256, lane, VEC, C);
+  const bool writer = sl.ok && sl.fl == sl.hs * sl.L;
   const int32_t beg = a.rowptr[r], end = a.rowptr[r + 1];
-  const int32_t npair = (end - beg) << g.lgH;
-  const int hl = tid & (H - 1);
-  const float adr = a.a_d[r * H + hl];
+  const float adr = a.a_d[r * H + sl.hs];
   const float inv_h = a.concat ? 1.0f : 1.0f / (float)H;
-  const float* dor = a.dout + r * a.ld_dout + (a.concat ? (int64_t)hl * C : 0);
-  const float* alpha_r = a.alpha + (int64_t)beg * H;
-  float* dz_r = a.dz + (int64_t)beg * H;
-  float t = 0.0f;
-  for (int32_t idx = tid; idx < npair; idx += 256) {
-    const int32_t j = a.col[beg + (idx >> g.lgH)];
-    const float* xr = a.xh + (int64_t)j * a.ld_xh + (int64_t)hl * C;
-    float da = 0.0f;
-    for (int c = 0; c < C; c += VEC) {
-      const VecF<VEC> d = ldv<VEC>(dor + c), x = ldv<VEC>(xr + c);
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) da += d.v[i] * x.v[i];
-    }
-    da *= inv_h;
-    dz_r[idx] = da;
-    t += alpha_r[idx] * da;
-  }
-  for (int off = 32; off >= H; off >>= 1) t += __shfl_xor(t, off);
-  if (lane < H) sh[wave * 64 + lane] = t;
+  const VecF<VEC> dO = load_dO<VEC>(a, sl, r, true);
+  BwdSlot q0{0.0f, 0.0f, false}, q1{0.0f, 0.0f, false};
+  float t = sl.ok ? bwd_pass1<VEC>(a, sl, beg, end, adr, dO, inv_h, writer, q0, q1) : 0.0f;
+  for (int off = 32; off >= g.FLp; off >>= 1) t += __shfl_xor(t, off);
+  if (lane < g.FLp) sh[wave * 64 + sl.fl] = t;
   __syncthreads();
-  t = ((sh[hl] + sh[64 + hl]) + sh[128 + hl]) + sh[192 + hl];
-  float sdz = 0.0f;
-  for (int32_t idx = tid; idx < npair; idx += 256) {
-    const int32_t j = a.col[beg + (idx >> g.lgH)];
-    const float de = alpha_r[idx] * (dz_r[idx] - t);
-    const float z = a.a_s[(int64_t)j * H + hl] + adr;
-    const float dzv = z > 0.0f ? de : de * a.slope;
-    dz_r[idx] = dzv;
-    sdz += dzv;
-  }
-  for (int off = 32; off >= H; off >>= 1) sdz += __shfl_xor(sdz, off);
-  if (lane < H) sh[256 + wave * 64 + lane] = sdz;
+  t = ((sh[sl.fl] + sh[64 + sl.fl]) + sh[128 + sl.fl]) + sh[192 + sl.fl];
+  float sdz = writer ? bwd_pass2(a, sl, beg, end, adr, t, q0, q1) : 0.0f;
+  for (int off = 32; off >= g.FLp; off >>= 1) sdz += __shfl_xor(sdz, off);
+  if (lane < g.FLp) sh[256 + wave * 64 + sl.fl] = sdz;
   __syncthreads();
-  if (tid < H) a.dad[r * H + tid] = ((sh[256 + tid] + sh[320 + tid]) + sh[384 + tid]) + sh[448 + tid];
+  if (writer && sl.ep == 0)
+    a.dad[r * H + sl.hs] = ((sh[256 + sl.fl] + sh[320 + sl.fl]) + sh[384 + sl.fl]) + sh[448 + sl.fl];
 }
 
-// Backward rows pass (pair view, Gb lanes per row): d alpha per (slot, head) as a C-long dot
-// of the row's upstream gradient with the neighbour's features, kept in dz between the two
-// sweeps; then the softmax and leaky-relu backward and d a_dst = sum over the row.  The first
-// pair of each lane keeps its d alpha, alpha and score sign in registers, so a short row's
-// second sweep re-reads nothing.
 template <int VEC>
 __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatGeom g, GatLong lg) {
   __shared__ float sh[512];
@@ -702,63 +798,27 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatG
   const int64_t bid = blockIdx.x - lg.n, nblk = gridDim.x - lg.n;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int H = a.H, C = a.C, G = g.Gb;
+  const int H = a.H, C = a.C, G = g.G;
   const int lig = lane & (G - 1);
-  const int rpw = 64 >> g.lgGb;
-  const int hl = lig & (H - 1);
+  const int rpw = 64 >> g.lgG;
+  const SlotLane sl = slot_lane(g, lig, G, lane, VEC, C);
+  const bool writer = sl.ok && sl.fl == sl.hs * sl.L;
   const float inv_h = a.concat ? 1.0f : 1.0f / (float)H;
   const int64_t rpb = 4 * (int64_t)rpw;
   for (int64_t base = bid * rpb; base < a.N; base += nblk * rpb) {
-    const int64_t r = base + wave * rpw + (lane >> g.lgGb);
+    const int64_t r = base + wave * rpw + (lane >> g.lgG);
     int32_t beg = 0, end = 0;
     if (r < a.N) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
+    const VecF<VEC> dO = load_dO<VEC>(a, sl, r, r < a.N);  // issued beside the rowptr loads
+    const float adr = r < a.N ? a.a_d[r * H + sl.hs] : 0.0f;
     const bool own = r < a.N && end - beg <= lg.T;
     if (!own) end = beg;
-    const int32_t npair = (end - beg) << g.lgH;
-    const float adr = own ? a.a_d[r * H + hl] : 0.0f;
-    const float* dor = a.dout + (own ? r : 0) * a.ld_dout + (a.concat ? (int64_t)hl * C : 0);
-    const float* alpha_r = a.alpha + (int64_t)beg * H;
-    float* dz_r = a.dz + (int64_t)beg * H;
-    float t = 0.0f, da0 = 0.0f, al0 = 0.0f;
-    bool pos0 = false;
-    for (int32_t idx = lig; idx < npair; idx += G) {
-      const int32_t j = a.col[beg + (idx >> g.lgH)];
-      const float* xr = a.xh + (int64_t)j * a.ld_xh + (int64_t)hl * C;
-      float da = 0.0f;
-      for (int c = 0; c < C; c += VEC) {
-        const VecF<VEC> d = ldv<VEC>(dor + c), x = ldv<VEC>(xr + c);
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) da += d.v[i] * x.v[i];
-      }
-      da *= inv_h;
-      const float al = alpha_r[idx];
-      if (idx == lig) {
-        da0 = da;
-        al0 = al;
-        pos0 = a.a_s[(int64_t)j * H + hl] + adr > 0.0f;
-      } else {
-        dz_r[idx] = da;
-      }
-      t += al * da;
-    }
-    for (int off = G >> 1; off >= H; off >>= 1) t += __shfl_xor(t, off);
-    float sdz = 0.0f;
-    if (lig < npair) {
-      const float de = al0 * (da0 - t);
-      const float dzv = pos0 ? de : de * a.slope;
-      dz_r[lig] = dzv;
-      sdz = dzv;
-    }
-    for (int32_t idx = lig + G; idx < npair; idx += G) {
-      const int32_t j = a.col[beg + (idx >> g.lgH)];
-      const float de = alpha_r[idx] * (dz_r[idx] - t);
-      const float z = a.a_s[(int64_t)j * H + hl] + adr;
-      const float dzv = z > 0.0f ? de : de * a.slope;
-      dz_r[idx] = dzv;
-      sdz += dzv;
-    }
-    for (int off = G >> 1; off >= H; off >>= 1) sdz += __shfl_xor(sdz, off);
-    if (own && lig < H) a.dad[r * H + lig] = sdz;
+    BwdSlot q0{0.0f, 0.0f, false}, q1{0.0f, 0.0f, false};
+    float t = sl.ok ? bwd_pass1<VEC>(a, sl, beg, end, adr, dO, inv_h, writer, q0, q1) : 0.0f;
+    for (int off = G >> 1; off >= g.FLp; off >>= 1) t += __shfl_xor(t, off);
+    float sdz = writer ? bwd_pass2(a, sl, beg, end, adr, t, q0, q1) : 0.0f;
+    for (int off = G >> 1; off >= g.FLp; off >>= 1) sdz += __shfl_xor(sdz, off);
+    if (own && writer && sl.ep == 0) a.dad[r * H + sl.hs] = sdz;
   }
 }
 
@@ -959,6 +1019,13 @@ unsigned group_blocks(int64_t N, int G, int64_t cap) {
   return (unsigned)(b > 0 ? b : 1);
 }
 
+// The lane-group kernels index rows and slots with 24-bit multiplies (roff).
+bool idx24_ok(const gnn_graph* g, int64_t ld_xh, int H) {
+  const int64_t lim = (int64_t)1 << 24;
+  return g->num_nodes < lim && g->num_slots < lim && ld_xh < lim && H < lim &&
+         g->num_nodes * ld_xh < ((int64_t)1 << 32) && g->num_slots * H < ((int64_t)1 << 32);
+}
+
 // Long-row list of the plan's CSR split (K0b); none when the plan has no split.
 GatLong long_rows(const gnn_graph* g) {
   const gnn_split* sp = g->csr_split;
@@ -1030,7 +1097,7 @@ extern "C" gnn_status gnn_gat_fwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
   hipStream_t st = (hipStream_t)stream;
   GatGeom gg;
   int vec = 1;
-  if (gat_geom(H, C, concat, {{xh, ld_xh}, {out, ldo}}, &gg, &vec)) {
+  if (idx24_ok(g, ld_xh, H) && gat_geom(H, C, concat, {{xh, ld_xh}, {out, ldo}}, &gg, &vec)) {
     const GatLong lg = long_rows(g);
     const unsigned nb = group_blocks(a.N, gg.G, (int64_t)1 << 20) + (unsigned)lg.n;
     const GatEpi ep{};
@@ -1061,13 +1128,15 @@ extern "C" gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fw
   a.xh = p->xh; a.ld_xh = p->ld_xh; a.a_s = p->a_src; a.a_d = p->a_dst; a.bias = p->bias;
   a.att_s = p->att_src; a.att_d = p->att_dst;
   a.alpha = p->alpha; a.out = p->out; a.ldo = p->ldo;
+  a.ew = p->edge_w;
   GatEpi ep = make_epi(p->act, p->dropout_p, p->seed, p->seed_ptr);
   ep.as_out = p->a_src;
   ep.ad_out = p->a_dst;
   hipStream_t st = (hipStream_t)stream;
   GatGeom gg;
   int vec = 1;
-  if (gat_geom(H, C, concat, {{p->xh, p->ld_xh}, {p->out, p->ldo}, {p->att_src, 0}, {p->att_dst, 0}}, &gg, &vec)) {
+  if (!p->edge_w && idx24_ok(g, p->ld_xh, H) &&
+      gat_geom(H, C, concat, {{p->xh, p->ld_xh}, {p->out, p->ldo}, {p->att_src, 0}, {p->att_dst, 0}}, &gg, &vec)) {
     const GatLong lg = long_rows(g);
     const unsigned nb = group_blocks(a.N, gg.G, (int64_t)1 << 20) + (unsigned)lg.n;
     if (vec == 4) gat_fwd_group_kernel<4, true><<<nb, 256, 0, st>>>(a, gg, lg, ep);
@@ -1115,17 +1184,18 @@ extern "C" gnn_status gnn_gat_bwd_workspace_size(int64_t N, int64_t S, int32_t H
   return GNN_OK;
 }
 
-extern "C" gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t concat, float slope,
-                                      const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst,
-                                      const float* att_src, const float* att_dst, const float* alpha,
-                                      const float* dout, int64_t ld_dout, float* dxh, int64_t ld_dxh,
-                                      float* d_att_src, float* d_att_dst, void* workspace,
-                                      size_t workspace_bytes, gnn_stream_t stream) {
-  if (!g) return fail(GNN_ERR_INVALID_ARG, __func__, "null graph");
-  if (!pow2_heads(H)) return fail(GNN_ERR_UNSUPPORTED, __func__, "heads must be a power of two <= 64");
+namespace gnnmp {
+namespace {
+gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C, int32_t concat, float slope,
+                        const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst, const float* att_src,
+                        const float* att_dst, const float* alpha, const float* dout, int64_t ld_dout, float* dxh,
+                        int64_t ld_dxh, float* d_att_src, float* d_att_dst, const float* edge_w, float* d_edge_w,
+                        void* workspace, size_t workspace_bytes, gnn_stream_t stream) {
+  if (!g) return fail(GNN_ERR_INVALID_ARG, fn, "null graph");
+  if (!pow2_heads(H)) return fail(GNN_ERR_UNSUPPORTED, fn, "heads must be a power of two <= 64");
   const int64_t F = (int64_t)H * C;
   if (C < 1 || ld_xh < F || ld_dxh < F || ld_dout < (concat ? F : C))
-    return fail(GNN_ERR_INVALID_ARG, __func__, "bad sizes");
+    return fail(GNN_ERR_INVALID_ARG, fn, "bad sizes");
   hipStream_t st = (hipStream_t)stream;
   if (g->num_nodes == 0) {
     GNN_HIP_TRY(hipMemsetAsync(d_att_src, 0, F * sizeof(float), st));
@@ -1134,23 +1204,24 @@ extern "C" gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
   }
   if (!xh || !a_src || !a_dst || !att_src || !att_dst || !alpha || !dout || !dxh || !d_att_src || !d_att_dst ||
       !g->colptr || !g->row || !g->csc2csr)
-    return fail(GNN_ERR_INVALID_ARG, __func__, "null");
+    return fail(GNN_ERR_INVALID_ARG, fn, "null");
   WorkspaceCarver c(workspace, workspace_bytes);
   GatArgs a{};
   float* part = nullptr;
   carve_bwd(c, g->num_nodes, g->num_slots, H, C, &a.dz, &a.dad, &a.das, &part);
-  if (!c.ok) return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
+  if (!c.ok) return fail(GNN_ERR_WORKSPACE, fn, "workspace too small");
   a.rowptr = g->rowptr; a.col = g->col; a.colptr = g->colptr; a.row = g->row; a.csc2csr = g->csc2csr;
   a.N = g->num_nodes; a.H = H; a.C = C; a.concat = concat; a.slope = slope;
   a.xh = xh; a.ld_xh = ld_xh; a.a_s = a_src; a.a_d = a_dst;
   a.att_s = att_src; a.att_d = att_dst; a.alpha = const_cast<float*>(alpha);
   a.dout = dout; a.ld_dout = ld_dout; a.dxh = dxh; a.ld_dxh = ld_dxh;
+  a.ew = edge_w; a.dew = d_edge_w;
   GatGeom gg;
   int vec = 1;
-  if (gat_geom(H, C, concat, {{xh, ld_xh}, {dout, ld_dout}, {dxh, ld_dxh}, {att_src, 0}, {att_dst, 0}}, &gg,
-               &vec)) {
+  if (!edge_w && idx24_ok(g, ld_xh, H) &&
+      gat_geom(H, C, concat, {{xh, ld_xh}, {dout, ld_dout}, {dxh, ld_dxh}, {att_src, 0}, {att_dst, 0}}, &gg, &vec)) {
     const GatLong lg = long_rows(g);
-    const unsigned nbr = group_blocks(a.N, gg.Gb, (int64_t)1 << 20) + (unsigned)lg.n;
+    const unsigned nbr = group_blocks(a.N, gg.G, (int64_t)1 << 20) + (unsigned)lg.n;
     const unsigned nbc = group_blocks(a.N, gg.G, kColsBlocks);
     switch (vec) {
 #define GNN_GAT_BWD(V)                                                            \
@@ -1181,4 +1252,30 @@ extern "C" gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
   gat_att_final_kernel<<<(unsigned)ceil_div(F, 256), 256, 0, st>>>((int)F, (int)nblk, part, d_att_src, d_att_dst);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
+}
+}  // namespace
+}  // namespace gnnmp
+
+extern "C" gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t concat, float slope,
+                                      const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst,
+                                      const float* att_src, const float* att_dst, const float* alpha,
+                                      const float* dout, int64_t ld_dout, float* dxh, int64_t ld_dxh,
+                                      float* d_att_src, float* d_att_dst, void* workspace,
+                                      size_t workspace_bytes, gnn_stream_t stream) {
+  return gat_bwd_impl(__func__, g, H, C, concat, slope, xh, ld_xh, a_src, a_dst, att_src, att_dst, alpha, dout,
+                      ld_dout, dxh, ld_dxh, d_att_src, d_att_dst, nullptr, nullptr, workspace, workspace_bytes,
+                      stream);
+}
+
+extern "C" gnn_status gnn_gat_bwd_ew_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t concat, float slope,
+                                         const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst,
+                                         const float* att_src, const float* att_dst, const float* alpha,
+                                         const float* dout, int64_t ld_dout, float* dxh, int64_t ld_dxh,
+                                         float* d_att_src, float* d_att_dst, const float* edge_w, float* d_edge_w,
+                                         void* workspace, size_t workspace_bytes, gnn_stream_t stream) {
+  if (!edge_w || (g && g->num_slots > 0 && !d_edge_w))
+    return fail(GNN_ERR_INVALID_ARG, __func__, "edge_w and d_edge_w are required");
+  return gat_bwd_impl(__func__, g, H, C, concat, slope, xh, ld_xh, a_src, a_dst, att_src, att_dst, alpha, dout,
+                      ld_dout, dxh, ld_dxh, d_att_src, d_att_dst, edge_w, d_edge_w, workspace, workspace_bytes,
+                      stream);
 }

@@ -211,27 +211,46 @@ def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cf
 
 
 class CapturedStep:
-    """A training step captured once into a HIP graph and replayed (torch.cuda.CUDAGraph).
+    """A training step captured into HIP graphs and replayed (torch.cuda.CUDAGraph).
 
-    ``step_fn`` must be capture-safe: static input tensors, no host syncs, optimizer built
-    with ``capturable=True``.  The fused SAGE path switches its dropout seed to a device
-    counter under capture, so every replay draws a new mask.  Replaying removes the host's
-    per-kernel launch cost (≈40 launches per step) and the gaps between kernels.
+    ``step_fn`` must be capture-safe: static input tensors, no host syncs, an optimizer whose
+    state advances on the device (ClipAdam, or torch Adam with ``capturable=True``).  The fused
+    SAGE / GAT paths switch their dropout seed to a device counter under capture, so every replay
+    draws a new mask.  Replaying removes the host's per-kernel launch cost and the gaps between
+    kernels.
+
+    Split form (``mid`` and ``tail`` given): ``step_fn`` (forward + backward) is graph A, ``mid``
+    runs eagerly (the data-parallel gradient all-reduce: the collective stays outside the
+    graphs) and ``tail`` (the optimizer step) is graph B.
     """
 
-    def __init__(self, step_fn, warmup: int = 3):
+    def __init__(self, step_fn, warmup: int = 3, mid=None, tail=None):
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 step_fn()
+                if mid is not None:
+                    mid()
+                if tail is not None:
+                    tail()
         torch.cuda.current_stream().wait_stream(side)
+        self.mid = mid
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = step_fn()
+        self.tail_graph = None
+        if tail is not None:
+            self.tail_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.tail_graph, pool=self.graph.pool()):
+                tail()
 
     def __call__(self):
         self.graph.replay()
+        if self.mid is not None:
+            self.mid()
+        if self.tail_graph is not None:
+            self.tail_graph.replay()
         return self.out
 
 

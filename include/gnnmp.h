@@ -215,6 +215,9 @@ typedef struct {
   float* a_src; float* a_dst;             /* out [N, H] */
   float* alpha;                           /* out [S, H] */
   float* out; int64_t ldo;                /* out [N, F_out] */
+  const float* edge_w;                    /* optional [S]: explain mode (PyG propagate with
+                                             `_explain`): every message alpha * xh[j] of CSR slot s is
+                                             multiplied by edge_w[s] after the softmax */
 } gnn_gat_fwd_params;
 gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fwd_params* p, gnn_stream_t stream);
 
@@ -235,6 +238,15 @@ gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t con
                            const float* dout, int64_t ld_dout, float* dxh, int64_t ld_dxh,
                            float* d_att_src, float* d_att_dst, void* workspace,
                            size_t workspace_bytes, gnn_stream_t stream);
+
+/* Explain-mode backward (messages scaled by edge_w[s], see gnn_gat_fwd_params.edge_w): as
+ * gnn_gat_bwd_f32, plus d_edge_w[s] = sum_h alpha[s,h] * <dout_i(h), xh[j,h,:]> for every CSR slot. */
+gnn_status gnn_gat_bwd_ew_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t concat, float slope,
+                              const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst,
+                              const float* att_src, const float* att_dst, const float* alpha,
+                              const float* dout, int64_t ld_dout, float* dxh, int64_t ld_dxh,
+                              float* d_att_src, float* d_att_dst, const float* edge_w, float* d_edge_w,
+                              void* workspace, size_t workspace_bytes, gnn_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* K7  fp32 MFMA GEMMs with the surrounding elementwise work fused in.      */

@@ -157,6 +157,29 @@ def gat_conv(x: Tensor, edge_index: Tensor, lin_w: Tensor, att_src: Tensor, att_
     return (out, alpha, ei) if return_alpha else out
 
 
+def gat_conv_explain(x: Tensor, edge_index: Tensor, edge_mask: Tensor, lin_w: Tensor, att_src: Tensor,
+                     att_dst: Tensor, bias: Optional[Tensor], heads: int, chans: int, concat: bool = True,
+                     negative_slope: float = 0.2, apply_sigmoid: bool = True) -> Tensor:
+    """GATConv in explain mode [PyG 2.5.3 MessagePassing.propagate, `if self._explain`]: the
+    message alpha * xh_j (after the edge softmax) is multiplied by the edge mask; the mask of the
+    non-loop input edges is kept (`edge_mask[self._loop_mask]`) and the appended loops get 1.
+    The reference drives it through GNNExplainer on GAT models (src/analysis/explain.py:309,593-672)."""
+    N = x.size(0)
+    m = edge_mask.sigmoid() if apply_sigmoid else edge_mask
+    keep = edge_index[0] != edge_index[1]
+    m = torch.cat([m[keep], m.new_ones(N)])
+    xh = F.linear(x, lin_w).view(-1, heads, chans)
+    a_src = (xh * att_src).sum(dim=-1)
+    a_dst = (xh * att_dst).sum(dim=-1)
+    ei = add_self_loops(remove_self_loops(edge_index), N)
+    alpha = F.leaky_relu(a_src.index_select(0, ei[0]) + a_dst.index_select(0, ei[1]), negative_slope)
+    alpha = softmax(alpha, ei[1], N)
+    msg = (alpha.unsqueeze(-1) * xh.index_select(0, ei[0])) * m.view(-1, 1, 1)
+    out = scatter(msg, ei[1], N, reduce="sum")
+    out = out.reshape(N, heads * chans) if concat else out.mean(dim=1)
+    return out + bias if bias is not None else out
+
+
 # ----------------------------------------------------------------------------- models (gnn.py)
 def _dropout(h: Tensor, p: float, training: bool, mask: Optional[Tensor]) -> Tensor:
     if not training or p == 0.0:

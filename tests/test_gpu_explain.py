@@ -122,3 +122,43 @@ def test_gcn_conv_explain_mode(device, name):
     assert rel_l2(mg.grad, mr.grad) <= 1e-5
     assert rel_l2(conv.lin.weight.grad, w.grad) <= 1e-5
     assert rel_l2(conv.bias.grad, b.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("name", list(GRAPHS))
+@pytest.mark.parametrize("cfg", [(24, 8, 4, True), (16, 2, 1, False), (12, 3, 2, False)])
+def test_gat_conv_explain_mode(device, name, cfg):
+    """GATConv explain mode: messages alpha * xh_j scaled by the sigmoided mask after
+    the softmax, input self loops lose their mask, appended loops carry 1; outputs and the mask /
+    weight / attention / bias gradients vs the oracle's PyG restatement."""
+    from elliptic_gnn_project_amd.conv import GATConv, clear_masks, set_masks
+
+    fin, C, H, concat = cfg
+    spec = GRAPHS[name]
+    ei = rand_graph(**spec)
+    n, E = spec["n"], ei.size(1)
+    torch.manual_seed(10)
+    conv = GATConv(fin, C, heads=H, concat=concat).to(device)
+    with torch.no_grad():
+        conv.bias.normal_()
+    p = {k: v.detach().cpu() for k, v in conv.state_dict().items()}
+    x = torch.randn(n, fin, generator=torch.Generator().manual_seed(4))
+    logit = torch.randn(E, generator=torch.Generator().manual_seed(5)) * 2.0
+    mg = logit.to(device).requires_grad_(True)
+    set_masks(conv, mg, ei.to(device))
+    out = conv(x.to(device), ei.to(device))
+    mr = logit.clone().requires_grad_(True)
+    leaf = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    ref = pyg_ref.gat_conv_explain(x, ei, mr, leaf["lin.weight"], leaf["att_src"], leaf["att_dst"], leaf["bias"],
+                                   H, C, concat=concat)
+    torch.testing.assert_close(out.detach().cpu(), ref.detach(), rtol=1e-5, atol=1e-5)
+    dy = torch.randn(ref.shape, generator=torch.Generator().manual_seed(6))
+    out.backward(dy.to(device))
+    ref.backward(dy)
+    assert rel_l2(mg.grad, mr.grad) <= 1e-5
+    for k, v in conv.named_parameters():
+        assert rel_l2(v.grad, leaf[k].grad) <= 1e-5, k
+    clear_masks(conv)  # back to the fused path: equals the unmasked oracle
+    with torch.no_grad():
+        plain = conv(x.to(device), ei.to(device))
+    ref0 = pyg_ref.gat_conv(x, ei, p["lin.weight"], p["att_src"], p["att_dst"], p["bias"], H, C, concat=concat)
+    torch.testing.assert_close(plain.cpu(), ref0, rtol=1e-5, atol=1e-5)
