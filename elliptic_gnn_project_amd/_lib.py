@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -246,6 +246,12 @@ SIGNATURES = {
         [c_i64, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr],
     ),
     "gnn_clip_adam_workspace_size": (ctypes.c_int, [ctypes.POINTER(c_size)]),
+    "gnn_neighbor_sample_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_size)]),
+    "gnn_neighbor_sample": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i32, c_ptr, ctypes.c_uint64, c_ptr, c_i64, c_ptr, c_ptr,
+         c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+    ),
     "gnn_clip_adam_f32": (ctypes.c_int, [ctypes.POINTER(GnnAdamGroup), c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
 }
 

@@ -85,6 +85,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   constexpr int KH = KH0;                  // register slots per wave (the second part has <= KH0)
   constexpr int QN = (128 * NKS + WS_THREADS - 1) / WS_THREADS;  // staged quads per thread per tile
   constexpr int RV = 16 / KS;              // accumulator rows (r-slots) a wave finishes
+  constexpr bool TWO = (LAB & 16) != 0;    // two independent accumulator chains
   // LDS: two A buffers, the C tile of the epilogue ([32 rows][128] f32: coalesced C stores and
   // the projection read it), the K-half exchange (KS 2: aliased onto the C tile when the A
   // buffers leave no room — one more barrier per tile) and the projection weights.
@@ -216,7 +217,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
 
   // MFMAs of this wave's K half from `cur`; the next tile's quads split into `nxt` in between
   auto kloop = [&](const char* cur, char* nxt, int sb, int tload) {
-    floatx16 acc;
+    floatx16 acc, acc2;
     constexpr int SQ0 = KH - QN > 0 ? KH - QN : 0;  // k-steps SQ0.. stage one quad each
     // one fragment set, each plane re-read for step s+1 right after its last use in step s:
     // plane 2 after MFMA 1, plane 1 after MFMA 3, plane 0 after MFMA 6 — each read has 3-5
@@ -243,7 +244,12 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       if (s + 1 < KH) x[2] = frag(sn, 2);
       if (stg) stage_pair(nxt, sb, qi, 0);
       WS_FENCE;
-      if (mm) ws_mfma<false>(acc, x[1], bw[s][1]);
+      if (mm) {
+        if constexpr (TWO) {
+          if (s == 0) ws_mfma<true>(acc2, x[1], bw[s][1]);
+          else ws_mfma<false>(acc2, x[1], bw[s][1]);
+        } else ws_mfma<false>(acc, x[1], bw[s][1]);
+      }
       WS_FENCE;
       if (stg) stage_pair(nxt, sb, qi, 1);
       WS_FENCE;
@@ -253,9 +259,9 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       if (stg) load_quad(sb, qi, tload);
       WS_FENCE;
       if (mm) {
-        ws_mfma<false>(acc, x[0], bw[s][2]);
+        ws_mfma<false>(TWO ? acc2 : acc, x[0], bw[s][2]);
         ws_mfma<false>(acc, x[0], bw[s][1]);
-        ws_mfma<false>(acc, x[0], bw[s][0]);
+        ws_mfma<false>(TWO ? acc2 : acc, x[0], bw[s][0]);
       }
       WS_FENCE;
       if (s + 1 < KH) x[0] = frag(sn, 0);
@@ -274,6 +280,11 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       for (int r = 0; r < 16; ++r) acc[r] = x[0][r & 7];
     }
     ws_mfma_end(acc);
+    if constexpr (TWO) {
+      ws_mfma_end(acc2);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
+    }
     return acc;
   };
 
@@ -520,6 +531,8 @@ void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks) {
         case 2: GNN_WSL(21, 1, 2); break;
         case 3: GNN_WSL(21, 1, 3); break;
         case 4: GNN_WSL(21, 1, 4); break;
+        case 6: GNN_WSL(21, 1, 19); break;
+        case 7: GNN_WSL(21, 1, 16); break;
         default: GNN_WSL(21, 1, 8); break;
       }
       return;

@@ -737,7 +737,11 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
     case 7: launch_nt_x3_b<16, 1, 2, 2, 2, 2>(a, bimg, st); break;  // ablation: no global loads in the loop
     case 8: launch_nt_x3_b<16, 1, 2, 2, 2, 6>(a, bimg, st); break;  // ablation: MFMA phase + barriers only
     case 9: launch_nt_x3_b<16, 1, 2, 2, 2, 3>(a, bimg, st); break;  // ablation: LDS staging + barriers only
-    case 10: case 11: case 12: case 13: case 14:  // lab: weight-stationary ablations (gemm_ws.hip)
+    case 5:  // lab: ws, two accumulator chains (-7), and the same without staging / epilogue (15 -> -6)
+      if (nt_ws_ok(a)) launch_nt_ws(a, const_cast<uint4*>(bimg), st, -7);
+      else launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
+      break;
+    case 10: case 11: case 12: case 13: case 14: case 15:  // lab: weight-stationary ablations (gemm_ws.hip)
       if (nt_ws_ok(a)) launch_nt_ws(a, const_cast<uint4*>(bimg), st, -(variant - 9));
       else launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
       break;

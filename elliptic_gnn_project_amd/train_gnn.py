@@ -12,7 +12,7 @@ Kept from the reference (same names, same YAML keys, same semantics):
                                   best.ckpt, optional hub ablation)
 New optional keys: ``synthetic`` (dict of synthetic_elliptic kwargs, used when no
 processed graph exists), ``graph_file`` (PyG-free .npz written by dataset_elliptic.save_graph).
-The mini-batch NeighborLoader path (:212-245, :329-348) is not implemented.
+The mini-batch path (:212-245, :260-276, :329-348) runs on loader.NeighborLoader (K11 sampling).
 """
 from __future__ import annotations
 
@@ -208,6 +208,51 @@ def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cf
         loss = loss.detach().clone()
         dist.all_reduce(loss)  # the global loss (sum of the ranks' partial means)
     return float(loss.item()) if sync else loss.detach()
+
+
+def train_epoch_minibatch(model, loader, optimizer, loss_fn, scaler, use_amp, cfg, device):
+    """One epoch over NeighborLoader batches (src/train_gnn.py:212-245): the loss is taken on the
+    first ``batch.batch_size`` rows (the seeds), one optimizer step per batch; returns the
+    seed-weighted mean loss."""
+    model.train()
+    total_loss, total_examples = 0.0, 0
+    uses_t = _model_uses_time_embed(model)
+    weighted = cfg.get("time_loss_weighting", "none") != "none"
+    for batch in loader:
+        batch = batch.to(device)
+        bs = int(batch.batch_size)
+        optimizer.zero_grad(set_to_none=True)
+        with _autocast(device, use_amp):
+            logits = model(batch.x, batch.edge_index, batch.timestep if uses_t else None)
+            t_idx = batch.timestep[:bs] if weighted else None
+            loss = loss_fn(logits[:bs], batch.y[:bs], t_idx)
+        scaler.scale(loss).backward()
+        if cfg.get("grad_clip", 0) and cfg["grad_clip"] > 0 and not _clips_itself(optimizer):
+            scaler.unscale_(optimizer)
+            torch.nn.utils.clip_grad_norm_(model.parameters(), cfg["grad_clip"])
+        scaler.step(optimizer)
+        scaler.update()
+        optimizer.zero_grad(set_to_none=True)
+        total_loss += float(loss.item()) * bs
+        total_examples += bs
+    return 0.0 if total_examples == 0 else float(total_loss / total_examples)
+
+
+@torch.no_grad()
+def eval_val_minibatch(model, loader, device):
+    """src/train_gnn.py:260-276: P(illicit) of every batch's seed rows, concatenated."""
+    model.eval()
+    ys, ps = [], []
+    uses_t = _model_uses_time_embed(model)
+    for batch in loader:
+        batch = batch.to(device)
+        bs = int(batch.batch_size)
+        logits = model(batch.x, batch.edge_index, batch.timestep if uses_t else None)[:bs]
+        ps.append(torch.softmax(logits, dim=1)[:, 1].detach().cpu())
+        ys.append(batch.y[:bs].detach().cpu())
+    if not ys:
+        return np.array([]), np.array([])
+    return torch.cat(ys).numpy(), torch.cat(ps).numpy()
 
 
 class CapturedStep:
@@ -427,8 +472,10 @@ def main(cfg: Dict) -> Dict:
     outdir = os.path.join(cfg.get("output_root", "outputs"), "gnn", cfg["run_name"])
     logger = RunLogger(outdir) if is_main else None
     device = get_device(cfg)
-    if bool(cfg.get("mini_batch", False)):
-        raise NotImplementedError("mini_batch: NeighborLoader sampling is not implemented yet (SURVEY §8f #3)")
+    use_mini_batch = bool(cfg.get("mini_batch", False))
+    if use_mini_batch and dist is not None:
+        raise NotImplementedError("mini_batch with world_size > 1: the reference's NeighborLoader path is "
+                                  "single-device (src/train_gnn.py:329-348)")
     use_amp = bool(cfg.get("amp", True))
     scaler = torch.amp.GradScaler(device=device.type, enabled=use_amp)
 
@@ -451,12 +498,26 @@ def main(cfg: Dict) -> Dict:
     gmask = (lambda name: getattr(full, name)) if dist is not None else (lambda name: getattr(data, name))
     ev = dict(dist=dist, num_nodes=N) if dist is not None else {}
 
+    train_loader = val_loader = None
+    if use_mini_batch:  # src/train_gnn.py:329-348 (loaders over the symmetrized graph)
+        from .loader import NeighborLoader
+        fanout = cfg.get("fanout", [10, 10])
+        bsz = int(cfg.get("batch_size", 8192))
+        train_loader = NeighborLoader(data, num_neighbors=fanout, batch_size=bsz,
+                                      input_nodes=data.train_mask.nonzero().view(-1), shuffle=True)
+        val_loader = NeighborLoader(data, num_neighbors=fanout, batch_size=bsz,
+                                    input_nodes=data.val_mask.nonzero().view(-1), shuffle=False)
+
     best_val, best_state, bad = -1.0, None, 0
     patience = cfg.get("patience", 20)
     for epoch in range(1, cfg["max_epochs"] + 1):
-        loss = train_epoch(model, data, ei, opt, loss_fn, scaler, use_amp, cfg, device, denom=n_train,
-                           bucket=bucket, dist=dist)
-        y_val, p_val, _ = eval_split(model, data, ei, gmask("val_mask"), **ev)
+        if use_mini_batch:
+            loss = train_epoch_minibatch(model, train_loader, opt, loss_fn, scaler, use_amp, cfg, device)
+            y_val, p_val = eval_val_minibatch(model, val_loader, device)
+        else:
+            loss = train_epoch(model, data, ei, opt, loss_fn, scaler, use_amp, cfg, device, denom=n_train,
+                               bucket=bucket, dist=dist)
+            y_val, p_val, _ = eval_split(model, data, ei, gmask("val_mask"), **ev)
         pr_val = 0.0 if y_val.size == 0 else pr_auc_illicit((y_val == 1).astype(int), p_val)
         if logger is not None:
             logger.log_epoch(epoch, loss, pr_val)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 9
+#define GNNMP_ABI_VERSION 10
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -355,6 +355,33 @@ typedef struct {
 gnn_status gnn_clip_adam_workspace_size(size_t* bytes);
 gnn_status gnn_clip_adam_f32(const gnn_adam_group* group, float* step, float* norm_out, void* workspace,
                              size_t workspace_bytes, gnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* K11 NeighborLoader neighbour sampling (torch_geometric.loader.NeighborLoader + pyg-lib
+ *     neighbor_sample, built at src/train_gnn.py:329-348 and consumed by
+ *     train_epoch_minibatch / eval_val_minibatch, src/train_gnn.py:212-276)            */
+/* ------------------------------------------------------------------------ */
+/* Workspace for gnn_neighbor_sample over a graph of num_nodes with the given capacities. */
+gnn_status gnn_neighbor_sample_workspace_size(int64_t num_nodes, int64_t node_cap, int64_t edge_cap,
+                                              size_t* bytes);
+
+/* Sample one batch over the CSR-by-target direction of `g` (a GNN_LOOPS_KEEP plan of the
+ * full graph's edge_index): seeds[num_seeds] (distinct, device int32) become local nodes
+ * 0..B-1; hop h samples up to fanout[h] (host array; -1 = all, else 1..256) in-neighbours of
+ * every node first discovered in hop h-1, uniformly without replacement (all of them when the
+ * in-degree is <= fanout), from a counter hash of (seed, hop, node, draw).  New nodes are
+ * appended to n_id in order of first appearance in the hop's edge list (disjoint=False dedup).
+ * Edges: e_src[s] -> e_dst[s] in local ids (the original edge direction), e_id[s] = PyG edge
+ * id (csr_eid[slot], or the CSR slot when csr_eid is NULL); hop-major, then frontier node,
+ * then PyG edge order.  hop_nodes[num_hops+1] / hop_edges[num_hops] (HOST arrays) receive
+ * PyG's num_sampled_nodes / num_sampled_edges.  Output sizes are data dependent: the call
+ * synchronises `stream` twice per hop to read them.  INVALID_ARG when a capacity is exceeded
+ * or seeds repeat, INDEX_OUT_OF_RANGE for a seed outside [0, N). */
+gnn_status gnn_neighbor_sample(const gnn_graph* g, const int32_t* csr_eid, const int32_t* seeds,
+                               int64_t num_seeds, int32_t num_hops, const int32_t* fanout, uint64_t seed,
+                               int32_t* n_id, int64_t node_cap, int32_t* e_src, int32_t* e_dst,
+                               int32_t* e_id, int64_t edge_cap, int64_t* hop_nodes, int64_t* hop_edges,
+                               void* workspace, size_t workspace_bytes, gnn_stream_t stream);
 
 #ifdef __cplusplus
 }

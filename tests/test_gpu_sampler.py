@@ -1,0 +1,173 @@
+"""GPU: K11 NeighborLoader sampling (csrc/sample.hip) through the C ABI.
+
+* bit-exact against the CPU restatement (oracle/neighbor_sample.py, same counter hash and
+  Floyd draws) on graphs with hubs, duplicate edges, self loops and isolated nodes, for the
+  reference's fan-out [10, 10] and others, including -1 (all: PyG's deterministic k-hop case,
+  pinned in tests/test_sampler_oracle.py against a BFS statement of PyG's semantics);
+* at the Elliptic size (203,769 nodes, batch 8192, fan-out [10, 10], src/train_gnn.py:333-348)
+  the size-independent contract: edges ⊆ graph with the right direction, per-node fan-out
+  bound, no cross-timestep edges, unique n_id with the seeds first, determinism per seed;
+* the loader covers every input node once per epoch, and train_epoch_minibatch /
+  eval_val_minibatch / main(mini_batch=True) run end to end.
+PyG's own choice of subset (pyg-lib RNG) is not reproducible: "parity unpinned" for that.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import neighbor_sample as NS
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(device, n=3000, e=6000, seed=3):
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+
+    d = prepare_inputs(synthetic_elliptic(num_nodes=n, num_edges=e, seed=seed),
+                       dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+    return d.to(device)
+
+
+def _graph(n, e, seed):
+    rng = np.random.default_rng(seed)
+    src, dst = rng.integers(0, n, e), rng.integers(0, n, e)
+    hub = 5  # hub with duplicate in-edges and a self loop; node n-1 left isolated
+    src = np.concatenate([src, rng.integers(0, n - 1, 300), [hub, 0, 0]])
+    dst = np.concatenate([dst, np.full(300, hub), [hub, 1, 1]])
+    src[src == n - 1] = 0
+    dst[dst == n - 1] = 0
+    return np.stack([src, dst])
+
+
+def _loader_for(device, ei, n, fanout, bs):
+    from elliptic_gnn_project_amd.dataset_elliptic import GraphData
+    from elliptic_gnn_project_amd.loader import NeighborLoader
+
+    x = torch.arange(n, dtype=torch.float32, device=device).view(n, 1)
+    data = GraphData(x=x, edge_index=torch.from_numpy(ei).to(device))
+    return NeighborLoader(data, num_neighbors=fanout, batch_size=bs)
+
+
+@pytest.mark.parametrize("fanout", [[10, 10], [2, 3], [-1, -1], [1], [25, 10, 5], [3, -1]])
+def test_sampler_matches_oracle(device, fanout):
+    n = 400
+    ei = _graph(n, 1500, 1)
+    ld = _loader_for(device, ei, n, fanout, 64)
+    for seeds, sd in (([5, 17, 399, 0, 200, 33], 7), (list(range(0, 400, 7)), 12345678901234567)):
+        b = ld.sample(torch.tensor(seeds), seed=sd)
+        n_id, eil, e_id, hn, he = NS.neighbor_sample(ei, n, seeds, fanout, sd)
+        assert b.n_id.cpu().tolist() == n_id.tolist()
+        assert torch.equal(b.edge_index.cpu(), torch.from_numpy(eil))
+        assert b.e_id.cpu().tolist() == e_id.tolist()
+        assert b.num_sampled_nodes == hn and b.num_sampled_edges == he
+        assert b.batch_size == len(seeds)
+        assert torch.equal(b.x.view(-1).long().cpu(), b.n_id.cpu())  # node features follow n_id
+
+
+def test_sampler_errors(device):
+    n = 50
+    ei = _graph(n, 100, 2)
+    ld = _loader_for(device, ei, n, [3], 8)
+    with pytest.raises(ValueError):
+        ld.sample(torch.tensor([1, 1]), seed=0)
+    with pytest.raises(IndexError):
+        ld.sample(torch.tensor([1, 50]), seed=0)
+    b = ld.sample(torch.tensor([], dtype=torch.int64), seed=0)
+    assert b.n_id.numel() == 0 and b.edge_index.shape == (2, 0)
+    with pytest.raises(ValueError):
+        _loader_for(device, ei, n, [300], 8)
+
+
+def test_sampler_elliptic_size_contract(device):
+    from elliptic_gnn_project_amd.loader import NeighborLoader
+
+    data = _data(device, n=203_769, e=234_355, seed=42)
+    train_idx = data.train_mask.nonzero().view(-1)
+    ld = NeighborLoader(data, num_neighbors=[10, 10], batch_size=8192, input_nodes=train_idx, shuffle=True)
+    torch.manual_seed(0)
+    b = next(iter(ld))
+    ei = data.edge_index
+    n_id, e_id, lei = b.n_id, b.e_id, b.edge_index
+    B = b.batch_size
+    assert B == min(8192, train_idx.numel())
+    assert torch.unique(n_id).numel() == n_id.numel()
+    assert torch.isin(n_id[:B], train_idx).all()
+    # every sampled edge is a graph edge, direction kept: neighbour -> frontier node
+    assert torch.equal(ei[0][e_id], n_id[lei[0]]) and torch.equal(ei[1][e_id], n_id[lei[1]])
+    # no cross-timestep edges (src/data/dataset_elliptic.py:235-243)
+    assert torch.equal(data.timestep[n_id[lei[0]]], data.timestep[n_id[lei[1]]])
+    # fan-out bound per hop: min(in-degree, 10) picks per frontier node, hop 1 targets are seeds
+    indeg = torch.bincount(ei[1], minlength=data.num_nodes)
+    e1 = b.num_sampled_edges[0]
+    c1 = torch.bincount(lei[1][:e1], minlength=B)
+    assert torch.equal(c1, torch.clamp(indeg[n_id[:B]], max=10))
+    f0, f1 = B, B + b.num_sampled_nodes[1]
+    c2 = torch.bincount(lei[1][e1:] - f0, minlength=f1 - f0)
+    assert torch.equal(c2, torch.clamp(indeg[n_id[f0:f1]], max=10))
+    # determinism: same seeds + seed -> identical batch
+    s = n_id[:B]
+    b1, b2 = ld.sample(s, seed=99), ld.sample(s, seed=99)
+    assert torch.equal(b1.edge_index, b2.edge_index) and torch.equal(b1.n_id, b2.n_id)
+    b3 = ld.sample(s, seed=100)
+    assert b3.n_id[:B].equal(s)
+
+
+def test_loader_epoch_covers_inputs(device):
+    from elliptic_gnn_project_amd.loader import NeighborLoader
+
+    data = _data(device)
+    idx = data.train_mask.nonzero().view(-1)
+    ld = NeighborLoader(data, num_neighbors=[5, 5], batch_size=97, input_nodes=data.train_mask, shuffle=True)
+    seen = torch.cat([b.n_id[:b.batch_size] for b in ld])
+    assert len(ld) == (idx.numel() + 96) // 97
+    assert torch.equal(torch.sort(seen).values, idx)
+
+
+def test_minibatch_epoch_and_batch_parity(device):
+    """A sampled batch is an ordinary graph: the SAGE logits on it match the oracle; an epoch of
+    train_epoch_minibatch + eval_val_minibatch runs and lowers the loss."""
+    from elliptic_gnn_project_amd.gnn import SAGENet
+    from elliptic_gnn_project_amd.loader import NeighborLoader
+    from elliptic_gnn_project_amd.train_gnn import (_make_loss_fn, class_weight, eval_val_minibatch,
+                                                    make_optimizer, train_epoch_minibatch)
+    from oracle import pyg_ref
+
+    data = _data(device)
+    torch.manual_seed(0)
+    model = SAGENet(data.x.size(1), 32, layers=2, dropout=0.0).to(device)
+    ld = NeighborLoader(data, num_neighbors=[10, 10], batch_size=256, input_nodes=data.train_mask, shuffle=True)
+    b = next(iter(ld))
+    params = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    model.eval()
+    with torch.no_grad():
+        got = model(b.x, b.edge_index).cpu()
+    ref = pyg_ref.model_forward("sage", params, b.x.cpu(), b.edge_index.cpu(), layers=2)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+    cfg = dict(lr=0.01, weight_decay=0.0, grad_clip=1.0)
+    cw = class_weight(data.y[data.train_mask].cpu())
+    loss_fn = _make_loss_fn(cfg, cw, model, 0, 49)
+    opt = make_optimizer(model, cfg, device, False)
+    scaler = torch.amp.GradScaler(device="cuda", enabled=False)
+    losses = [train_epoch_minibatch(model, ld, opt, loss_fn, scaler, False, cfg, device) for _ in range(4)]
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+    vl = NeighborLoader(data, num_neighbors=[10, 10], batch_size=300, input_nodes=data.val_mask)
+    y, p = eval_val_minibatch(model, vl, device)
+    assert len(y) == int(data.val_mask.sum()) and np.all((p >= 0) & (p <= 1))
+
+
+def test_main_minibatch(device, tmp_path):
+    import json
+
+    from elliptic_gnn_project_amd.train_gnn import main
+
+    cfg = dict(run_name="mb", output_root=str(tmp_path), arch="sage", hidden_dim=32, layers=2, dropout=0.2, lr=0.005,
+               weight_decay=1e-4, max_epochs=3, patience=10, grad_clip=1.0, amp=False, symmetrize_edges=True,
+               use_time_scalar=True, train_window_k=10, calibrate_temperature=True, topk=50,
+               mini_batch=True, fanout=[10, 10], batch_size=1024,
+               synthetic=dict(num_nodes=8000, num_edges=12000, seed=5))
+    m = main(cfg)
+    out = tmp_path / "gnn" / "mb"
+    assert (out / "metrics.json").exists() and (out / "best.ckpt").exists()
+    assert json.loads((out / "metrics.json").read_text())["best_val_pr_auc"] == m["best_val_pr_auc"]
+    assert len((out / "training_log.csv").read_text().strip().splitlines()) == 1 + 3
