@@ -174,14 +174,24 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   // the quad being staged instead of draining every prefetch in flight.
   const float* const tail1 = tail;
   const float* const tail2 = tail + WS_ROWS * k1;
-  auto load_quad = [&](int sb, int i, int t) {
-    const bool s2 = (qseg2 >> i) & 1u;
+  // the tile's two segment bases, formed once per tile (not per quad: per-quad forms compiled
+  // to a scalar branch pair per load inside the MFMA stream)
+  auto tile_base = [&](int t, const float*& b1, const float*& b2) {
     const int tc = (LAB & 8) ? blockIdx.x : min(t, ntiles - 1);  // LAB 8: re-read an L2-hot tile
     const bool last = tc == ntiles - 1;
-    const float* b1 = last ? tail1 : pa1 + (int64_t)tc * WS_ROWS * k1;
-    const float* b2 = last ? tail2 : pa2 + (int64_t)tc * WS_ROWS * k2;
+    b1 = last ? tail1 : pa1 + (int64_t)tc * WS_ROWS * k1;
+    b2 = last ? tail2 : pa2 + (int64_t)tc * WS_ROWS * k2;
+  };
+  auto load_quad_b = [&](int sb, int i, const float* b1, const float* b2) {
+    const bool s2 = (qseg2 >> i) & 1u;
+    // idle quads (qf = 0) re-load the tile's first quad and stage it into the never-read pad
+    // bytes; no zeroing (a select on the loaded value made hipcc wait for the load right there)
     st[sb][i] = *reinterpret_cast<const float4*>((s2 ? b2 : b1) + qf[i]);
-    if ((qidle >> i) & 1u) st[sb][i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto load_quad = [&](int sb, int i, int t) {
+    const float *b1, *b2;
+    tile_base(t, b1, b2);
+    load_quad_b(sb, i, b1, b2);
   };
   // stage one pair (half a quad: elements 2h, 2h+1) of quad i: split + 3 plane writes
   auto stage_pair = [&](char* buf, int sb, int i, int h) {
@@ -212,11 +222,20 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   }
   float* const cptr = a.c;
   const int64_t ldc = a.ldc;
-  // C stores as dwordx4 from the LDS tile when rows are 16-byte aligned (else one dword per lane)
-  const bool cvec = cptr && (ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(cptr) & 15) == 0);
+  // C and z leave through buffer stores: the descriptor's range check drops rows >= M (and a
+  // NULL C), so every tile issues the same store instructions on every path — with branches
+  // around them hipcc's vmcnt bookkeeping had to assume skipped stores and waited for A
+  // prefetches issued after the quad being staged.  (nt_ws_ok: C rows 16-byte aligned,
+  // Nc % 4 == 0, both buffers < 2 GB.)
+  const __amdgpu_buffer_rsrc_t crsrc =
+      __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? (int)(M * ldc * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t zrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(a.z, 0, (EPI & WS_PROJ) != 0 ? (int)(M * a.ldz * 4) : 0, 0x00020000);
 
   // MFMAs of this wave's K half from `cur`; the next tile's quads split into `nxt` in between
   auto kloop = [&](const char* cur, char* nxt, int sb, int tload) {
+    const float *lb1, *lb2;
+    tile_base(tload, lb1, lb2);
     floatx16 acc, acc2;
     constexpr int SQ0 = KH - QN > 0 ? KH - QN : 0;  // k-steps SQ0.. stage one quad each
     // one fragment set, each plane re-read for step s+1 right after its last use in step s:
@@ -256,7 +275,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       if (mm) ws_mfma<false>(acc, x[1], bw[s][0]);
       WS_FENCE;
       if (s + 1 < KH) x[1] = frag(sn, 1);
-      if (stg) load_quad(sb, qi, tload);
+      if (stg) load_quad_b(sb, qi, lb1, lb2);
       WS_FENCE;
       if (mm) {
         ws_mfma<false>(TWO ? acc2 : acc, x[0], bw[s][2]);
@@ -272,7 +291,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
 #pragma unroll
       for (int i = KH; i < QN; ++i) {
         stage_quad(nxt, sb, i);
-        load_quad(sb, i, tload);
+        load_quad_b(sb, i, lb1, lb2);
       }
     }
     if constexpr ((LAB & 4) != 0) {
@@ -313,11 +332,13 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   };
   // E1: this wave's rows of tile t -> bias, ReLU, dropout (element row·Nc + col, bit-identical to
   // keep_elem) -> the LDS C tile.
+  // bias of this lane's column, loaded once: a global load in the epilogue made hipcc wait
+  // vmcnt(0) there, i.e. for every A prefetch in flight, once per tile
+  float bv = 0.f;
+  if constexpr ((EPI & WS_BIAS) != 0) bv = colok ? a.bias[col] : 0.f;
   auto epi_tile = [&](const float (&v)[RV], int t) {
     const int64_t rbase = (int64_t)t * WS_ROWS + 4 * (lane >> 5);
     const uint32_t h0 = ((uint32_t)rbase * (uint32_t)Nc + (uint32_t)col) * kDropGolden + (uint32_t)seed;
-    float bv = 0.f;
-    if constexpr ((EPI & WS_BIAS) != 0) bv = colok ? a.bias[col] : 0.f;
 #pragma unroll
     for (int j = 0; j < RV; ++j) {
       const int r = half * RV + j;
@@ -334,25 +355,18 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   // are summed in a fixed order.
   auto epi_store = [&](int t) {
     const int64_t r0 = (int64_t)t * WS_ROWS;
-    if (cptr) {
+    {
       constexpr int NQ4 = WS_ROWS * BN / 4 / WS_THREADS;  // float4 chunks per thread
 #pragma unroll
       for (int i = 0; i < NQ4; ++i) {
         const int u = tid + WS_THREADS * i;
         const int rl = u / (BN / 4), c4 = (u % (BN / 4)) * 4;
-        const int64_t row = r0 + rl;
         const float4 x = *reinterpret_cast<const float4*>(ctile + rl * BN + c4);
-        if (row < M) {
-          if (cvec && c4 + 3 < Nc) {
-            *reinterpret_cast<float4*>(cptr + row * ldc + c4) = x;
-          } else {
-            float* d = cptr + row * ldc + c4;
-            if (c4 < Nc) d[0] = x.x;
-            if (c4 + 1 < Nc) d[1] = x.y;
-            if (c4 + 2 < Nc) d[2] = x.z;
-            if (c4 + 3 < Nc) d[3] = x.w;
-          }
-        }
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 xv = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
+        // columns >= Nc: an offset past the range (dropped); rows >= M fall past it by themselves
+        const uint32_t off = c4 < Nc ? (uint32_t)(((r0 + rl) * ldc + c4) * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(xv, crsrc, (int)off, 0, 0);
       }
     }
     if constexpr ((EPI & WS_PROJ) != 0) {
@@ -376,7 +390,8 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       zsum += __shfl_xor(zsum, 1);
       if constexpr (NP == 4) zsum += __shfl_xor(zsum, 2);
       const int64_t row = r0 + rl;
-      if (part == 0 && q < a.nproj && row < M) a.z[row * a.ldz + q] = zsum;
+      const uint32_t zoff = (part == 0 && q < a.nproj) ? (uint32_t)((row * a.ldz + q) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zsum), zrsrc, (int)zoff, 0, 0);
     }
   };
 
@@ -393,11 +408,12 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   for (int i = 0; i < QN; ++i) load_quad(0, i, t);
 #pragma unroll
   for (int i = 0; i < QN; ++i) stage_quad(A0, 0, i);
+  // the steady state's issue order (set 1 quads 0..QN-1, then set 0): the first trip's staging
+  // waits are then the loop's own (one vmcnt per quad, counted from the same order)
 #pragma unroll
-  for (int i = 0; i < QN; ++i) {
-    load_quad(1, i, t + G);       // tile t + G: staged during tile t
-    load_quad(0, i, t + 2 * G);   // tile t + 2G: staged during tile t + G
-  }
+  for (int i = 0; i < QN; ++i) load_quad(1, i, t + G);      // tile t + G: staged during tile t
+#pragma unroll
+  for (int i = 0; i < QN; ++i) load_quad(0, i, t + 2 * G);  // tile t + 2G: staged during tile t + G
   __syncthreads();
   float v[RV];
   auto finish = [&](const floatx16& acc) {
@@ -498,6 +514,9 @@ bool nt_ws_ok(const NTArgs& a) {
   if (a.a_bf16 || a.c_bf16 || !a.w1 || a.Nc > BN || a.Nc < 1) return false;
   auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (a.lda1 != a.k1 || (a.k1 & 1) || !al(a.a1)) return false;
+  // buffer-store epilogue: 16-byte C rows, whole float4 column chunks, 31-bit byte offsets
+  if (a.c && (!al(a.c) || a.ldc % 4 != 0 || a.M * a.ldc * 4 >= ((int64_t)1 << 31))) return false;
+  if (a.Nc % 4 != 0 || (a.nproj > 0 && a.M * a.ldz * 4 >= ((int64_t)1 << 31))) return false;
   if (a.k2 > 0 && (a.lda2 != a.k2 || (a.k2 & 1) || !al(a.a2))) return false;
   const int nks = (a.k1 + a.k2 + 15) / 16;
   if (nks != 8 && nks != 11 && nks != 16 && nks != 21) return false;
