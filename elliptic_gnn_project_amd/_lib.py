@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -93,6 +93,9 @@ class GnnAggParams(ctypes.Structure):
         ("relu", c_i32),
         ("part", c_ptr),
         ("part_bytes", c_size),
+        ("dropout_p", ctypes.c_float),
+        ("seed", ctypes.c_uint64),
+        ("seed_ptr", c_ptr),
     ]
 
 
@@ -113,6 +116,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("math", c_i32),
         ("workspace", c_ptr), ("workspace_bytes", c_size),
         ("a_dtype", c_i32), ("c_dtype", c_i32),
+        ("mask", c_ptr), ("ldmask", c_i64), ("mask_scale", ctypes.c_float),
     ]
 
 

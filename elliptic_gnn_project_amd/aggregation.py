@@ -87,9 +87,13 @@ def _ld(x: torch.Tensor) -> int:
 def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = False,
               nodew: torch.Tensor | None = None, ew: torch.Tensor | None = None, heads: int = 1,
               addend: torch.Tensor | None = None, bias: torch.Tensor | None = None,
-              relu: bool = False, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Raw call of gnn_aggregate_f32 (no autograd); bf16 rows go to gnn_aggregate_bf16 (bf16 out)."""
+              relu: bool = False, out: torch.Tensor | None = None, dropout_p: float = 0.0, seed: int = 0,
+              seed_ptr: torch.Tensor | None = None) -> torch.Tensor:
+    """Raw call of gnn_aggregate_f32 (no autograd); bf16 rows go to gnn_aggregate_bf16 (bf16 out).
+    ``dropout_p`` > 0: counter-hash dropout of element r·F + f after bias / ReLU (fp32 path)."""
     if x.dtype == torch.bfloat16:
+        if dropout_p > 0:
+            raise NotImplementedError("dropout epilogue on the bf16-storage aggregation")
         return _aggregate_bf16(plan, x, mode, transpose, nodew, addend, bias, relu, out)
     x = _as_f32_rows(x)
     N, F = plan.num_nodes, x.size(1)
@@ -107,6 +111,7 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
         mode, int(transpose), _lib.ptr(nodew), _lib.ptr(ew), int(heads),
         _lib.ptr(addend), _ld(addend) if addend is not None else 0,
         _lib.ptr(bias), int(relu), _lib.ptr(part), part.numel() * 4 if part is not None else 0,
+        float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ptr),
     )
     if KernelTimer.active:
         a = torch.cuda.Event(enable_timing=True)

@@ -13,7 +13,7 @@
 // agg_flat_kernel).  Slots are summed in plan order (PyG edge order) with one accumulator
 // per feature: no atomics, bitwise reproducible.  Rows with F <= 8 (2-class logits) use a
 // group of 8 lanes per row with lanes over slots instead.
-#include "common.hpp"
+#include "gemm_common.hpp"  // keep_elem: the counter-hash dropout shared with the NT epilogue
 
 namespace gnnmp {
 namespace {
@@ -102,7 +102,22 @@ struct AggArgs {
   const int32_t* fptr;
   const int32_t* fnbr;
   int32_t seg_len;
+  // dropout after bias / ReLU (element r·F + f, keep_elem of the NT epilogue)
+  int32_t dropout; uint32_t keep_thresh; float drop_scale; uint64_t seed; const int64_t* seed_ptr;
 };
+
+__device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
+  return a.seed_ptr ? (uint64_t)(*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+}
+
+template <int VEC>
+__device__ __forceinline__ void agg_dropout(const AggArgs& a, uint64_t seed, int64_t r, int f0, float (&t)[VEC]) {
+  if (a.dropout) {
+    const uint32_t i0 = (uint32_t)r * (uint32_t)a.F + (uint32_t)f0;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) t[q] = keep_elem(seed, i0 + (uint32_t)q, a.keep_thresh) ? t[q] * a.drop_scale : 0.0f;
+  }
+}
 
 // Per-slot scaled contribution.
 template <int MODE, int VEC>
@@ -145,6 +160,7 @@ __device__ __forceinline__ void finish(const AggArgs& a, int64_t r, int f0, floa
 #pragma unroll
     for (int q = 0; q < VEC; ++q) acc[q] = fmaxf(acc[q], 0.0f);
   }
+  if (a.dropout) agg_dropout<VEC>(a, agg_seed(a), r, f0, acc);
 }
 
 // Wide rows (F > 8): flat-slot walk.  A group of LPS lanes (LPS = the power of two that
@@ -178,6 +194,7 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
     for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
 
+  const uint64_t dseed = a.dropout ? agg_seed(a) : 0;
   auto flush = [&](int j) {
     const int64_t r = r0 + j;
     float d = 1.0f;
@@ -207,6 +224,7 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
           for (int q = 0; q < VEC; ++q) t[q] = fmaxf(t[q], 0.0f);
         }
+        if (a.dropout) agg_dropout<VEC>(a, dseed, r, f0, t);
         vstore<VEC>(a.y + r * a.ldy + f0, t);
       }
 #pragma unroll
@@ -278,6 +296,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
     for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
 
+  const uint64_t dseed = a.dropout ? agg_seed(a) : 0;
   auto flush = [&](int j) {
     const int64_t r = r0 + j;
     float d = 1.0f;
@@ -307,6 +326,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
           for (int q = 0; q < VEC; ++q) t[q] = fmaxf(t[q], 0.0f);
         }
+        if (a.dropout) agg_dropout<VEC>(a, dseed, r, f0, t);
         if constexpr (BF) vstore_bf<VEC>(reinterpret_cast<uint16_t*>(a.y) + r * a.ldy + f0, t);
         else vstore<VEC>(a.y + r * a.ldy + f0, t);
       }
@@ -495,6 +515,7 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
           if (a.add) t[0] += padd[f];
           if (a.bias) t[0] += pbias[f];
           if (a.relu) t[0] = fmaxf(t[0], 0.0f);
+          if (a.dropout) agg_dropout<1>(a, agg_seed(a), r, f, t);
           a.y[r * a.ldy + f] = t[0];
         }
       }
@@ -785,6 +806,12 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
   a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy;
   a.add = p->addend; a.ld_add = p->ld_add;
   a.bias = p->bias; a.relu = p->relu;
+  if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout p in [0,1)");
+  a.dropout = p->dropout_p > 0.f;
+  a.keep_thresh = (uint32_t)((1.0 - (double)p->dropout_p) * 16777216.0);
+  a.drop_scale = a.dropout ? (float)(1.0 / (1.0 - (double)p->dropout_p)) : 1.0f;
+  a.seed = p->seed;
+  a.seed_ptr = p->seed_ptr;
   a.nrows = g->num_nodes;
   a.F = (int32_t)F;
   if (!a.ptr || (g->num_slots > 0 && !a.nbr)) return fail(GNN_ERR_INVALID_ARG, __func__, "plan arrays null");
@@ -887,6 +914,12 @@ extern "C" gnn_status gnn_aggregate_bf16(const gnn_graph* g, const gnn_agg_param
   a.y = static_cast<float*>(y); a.ldy = ldy;
   a.add = p->addend; a.ld_add = p->ld_add;
   a.bias = p->bias; a.relu = p->relu;
+  if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout p in [0,1)");
+  a.dropout = p->dropout_p > 0.f;
+  a.keep_thresh = (uint32_t)((1.0 - (double)p->dropout_p) * 16777216.0);
+  a.drop_scale = a.dropout ? (float)(1.0 / (1.0 - (double)p->dropout_p)) : 1.0f;
+  a.seed = p->seed;
+  a.seed_ptr = p->seed_ptr;
   a.nrows = g->num_nodes;
   a.F = (int32_t)F;
   auto ok_vec = [&](int v) {

@@ -52,6 +52,7 @@ struct NTArgs {
   const float* proj; int32_t nproj; float* z; int64_t ldz;
   int32_t a_bf16;  // A1/A2 hold bf16 (the float pointers are reinterpreted; ld in elements)
   int32_t c_bf16;  // C is stored as bf16 (RNE), and the projection reads the rounded values
+  const float* mask; int64_t ldmask; float mask_scale;  // skinny kernels: C *= mask > 0 ? scale : 0
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }

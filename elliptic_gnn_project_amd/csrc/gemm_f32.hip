@@ -791,7 +791,10 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   hipStream_t st = (hipStream_t)stream;
   a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16;
   a.c_bf16 = p->c_dtype == GNN_DTYPE_BF16;
+  a.mask = p->mask; a.ldmask = p->ldmask; a.mask_scale = p->mask_scale;
+  if (p->mask && p->ldmask < p->N) return fail(GNN_ERR_INVALID_ARG, fn, "bad ldmask");
   if (variant == 0 && launch_nt_skinny(a, st)) return hip_check(hipGetLastError(), fn);  // Nc <= 8 or K <= 8
+  if (p->mask) return fail(GNN_ERR_UNSUPPORTED, fn, "the mask epilogue needs a skinny shape (K <= 8 or N <= 8)");
   if (a.a_bf16 || a.c_bf16) {
     if (!a.a_bf16 || !a.w1 || a.Nc > BN || p->math == GNN_MATH_F32)
       return fail(GNN_ERR_UNSUPPORTED, fn, "bf16 NT needs bf16 A, the w1/w2 form, N <= 128 and split math");

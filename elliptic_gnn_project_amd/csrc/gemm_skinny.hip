@@ -44,6 +44,7 @@ __device__ __forceinline__ float nt_epi(const NTArgs& a, float v, int64_t row, i
   if (a.relu) v = fmaxf(v, 0.0f);
   if (a.dropout)
     v = keep_elem(seed, (uint32_t)row * (uint32_t)a.Nc + (uint32_t)col, a.keep_thresh) ? v * a.drop_scale : 0.0f;
+  if (a.mask) v = a.mask[row * a.ldmask + col] > 0.0f ? v * a.mask_scale : 0.0f;
   return v;
 }
 

@@ -68,7 +68,7 @@ def _nt_workspace(device, n, k1, k2):
 
 
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
-            out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None):
+            out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None, mask=None, mask_scale=1.0):
     """C = epilogue([a1 | a2] · B) on the NT kernels; B = bt ([K, n] row-major) or, with bt None,
     [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2].
     bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too."""
@@ -93,6 +93,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.ptr(ws), ws.numel() * 4 if ws is not None else 0,
         _lib.DTYPE_BF16 if bf else _lib.DTYPE_F32,
         _lib.DTYPE_BF16 if (out is not None and out.dtype == torch.bfloat16) else _lib.DTYPE_F32,
+        _lib.ptr(mask), _ld(mask) if mask is not None else 0, float(mask_scale),
     )
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
@@ -251,6 +252,93 @@ class _FusedSAGE(torch.autograd.Function):
             # g: next (lower) layer's upstream gradient w.r.t. h_l, masked inside its TN
         dx = g.to(hs[0].dtype) if need_x else None
         return (dx, None, None, None, None, *grads)
+
+
+class _FusedGCN(torch.autograd.Function):
+    """GCNNet (src/models/gnn.py:14-32) as one autograd node, transform first (PyG's order):
+
+        y_l      = h_l · W_lᵀ                               K7 NT (w1 form, weight in place)
+        h_{l+1}  = dropout(relu(Â y_l + b_l))               K4 CSR, bias / ReLU / counter-hash
+                                                            dropout in the aggregation's store
+        logits   = Â (h_{L-1} · W_{L-1}ᵀ) + b_{L-1}         K7 skinny NT + K4 (bias)
+    Backward, layer by layer from the top (g = dL/d(Â y + b), g_top = dlogits):
+        dy = Âᵀ g (K4 CSC),  db = Σ_rows g,  dW = dyᵀ · h_l (K7 TN)
+        g_below = (dy · W_l) ⊙ [h_l > 0] / (1 − p)          skinny NT with the mask epilogue
+    (h_l > 0 exactly where ReLU passed and dropout kept).  Saved: the layer inputs h_l only;
+    no torch elementwise kernels on the path."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x, plan: GraphPlan, dropout_p: float, seeds: List[int], seed_ctr, *params):
+        L = len(params) // 2
+        W, b = params[0::2], params[1::2]
+        hs = [x.contiguous()]
+        dinv = plan.dinv
+        for l in range(L - 1):
+            y = gemm_nt(hs[-1], None, W[l].size(0), w1=W[l])
+            hs.append(aggregate(plan, y, _lib.AGG_GCN, nodew=dinv, bias=b[l], relu=True,
+                                dropout_p=dropout_p, seed=seeds[l], seed_ptr=seed_ctr))
+        y = gemm_nt(hs[-1], None, W[-1].size(0), w1=W[-1])
+        logits = aggregate(plan, y, _lib.AGG_GCN, nodew=dinv, bias=b[-1])
+        ctx.plan = plan
+        ctx.meta = (L, float(dropout_p))
+        ctx.save_for_backward(*hs, *params)
+        return logits
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dlogits):
+        from .aggregation import colsum
+
+        plan = ctx.plan
+        L, p = ctx.meta
+        saved = ctx.saved_tensors
+        hs, params = saved[:L], saved[L:]
+        W = params[0::2]
+        scale = 1.0 / (1.0 - p) if p > 0 else 1.0
+        dinv = plan.dinv
+        grads = [None] * (2 * L)
+        g = dlogits.contiguous()
+        dx = None
+        for l in range(L - 1, -1, -1):
+            dy = aggregate(plan, g, _lib.AGG_GCN, transpose=True, nodew=dinv)
+            grads[2 * l + 1] = colsum(g)
+            (dW, _), _, _, _ = gemm_tn(W[l].size(0), hs[l], g=dy)
+            grads[2 * l] = dW
+            fo, fi = W[l].shape
+            if l > 0:  # W [fo, fi] is the row-major [K, N] operand of dh = dy · W
+                if fo <= 8 or fi <= 8:
+                    g = gemm_nt(dy, W[l], fi, mask=hs[l], mask_scale=scale)
+                else:
+                    g = gemm_nt(dy, W[l], fi)
+                    g.mul_((hs[l] > 0).to(g.dtype) * scale)
+            elif ctx.needs_input_grad[0]:
+                dx = gemm_nt(dy, W[l], fi)
+        return (dx, None, None, None, None, *grads)
+
+
+def gcn_fusable(model) -> bool:
+    """GCNNet of GCNConv(bias) layers within the kernels' widths, not in explain mode."""
+    convs = list(model.convs)
+    if len(convs) < 2:
+        return False
+    for c in convs:
+        if getattr(c, "explain", False) or c.bias is None:
+            return False
+        if c.out_channels > 128 or c.in_channels > 384:
+            return False
+    return True
+
+
+def gcn_forward(model, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+    plan = get_plan(edge_index, x.size(0), _lib.LOOPS_REPLACE)
+    L = len(model.convs)
+    p = float(model.dropout) if model.training else 0.0
+    seeds, ctr = dropout_seeds(L, p, x)
+    params = []
+    for c in model.convs:
+        params += [c.lin.weight, c.bias]
+    return _FusedGCN.apply(x, plan, p, seeds, ctr, *params)
 
 
 def fusable(model) -> bool:

@@ -56,8 +56,19 @@ def _widths(in_dim: int, hidden_dim: int, layers: int, num_classes: int):
 
 
 class GCNNet(_StackedConvNet):
+    """On the GPU the whole network runs as one fused autograd node (fused.py _FusedGCN): bias,
+    ReLU and dropout in the aggregation's store, their backward in the skinny GEMM's epilogue
+    (counter-hash dropout, as SAGENet).  ``fused = False`` selects the per-conv path."""
+
+    fused = True
+
     def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2):
         super().__init__([GCNConv(a, b) for a, b in _widths(in_dim, hidden_dim, layers, num_classes)], dropout)
+
+    def forward(self, x: torch.Tensor, edge_index: torch.Tensor, t_idx: Optional[torch.Tensor] = None):
+        if self.fused and x.is_cuda and _fused.gcn_fusable(self):
+            return _fused.gcn_forward(self, x, edge_index)
+        return super().forward(x, edge_index, t_idx)
 
 
 class SAGENet(_StackedConvNet):

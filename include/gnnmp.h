@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 10
+#define GNNMP_ABI_VERSION 11
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -153,6 +153,11 @@ typedef struct {
   float* part;            /* partial sums for a split direction: >= num_pieces * F floats; NULL or
                              too small -> the direction is aggregated unsplit */
   size_t part_bytes;
+  float dropout_p;        /* > 0: F.dropout after bias / ReLU, element r*F + f kept by the counter
+                             hash of gnn_gemm_nt_params (oracle/dropout_hash.py), kept values
+                             scaled by 1/(1-p) — GCNNet's hidden layers (src/models/gnn.py:29-30) */
+  uint64_t seed;
+  const int64_t* seed_ptr; /* optional device counter: seed = *seed_ptr * 0x9E3779B97F4A7C15 + seed */
 } gnn_agg_params;
 
 /* Generic fp32 aggregation: y[r, 0:F] for r in [0, N). */
@@ -289,6 +294,11 @@ typedef struct {
   int32_t a_dtype;                       /* gnn_dtype of A1/A2 (BF16: w1/w2 form; B rounded to bf16,
                                             one bf16 product, f32 accumulate — the bf16-storage path) */
   int32_t c_dtype;                       /* gnn_dtype of C (BF16 needs a_dtype BF16); z stays f32 */
+  const float* mask;                     /* optional [M, N] (ldmask): C *= (mask > 0 ? mask_scale : 0)
+                                            after the other epilogue steps — the ReLU + dropout
+                                            backward of a saved activation (K <= 8 or N <= 8 shapes) */
+  int64_t ldmask;
+  float mask_scale;
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */

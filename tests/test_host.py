@@ -73,12 +73,13 @@ STRUCTS = {
     "gnn_graph": ("GnnGraph", ["num_nodes", "num_slots", "rowptr", "col", "colptr", "row", "csc2csr",
                                "csr_split", "csc_split"]),
     "gnn_agg_params": ("GnnAggParams", ["mode", "transpose", "nodew", "ew", "heads", "addend", "ld_add", "bias",
-                                        "relu", "part", "part_bytes"]),
+                                        "relu", "part", "part_bytes", "dropout_p", "seed", "seed_ptr"]),
     "gnn_gemm_nt_params": ("GnnGemmNTParams", ["M", "N", "a1", "lda1", "k1", "a2", "lda2", "k2", "bt", "ldb",
                                                "w1", "w2", "ldw1", "ldw2", "c",
                                                "ldc", "bias", "relu", "dropout_p", "seed", "seed_ptr", "proj",
                                                "nproj", "z", "ldz", "math", "workspace",
-                                               "workspace_bytes", "a_dtype", "c_dtype"]),
+                                               "workspace_bytes", "a_dtype", "c_dtype", "mask", "ldmask",
+                                               "mask_scale"]),
     "gnn_adam_tensor": ("GnnAdamTensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel"]),
     "gnn_adam_group": ("GnnAdamGroup", ["num_tensors", "lr", "beta1", "beta2", "eps", "weight_decay", "max_norm",
                                         "tensors"]),
