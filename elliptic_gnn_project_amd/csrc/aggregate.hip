@@ -652,6 +652,9 @@ void launch_split_v(const AggArgs& a, const gnn_split* sp, hipStream_t st) {
   else launch_split_passes<MODE, VEC, 4>(a, sp, st);
 }
 
+// Kernel-lab knob (gnnx_set_agg_variant, not part of the public ABI): 0 = production.
+int g_agg_lab_variant = 0;
+
 template <int MODE>
 gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp);
 
@@ -692,7 +695,13 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     else if (nchunk <= 16) lps = 16;
     else if (nchunk <= 32) lps = 32;
     if (nchunk > 64 * 4) return fail(GNN_ERR_UNSUPPORTED, "gnn_aggregate_f32", "F too wide for the gather kernel");
-    const int rpg = lps == 8 ? 7 : 8;
+    // rows per group: the group's lanes hold rpg + 1 row pointers, so rpg <= lps - 1.  16-lane
+    // groups (F = 64): 2 rows — the 4 groups of a wave walk their rows in lockstep more often and
+    // flush (divergently) fewer rows per pass: GCN preset F = 64, CSR fwd with bias / ReLU /
+    // dropout 97.5 -> 89.2 us, CSC bwd 49.4 -> 41.3 us (profiles/lab_agg.py, r08; 4 rows: 91.5 /
+    // 41.7, lps - 1 = 15 rows: 116.9 / 48.7).  Lab 5 / 6 / 8: 4 / 8 / lps - 1 rows.
+    const int lv = g_agg_lab_variant;
+    const int rpg = lv == 5 ? 4 : lv == 6 ? 8 : lv == 8 ? lps - 1 : (lps == 8 ? 7 : lps == 16 ? 2 : 8);
     const int64_t groups = ceil_div(a.nrows, rpg);
     const unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
 #define GNN_FLAT(V, L, NC) agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg)
@@ -704,7 +713,11 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     else GNN_FLAT(V, 8, 1);                \
   } while (0)
     if (lps == 64 && nchunk <= 128) {  // wave-uniform fast path (scalar row/neighbour handling)
-      const int rpw = 16;
+      // 16 rows per wave.  r08 lab (profiles/lab_agg.py, SAGE preset F = 166 CSR, 89.4 us = 63 %
+      // of HBM): 8 rows 89.2, 4 rows 95.7, 32 rows 99.1; U = 4 rows in flight 91.9; a 168-float
+      // padded pitch (dwordx4, one load per row) 89.0 — the gather is not instruction-bound.
+      // Lab 1 / 2 / 3: 8 / 4 / 32 rows.
+      const int rpw = lv == 1 ? 8 : lv == 2 ? 4 : lv == 3 ? 32 : 16;
       const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
       if (vec == 4) agg_wave_kernel<MODE, 4, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
       else if (vec == 2) agg_wave_kernel<MODE, 2, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
@@ -788,6 +801,9 @@ constexpr int64_t kColsumBlocks = 1024;
 
 using namespace gnnmp;
 
+// Tuning entry (not part of the public ABI): selects lab launch shapes of the wide gather.
+extern "C" void gnnx_set_agg_variant(int v) { g_agg_lab_variant = v; }
+
 extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params* p, const float* x,
                                         int64_t ldx, int64_t F, float* y, int64_t ldy,
                                         gnn_stream_t stream) {
@@ -850,7 +866,7 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
   // The split pays only for the lane-group gather (8..32 lanes per row, one row at a time per
   // group): r01 measurements — F=64 GCN fwd 72 -> 37 µs; the wave-wide gather (F/vec > 32) and
   // the narrow LDS/group kernels lose to the two extra launches.
-  if (sp && (F <= 8 || F / vec > 32)) sp = nullptr;
+  if (sp && (F <= 8 || F / vec > 32 || g_agg_lab_variant == 7)) sp = nullptr;  // lab 7: no split
   if (!sp) {
     a.ptr = p->transpose ? g->colptr : g->rowptr;
     a.nbr = p->transpose ? g->row : g->col;

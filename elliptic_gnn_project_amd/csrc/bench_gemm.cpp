@@ -239,16 +239,20 @@ int main(int argc, char** argv) {
                   (long long)Mc, std::sqrt(se / sr), mx, rmx, dbe);
     }
   }
-  const int tmaths[4] = {1, 0, 3, 4};
-  std::vector<float> tt[4];
+  std::vector<int> tmaths = {1, 0, 3, 4};  // 1 exact f32, 0 production, >= 2 lab variants
+  if (const char* q = std::getenv("LAB_TN_VARIANTS")) {
+    tmaths.clear();
+    for (const char* t = q; *t;) { tmaths.push_back(std::atoi(t)); while (*t && *t != ',') ++t; if (*t) ++t; }
+  }
+  std::vector<std::vector<float>> tt(tmaths.size());
   auto tn_run = [&](int math) {
     q.math = math >= 2 ? 0 : math;
     return T.run([&] { gnnx_gemm_tn_variant_f32(&q, out, ws, wsb, math >= 2 ? math : 0, nullptr); }, 5);
   };
   for (int m : tmaths) tn_run(m);  // warm-up
   for (int r = 0; r < rounds; ++r)
-    for (int i = 0; i < 4; ++i) tt[i].push_back(tn_run(tmaths[i]));
-  for (int i = 0; i < 4; ++i)
+    for (size_t i = 0; i < tmaths.size(); ++i) tt[i].push_back(tn_run(tmaths[i]));
+  for (size_t i = 0; i < tmaths.size(); ++i)
     std::printf("TN dz+mask math=%d: %8.1f us (%6.1f TF)\n", tmaths[i], med(tt[i]), flops / med(tt[i]) * 1e-6);
   return 0;
 }

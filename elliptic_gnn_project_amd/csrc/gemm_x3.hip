@@ -558,7 +558,7 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
     }
   };
 
-  if (nch > 0) {
+  auto prologue = [&]() {
     if constexpr (PROJ) {  // dz of chunk 0
       const int mb0 = ldbase(0);
       const bool ok0 = tid < TMC * MAXPROJ && zq < a.nproj && zr >= (int)mbeg - mb0 && zr < (int)mend - mb0;
@@ -566,6 +566,47 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) load(d, min(d, nch - 1));
+  };
+
+  // ---- this block's partial dW (segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2])
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
+  auto write_slab = [&]() {
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      if (t >= nkt) continue;
+      const int col = t * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int64_t idx = col < a.k1 ? (int64_t)row * a.k1 + col
+                                       : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (col - a.k1);
+        if (row < a.Nr && col < Kc) slab[idx] = acc[t][r];
+      }
+    }
+  };
+  // ---- side sums of the two row octets (G slots, threads < 256), combined in a fixed order via
+  //      LDS (At[0], free once every MFMA has read it: the caller's barrier)
+  float* red = reinterpret_cast<float*>(&At[0][0]);
+  constexpr int ns = 2 + MAXPROJ;
+  auto side_put = [&]() {
+    red[(go * 128 + gn) * ns + 0] = db;
+    red[(go * 128 + gn) * ns + 1] = dzs;
+#pragma unroll
+    for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
+  };
+  auto side_write = [&]() {
+    if (tid < 128 && tid < a.Nr) {
+      float* side = slab + (int64_t)a.Nr * Kc;
+      side[tid] = red[tid * ns] + red[(128 + tid) * ns];
+      for (int q = 0; q < a.nproj; ++q)
+        side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+    }
+    if (PROJ && tid < a.nproj)
+      slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+  };
+
+  if (nch > 0) {
+    prologue();
     __syncthreads();  // Ps, dzL[0]
     if constexpr (PIPE != 0) {
       // software-pipelined order: between two barriers, chunk c+1 is staged into the other
@@ -627,37 +668,11 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
     }
   }
 
-  // ---- this block's partial dW (segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2])
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    if (t >= nkt) continue;
-    const int col = t * 32 + (lane & 31);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int64_t idx = col < a.k1 ? (int64_t)row * a.k1 + col
-                                     : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (col - a.k1);
-      if (row < a.Nr && col < Kc) slab[idx] = acc[t][r];
-    }
-  }
-  // ---- side sums of the two row octets (G slots), combined in a fixed order via LDS
-  float* red = reinterpret_cast<float*>(&At[0][0]);
-  constexpr int ns = 2 + MAXPROJ;
+  write_slab();
   __syncthreads();
-  red[(go * 128 + gn) * ns + 0] = db;
-  red[(go * 128 + gn) * ns + 1] = dzs;
-#pragma unroll
-  for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
+  side_put();
   __syncthreads();
-  if (tid < 128 && tid < a.Nr) {
-    float* side = slab + (int64_t)a.Nr * Kc;
-    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
-    for (int q = 0; q < a.nproj; ++q)
-      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
-  }
-  if (PROJ && tid < a.nproj)
-    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+  side_write();
 }
 
 }  // namespace
@@ -772,6 +787,12 @@ void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
 // staging VALU cut from ~530 to ~325 per chunk (unmasked A, row offsets by adds, no per-row masks
 // in the dz form) the classic order runs 156 us and the pipelined order with interleave hints
 // 183 (before the cuts: 207 vs 196).  A 32-row-chunk variant measured 217-227 and was removed.
+// r08 (removed after measuring): a deeper load ring D = 2 / 3 in the classic order 166 / 159 us
+// vs 156; a wave-specialised form (512 threads: 4 producer waves stage chunk c + 1 while 4
+// consumer waves run chunk c's MFMAs, one barrier per chunk, 218-230 VGPRs, no spills) 150 / 148
+// (D = 1 / 2) vs 153 — no overlap materialised.  PMC of the production kernel per wave and
+// 16-row chunk (6,080 cycles): ~420 VALU (1,700 issue cycles: split ~265, load addressing ~95),
+// 66 MFMAs (2,112 cycles), waits at s_waitcnt / barrier ~1,560 — the VALU and MFMA phases add.
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
   constexpr int D = 1;
