@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -257,6 +257,30 @@ SIGNATURES = {
          c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
     "gnn_clip_adam_f32": (ctypes.c_int, [ctypes.POINTER(GnnAdamGroup), c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
+    "gnn_bn_workspace_size": (ctypes.c_int, [c_i64, ctypes.POINTER(c_size)]),
+    "gnn_bn_stats_f32": (
+        ctypes.c_int,
+        [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i32, ctypes.c_float, ctypes.c_float, c_ptr, c_ptr, c_ptr, c_ptr,
+         c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_bn_finalize_f32": (
+        ctypes.c_int, [c_ptr, c_i64, ctypes.c_float, ctypes.c_float, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr],
+    ),
+    "gnn_bn_act_res_fwd_f32": (
+        ctypes.c_int,
+        [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, ctypes.c_float, ctypes.c_uint64,
+         c_ptr, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_bn_act_bwd_reduce_f32": (
+        ctypes.c_int,
+        [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, ctypes.c_float, ctypes.c_uint64,
+         c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_bn_act_bwd_f32": (
+        ctypes.c_int,
+        [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, ctypes.c_float, ctypes.c_uint64,
+         c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
+    ),
 }
 
 _LIB: ctypes.CDLL | None = None

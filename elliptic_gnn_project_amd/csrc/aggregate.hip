@@ -104,7 +104,15 @@ struct AggArgs {
   int32_t seg_len;
   // dropout after bias / ReLU (element r·F + f, keep_elem of the NT epilogue)
   int32_t dropout; uint32_t keep_thresh; float drop_scale; uint64_t seed; const int64_t* seed_ptr;
+  // XCD-grouped block order (0: off): hardware block b runs on XCD b % 8; it takes logical
+  // block (b % 8)·xcdb + b / 8, so each XCD sweeps one contiguous eighth of the rows and its L2
+  // sees the neighbour rows of few timesteps at a time
+  int32_t xcdb;
 };
+
+__device__ __forceinline__ int64_t agg_block(const AggArgs& a) {
+  return a.xcdb ? (int64_t)(blockIdx.x & 7) * a.xcdb + (blockIdx.x >> 3) : (int64_t)blockIdx.x;
+}
 
 __device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
   return a.seed_ptr ? (uint64_t)(*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
@@ -176,7 +184,7 @@ template <int MODE, int VEC, int LPS, int NCHMAX>
 __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
   const int gl = threadIdx.x & (LPS - 1);
   const int gbase = (threadIdx.x & 63) & ~(LPS - 1);
-  const int64_t group = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPS;
+  const int64_t group = (agg_block(a) * 256 + threadIdx.x) / LPS;
   const int64_t r0 = group * rpg;
   if (r0 >= a.nrows) return;  // group-uniform
   const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 template <int MODE, int VEC, int NCH, bool BF = false, int U = 8>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t wave = (agg_block(a) * 256 + threadIdx.x) >> 6;
   const int64_t r0 = wave * rpg;
   if (r0 >= a.nrows) return;
   const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
@@ -703,8 +711,13 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     const int lv = g_agg_lab_variant;
     const int rpg = lv == 5 ? 4 : lv == 6 ? 8 : lv == 8 ? lps - 1 : (lps == 8 ? 7 : lps == 16 ? 2 : 8);
     const int64_t groups = ceil_div(a.nrows, rpg);
-    const unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
-#define GNN_FLAT(V, L, NC) agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg)
+    unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
+    AggArgs ax = a;  // lab 9: XCD-grouped block order
+    if (lv == 9) {
+      ax.xcdb = (int32_t)ceil_div(blocks, 8);
+      blocks = (unsigned)ax.xcdb * 8;
+    }
+#define GNN_FLAT(V, L, NC) agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(ax, rpg)
 #define GNN_FLAT_V(V)                      \
   do {                                     \
     if (lps == 64) GNN_FLAT(V, 64, 4);     \
@@ -718,10 +731,15 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
       // padded pitch (dwordx4, one load per row) 89.0 — the gather is not instruction-bound.
       // Lab 1 / 2 / 3: 8 / 4 / 32 rows.
       const int rpw = lv == 1 ? 8 : lv == 2 ? 4 : lv == 3 ? 32 : 16;
-      const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
-      if (vec == 4) agg_wave_kernel<MODE, 4, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
-      else if (vec == 2) agg_wave_kernel<MODE, 2, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
-      else agg_wave_kernel<MODE, 1, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
+      unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
+      AggArgs aw = a;
+      if (lv == 9) {
+        aw.xcdb = (int32_t)ceil_div(wblocks, 8);
+        wblocks = (unsigned)aw.xcdb * 8;
+      }
+      if (vec == 4) agg_wave_kernel<MODE, 4, 2, false, 8><<<wblocks, 256, 0, st>>>(aw, rpw);
+      else if (vec == 2) agg_wave_kernel<MODE, 2, 2, false, 8><<<wblocks, 256, 0, st>>>(aw, rpw);
+      else agg_wave_kernel<MODE, 1, 2, false, 8><<<wblocks, 256, 0, st>>>(aw, rpw);
     } else if (vec == 4) GNN_FLAT_V(4);
     else if (vec == 2) GNN_FLAT_V(2);
     else GNN_FLAT_V(1);

@@ -793,6 +793,11 @@ void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
 // (D = 1 / 2) vs 153 — no overlap materialised.  PMC of the production kernel per wave and
 // 16-row chunk (6,080 cycles): ~420 VALU (1,700 issue cycles: split ~265, load addressing ~95),
 // 66 MFMAs (2,112 cycles), waits at s_waitcnt / barrier ~1,560 — the VALU and MFMA phases add.
+// Further r09 forms, all correct vs float64 and all removed: a fenced interleave (chunk k+1 staged
+// in ~20 units placed between chunk k's MFMAs by sched_barrier fences, 2-deep ring, loads issued
+// right after each slot is consumed) 150-155 us; its ablations: no MFMAs 103, L2-hot loads 153
+// (not HBM-bound); two waves per SIMD (512 threads, half the k-tiles per wave, 2 A slots + a
+// 4-row G slot per thread) 164.  Every form lands at ~6,000 cycles per chunk per SIMD.
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
   constexpr int D = 1;

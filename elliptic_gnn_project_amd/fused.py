@@ -400,3 +400,92 @@ def sage_forward(model, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tens
     for c in model.convs:
         params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]
     return _FusedSAGE.apply(x, plan, p, seeds, ctr, *params)
+
+
+# --------------------------------------------------------------------------- SAGEResBNNet layer tail
+@functools.lru_cache(maxsize=64)
+def _bn_ws_bytes(C: int) -> int:
+    nb = _lib.c_size(0)
+    _lib.call("gnn_bn_workspace_size", C, nb)
+    return int(nb.value)
+
+
+def _bn_group(bn):
+    """torch.distributed when ``bn`` is a SyncBatchNorm1d of an initialised process group, else None."""
+    d = getattr(bn, "dist", None)
+    return d if (d is not None and d.is_initialized()) else None
+
+
+class _BNActRes(torch.autograd.Function):
+    """h = dropout(relu(BatchNorm1d(z))) + r, training mode (src/models/gnn.py:182-194), on K12
+    (csrc/bn.hip): batch statistics in float64 with the nn.BatchNorm1d running-stat update
+    (SyncBN: one all-reduce of [Σz | Σz² | n] forward, one of [Σdy | Σdy·x̂] backward), the
+    counter-hash dropout of the fused SAGE path, and the whole backward in two passes over z."""
+
+    @staticmethod
+    def forward(ctx, z, r, weight, bias, bn, p: float, seed: int, seed_ctr, group):
+        z = z.contiguous()
+        N, C = z.shape
+        dev = z.device
+        st = _lib.stream_handle(dev)
+        stats = torch.empty(2 * C + 1, dtype=torch.float64, device=dev)
+        mean = torch.empty(C, dtype=torch.float32, device=dev)
+        invstd = torch.empty(C, dtype=torch.float32, device=dev)
+        ws = torch.empty(max(_bn_ws_bytes(C) // 4, 1), dtype=torch.float32, device=dev)
+        track = bn.track_running_stats and bn.running_mean is not None
+        rm = _lib.ptr(bn.running_mean) if track else None
+        rv = _lib.ptr(bn.running_var) if track else None
+        nbt = _lib.ptr(bn.num_batches_tracked) if track else None
+        mom = -1.0 if bn.momentum is None else float(bn.momentum)
+        eps = float(bn.eps)
+        _lib.call("gnn_bn_stats_f32", z.data_ptr(), C, N, C, stats.data_ptr(), int(group is None), eps, mom,
+                  mean.data_ptr(), invstd.data_ptr(), rm, rv, nbt, ws.data_ptr(), ws.numel() * 4, st)
+        if group is not None:
+            group.all_reduce(stats)
+            _lib.call("gnn_bn_finalize_f32", stats.data_ptr(), C, eps, mom, mean.data_ptr(), invstd.data_ptr(),
+                      rm, rv, nbt, st)
+        h = torch.empty_like(z)
+        if r is not None:
+            r = r.contiguous()
+        _lib.call("gnn_bn_act_res_fwd_f32", z.data_ptr(), C, _lib.ptr(r), C, N, C, mean.data_ptr(),
+                  invstd.data_ptr(), weight.data_ptr(), bias.data_ptr(), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                  _lib.ptr(seed_ctr), h.data_ptr(), C, st)
+        ctx.save_for_backward(z, mean, invstd, weight, bias, stats)
+        ctx.meta = (float(p), int(seed), seed_ctr, group, r is not None)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        z, mean, invstd, weight, bias, stats = ctx.saved_tensors
+        p, seed, seed_ctr, group, has_r = ctx.meta
+        dh = dh.contiguous()
+        N, C = z.shape
+        dev = z.device
+        st = _lib.stream_handle(dev)
+        sums = torch.empty(2 * C, dtype=torch.float32, device=dev)
+        ws = torch.empty(max(_bn_ws_bytes(C) // 4, 1), dtype=torch.float32, device=dev)
+        args = (mean.data_ptr(), invstd.data_ptr(), weight.data_ptr(), bias.data_ptr(), p,
+                seed & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ctr))
+        _lib.call("gnn_bn_act_bwd_reduce_f32", dh.data_ptr(), C, z.data_ptr(), C, N, C, *args, sums.data_ptr(),
+                  ws.data_ptr(), ws.numel() * 4, st)
+        local = sums
+        if group is not None:  # parameter grads are LOCAL sums (the gradient all-reduce adds the rest)
+            local = sums.clone()
+            group.all_reduce(sums)
+        dz = torch.empty_like(z)
+        _lib.call("gnn_bn_act_bwd_f32", dh.data_ptr(), C, z.data_ptr(), C, N, C, *args, sums.data_ptr(),
+                  stats[2 * C:].data_ptr(), dz.data_ptr(), C, st)
+        return dz, (dh if has_r else None), local[C:], local[:C], None, None, None, None, None
+
+
+def bn_fusable(bn) -> bool:
+    """nn.BatchNorm1d (or SyncBatchNorm1d) with affine parameters, float32, in training mode."""
+    return (isinstance(bn, torch.nn.BatchNorm1d) and bn.training and bn.affine and bn.weight is not None
+            and bn.weight.dtype == torch.float32 and bn.weight.is_cuda)
+
+
+def bn_relu_dropout_residual(z: torch.Tensor, r, bn, p: float, seed: int, seed_ctr) -> torch.Tensor:
+    """dropout(relu(bn(z)), p) + r on K12 (training-mode BatchNorm1d / SyncBatchNorm1d)."""
+    if z.dtype != torch.float32:
+        z = z.float()
+    return _BNActRes.apply(z, r, bn.weight, bn.bias, bn, float(p), seed, seed_ctr, _bn_group(bn))

@@ -118,6 +118,11 @@ class SAGEResBNNet(nn.Module):
 
     time_embed_type: 'learned' (nn.Embedding(max_timestep, dim)), 'sin' (fixed sin/cos of
     2π·k·(t-1)/(T-1), k = 1..dim/2, zero-padded to dim), anything else / dim 0: none.
+
+    On the GPU in training mode each hidden layer's ``dropout(relu(bn(z))) + res_proj(h)`` runs
+    on K12 (fused.bn_relu_dropout_residual: float64 batch statistics, the BatchNorm1d running-stat
+    update, SyncBN when the BN is a SyncBatchNorm1d, counter-hash dropout as SAGENet); eval mode
+    and CPU keep nn.BatchNorm1d / F.relu / F.dropout.  ``fused_bn = False`` selects that path.
     """
 
     def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2, use_bn=True,
@@ -172,11 +177,19 @@ class SAGEResBNNet(nn.Module):
             return x
         return torch.cat([x, te], dim=1)
 
+    fused_bn = True  # training-mode BN + ReLU + dropout + residual on K12 (fused.bn_relu_dropout_residual)
+
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor, t_idx: Optional[torch.Tensor] = None):
         h = self._inject_time(x, t_idx)
         *hidden, last = self.convs
+        fuse = self.fused_bn and self.use_bn and self.training and x.is_cuda
+        seeds, ctr = (_fused.dropout_seeds(len(self.convs), self.dropout, h) if fuse else (None, None))
         for li, conv in enumerate(hidden):
             z = conv(h, edge_index)
+            if fuse and _fused.bn_fusable(self.bns[li]):
+                h = _fused.bn_relu_dropout_residual(z, self.res_projs[li](h), self.bns[li], self.dropout,
+                                                    seeds[li], ctr)
+                continue
             if self.use_bn:
                 z = self.bns[li](z)
             z = F.dropout(F.relu(z), p=self.dropout, training=self.training)

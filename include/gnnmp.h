@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 11
+#define GNNMP_ABI_VERSION 12
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -334,6 +334,48 @@ gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* worksp
 gnn_status gnn_colsum_workspace_size(int64_t rows, int64_t F, size_t* bytes);
 gnn_status gnn_colsum_f32(int64_t rows, int64_t F, const float* x, int64_t ldx, float* out,
                           void* workspace, size_t workspace_bytes, gnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* K12 SAGEResBNNet layer tail, training mode (src/models/gnn.py:182-194):   */
+/*     h = dropout(relu(BatchNorm1d(z))) + r,   r = res_proj(h_prev)          */
+/* Replaces nn.BatchNorm1d.forward (batch statistics + running-stat update),  */
+/* F.relu, F.dropout and the residual add, and their backward passes.         */
+/* ------------------------------------------------------------------------ */
+/* Workspace of gnn_bn_stats_f32 / gnn_bn_act_bwd_reduce_f32 for C channels. */
+gnn_status gnn_bn_workspace_size(int64_t C, size_t* bytes);
+/* Batch statistics of z [N, C]: stats (device float64 [2C + 1]) = [Σz | Σz² | N] — summable
+ * across ranks (SyncBN: all-reduce them, then gnn_bn_finalize_f32).  finalize != 0 also does
+ * gnn_bn_finalize_f32 in the same launch sequence (single device). */
+gnn_status gnn_bn_stats_f32(const float* z, int64_t ldz, int64_t N, int64_t C, double* stats, int32_t finalize,
+                            float eps, float momentum, float* mean, float* invstd, float* running_mean,
+                            float* running_var, int64_t* num_batches_tracked, void* workspace,
+                            size_t workspace_bytes, gnn_stream_t stream);
+/* mean = Σz/n, var = Σz²/n − mean² (biased, float64), invstd = 1/sqrt(var + eps); when
+ * running_mean != NULL the nn.BatchNorm1d update: running = (1−m)·running + m·stat with the
+ * unbiased variance, m = momentum (momentum < 0: PyTorch's momentum=None cumulative average
+ * 1/(num_batches_tracked+1)), and num_batches_tracked += 1 (optional pointer). */
+gnn_status gnn_bn_finalize_f32(const double* stats, int64_t C, float eps, float momentum, float* mean,
+                               float* invstd, float* running_mean, float* running_var,
+                               int64_t* num_batches_tracked, gnn_stream_t stream);
+/* h = dropout(relu((z − mean)·invstd·weight + bias)) + r   (r optional; counter-hash dropout of
+ * element r·C + c as gnn_agg_params; N·C < 2^32). */
+gnn_status gnn_bn_act_res_fwd_f32(const float* z, int64_t ldz, const float* r, int64_t ldr, int64_t N, int64_t C,
+                                  const float* mean, const float* invstd, const float* weight, const float* bias,
+                                  float dropout_p, uint64_t seed, const int64_t* seed_ptr, float* h, int64_t ldh,
+                                  gnn_stream_t stream);
+/* Backward, step 1: sums (device float [2C]) = [Σ dy | Σ dy·x̂] over the N rows, with
+ * dy = dh ⊙ dropout-mask/(1−p) ⊙ [y > 0] recomputed from z (the BN weight / bias gradients are
+ * these local sums; SyncBN all-reduces a copy before step 2). */
+gnn_status gnn_bn_act_bwd_reduce_f32(const float* dh, int64_t lddh, const float* z, int64_t ldz, int64_t N,
+                                     int64_t C, const float* mean, const float* invstd, const float* weight,
+                                     const float* bias, float dropout_p, uint64_t seed, const int64_t* seed_ptr,
+                                     float* sums, void* workspace, size_t workspace_bytes, gnn_stream_t stream);
+/* Backward, step 2: dz = weight·invstd·(dy − Σdy/n − x̂·Σdy·x̂/n) with the (global) sums and the
+ * device row count *n_total (stats[2C] of the forward; torch.batch_norm_backward_elemt). */
+gnn_status gnn_bn_act_bwd_f32(const float* dh, int64_t lddh, const float* z, int64_t ldz, int64_t N, int64_t C,
+                              const float* mean, const float* invstd, const float* weight, const float* bias,
+                              float dropout_p, uint64_t seed, const int64_t* seed_ptr, const float* sums,
+                              const double* n_total, float* dz, int64_t lddz, gnn_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Step ops around the hot path (src/train_gnn.py:136-183, 201-206)          */

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--variants", default="0,1,2,3,4")
     ap.add_argument("--cases", default="sage,gcn")
+    ap.add_argument("--cold", action="store_true",
+                    help="evict L2 / Infinity Cache (write 1 GB) before every timed call, time calls one at a time")
     args = ap.parse_args()
     variants = [int(v) for v in args.variants.split(",")]
     lib = _lib.load()
@@ -55,6 +57,7 @@ def main():
                   dict(mode=_lib.AGG_GCN, nodew=pg.dinv, bias=b, relu=True, dropout_p=0.5, seed=7)))
     cases.append(("gcn bwd F=64 (csc)", pg, y, dict(mode=_lib.AGG_GCN, transpose=True, nodew=pg.dinv)))
     cases = [c for c in cases if c[0].split()[0] in want]
+    flush = torch.zeros(256 * 1024 * 1024, device=dev) if args.cold else None  # 1 GB
     for name, plan, inp, kw in cases:
         ref = None
         times = {v: [] for v in variants}
@@ -62,14 +65,17 @@ def main():
         for r in range(args.rounds + 1):
             for v in variants:
                 setv(v)
+                reps = 1 if args.cold else 5
+                if args.cold:
+                    flush.add_(1.0)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(5):
+                for _ in range(reps):
                     o = aggregate(plan, inp, **kw)
                 e1.record()
                 torch.cuda.synchronize()
                 if r > 0:
-                    times[v].append(e0.elapsed_time(e1) * 1000 / 5)
+                    times[v].append(e0.elapsed_time(e1) * 1000 / reps)
                 outs[v] = o
         setv(0)
         ref = outs[variants[0]]
