@@ -104,15 +104,7 @@ struct AggArgs {
   int32_t seg_len;
   // dropout after bias / ReLU (element r·F + f, keep_elem of the NT epilogue)
   int32_t dropout; uint32_t keep_thresh; float drop_scale; uint64_t seed; const int64_t* seed_ptr;
-  // XCD-grouped block order (0: off): hardware block b runs on XCD b % 8; it takes logical
-  // block (b % 8)·xcdb + b / 8, so each XCD sweeps one contiguous eighth of the rows and its L2
-  // sees the neighbour rows of few timesteps at a time
-  int32_t xcdb;
 };
-
-__device__ __forceinline__ int64_t agg_block(const AggArgs& a) {
-  return a.xcdb ? (int64_t)(blockIdx.x & 7) * a.xcdb + (blockIdx.x >> 3) : (int64_t)blockIdx.x;
-}
 
 __device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
   return a.seed_ptr ? (uint64_t)(*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
@@ -184,7 +176,7 @@ template <int MODE, int VEC, int LPS, int NCHMAX>
 __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
   const int gl = threadIdx.x & (LPS - 1);
   const int gbase = (threadIdx.x & 63) & ~(LPS - 1);
-  const int64_t group = (agg_block(a) * 256 + threadIdx.x) / LPS;
+  const int64_t group = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPS;
   const int64_t r0 = group * rpg;
   if (r0 >= a.nrows) return;  // group-uniform
   const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
@@ -283,7 +275,7 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 template <int MODE, int VEC, int NCH, bool BF = false, int U = 8>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (agg_block(a) * 256 + threadIdx.x) >> 6;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t r0 = wave * rpg;
   if (r0 >= a.nrows) return;
   const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
@@ -386,8 +378,10 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 
 // Narrow rows (F <= 8, e.g. 2-class logits): a group of 8 lanes per row, lanes over the
 // row's slots (hubs are shared by 8 lanes), then a 3-step xor-shuffle reduction.
+// NF: compile-time bound on F (2, 4 or 8): every row value is loaded unconditionally (clamped
+// index), so a slot's loads issue together instead of one per feature behind its own branch.
 constexpr int kGroup = 8;
-template <int MODE>
+template <int MODE, int NF>
 __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
   const int sub = threadIdx.x & (kGroup - 1);
   for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kGroup; r < a.nrows;
@@ -397,35 +391,59 @@ __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
     float acc[8];
 #pragma unroll
     for (int f = 0; f < 8; ++f) acc[f] = 0.0f;
+    const float wr = MODE == GNN_AGG_GCN ? a.nodew[r] : 1.0f;  // the row's weight, once
     for (int32_t k = beg + sub; k < end; k += kGroup) {
       const int32_t n = a.nbr[k];
       const float* xr = a.x + (int64_t)n * a.ldx;
+      float xv[NF];
 #pragma unroll
-      for (int f = 0; f < 8; ++f) {
-        if (f < a.F) {
-          float v[1] = {xr[f]};
-          contrib<MODE, 1>(a, n, (int32_t)r, k, f, v);
-          acc[f] += v[0];
+      for (int f = 0; f < NF; ++f) xv[f] = xr[f < a.F ? f : 0];
+      // the slot's weight loaded beside its row values (contrib's arithmetic, same rounding)
+      const float wn = (MODE == GNN_AGG_GCN || MODE == GNN_AGG_MEAN_BWD) ? a.nodew[n] : 1.0f;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        float v = xv[f];
+        if constexpr (MODE == GNN_AGG_GCN) {
+          v = (wn * wr) * v;
+        } else if constexpr (MODE == GNN_AGG_MEAN_BWD) {
+          v = v / fmaxf(wn, 1.0f);
+        } else {
+          float t[1] = {v};
+          contrib<MODE, 1>(a, n, (int32_t)r, k, f, t);
+          v = t[0];
         }
+        acc[f] += f < a.F ? v : 0.0f;
       }
     }
 #pragma unroll
-    for (int f = 0; f < 8; ++f) {
-      if (f < a.F) {
+    for (int f = 0; f < NF; ++f) {
 #pragma unroll
-        for (int off = kGroup / 2; off >= 1; off >>= 1) acc[f] += __shfl_xor(acc[f], off);
-      }
+      for (int off = kGroup / 2; off >= 1; off >>= 1) acc[f] += __shfl_xor(acc[f], off);
     }
     if (sub == 0) {
+      // epilogue operands loaded together (clamped indices) — finish<MODE, 1>'s arithmetic
       const int32_t p0 = a.piece0 ? a.piece0[r] : -1;
+      const float dr = MODE == GNN_AGG_MEAN ? fmaxf(a.nodew[r], 1.0f) : 1.0f;
+      float addv[NF], bv[NF];
 #pragma unroll
-      for (int f = 0; f < 8; ++f) {
+      for (int f = 0; f < NF; ++f) {
+        const int fc = f < a.F ? f : 0;
+        addv[f] = a.add ? a.add[r * a.ld_add + fc] : 0.0f;
+        bv[f] = a.bias ? a.bias[fc] : 0.0f;
+      }
+      const uint64_t dseed = a.dropout ? agg_seed(a) : 0;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
         if (f < a.F) {
           float t[1] = {acc[f]};
           if (p0 >= 0) {
             a.part[(int64_t)p0 * a.F + f] = t[0];
           } else {
-            finish<MODE, 1>(a, r, f, t);
+            if constexpr (MODE == GNN_AGG_MEAN) t[0] = t[0] / dr;
+            if (a.add) t[0] += addv[f];
+            if (a.bias) t[0] += bv[f];
+            if (a.relu) t[0] = fmaxf(t[0], 0.0f);
+            if (a.dropout) agg_dropout<1>(a, dseed, r, f, t);
             a.y[r * a.ldy + f] = t[0];
           }
         }
@@ -438,8 +456,11 @@ __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
 // (one per lane).  Their slots are staged through LDS with lanes over SLOTS — neighbour ids
 // and the F-wide neighbour rows of 64 slots per instruction, all in flight together — and then
 // each lane adds its own row's slots from LDS in edge order (sequential, deterministic).
-constexpr int kNarrowCap = 256;  // slots staged per pass per wave
-template <int MODE>
+// NF (2 or 4): compile-time bound on F.  The staging is branch-free: all neighbour ids of the
+// pass, then all their row values (clamped feature index) and weights, then the LDS writes — a
+// per-feature `f < F` branch had compiled to one dependent load + vmcnt(0) per value (r10: 16 us
+// warm, 21 us cold for ~11 MB).
+template <int MODE, int NF, int kNarrowCap = 256>  // kNarrowCap: slots staged per pass per wave
 __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   __shared__ float sv[4][kNarrowCap * 4];
   const int lane = threadIdx.x & 63;
@@ -472,18 +493,28 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   float* buf = sv[w];
   for (int32_t pb = base; pb < wend; pb += kNarrowCap) {
     const int32_t pe = min(pb + kNarrowCap, wend);
+    constexpr int NI = kNarrowCap / 64;
+    int32_t nn[NI];
 #pragma unroll
-    for (int i = 0; i < kNarrowCap / 64; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int32_t k = pb + lane + 64 * i;
-      const int32_t kc = k < pe ? k : pb;
-      const int32_t n = a.nbr[kc];
-      const float* xr = a.x + (int64_t)n * a.ldx;
-      float d = 1.0f;
-      if constexpr (MODE == GNN_AGG_MEAN_BWD) d = fmaxf(a.nodew[n], 1.0f);
+      nn[i] = a.nbr[k < pe ? k : pb];
+    }
+    float xv[NI][NF], dd[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const float* xr = a.x + (int64_t)nn[i] * a.ldx;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) xv[i][f] = xr[f < F ? f : 0];
+      dd[i] = 1.0f;
+      if constexpr (MODE == GNN_AGG_MEAN_BWD) dd[i] = a.nodew[nn[i]];
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
-        float v = f < F ? xr[f] : 0.0f;
-        if constexpr (MODE == GNN_AGG_MEAN_BWD) v = v / d;
+        float v = (f < NF && f < F) ? xv[i][f < NF ? f : 0] : 0.0f;
+        if constexpr (MODE == GNN_AGG_MEAN_BWD) v = v / fmaxf(dd[i], 1.0f);
         buf[f * kNarrowCap + lane + 64 * i] = v;
       }
     }
@@ -691,11 +722,15 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
   if (a.nrows == 0 || a.F == 0) return GNN_OK;
   if (sp) return launch_mode_split<MODE>(a, vec, st, sp);
   if (a.F <= 4 && (MODE == GNN_AGG_MEAN || MODE == GNN_AGG_MEAN_BWD || MODE == GNN_AGG_SUM)) {
-    agg_narrow_lds_kernel<MODE><<<(unsigned)ceil_div(a.nrows, 256), 256, 0, st>>>(a);
+    // slots staged per pass: 512 / 128 measured 15.3 / 17.2 us vs 16.1 at 256 (r10, warm)
+    if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2><<<(unsigned)ceil_div(a.nrows, 256), 256, 0, st>>>(a);
+    else agg_narrow_lds_kernel<MODE, 4><<<(unsigned)ceil_div(a.nrows, 256), 256, 0, st>>>(a);
   } else if (a.F <= 8) {
     int64_t blocks = ceil_div(a.nrows * kGroup, 256);
     if (blocks > ((int64_t)1 << 20)) blocks = (int64_t)1 << 20;
-    agg_group_kernel<MODE><<<(unsigned)blocks, 256, 0, st>>>(a);
+    if (a.F <= 2) agg_group_kernel<MODE, 2><<<(unsigned)blocks, 256, 0, st>>>(a);
+    else if (a.F <= 4) agg_group_kernel<MODE, 4><<<(unsigned)blocks, 256, 0, st>>>(a);
+    else agg_group_kernel<MODE, 8><<<(unsigned)blocks, 256, 0, st>>>(a);
   } else {
     const int nchunk = a.F / vec;
     int lps = 64;
@@ -711,13 +746,8 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     const int lv = g_agg_lab_variant;
     const int rpg = lv == 5 ? 4 : lv == 6 ? 8 : lv == 8 ? lps - 1 : (lps == 8 ? 7 : lps == 16 ? 2 : 8);
     const int64_t groups = ceil_div(a.nrows, rpg);
-    unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
-    AggArgs ax = a;  // lab 9: XCD-grouped block order
-    if (lv == 9) {
-      ax.xcdb = (int32_t)ceil_div(blocks, 8);
-      blocks = (unsigned)ax.xcdb * 8;
-    }
-#define GNN_FLAT(V, L, NC) agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(ax, rpg)
+    const unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
+#define GNN_FLAT(V, L, NC) agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg)
 #define GNN_FLAT_V(V)                      \
   do {                                     \
     if (lps == 64) GNN_FLAT(V, 64, 4);     \
@@ -729,17 +759,13 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
       // 16 rows per wave.  r08 lab (profiles/lab_agg.py, SAGE preset F = 166 CSR, 89.4 us = 63 %
       // of HBM): 8 rows 89.2, 4 rows 95.7, 32 rows 99.1; U = 4 rows in flight 91.9; a 168-float
       // padded pitch (dwordx4, one load per row) 89.0 — the gather is not instruction-bound.
-      // Lab 1 / 2 / 3: 8 / 4 / 32 rows.
+      // XCD-grouped block order (each XCD sweeping one contiguous eighth of the rows) measured
+      // slower with cold caches (r10: 130.4 -> 138.5 us).  Lab 1 / 2 / 3: 8 / 4 / 32 rows.
       const int rpw = lv == 1 ? 8 : lv == 2 ? 4 : lv == 3 ? 32 : 16;
-      unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
-      AggArgs aw = a;
-      if (lv == 9) {
-        aw.xcdb = (int32_t)ceil_div(wblocks, 8);
-        wblocks = (unsigned)aw.xcdb * 8;
-      }
-      if (vec == 4) agg_wave_kernel<MODE, 4, 2, false, 8><<<wblocks, 256, 0, st>>>(aw, rpw);
-      else if (vec == 2) agg_wave_kernel<MODE, 2, 2, false, 8><<<wblocks, 256, 0, st>>>(aw, rpw);
-      else agg_wave_kernel<MODE, 1, 2, false, 8><<<wblocks, 256, 0, st>>>(aw, rpw);
+      const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
+      if (vec == 4) agg_wave_kernel<MODE, 4, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
+      else if (vec == 2) agg_wave_kernel<MODE, 2, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
+      else agg_wave_kernel<MODE, 1, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
     } else if (vec == 4) GNN_FLAT_V(4);
     else if (vec == 2) GNN_FLAT_V(2);
     else GNN_FLAT_V(1);

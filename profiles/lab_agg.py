@@ -49,6 +49,11 @@ def main():
     cases.append(("sage mean fwd F=166", ps, x, dict(mode=_lib.AGG_MEAN, nodew=ps.deg)))
     cases.append(("sage mean fwd F=168 (padded pitch)", ps, xp, dict(mode=_lib.AGG_MEAN, nodew=ps.deg)))
     cases.append(("sage mean bwd F=166", ps, x, dict(mode=_lib.AGG_MEAN_BWD, transpose=True, nodew=ps.deg)))
+    z4 = torch.randn((x.size(0), 4), device=dev)
+    cases.append(("narrow mean fwd F=2 (+root, bias)", ps, z4[:, :2],
+                  dict(mode=_lib.AGG_MEAN, nodew=ps.deg, addend=z4[:, 2:], bias=torch.randn(2, device=dev))))
+    cases.append(("narrow mean bwd F=2 (csc)", ps, torch.randn((x.size(0), 2), device=dev),
+                  dict(mode=_lib.AGG_MEAN_BWD, transpose=True, nodew=ps.deg)))
     gcn = prepare_inputs(synthetic_elliptic(seed=42), dict(use_time_scalar=True, symmetrize_edges=False))
     pg = get_plan(gcn.edge_index.to(dev), gcn.x.size(0), _lib.LOOPS_REPLACE)
     y = torch.randn((gcn.x.size(0), 64), device=dev)
@@ -56,6 +61,8 @@ def main():
     cases.append(("gcn fwd F=64 (+bias relu dropout)", pg, y,
                   dict(mode=_lib.AGG_GCN, nodew=pg.dinv, bias=b, relu=True, dropout_p=0.5, seed=7)))
     cases.append(("gcn bwd F=64 (csc)", pg, y, dict(mode=_lib.AGG_GCN, transpose=True, nodew=pg.dinv)))
+    y2 = torch.randn((gcn.x.size(0), 2), device=dev)
+    cases.append(("narrow gcn fwd F=2 (+bias)", pg, y2, dict(mode=_lib.AGG_GCN, nodew=pg.dinv, bias=b[:2])))
     cases = [c for c in cases if c[0].split()[0] in want]
     flush = torch.zeros(256 * 1024 * 1024, device=dev) if args.cold else None  # 1 GB
     for name, plan, inp, kw in cases:
