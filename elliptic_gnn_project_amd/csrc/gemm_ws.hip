@@ -75,6 +75,10 @@ constexpr int WS_BIAS = 1, WS_RELU = 2, WS_DROP = 4, WS_PROJ = 8;
 //         k-steps; the pair's partial sums meet through LDS.
 // LAB (timing ablations only, bench_gemm variants 10-14): bit 1 no A loads / staging, bit 2 no
 // epilogue, bit 4 no MFMAs, bit 8 every tile's A re-read from the block's first tile (L2-hot).
+// r10 (layer-1 shape, fused epilogue / plain store, us): production 145 / 117, no staging 120 / 91,
+// no epilogue 110, neither 78.5 (the bare MFMA loop at 53 % of its 42 us floor: one wave per SIMD
+// exposes the fragment reads and the two barriers per tile), no MFMAs 89 / 83, L2-hot A 140 / 109
+// (HBM costs ~6 us).  So: MFMA loop 78 + staging ~27 + fused epilogue ~30 (projection, dropout).
 template <int NKS, int EPI, int KS, int LAB = 0>
 __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const uint4* __restrict__ bimg, int ntiles,
                                                              const float* __restrict__ tail) {

@@ -390,8 +390,10 @@ constexpr int TX_AS = 3;           // A unit slots per thread (u = tid + 256·s 
 // from LDS instead of 32 registers of replicated dz rows per thread.
 // NPL = 3: f32 operands split (6 products).  NPL = 1: the bf16-storage path — A (ABF) and h
 // (HBF) are read as bf16, G is rounded to bf16, one product per MFMA.
+// HALFN (Nr <= 64): waves 0-1 / 2-3 take the two 32-row halves of the output for the first /
+// second half of the k-tiles (KT per wave), instead of waves 2-3 running MFMAs on all-zero rows.
 template <bool PROJ, bool MASK, int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0,
-          bool GOUT = true>
+          bool GOUT = true, bool HALFN = false>
 __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   constexpr int NS = TX_AS + ((!PROJ && MASK) ? 2 : 1);  // + G slot (+ g slot)
   constexpr int GS = TX_AS;                              // the G slot index
@@ -402,7 +404,8 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int ntile = wave;
+  const int ntile = HALFN ? (wave & 1) : wave;
+  const int t0 = HALFN ? (wave >> 1) * KT : 0;  // first k-tile of this wave
   const int Kc = a.k1 + a.k2;
   const int nkt = (Kc + 31) / 32;
   const int KP = nkt * 32;
@@ -547,12 +550,12 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 #pragma unroll
     for (int p = 0; p < NPL; ++p) gf[p] = lds_frag(Gt[buf] + p * TGPL + ntile * 32 * TP + fr);
 #pragma unroll
-    for (int p = 0; p < NPL; ++p) af[0][p] = lds_frag(At[buf] + p * TAPL + fr);
+    for (int p = 0; p < NPL; ++p) af[0][p] = lds_frag(At[buf] + p * TAPL + t0 * 32 * TP + fr);
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       if (t + 1 < KT) {
 #pragma unroll
-        for (int p = 0; p < NPL; ++p) af[(t + 1) & 1][p] = lds_frag(At[buf] + p * TAPL + (t + 1) * 32 * TP + fr);
+        for (int p = 0; p < NPL; ++p) af[(t + 1) & 1][p] = lds_frag(At[buf] + p * TAPL + (t0 + t + 1) * 32 * TP + fr);
       }
       acc[t] = mfma_planes<NPL>(gf, af[t & 1], acc[t]);
     }
@@ -573,8 +576,8 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   auto write_slab = [&]() {
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      if (t >= nkt) continue;
-      const int col = t * 32 + (lane & 31);
+      if (t0 + t >= nkt) continue;
+      const int col = (t0 + t) * 32 + (lane & 31);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -766,20 +769,21 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
   }
 }
 
-template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0, bool GO = false>
+template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0, bool GO = false,
+          bool HN = false>
 void launch_tn_x3_kg(const TNArgs& a, int nblk, hipStream_t st) {
   const bool proj = a.dz != nullptr, mask = a.h != nullptr;
-  if (proj && mask) gemm_tn_x3_kernel<true, true, D, KT, NPL, ABF, HBF, PIPE, GO><<<nblk, TX_THREADS, 0, st>>>(a);
-  else if (proj) gemm_tn_x3_kernel<true, false, D, KT, NPL, ABF, HBF, PIPE, GO><<<nblk, TX_THREADS, 0, st>>>(a);
-  else if (mask) gemm_tn_x3_kernel<false, true, D, KT, NPL, ABF, HBF, PIPE, GO><<<nblk, TX_THREADS, 0, st>>>(a);
-  else gemm_tn_x3_kernel<false, false, D, KT, NPL, ABF, HBF, PIPE, GO><<<nblk, TX_THREADS, 0, st>>>(a);
+  if (proj && mask) gemm_tn_x3_kernel<true, true, D, KT, NPL, ABF, HBF, PIPE, GO, HN><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (proj) gemm_tn_x3_kernel<true, false, D, KT, NPL, ABF, HBF, PIPE, GO, HN><<<nblk, TX_THREADS, 0, st>>>(a);
+  else if (mask) gemm_tn_x3_kernel<false, true, D, KT, NPL, ABF, HBF, PIPE, GO, HN><<<nblk, TX_THREADS, 0, st>>>(a);
+  else gemm_tn_x3_kernel<false, false, D, KT, NPL, ABF, HBF, PIPE, GO, HN><<<nblk, TX_THREADS, 0, st>>>(a);
 }
 
 // the G write-out (gout, needed only when a further layer's dh follows) is a compile-time branch
-template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0>
+template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0, bool HN = false>
 void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
-  if (a.gout) launch_tn_x3_kg<D, KT, NPL, ABF, HBF, PIPE, true>(a, nblk, st);
-  else launch_tn_x3_kg<D, KT, NPL, ABF, HBF, PIPE, false>(a, nblk, st);
+  if (a.gout) launch_tn_x3_kg<D, KT, NPL, ABF, HBF, PIPE, true, HN>(a, nblk, st);
+  else launch_tn_x3_kg<D, KT, NPL, ABF, HBF, PIPE, false, HN>(a, nblk, st);
 }
 
 
@@ -821,7 +825,16 @@ void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
     }
     return;
   }
-  // production: classic order (stage c; barrier; MFMAs of c)
+  // production: classic order (stage c; barrier; MFMAs of c).  Nr <= 64 (GCN / GAT / SAGE-ResBN
+  // hidden width 64): the half-N mapping, ceil(nkt / 2) k-tiles per wave
+  if (a.Nr <= 64 && variant != 8) {
+    const int kh = (nkt + 1) / 2;
+    if (kh <= 2) launch_tn_x3_k<D, 2, 3, false, false, 0, true>(a, nblk, st);
+    else if (kh <= 3) launch_tn_x3_k<D, 3, 3, false, false, 0, true>(a, nblk, st);
+    else if (kh <= 4) launch_tn_x3_k<D, 4, 3, false, false, 0, true>(a, nblk, st);
+    else launch_tn_x3_k<D, 6, 3, false, false, 0, true>(a, nblk, st);
+    return;
+  }
   if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 0>(a, nblk, st);
   else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 0>(a, nblk, st);
   else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 0>(a, nblk, st);
