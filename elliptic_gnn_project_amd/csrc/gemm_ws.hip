@@ -458,10 +458,10 @@ int ws_num_cus() {
 }
 
 // The last (partial) row tile, zero-padded to 32 rows: [32][k1] then [32][k2] f32.
-__global__ __launch_bounds__(256) void ws_tail_kernel(NTArgs a, float* __restrict__ tail, int64_t r0) {
+__device__ __forceinline__ void ws_tail_block(const NTArgs& a, float* __restrict__ tail, int64_t r0, int blk) {
   const int n1 = WS_ROWS * a.k1, n = n1 + WS_ROWS * a.k2;
   {
-    const int i = blockIdx.x * 256 + threadIdx.x;  // one element per thread
+    const int i = blk * 256 + threadIdx.x;  // one element per thread
     if (i >= n) return;
     const bool s2 = i >= n1;
     const int kg = s2 ? a.k2 : a.k1;
@@ -474,8 +474,8 @@ __global__ __launch_bounds__(256) void ws_tail_kernel(NTArgs a, float* __restric
 
 // B image over the CONCATENATED K (k < k1: W1, else W2 at k - k1): per 16-deep chunk c,
 // [plane hi/mid/lo][2n + khalf] uint4 (8 bf16), zero for n >= Nc and k >= k1 + k2.
-__global__ __launch_bounds__(256) void ws_presplit_b_kernel(NTArgs a, uint4* __restrict__ img, int nchunks) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;  // (chunk, n, khalf)
+__device__ __forceinline__ void ws_presplit_block(const NTArgs& a, uint4* __restrict__ img, int nchunks, int blk) {
+  const int idx = blk * 256 + threadIdx.x;  // (chunk, n, khalf)
   if (idx >= nchunks * 256) return;
   const int c = idx >> 8, n = (idx & 255) >> 1, kh = idx & 1;
   float e[8];
@@ -492,6 +492,13 @@ __global__ __launch_bounds__(256) void ws_presplit_b_kernel(NTArgs a, uint4* __r
   for (int j = 0; j < 4; ++j) ws_split(e[2 * j], e[2 * j + 1], w[j][0], w[j][1], w[j][2]);
 #pragma unroll
   for (int p = 0; p < 3; ++p) img[((int64_t)c * 3 + p) * 256 + (idx & 255)] = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+}
+
+// One launch for both per-call preparations (blocks [0, nchunks): B image; the rest: tail tile).
+__global__ __launch_bounds__(256) void ws_prep_kernel(NTArgs a, uint4* __restrict__ img, int nchunks,
+                                                      float* __restrict__ tail, int64_t r0) {
+  if ((int)blockIdx.x < nchunks) ws_presplit_block(a, img, nchunks, blockIdx.x);
+  else ws_tail_block(a, tail, r0, blockIdx.x - nchunks);
 }
 
 template <int NKS, int KS, int LAB = 0>
@@ -542,8 +549,7 @@ size_t nt_ws_tail_offset(int64_t k1, int64_t k2) {  // the B image (<= 24 chunks
 void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks) {
   const int nks = (a.k1 + a.k2 + 15) / 16;
   float* tail = reinterpret_cast<float*>(reinterpret_cast<char*>(img) + nt_ws_tail_offset(a.k1, a.k2));
-  ws_presplit_b_kernel<<<nks, 256, 0, st>>>(a, img, nks);
-  ws_tail_kernel<<<(unsigned)ceil_div(WS_ROWS * (a.k1 + a.k2), 256), 256, 0, st>>>(a, tail,
+  ws_prep_kernel<<<(unsigned)(nks + ceil_div(WS_ROWS * (a.k1 + a.k2), 256)), 256, 0, st>>>(a, img, nks, tail,
                                                                               (ceil_div(a.M, WS_ROWS) - 1) * WS_ROWS);
 #define GNN_WSL(N, K, L) launch_ws_k<N, K, L>(a, img, tail, st)
   if (ks < 0) {  // lab ablations of the production NKS = 21 instance (KS 1)

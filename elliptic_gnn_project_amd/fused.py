@@ -210,11 +210,17 @@ class _FusedSAGE(torch.autograd.Function):
         params = saved[2 * L - 1:]
         Wl, Wr = params[0::3], params[2::3]
         hscale = 1.0 / (1.0 - p) if p > 0 else 1.0
-        dlogits = dlogits.contiguous()
         N = dlogits.size(0)
-        dz = torch.empty((N, 2 * C), dtype=torch.float32, device=dlogits.device)
-        aggregate(plan, dlogits, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dz[:, :C])
-        dz[:, C:].copy_(dlogits)
+        buf = getattr(dlogits, "_gnnmp_dz", None)  # the fused CE's [N, 2C] buffer, dlogits its right half
+        if (buf is not None and buf.shape == (N, 2 * C) and dlogits.stride() == (2 * C, 1)
+                and dlogits.data_ptr() == buf.data_ptr() + C * buf.element_size()):
+            dz = buf
+            aggregate(plan, dlogits, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dz[:, :C])
+        else:
+            dlogits = dlogits.contiguous()
+            dz = torch.empty((N, 2 * C), dtype=torch.float32, device=dlogits.device)
+            aggregate(plan, dlogits, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dz[:, :C])
+            dz[:, C:].copy_(dlogits)
         P = ctx.P
         grads = [None] * (3 * L)
         need_x = ctx.needs_input_grad[0]

@@ -195,7 +195,12 @@ def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cf
         else:
             loss = loss_fn(_rows(logits, data, "train"), _rows(data.y, data, "train"), t_idx,
                            denom=denom if bucket is not None else None)
-    scaler.scale(loss).backward()
+    if scaler.is_enabled() or not loss.is_cuda:
+        scaler.scale(loss).backward()
+    else:  # = loss.backward(): a persistent unit gradient (no fill kernel; the fused CE skips `* g`)
+        from .train_ops import unit_gradient
+
+        loss.backward(unit_gradient(loss.device))
     if bucket is not None:
         bucket.allreduce_(dist)
     if cfg.get("grad_clip", 0) and cfg["grad_clip"] > 0 and not _clips_itself(optimizer):

@@ -29,23 +29,46 @@ def _ce_ws_bytes(N: int) -> int:
     return int(nb.value)
 
 
+_ONES = {}
+
+
+def unit_gradient(device) -> torch.Tensor:
+    """A persistent scalar 1.0 for ``loss.backward(unit_gradient(dev))``: no per-step fill kernel for
+    the implicit gradient, and the fused CE below returns its dlogits without the ``* g`` pass."""
+    t = _ONES.get(device)
+    if t is None:
+        t = torch.ones((), dtype=torch.float32, device=device)
+        _ONES[device] = t
+    return t
+
+
 class _MaskedCE(torch.autograd.Function):
+    """dlogits is written into the right half of an [N, 2C] buffer (``dl._gnnmp_dz``): the fused
+    SAGE backward needs dz = [meanᵀ(dlogits) | dlogits] and fills only the left half (no copy)."""
+
     @staticmethod
     def forward(ctx, logits, y, mask_u8, class_w, inv_denom: float):
         logits = logits.contiguous()
         N, C = logits.shape
-        dl = torch.empty_like(logits)
+        buf = torch.empty((N, 2 * C), dtype=logits.dtype, device=logits.device)
+        dl = buf[:, C:]
         loss = torch.empty((), dtype=torch.float32, device=logits.device)
         ws = _ws(_ce_ws_bytes(N), logits.device)
         _lib.call("gnn_masked_ce_f32", N, C, logits.data_ptr(), C, y.data_ptr(), mask_u8.data_ptr(),
-                  class_w.data_ptr(), float(inv_denom), dl.data_ptr(), C, loss.data_ptr(), ws.data_ptr(),
+                  class_w.data_ptr(), float(inv_denom), dl.data_ptr(), 2 * C, loss.data_ptr(), ws.data_ptr(),
                   ws.numel() * 4, _lib.stream_handle(logits.device))
-        ctx.save_for_backward(dl)
+        ctx.save_for_backward(buf)
+        ctx.C = C
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        (dl,) = ctx.saved_tensors
+        (buf,) = ctx.saved_tensors
+        dl = buf[:, ctx.C:]
+        ones = _ONES.get(g.device)
+        if ones is not None and g.data_ptr() == ones.data_ptr():  # d(loss)/d(loss) = 1: dl as is
+            dl._gnnmp_dz = buf
+            return dl, None, None, None, None
         return dl * g, None, None, None, None
 
 

@@ -89,3 +89,38 @@ def test_clip_adam_graph_replay(device):
     assert float(ob.param_groups[0]["step_t"]) == 4.0
     for p, q in zip(pa, pb):
         assert torch.equal(p, q)
+
+
+def test_unit_gradient_paths_match_plain_backward(device):
+    """loss.backward(unit_gradient) (no fill, no `* g`, dz buffer shared with the fused SAGE
+    backward) gives bitwise the gradients of loss.backward(); a leaf logits tensor gets dlogits."""
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.gnn import SAGENet
+    from elliptic_gnn_project_amd.train_ops import masked_cross_entropy, unit_gradient
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=3000, num_edges=4000, seed=5),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+    x, ei = data.x.to(device), data.edge_index.to(device)
+    y, mask = data.y.to(device), data.train_mask.to(device)
+    w = torch.tensor([0.6, 3.0], device=device)
+    grads = []
+    for unit in (False, True):
+        torch.manual_seed(1)
+        model = SAGENet(x.size(1), 64, layers=2, dropout=0.0).to(device)
+        loss = masked_cross_entropy(model(x, ei), y, mask, w, denom=float(mask.sum()))
+        if unit:
+            loss.backward(unit_gradient(device))
+        else:
+            loss.backward()
+        grads.append([p.grad.clone() for p in model.parameters()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+    logits = torch.randn(500, 2, device=device, requires_grad=True)
+    yy = torch.randint(0, 2, (500,), device=device)
+    mm = torch.rand(500, device=device) < 0.5
+    l1 = masked_cross_entropy(logits, yy, mm, w, denom=float(mm.sum()))
+    l1.backward(unit_gradient(device))
+    g1 = logits.grad.clone()
+    logits.grad = None
+    masked_cross_entropy(logits, yy, mm, w, denom=float(mm.sum())).backward()
+    assert torch.equal(g1, logits.grad)
