@@ -124,6 +124,8 @@ template <int MODE, int VEC>
 __device__ __forceinline__ void contrib(const AggArgs& a, int32_t n, int32_t r, int64_t slot,
                                         int f0, float (&v)[VEC]) {
   if constexpr (MODE == GNN_AGG_MEAN_BWD) {
+    // PyG's grad / count per element (correctly rounded division).  r11 lab: one reciprocal per
+    // slot (v · (1/d), <= 1 ulp off) would save 11 of 105 us on the SAGE-graph F = 64 CSC pass.
     float d = fmaxf(a.nodew[n], 1.0f);
 #pragma unroll
     for (int q = 0; q < VEC; ++q) v[q] = v[q] / d;

@@ -49,6 +49,9 @@ def main():
     cases.append(("sage mean fwd F=166", ps, x, dict(mode=_lib.AGG_MEAN, nodew=ps.deg)))
     cases.append(("sage mean fwd F=168 (padded pitch)", ps, xp, dict(mode=_lib.AGG_MEAN, nodew=ps.deg)))
     cases.append(("sage mean bwd F=166", ps, x, dict(mode=_lib.AGG_MEAN_BWD, transpose=True, nodew=ps.deg)))
+    h64 = torch.randn((x.size(0), 64), device=dev)
+    cases.append(("sage64 mean fwd F=64", ps, h64, dict(mode=_lib.AGG_MEAN, nodew=ps.deg)))
+    cases.append(("sage64 mean bwd F=64 (csc)", ps, h64, dict(mode=_lib.AGG_MEAN_BWD, transpose=True, nodew=ps.deg)))
     z4 = torch.randn((x.size(0), 4), device=dev)
     cases.append(("narrow mean fwd F=2 (+root, bias)", ps, z4[:, :2],
                   dict(mode=_lib.AGG_MEAN, nodew=ps.deg, addend=z4[:, 2:], bias=torch.randn(2, device=dev))))
