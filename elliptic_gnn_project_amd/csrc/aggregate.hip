@@ -172,7 +172,8 @@ __device__ __forceinline__ void finish(const AggArgs& a, int64_t r, int f0, floa
 // the group's lanes (no global load on the flush path); a row is flushed (mean divide,
 // root addend, bias, ReLU, store) when the walk passes its end, empty rows included.  Slots
 // are added in plan order: each output is the sequential edge-order sum PyG computes.
-constexpr int kU = 4;
+
+constexpr int kU = 4;  // slots in flight per group (r11 lab: 8 measured 12-25 % slower on every F = 64 case)
 
 template <int MODE, int VEC, int LPS, int NCHMAX>
 __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
