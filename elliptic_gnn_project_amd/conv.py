@@ -55,10 +55,18 @@ class _MeanAggRootBias(torch.autograd.Function):
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dout):
         plan, fo = ctx.plan, ctx.fo
-        dout = dout.contiguous()
+        N = dout.size(0)
         dy = None
-        if ctx.needs_input_grad[0]:
-            dy = torch.empty((dout.size(0), 2 * fo), dtype=torch.float32, device=dout.device)
+        # dout may already be the right half of an [N, 2·fo] buffer (the fused CE's dlogits, K12's
+        # dz): then only the left half is written here, no copy
+        buf = getattr(dout, "_gnnmp_dz", None)
+        if (ctx.needs_input_grad[0] and buf is not None and buf.shape == (N, 2 * fo)
+                and dout.stride() == (2 * fo, 1) and dout.data_ptr() == buf.data_ptr() + fo * buf.element_size()):
+            dy = buf
+            aggregate(plan, dout, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dy[:, :fo])
+        elif ctx.needs_input_grad[0]:
+            dout = dout.contiguous()
+            dy = torch.empty((N, 2 * fo), dtype=torch.float32, device=dout.device)
             aggregate(plan, dout, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dy[:, :fo])
             dy[:, fo:].copy_(dout)
         db = colsum(dout) if ctx.has_bias and ctx.needs_input_grad[1] else None

@@ -478,9 +478,13 @@ class _BNActRes(torch.autograd.Function):
         if group is not None:  # parameter grads are LOCAL sums (the gradient all-reduce adds the rest)
             local = sums.clone()
             group.all_reduce(sums)
-        dz = torch.empty_like(z)
+        # dz is written as the right half of an [N, 2C] buffer (tagged): a transform-first SAGEConv
+        # below assembles its GEMM gradient [meanᵀ(dz) | dz] in that buffer without a copy
+        zbuf = torch.empty((N, 2 * C), dtype=torch.float32, device=dev)
+        dz = zbuf[:, C:]
         _lib.call("gnn_bn_act_bwd_f32", dh.data_ptr(), C, z.data_ptr(), C, N, C, *args, sums.data_ptr(),
-                  stats[2 * C:].data_ptr(), dz.data_ptr(), C, st)
+                  stats[2 * C:].data_ptr(), dz.data_ptr(), 2 * C, st)
+        dz._gnnmp_dz = zbuf
         return dz, (dh if has_r else None), local[C:], local[:C], None, None, None, None, None
 
 
