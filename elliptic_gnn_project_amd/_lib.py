@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -280,6 +280,10 @@ SIGNATURES = {
         ctypes.c_int,
         [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, ctypes.c_float, ctypes.c_uint64,
          c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
+    ),
+    "gnn_time_inject_sin_f32": (
+        ctypes.c_int,
+        [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
     ),
 }
 

@@ -73,6 +73,48 @@ class _MeanAggRootBias(torch.autograd.Function):
         return dy, db, None, None
 
 
+class _SAGEAggregateFirst(torch.autograd.Function):
+    """out = [mean_{j->i} x_j | x_i] · [W_l | W_r]ᵀ + b (PyG's order) with a one-pass backward for
+    the input: [dG_l | dG_r] = dout · [W_l | W_r] as ONE split-bf16 NT GEMM (dout read once), then
+    dx = meanᵀ(dG_l) + dG_r with dG_r added in the transposed aggregation's epilogue — instead of
+    two NT GEMMs and an add kernel.  dW_l, dW_r, db from one TN over [agg | x] as linear2."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x, wl, wr, bias, plan: GraphPlan):
+        from .fused import gemm_nt
+        from .linear import _rows
+        x = _rows(x)
+        agg = aggregate(plan, x, _lib.AGG_MEAN, nodew=plan.deg)
+        wl = wl.contiguous()
+        wr = wr.contiguous()
+        y = gemm_nt(agg, None, wl.size(0), a2=x, bias=bias, w1=wl, w2=wr)
+        ctx.save_for_backward(agg, x, wl, wr)
+        ctx.plan = plan
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        from .fused import gemm_nt, gemm_tn
+        from .linear import _rows
+        agg, x, wl, wr = ctx.saved_tensors
+        plan = ctx.plan
+        dy = _rows(dy)
+        need = ctx.needs_input_grad
+        dWl = dWr = db = dx = None
+        if need[1] or need[2] or need[3]:
+            (dWl, dWr), db, _, _ = gemm_tn(wl.size(0), agg, x, g=dy)
+        if need[0]:
+            fi = wl.size(1)
+            wt = torch.cat([wl, wr], dim=1).t().contiguous()  # [2·F_in, F_out]: Linear-weight form
+            d = gemm_nt(dy, None, 2 * fi, w1=wt)
+            dx = aggregate(plan, d[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, addend=d[:, fi:])
+        return (dx, dWl if need[1] else None, dWr if need[2] else None,
+                db if (ctx.has_bias and need[3]) else None, None)
+
+
 class SAGEConv(nn.Module):
     """GraphSAGE ``out_i = W_l · mean_{j->i} x_j + b_l + W_r · x_i`` (PyG SAGEConv, aggr='mean').
 
@@ -121,6 +163,10 @@ class SAGEConv(nn.Module):
             y = linear(x, w)  # [N, 2*F_out]: MFMA GEMM (K7)
             plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
             return _MeanAggRootBias.apply(y, self.lin_l.bias, plan, fo)
+        if (x.is_cuda and x.dim() == 2 and x.size(0) > 0 and x.dtype != torch.bfloat16
+                and 2 * self.in_channels <= 128 and self.out_channels <= 128):
+            plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
+            return _SAGEAggregateFirst.apply(x, self.lin_l.weight, self.lin_r.weight, self.lin_l.bias, plan)
         agg = mean_aggregate(x, edge_index)
         return linear2(agg, x, self.lin_l.weight, self.lin_r.weight, self.lin_l.bias)  # one K7 GEMM
 

@@ -357,3 +357,62 @@ extern "C" gnn_status gnn_bn_act_bwd_f32(const float* dh, int64_t lddh, const fl
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }
+
+// ---- K13: SAGEResBNNet's input h0 = [x | sinusoid(t)] (src/models/gnn.py:145-160 the fixed
+// sin/cos time features, :172-176 the concatenation), written in one pass.  torch runs it as ~10
+// launches (long add, clamp, cast, reciprocal-multiply, arange, two muls, sin, cos, two cats), the
+// last a full [N, F + dim] copy.  Same float32 operation order as torch's: t = (float)clamp(t-1) ·
+// (1 / (T - 1)), freq_k = (float)k · (float)2π, sin / cos of t · freq_k.
+namespace gnnmp {
+namespace {
+
+__global__ __launch_bounds__(256) void time_inject_sin_kernel(const float* __restrict__ x, int64_t ldx, int64_t N,
+                                                              int F, const int64_t* __restrict__ t, int dim, int T,
+                                                              float inv, float* __restrict__ out, int64_t ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int W = F + dim;
+  const int half = dim / 2;
+  constexpr float kTwoPi = 6.283185307179586f;
+  for (int64_t r = wave; r < N; r += nwaves) {
+    int64_t tc = t[r] - 1;
+    tc = tc < 0 ? 0 : (tc > T - 1 ? T - 1 : tc);
+    const float tt = (float)tc * inv;
+    const float* xr = x + r * ldx;
+    float* orow = out + r * ldo;
+    for (int c = lane; c < W; c += 64) {
+      float v;
+      if (c < F) {
+        v = xr[c];
+      } else {
+        const int j = c - F;
+        if (j < half) v = sinf(tt * ((float)(j + 1) * kTwoPi));
+        else if (j < 2 * half) v = cosf(tt * ((float)(j - half + 1) * kTwoPi));
+        else v = 0.0f;
+      }
+      orow[c] = v;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace gnnmp
+
+using namespace gnnmp;
+
+extern "C" gnn_status gnn_time_inject_sin_f32(const float* x, int64_t ldx, int64_t N, int64_t F, const int64_t* t_idx,
+                                              int64_t dim, int64_t max_timestep, float* out, int64_t ldo,
+                                              gnn_stream_t stream) {
+  if (N < 0 || F < 0 || dim < 1 || max_timestep < 1 || F + dim > (1 << 20) || ldx < F || ldo < F + dim ||
+      (N > 0 && (!x || !t_idx || !out)))
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
+  if (N == 0) return GNN_OK;
+  const float inv = 1.0f / (float)(max_timestep - 1 > 1 ? max_timestep - 1 : 1);
+  int64_t blocks = ceil_div(N, 4 * 4);  // ~4 rows per wave
+  if (blocks > 8192) blocks = 8192;
+  time_inject_sin_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(x, ldx, N, (int)F, t_idx, (int)dim,
+                                                                             (int)max_timestep, inv, out, ldo);
+  GNN_LAUNCH_CHECK();
+  return GNN_OK;
+}

@@ -499,3 +499,20 @@ def bn_relu_dropout_residual(z: torch.Tensor, r, bn, p: float, seed: int, seed_c
     if z.dtype != torch.float32:
         z = z.float()
     return _BNActRes.apply(z, r, bn.weight, bn.bias, bn, float(p), seed, seed_ctr, _bn_group(bn))
+
+
+def time_inject_sin(x: torch.Tensor, t_idx: torch.Tensor, dim: int, max_timestep: int) -> torch.Tensor:
+    """K13: ``torch.cat([x, sinusoid(t_idx)], 1)`` of SAGEResBNNet (src/models/gnn.py:145-160,
+    172-176) in one pass; x float32 [N, F] with unit column stride, no gradient."""
+    if x.dim() != 2 or x.stride(1) != 1 or x.dtype != torch.float32:
+        x = x.float().contiguous()
+    N, Fin = x.shape
+    t = t_idx.reshape(-1)
+    if t.dtype != torch.int64 or t.stride(0) != 1:
+        t = t.to(torch.int64).contiguous()
+    if t.numel() != N:
+        raise ValueError(f"t_idx has {t.numel()} entries for {N} rows")
+    out = torch.empty((N, Fin + dim), dtype=torch.float32, device=x.device)
+    _lib.call("gnn_time_inject_sin_f32", x.data_ptr(), _ld(x), N, Fin, t.data_ptr(), int(dim), int(max_timestep),
+              out.data_ptr(), _ld(out), _lib.stream_handle(x.device))
+    return out

@@ -172,6 +172,8 @@ class SAGEResBNNet(nn.Module):
         if self.time_embed_type == "learned":
             te = self.time_emb((t_idx.long() - 1).clamp(0, self.max_timestep - 1))
         elif self.time_embed_type == "sin":
+            if x.is_cuda and not x.requires_grad and x.dim() == 2:
+                return _fused.time_inject_sin(x, t_idx, self.time_embed_dim, self.max_timestep)  # K13
             te = self._sinusoid(t_idx)
         else:
             return x

@@ -48,7 +48,7 @@ class _MfmaLinear(torch.autograd.Function):
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dy):
         a1, w1, a2, w2 = ctx.saved_tensors
-        dy = dy.contiguous()
+        dy = _rows(dy)  # row-strided views (K12's dz is the right half of a [N, 2C] buffer) read in place
         need = ctx.needs_input_grad
         dW1 = db = dW2 = None
         if need[1] or need[2] or need[4]:

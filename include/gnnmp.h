@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 12
+#define GNNMP_ABI_VERSION 13
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -376,6 +376,14 @@ gnn_status gnn_bn_act_bwd_f32(const float* dh, int64_t lddh, const float* z, int
                               const float* mean, const float* invstd, const float* weight, const float* bias,
                               float dropout_p, uint64_t seed, const int64_t* seed_ptr, const float* sums,
                               const double* n_total, float* dz, int64_t lddz, gnn_stream_t stream);
+
+/* K13: SAGEResBNNet's input with the fixed sinusoid time features, out = [x | te(t)] in one pass
+ * (replaces SAGEResBN._time_embed / torch.cat of src/models/gnn.py:145-160, 172-176):
+ * te_k = sin(t·2π(k+1)) for k < dim/2, cos(t·2π(k-dim/2+1)) for k < 2·(dim/2), 0 after, with
+ * t = clamp(t_idx - 1, 0, T - 1) / max(T - 1, 1) (T = max_timestep).  x [N, F] (ldx), t_idx int64
+ * [N], out [N, F + dim] (ldo).  No gradient: the features carry no parameters. */
+gnn_status gnn_time_inject_sin_f32(const float* x, int64_t ldx, int64_t N, int64_t F, const int64_t* t_idx,
+                                   int64_t dim, int64_t max_timestep, float* out, int64_t ldo, gnn_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Step ops around the hot path (src/train_gnn.py:136-183, 201-206)          */

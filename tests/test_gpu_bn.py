@@ -174,3 +174,21 @@ def test_sage_resbn_fused_equals_unfused(device):
         assert rel_l2(a, b) < 1e-5, k
     for k in res[0][2]:
         torch.testing.assert_close(res[0][2][k], res[1][2][k], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dim,T", [(2, 50), (5, 50), (8, 1)])
+def test_time_inject_sin_matches_torch(device, dim, T):
+    """K13 vs SAGEResBNNet's torch path (_sinusoid + cat), including out-of-range timesteps."""
+    from elliptic_gnn_project_amd.fused import time_inject_sin
+    from elliptic_gnn_project_amd.gnn import SAGEResBNNet
+
+    g = torch.Generator().manual_seed(dim)
+    N, Fin = 3001, 166
+    x = torch.randn(N, Fin, generator=g).to(device)
+    t = torch.randint(-2, 60, (N,), generator=g).to(device)
+    m = SAGEResBNNet(Fin, 16, layers=2, time_embed_dim=dim, time_embed_type="sin", max_timestep=T).to(device)
+    ref = torch.cat([x, m._sinusoid(t)], dim=1)
+    out = time_inject_sin(x, t, dim, T)
+    torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
+    assert torch.equal(out[:, :Fin], x)
+    assert torch.equal(m._inject_time(x, t), out)
