@@ -677,6 +677,9 @@ __global__ __launch_bounds__(256) void agg_combine_kernel(AggArgs a, int64_t nlo
 
 bool aligned(const void* p, int bytes) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0; }
 
+// Kernel-lab knob (gnnx_set_agg_variant, not part of the public ABI): 0 = production.
+int g_agg_lab_variant = 0;
+
 template <int MODE, int VEC, int NCH>
 void launch_split_passes(const AggArgs& a, const gnn_split* sp, hipStream_t st) {
   if (sp->num_pieces > sp->num_long)
@@ -689,13 +692,13 @@ void launch_split_passes(const AggArgs& a, const gnn_split* sp, hipStream_t st) 
 template <int MODE, int VEC>
 void launch_split_v(const AggArgs& a, const gnn_split* sp, hipStream_t st) {
   const int nch = (int)ceil_div(a.F / VEC, 64);
+  // (r12: 16- / 32-lane groups per piece and per combined row, 4 / 2 per wave, measured 6 us slower
+  // per F = 64 pass than one wave each — per-lane id loads and divergent piece lengths)
   if (nch <= 1) launch_split_passes<MODE, VEC, 1>(a, sp, st);
   else if (nch <= 2) launch_split_passes<MODE, VEC, 2>(a, sp, st);
   else launch_split_passes<MODE, VEC, 4>(a, sp, st);
 }
 
-// Kernel-lab knob (gnnx_set_agg_variant, not part of the public ABI): 0 = production.
-int g_agg_lab_variant = 0;
 
 template <int MODE>
 gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp);

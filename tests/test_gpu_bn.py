@@ -177,13 +177,14 @@ def test_sage_resbn_fused_equals_unfused(device):
 
 
 @pytest.mark.parametrize("dim,T", [(2, 50), (5, 50), (8, 1)])
-def test_time_inject_sin_matches_torch(device, dim, T):
+@pytest.mark.parametrize("Fin", [165, 166, 300])
+def test_time_inject_sin_matches_torch(device, dim, T, Fin):
     """K13 vs SAGEResBNNet's torch path (_sinusoid + cat), including out-of-range timesteps."""
     from elliptic_gnn_project_amd.fused import time_inject_sin
     from elliptic_gnn_project_amd.gnn import SAGEResBNNet
 
     g = torch.Generator().manual_seed(dim)
-    N, Fin = 3001, 166
+    N = 3001
     x = torch.randn(N, Fin, generator=g).to(device)
     t = torch.randint(-2, 60, (N,), generator=g).to(device)
     m = SAGEResBNNet(Fin, 16, layers=2, time_embed_dim=dim, time_embed_type="sin", max_timestep=T).to(device)
