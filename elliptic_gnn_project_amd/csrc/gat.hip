@@ -455,7 +455,7 @@ __device__ __forceinline__ void slot_pass(const GatArgs& a, const SlotLane& sl, 
   for (int32_t k = k0; k < end; k += 2 * sl.EP) {
     const bool two = k + sl.EP < end;
     const int32_t j0 = a.col[k];
-    const int32_t j1 = two ? a.col[k + sl.EP] : j0;
+    const int32_t j1 = a.col[two ? k + sl.EP : k];  // unconditional (clamped) load: no join wait
     const VecF<VEC> x0 = ldv<VEC>(a.xh + roff(j0, a.ld_xh) + sl.f0);
     const VecF<VEC> x1 = ldv<VEC>(a.xh + roff(j1, a.ld_xh) + sl.f0);
     float s0, s1;
@@ -638,7 +638,8 @@ __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g
         ep_.ad_out[r * H + sl.hs] = adr;
       }
     } else {
-      adr = own ? a.a_d[r * H + sl.hs] : 0.0f;
+      adr = a.a_d[(own ? r : 0) * H + sl.hs];
+      adr = own ? adr : 0.0f;
     }
     Online<VEC> st;
     st.init();
@@ -700,11 +701,11 @@ __device__ __forceinline__ float bwd_pass1(const GatArgs& a, const SlotLane& sl,
   for (int32_t k = k0; k < end; k += 2 * sl.EP) {
     const bool two = k + sl.EP < end;
     const int32_t j0 = a.col[k];
-    const int32_t j1 = two ? a.col[k + sl.EP] : j0;
+    const int32_t j1 = a.col[two ? k + sl.EP : k];  // unconditional (clamped) load: no join wait
     const VecF<VEC> x0 = ldv<VEC>(a.xh + roff(j0, a.ld_xh) + sl.f0);
     const VecF<VEC> x1 = ldv<VEC>(a.xh + roff(j1, a.ld_xh) + sl.f0);
     const float al0 = a.alpha[roff(k, H) + sl.hs];
-    const float al1 = two ? a.alpha[roff(k + sl.EP, H) + sl.hs] : 0.0f;
+    const float al1 = a.alpha[roff(two ? k + sl.EP : k, H) + sl.hs];  // used only when two
     const float z0 = a.a_s[roff(j0, H) + sl.hs] + adr;
     const float z1 = a.a_s[roff(j1, H) + sl.hs] + adr;
     const float da0 = head_sum(vdot<VEC>(x0, dO), sl.L, sl.hfirst) * inv_h;
@@ -810,7 +811,8 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatG
     int32_t beg = 0, end = 0;
     if (r < a.N) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
     const VecF<VEC> dO = load_dO<VEC>(a, sl, r, r < a.N);  // issued beside the rowptr loads
-    const float adr = r < a.N ? a.a_d[r * H + sl.hs] : 0.0f;
+    const float adr_ = a.a_d[(r < a.N ? r : 0) * H + sl.hs];
+    const float adr = r < a.N ? adr_ : 0.0f;
     const bool own = r < a.N && end - beg <= lg.T;
     if (!own) end = beg;
     BwdSlot q0{0.0f, 0.0f, false}, q1{0.0f, 0.0f, false};
