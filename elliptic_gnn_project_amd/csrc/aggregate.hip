@@ -480,17 +480,17 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   const int F = a.F;
   // the row's epilogue operands (1/deg, root addend, bias) are loaded up front, in flight with
   // the gather instead of one more dependent round trip after it
+  // (clamped row / feature indices, no per-value branch: the epilogue reads only f < F)
+  const int64_t rr = rok ? r : r0;
   float pdeg = 1.0f, padd[4] = {0.f, 0.f, 0.f, 0.f}, pbias[4] = {0.f, 0.f, 0.f, 0.f};
-  if (rok) {
-    if constexpr (MODE == GNN_AGG_MEAN) pdeg = fmaxf(a.nodew[r], 1.0f);
-    if (a.add) {
+  if constexpr (MODE == GNN_AGG_MEAN) pdeg = fmaxf(a.nodew[rr], 1.0f);
+  if (a.add) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) padd[f] = f < F ? a.add[r * a.ld_add + f] : 0.0f;
-    }
+    for (int f = 0; f < NF; ++f) padd[f] = a.add[rr * a.ld_add + (f < F ? f : 0)];
   }
   if (a.bias) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) pbias[f] = f < F ? a.bias[f] : 0.0f;
+    for (int f = 0; f < NF; ++f) pbias[f] = a.bias[f < F ? f : 0];
   }
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float* buf = sv[w];
