@@ -137,7 +137,8 @@ __device__ __forceinline__ float bn_y(const BnArgs& a, float z, int c) {
 }
 
 // forward apply: out = dropout(relu(y)) + r.  Threads as (column, row lane) like the reductions
-// (no per-element division); blocks stride over row groups.
+// (no per-element division); blocks stride over row groups.  (r12: 4 rows in flight per thread,
+// loads first, measured 28.8 -> 29.5 us here and 26.4 -> 29.9 us in the backward apply: kept 1.)
 __global__ __launch_bounds__(kBnThreads) void bn_act_res_fwd_kernel(BnArgs a) {
   const uint64_t seed = a.dropout ? bn_seed(a) : 0;
   const int C = a.C;
