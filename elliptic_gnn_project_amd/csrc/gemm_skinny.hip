@@ -49,7 +49,7 @@ __device__ __forceinline__ float nt_epi(const NTArgs& a, float v, int64_t row, i
 }
 
 constexpr int SK_MAXN = 8;
-constexpr int kSkU = 4;  // rows in flight per thread in nt_skinny_k_kernel
+constexpr int kSkU = 4;  // rows in flight per thread in the skinny NT kernels
 constexpr int SK_KMAX = KMAX;  // 384
 
 // C[r, n] = Σ_k A[r, k] W[n, k]: TPR lanes per row each own K/VEC/TPR chunks of VEC columns,
@@ -72,32 +72,47 @@ __global__ __launch_bounds__(256) void nt_skinny_n_kernel(NTArgs a, int lg_tpr) 
   const int rpb = 256 >> lg_tpr;
   const int nch = K / VEC;
   const uint64_t seed = a.dropout ? nt_seed(a) : 0;
-  for (int64_t r0 = (int64_t)blockIdx.x * rpb; r0 < a.M; r0 += (int64_t)gridDim.x * rpb) {
-    const int64_t r = r0 + (threadIdx.x >> lg_tpr);
-    float acc[NC];
+  // kSkU rows per thread per pass (block-uniform trip count: every lane reaches the shuffles), the
+  // rows' A chunks loaded together from clamped rows
+  const int64_t stride = (int64_t)gridDim.x * rpb;
+  for (int64_t b0 = (int64_t)blockIdx.x * rpb; b0 < a.M; b0 += kSkU * stride) {
+    const int64_t rt = b0 + (threadIdx.x >> lg_tpr);
+    float acc[kSkU][NC];
 #pragma unroll
-    for (int n = 0; n < NC; ++n) acc[n] = 0.0f;
-    if (r < a.M) {
-      for (int c = lig; c < nch; c += TPR) {
-        const int k = c * VEC;
-        const float* src = k < a.k1 ? a.a1 + r * a.lda1 + k : a.a2 + r * a.lda2 + (k - a.k1);
-        const Vf<VEC> x = ldf<VEC>(src);
+    for (int u = 0; u < kSkU; ++u)
+#pragma unroll
+      for (int n = 0; n < NC; ++n) acc[u][n] = 0.0f;
+    for (int c = lig; c < nch; c += TPR) {
+      const int k = c * VEC;
+      Vf<VEC> x[kSkU];
+#pragma unroll
+      for (int u = 0; u < kSkU; ++u) {
+        const int64_t r = rt + u * stride < a.M ? rt + u * stride : (rt < a.M ? rt : b0);
+        x[u] = ldf<VEC>(k < a.k1 ? a.a1 + r * a.lda1 + k : a.a2 + r * a.lda2 + (k - a.k1));
+      }
+#pragma unroll
+      for (int u = 0; u < kSkU; ++u)
 #pragma unroll
         for (int n = 0; n < NC; ++n)
 #pragma unroll
-          for (int i = 0; i < VEC; ++i) acc[n] = fmaf(x.v[i], ws[n * K + k + i], acc[n]);
+          for (int i = 0; i < VEC; ++i) acc[u][n] = fmaf(x[u].v[i], ws[n * K + k + i], acc[u][n]);
+    }
+#pragma unroll
+    for (int u = 0; u < kSkU; ++u)
+      for (int off = TPR >> 1; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int n = 0; n < NC; ++n) acc[u][n] += __shfl_xor(acc[u][n], off);
       }
-    }
-    for (int off = TPR >> 1; off >= 1; off >>= 1) {
 #pragma unroll
-      for (int n = 0; n < NC; ++n) acc[n] += __shfl_xor(acc[n], off);
-    }
-    if (r < a.M && lig < a.Nc) {
-      float v = acc[0];
+    for (int u = 0; u < kSkU; ++u) {
+      const int64_t r = rt + u * stride;
+      if (r < a.M && lig < a.Nc) {
+        float v = acc[u][0];
 #pragma unroll
-      for (int n = 1; n < NC; ++n) v = lig == n ? acc[n] : v;
-      v = nt_epi(a, v, r, lig, seed);
-      if (a.c) a.c[r * a.ldc + lig] = v;
+        for (int n = 1; n < NC; ++n) v = lig == n ? acc[u][n] : v;
+        v = nt_epi(a, v, r, lig, seed);
+        if (a.c) a.c[r * a.ldc + lig] = v;
+      }
     }
   }
 }
@@ -244,7 +259,7 @@ bool launch_nt_skinny(const NTArgs& a, hipStream_t st) {
     // TPR lanes per row: enough for K/VEC chunks (capped at a wave) and at least Nc, since lane
     // n of the row writes column n
     const int lg = std::max(lg2ceil(a.Nc), std::min(6, lg2ceil(K / VEC)));
-    const unsigned nb = grid_for(a.M, 256 >> lg, 8192);
+    const unsigned nb = grid_for(ceil_div(a.M, kSkU), 256 >> lg, 8192);
     const int NC = a.Nc <= 1 ? 1 : a.Nc <= 2 ? 2 : a.Nc <= 4 ? 4 : 8;
 #define GNN_SKN(V, N) nt_skinny_n_kernel<V, N><<<nb, 256, 0, st>>>(a, lg)
 #define GNN_SKN_V(V) \
