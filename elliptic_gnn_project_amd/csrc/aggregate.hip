@@ -769,6 +769,8 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
       // slower with cold caches (r10: 130.4 -> 138.5 us).  Lab 1 / 2 / 3: 8 / 4 / 32 rows.
       const int rpw = lv == 1 ? 8 : lv == 2 ? 4 : lv == 3 ? 32 : 16;
       const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
+      // (r13 lab: U = 16 neighbour rows in flight instead of 8, 98.5 -> 308.7 us warm — register
+      // pressure; not kept)
       if (vec == 4) agg_wave_kernel<MODE, 4, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
       else if (vec == 2) agg_wave_kernel<MODE, 2, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
       else agg_wave_kernel<MODE, 1, 2, false, 8><<<wblocks, 256, 0, st>>>(a, rpw);
