@@ -140,7 +140,7 @@ def _params(model):
 
 
 @pytest.mark.parametrize("order", ["aggregate_first", "transform_first"])
-@pytest.mark.parametrize("dims", [(166, 128), (128, 2), (16, 16)])
+@pytest.mark.parametrize("dims", [(166, 128), (128, 2), (16, 16), (64, 64), (64, 3)])
 def test_sage_conv(device, order, dims):
     from elliptic_gnn_project_amd.conv import SAGEConv
 
