@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -117,6 +117,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("workspace", c_ptr), ("workspace_bytes", c_size),
         ("a_dtype", c_i32), ("c_dtype", c_i32),
         ("mask", c_ptr), ("ldmask", c_i64), ("mask_scale", ctypes.c_float),
+        ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
     ]
 
 
@@ -132,6 +133,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("a2", c_ptr), ("lda2", c_i64), ("k2", c_i64),
         ("math", c_i32),
         ("a_dtype", c_i32), ("h_dtype", c_i32),
+        ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
     ]
 
 
@@ -204,6 +206,11 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
     ),
+    "gnn_split_planes_f32": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr]),
+    "gnn_sage_mean_fwd_planes": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr],
+    ),
     "gnn_sage_mean_bwd_f32": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],
@@ -242,6 +249,8 @@ SIGNATURES = {
     "gnn_gemm_nt_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),
     "gnn_gemm_tn_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32, ctypes.POINTER(c_size)]),
     "gnn_gemm_tn_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams), c_ptr, c_ptr, c_size, c_ptr]),
+    "gnn_gemm_nt_planes_ok": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams)]),
+    "gnn_gemm_tn_planes_ok": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams)]),
     "gnn_colsum_workspace_size": (ctypes.c_int, [c_i64, c_i64, ctypes.POINTER(c_size)]),
     "gnn_colsum_f32": (ctypes.c_int, [c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_masked_ce_workspace_size": (ctypes.c_int, [c_i64, ctypes.POINTER(c_size)]),

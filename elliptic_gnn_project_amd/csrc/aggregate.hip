@@ -104,6 +104,9 @@ struct AggArgs {
   int32_t seg_len;
   // dropout after bias / ReLU (element r·F + f, keep_elem of the NT epilogue)
   int32_t dropout; uint32_t keep_thresh; float drop_scale; uint64_t seed; const int64_t* seed_ptr;
+  // split-image output (gnn_sage_mean_fwd_planes): hi / mid / lo bf16 planes at yp + p·yps, row
+  // pitch ldy, columns [F, ywidth) zero
+  uint16_t* yp; int64_t yps; int32_t ywidth;
 };
 
 __device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
@@ -275,7 +278,8 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 // Wave-wide groups (LPS = 64, F/VEC > 32 chunks, e.g. the 166-wide layer-1 features):
 // every row boundary and neighbour id is wave-uniform, so they live in SGPRs (scalar loads,
 // v_readlane) and the next U neighbour ids are prefetched while the current U rows load.
-template <int MODE, int VEC, int NCH, bool BF = false, int U = 8>  // BF: x and y hold bf16 (no split partials)
+// PLN: y is written as a split image (3 bf16 planes, VEC even), no split partials.
+template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, bool PLN = false>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
@@ -308,6 +312,27 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + 64 * i;
+      if constexpr (PLN) {
+        static_assert(VEC % 2 == 0, "planes are written in column pairs");
+        if (c < nchunk || c * VEC < a.ywidth) {
+          uint32_t w[VEC / 2][3];
+#pragma unroll
+          for (int q = 0; q < VEC / 2; ++q) {
+            const float t0 = c < nchunk ? acc[i][2 * q] / d : 0.0f;
+            const float t1 = c < nchunk ? acc[i][2 * q + 1] / d : 0.0f;
+            split3_pair(t0, t1, w[q][0], w[q][1], w[q][2]);
+          }
+          uint16_t* dst = a.yp + r * a.ldy + c * VEC;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            if constexpr (VEC == 4) *reinterpret_cast<uint2*>(dst + p * a.yps) = make_uint2(w[0][p], w[1][p]);
+            else *reinterpret_cast<uint32_t*>(dst + p * a.yps) = w[0][p];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+        continue;
+      }
       if (!BF && c < nchunk && p0 >= 0) {  // long row: raw partial of piece 0
         vstore<VEC>(a.part + (int64_t)p0 * a.F + c * VEC, acc[i]);
       } else if (c < nchunk) {
@@ -1014,6 +1039,44 @@ extern "C" gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg
   p.transpose = 0;
   p.nodew = deg;
   return gnn_aggregate_f32(g, &p, x, ldx, F, out, ldo, stream);
+}
+
+// K1 with a split-image store: y = mean_{j->i} x[j] (MEAN over the CSR rows, PyG's order and
+// rounding) written as 3 bf16 planes (hi = RNE(y), mid = RNE(y - hi), lo = RNE(y - hi - mid)) at
+// img + p·plane_stride, row pitch ld, columns [F, width) zero.  Wide rows only (the wave gather).
+extern "C" gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
+                                               int64_t F, void* img, int64_t ld, int64_t plane_stride, int64_t width,
+                                               gnn_stream_t stream) {
+  if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, __func__, "null graph or deg");
+  if (F < 2 || ldx < F || width < F || width > ld || plane_stride < g->num_nodes * ld)
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad F / width / leading dimensions");
+  if (g->num_nodes > 0 && (!x || !img)) return fail(GNN_ERR_INVALID_ARG, __func__, "null x / image");
+  if (!g->rowptr || (g->num_slots > 0 && !g->col)) return fail(GNN_ERR_INVALID_ARG, __func__, "plan arrays null");
+  AggArgs a{};
+  a.ptr = g->rowptr;
+  a.nbr = g->col;
+  a.nodew = deg;
+  a.heads = 1;
+  a.chan = (int32_t)F;
+  a.x = x; a.ldx = ldx;
+  a.yp = static_cast<uint16_t*>(img); a.ldy = ld; a.yps = plane_stride; a.ywidth = (int32_t)width;
+  a.nrows = g->num_nodes;
+  a.F = (int32_t)F;
+  auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
+  const bool v4 = F % 4 == 0 && ldx % 4 == 0 && width % 4 == 0 && ld % 4 == 0 && plane_stride % 4 == 0 &&
+                  al(x, 16) && al(img, 8);
+  const bool v2 = F % 2 == 0 && ldx % 2 == 0 && width % 2 == 0 && ld % 2 == 0 && plane_stride % 2 == 0 &&
+                  al(x, 8) && al(img, 4);
+  const int vec = v4 ? 4 : 2;
+  if (!v2 || F / vec <= 32 || ceil_div(width, vec) > 128)
+    return fail(GNN_ERR_UNSUPPORTED, __func__, "needs even F, 32 < F / vec, width / vec <= 128 and aligned rows");
+  if (a.nrows == 0) return GNN_OK;
+  const int rpw = 16;
+  const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
+  hipStream_t st = (hipStream_t)stream;
+  if (vec == 4) agg_wave_kernel<GNN_AGG_MEAN, 4, 2, false, 8, true><<<wblocks, 256, 0, st>>>(a, rpw);
+  else agg_wave_kernel<GNN_AGG_MEAN, 2, 2, false, 8, true><<<wblocks, 256, 0, st>>>(a, rpw);
+  return hip_check(hipGetLastError(), __func__);
 }
 
 extern "C" gnn_status gnn_sage_mean_bwd_f32(const gnn_graph* g, const float* deg, const float* dout,

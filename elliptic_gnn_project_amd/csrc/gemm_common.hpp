@@ -53,6 +53,10 @@ struct NTArgs {
   int32_t a_bf16;  // A1/A2 hold bf16 (the float pointers are reinterpreted; ld in elements)
   int32_t c_bf16;  // C is stored as bf16 (RNE), and the projection reads the rounded values
   const float* mask; int64_t ldmask; float mask_scale;  // skinny kernels: C *= mask > 0 ? scale : 0
+  // optional split image of [A1 | A2] (gnn_planes): 3 bf16 planes hi/mid/lo, plane p at
+  // ap + p·ap_ps, row r at r·ap_ld; A1 in columns [0, k1), A2 in [ap_col2, ap_col2 + k2), zeros
+  // elsewhere.  The weight-stationary kernel then stages A by plain copies (no split VALU).
+  const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
@@ -153,6 +157,7 @@ struct TNArgs {
   int32_t want_db;
   int32_t a_bf16;  // A1/A2 hold bf16
   int32_t h_bf16;  // h holds bf16
+  const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;  // split image of [A1 | A2] (as NTArgs)
 };
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,
@@ -167,6 +172,23 @@ void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant = 0);  
 bool nt_ws_ok(const NTArgs& a);
 size_t nt_ws_tail_offset(int64_t k1, int64_t k2);
 void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks = 0);
+// the split-image forms (gemm_ws.hip NT, gemm_planes.hip TN): shapes they take, launchers
+bool nt_planes_ok(const NTArgs& a);
+void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st);
+bool tn_planes_ok(const TNArgs& a);
+void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st, int variant = 0);
+// 3 planes of one f32 split: hi = RNE(v), mid = RNE(v - hi), lo = RNE(v - hi - mid), exact sum
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+  typedef float f32x2_ __attribute__((ext_vector_type(2)));
+  h = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{a, b}, bf16x2_));
+  a -= __uint_as_float(h << 16);
+  b -= __uint_as_float(h & 0xffff0000u);
+  m = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{a, b}, bf16x2_));
+  a -= __uint_as_float(m << 16);
+  b -= __uint_as_float(m & 0xffff0000u);
+  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{a, b}, bf16x2_));
+}
 
 // VALU kernels for the narrow output-layer shapes (gemm_skinny.hip).  launch_nt_skinny returns
 // false (launching nothing) when the shape/epilogue is outside its envelope.

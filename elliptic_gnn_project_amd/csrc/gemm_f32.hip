@@ -749,13 +749,16 @@ using namespace gnnmp;
 
 static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn_stream_t stream, const char* fn) {
   if (!p) return fail(GNN_ERR_INVALID_ARG, fn, "null params");
-  if (p->M < 0 || p->N < 1 || p->k1 < 1 || p->k2 < 0 || !p->a1 || (p->k2 > 0 && !p->a2))
+  const bool planes_only = p->a_planes && !p->a1;  // A given only as a split image
+  if (p->M < 0 || p->N < 1 || p->k1 < 1 || p->k2 < 0 || (!p->a1 && !p->a_planes) ||
+      (p->k2 > 0 && !p->a2 && !planes_only))
     return fail(GNN_ERR_INVALID_ARG, fn, "bad shapes / null operands");
   if (!p->bt && !(p->w1 && (p->k2 == 0 || p->w2)))
     return fail(GNN_ERR_INVALID_ARG, fn, "need bt or w1 (and w2 when k2 > 0)");
   if (p->w1 && (p->N > BN || p->ldw1 < p->k1 || (p->k2 > 0 && p->ldw2 < p->k2)))
     return fail(GNN_ERR_INVALID_ARG, fn, "w1/w2 form needs N <= 128 and ldw >= k");
-  if (p->lda1 < p->k1 || (p->k2 > 0 && p->lda2 < p->k2) || (p->bt && p->ldb < p->N) || (p->c && p->ldc < p->N))
+  if ((!planes_only && (p->lda1 < p->k1 || (p->k2 > 0 && p->lda2 < p->k2))) || (p->bt && p->ldb < p->N) ||
+      (p->c && p->ldc < p->N))
     return fail(GNN_ERR_INVALID_ARG, fn, "bad leading dimensions");
   if (p->nproj < 0 || p->nproj > 4 || (p->nproj > 0 && (p->N > BN || !p->proj || !p->z || p->ldz < p->nproj)))
     return fail(GNN_ERR_INVALID_ARG, fn, "projection needs N <= 128, nproj <= 4, proj and z");
@@ -793,6 +796,20 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
   a.c_bf16 = p->c_dtype == GNN_DTYPE_BF16;
   a.mask = p->mask; a.ldmask = p->ldmask; a.mask_scale = p->mask_scale;
   if (p->mask && p->ldmask < p->N) return fail(GNN_ERR_INVALID_ARG, fn, "bad ldmask");
+  if (p->a_planes) {
+    a.ap = static_cast<const uint16_t*>(p->a_planes);
+    a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
+    a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
+    a.ap_ps = p->planes_stride;
+    const size_t img_bytes = (size_t)(a.ap_ld / 16) * 3 * 256 * sizeof(uint4);
+    if (p->math != GNN_MATH_F32 && variant == 0 && !p->mask && nt_planes_ok(a) && p->workspace &&
+        p->workspace_bytes >= img_bytes) {
+      launch_nt_ws_planes(a, static_cast<uint4*>(p->workspace), st);
+      return hip_check(hipGetLastError(), fn);
+    }
+    if (planes_only) return fail(GNN_ERR_UNSUPPORTED, fn, "split-image A outside the planes kernel's shapes");
+    a.ap = nullptr;  // the f32 operands serve
+  }
   if (variant == 0 && launch_nt_skinny(a, st)) return hip_check(hipGetLastError(), fn);  // Nc <= 8 or K <= 8
   if (p->mask) return fail(GNN_ERR_UNSUPPORTED, fn, "the mask epilogue needs a skinny shape (K <= 8 or N <= 8)");
   if (a.a_bf16 || a.c_bf16) {
@@ -857,7 +874,8 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   if (!p || !out) return fail(GNN_ERR_INVALID_ARG, __fn, "null params/out");
   if (p->M < 0 || p->Nr < 1 || p->Nr > 128 || p->k1 < 1 || p->k2 < 0 || p->k1 + p->k2 > KMAX)
     return fail(GNN_ERR_UNSUPPORTED, __fn, "needs 1 <= Nr <= 128 and k1 + k2 <= 384");
-  if (!p->a1 || (p->k2 > 0 && !p->a2) || p->lda1 < p->k1 || (p->k2 > 0 && p->lda2 < p->k2))
+  const bool planes_only = p->a_planes && !p->a1;
+  if (!planes_only && (!p->a1 || (p->k2 > 0 && !p->a2) || p->lda1 < p->k1 || (p->k2 > 0 && p->lda2 < p->k2)))
     return fail(GNN_ERR_INVALID_ARG, __fn, "bad A operands");
   if (p->dz) {
     if (p->nproj < 1 || p->nproj > MAXPROJ || !p->proj || p->lddz < p->nproj)
@@ -897,6 +915,21 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   if (a.h_bf16 && !a.a_bf16) return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 h needs bf16 A");
   // widest row pitch of any operand (the split kernel uses 32-bit element offsets)
   const int64_t ldmax = std::max({a.lda1, a.k2 > 0 ? a.lda2 : 0, a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
+  if (p->a_planes) {
+    a.ap = static_cast<const uint16_t*>(p->a_planes);
+    a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
+    a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
+    a.ap_ps = p->planes_stride;
+    if (p->math != GNN_MATH_F32 && tn_planes_ok(a)) {
+      launch_tn_planes(a, nblk, st, variant);
+      GNN_LAUNCH_CHECK();
+      slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+      GNN_LAUNCH_CHECK();
+      return GNN_OK;
+    }
+    if (planes_only) return fail(GNN_ERR_UNSUPPORTED, __fn, "split-image A outside the planes kernel's shapes");
+    a.ap = nullptr;
+  }
   if (variant == 0 && tn_skinny_ok(a)) {  // Nr <= 8 plain g form: VALU stream (gemm_skinny.hip)
     nblk = tn_skinny_blocks(a.M);
     if (workspace_bytes < (size_t)nblk * stride * sizeof(float))
@@ -928,4 +961,32 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
+}
+
+// Whether a call would run the split-image kernels (the caller then needs no f32 A).
+extern "C" int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p) {
+  if (!p || !p->a_planes || p->math == GNN_MATH_F32 || p->mask || p->M < 1) return 0;
+  NTArgs a{};
+  a.M = p->M; a.Nc = (int32_t)p->N; a.k1 = (int32_t)p->k1; a.k2 = (int32_t)p->k2;
+  a.w1 = p->w1; a.w2 = p->w2; a.c = p->c; a.ldc = p->ldc; a.bias = p->bias; a.relu = p->relu;
+  a.dropout = p->dropout_p > 0.f; a.nproj = p->nproj; a.ldz = p->ldz;
+  a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16; a.c_bf16 = p->c_dtype == GNN_DTYPE_BF16;
+  a.ap = static_cast<const uint16_t*>(p->a_planes);
+  a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
+  a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
+  a.ap_ps = p->planes_stride;
+  return nt_planes_ok(a) ? 1 : 0;
+}
+
+extern "C" int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p) {
+  if (!p || !p->a_planes || p->math == GNN_MATH_F32 || p->M < 1 || p->Nr < 1 || p->Nr > 128) return 0;
+  TNArgs a{};
+  a.M = p->M; a.Nr = (int32_t)p->Nr; a.g = p->g; a.ldg = p->ldg; a.dz = p->dz; a.lddz = p->lddz;
+  a.h = p->h; a.ldh = p->ldh; a.k1 = (int32_t)p->k1; a.k2 = (int32_t)p->k2;
+  a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16; a.h_bf16 = p->h_dtype == GNN_DTYPE_BF16;
+  a.ap = static_cast<const uint16_t*>(p->a_planes);
+  a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
+  a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
+  a.ap_ps = p->planes_stride;
+  return tn_planes_ok(a) ? 1 : 0;
 }

@@ -79,7 +79,11 @@ constexpr int WS_BIAS = 1, WS_RELU = 2, WS_DROP = 4, WS_PROJ = 8;
 // no epilogue 110, neither 78.5 (the bare MFMA loop at 53 % of its 42 us floor: one wave per SIMD
 // exposes the fragment reads and the two barriers per tile), no MFMAs 89 / 83, L2-hot A 140 / 109
 // (HBM costs ~6 us).  So: MFMA loop 78 + staging ~27 + fused epilogue ~30 (projection, dropout).
-template <int NKS, int EPI, int KS, int LAB = 0>
+// PLN: A is read from a split image (NTArgs::ap, gemm_planes.hip): every (plane, k-step) block
+// of a tile — [row 32][16 k] bf16, 1 KB — is one 16-byte load per lane (lane l: row l/2, k-half
+// (l & 1) ^ bit 3 of the row, i.e. the buffer's swizzled position 16·l) and one ds_write_b128; no
+// split, no tail copy (rows past M read zeros or the next plane's rows: their C rows are dropped).
+template <int NKS, int EPI, int KS, int LAB = 0, bool PLN = false>
 __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const uint4* __restrict__ bimg, int ntiles,
                                                              const float* __restrict__ tail) {
   constexpr int WS_THREADS = 256 * KS;
@@ -87,7 +91,10 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   constexpr int BUF = 3 * PLB;             // bytes per A buffer
   constexpr int KH0 = (NKS + KS - 1) / KS; // k-steps of the first K part (waves 0-3)
   constexpr int KH = KH0;                  // register slots per wave (the second part has <= KH0)
-  constexpr int QN = (128 * NKS + WS_THREADS - 1) / WS_THREADS;  // staged quads per thread per tile
+  constexpr int QF = (128 * NKS + WS_THREADS - 1) / WS_THREADS;  // staged f32 quads per thread per tile
+  constexpr int QP = (3 * NKS + WS_THREADS / 64 - 1) / (WS_THREADS / 64);  // PLN: 1 KB blocks per wave per tile
+  constexpr int QN = PLN ? QP : QF;                                // staging units per thread per tile
+  static_assert(!PLN || KS == 1, "the planes form runs one wave per SIMD");
   constexpr int RV = 16 / KS;              // accumulator rows (r-slots) a wave finishes
   constexpr bool TWO = (LAB & 16) != 0;    // two independent accumulator chains
   // LDS: two A buffers, the C tile of the epilogue ([32 rows][128] f32: coalesced C stores and
@@ -132,8 +139,8 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   }
 
   // ---- zero the pad columns of both buffers once (k in [k1 + k2, 16·NKS): the staging never
-  //      writes them; B is zero there but LDS garbage could be NaN)
-  {
+  //      writes them; B is zero there but LDS garbage could be NaN).  PLN: the image has them.
+  if constexpr (!PLN) {
     const int npad = NKS * 16 - k1 - k2;
     for (int i = tid; i < 2 * 3 * WS_ROWS * npad; i += WS_THREADS) {
       const int c = i % npad, rest = i / npad;
@@ -146,12 +153,12 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
 
   // ---- per-thread staging map (tile-invariant): quad i -> flat element f = 4q of segment g.
   //      Idle quads (q >= nq) stage zeros into the pad bytes of k-step 0 (never read).
-  uint32_t qoff[QN];               // LDS byte offsets of the quad's two pairs (pair 2 << 16 | pair 1)
-  int32_t qf[QN];                  // flat element offset inside the tile's segment
+  uint32_t qoff[QF];               // LDS byte offsets of the quad's two pairs (pair 2 << 16 | pair 1)
+  int32_t qf[QF];                  // flat element offset inside the tile's segment
   uint32_t qseg2 = 0, qidle = 0;   // bit i: quad i in segment 2 / idle
   const int nq1 = 8 * k1, nq = nq1 + 8 * k2;  // quads per tile (32 rows · k / 4)
 #pragma unroll
-  for (int i = 0; i < QN; ++i) {
+  for (int i = 0; i < (PLN ? 0 : QF); ++i) {
     const int q = tid + WS_THREADS * i;
     const bool seg2 = q >= nq1;
     const int kg = seg2 ? k2 : k1;
@@ -170,7 +177,16 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   // Staging registers, two sets: the quads of tile t+G are staged from one set during tile t's
   // k-loop, and each quad's registers are refilled with tile t+3G right after (prefetch depth 2:
   // every load has two tiles of MFMAs to land).
-  float4 st[2][QN];
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  using StT = std::conditional_t<PLN, u32x4, float4>;
+  StT st[2][QN];
+  // PLN: lane-constant image offset of this lane's piece, block b = wave + 4i of a tile (the last
+  // wave's spare slot repeats the last block: same bytes to the same place)
+  const int prow = lane >> 1;
+  const uint32_t pvoff = (uint32_t)((prow * a.ap_ld + 8 * ((lane & 1) ^ ((prow >> 3) & 1))) * 2);
+  const __amdgpu_buffer_rsrc_t prsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.ap), 0, PLN ? (int)(3 * a.ap_ps * 2) : 0, 0x00020000);
+  auto pblock = [&](int i) { return min(wave + 4 * i, 3 * NKS - 1); };
   // quad i of tile t into set `sb`: one unconditional 16-byte load (tile starts are 16-byte
   // aligned: 32·k·4 bytes).  The last tile is read from `tail`, a zero-padded copy of its rows
   // made by ws_tail_kernel, and tiles past the end re-read it (never staged into a used
@@ -180,32 +196,48 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   const float* const tail2 = tail + WS_ROWS * k1;
   // the tile's two segment bases, formed once per tile (not per quad: per-quad forms compiled
   // to a scalar branch pair per load inside the MFMA stream)
-  auto tile_base = [&](int t, const float*& b1, const float*& b2) {
+  // (PLN: toff = the tile's byte offset inside a plane)
+  auto tile_base = [&](int t, const float*& b1, const float*& b2, int& toff) {
     const int tc = (LAB & 8) ? blockIdx.x : min(t, ntiles - 1);  // LAB 8: re-read an L2-hot tile
     const bool last = tc == ntiles - 1;
     b1 = last ? tail1 : pa1 + (int64_t)tc * WS_ROWS * k1;
     b2 = last ? tail2 : pa2 + (int64_t)tc * WS_ROWS * k2;
+    toff = tc * WS_ROWS * a.ap_ld * 2;
   };
-  auto load_quad_b = [&](int sb, int i, const float* b1, const float* b2) {
-    const bool s2 = (qseg2 >> i) & 1u;
-    // idle quads (qf = 0) re-load the tile's first quad and stage it into the never-read pad
-    // bytes; no zeroing (a select on the loaded value made hipcc wait for the load right there)
-    st[sb][i] = *reinterpret_cast<const float4*>((s2 ? b2 : b1) + qf[i]);
+  auto load_quad_b = [&](int sb, int i, const float* b1, const float* b2, int toff) {
+    if constexpr (PLN) {
+      const int b = pblock(i), p = b / NKS, s = b - p * NKS;
+      st[sb][i] = __builtin_amdgcn_raw_buffer_load_b128(prsrc, (int)pvoff, (int)((p * a.ap_ps + 16 * s) * 2) + toff, 0);
+    } else {
+      const bool s2 = (qseg2 >> i) & 1u;
+      // idle quads (qf = 0) re-load the tile's first quad and stage it into the never-read pad
+      // bytes; no zeroing (a select on the loaded value made hipcc wait for the load right there)
+      st[sb][i] = *reinterpret_cast<const float4*>((s2 ? b2 : b1) + qf[i]);
+    }
   };
   auto load_quad = [&](int sb, int i, int t) {
     const float *b1, *b2;
-    tile_base(t, b1, b2);
-    load_quad_b(sb, i, b1, b2);
+    int toff;
+    tile_base(t, b1, b2, toff);
+    load_quad_b(sb, i, b1, b2, toff);
   };
   // stage one pair (half a quad: elements 2h, 2h+1) of quad i: split + 3 plane writes
+  // (PLN: the whole 16-byte piece on h == 0, one ds_write_b128)
   auto stage_pair = [&](char* buf, int sb, int i, int h) {
-    uint32_t hi, mi, lo;
-    if (h == 0) ws_split(st[sb][i].x, st[sb][i].y, hi, mi, lo);
-    else ws_split(st[sb][i].z, st[sb][i].w, hi, mi, lo);
-    const uint32_t o = h == 0 ? (qoff[i] & 0xffffu) : (qoff[i] >> 16);
-    *reinterpret_cast<uint32_t*>(buf + o) = hi;
-    *reinterpret_cast<uint32_t*>(buf + PLB + o) = mi;
-    *reinterpret_cast<uint32_t*>(buf + 2 * PLB + o) = lo;
+    if constexpr (PLN) {
+      if (h == 0) {
+        const int b = pblock(i), p = b / NKS, s = b - p * NKS;
+        *reinterpret_cast<u32x4*>(buf + p * PLB + s * WS_KSB + 16 * lane) = st[sb][i];
+      }
+    } else {
+      uint32_t hi, mi, lo;
+      if (h == 0) ws_split(st[sb][i].x, st[sb][i].y, hi, mi, lo);
+      else ws_split(st[sb][i].z, st[sb][i].w, hi, mi, lo);
+      const uint32_t o = h == 0 ? (qoff[i] & 0xffffu) : (qoff[i] >> 16);
+      *reinterpret_cast<uint32_t*>(buf + o) = hi;
+      *reinterpret_cast<uint32_t*>(buf + PLB + o) = mi;
+      *reinterpret_cast<uint32_t*>(buf + 2 * PLB + o) = lo;
+    }
   };
   auto stage_quad = [&](char* buf, int sb, int i) {
     stage_pair(buf, sb, i, 0);
@@ -239,7 +271,8 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   // MFMAs of this wave's K half from `cur`; the next tile's quads split into `nxt` in between
   auto kloop = [&](const char* cur, char* nxt, int sb, int tload) {
     const float *lb1, *lb2;
-    tile_base(tload, lb1, lb2);
+    int ltoff;
+    tile_base(tload, lb1, lb2, ltoff);
     floatx16 acc, acc2;
     constexpr int SQ0 = KH - QN > 0 ? KH - QN : 0;  // k-steps SQ0.. stage one quad each
     // one fragment set, each plane re-read for step s+1 right after its last use in step s:
@@ -279,7 +312,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       if (mm) ws_mfma<false>(acc, x[1], bw[s][0]);
       WS_FENCE;
       if (s + 1 < KH) x[1] = frag(sn, 1);
-      if (stg) load_quad_b(sb, qi, lb1, lb2);
+      if (stg) load_quad_b(sb, qi, lb1, lb2, ltoff);
       WS_FENCE;
       if (mm) {
         ws_mfma<false>(TWO ? acc2 : acc, x[0], bw[s][2]);
@@ -295,7 +328,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
 #pragma unroll
       for (int i = KH; i < QN; ++i) {
         stage_quad(nxt, sb, i);
-        load_quad_b(sb, i, lb1, lb2);
+        load_quad_b(sb, i, lb1, lb2, ltoff);
       }
     }
     if constexpr ((LAB & 4) != 0) {
@@ -474,7 +507,9 @@ __device__ __forceinline__ void ws_tail_block(const NTArgs& a, float* __restrict
 
 // B image over the CONCATENATED K (k < k1: W1, else W2 at k - k1): per 16-deep chunk c,
 // [plane hi/mid/lo][2n + khalf] uint4 (8 bf16), zero for n >= Nc and k >= k1 + k2.
-__device__ __forceinline__ void ws_presplit_block(const NTArgs& a, uint4* __restrict__ img, int nchunks, int blk) {
+// col2: first K index of W2 (k1, or the split image's ap_col2 with zeros in between)
+__device__ __forceinline__ void ws_presplit_block(const NTArgs& a, uint4* __restrict__ img, int nchunks, int blk,
+                                                  int col2) {
   const int idx = blk * 256 + threadIdx.x;  // (chunk, n, khalf)
   if (idx >= nchunks * 256) return;
   const int c = idx >> 8, n = (idx & 255) >> 1, kh = idx & 1;
@@ -484,7 +519,7 @@ __device__ __forceinline__ void ws_presplit_block(const NTArgs& a, uint4* __rest
     const int k = 16 * c + 8 * kh + j;
     float v = 0.f;
     if (n < a.Nc && k < a.k1) v = a.w1[(int64_t)n * a.ldw1 + k];
-    else if (n < a.Nc && k < a.k1 + a.k2) v = a.w2[(int64_t)n * a.ldw2 + (k - a.k1)];
+    else if (n < a.Nc && k >= col2 && k < col2 + a.k2) v = a.w2[(int64_t)n * a.ldw2 + (k - col2)];
     e[j] = v;
   }
   uint32_t w[4][3];
@@ -496,17 +531,17 @@ __device__ __forceinline__ void ws_presplit_block(const NTArgs& a, uint4* __rest
 
 // One launch for both per-call preparations (blocks [0, nchunks): B image; the rest: tail tile).
 __global__ __launch_bounds__(256) void ws_prep_kernel(NTArgs a, uint4* __restrict__ img, int nchunks,
-                                                      float* __restrict__ tail, int64_t r0) {
-  if ((int)blockIdx.x < nchunks) ws_presplit_block(a, img, nchunks, blockIdx.x);
+                                                      float* __restrict__ tail, int64_t r0, int col2) {
+  if ((int)blockIdx.x < nchunks) ws_presplit_block(a, img, nchunks, blockIdx.x, col2);
   else ws_tail_block(a, tail, r0, blockIdx.x - nchunks);
 }
 
-template <int NKS, int KS, int LAB = 0>
+template <int NKS, int KS, int LAB = 0, bool PLN = false>
 void launch_ws_k(const NTArgs& a, const uint4* bimg, const float* tail, hipStream_t st) {
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
   const int grid = std::min(ntiles, ws_num_cus());
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
-#define GNN_WS(E) gemm_nt_ws_kernel<NKS, E, KS, LAB><<<grid, 256 * KS, 0, st>>>(a, bimg, ntiles, tail)
+#define GNN_WS(E) gemm_nt_ws_kernel<NKS, E, KS, LAB, PLN><<<grid, 256 * KS, 0, st>>>(a, bimg, ntiles, tail)
   if (proj && drop) GNN_WS(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
   else if (proj) GNN_WS(WS_BIAS | WS_RELU | WS_PROJ);
   else if (drop) GNN_WS(WS_BIAS | WS_RELU | WS_DROP);
@@ -549,8 +584,8 @@ size_t nt_ws_tail_offset(int64_t k1, int64_t k2) {  // the B image (<= 24 chunks
 void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks) {
   const int nks = (a.k1 + a.k2 + 15) / 16;
   float* tail = reinterpret_cast<float*>(reinterpret_cast<char*>(img) + nt_ws_tail_offset(a.k1, a.k2));
-  ws_prep_kernel<<<(unsigned)(nks + ceil_div(WS_ROWS * (a.k1 + a.k2), 256)), 256, 0, st>>>(a, img, nks, tail,
-                                                                              (ceil_div(a.M, WS_ROWS) - 1) * WS_ROWS);
+  ws_prep_kernel<<<(unsigned)(nks + ceil_div(WS_ROWS * (a.k1 + a.k2), 256)), 256, 0, st>>>(
+      a, img, nks, tail, (ceil_div(a.M, WS_ROWS) - 1) * WS_ROWS, a.k1);
 #define GNN_WSL(N, K, L) launch_ws_k<N, K, L>(a, img, tail, st)
   if (ks < 0) {  // lab ablations of the production NKS = 21 instance (KS 1)
     if (nks != 21) ks = 0;
@@ -575,6 +610,33 @@ void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks) {
     default: if (ks == 2) GNN_WSL(21, 2, 0); else GNN_WSL(21, 1, 0); break;
   }
 #undef GNN_WSL
+}
+
+}  // namespace gnnmp
+
+namespace gnnmp {
+
+// The split-image form (PLN): f32 C, the w1/w2 B form, A from NTArgs::ap with a 336-wide image
+// row (21 k-steps: the SAGE layer-1 [agg | x] of 166 + 166 features, each padded to 168),
+// 64 < N <= 128, M >= 32, the nt_ws_ok epilogues.
+bool nt_planes_ok(const NTArgs& a) {
+  if (!a.ap || a.a_bf16 || a.c_bf16 || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc <= 64) return false;
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!al(a.ap) || a.ap_ld != 336 || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld)
+    return false;
+  if (a.ap_ps < a.M * (int64_t)a.ap_ld || 3 * a.ap_ps * 2 >= ((int64_t)1 << 31)) return false;
+  if (a.c && (!al(a.c) || a.ldc % 4 != 0 || a.M * a.ldc * 4 >= ((int64_t)1 << 31))) return false;
+  if (a.Nc % 4 != 0 || (a.nproj > 0 && a.M * a.ldz * 4 >= ((int64_t)1 << 31))) return false;
+  if (a.M < WS_ROWS) return false;
+  const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
+  if ((drop || proj || relu) && !(relu && bias)) return false;
+  return true;
+}
+
+void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st) {
+  const int nks = a.ap_ld / 16;
+  ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // the B image only
+  launch_ws_k<21, 1, 0, true>(a, img, nullptr, st);
 }
 
 }  // namespace gnnmp

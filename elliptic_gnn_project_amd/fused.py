@@ -29,6 +29,11 @@ import torch
 from . import _lib
 from .aggregation import KernelTimer, aggregate, agg_bytes
 from .graph import GraphPlan, get_plan
+from .planes import mean_planes_ok, x_image
+
+# The layer-1 operand [agg | x] as a split image (planes.py): on by default, GNNMP_PLANES=0 runs
+# the in-kernel split forms instead (same results within the split's error; A/B timing).
+_PLANES = os.environ.get("GNNMP_PLANES", "1") != "0"
 
 MAX_PROJ = 4  # nproj = 2 * num_classes <= 4
 
@@ -67,23 +72,34 @@ def _nt_workspace(device, n, k1, k2):
     return torch.empty(max(_nt_ws_bytes(n, k1, k2) // 4, 1), dtype=torch.float32, device=device)
 
 
+def _planes_fields(planes):
+    if planes is None:
+        return (None, 0, 0, 0)
+    return (planes.ptr, planes.ld, planes.ps, planes.col2)
+
+
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
-            out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None, mask=None, mask_scale=1.0):
+            out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None, mask=None, mask_scale=1.0,
+            planes=None, check_planes=False):
     """C = epilogue([a1 | a2] · B) on the NT kernels; B = bt ([K, n] row-major) or, with bt None,
     [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2].
-    bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too."""
-    M = a1.size(0)
-    bf = a1.dtype == torch.bfloat16
-    if out is None and want_c:
-        out = torch.empty((M, n), dtype=torch.bfloat16 if bf else torch.float32, device=a1.device)
+    bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too.
+    ``planes`` (planes.SplitImage): A read from the split image; a1 / a2 may then be None.
+    ``check_planes``: only report whether the call would take the split-image kernel (no launch)."""
+    if planes is not None:
+        M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
+    else:
+        M, k1, k2, dev = a1.size(0), a1.size(1), (a2.size(1) if a2 is not None else 0), a1.device
+    bf = a1 is not None and a1.dtype == torch.bfloat16
+    if out is None and want_c and not check_planes:
+        out = torch.empty((M, n), dtype=torch.bfloat16 if bf else torch.float32, device=dev)
     ws = None
     if w1 is not None:  # B pre-split image for the streaming split-bf16 kernel (≈24 KB per 32 of K)
-        k2_ = a2.size(1) if a2 is not None else 0
-        ws = _nt_workspace(a1.device, n, a1.size(1), k2_)
+        ws = _nt_workspace(dev, n, k1, k2)
     p = _lib.GnnGemmNTParams(
         M, n,
-        a1.data_ptr(), _ld(a1), a1.size(1),
-        _lib.ptr(a2), _ld(a2) if a2 is not None else 0, a2.size(1) if a2 is not None else 0,
+        _lib.ptr(a1), _ld(a1) if a1 is not None else 0, k1,
+        _lib.ptr(a2), _ld(a2) if a2 is not None else 0, k2,
         _lib.ptr(bt), _ld(bt) if bt is not None else 0,
         _lib.ptr(w1), _lib.ptr(w2), _ld(w1) if w1 is not None else 0, _ld(w2) if w2 is not None else 0,
         _lib.ptr(out), _ld(out) if out is not None else 0,
@@ -94,18 +110,22 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.DTYPE_BF16 if bf else _lib.DTYPE_F32,
         _lib.DTYPE_BF16 if (out is not None and out.dtype == torch.bfloat16) else _lib.DTYPE_F32,
         _lib.ptr(mask), _ld(mask) if mask is not None else 0, float(mask_scale),
+        *_planes_fields(planes),
     )
+    if check_planes:
+        return bool(_lib.load().gnn_gemm_nt_planes_ok(p))
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-    _lib.call("gnn_gemm_nt_f32", p, _lib.stream_handle(a1.device))
+    _lib.call("gnn_gemm_nt_f32", p, _lib.stream_handle(dev))
     if KernelTimer.active:
         e1.record()
-        k = a1.size(1) + (a2.size(1) if a2 is not None else 0)
+        k = k1 + k2
         # tag: kind, M, K, N, A element bytes, C element bytes, MFMA products per bf16 term
-        # (6 split-bf16, 1 bf16 storage, 0 exact f32, -1 the VALU kernels of the skinny shapes)
-        ea = a1.element_size()
+        # (6 split-bf16, 1 bf16 storage, 0 exact f32, -1 the VALU kernels of the skinny shapes).
+        # A split image is priced at the algorithmic f32 bytes; it moves 6 B / element.
+        ea = 4 if a1 is None else a1.element_size()
         prod = 0 if (_math(math) == _lib.MATH_F32 or w1 is None) else (1 if ea == 2 else 6)
         if ea == 4 and proj is None and (n <= 8 or (k <= 8 and a2 is None)):
             prod = -1
@@ -114,15 +134,16 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
     return out
 
 
-def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gout=None, math=None):
-    """((Gᵀ·a1, Gᵀ·a2), db, dzᵀ·h, dzsum) from one flat fp32 buffer — the MFMA TN kernel."""
-    M = a1.size(0)
-    k1 = a1.size(1)
-    k2 = a2.size(1) if a2 is not None else 0
+def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gout=None, math=None,
+            planes=None, check_planes=False):
+    """((Gᵀ·a1, Gᵀ·a2), db, dzᵀ·h, dzsum) from one flat fp32 buffer — the MFMA TN kernel.
+    ``planes``: A read from a split image (a1 / a2 may be None); ``check_planes`` as gemm_nt."""
+    if planes is not None:
+        M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
+    else:
+        M, k1, k2, dev = a1.size(0), a1.size(1), (a2.size(1) if a2 is not None else 0), a1.device
     nproj = proj.size(0) if dz is not None else 0
     n_out = nr * (k1 + k2) + nr + nproj * nr + nproj
-    out = torch.empty(n_out, dtype=torch.float32, device=a1.device)
-    ws = torch.empty(max(_tn_ws_bytes(M, nr, k1 + k2, nproj) // 4, 1), dtype=torch.float32, device=a1.device)
     p = _lib.GnnGemmTNParams(
         M, nr,
         _lib.ptr(g), _ld(g) if g is not None else 0,
@@ -130,20 +151,25 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         _lib.ptr(proj), nproj,
         _lib.ptr(h), _ld(h) if h is not None else 0, float(hscale),
         _lib.ptr(gout), _ld(gout) if gout is not None else 0,
-        a1.data_ptr(), _ld(a1), k1,
+        _lib.ptr(a1), _ld(a1) if a1 is not None else 0, k1,
         _lib.ptr(a2), _ld(a2) if a2 is not None else 0, k2,
         _math(math),
-        _lib.DTYPE_BF16 if a1.dtype == torch.bfloat16 else _lib.DTYPE_F32,
+        _lib.DTYPE_BF16 if (a1 is not None and a1.dtype == torch.bfloat16) else _lib.DTYPE_F32,
         _lib.DTYPE_BF16 if (h is not None and h.dtype == torch.bfloat16) else _lib.DTYPE_F32,
+        *_planes_fields(planes),
     )
+    if check_planes:
+        return bool(_lib.load().gnn_gemm_tn_planes_ok(p))
+    out = torch.empty(n_out, dtype=torch.float32, device=dev)
+    ws = torch.empty(max(_tn_ws_bytes(M, nr, k1 + k2, nproj) // 4, 1), dtype=torch.float32, device=dev)
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
-    _lib.call("gnn_gemm_tn_f32", p, out.data_ptr(), ws.data_ptr(), ws.numel() * 4, _lib.stream_handle(a1.device))
+    _lib.call("gnn_gemm_tn_f32", p, out.data_ptr(), ws.data_ptr(), ws.numel() * 4, _lib.stream_handle(dev))
     if KernelTimer.active:
         e1.record()
-        ea = a1.element_size()
+        ea = 4 if a1 is None else a1.element_size()
         prod = 0 if _math(math) == _lib.MATH_F32 else (1 if ea == 2 else 6)
         if ea == 4 and nr <= 8 and dz is None and h is None and gout is None:
             prod = -1
@@ -160,6 +186,19 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     o += nproj * nr
     dzs = out[o: o + nproj] if nproj else None
     return (dW1, dW2_), db, dW2, dzs
+
+
+def _layer0_image(x: torch.Tensor, n_out: int, nt_kw):
+    """The split image of [agg | x] when the planes path takes this layer (else None)."""
+    if not (_PLANES and mean_planes_ok(x)) or x.size(0) < 32:
+        return None
+    ld = ((x.size(1) + 7) // 8 * 16 + 15) // 16 * 16  # [agg | x], each padded to 8 columns
+    if 3 * x.size(0) * ld * 2 >= 2 ** 31:  # the kernels address the planes with 31-bit offsets
+        return None
+    im = x_image(x)
+    if not gemm_nt(None, None, n_out, planes=im, check_planes=True, **nt_kw):
+        return None
+    return im
 
 
 class _FusedSAGE(torch.autograd.Function):
@@ -179,17 +218,24 @@ class _FusedSAGE(torch.autograd.Function):
         aggs = []
         P = torch.cat([Wl[-1], Wr[-1]], dim=0).contiguous()  # [2C, F_{L-1}]
         z = None
+        ctx.image = None
         for l in range(L - 1):
             h = hs[-1]
-            agg = aggregate(plan, h, _lib.AGG_MEAN, nodew=plan.deg)
             last_hidden = l == L - 2
             if last_hidden:
                 z = torch.empty((h.size(0), 2 * C), dtype=torch.float32, device=h.device)
             # B = [W_l | W_r]ᵀ read in place from the Linear weights (K-contiguous [n][k] rows are
             # the NT kernel's LDS image): no transposed copy
-            hn = gemm_nt(agg, None, Wl[l].size(0), a2=h, w1=Wl[l], w2=Wr[l], bias=bl[l], relu=True,
-                         dropout_p=train_drop, seed=seeds[l], proj=P if last_hidden else None,
-                         z=z if last_hidden else None, seed_ptr=seed_ctr)
+            nt_kw = dict(w1=Wl[l], w2=Wr[l], bias=bl[l], relu=True, dropout_p=train_drop, seed=seeds[l],
+                         proj=P if last_hidden else None, z=z if last_hidden else None, seed_ptr=seed_ctr)
+            im = _layer0_image(h, Wl[0].size(0), nt_kw) if l == 0 else None
+            if im is not None:  # agg written straight into the split image by K1; A staged as planes
+                ctx.image = (im, im.fill_mean(plan, h))
+                hn = gemm_nt(None, None, Wl[l].size(0), planes=im, **nt_kw)
+                agg = None
+            else:
+                agg = aggregate(plan, h, _lib.AGG_MEAN, nodew=plan.deg)
+                hn = gemm_nt(agg, None, Wl[l].size(0), a2=h, **nt_kw)
             aggs.append(agg)
             hs.append(hn)
         logits = aggregate(plan, z[:, :C], _lib.AGG_MEAN, nodew=plan.deg, addend=z[:, C:], bias=bl[-1])
@@ -229,14 +275,23 @@ class _FusedSAGE(torch.autograd.Function):
             fo, fi = Wl[l].shape
             need_g = l > 0 or need_x
             gout = torch.empty((N, fo), dtype=torch.float32, device=dz.device) if need_g else None
+            a_l, im = aggs[l], None
+            if a_l is None:  # layer 0 on the split image (refreshed if another forward reused it)
+                im, gen = ctx.image
+                if im.gen != gen:
+                    im.fill_mean(plan, hs[0])
+                tn_kw = dict(dz=dz, proj=P) if l == L - 2 else dict(g=g)
+                if not gemm_tn(fo, None, None, h=hs[l + 1], hscale=hscale, gout=gout, planes=im,
+                               check_planes=True, **tn_kw):
+                    a_l, im = aggregate(plan, hs[0], _lib.AGG_MEAN, nodew=plan.deg), None
             if l == L - 2:
-                dW, db, dW2, dzs = gemm_tn(fo, aggs[l], hs[l], dz=dz, proj=P, h=hs[l + 1], hscale=hscale,
-                                           gout=gout)
+                dW, db, dW2, dzs = gemm_tn(fo, a_l, hs[l], dz=dz, proj=P, h=hs[l + 1], hscale=hscale,
+                                           gout=gout, planes=im)
                 grads[3 * (L - 1) + 0] = dW2[:C]
                 grads[3 * (L - 1) + 1] = dzs[C:]
                 grads[3 * (L - 1) + 2] = dW2[C:]
             else:
-                dW, db, _, _ = gemm_tn(fo, aggs[l], hs[l], g=g, h=hs[l + 1], hscale=hscale, gout=gout)
+                dW, db, _, _ = gemm_tn(fo, a_l, hs[l], g=g, h=hs[l + 1], hscale=hscale, gout=gout, planes=im)
             grads[3 * l + 0] = dW[0]
             grads[3 * l + 1] = db
             grads[3 * l + 2] = dW[1]

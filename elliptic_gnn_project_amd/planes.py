@@ -1,0 +1,92 @@
+"""Split images ("planes") of the SAGE layer-1 GEMM operand [agg | x].
+
+The split-bf16 GEMMs run every f32 operand as three bf16 terms, v = hi + mid + lo exactly
+(hi = RNE(v), mid = RNE(v - hi), lo = RNE(v - hi - mid)).  Splitting inside the GEMMs costs
+~5.5 VALU per element, twice per step for the [N, 332] layer-1 operand.  A ``SplitImage`` holds
+the three planes in HBM instead ([3, N, ld] bf16, include/gnnmp.h gnn_split_planes_f32):
+
+    columns [0, k1)               agg = mean_{j->i} x[j]   K1 writes them every forward
+                                                           (gnn_sage_mean_fwd_planes)
+    columns [col2, col2 + k2)     x                        written once per input tensor
+    everything else               zero
+
+``x`` is a constant of the training run (the reference prepares it once, src/train_gnn.py:
+315-350), so its planes are cached on the tensor like the graph plan (graph.py), keyed on
+(data_ptr, _version): an in-place edit of x rebuilds them.  The agg half is recomputed on every
+forward — nothing computed from the weights or the step's inputs is reused across steps.
+
+A forward stamps the image with a generation number; the backward checks it, and recomputes
+the agg half (deterministically: the same bits) if another grad-enabled forward over the same x
+ran in between.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+_ATTR = "_gnnmp_split_image"
+
+
+def _pad8(k: int) -> int:
+    return (k + 7) // 8 * 8
+
+
+class SplitImage:
+    """[3, N, ld] bf16 planes of [A1 | A2] with A1 at column 0 and A2 at column ``col2``."""
+
+    def __init__(self, n: int, k1: int, k2: int, device: torch.device):
+        self.n, self.k1, self.k2 = int(n), int(k1), int(k2)
+        self.col2 = _pad8(k1)
+        self.ld = (self.col2 + _pad8(k2) + 15) // 16 * 16
+        self.ps = self.n * self.ld
+        self.img = torch.empty((3, self.n, self.ld), dtype=torch.bfloat16, device=device)
+        self.gen = 0
+        self.x_key = None
+
+    @property
+    def ptr(self) -> int:
+        return self.img.data_ptr()
+
+    def fill_x(self, x: torch.Tensor) -> None:
+        """Planes of x into columns [col2, ld) (zeros past k2)."""
+        with torch.cuda.device(x.device):
+            _lib.call("gnn_split_planes_f32", x.data_ptr(), int(x.stride(0)), self.n, self.k2, self.ptr, self.ld,
+                      self.ps, self.col2, self.ld - self.col2, _lib.stream_handle(x.device))
+
+    def fill_mean(self, plan, x: torch.Tensor) -> int:
+        """K1: planes of mean_{j->i} x[j] into columns [0, col2); returns the new generation."""
+        from .aggregation import KernelTimer, agg_bytes
+
+        e0 = KernelTimer.begin()
+        _lib.call("gnn_sage_mean_fwd_planes", plan.c_graph, plan.deg.data_ptr(), x.data_ptr(), int(x.stride(0)),
+                  self.k1, self.ptr, self.ld, self.ps, self.col2, _lib.stream_handle(x.device))
+        # algorithmic bytes of K1 as SURVEY §8(d) counts them (f32 output); the planes store 6 B
+        KernelTimer.end(e0, ("agg", _lib.AGG_MEAN, False, self.k1), agg_bytes(plan, self.k1, _lib.AGG_MEAN, False, False))
+        self.gen += 1
+        return self.gen
+
+
+def mean_planes_ok(x: torch.Tensor) -> bool:
+    """Whether gnn_sage_mean_fwd_planes takes x (f32 rows, even F with 32 < F/vec, F <= 256)."""
+    if x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1 or not x.is_cuda:
+        return False
+    F = x.size(1)
+    vec = 4 if (F % 4 == 0 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0) else 2
+    return F % 2 == 0 and x.stride(0) % 2 == 0 and F // vec > 32 and _pad8(F) // vec <= 128
+
+
+def x_image(x: torch.Tensor) -> SplitImage:
+    """The cached split image of [agg | x] for x (its x half filled), rebuilt after in-place edits."""
+    key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
+    im = getattr(x, _ATTR, None)
+    if im is None or im.n != x.size(0) or im.k2 != x.size(1):
+        im = SplitImage(x.size(0), x.size(1), x.size(1), x.device)
+        try:
+            setattr(x, _ATTR, im)
+        except (AttributeError, RuntimeError):  # e.g. inference tensors: no caching
+            pass
+    if im.x_key != key:
+        im.fill_x(x)
+        im.x_key = key
+    return im

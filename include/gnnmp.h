@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 13
+#define GNNMP_ABI_VERSION 14
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -169,6 +169,22 @@ gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params* p, const 
 gnn_status gnn_aggregate_bf16(const gnn_graph* g, const gnn_agg_params* p, const void* x, int64_t ldx,
                               int64_t F, void* y, int64_t ldy, gnn_stream_t stream);
 
+/* Split images ("planes"): an f32 matrix held as three bf16 planes hi / mid / lo with
+ * v = hi + mid + lo exactly (hi = RNE(v), mid = RNE(v - hi), lo = RNE(v - hi - mid)); plane p
+ * at img + p*plane_stride elements, element (r, c) at r*ld + c.  The split-bf16 GEMMs read them
+ * instead of splitting f32 operands in-kernel (gnn_gemm_nt_params / gnn_gemm_tn_params .a_planes).
+ *
+ * gnn_split_planes_f32: columns [col0, col0 + width) of rows [0, rows) <- planes of x [rows, F]
+ * (zeros at columns >= F; width, col0, ld, plane_stride even). */
+gnn_status gnn_split_planes_f32(const float* x, int64_t ldx, int64_t rows, int64_t F, void* img, int64_t ld,
+                                int64_t plane_stride, int64_t col0, int64_t width, gnn_stream_t stream);
+/* K1 with a split-image store: columns [0, width) of img <- planes of mean_{j->i} x[j]
+ * (SAGEConv aggr='mean', the same arithmetic as gnn_sage_mean_fwd_f32), zeros at columns >= F.
+ * Wide rows only (even F, 32 < F / vec with vec = 4 or 2, width / vec <= 128): UNSUPPORTED otherwise. */
+gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
+                                    void* img, int64_t ld, int64_t plane_stride, int64_t width,
+                                    gnn_stream_t stream);
+
 /* Named forms of the above (what an FFI binding of SAGEConv would call). */
 gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
                                  int64_t F, float* out, int64_t ldo, gnn_stream_t stream);
@@ -299,6 +315,12 @@ typedef struct {
                                             backward of a saved activation (K <= 8 or N <= 8 shapes) */
   int64_t ldmask;
   float mask_scale;
+  const void* a_planes;                  /* optional split image of [A1 | A2] (see gnn_split_planes_f32):
+                                            A1 in columns [0, k1), A2 in [planes_col2, planes_col2 + k2),
+                                            zeros elsewhere.  When the shape is one the split-image kernel
+                                            takes (gnn_gemm_nt_planes_ok) A is read from it and a1 / a2 may
+                                            be NULL; otherwise a1 / a2 are used (UNSUPPORTED if NULL). */
+  int64_t planes_ld, planes_stride, planes_col2;
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
@@ -318,6 +340,8 @@ typedef struct {
   int32_t a_dtype;                       /* gnn_dtype of A1/A2 (BF16: G rounded to bf16, one product;
                                             needs M >= 16) */
   int32_t h_dtype;                       /* gnn_dtype of h */
+  const void* a_planes;                  /* optional split image of [A1 | A2], as gnn_gemm_nt_params */
+  int64_t planes_ld, planes_stride, planes_col2;
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).
@@ -326,6 +350,12 @@ typedef struct {
 gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t Kc, int32_t nproj, size_t* bytes);
 gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* workspace, size_t workspace_bytes,
                            gnn_stream_t stream);
+/* 1 when the call would read A from p->a_planes (the f32 A operands are then not needed), else 0.
+ * Split-image shapes: NT image rows of 336 (the SAGE layer-1 [agg | x], 166 + 166 padded to 168
+ * each), 64 < N <= 128, f32 C; TN image rows of 32..336 (multiple of 16), f32 h; both need the
+ * three planes to span < 2 GiB. */
+int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p);
+int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p);
 
 /* ------------------------------------------------------------------------ */
 /* Dense helpers used by the fused conv paths                               */
