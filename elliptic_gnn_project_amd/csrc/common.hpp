@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <string>
 #include <type_traits>
+#include <utility>
 
 #include "../../include/gnnmp.h"
 

@@ -69,28 +69,23 @@ __device__ __forceinline__ bf16x8 cat_frag(s16x4 a, s16x4 b) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-__device__ __forceinline__ floatx16 mfma6p(const bf16x8 (&x)[3], const bf16x8 (&y)[3], floatx16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[1], y[1], c, 0, 0, 0);  // small terms first
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[2], y[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[1], y[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x[0], y[0], c, 0, 0, 0);
-  return c;
-}
-
 // Block: 4 waves (one per SIMD); wave w owns dW rows 32w .. +32 (G columns) x all KT k-tiles of
 // the image width.  Rows: blockIdx.x·rows_per_block .. in chunks of 16, each LOADED from row
 // min(start, M - 16) so every load is in bounds (the G mask zeroes rows outside the block).
-// Staging per thread and chunk: PT_NP A pieces (one 16-byte buffer load + one ds_write_b128
-// each) and one G slot (column n = tid mod 128, 8 consecutive rows) — h (MASK) or g values,
-// G = (dz·P) ⊙ mask formed from a 2-slot LDS ring of dz rows (PROJ).
-template <bool PROJ, bool MASK, int KT, bool GOUT>
+// Software-pipelined: iteration c runs chunk c's 6·KT MFMAs and, between them (sched_barrier
+// fences pin the order), stages chunk c+1 into the other LDS buffers in 22 units — per thread
+// PT_NP A pieces (one ds_write_b128 each, then the refill load of chunk c+2), one G slot
+// (column n = tid mod 128, 8 consecutive rows: G = (dz·P) ⊙ mask or g ⊙ mask, split, 3
+// ds_write_b128) and the dz ring slot of chunk c+2.  One barrier per chunk.  With one wave per
+// SIMD the staging issues in the MFMAs' shadow instead of in a phase of its own.
+// LAB (timing ablations, csrc/lab/lab_tn.hip only; the library instantiates 0): bit 1 no MFMAs,
+// bit 2 no staging slots, bit 4 no fragment reads in the loop, bit 8 no per-chunk barrier.
+template <bool PROJ, bool MASK, int KT, bool GOUT, int LAB = 0>
 __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Gt[2][3 * PT_GPL];
   __shared__ __attribute__((aligned(16))) uint16_t At[2][3 * PT_APL];
-  __shared__ float Ps[MAXPROJ * 128];
-  __shared__ float dzL[2][256];
+  __shared__ float dzL[2][256];  // dz rows of a chunk (16 x 4), threads 0..63 write theirs
+  constexpr int NU = 2 * PT_NP + 31;  // staging slots per chunk (<= 6·KT for the MFMA shadow)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -105,13 +100,6 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   for (int t = 0; t < KT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-
-  if constexpr (PROJ) {
-    if (tid < 128) {
-#pragma unroll
-      for (int q = 0; q < MAXPROJ; ++q) Ps[q * 128 + tid] = (q < a.nproj && tid < a.Nr) ? a.proj[q * a.Nr + tid] : 0.0f;
-    }
-  }
 
   // ---- A pieces of this thread (chunk-invariant): byte offsets in the image (relative to the
   //      chunk's first row) and in the LDS chunk.  Idle pieces re-load piece 0 into a pad slot
@@ -143,18 +131,20 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   const int zqc = PROJ ? min(zq, a.nproj - 1) : 0;
   float pcol[MAXPROJ];
 #pragma unroll
-  for (int q = 0; q < MAXPROJ; ++q) pcol[q] = 0.f;
+  for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (PROJ && q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
 
   const int Mi = (int)a.M;
   auto ldbase = [&](int c) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
+  const int clast = max(nch - 1, 0);
   u32x4 ra[PT_NP];
   float rg[8], rg2[8];
   float rz = 0.f;
-  auto load = [&](int c) {
+  // loads of chunk c into the stage registers (c clamped by the callers: always in bounds)
+  auto load_a = [&](int j, int c) {
+    ra[j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], ldbase(c) * ld * 2, 0);
+  };
+  auto load_g = [&](int c) {
     const int mb = ldbase(c);
-    const int soff = mb * ld * 2;
-#pragma unroll
-    for (int j = 0; j < PT_NP; ++j) ra[j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], soff, 0);
     if constexpr (MASK || !PROJ) {  // the dz form without a mask reads no G column
       uint32_t o = (uint32_t)((mb + 8 * go) * gld);
 #pragma unroll
@@ -171,65 +161,122 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
         o2 += (uint32_t)g2ld;
       }
     }
-    if constexpr (PROJ) rz = a.dz[(uint32_t)((ldbase(c + 1) + zr) * (int)a.lddz + zqc)];  // dz rows of chunk c + 1
+  };
+  auto load_z = [&](int c) {
+    if constexpr (PROJ) rz = a.dz[(uint32_t)((ldbase(c) + zr) * (int)a.lddz + zqc)];
+  };
+  // the dz ring slot of chunk k (zero outside the block's rows: G, dzᵀh and Σdz need no row masks)
+  auto put_z = [&](int k) {
+    if constexpr (PROJ) {
+      const int mb = ldbase(k);
+      const bool ok = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + k * PT_ROWS - mb &&
+                      zr < (int)mend - mb;
+      dzL[k & 1][tid] = ok ? rz : 0.0f;
+    }
   };
 
   float db = 0.f, dzs = 0.f;
   float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
-  auto store = [&](int c) {
-    const int buf = c & 1;
-    const int mb = ldbase(c);
-    const int rlo = (int)mbeg + c * PT_ROWS - mb;  // valid loaded rows: [rlo, rhi)
-    const int rhi = (int)mend - mb;
-    if constexpr (PROJ) {  // dz ring slot of chunk c + 1 (slot read by G(c - 1): behind barrier c - 1)
-      const int mb1 = ldbase(c + 1);
-      const bool ok = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + (c + 1) * PT_ROWS - mb1 &&
-                      zr < (int)mend - mb1;
-      dzL[(c + 1) & 1][tid] = ok ? rz : 0.0f;
+  float e[8];
+  uint32_t w[4][3];
+  float4 zv[8];  // dz rows of the G slot (read in one unit, ahead of their use)
+  float zsv[8];
+  auto z_read = [&](int c, int i0, int n) {  // rows i0 .. i0 + n of the G slot
+    if constexpr (PROJ) {
+      const int buf = c & 1;
+#pragma unroll
+      for (int i = i0; i < i0 + n; ++i) {
+        const int r = 8 * go + i;
+        zv[i] = *reinterpret_cast<const float4*>(&dzL[buf][r * MAXPROJ]);
+        zsv[i] = dzL[buf][r * MAXPROJ + (gn & (MAXPROJ - 1))];
+      }
     }
-    char* ab = reinterpret_cast<char*>(At[buf]);
-#pragma unroll
-    for (int j = 0; j < PT_NP; ++j) *reinterpret_cast<u32x4*>(ab + loff[j]) = ra[j];
-    float e[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = 8 * go + i;
-      const bool ok = r >= rlo && r < rhi && gcol;
-      float g;
+  };
+  auto put_a = [&](int j, int c) {
+    *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(At[c & 1]) + loff[j]) = ra[j];
+  };
+  // G row i of the slot (after z_read), in two halves (e[i] carries the raw value between them)
+  auto g_row = [&](int i, int c, int half) {
+    if (half == 0) {
       if constexpr (PROJ) {
-        const float4 z = *reinterpret_cast<const float4*>(&dzL[buf][r * MAXPROJ]);
-        g = z.x * pcol[0];
+        const float4 z = zv[i];
+        float g = z.x * pcol[0];
         g = fmaf(z.y, pcol[1], g);
         g = fmaf(z.z, pcol[2], g);
-        g = fmaf(z.w, pcol[3], g);
-        // staged dz rows are zero outside [rlo, rhi) and P is zero past Nr: no per-row masks
+        e[i] = fmaf(z.w, pcol[3], g);
         if constexpr (MASK) {
           dw2[0] = fmaf(z.x, rg[i], dw2[0]);
           dw2[1] = fmaf(z.y, rg[i], dw2[1]);
           dw2[2] = fmaf(z.z, rg[i], dw2[2]);
           dw2[3] = fmaf(z.w, rg[i], dw2[3]);
         }
-        const float zs = dzL[buf][r * MAXPROJ + (gn & (MAXPROJ - 1))];  // unconditional read + select:
-        dzs += gn < MAXPROJ ? zs : 0.0f;                                 // no per-row branch
       } else {
-        g = MASK ? rg2[i] : rg[i];
+        e[i] = MASK ? rg2[i] : rg[i];
       }
-      if constexpr (MASK) g = rg[i] > 0.0f ? g * a.hscale : 0.0f;
-      if constexpr (!PROJ) g = ok ? g : 0.0f;
-      db += g;
-      if constexpr (GOUT) {
-        if (a.gout && ok) a.gout[(int64_t)(mb + r) * a.ldgout + gn] = g;
-      }
-      e[i] = g;
+      return;
     }
-    uint32_t w[4][3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) split3_pair(e[2 * j], e[2 * j + 1], w[j][0], w[j][1], w[j][2]);
-    uint16_t* gd = Gt[buf] + gn * PT_GP + 8 * go;
+    const int mb = ldbase(c);
+    const int r = 8 * go + i;
+    const bool ok = r >= (int)mbeg + c * PT_ROWS - mb && r < (int)mend - mb && gcol;
+    float g = e[i];
+    if constexpr (PROJ) dzs += gn < MAXPROJ ? zsv[i] : 0.0f;  // unconditional read + select: no branch
+    if constexpr (MASK) g = rg[i] > 0.0f ? g * a.hscale : 0.0f;
+    if constexpr (!PROJ) g = ok ? g : 0.0f;
+    db += g;
+    if constexpr (GOUT) {
+      if (a.gout && ok) a.gout[(int64_t)(mb + r) * a.ldgout + gn] = g;
+    }
+    e[i] = g;
+  };
+  // split3_pair of (e[2j], e[2j+1]) in two halves: hi and the first remainders, then mid / lo
+  auto split_half = [&](int j, int half) {
+    typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));
+    typedef float f32x2_ __attribute__((ext_vector_type(2)));
+    float& x0 = e[2 * j];
+    float& x1 = e[2 * j + 1];
+    if (half == 0) {
+      const uint32_t h = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{x0, x1}, bf16x2_));
+      w[j][0] = h;
+      x0 -= __uint_as_float(h << 16);
+      x1 -= __uint_as_float(h & 0xffff0000u);
+    } else {
+      const uint32_t m = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{x0, x1}, bf16x2_));
+      w[j][1] = m;
+      const float y0 = x0 - __uint_as_float(m << 16);
+      const float y1 = x1 - __uint_as_float(m & 0xffff0000u);
+      w[j][2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{y0, y1}, bf16x2_));
+    }
+  };
+  auto g_put = [&](int c) {
+    uint16_t* gd = Gt[c & 1] + gn * PT_GP + 8 * go;
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       *reinterpret_cast<uint4*>(gd + p * PT_GPL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
   };
+  // staging slot k of chunk c + 1, issued right after one MFMA of chunk c (a few instructions in
+  // the MFMA's shadow); refills for chunks c + 2 / c + 3
+  auto unit = [&](int k, int c) {
+    constexpr int A0 = 0, Z0 = 2 * PT_NP, G0 = Z0 + 4, S0 = G0 + 16, P0 = S0 + 8;
+    if (k < Z0) {
+      if (k & 1) load_a(k >> 1, min(c + 2, clast));
+      else put_a(k >> 1, c + 1);
+    } else if (k < G0) {
+      z_read(c + 1, 2 * (k - Z0), 2);
+    } else if (k < S0) {
+      g_row((k - G0) >> 1, c + 1, (k - G0) & 1);
+    } else if (k < P0) {
+      split_half((k - S0) >> 1, (k - S0) & 1);
+    } else if (k == P0) {
+      g_put(c + 1);
+    } else if (k == P0 + 1) {
+      load_g(min(c + 2, clast));
+    } else if (k == P0 + 2) {
+      put_z(c + 2);
+      load_z(min(c + 3, clast));
+    }
+    (void)A0;
+  };
+  static_assert(2 * PT_NP + 4 + 16 + 8 + 3 == NU, "slot count");
 
   // fragment addresses: G rows 32·wave + (lane & 31), k = 8·(lane >> 5); A (transposed reads)
   // lane 4q + p of 16-lane group g supplies row 8·(g >> 1) + q, columns 16·(g & 1) + 4p ..
@@ -240,6 +287,7 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
     const uint16_t* q = base + p * PT_APL + t * 32;
     return cat_frag(tr_read(q), tr_read(q + 4 * PT_AP));
   };
+#define PT_FENCE __builtin_amdgcn_sched_barrier(0)
   auto compute = [&](int c) {
     const int buf = c & 1;
     bf16x8 gf[3], af[2][3];
@@ -248,35 +296,64 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
     const uint16_t* ab = At[buf] + afo;
 #pragma unroll
     for (int p = 0; p < 3; ++p) af[0][p] = afrag(ab, 0, p);
-    // tile t+1's fragment reads are issued before tile t's six MFMAs; the fences keep hipcc from
-    // sinking them next to their use (it did: one exposed lgkmcnt(0) wait per tile)
+    // tile t+1's fragment reads are issued before tile t's MFMAs (in flight across them); one
+    // staging slot after each MFMA (fences pin the order: the slot issues in the MFMA's shadow)
+    constexpr int pa[6] = {1, 2, 0, 1, 0, 0}, pb[6] = {1, 0, 2, 0, 1, 0};  // small terms first
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      if (t + 1 < KT) {
+      if (t + 1 < KT && !(LAB & 4)) {
 #pragma unroll
         for (int p = 0; p < 3; ++p) af[(t + 1) & 1][p] = afrag(ab, t + 1, p);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      acc[t] = mfma6p(gf, af[t & 1], acc[t]);
-      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        PT_FENCE;
+        if constexpr (!(LAB & 1))
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[pa[m]], af[(LAB & 4) ? 0 : (t & 1)][pb[m]], acc[t], 0, 0, 0);
+        PT_FENCE;
+        if (6 * t + m < NU && !(LAB & 2)) unit(6 * t + m, c);
+      }
+      PT_FENCE;
+    }
+#pragma unroll
+    for (int u = 6 * KT; u < NU; ++u)  // narrow images: the slots past the MFMAs
+      if (!(LAB & 2)) unit(u, c);
+    if constexpr ((LAB & 1) != 0) {  // keep the fragments live
+#pragma unroll
+      for (int t = 0; t < KT; ++t) acc[t][0] += (float)gf[0][0] + (float)af[0][0][0] + (float)af[1][1][1];
     }
   };
+#undef PT_FENCE
 
   if (nch > 0) {
-    if constexpr (PROJ) {
+    // prologue: dz ring slots of chunks 0 and 1, chunk 0 staged directly, chunk 1 and dz(2) loaded
+    rz = PROJ ? a.dz[(uint32_t)((ldbase(0) + zr) * (int)a.lddz + zqc)] : 0.f;
+    put_z(0);
+    load_z(min(1, clast));
+    put_z(1);
+    load_z(min(2, clast));
 #pragma unroll
-      for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
-      const int mb0 = ldbase(0);
-      const bool ok0 = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg - mb0 && zr < (int)mend - mb0;
-      dzL[0][tid] = ok0 ? a.dz[(int64_t)(mb0 + zr) * a.lddz + zqc] : 0.0f;
+    for (int j = 0; j < PT_NP; ++j) load_a(j, 0);
+    load_g(0);
+    __syncthreads();  // dzL
+#pragma unroll
+    for (int j = 0; j < PT_NP; ++j) put_a(j, 0);
+    z_read(0, 0, 8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      g_row(i, 0, 0);
+      g_row(i, 0, 1);
     }
-    load(0);
-    __syncthreads();  // Ps, dzL[0]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split3_pair(e[2 * j], e[2 * j + 1], w[j][0], w[j][1], w[j][2]);
+    g_put(0);
+#pragma unroll
+    for (int j = 0; j < PT_NP; ++j) load_a(j, min(1, clast));
+    load_g(min(1, clast));
+    __syncthreads();
     for (int c = 0; c < nch; ++c) {
-      store(c);  // buffers of chunk c - 2: last read before barrier c - 1
-      __syncthreads();
-      load(min(c + 1, nch - 1));
-      compute(c);
+      compute(c);       // + staging of chunk c + 1 into the other buffers (read by chunk c - 1:
+      if constexpr (!(LAB & 8)) __syncthreads();  //   retired by the previous barrier)
     }
   }
 

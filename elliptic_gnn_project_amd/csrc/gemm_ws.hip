@@ -79,11 +79,7 @@ constexpr int WS_BIAS = 1, WS_RELU = 2, WS_DROP = 4, WS_PROJ = 8;
 // no epilogue 110, neither 78.5 (the bare MFMA loop at 53 % of its 42 us floor: one wave per SIMD
 // exposes the fragment reads and the two barriers per tile), no MFMAs 89 / 83, L2-hot A 140 / 109
 // (HBM costs ~6 us).  So: MFMA loop 78 + staging ~27 + fused epilogue ~30 (projection, dropout).
-// PLN: A is read from a split image (NTArgs::ap, gemm_planes.hip): every (plane, k-step) block
-// of a tile — [row 32][16 k] bf16, 1 KB — is one 16-byte load per lane (lane l: row l/2, k-half
-// (l & 1) ^ bit 3 of the row, i.e. the buffer's swizzled position 16·l) and one ds_write_b128; no
-// split, no tail copy (rows past M read zeros or the next plane's rows: their C rows are dropped).
-template <int NKS, int EPI, int KS, int LAB = 0, bool PLN = false>
+template <int NKS, int EPI, int KS, int LAB = 0>
 __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const uint4* __restrict__ bimg, int ntiles,
                                                              const float* __restrict__ tail) {
   constexpr int WS_THREADS = 256 * KS;
@@ -91,10 +87,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   constexpr int BUF = 3 * PLB;             // bytes per A buffer
   constexpr int KH0 = (NKS + KS - 1) / KS; // k-steps of the first K part (waves 0-3)
   constexpr int KH = KH0;                  // register slots per wave (the second part has <= KH0)
-  constexpr int QF = (128 * NKS + WS_THREADS - 1) / WS_THREADS;  // staged f32 quads per thread per tile
-  constexpr int QP = (3 * NKS + WS_THREADS / 64 - 1) / (WS_THREADS / 64);  // PLN: 1 KB blocks per wave per tile
-  constexpr int QN = PLN ? QP : QF;                                // staging units per thread per tile
-  static_assert(!PLN || KS == 1, "the planes form runs one wave per SIMD");
+  constexpr int QN = (128 * NKS + WS_THREADS - 1) / WS_THREADS;  // staged quads per thread per tile
   constexpr int RV = 16 / KS;              // accumulator rows (r-slots) a wave finishes
   constexpr bool TWO = (LAB & 16) != 0;    // two independent accumulator chains
   // LDS: two A buffers, the C tile of the epilogue ([32 rows][128] f32: coalesced C stores and
@@ -139,8 +132,8 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   }
 
   // ---- zero the pad columns of both buffers once (k in [k1 + k2, 16·NKS): the staging never
-  //      writes them; B is zero there but LDS garbage could be NaN).  PLN: the image has them.
-  if constexpr (!PLN) {
+  //      writes them; B is zero there but LDS garbage could be NaN)
+  {
     const int npad = NKS * 16 - k1 - k2;
     for (int i = tid; i < 2 * 3 * WS_ROWS * npad; i += WS_THREADS) {
       const int c = i % npad, rest = i / npad;
@@ -153,12 +146,12 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
 
   // ---- per-thread staging map (tile-invariant): quad i -> flat element f = 4q of segment g.
   //      Idle quads (q >= nq) stage zeros into the pad bytes of k-step 0 (never read).
-  uint32_t qoff[QF];               // LDS byte offsets of the quad's two pairs (pair 2 << 16 | pair 1)
-  int32_t qf[QF];                  // flat element offset inside the tile's segment
-  uint32_t qseg2 = 0, qidle = 0;   // bit i: quad i in segment 2 / idle
+  uint32_t qoff[QN];               // LDS byte offsets of the quad's two pairs (pair 2 << 16 | pair 1)
+  int32_t qf[QN];                  // flat element offset inside the tile's segment
+  uint32_t qseg2 = 0;              // bit i: quad i in segment 2
   const int nq1 = 8 * k1, nq = nq1 + 8 * k2;  // quads per tile (32 rows · k / 4)
 #pragma unroll
-  for (int i = 0; i < (PLN ? 0 : QF); ++i) {
+  for (int i = 0; i < QN; ++i) {
     const int q = tid + WS_THREADS * i;
     const bool seg2 = q >= nq1;
     const int kg = seg2 ? k2 : k1;
@@ -171,22 +164,12 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
     qoff[i] = (o1 << 16) | o0;  // PLB < 64 KB
     qf[i] = ok ? f : 0;
     qseg2 |= (ok && seg2) ? (1u << i) : 0u;
-    qidle |= ok ? 0u : (1u << i);
   }
 
   // Staging registers, two sets: the quads of tile t+G are staged from one set during tile t's
   // k-loop, and each quad's registers are refilled with tile t+3G right after (prefetch depth 2:
   // every load has two tiles of MFMAs to land).
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  using StT = std::conditional_t<PLN, u32x4, float4>;
-  StT st[2][QN];
-  // PLN: lane-constant image offset of this lane's piece, block b = wave + 4i of a tile (the last
-  // wave's spare slot repeats the last block: same bytes to the same place)
-  const int prow = lane >> 1;
-  const uint32_t pvoff = (uint32_t)((prow * a.ap_ld + 8 * ((lane & 1) ^ ((prow >> 3) & 1))) * 2);
-  const __amdgpu_buffer_rsrc_t prsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.ap), 0, PLN ? (int)(3 * a.ap_ps * 2) : 0, 0x00020000);
-  auto pblock = [&](int i) { return min(wave + 4 * i, 3 * NKS - 1); };
+  float4 st[2][QN];
   // quad i of tile t into set `sb`: one unconditional 16-byte load (tile starts are 16-byte
   // aligned: 32·k·4 bytes).  The last tile is read from `tail`, a zero-padded copy of its rows
   // made by ws_tail_kernel, and tiles past the end re-read it (never staged into a used
@@ -196,48 +179,32 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   const float* const tail2 = tail + WS_ROWS * k1;
   // the tile's two segment bases, formed once per tile (not per quad: per-quad forms compiled
   // to a scalar branch pair per load inside the MFMA stream)
-  // (PLN: toff = the tile's byte offset inside a plane)
-  auto tile_base = [&](int t, const float*& b1, const float*& b2, int& toff) {
+  auto tile_base = [&](int t, const float*& b1, const float*& b2) {
     const int tc = (LAB & 8) ? blockIdx.x : min(t, ntiles - 1);  // LAB 8: re-read an L2-hot tile
     const bool last = tc == ntiles - 1;
     b1 = last ? tail1 : pa1 + (int64_t)tc * WS_ROWS * k1;
     b2 = last ? tail2 : pa2 + (int64_t)tc * WS_ROWS * k2;
-    toff = tc * WS_ROWS * a.ap_ld * 2;
   };
-  auto load_quad_b = [&](int sb, int i, const float* b1, const float* b2, int toff) {
-    if constexpr (PLN) {
-      const int b = pblock(i), p = b / NKS, s = b - p * NKS;
-      st[sb][i] = __builtin_amdgcn_raw_buffer_load_b128(prsrc, (int)pvoff, (int)((p * a.ap_ps + 16 * s) * 2) + toff, 0);
-    } else {
-      const bool s2 = (qseg2 >> i) & 1u;
-      // idle quads (qf = 0) re-load the tile's first quad and stage it into the never-read pad
-      // bytes; no zeroing (a select on the loaded value made hipcc wait for the load right there)
-      st[sb][i] = *reinterpret_cast<const float4*>((s2 ? b2 : b1) + qf[i]);
-    }
+  auto load_quad_b = [&](int sb, int i, const float* b1, const float* b2) {
+    const bool s2 = (qseg2 >> i) & 1u;
+    // idle quads (qf = 0) re-load the tile's first quad and stage it into the never-read pad
+    // bytes; no zeroing (a select on the loaded value made hipcc wait for the load right there)
+    st[sb][i] = *reinterpret_cast<const float4*>((s2 ? b2 : b1) + qf[i]);
   };
   auto load_quad = [&](int sb, int i, int t) {
     const float *b1, *b2;
-    int toff;
-    tile_base(t, b1, b2, toff);
-    load_quad_b(sb, i, b1, b2, toff);
+    tile_base(t, b1, b2);
+    load_quad_b(sb, i, b1, b2);
   };
   // stage one pair (half a quad: elements 2h, 2h+1) of quad i: split + 3 plane writes
-  // (PLN: the whole 16-byte piece on h == 0, one ds_write_b128)
   auto stage_pair = [&](char* buf, int sb, int i, int h) {
-    if constexpr (PLN) {
-      if (h == 0) {
-        const int b = pblock(i), p = b / NKS, s = b - p * NKS;
-        *reinterpret_cast<u32x4*>(buf + p * PLB + s * WS_KSB + 16 * lane) = st[sb][i];
-      }
-    } else {
-      uint32_t hi, mi, lo;
-      if (h == 0) ws_split(st[sb][i].x, st[sb][i].y, hi, mi, lo);
-      else ws_split(st[sb][i].z, st[sb][i].w, hi, mi, lo);
-      const uint32_t o = h == 0 ? (qoff[i] & 0xffffu) : (qoff[i] >> 16);
-      *reinterpret_cast<uint32_t*>(buf + o) = hi;
-      *reinterpret_cast<uint32_t*>(buf + PLB + o) = mi;
-      *reinterpret_cast<uint32_t*>(buf + 2 * PLB + o) = lo;
-    }
+    uint32_t hi, mi, lo;
+    if (h == 0) ws_split(st[sb][i].x, st[sb][i].y, hi, mi, lo);
+    else ws_split(st[sb][i].z, st[sb][i].w, hi, mi, lo);
+    const uint32_t o = h == 0 ? (qoff[i] & 0xffffu) : (qoff[i] >> 16);
+    *reinterpret_cast<uint32_t*>(buf + o) = hi;
+    *reinterpret_cast<uint32_t*>(buf + PLB + o) = mi;
+    *reinterpret_cast<uint32_t*>(buf + 2 * PLB + o) = lo;
   };
   auto stage_quad = [&](char* buf, int sb, int i) {
     stage_pair(buf, sb, i, 0);
@@ -271,8 +238,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   // MFMAs of this wave's K half from `cur`; the next tile's quads split into `nxt` in between
   auto kloop = [&](const char* cur, char* nxt, int sb, int tload) {
     const float *lb1, *lb2;
-    int ltoff;
-    tile_base(tload, lb1, lb2, ltoff);
+    tile_base(tload, lb1, lb2);
     floatx16 acc, acc2;
     constexpr int SQ0 = KH - QN > 0 ? KH - QN : 0;  // k-steps SQ0.. stage one quad each
     // one fragment set, each plane re-read for step s+1 right after its last use in step s:
@@ -312,7 +278,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       if (mm) ws_mfma<false>(acc, x[1], bw[s][0]);
       WS_FENCE;
       if (s + 1 < KH) x[1] = frag(sn, 1);
-      if (stg) load_quad_b(sb, qi, lb1, lb2, ltoff);
+      if (stg) load_quad_b(sb, qi, lb1, lb2);
       WS_FENCE;
       if (mm) {
         ws_mfma<false>(TWO ? acc2 : acc, x[0], bw[s][2]);
@@ -328,7 +294,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
 #pragma unroll
       for (int i = KH; i < QN; ++i) {
         stage_quad(nxt, sb, i);
-        load_quad_b(sb, i, lb1, lb2, ltoff);
+        load_quad_b(sb, i, lb1, lb2);
       }
     }
     if constexpr ((LAB & 4) != 0) {
@@ -479,6 +445,280 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   }
 }
 
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// ---------------------------------------------------------------- the split-image form (K7a-p)
+// A read from a split image (NTArgs::ap, gemm_planes.hip): every (plane, k-step) block of a
+// tile — [row 32][16 k] bf16 in the buffer layout above, 1 KB — is ONE 16-byte buffer load per
+// lane (lane l: row l/2, k-half (l & 1) ^ bit 3 of the row, i.e. its swizzled position 16·l)
+// and one ds_write_b128: no split, no tail copy (rows past M read zeros or the next plane's rows;
+// their C rows are dropped by the store range check).  4 waves (one per SIMD), each all 21
+// k-steps of its 32 columns (252 AGPRs of B).
+//
+// Software-pipelined epilogue: tile t's MFMA chain (126 per wave) carries, one slot after each
+// MFMA (sched_barrier fences pin the order, so each slot issues in an MFMA's shadow):
+//   slots  0..47  E1 of the previous tile t': bias, ReLU, counter-hash dropout -> LDS C tile
+//   slots 48..59  staging of tile t+G (6 pieces: ds_write_b128, then the refill load of t+2G)
+//   -- barrier (every wave's E1 in the C tile) --
+//   slots 60..84  E2 of t': coalesced C stores from the C tile, projection z = h·Pᵀ
+//   slots 86..105 staging, the other 10 pieces
+//   -- barrier at the end of the tile (A(t+G) published, C tile reads retired) --
+// The last tile's epilogue runs after the loop.  Accumulators alternate between two register
+// sets (two tiles per loop trip: static roles).
+// LAB (timing ablations, csrc/lab/lab_nt.hip only; the library instantiates 0): bit 1 no MFMAs,
+// bit 2 no epilogue slots, bit 4 no staging slots, bit 8 no mid-tile barrier.
+template <int EPI, int LAB = 0>
+__global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uint4* __restrict__ bimg, int ntiles) {
+  constexpr int NKS = 21;
+  constexpr int PLB = NKS * WS_KSB;  // bytes per plane of an A buffer
+  constexpr int BUF = 3 * PLB;
+  constexpr int QP = 16;             // 1 KB blocks per wave per tile (63 real + 1 repeat)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) char A0[BUF];
+  __shared__ __attribute__((aligned(16))) char A1[BUF];
+  __shared__ __attribute__((aligned(16))) float CT[WS_ROWS * BN];
+  constexpr int PLP = BN + 16;  // PL row pitch: the 4 q rows x 4 part chunks of a read hit distinct banks
+  __shared__ __attribute__((aligned(16))) float PL[MAXPROJ * PLP];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int64_t M = a.M;
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+
+  // ---- stationary B: columns 32·wave .. +32, all k-steps, 3 planes
+  bf16x8 bw[NKS][3];
+  {
+    const int slot = 2 * (32 * wave + (lane & 31)) + (lane >> 5);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bw[s][p] = __builtin_bit_cast(bf16x8, bimg[(s * 3 + p) * 256 + slot]);
+  }
+
+  // ---- staging: block b = wave + 4i of a tile, this lane's piece at pvoff
+  const int ld = a.ap_ld;
+  const int prow = lane >> 1;
+  const int pvoff = (prow * ld + 8 * ((lane & 1) ^ ((prow >> 3) & 1))) * 2;
+  const __amdgpu_buffer_rsrc_t prsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.ap), 0, (int)(3 * a.ap_ps * 2), 0x00020000);
+  u32x4 st[QP];
+  auto pblk = [&](int i) { return min(wave + 4 * i, 3 * NKS - 1); };
+  auto load_piece = [&](int i, int t) {
+    const int b = pblk(i), p = b / NKS, s = b - p * NKS;
+    const int tc = min(t, ntiles - 1);
+    st[i] = __builtin_amdgcn_raw_buffer_load_b128(prsrc, pvoff, (int)((p * a.ap_ps + 16 * s) * 2) + tc * WS_ROWS * ld * 2, 0);
+  };
+  auto put_piece = [&](char* buf, int i) {
+    const int b = pblk(i), p = b / NKS, s = b - p * NKS;
+    *reinterpret_cast<u32x4*>(buf + p * PLB + s * WS_KSB + 16 * lane) = st[i];
+  };
+
+  const int frow = lane & 31;
+  const uint32_t foff = (uint32_t)(frow * 32 + (((lane >> 5) ^ ((frow >> 3) & 1)) << 4));
+  const int col = 32 * wave + (lane & 31);
+  const int Nc = a.Nc;
+  const bool colok = col < Nc;
+  const uint32_t hstep = (uint32_t)Nc * kDropGolden;
+  if constexpr ((EPI & WS_PROJ) != 0) {
+    for (int i = tid; i < MAXPROJ * BN; i += 256) {
+      const int q = i / BN, c = i % BN;
+      PL[q * PLP + c] = (q < a.nproj && c < Nc) ? a.proj[(int64_t)q * Nc + c] : 0.f;
+    }
+  }
+  float bv = 0.f;
+  if constexpr ((EPI & WS_BIAS) != 0) bv = colok ? a.bias[col] : 0.f;
+  float* const cptr = a.c;
+  const int64_t ldc = a.ldc;
+  const __amdgpu_buffer_rsrc_t crsrc =
+      __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? (int)(M * ldc * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t zrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(a.z, 0, (EPI & WS_PROJ) != 0 ? (int)(M * a.ldz * 4) : 0, 0x00020000);
+
+  // ---- epilogue pieces of a finished tile tp (tp < 0: none yet; its stores are dropped)
+  float xv[16];
+  auto e1 = [&](const floatx16& acc, int j, int part, int tp) {
+    const int rl = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+    if (part == 0) {
+      float x = acc[j] + bv;
+      if constexpr ((EPI & WS_RELU) != 0) x = fmaxf(x, 0.f);
+      xv[j] = x;
+    } else if (part == 1) {
+      if constexpr ((EPI & WS_DROP) != 0) {  // == keep_elem(seed, row·Nc + col), bit for bit
+        const uint32_t h0 = ((uint32_t)(tp * WS_ROWS + 4 * (lane >> 5)) * (uint32_t)Nc + (uint32_t)col) * kDropGolden +
+                            (uint32_t)seed;
+        xv[j] = keep_premixed(h0 + (uint32_t)(rl - 4 * (lane >> 5)) * hstep, seed, a.keep_thresh) ? xv[j] * a.drop_scale
+                                                                                                  : 0.f;
+      }
+    } else {
+      CT[rl * BN + col] = colok ? xv[j] : 0.f;
+    }
+  };
+  float4 cv[4];
+  float4 ph[2][4];  // projection: two trips of (h_j, p_j, h_j+NP, p_j+NP) in flight
+  float pacc0 = 0.f, pacc1 = 0.f;
+  constexpr int NP = 2;  // parts per projection dot product (256 threads / (32 rows · 4 q))
+  const int ppart = tid % NP, pq = (tid / NP) % MAXPROJ, prl = tid / (NP * MAXPROJ);
+  auto c_read = [&](int i) {
+    const int u = tid + 256 * i;
+    cv[i] = *reinterpret_cast<const float4*>(CT + (u / (BN / 4)) * BN + (u % (BN / 4)) * 4);
+  };
+  auto c_store = [&](int i, int tp) {
+    const int u = tid + 256 * i;
+    const int rl = u / (BN / 4), c4 = (u % (BN / 4)) * 4;
+    const u32x4 xv4 = {__float_as_uint(cv[i].x), __float_as_uint(cv[i].y), __float_as_uint(cv[i].z),
+                       __float_as_uint(cv[i].w)};
+    // columns >= Nc and no tile: an offset past the range (dropped); rows >= M fall past it by themselves
+    const uint32_t off = (c4 < Nc && tp >= 0) ? (uint32_t)((((int64_t)tp * WS_ROWS + rl) * ldc + c4) * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b128(xv4, crsrc, (int)off, 0, 0);
+  };
+  auto p_read = [&](int tt) {  // chunks j = part + 4·tt and j + NP of row prl / projection row pq
+    const float4* hrow = reinterpret_cast<const float4*>(CT + prl * BN);
+    const float4* prw = reinterpret_cast<const float4*>(PL + pq * PLP);
+    const int j = ppart + 2 * NP * tt;
+    ph[tt & 1][0] = hrow[j];
+    ph[tt & 1][1] = prw[j];
+    ph[tt & 1][2] = hrow[j + NP];
+    ph[tt & 1][3] = prw[j + NP];
+  };
+  auto p_fma = [&](int tt) {
+    const float4 h0_ = ph[tt & 1][0], p0 = ph[tt & 1][1], h1_ = ph[tt & 1][2], p1 = ph[tt & 1][3];
+    pacc0 = fmaf(h0_.x, p0.x, pacc0); pacc0 = fmaf(h0_.y, p0.y, pacc0);
+    pacc0 = fmaf(h0_.z, p0.z, pacc0); pacc0 = fmaf(h0_.w, p0.w, pacc0);
+    pacc1 = fmaf(h1_.x, p1.x, pacc1); pacc1 = fmaf(h1_.y, p1.y, pacc1);
+    pacc1 = fmaf(h1_.z, p1.z, pacc1); pacc1 = fmaf(h1_.w, p1.w, pacc1);
+  };
+  auto p_done = [&](int tp) {
+    float zsum = pacc0 + pacc1;
+    zsum += __shfl_xor(zsum, 1);
+    pacc0 = pacc1 = 0.f;
+    const int64_t row = (int64_t)tp * WS_ROWS + prl;
+    const uint32_t zoff = (ppart == 0 && pq < a.nproj && tp >= 0) ? (uint32_t)((row * a.ldz + pq) * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zsum), zrsrc, (int)zoff, 0, 0);
+  };
+  constexpr int PTRIPS = BN / 4 / (2 * NP);  // 8
+  // E2 slot q (0..24): C reads 0-3, C stores 4-7, projection R0 R1 F0 R2 F1 ... R7 F6 F7, done
+  auto e2 = [&](int q, int tp) {
+    if (q < 4) c_read(q);
+    else if (q < 8) c_store(q - 4, tp);
+    else if constexpr ((EPI & WS_PROJ) != 0) {
+      const int k = q - 8;  // 0..16
+      if (k == 0) p_read(0);
+      else if (k < 2 * PTRIPS - 1) {
+        if (k & 1) p_read((k + 1) / 2);
+        else p_fma(k / 2 - 1);
+      } else if (k == 2 * PTRIPS - 1) {
+        p_fma(PTRIPS - 2);
+      } else if (k == 2 * PTRIPS) {
+        p_fma(PTRIPS - 1);
+      } else if (k == 2 * PTRIPS + 1) {
+        p_done(tp);
+      }
+    }
+  };
+
+  // one slot of tile t's chain: staging of tile t+G into nxt, epilogue of tile tp from accp
+  auto slot = [&](int k, char* nxt, const floatx16& accp, int tp, int t) {
+    if (k < 48) {
+      if constexpr (!(LAB & 2)) e1(accp, k / 3, k % 3, tp);
+    } else if (k < 60 || (k >= 86 && k < 106)) {
+      if constexpr (!(LAB & 4)) {
+        const int i = k < 60 ? (k - 48) / 2 : 6 + (k - 86) / 2;
+        if (k & 1) load_piece(i, t + 2 * (int)gridDim.x);
+        else put_piece(nxt, i);
+      }
+    } else if (k < 86) {
+      if constexpr (!(LAB & 2)) e2(k - 60, tp);
+    }
+  };
+#define NTP_FENCE __builtin_amdgcn_sched_barrier(0)
+  auto kloop = [&](const char* cur, char* nxt, floatx16& acc, const floatx16& accp, int t, int tp) {
+    // fragments: plane 2 re-read for step s+1 after its last use (MFMA 0), plane 1 after MFMA 2,
+    // plane 0 after MFMA 5 (the products run small terms first)
+    bf16x8 x[3];
+    auto frag = [&](int s, int p) { return *reinterpret_cast<const bf16x8*>(cur + p * PLB + s * WS_KSB + foff); };
+#pragma unroll
+    for (int p = 0; p < 3; ++p) x[p] = frag(0, p);
+    constexpr int fa[6] = {2, 1, 1, 0, 0, 0}, fb[6] = {0, 1, 0, 2, 1, 0};
+    // (static_for: a #pragma unroll of this 126-slot body was refused, leaving bw / st indexed
+    // dynamically, i.e. in scratch)
+    static_for<NKS>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      static_for<6>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        NTP_FENCE;
+        if constexpr (!(LAB & 1)) {
+          if constexpr (s == 0 && m == 0) ws_mfma<true>(acc, x[fa[m]], bw[s][fb[m]]);
+          else ws_mfma<false>(acc, x[fa[m]], bw[s][fb[m]]);
+        }
+        NTP_FENCE;
+        if constexpr (s + 1 < NKS) {
+          if constexpr (m == 0) x[2] = frag(s + 1, 2);
+          if constexpr (m == 2) x[1] = frag(s + 1, 1);
+          if constexpr (m == 5) x[0] = frag(s + 1, 0);
+        }
+        slot(6 * s + m, nxt, accp, tp, t);
+        if constexpr (6 * s + m == 59 && !(LAB & 8)) __syncthreads();  // every wave's E1 is in the C tile
+      });
+    });
+    NTP_FENCE;
+    if constexpr ((LAB & 1) != 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = x[0][r & 7];
+    }
+    ws_mfma_end(acc);
+  };
+#undef NTP_FENCE
+  auto finish = [&](const floatx16& acc, int tp) {  // the last tile's epilogue, not interleaved
+#pragma unroll
+    for (int k = 0; k < 48; ++k) e1(acc, k / 3, k % 3, tp);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 25; ++q) e2(q, tp);
+  };
+
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  const int G = gridDim.x;
+  // prologue: tile t staged into A0, tile t+G loaded
+#pragma unroll
+  for (int i = 0; i < QP; ++i) load_piece(i, t);
+#pragma unroll
+  for (int i = 0; i < QP; ++i) put_piece(A0, i);
+#pragma unroll
+  for (int i = 0; i < QP; ++i) load_piece(i, t + G);
+  floatx16 accA, accB;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) accA[r] = accB[r] = 0.f;
+  __syncthreads();
+  int tp = -1;
+  while (true) {
+    kloop(A0, A1, accA, accB, t, tp);  // stages t+G into A1; epilogue of tp from accB
+    __syncthreads();
+    tp = t;
+    t += G;
+    if (t >= ntiles) {
+      finish(accA, tp);
+      break;
+    }
+    kloop(A1, A0, accB, accA, t, tp);
+    __syncthreads();
+    tp = t;
+    t += G;
+    if (t >= ntiles) {
+      finish(accB, tp);
+      break;
+    }
+  }
+}
+
 int ws_num_cus() {
   static int cus = 0;
   if (!cus) {
@@ -536,12 +776,12 @@ __global__ __launch_bounds__(256) void ws_prep_kernel(NTArgs a, uint4* __restric
   else ws_tail_block(a, tail, r0, blockIdx.x - nchunks);
 }
 
-template <int NKS, int KS, int LAB = 0, bool PLN = false>
+template <int NKS, int KS, int LAB = 0>
 void launch_ws_k(const NTArgs& a, const uint4* bimg, const float* tail, hipStream_t st) {
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
   const int grid = std::min(ntiles, ws_num_cus());
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
-#define GNN_WS(E) gemm_nt_ws_kernel<NKS, E, KS, LAB, PLN><<<grid, 256 * KS, 0, st>>>(a, bimg, ntiles, tail)
+#define GNN_WS(E) gemm_nt_ws_kernel<NKS, E, KS, LAB><<<grid, 256 * KS, 0, st>>>(a, bimg, ntiles, tail)
   if (proj && drop) GNN_WS(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
   else if (proj) GNN_WS(WS_BIAS | WS_RELU | WS_PROJ);
   else if (drop) GNN_WS(WS_BIAS | WS_RELU | WS_DROP);
@@ -616,8 +856,8 @@ void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks) {
 
 namespace gnnmp {
 
-// The split-image form (PLN): f32 C, the w1/w2 B form, A from NTArgs::ap with a 336-wide image
-// row (21 k-steps: the SAGE layer-1 [agg | x] of 166 + 166 features, each padded to 168),
+// The split-image form: f32 C, the w1/w2 B form, A from NTArgs::ap with a 336-wide image row
+// (21 k-steps: the SAGE layer-1 [agg | x] of 166 + 166 features, each padded to 168),
 // 64 < N <= 128, M >= 32, the nt_ws_ok epilogues.
 bool nt_planes_ok(const NTArgs& a) {
   if (!a.ap || a.a_bf16 || a.c_bf16 || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc <= 64) return false;
@@ -636,7 +876,17 @@ bool nt_planes_ok(const NTArgs& a) {
 void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st) {
   const int nks = a.ap_ld / 16;
   ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // the B image only
-  launch_ws_k<21, 1, 0, true>(a, img, nullptr, st);
+  const int ntiles = (int)ceil_div(a.M, WS_ROWS);
+  const int grid = std::min(ntiles, ws_num_cus());
+  const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
+#define GNN_WSP(E) gemm_nt_planes_kernel<E><<<grid, 256, 0, st>>>(a, img, ntiles)
+  if (proj && drop) GNN_WSP(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
+  else if (proj) GNN_WSP(WS_BIAS | WS_RELU | WS_PROJ);
+  else if (drop) GNN_WSP(WS_BIAS | WS_RELU | WS_DROP);
+  else if (relu) GNN_WSP(WS_BIAS | WS_RELU);
+  else if (bias) GNN_WSP(WS_BIAS);
+  else GNN_WSP(0);
+#undef GNN_WSP
 }
 
 }  // namespace gnnmp
