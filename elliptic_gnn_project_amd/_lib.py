@@ -172,6 +172,7 @@ class GnnAdamGroup(ctypes.Structure):
         ("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double), ("eps", ctypes.c_double),
         ("weight_decay", ctypes.c_double), ("max_norm", ctypes.c_double),
         ("tensors", GnnAdamTensor * ADAM_MAX_TENSORS),
+        ("skip_nonfinite", c_i32),
     ]
 
 

@@ -468,7 +468,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 //   slots  0..47  E1 of the previous tile t': bias, ReLU, counter-hash dropout -> LDS C tile
 //   slots 48..59  staging of tile t+G (6 pieces: ds_write_b128, then the refill load of t+2G)
 //   -- barrier (every wave's E1 in the C tile) --
-//   slots 60..84  E2 of t': coalesced C stores from the C tile, projection z = h·Pᵀ
+//   slots 60..84  E2 of t': coalesced C stores from the C tile, projection z = h·Pᵀ (NE2 = 25)
 //   slots 86..105 staging, the other 10 pieces
 //   -- barrier at the end of the tile (A(t+G) published, C tile reads retired) --
 // The last tile's epilogue runs after the loop.  Accumulators alternate between two register
@@ -604,21 +604,21 @@ __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uin
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zsum), zrsrc, (int)zoff, 0, 0);
   };
   constexpr int PTRIPS = BN / 4 / (2 * NP);  // 8
-  // E2 slot q (0..24): C reads 0-3, C stores 4-7, projection R0 R1 F0 R2 F1 ... R7 F6 F7, done
+  // E2 slot q (0..24): C reads 0-3, C stores 4-7, then the projection R0 R1 F0 R2 F1 ... R7 F6
+  // F7 done (trip tt's reads two slots ahead of its FMAs)
+  constexpr int NE2 = 8 + 2 * PTRIPS + 1;
   auto e2 = [&](int q, int tp) {
     if (q < 4) c_read(q);
     else if (q < 8) c_store(q - 4, tp);
     else if constexpr ((EPI & WS_PROJ) != 0) {
-      const int k = q - 8;  // 0..16
+      const int k = q - 8;  // 0 .. 2·PTRIPS
       if (k == 0) p_read(0);
-      else if (k < 2 * PTRIPS - 1) {
+      else if (k < 2 * PTRIPS - 1) {  // 1 .. 14: R(k+1)/2 on odd k, F(k/2 - 1) on even k
         if (k & 1) p_read((k + 1) / 2);
         else p_fma(k / 2 - 1);
       } else if (k == 2 * PTRIPS - 1) {
-        p_fma(PTRIPS - 2);
-      } else if (k == 2 * PTRIPS) {
         p_fma(PTRIPS - 1);
-      } else if (k == 2 * PTRIPS + 1) {
+      } else if (k == 2 * PTRIPS) {
         p_done(tp);
       }
     }
@@ -634,7 +634,7 @@ __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uin
         if (k & 1) load_piece(i, t + 2 * (int)gridDim.x);
         else put_piece(nxt, i);
       }
-    } else if (k < 86) {
+    } else if (k < 60 + NE2) {
       if constexpr (!(LAB & 2)) e2(k - 60, tp);
     }
   };
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uin
     for (int k = 0; k < 48; ++k) e1(acc, k / 3, k % 3, tp);
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 25; ++q) e2(q, tp);
+    for (int q = 0; q < NE2; ++q) e2(q, tp);
   };
 
   int t = blockIdx.x;

@@ -7,6 +7,7 @@
 #include "../gemm_ws.hip"
 
 #include <algorithm>
+#include <cstring>
 #include <cstdio>
 #include <random>
 #include <vector>
@@ -36,6 +37,57 @@ static float* dev_rand(size_t n, float scale, unsigned seed) {
 }
 
 using namespace gnnmp;
+
+// MFMA issue microbenchmark: one wave per SIMD (256 x 256 threads), 24·iters
+// v_mfma_f32_32x32x16_bf16 per wave on random data, as NCH interleaved accumulator chains;
+// shader clocks (s_memtime) and 100 MHz ticks (s_memrealtime) of wave 0 of block 0.
+template <int NCH>
+__global__ __launch_bounds__(256) void mfma_chain_kernel(const uint4* in, float* out, int iters,
+                                                         unsigned long long* clk) {
+  const bf16x8 x = __builtin_bit_cast(bf16x8, in[threadIdx.x]);
+  const bf16x8 y = __builtin_bit_cast(bf16x8, in[256 + threadIdx.x]);
+  floatx16 acc[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 24 / NCH; ++k)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, acc[c], 0, 0, 0);
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) s += acc[c][0] + acc[c][15];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    clk[0] = t1 - t0;
+    clk[1] = r1 - r0;
+  }
+}
+
+template <int NCH>
+void mfma_probe(const uint4* in, float* out, unsigned long long* clk) {
+  const int iters = 2000;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  mfma_chain_kernel<NCH><<<256, 256>>>(in, out, iters, clk);
+  CK(hipEventRecord(e0));
+  mfma_chain_kernel<NCH><<<256, 256>>>(in, out, iters, clk);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long h[2];
+  CK(hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost));
+  const double n = 24.0 * iters;
+  std::printf("MFMA chains=%d: %.1f us, %.1f shader cycles / MFMA, clock %.2f GHz, %.0f TF/s bf16\n", NCH,
+              ms * 1e3, h[0] / n, h[0] / (h[1] * 10.0), n * 1024 * 32768.0 / (ms * 1e-3) / 1e12);
+}
 
 template <int LAB>
 void tn(const TNArgs& a, const NTArgs&, const uint4*, int nblk, int) {
@@ -89,6 +141,28 @@ int main(int argc, char** argv) {
       {"NT production", nt<0>, {}}, {"NT no MFMA", nt<1>, {}}, {"NT no epilogue", nt<2>, {}},
       {"NT no staging", nt<4>, {}}, {"NT no mid barrier", nt<8>, {}}, {"NT MFMA+frags only", nt<2 | 4 | 8>, {}},
       {"NT epilogue only", nt<1 | 4>, {}}};
+  {
+    std::vector<uint16_t> hb(512 * 8);  // random bf16 operands (truncated normal floats: no NaN)
+    std::mt19937 g(9);
+    std::normal_distribution<float> d(0.f, 1.f);
+    for (auto& v : hb) {
+      const float f = d(g);
+      uint32_t u;
+      std::memcpy(&u, &f, 4);
+      v = (uint16_t)(u >> 16);
+    }
+    uint4* in;
+    CK(hipMalloc(&in, hb.size() * 2));
+    CK(hipMemcpy(in, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+    float* out;
+    unsigned long long* clk;
+    CK(hipMalloc(&out, 256 * 256 * 4));
+    CK(hipMalloc(&clk, 16));
+    mfma_probe<1>(in, out, clk);
+    mfma_probe<2>(in, out, clk);
+    mfma_probe<4>(in, out, clk);
+    mfma_probe<1>(in, out, clk);
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

@@ -95,9 +95,11 @@ struct AdamTable {
   int64_t off[GNN_ADAM_MAX_TENSORS + 1];  // element offsets of the flattened parameter list
 };
 
-// Σ g² over this block's slice of the flattened gradients; block 0 also advances the step.
+// Σ g² over this block's slice of the flattened gradients; block 0 also keeps the step count
+// before this call in partial[kAdamBlocks] (clip_adam_kernel advances step[0] once it knows the
+// step is taken: no block reads step[0] while another may write it).
 __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, float* __restrict__ partial,
-                                                                float* __restrict__ step) {
+                                                                const float* __restrict__ step) {
   __shared__ float sh[kAdamThreads / 64];
   const int64_t total = tb.off[tb.n];
   const int64_t per = (total + gridDim.x - 1) / gridDim.x;
@@ -112,33 +114,42 @@ __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, flo
   const float t = block_sum(s, sh);
   if (threadIdx.x == 0) {
     partial[blockIdx.x] = t;
-    if (blockIdx.x == 0) step[0] += 1.0f;
+    if (blockIdx.x == 0) partial[kAdamBlocks] = step[0];
   }
 }
 
 // Mirrors torch.optim.Adam's default (foreach, non-capturable) update: bias corrections and
 // 1 - beta in double, as the Python scalars are; m.lerp_(g, 1 - b1); v = v·b2 + (1 - b2)·g·g;
 // p += -lr/bc1 · m / (sqrt(v)/sqrt(bc2) + eps).
+// skip_nonfinite (torch.amp.GradScaler.step's found_inf): a non-finite Σg² leaves parameters,
+// moments, gradients and the step count untouched.
 __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, const float* __restrict__ partial,
-                                                                  int nblk, const float* __restrict__ step,
+                                                                  int nblk, float* __restrict__ step,
                                                                   double max_norm, double lr, double beta1,
                                                                   double beta2, double eps, double wd,
-                                                                  float* __restrict__ norm_out) {
+                                                                  float* __restrict__ norm_out, int skip_nonfinite) {
   __shared__ float coef_sh;
+  __shared__ int skip_sh;
   if (threadIdx.x < 64) {  // the nblk <= 64 partials: one per lane, fixed butterfly (same in every block)
     float tot = threadIdx.x < nblk ? partial[threadIdx.x] : 0.f;
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
     const float norm = sqrtf(tot);
     float coef = 1.0f;
     if (max_norm > 0.0) coef = fminf((float)max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
+    const bool skip = skip_nonfinite && !isfinite(tot);
     if (threadIdx.x == 0) {
       coef_sh = coef;
-      if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+      skip_sh = skip;
+      if (blockIdx.x == 0) {
+        if (norm_out) norm_out[0] = norm;
+        step[0] = partial[nblk] + (skip ? 0.0f : 1.0f);
+      }
     }
   }
   __syncthreads();
+  if (skip_sh) return;  // block-uniform
   const float coef = coef_sh;
-  const double t = (double)step[0];
+  const double t = (double)partial[nblk] + 1.0;
   const double bc1 = 1.0 - pow(beta1, t), bc2 = 1.0 - pow(beta2, t);
   const float neg_step = (float)(-lr / bc1), bc2s = (float)sqrt(bc2);
   const float b2 = (float)beta2, omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
@@ -200,7 +211,7 @@ extern "C" gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logit
 
 extern "C" gnn_status gnn_clip_adam_workspace_size(size_t* bytes) {
   if (!bytes) return fail(GNN_ERR_INVALID_ARG, __func__, "null");
-  *bytes = kAdamBlocks * sizeof(float);
+  *bytes = (kAdamBlocks + 1) * sizeof(float);
   return GNN_OK;
 }
 
@@ -208,7 +219,7 @@ extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, 
                                         size_t workspace_bytes, gnn_stream_t stream) {
   if (!grp || !step || grp->num_tensors < 0 || grp->num_tensors > GNN_ADAM_MAX_TENSORS)
     return fail(GNN_ERR_INVALID_ARG, __func__, "bad group");
-  if (!workspace || workspace_bytes < kAdamBlocks * sizeof(float))
+  if (!workspace || workspace_bytes < (kAdamBlocks + 1) * sizeof(float))
     return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
   AdamTable tb{};
   tb.n = grp->num_tensors;
@@ -225,7 +236,8 @@ extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, 
   grad_sq_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, step);
   GNN_LAUNCH_CHECK();
   clip_adam_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, kAdamBlocks, step, grp->max_norm, grp->lr,
-                                                         grp->beta1, grp->beta2, grp->eps, grp->weight_decay, norm_out);
+                                                         grp->beta1, grp->beta2, grp->eps, grp->weight_decay, norm_out,
+                                                         grp->skip_nonfinite);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }

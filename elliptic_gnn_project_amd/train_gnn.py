@@ -161,17 +161,34 @@ def _clips_itself(optimizer) -> bool:
     return isinstance(optimizer, ClipAdam) and bool(optimizer.max_norm)
 
 
+def amp_is_exact(model) -> bool:
+    """True when the model's whole training forward runs as one fp32 libgnnmp autograd node (fused
+    SAGENet / GCNNet): autocast changes nothing inside it (custom_fwd casts to fp32), and
+    GradScaler's power-of-two scale and unscale are exact on its fp32 gradients, so the reference's
+    AMP step (src/train_gnn.py:192-207) equals the unscaled step except for GradScaler's skip of a
+    non-finite update — which ClipAdam(skip_nonfinite) reproduces."""
+    from . import fused
+    from .gnn import GCNNet, SAGENet
+
+    if isinstance(model, SAGENet):
+        return model.fused and fused.fusable(model)
+    if isinstance(model, GCNNet):
+        return model.fused and fused.gcn_fusable(model)
+    return False
+
+
 def make_optimizer(model, cfg: Dict, device, use_amp: bool):
-    """Adam(lr, weight_decay) (src/train_gnn.py:357).  On the GPU without AMP: ClipAdam, the
-    fused clip_grad_norm_(grad_clip) + Adam step (train_ops.py), when one launch pair covers the
-    parameters (≤ ADAM_MAX_TENSORS tensors); otherwise torch.optim.Adam (train_epoch then clips
-    with clip_grad_norm_ as the reference does)."""
-    if device.type == "cuda" and not use_amp:
+    """Adam(lr, weight_decay) (src/train_gnn.py:357).  On the GPU: ClipAdam, the fused
+    clip_grad_norm_(grad_clip) + Adam step (train_ops.py), when one launch pair covers the
+    parameters (≤ ADAM_MAX_TENSORS tensors) and, under AMP, when the AMP step is exact on the
+    model (amp_is_exact: ClipAdam then also takes GradScaler's skip of a non-finite update);
+    otherwise torch.optim.Adam (train_epoch then clips with clip_grad_norm_ as the reference does)."""
+    if device.type == "cuda" and (not use_amp or amp_is_exact(model)):
         from .train_ops import ClipAdam
         if ClipAdam.supports(model.parameters()):
             clip = cfg.get("grad_clip", 0)
             return ClipAdam(model.parameters(), lr=cfg["lr"], weight_decay=cfg["weight_decay"],
-                            max_norm=float(clip) if clip and clip > 0 else None)
+                            max_norm=float(clip) if clip and clip > 0 else None, skip_nonfinite=use_amp)
     return torch.optim.Adam(model.parameters(), lr=cfg["lr"], weight_decay=cfg["weight_decay"])
 
 
@@ -187,15 +204,19 @@ def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cf
     optimizer.zero_grad(set_to_none=bucket is None)
     if denom is None:
         denom = getattr(data, "n_train", None)
+    # AMP on an fp32 libgnnmp model (amp_is_exact): the fused step, GradScaler's scale / unscale
+    # left out (exact on fp32 gradients) and its skip of a non-finite update done by ClipAdam
+    amp_fused = use_amp and getattr(optimizer, "skip_nonfinite", False)
     with _autocast(device, use_amp):
         logits = model(data.x, edge_index, data.timestep if _model_uses_time_embed(model) else None)
         t_idx = _rows(data.timestep, data, "train") if cfg.get("time_loss_weighting", "none") != "none" else None
-        if getattr(loss_fn, "plain", False) and logits.is_cuda and not use_amp:
+        if (getattr(loss_fn, "plain", False) and logits.is_cuda and logits.dtype == torch.float32
+                and (not use_amp or amp_fused)):
             loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
         else:
             loss = loss_fn(_rows(logits, data, "train"), _rows(data.y, data, "train"), t_idx,
                            denom=denom if bucket is not None else None)
-    if scaler.is_enabled() or not loss.is_cuda:
+    if (scaler.is_enabled() and not amp_fused) or not loss.is_cuda:
         scaler.scale(loss).backward()
     else:  # = loss.backward(): a persistent unit gradient (no fill kernel; the fused CE skips `* g`)
         from .train_ops import unit_gradient
@@ -206,8 +227,11 @@ def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cf
     if cfg.get("grad_clip", 0) and cfg["grad_clip"] > 0 and not _clips_itself(optimizer):
         scaler.unscale_(optimizer)
         torch.nn.utils.clip_grad_norm_(model.parameters(), cfg["grad_clip"])
-    scaler.step(optimizer)
-    scaler.update()
+    if amp_fused:
+        optimizer.step()
+    else:
+        scaler.step(optimizer)
+        scaler.update()
     optimizer.zero_grad(set_to_none=bucket is None)
     if bucket is not None:
         loss = loss.detach().clone()
@@ -481,7 +505,7 @@ def main(cfg: Dict) -> Dict:
     if use_mini_batch and dist is not None:
         raise NotImplementedError("mini_batch with world_size > 1: the reference's NeighborLoader path is "
                                   "single-device (src/train_gnn.py:329-348)")
-    use_amp = bool(cfg.get("amp", True))
+    use_amp = device.type == "cuda" and bool(cfg.get("amp", True))  # src/train_gnn.py:291
     scaler = torch.amp.GradScaler(device=device.type, enabled=use_amp)
 
     full = prepare_inputs(load_data(cfg), cfg)  # host: masks window, time scalar, symmetrize

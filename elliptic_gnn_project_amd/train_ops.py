@@ -102,8 +102,11 @@ class ClipAdam(torch.optim.Optimizer):
     """
 
     def __init__(self, params: Iterable, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-                 max_norm: float | None = 1.0):
+                 max_norm: float | None = 1.0, skip_nonfinite: bool = False):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        # skip_nonfinite: GradScaler.step's skip of an update whose gradients hold inf / NaN (the
+        # AMP configurations, src/train_gnn.py:202-207; train_gnn.train_epoch)
+        self.skip_nonfinite = bool(skip_nonfinite)
         if max_norm and len(self.param_groups) > 1:
             raise ValueError("ClipAdam clips over one parameter group (as clip_grad_norm_ over model.parameters())")
         self.max_norm = max_norm
@@ -131,7 +134,7 @@ class ClipAdam(torch.optim.Optimizer):
             # the ctypes argument block is rebuilt only when a pointer or a hyper-parameter changed
             # (the caching allocator usually hands every step's grads the same addresses)
             key = (tuple(p.grad.data_ptr() for p in ps), tuple(p.data_ptr() for p in ps), group["lr"],
-                   group["betas"], group["eps"], group["weight_decay"], self.max_norm)
+                   group["betas"], group["eps"], group["weight_decay"], self.max_norm, self.skip_nonfinite)
             cached = self._groups.get(gi)
             if cached is None or cached[0] != key:
                 cached = (key, self._build(group, ps))
@@ -156,6 +159,7 @@ class ClipAdam(torch.optim.Optimizer):
         grp.lr, (grp.beta1, grp.beta2) = group["lr"], group["betas"]
         grp.eps, grp.weight_decay = group["eps"], group["weight_decay"]
         grp.max_norm = float(self.max_norm) if self.max_norm else 0.0
+        grp.skip_nonfinite = int(self.skip_nonfinite)
         for j, p in enumerate(ps):
             st = self.state[p]
             if not st:

@@ -441,6 +441,8 @@ typedef struct {
   int32_t num_tensors;
   double lr, beta1, beta2, eps, weight_decay, max_norm;  /* double, as torch's Python scalars */
   gnn_adam_tensor tensors[GNN_ADAM_MAX_TENSORS];
+  int32_t skip_nonfinite;  /* != 0: torch.amp.GradScaler.step semantics — a non-finite gradient norm
+                              skips the update (params, moments, grads and step count untouched) */
 } gnn_adam_group;
 gnn_status gnn_clip_adam_workspace_size(size_t* bytes);
 gnn_status gnn_clip_adam_f32(const gnn_adam_group* group, float* step, float* norm_out, void* workspace,

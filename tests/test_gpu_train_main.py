@@ -75,3 +75,71 @@ def test_make_optimizer_many_tensors_falls_back(device):
     assert not isinstance(opt, ClipAdam)
     small = build_model("sage", 20, dict(hidden_dim=16, layers=2, dropout=0.1)).to(device)
     assert isinstance(make_optimizer(small, dict(cfg), device, use_amp=False), ClipAdam)
+
+
+def test_amp_config_runs_the_fused_step(device, tmp_path, monkeypatch):
+    """configs/sage.yaml keeps the reference's amp: true (src/train_gnn.py:291-292).  On the fp32
+    fused SAGENet that is the fused step (ClipAdam with GradScaler's non-finite skip, the fused
+    masked CE) and it trains exactly as amp: false: identical losses and best weights after 3 epochs."""
+    from pathlib import Path
+
+    import yaml
+
+    from elliptic_gnn_project_amd import train_gnn, train_ops
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+
+    base = yaml.safe_load((Path(__file__).resolve().parents[1] / "configs" / "sage.yaml").read_text())
+    assert base["amp"] is True
+    opts, ce_calls = {}, []
+    make = train_gnn.make_optimizer
+    ce = train_ops.masked_cross_entropy
+
+    def spy_make(model, cfg, dev, use_amp):
+        opts[use_amp] = make(model, cfg, dev, use_amp)
+        return opts[use_amp]
+
+    def spy_ce(*a, **k):
+        ce_calls.append(1)
+        return ce(*a, **k)
+
+    monkeypatch.setattr(train_gnn, "make_optimizer", spy_make)
+    monkeypatch.setattr(train_ops, "masked_cross_entropy", spy_ce)
+    res = {}
+    for amp in (True, False):
+        cfg = dict(base, amp=amp, run_name=f"amp_{amp}", output_root=str(tmp_path), max_epochs=3, patience=10,
+                   processed_dir=str(tmp_path / "none"), synthetic=dict(num_nodes=6000, num_edges=9000, seed=3))
+        n0 = len(ce_calls)
+        train_gnn.main(cfg)
+        assert len(ce_calls) - n0 == 3, "the fused masked CE ran every epoch"
+        out = tmp_path / "gnn" / cfg["run_name"]
+        res[amp] = ((out / "training_log.csv").read_text(), torch.load(out / "best.ckpt", weights_only=True))
+    assert isinstance(opts[True], ClipAdam) and opts[True].skip_nonfinite
+    assert isinstance(opts[False], ClipAdam) and not opts[False].skip_nonfinite
+    assert res[True][0] == res[False][0]
+    for k, v in res[True][1].items():
+        assert torch.equal(v, res[False][1][k]), k
+
+
+def test_clip_adam_skips_nonfinite_update(device):
+    """GradScaler.step semantics of ClipAdam(skip_nonfinite): an inf gradient leaves parameters,
+    moments and the step count untouched; the next finite step proceeds as step 1."""
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+
+    torch.manual_seed(0)
+    p = torch.nn.Parameter(torch.randn(100, device=device))
+    q = torch.nn.Parameter(p.detach().clone())
+    a = ClipAdam([p], lr=0.01, max_norm=1.0, skip_nonfinite=True)
+    b = ClipAdam([q], lr=0.01, max_norm=1.0)
+    g = torch.randn(100, device=device)
+    p.grad = g.clone()
+    p.grad[7] = float("inf")
+    before = p.detach().clone()
+    a.step()
+    torch.cuda.synchronize()
+    assert torch.equal(p.detach(), before) and float(a.param_groups[0]["step_t"]) == 0.0
+    p.grad = g.clone()
+    q.grad = g.clone()
+    a.step()
+    b.step()
+    assert torch.equal(p.detach(), q.detach())
+    assert float(a.param_groups[0]["step_t"]) == 1.0
