@@ -162,21 +162,21 @@ struct TNArgs {
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,
 // defined in gemm_x3.hip.  Only the w1/w2 (in-place Linear weight) B form runs split.
-void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipStream_t st);
+void launch_nt_x3(const NTArgs& a, void* ws, size_t ws_bytes, hipStream_t st);
 size_t nt_x3_workspace(int64_t k1, int64_t k2);
-void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant = 0);  // NPL = 3, or 1 when a_bf16
+void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st);  // NPL = 3, or 1 when a_bf16
 
 // weight-stationary persistent split-bf16 NT (gemm_ws.hip): B fragments resident in registers,
 // one block per CU sweeping 32-row tiles.  nt_ws_ok: the shapes/epilogues it takes.  `img`: at
 // least nt_x3_workspace(k1, k2) bytes of workspace for its pre-split B image (concatenated K).
 bool nt_ws_ok(const NTArgs& a);
 size_t nt_ws_tail_offset(int64_t k1, int64_t k2);
-void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks = 0);
+void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st);
 // the split-image forms (gemm_ws.hip NT, gemm_planes.hip TN): shapes they take, launchers
 bool nt_planes_ok(const NTArgs& a);
 void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st);
 bool tn_planes_ok(const TNArgs& a);
-void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st, int variant = 0);
+void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st);
 // 3 planes of one f32 split: hi = RNE(v), mid = RNE(v - hi), lo = RNE(v - hi - mid), exact sum
 __device__ __forceinline__ void split3_pair(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
   typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));

@@ -462,18 +462,11 @@ void launch_nt2_b(const NTArgs& a, hipStream_t st) {
   else launch_nt2<AVEC, 1, KC, true, EXP, DEPTH>(a, st);
 }
 
-// Variant table (tuning harness csrc/bench_gemm.hip); variant 0 is the production choice.
+// The exact-f32 NT: 16-deep chunks, one chunk of loads in flight (r01 lab, the fastest of the
+// [k][n]-image, 32-deep-chunk and two-chunks-in-flight forms).
 template <int AVEC>
-void launch_nt_variant(const NTArgs& a, int variant, hipStream_t st) {
-  switch (variant) {
-    case 1: launch_nt<AVEC, 16, 1, false>(a, st); break;     // r01 kernel: b32 fragment reads, [k][n] B image
-    case 2: launch_nt2_b<AVEC, 32>(a, st); break;            // 32-deep chunks (LDS: 2 blocks/CU)
-    case 3: launch_nt2_b<AVEC, 16, 0, 2>(a, st); break;      // two chunks of loads in flight
-    case 4: launch_nt2_b<AVEC, 16, 1>(a, st); break;         // ablation: no staging (MFMAs + LDS reads + barriers)
-    case 5: launch_nt2_b<AVEC, 16, 6>(a, st); break;         // ablation: global loads, no LDS stores
-    case 6: launch_nt2_b<AVEC, 16, 7>(a, st); break;         // ablation: LDS stores, no global loads
-    default: launch_nt2_b<AVEC, 16>(a, st); break;           // production (r01 lab: fastest)
-  }
+void launch_nt_f32(const NTArgs& a, hipStream_t st) {
+  launch_nt2_b<AVEC, 16>(a, st);
 }
 
 // ------------------------------------------------------------------------------------ TN
@@ -747,7 +740,7 @@ int tn_blocks(int64_t M) {
 
 using namespace gnnmp;
 
-static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn_stream_t stream, const char* fn) {
+static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t stream, const char* fn) {
   if (!p) return fail(GNN_ERR_INVALID_ARG, fn, "null params");
   const bool planes_only = p->a_planes && !p->a1;  // A given only as a split image
   if (p->M < 0 || p->N < 1 || p->k1 < 1 || p->k2 < 0 || (!p->a1 && !p->a_planes) ||
@@ -802,7 +795,7 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
     a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
     a.ap_ps = p->planes_stride;
     const size_t img_bytes = (size_t)(a.ap_ld / 16) * 3 * 256 * sizeof(uint4);
-    if (p->math != GNN_MATH_F32 && variant == 0 && !p->mask && nt_planes_ok(a) && p->workspace &&
+    if (p->math != GNN_MATH_F32 && !p->mask && nt_planes_ok(a) && p->workspace &&
         p->workspace_bytes >= img_bytes) {
       launch_nt_ws_planes(a, static_cast<uint4*>(p->workspace), st);
       return hip_check(hipGetLastError(), fn);
@@ -810,22 +803,21 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, int variant, gnn
     if (planes_only) return fail(GNN_ERR_UNSUPPORTED, fn, "split-image A outside the planes kernel's shapes");
     a.ap = nullptr;  // the f32 operands serve
   }
-  if (variant == 0 && launch_nt_skinny(a, st)) return hip_check(hipGetLastError(), fn);  // Nc <= 8 or K <= 8
+  if (launch_nt_skinny(a, st)) return hip_check(hipGetLastError(), fn);  // Nc <= 8 or K <= 8
   if (p->mask) return fail(GNN_ERR_UNSUPPORTED, fn, "the mask epilogue needs a skinny shape (K <= 8 or N <= 8)");
   if (a.a_bf16 || a.c_bf16) {
     if (!a.a_bf16 || !a.w1 || a.Nc > BN || p->math == GNN_MATH_F32)
       return fail(GNN_ERR_UNSUPPORTED, fn, "bf16 NT needs bf16 A, the w1/w2 form, N <= 128 and split math");
-    launch_nt_x3(a, 0, p->workspace, p->workspace_bytes, st);
+    launch_nt_x3(a, p->workspace, p->workspace_bytes, st);
     return hip_check(hipGetLastError(), fn);
   }
-  if (p->math != GNN_MATH_F32 && a.w1 && a.Nc <= BN && variant < 16) {
-    launch_nt_x3(a, variant, p->workspace, p->workspace_bytes, st);  // split-bf16 MFMA (gemm_x3.hip)
+  if (p->math != GNN_MATH_F32 && a.w1 && a.Nc <= BN) {
+    launch_nt_x3(a, p->workspace, p->workspace_bytes, st);  // split-bf16 MFMA (gemm_x3.hip)
     return hip_check(hipGetLastError(), fn);
   }
-  if (variant >= 16) variant -= 16;  // lab: exact-f32 kernel variants
-  if (v4) launch_nt_variant<4>(a, variant, st);
-  else if (v2) launch_nt_variant<2>(a, variant, st);
-  else launch_nt_variant<1>(a, variant, st);
+  if (v4) launch_nt_f32<4>(a, st);
+  else if (v2) launch_nt_f32<2>(a, st);
+  else launch_nt_f32<1>(a, st);
   return hip_check(hipGetLastError(), fn);
 }
 
@@ -836,13 +828,9 @@ extern "C" gnn_status gnn_gemm_nt_workspace_size(int64_t N, int64_t k1, int64_t 
 }
 
 extern "C" gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream) {
-  return gemm_nt_dispatch(p, 0, stream, __func__);
+  return gemm_nt_dispatch(p, stream, __func__);
 }
 
-// Tuning entry (not part of the public ABI): run NT tiling variant `variant`.
-extern "C" gnn_status gnnx_gemm_nt_variant_f32(const gnn_gemm_nt_params* p, int variant, gnn_stream_t stream) {
-  return gemm_nt_dispatch(p, variant, stream, __func__);
-}
 
 extern "C" gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t Kc, int32_t nproj, size_t* bytes) {
   if (!bytes || M < 0 || Nr < 1 || Kc < 1 || nproj < 0) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
@@ -855,21 +843,16 @@ extern "C" gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t 
 }
 
 static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void* workspace,
-                                   size_t workspace_bytes, gnn_stream_t stream, int variant);
+                                   size_t workspace_bytes, gnn_stream_t stream);
 
 extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* workspace,
                                       size_t workspace_bytes, gnn_stream_t stream) {
-  return gemm_tn_dispatch(p, out, workspace, workspace_bytes, stream, 0);
+  return gemm_tn_dispatch(p, out, workspace, workspace_bytes, stream);
 }
 
-// Tuning entry (not part of the public ABI): split-bf16 TN tiling `variant` (gemm_x3.hip).
-extern "C" gnn_status gnnx_gemm_tn_variant_f32(const gnn_gemm_tn_params* p, float* out, void* workspace,
-                                               size_t workspace_bytes, int variant, gnn_stream_t stream) {
-  return gemm_tn_dispatch(p, out, workspace, workspace_bytes, stream, variant);
-}
 
 static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void* workspace,
-                                   size_t workspace_bytes, gnn_stream_t stream, int variant) {
+                                   size_t workspace_bytes, gnn_stream_t stream) {
   const char* __fn = "gnn_gemm_tn_f32";
   if (!p || !out) return fail(GNN_ERR_INVALID_ARG, __fn, "null params/out");
   if (p->M < 0 || p->Nr < 1 || p->Nr > 128 || p->k1 < 1 || p->k2 < 0 || p->k1 + p->k2 > KMAX)
@@ -921,7 +904,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
     a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
     a.ap_ps = p->planes_stride;
     if (p->math != GNN_MATH_F32 && tn_planes_ok(a)) {
-      launch_tn_planes(a, nblk, st, variant);
+      launch_tn_planes(a, nblk, st);
       GNN_LAUNCH_CHECK();
       slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
       GNN_LAUNCH_CHECK();
@@ -930,7 +913,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
     if (planes_only) return fail(GNN_ERR_UNSUPPORTED, __fn, "split-image A outside the planes kernel's shapes");
     a.ap = nullptr;
   }
-  if (variant == 0 && tn_skinny_ok(a)) {  // Nr <= 8 plain g form: VALU stream (gemm_skinny.hip)
+  if (tn_skinny_ok(a)) {  // Nr <= 8 plain g form: VALU stream (gemm_skinny.hip)
     nblk = tn_skinny_blocks(a.M);
     if (workspace_bytes < (size_t)nblk * stride * sizeof(float))
       return fail(GNN_ERR_WORKSPACE, __fn, "workspace too small");
@@ -944,7 +927,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   if (a.a_bf16 && (p->math == GNN_MATH_F32 || (a.M + 32) * ldmax >= ((int64_t)1 << 31) || a.M < 16))
     return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 TN needs split math, M >= 16 and M*ld < 2^31");
   if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31) && a.M >= 16) {
-    launch_tn_x3(a, nblk, st, variant);  // split-bf16 MFMA (gemm_x3.hip)
+    launch_tn_x3(a, nblk, st);  // split-bf16 MFMA (gemm_x3.hip)
     GNN_LAUNCH_CHECK();
     slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
     GNN_LAUNCH_CHECK();

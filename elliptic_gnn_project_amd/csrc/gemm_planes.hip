@@ -418,8 +418,7 @@ bool tn_planes_ok(const TNArgs& a) {
   return (a.M + 32) * ldmax < ((int64_t)1 << 31);
 }
 
-void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st, int variant) {
-  (void)variant;
+void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st) {
   const int kt = (a.ap_ld + 31) / 32;
   if (kt <= 4) launch_tn_planes_kt<4>(a, nblk, st);
   else if (kt <= 6) launch_tn_planes_kt<6>(a, nblk, st);

@@ -73,13 +73,11 @@ constexpr int WS_BIAS = 1, WS_RELU = 2, WS_DROP = 4, WS_PROJ = 8;
 // KS = 1: 4 waves (one per SIMD), every wave holds all NKS k-steps of its columns (≤ 264 VGPRs
 //         of B; 512-register waves).  KS = 2: 8 waves (two per SIMD), each holds half the
 //         k-steps; the pair's partial sums meet through LDS.
-// LAB (timing ablations only, bench_gemm variants 10-14): bit 1 no A loads / staging, bit 2 no
-// epilogue, bit 4 no MFMAs, bit 8 every tile's A re-read from the block's first tile (L2-hot).
-// r10 (layer-1 shape, fused epilogue / plain store, us): production 145 / 117, no staging 120 / 91,
-// no epilogue 110, neither 78.5 (the bare MFMA loop at 53 % of its 42 us floor: one wave per SIMD
-// exposes the fragment reads and the two barriers per tile), no MFMAs 89 / 83, L2-hot A 140 / 109
-// (HBM costs ~6 us).  So: MFMA loop 78 + staging ~27 + fused epilogue ~30 (projection, dropout).
-template <int NKS, int EPI, int KS, int LAB = 0>
+// r10 ablations (layer-1 shape, fused epilogue / plain store, us): production 145 / 117, no staging
+// 120 / 91, no epilogue 110, neither 78.5 (the bare MFMA loop), no MFMAs 89 / 83, L2-hot A 140 /
+// 109: MFMA loop 78 + staging ~27 + fused epilogue ~30.  The split-image form below (planes)
+// interleaves the staging and the epilogue into the MFMA chain.
+template <int NKS, int EPI, int KS>
 __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const uint4* __restrict__ bimg, int ntiles,
                                                              const float* __restrict__ tail) {
   constexpr int WS_THREADS = 256 * KS;
@@ -89,7 +87,6 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   constexpr int KH = KH0;                  // register slots per wave (the second part has <= KH0)
   constexpr int QN = (128 * NKS + WS_THREADS - 1) / WS_THREADS;  // staged quads per thread per tile
   constexpr int RV = 16 / KS;              // accumulator rows (r-slots) a wave finishes
-  constexpr bool TWO = (LAB & 16) != 0;    // two independent accumulator chains
   // LDS: two A buffers, the C tile of the epilogue ([32 rows][128] f32: coalesced C stores and
   // the projection read it), the K-half exchange (KS 2: aliased onto the C tile when the A
   // buffers leave no room — one more barrier per tile) and the projection weights.
@@ -180,7 +177,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   // the tile's two segment bases, formed once per tile (not per quad: per-quad forms compiled
   // to a scalar branch pair per load inside the MFMA stream)
   auto tile_base = [&](int t, const float*& b1, const float*& b2) {
-    const int tc = (LAB & 8) ? blockIdx.x : min(t, ntiles - 1);  // LAB 8: re-read an L2-hot tile
+    const int tc = min(t, ntiles - 1);
     const bool last = tc == ntiles - 1;
     b1 = last ? tail1 : pa1 + (int64_t)tc * WS_ROWS * k1;
     b2 = last ? tail2 : pa2 + (int64_t)tc * WS_ROWS * k2;
@@ -239,7 +236,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   auto kloop = [&](const char* cur, char* nxt, int sb, int tload) {
     const float *lb1, *lb2;
     tile_base(tload, lb1, lb2);
-    floatx16 acc, acc2;
+    floatx16 acc;
     constexpr int SQ0 = KH - QN > 0 ? KH - QN : 0;  // k-steps SQ0.. stage one quad each
     // one fragment set, each plane re-read for step s+1 right after its last use in step s:
     // plane 2 after MFMA 1, plane 1 after MFMA 3, plane 0 after MFMA 6 — each read has 3-5
@@ -255,9 +252,9 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
 #pragma unroll
     for (int s = 0; s < KH; ++s) {
       const int sn = s + 1 < KH ? s + 1 : s;
-      const bool stg = (LAB & 1) == 0 && s >= SQ0 && s - SQ0 < QN;  // compile-time (unrolled)
+      const bool stg = s >= SQ0 && s - SQ0 < QN;  // compile-time (unrolled)
       const int qi = s - SQ0;
-      const bool mm = (LAB & 4) == 0 && (KS == 1 || NKS % 2 == 0 || s < ns);  // odd NKS, KS 2: the
+      const bool mm = KS == 1 || NKS % 2 == 0 || s < ns;  // odd NKS, KS 2: the
       if (mm) {                                                               // second part is 1 shorter
         if (s == 0) ws_mfma<true>(acc, x[2], bw[s][0]);  // small terms first
         else ws_mfma<false>(acc, x[2], bw[s][0]);
@@ -266,12 +263,7 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       if (s + 1 < KH) x[2] = frag(sn, 2);
       if (stg) stage_pair(nxt, sb, qi, 0);
       WS_FENCE;
-      if (mm) {
-        if constexpr (TWO) {
-          if (s == 0) ws_mfma<true>(acc2, x[1], bw[s][1]);
-          else ws_mfma<false>(acc2, x[1], bw[s][1]);
-        } else ws_mfma<false>(acc, x[1], bw[s][1]);
-      }
+      if (mm) ws_mfma<false>(acc, x[1], bw[s][1]);
       WS_FENCE;
       if (stg) stage_pair(nxt, sb, qi, 1);
       WS_FENCE;
@@ -281,32 +273,23 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
       if (stg) load_quad_b(sb, qi, lb1, lb2);
       WS_FENCE;
       if (mm) {
-        ws_mfma<false>(TWO ? acc2 : acc, x[0], bw[s][2]);
+        ws_mfma<false>(acc, x[0], bw[s][2]);
         ws_mfma<false>(acc, x[0], bw[s][1]);
-        ws_mfma<false>(TWO ? acc2 : acc, x[0], bw[s][0]);
+        ws_mfma<false>(acc, x[0], bw[s][0]);
       }
       WS_FENCE;
       if (s + 1 < KH) x[0] = frag(sn, 0);
       WS_FENCE;
     }
 #undef WS_FENCE
-    if constexpr (KH < QN && (LAB & 1) == 0) {
+    if constexpr (KH < QN) {
 #pragma unroll
       for (int i = KH; i < QN; ++i) {
         stage_quad(nxt, sb, i);
         load_quad_b(sb, i, lb1, lb2);
       }
     }
-    if constexpr ((LAB & 4) != 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = x[0][r & 7];
-    }
     ws_mfma_end(acc);
-    if constexpr (TWO) {
-      ws_mfma_end(acc2);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] += acc2[r];
-    }
     return acc;
   };
 
@@ -424,13 +407,9 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
     __syncthreads();
     exchange_recv(acc, v);
     if constexpr (XALIAS) __syncthreads();
-    if constexpr ((LAB & 2) == 0) {
-      epi_tile(v, t);
-      __syncthreads();
-      epi_store(t);
-    } else {
-      if (v[0] == 123.f) cptr[tid] = v[RV - 1];  // keep the accumulators live
-    }
+    epi_tile(v, t);
+    __syncthreads();
+    epi_store(t);
   };
   // two tiles per trip: static A buffers (A0 -> A1 -> A0) and register sets (1, 0), so the
   // compiler sees staging writes and fragment reads as disjoint.  Past the end the staging
@@ -776,12 +755,12 @@ __global__ __launch_bounds__(256) void ws_prep_kernel(NTArgs a, uint4* __restric
   else ws_tail_block(a, tail, r0, blockIdx.x - nchunks);
 }
 
-template <int NKS, int KS, int LAB = 0>
+template <int NKS, int KS>
 void launch_ws_k(const NTArgs& a, const uint4* bimg, const float* tail, hipStream_t st) {
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
   const int grid = std::min(ntiles, ws_num_cus());
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
-#define GNN_WS(E) gemm_nt_ws_kernel<NKS, E, KS, LAB><<<grid, 256 * KS, 0, st>>>(a, bimg, ntiles, tail)
+#define GNN_WS(E) gemm_nt_ws_kernel<NKS, E, KS><<<grid, 256 * KS, 0, st>>>(a, bimg, ntiles, tail)
   if (proj && drop) GNN_WS(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
   else if (proj) GNN_WS(WS_BIAS | WS_RELU | WS_PROJ);
   else if (drop) GNN_WS(WS_BIAS | WS_RELU | WS_DROP);
@@ -815,41 +794,23 @@ bool nt_ws_ok(const NTArgs& a) {
   return true;
 }
 
-// ks: K parts per column group (0 = the default: 2 when the half-K B fragments and the rest fit
-// a 256-register wave without spills, i.e. NKS <= 16; 1 for NKS = 21: 252 AGPRs of B).
 size_t nt_ws_tail_offset(int64_t k1, int64_t k2) {  // the B image (<= 24 chunks x 12 KB), then the tail tile
   return (size_t)((k1 + k2 + 15) / 16) * 3 * 256 * sizeof(uint4);
 }
 
-void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st, int ks) {
+void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st) {
   const int nks = (a.k1 + a.k2 + 15) / 16;
   float* tail = reinterpret_cast<float*>(reinterpret_cast<char*>(img) + nt_ws_tail_offset(a.k1, a.k2));
   ws_prep_kernel<<<(unsigned)(nks + ceil_div(WS_ROWS * (a.k1 + a.k2), 256)), 256, 0, st>>>(
       a, img, nks, tail, (ceil_div(a.M, WS_ROWS) - 1) * WS_ROWS, a.k1);
-#define GNN_WSL(N, K, L) launch_ws_k<N, K, L>(a, img, tail, st)
-  if (ks < 0) {  // lab ablations of the production NKS = 21 instance (KS 1)
-    if (nks != 21) ks = 0;
-    else {
-      switch (-ks) {
-        case 1: GNN_WSL(21, 1, 1); break;
-        case 2: GNN_WSL(21, 1, 2); break;
-        case 3: GNN_WSL(21, 1, 3); break;
-        case 4: GNN_WSL(21, 1, 4); break;
-        case 6: GNN_WSL(21, 1, 19); break;
-        case 7: GNN_WSL(21, 1, 16); break;
-        default: GNN_WSL(21, 1, 8); break;
-      }
-      return;
-    }
-  }
-  if (ks == 0) ks = nks <= 16 ? 2 : 1;
+  // K parts per column group: 2 when the half-K B fragments and the rest fit a 256-register wave
+  // without spills (NKS <= 16), 1 for NKS = 21 (252 AGPRs of B)
   switch (nks) {
-    case 8: if (ks == 2) GNN_WSL(8, 2, 0); else GNN_WSL(8, 1, 0); break;
-    case 11: if (ks == 2) GNN_WSL(11, 2, 0); else GNN_WSL(11, 1, 0); break;
-    case 16: if (ks == 2) GNN_WSL(16, 2, 0); else GNN_WSL(16, 1, 0); break;
-    default: if (ks == 2) GNN_WSL(21, 2, 0); else GNN_WSL(21, 1, 0); break;
+    case 8: launch_ws_k<8, 2>(a, img, tail, st); break;
+    case 11: launch_ws_k<11, 2>(a, img, tail, st); break;
+    case 16: launch_ws_k<16, 2>(a, img, tail, st); break;
+    default: launch_ws_k<21, 1>(a, img, tail, st); break;
   }
-#undef GNN_WSL
 }
 
 }  // namespace gnnmp

@@ -198,9 +198,9 @@ __device__ __forceinline__ void x3_chunk(const NTArgs& a, int c, int nch1, const
 // is short; without depth the loop waits on HBM latency).  One barrier per chunk.
 // NPL = 3: f32 operands split (6 products); NPL = 1 with ABF: bf16 operands as stored, B rounded
 // to bf16 (the image's hi plane), one product (the bf16-storage path); CBF: C stored as bf16.
-constexpr int NT_PIPE = 32, NT_HINTS = 64;  // gemm_nt_x3_kernel LAB flags (bits 1-16: lab ablations)
+constexpr int NT_PIPE = 32, NT_HINTS = 64;  // gemm_nt_x3_kernel schedule flags (the bf16-storage form)
 
-template <int KC, int TM, int AV, int AU, int BV, int D, int NPL = 3, bool ABF = false, bool CBF = false, int LAB = 0>
+template <int KC, int TM, int AV, int AU, int BV, int D, int NPL = 3, bool ABF = false, bool CBF = false, int SCHED = 0>
 __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* __restrict__ bimg) {
   constexpr int P = KC + 8;  // bf16 per LDS row: 24 or 40 (12 / 20 dwords)
   constexpr int BM = 128 * TM;
@@ -247,9 +247,8 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   auto store = [&](int c, int buf, const float* rA, const float* rB) {
     const float *A, *W; int64_t lda, ldw; int k0, klen;
     x3_chunk<KC>(a, c, nch1, A, lda, W, ldw, k0, klen);
-    if constexpr (!(LAB & 8)) x3_store_rows<AU, KC, BM, P, NPL>(As[buf], m0, a.M, klen, rA);
-    if constexpr (LAB & 16) {
-    } else if constexpr (BV == 0) {
+    x3_store_rows<AU, KC, BM, P, NPL>(As[buf], m0, a.M, klen, rA);
+    if constexpr (BV == 0) {
       const int n = threadIdx.x >> 1, kh = threadIdx.x & 1;
 #pragma unroll
       for (int p = 0; p < NPL; ++p)
@@ -290,7 +289,7 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   // in flight; a branch around a load makes it drain every stage at the next store.
 #pragma unroll
   for (int d = 0; d < D; ++d) load(min(d, nchunks - 1), ra[d], rb[d]);
-  if constexpr ((LAB & NT_PIPE) != 0) {
+  if constexpr ((SCHED & NT_PIPE) != 0) {
     // software-pipelined order: between two barriers, stage chunk c+1 into the other buffer
     // while the MFMAs of chunk c run, so VALU splits / LDS writes interleave with the MFMAs
     store(0, 0, ra[0], rb[0]);
@@ -305,7 +304,7 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
         store(cc + 1, (cc + 1) & 1, ra[d1], rb[d1]);
         load(min(cc + 1 + D, nchunks - 1), ra[d1], rb[d1]);
         compute(cc & 1, cc);
-        if constexpr ((LAB & NT_HINTS) != 0) {  // interleave: per MFMA, a few VALU / DS ops
+        if constexpr ((SCHED & NT_HINTS) != 0) {  // interleave: per MFMA, a few VALU / DS ops
 #pragma unroll
           for (int i = 0; i < 4 * TM * (NPL == 3 ? 6 : 1) * (KC / 16); ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -336,10 +335,10 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
     for (int d = 0; d < D; ++d) {
       const int c = c0 + d;
       const int buf = c & 1;
-      if constexpr (!(LAB & 4)) store(c, buf, ra[d], rb[d]);  // buf last read by compute(c - 2): behind barrier c - 1
+      store(c, buf, ra[d], rb[d]);  // buf last read by compute(c - 2): behind barrier c - 1
       __syncthreads();
-      if constexpr (!(LAB & 2)) load(min(c + D, nchunks - 1), ra[d], rb[d]);
-      if constexpr (!(LAB & 1)) compute(buf, c);
+      load(min(c + D, nchunks - 1), ra[d], rb[d]);
+      compute(buf, c);
     }
   }
 #pragma unroll
@@ -354,10 +353,10 @@ __global__ __launch_bounds__(256) void gemm_nt_x3_kernel(NTArgs a, const uint4* 
   nt_epilogue<TM, CBF>(a, acc, m0, n0, lane, wave, seed);
 }
 
-template <int KC, int TM, int AV, int AU, int D, int LAB = 0>
+template <int KC, int TM, int AV, int AU, int D>
 void launch_nt_x3_b(const NTArgs& a, const uint4* bimg, hipStream_t st) {
   dim3 grid((unsigned)ceil_div(a.M, 128 * TM), (unsigned)ceil_div(a.Nc, BN));
-  if (bimg) gemm_nt_x3_kernel<KC, TM, AV, AU, 0, D, 3, false, false, LAB><<<grid, 256, 0, st>>>(a, bimg);
+  if (bimg) gemm_nt_x3_kernel<KC, TM, AV, AU, 0, D><<<grid, 256, 0, st>>>(a, bimg);
   else if (a.wvec == 4) gemm_nt_x3_kernel<KC, TM, AV, AU, 4, D><<<grid, 256, 0, st>>>(a, nullptr);
   else if (a.wvec == 2) gemm_nt_x3_kernel<KC, TM, AV, AU, 2, D><<<grid, 256, 0, st>>>(a, nullptr);
   else gemm_nt_x3_kernel<KC, TM, AV, AU, 1, D><<<grid, 256, 0, st>>>(a, nullptr);
@@ -688,8 +687,7 @@ size_t nt_x3_workspace(int64_t k1, int64_t k2) {  // pre-split B image, 12 KB pe
   return x3 > ws ? x3 : ws;
 }
 
-// variant: 0 = production; others are lab tilings (bench_gemm.cpp).
-void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipStream_t st) {
+void launch_nt_x3(const NTArgs& a, void* ws, size_t ws_bytes, hipStream_t st) {
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
   auto av_ok = [&](int v) {
     return (a.k1 % v == 0) && (a.lda1 % v == 0) && al(a.a1, 4 * v) &&
@@ -720,10 +718,9 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
   }
   const int av = av_ok(4) ? 4 : (av_ok(2) ? 2 : 1);
   const bool pre = ws && ws_bytes >= nt_x3_workspace(a.k1, a.k2) && a.Nc <= BN;
-  if (pre && (variant == 0 || variant == 3 || variant == 4) && nt_ws_ok(a)) {
-    // production: weight-stationary persistent form (gemm_ws.hip, its own B image in `ws`);
-    // lab 3 / 4 force 1 / 2 K parts
-    launch_nt_ws(a, static_cast<uint4*>(ws), st, variant == 0 ? 0 : variant - 2);
+  if (pre && nt_ws_ok(a)) {
+    // the weight-stationary persistent form (gemm_ws.hip, its own B image in `ws`)
+    launch_nt_ws(a, static_cast<uint4*>(ws), st);
     return;
   }
   if (pre) {
@@ -731,42 +728,11 @@ void launch_nt_x3(const NTArgs& a, int variant, void* ws, size_t ws_bytes, hipSt
     x3_presplit_b_kernel<<<nch, 256, 0, st>>>(a, static_cast<uint4*>(ws), nch1, nch);
     bimg = static_cast<const uint4*>(ws);
   }
-  // Lab (bench_gemm.cpp, MI355X, Elliptic layer-1 shape, same process, plain / fused epilogue):
-  //   classic order (stage c; barrier; MFMAs of c)            171-182 / 202-228 us
-  //   pipelined order (barrier; stage c+1 with MFMAs of c)    164-169 / 189-194 us
-  //   pipelined + sched_group_barrier interleave (production) 155-159 / 182-185 us
-  // Ablations of the classic instance (what bounds it): no MFMA phase 122, no global loads 127,
-  // MFMA phase + barriers only 103, LDS staging only 70 (A 49, B 49), barriers + epilogue 30;
-  // D = 1 228, D = 3 188; A fragments loaded straight to registers (no A through LDS) 291
-  // (fragment-shaped loads touch 32 rows per instruction).  LDS-DMA form (gemm_nt_x3g_kernel,
-  // 3-stage ring, counted vmcnt, asm fragment reads): 167 with dword A DMA, 151 with dwordx4 A
-  // DMA on 16-byte rows, 102 with the A DMA removed — the A tile's 64-byte row pieces, not the
-  // MFMA phase, bound it; classic 145-154 in the same runs.  32-deep DMA chunks (x3h: full
-  // 128-byte row lines, 48 MFMAs per barrier, 2 or 3 stages of 40 KB) 143-149 = classic.
-  // TM = 2 (a wave owns 64 rows, 128 AGPRs, one wave per SIMD) 216-233.
-  if (!bimg) {  // no workspace: B split in-kernel
-    launch_nt_x3_a<16, 1, 2, 2>(a, av, nullptr, st);
-    return;
-  }
-  switch (variant) {
-    case 1: launch_nt_x3_b<16, 1, 2, 2, 2, NT_PIPE | NT_HINTS>(a, bimg, st); break;  // pipelined + hints
-    case 2: launch_nt_x3_b<16, 1, 2, 2, 2, NT_PIPE>(a, bimg, st); break;             // pipelined
-    case 6: launch_nt_x3_b<16, 1, 2, 2, 2, 1>(a, bimg, st); break;  // ablation: no MFMA phase
-    case 7: launch_nt_x3_b<16, 1, 2, 2, 2, 2>(a, bimg, st); break;  // ablation: no global loads in the loop
-    case 8: launch_nt_x3_b<16, 1, 2, 2, 2, 6>(a, bimg, st); break;  // ablation: MFMA phase + barriers only
-    case 9: launch_nt_x3_b<16, 1, 2, 2, 2, 3>(a, bimg, st); break;  // ablation: LDS staging + barriers only
-    case 5:  // lab: ws, two accumulator chains (-7), and the same without staging / epilogue (15 -> -6)
-      if (nt_ws_ok(a)) launch_nt_ws(a, const_cast<uint4*>(bimg), st, -7);
-      else launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
-      break;
-    case 10: case 11: case 12: case 13: case 14: case 15:  // lab: weight-stationary ablations (gemm_ws.hip)
-      if (nt_ws_ok(a)) launch_nt_ws(a, const_cast<uint4*>(bimg), st, -(variant - 9));
-      else launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
-      break;
-    default:  // classic order (branch-free MFMA phase): shapes outside nt_ws_ok; lab variant 20
-      launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
-      break;
-  }
+  // The classic order (stage c; barrier; MFMAs of c) for the shapes outside nt_ws_ok.  r05-r10 lab
+  // (Elliptic layer-1 shape): pipelined order + sched_group_barrier interleave 155-159 us vs
+  // classic 171-182; D = 1 / 3 ring 228 / 188; A fragments straight to registers 291; an LDS-DMA
+  // form 151-167; TM = 2 216-233 — the weight-stationary form (135 us) replaced them.
+  launch_nt_x3_a<16, 1, 2, 2>(a, av, bimg, st);
 }
 
 template <int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0, bool GO = false,
@@ -802,7 +768,7 @@ void launch_tn_x3_k(const TNArgs& a, int nblk, hipStream_t st) {
 // right after each slot is consumed) 150-155 us; its ablations: no MFMAs 103, L2-hot loads 153
 // (not HBM-bound); two waves per SIMD (512 threads, half the k-tiles per wave, 2 A slots + a
 // 4-row G slot per thread) 164.  Every form lands at ~6,000 cycles per chunk per SIMD.
-void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
+void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
   constexpr int D = 1;
   if (a.a_bf16) {
@@ -810,24 +776,9 @@ void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st, int variant) {
     else { if (a.h_bf16) launch_tn_x3_k<D, 12, 1, true, true, 0>(a, nblk, st); else launch_tn_x3_k<D, 12, 1, true, false, 0>(a, nblk, st); }
     return;
   }
-  if (variant == 3 || variant == 4) {  // lab: pipelined order (3: + interleave hints, 4: without)
-    const int pp = variant == 3 ? 2 : 1;
-    if (pp == 2) {
-      if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 2>(a, nblk, st);
-      else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 2>(a, nblk, st);
-      else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 2>(a, nblk, st);
-      else launch_tn_x3_k<D, 12, 3, false, false, 2>(a, nblk, st);
-    } else {
-      if (nkt <= 6) launch_tn_x3_k<D, 6, 3, false, false, 1>(a, nblk, st);
-      else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 1>(a, nblk, st);
-      else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 1>(a, nblk, st);
-      else launch_tn_x3_k<D, 12, 3, false, false, 1>(a, nblk, st);
-    }
-    return;
-  }
   // production: classic order (stage c; barrier; MFMAs of c).  Nr <= 64 (GCN / GAT / SAGE-ResBN
   // hidden width 64): the half-N mapping, ceil(nkt / 2) k-tiles per wave
-  if (a.Nr <= 64 && variant != 8) {
+  if (a.Nr <= 64) {
     const int kh = (nkt + 1) / 2;
     if (kh <= 2) launch_tn_x3_k<D, 2, 3, false, false, 0, true>(a, nblk, st);
     else if (kh <= 3) launch_tn_x3_k<D, 3, 3, false, false, 0, true>(a, nblk, st);

@@ -1,6 +1,6 @@
 """Kernel lab for the segmented aggregation (K1/K2/K4) on the bench graphs (not part of the product).
 
-Times gnn_aggregate_f32 launch shapes selected by gnnx_set_agg_variant on the SAGE-preset graph
+Times gnn_aggregate_f32 launch shapes selected by gnnx_set_agg_variant (a lab knob of aggregate.hip) on the SAGE-preset graph
 (symmetrized, 203,769 nodes / 468,710 slots) and the GCN-preset graph (self loops replaced),
 variants interleaved over rounds (median), each checked bitwise against variant 0.
 
