@@ -351,11 +351,14 @@ def main():
     if dist is not None:
         gdist.convert_sync_batchnorm(model, dist)  # exact full-graph BN (SAGE-ResBN); no-op otherwise
     state0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    # HIP-graph replay of the step (the MI355X stand-in for a tracing compiler): one graph at N=1;
-    # at N>1 the gradient all-reduce stays eager between a forward+backward graph and an optimizer
-    # graph.  SyncBatchNorm's in-forward collective (SAGE-ResBN at N>1) keeps that case eager.
+    # HIP-graph replay of the step (the MI355X stand-in for a tracing compiler).  N=1, and N>1 over
+    # RCCL: ONE graph for the whole step, the RCCL collectives (SyncBN statistics forward and
+    # backward, the gradient bucket) captured in it.  gloo (CPU collectives, tests only): a
+    # forward+backward graph and an optimizer graph with the all-reduce eager between them, and
+    # eager launch when SyncBatchNorm's collectives sit inside the forward/backward.
     has_sync_bn = any(isinstance(m, gdist.SyncBatchNorm1d) for m in model.modules())
-    use_graph = not args.eager and not (dist is not None and has_sync_bn)
+    rccl = dist is not None and args.dist_backend == "nccl"
+    use_graph = not args.eager and not (dist is not None and not rccl and has_sync_bn)
     if args.aten_step:
         opt = torch.optim.Adam(model.parameters(), lr=0.003, weight_decay=1e-4, fused=True, capturable=use_graph)
     else:  # clip_grad_norm_(1.0) + Adam fused (train_ops.ClipAdam: 2 launches, device step counter)
@@ -380,7 +383,7 @@ def main():
         else:  # the same masked weighted CE, one fused kernel (fwd + dlogits)
             loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
         loss.backward(unit_gradient(loss.device))  # = loss.backward(), without the per-step fill
-        return loss
+        return loss.detach()  # drop the autograd graph now (a live one would pin this step's streams)
 
     def allreduce():
         bucket.allreduce_(dist)
@@ -399,7 +402,7 @@ def main():
 
     if use_graph:
         from elliptic_gnn_project_amd.train_gnn import CapturedStep
-        if bucket is None:
+        if bucket is None or rccl:
             step = CapturedStep(eager_step)
         else:
             step = CapturedStep(fwd_bwd, mid=allreduce, tail=opt_step)
@@ -432,6 +435,10 @@ def main():
     if not args.no_roofline:
         KernelTimer.start()
         for _ in range(5):
+            # hold the stream in a spin kernel while Python enqueues the whole step, so each event
+            # pair brackets back-to-back GPU work only (an idle stream would count the host's
+            # launch latency between an event and its kernel as kernel time)
+            torch.cuda._sleep(50_000_000)
             eager_step()
         recs = KernelTimer.stop()
         roof = roofline(recs)
@@ -463,6 +470,7 @@ def main():
                 "parallelism": f"dp{world} timestep-partitioned ({args.scale})" if world > 1 else "single",
                 "collective": f"{args.dist_backend} all-reduce of one flat fp32 gradient bucket per step" if world > 1 else None,
                 "launch": ("eager" if not use_graph else "hip-graph replay of the whole step" if bucket is None
+                           else "hip-graph replay of the whole step, RCCL collectives captured" if rccl
                            else "hip-graph replay of fwd+bwd and of the optimizer, eager all-reduce between"),
             },
             "roofline": roof,

@@ -900,6 +900,8 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
   a.add = p->addend; a.ld_add = p->ld_add;
   a.bias = p->bias; a.relu = p->relu;
   if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout p in [0,1)");
+  if (p->dropout_p > 0.f && (int64_t)g->num_nodes * (int64_t)F >= ((int64_t)1 << 32))
+    return fail(GNN_ERR_UNSUPPORTED, __func__, "dropout element index (rows x width) must be < 2^32");
   a.dropout = p->dropout_p > 0.f;
   a.keep_thresh = (uint32_t)((1.0 - (double)p->dropout_p) * 16777216.0);
   a.drop_scale = a.dropout ? (float)(1.0 / (1.0 - (double)p->dropout_p)) : 1.0f;
@@ -1008,6 +1010,8 @@ extern "C" gnn_status gnn_aggregate_bf16(const gnn_graph* g, const gnn_agg_param
   a.add = p->addend; a.ld_add = p->ld_add;
   a.bias = p->bias; a.relu = p->relu;
   if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout p in [0,1)");
+  if (p->dropout_p > 0.f && (int64_t)g->num_nodes * (int64_t)F >= ((int64_t)1 << 32))
+    return fail(GNN_ERR_UNSUPPORTED, __func__, "dropout element index (rows x width) must be < 2^32");
   a.dropout = p->dropout_p > 0.f;
   a.keep_thresh = (uint32_t)((1.0 - (double)p->dropout_p) * 16777216.0);
   a.drop_scale = a.dropout ? (float)(1.0 / (1.0 - (double)p->dropout_p)) : 1.0f;

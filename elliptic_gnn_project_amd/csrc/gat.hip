@@ -359,7 +359,7 @@ __device__ __forceinline__ uint64_t gat_seed(const GatEpi& e) {
 }
 
 __device__ __forceinline__ float gat_store_val(const GatEpi& e, uint64_t seed, float v, int64_t r, int col, int Fo) {
-  if (e.act == GNN_ACT_ELU) v = v > 0.0f ? v : fexp(v) - 1.0f;
+  if (e.act == GNN_ACT_ELU) v = v > 0.0f ? v : expm1f(v);  // F.elu: expm1 (no cancellation near 0)
   if (e.dropout)
     v = keep_elem(seed, (uint32_t)r * (uint32_t)Fo + (uint32_t)col, e.keep_thresh) ? v * e.drop_scale : 0.0f;
   return v;
@@ -1121,6 +1121,8 @@ extern "C" gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fw
     return fail(GNN_ERR_INVALID_ARG, __func__, "bad sizes");
   if (p->act != GNN_ACT_NONE && p->act != GNN_ACT_ELU) return fail(GNN_ERR_INVALID_ARG, __func__, "unknown act");
   if (!(p->dropout_p >= 0.0f && p->dropout_p < 1.0f)) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout_p not in [0, 1)");
+  if (p->dropout_p > 0.0f && (int64_t)g->num_nodes * (concat ? (int64_t)H * C : (int64_t)C) >= ((int64_t)1 << 32))
+    return fail(GNN_ERR_UNSUPPORTED, __func__, "dropout element index (rows x width) must be < 2^32");
   if (g->num_nodes == 0) return GNN_OK;
   if (!p->xh || !p->att_src || !p->att_dst || !p->a_src || !p->a_dst || !p->alpha || !p->out || !g->rowptr || !g->col)
     return fail(GNN_ERR_INVALID_ARG, __func__, "null");
@@ -1168,6 +1170,7 @@ extern "C" gnn_status gnn_gat_act_bwd_f32(int64_t N, int64_t F, gnn_act act, flo
     return fail(GNN_ERR_INVALID_ARG, __func__, "bad sizes");
   if (act != GNN_ACT_NONE && act != GNN_ACT_ELU) return fail(GNN_ERR_INVALID_ARG, __func__, "unknown act");
   if (!(dropout_p >= 0.0f && dropout_p < 1.0f)) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout_p not in [0, 1)");
+  if (dropout_p > 0.0f && N * F >= ((int64_t)1 << 32)) return fail(GNN_ERR_UNSUPPORTED, __func__, "dropout element index (rows x width) must be < 2^32");
   if (N == 0) return GNN_OK;
   if (!y || !dy || !dpre) return fail(GNN_ERR_INVALID_ARG, __func__, "null");
   const GatEpi ep = make_epi(act, dropout_p, seed, seed_ptr);

@@ -756,6 +756,8 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
   if (p->nproj < 0 || p->nproj > 4 || (p->nproj > 0 && (p->N > BN || !p->proj || !p->z || p->ldz < p->nproj)))
     return fail(GNN_ERR_INVALID_ARG, fn, "projection needs N <= 128, nproj <= 4, proj and z");
   if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, fn, "dropout p in [0,1)");
+  if (p->dropout_p > 0.f && (int64_t)p->M * (int64_t)p->N >= ((int64_t)1 << 32))
+    return fail(GNN_ERR_UNSUPPORTED, fn, "dropout element index (rows x width) must be < 2^32");
   if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, fn, "bad math mode");
   if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->c_dtype != GNN_DTYPE_F32 && p->c_dtype != GNN_DTYPE_BF16))
     return fail(GNN_ERR_INVALID_ARG, fn, "bad dtype");

@@ -293,9 +293,12 @@ class CapturedStep:
     draws a new mask.  Replaying removes the host's per-kernel launch cost and the gaps between
     kernels.
 
-    Split form (``mid`` and ``tail`` given): ``step_fn`` (forward + backward) is graph A, ``mid``
-    runs eagerly (the data-parallel gradient all-reduce: the collective stays outside the
-    graphs) and ``tail`` (the optimizer step) is graph B.
+    Collectives: RCCL all-reduces (backend "nccl": SyncBN statistics, the gradient bucket) are
+    stream-captured like any kernel, so an N>1 step over RCCL is ONE graph (``step_fn`` calls
+    them; the communicator is set up by the eager warm-up before capture).  Split form (``mid``
+    and ``tail`` given), for CPU-side collectives (gloo): ``step_fn`` (forward + backward) is
+    graph A, ``mid`` runs eagerly (the gradient all-reduce) and ``tail`` (the optimizer step) is
+    graph B.
     """
 
     def __init__(self, step_fn, warmup: int = 3, mid=None, tail=None):

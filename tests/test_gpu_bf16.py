@@ -99,27 +99,62 @@ def test_gemm_tn_bf16(device, form):
 
 
 def _ref_sage_bf16(params, x_bf, ei, N, layers):
-    """float64 SAGE forward with the bf16-storage rounding points, autograd for the grads."""
+    """float64 SAGE forward with the bf16-storage rounding points (x, agg_l, h_l stored bf16; the
+    hidden layers' GEMM weights rounded to bf16).  Returns (logits, saved (agg_l, h_l) list)."""
     from oracle import pyg_ref
 
-    P = {k: v.double().requires_grad_(True) for k, v in params.items()}
-    h = x_bf.double()
+    P = {k: v.double() for k, v in params.items()}
+    h, saved = x_bf.double(), []
     for l in range(layers - 1):
         agg = rb(pyg_ref.scatter(h[ei[0]], ei[1], N, "mean"))
         pre = agg @ rb(P[f"convs.{l}.lin_l.weight"]).t() + P[f"convs.{l}.lin_l.bias"] + \
             h @ rb(P[f"convs.{l}.lin_r.weight"]).t()
+        saved.append((agg, h))
         h = rb(torch.relu(pre))
     l = layers - 1
     z_l = h @ P[f"convs.{l}.lin_l.weight"].t()
     z_r = h @ P[f"convs.{l}.lin_r.weight"].t()
     logits = pyg_ref.scatter(z_l[ei[0]], ei[1], N, "mean") + z_r + P[f"convs.{l}.lin_l.bias"]
-    return logits, P
+    saved.append((None, h))
+    return logits, saved
+
+
+def _ref_sage_bf16_grads(params, saved, dlogits, ei, N, layers):
+    """Backward of _ref_sage_bf16 in float64 with the kernels' one backward rounding point: the
+    TN's MFMA operand G = dL/dpre (f32 in the kernel) is rounded to bf16 for the weight gradients;
+    db = ΣG and the input gradients dh = [meanᵀ(G) | G]·[W_l; W_r] use G and the f32 weights
+    unrounded (split-bf16 NT), as fused._FusedSAGE.backward does."""
+    P = {k: v.double() for k, v in params.items()}
+    deg = torch.bincount(ei[1], minlength=N).double().clamp_min(1.0)
+
+    def mean_t(g):  # meanᵀ: dst-row gradient / in-degree, summed onto the sources
+        return torch.zeros(N, g.size(1), dtype=g.dtype).index_add_(0, ei[0], (g / deg[:, None])[ei[1]])
+
+    out = {}
+    l = layers - 1
+    h = saved[l][1]
+    g = dlogits.double()
+    mg = mean_t(g)
+    out[f"convs.{l}.lin_l.weight"] = mg.t() @ h
+    out[f"convs.{l}.lin_r.weight"] = g.t() @ h
+    out[f"convs.{l}.lin_l.bias"] = g.sum(0)
+    dh = mg @ P[f"convs.{l}.lin_l.weight"] + g @ P[f"convs.{l}.lin_r.weight"]
+    for l in range(layers - 2, -1, -1):
+        agg, hin = saved[l]
+        G = dh * (saved[l + 1][1] > 0).double()
+        out[f"convs.{l}.lin_l.weight"] = rb(G).t() @ agg
+        out[f"convs.{l}.lin_r.weight"] = rb(G).t() @ hin
+        out[f"convs.{l}.lin_l.bias"] = G.sum(0)
+        dh = mean_t(G) @ P[f"convs.{l}.lin_l.weight"] + G @ P[f"convs.{l}.lin_r.weight"]
+    return out
 
 
 def test_fused_sage_bf16_train_step(device):
-    """3-layer SAGE on bf16 features: logits within 2e-3 and parameter gradients within 2e-2
-    (relative L2) of the float64 reference with the same rounding points (gradient operands are
-    rounded to bf16 inside the kernels, the reference keeps them exact)."""
+    """3-layer SAGE on bf16 features: logits and every parameter gradient vs the float64 reference
+    with the kernels' rounding points in both directions (forward stores, the TN's bf16 G).  What
+    remains is f32 summation order, which moves a stored bf16 value by one ulp (2^-8 relative)
+    only where the f32 sum falls within f32 rounding of a bf16 rounding boundary (~1e-4 of the
+    values): relative L2 well under 1e-3 for the logits and 2e-4 for the gradients."""
     from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
     from elliptic_gnn_project_amd.gnn import SAGENet
 
@@ -134,8 +169,8 @@ def test_fused_sage_bf16_train_step(device):
     assert logits.dtype == torch.float32
     w = torch.randn(N, 2, generator=torch.Generator().manual_seed(1))
     (logits * w.to(device)).sum().backward()
-    ref, P = _ref_sage_bf16(params, x_bf, data.edge_index, N, 3)
-    assert rel_l2(logits, ref) < 2e-3
-    (ref * w.double()).sum().backward()
+    ref, saved = _ref_sage_bf16(params, x_bf, data.edge_index, N, 3)
+    assert rel_l2(logits, ref) < 1e-3, rel_l2(logits, ref)
+    grads = _ref_sage_bf16_grads(params, saved, w, data.edge_index, N, 3)
     for k, v in model.named_parameters():
-        assert rel_l2(v.grad, P[k].grad) < 2e-2, k
+        assert rel_l2(v.grad, grads[k]) < 2e-4, (k, rel_l2(v.grad, grads[k]))

@@ -179,3 +179,67 @@ def test_train_main_two_ranks(device, tmp_path):
     assert h["n_hubs"] == 60 and h["n_edges_remaining"] < 18000
     rows = (out / "training_log.csv").read_text().strip().splitlines()
     assert rows[0] == "epoch,train_loss,val_pr_auc" and len(rows) == 4
+
+
+def _nccl_capture_worker(port, out_path):
+    """World size 1 over RCCL on this device: the SAGE-ResBN step with SyncBatchNorm1d (K12's
+    statistics all-reduce forward, the (Σdy, Σdy·x̂) all-reduce backward) and the flat gradient
+    bucket, 5 eager steps vs 3 eager warm-up steps + capture + 2 replays of ONE graph."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from elliptic_gnn_project_amd import distributed as gdist
+    from elliptic_gnn_project_amd.train_gnn import CapturedStep, _make_loss_fn
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    full = _data()
+    d = full.to(dev)
+    cw, denom = gdist.global_class_weight_and_count(full.y, full.train_mask, None)
+    states = []
+    for captured in (False, True):
+        model = _model(dev)
+        gdist.convert_sync_batchnorm(model, dist)
+        assert sum(isinstance(m, gdist.SyncBatchNorm1d) for m in model.modules()) == 2
+        bucket = gdist.GradBucket(model)
+        opt = ClipAdam(model.parameters(), lr=0.01, weight_decay=1e-4, max_norm=1.0)
+        loss_fn = _make_loss_fn({}, cw.to(dev), model, 1, 34)
+
+        def step():
+            model.train()
+            opt.zero_grad(set_to_none=False)
+            loss = loss_fn.full(model(d.x, d.edge_index, d.timestep), d.y, d.train_mask, denom=denom)
+            loss.backward()
+            bucket.allreduce_(dist)
+            opt.step()
+            return loss.detach()
+
+        if captured:
+            cs = CapturedStep(step, warmup=3)
+            cs()
+            cs()
+        else:
+            for _ in range(5):
+                step()
+        torch.cuda.synchronize()
+        states.append({k: v.detach().cpu().clone() for k, v in model.state_dict().items()})
+    torch.save(states, out_path)
+    dist.destroy_process_group()
+
+
+def test_rccl_captured_step_matches_eager(device, tmp_path):
+    """The N>1 bench step over RCCL is one HIP graph with its collectives captured (bench.py,
+    train_gnn.CapturedStep): replaying it leaves exactly the parameters, BN running statistics
+    and counters of the eager steps (bitwise)."""
+    out_path = str(tmp_path / "nccl.pt")
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_nccl_capture_worker, args=(_free_port(), out_path))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0, p.exitcode
+    eager, graph = torch.load(out_path, weights_only=True)
+    assert eager.keys() == graph.keys()
+    for k in eager:
+        assert torch.equal(eager[k], graph[k]), k

@@ -67,6 +67,24 @@ def test_host_side_argument_validation(lib):
     assert lib.gnn_gemm_nt_f32(p, None) == 1
 
 
+def test_dropout_index_range_is_checked(lib):
+    """The counter-hash dropout keys on the 32-bit element index row·width + col: an output of
+    2^32 or more elements would repeat masks across rows, so it is refused (GNN_ERR_UNSUPPORTED)
+    before any device work instead (pointers below are never dereferenced)."""
+    from elliptic_gnn_project_amd import _lib
+
+    fake = 1 << 20
+    M, N, K = (1 << 25) + 1, 128, 128  # M·N just over 2^32
+    p = _lib.GnnGemmNTParams(M, N, fake, K, K, None, 0, 0, None, 0, fake, None, K, 0, fake, N)
+    p.dropout_p = 0.5
+    p.math = _lib.MATH_SPLIT_BF16
+    p.a_dtype = p.c_dtype = _lib.DTYPE_F32
+    assert lib.gnn_gemm_nt_f32(p, None) == 5
+    assert b"2^32" in lib.gnn_last_error()
+    F = 64  # GAT activation backward: N·F >= 2^32 with dropout
+    assert lib.gnn_gat_act_bwd_f32(1 << 26, F, 1, 0.5, 1, None, fake, F, fake, F, fake, F, None) == 5
+
+
 STRUCTS = {
     "gnn_split": ("GnnSplit", ["seg_len", "reserved", "num_long", "num_pieces", "ptr", "nbr", "piece0",
                                "piece_seg", "long_seg"]),
