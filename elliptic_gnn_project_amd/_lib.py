@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -63,6 +63,7 @@ class GnnSplit(ctypes.Structure):
         ("piece0", c_ptr),
         ("piece_seg", c_ptr),
         ("long_seg", c_ptr),
+        ("order", c_ptr),
     ]
 
 
@@ -191,7 +192,7 @@ SIGNATURES = {
     "gnn_split_count": (ctypes.c_int, [c_ptr, c_i64, c_i32, c_ptr, c_ptr]),
     "gnn_split_build": (
         ctypes.c_int,
-        [c_ptr, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+        [c_ptr, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
     "gnn_in_degree_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), c_ptr, c_ptr]),
     "gnn_gcn_norm_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), c_ptr, c_ptr]),

@@ -98,6 +98,7 @@ struct AggArgs {
   // long-segment split (gnn_split): main pass over truncated segments writes raw partials of
   // long segments to part[piece0[r]]; pieces / combine passes read the full segments
   const int32_t* piece0;   // null: no split
+  const int32_t* order;    // split main pass in degree order: position -> row (null: identity)
   float* part;
   const int32_t* fptr;
   const int32_t* fnbr;
@@ -189,10 +190,13 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
   const int nchunk = a.F / VEC;
   const int nch = (nchunk + LPS - 1) / LPS;
   const int32_t myptr = a.ptr[r0 + min(gl, nrow)];
+  // row of this lane's position (degree-ordered split main pass: positions are not rows)
+  const int32_t myrow = a.order ? a.order[r0 + min(gl, nrow - 1)] : (int32_t)(r0 + min(gl, nrow - 1));
   float mydeg = 1.0f;
-  if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[r0 + min(gl, nrow - 1)];
-  const int32_t mypiece = a.piece0 ? a.piece0[r0 + min(gl, nrow - 1)] : -1;
+  if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[myrow];
+  const int32_t mypiece = a.piece0 ? a.piece0[myrow] : -1;
   auto ptr_at = [&](int j) { return __shfl(myptr, gbase + j); };
+  auto row_at = [&](int j) { return a.order ? __shfl(myrow, gbase + j) : (int32_t)(r0 + j); };
 
   float acc[NCHMAX][VEC];
 #pragma unroll
@@ -202,7 +206,7 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 
   const uint64_t dseed = a.dropout ? agg_seed(a) : 0;
   auto flush = [&](int j) {
-    const int64_t r = r0 + j;
+    const int64_t r = row_at(j);
     float d = 1.0f;
     if constexpr (MODE == GNN_AGG_MEAN) d = fmaxf(__shfl(mydeg, gbase + j), 1.0f);
     const int32_t p0 = __shfl(mypiece, gbase + j);
@@ -241,6 +245,7 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
   const int32_t send = ptr_at(nrow);
   int j = 0;
   int32_t cend = ptr_at(1);
+  int32_t crow = row_at(0);
   for (int32_t s = ptr_at(0); s < send; s += kU) {
     int32_t n[kU];
 #pragma unroll
@@ -262,11 +267,12 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
         flush(j);
         ++j;
         cend = ptr_at(j + 1);
+        crow = row_at(j);
       }
 #pragma unroll
       for (int i = 0; i < NCHMAX; ++i)
         if (i < nch) {
-          contrib<MODE, VEC>(a, n[u], (int32_t)(r0 + j), k, (gl + LPS * i) * VEC, v[u][i]);
+          contrib<MODE, VEC>(a, n[u], crow, k, (gl + LPS * i) * VEC, v[u][i]);
 #pragma unroll
           for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];
         }
@@ -937,6 +943,7 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
     a.ptr = sp->ptr;
     a.nbr = sp->nbr;
     a.piece0 = sp->piece0;
+    a.order = sp->order;
     a.part = p->part;
     a.seg_len = sp->seg_len;
   }
@@ -950,6 +957,7 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
     a.ptr = p->transpose ? g->colptr : g->rowptr;
     a.nbr = p->transpose ? g->row : g->col;
     a.piece0 = nullptr;
+    a.order = nullptr;
     a.part = nullptr;
   }
   hipStream_t st = (hipStream_t)stream;

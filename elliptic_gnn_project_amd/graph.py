@@ -11,8 +11,9 @@ HBM layout of a plan (int32 throughout, N+1 / S entries):
     rowptr[N+1], col[S], csr_eid[S]       CSR by target (forward gathers)
     colptr[N+1], row[S], csc2csr[S]       CSC by source (backward gathers)
     deg[N] f32                             slots per target (mean count / GCN degree)
-    split (per direction, when a segment has > SPLIT_LEN slots): truncated ptr/nbr,
-      piece0[N], piece_seg[pieces], long_seg[long]   (K0b, graph_split.hip)
+    split (per direction, when a segment has > SPLIT_LEN slots): truncated ptr/nbr laid out
+      in degree order with order[N] (position -> segment), piece0[N], piece_seg[pieces],
+      long_seg[long]   (K0b, graph_split.hip)
     dinv[N] f32                            GCN deg^-1/2 (REPLACE plans only)
 """
 from __future__ import annotations
@@ -32,6 +33,11 @@ def _split_enabled() -> bool:
     return os.environ.get("GNNMP_SPLIT", "1") != "0"
 
 
+def _order_enabled() -> bool:
+    """Degree-ordered main pass of split directions (GNNMP_ORDER=0: plan order, for A/B timing)."""
+    return os.environ.get("GNNMP_ORDER", "1") != "0"
+
+
 def _build_split(lib, ptr: torch.Tensor, nbr: torch.Tensor, n: int, T: int, dev):
     """Long-segment split of one direction; None when no segment exceeds T slots."""
     counts = torch.zeros(3, dtype=torch.int64, device=dev)
@@ -48,17 +54,20 @@ def _build_split(lib, ptr: torch.Tensor, nbr: torch.Tensor, n: int, T: int, dev)
             "piece0": torch.empty(max(n, 1), **i32),
             "piece_seg": torch.empty(max(n_pieces, 1), **i32),
             "long_seg": torch.empty(max(n_long, 1), **i32),
+            "order": torch.empty(max(n, 1), **i32) if _order_enabled() else None,
         }
         nb = _lib.c_size(0)
         _lib.check(lib.gnn_split_workspace_size(n, nb), "gnn_split_workspace_size")
         ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
         _lib.check(lib.gnn_split_build(ptr.data_ptr(), nbr.data_ptr(), n, T, t["ptr"].data_ptr(),
                                        t["nbr"].data_ptr(), t["piece0"].data_ptr(), t["piece_seg"].data_ptr(),
-                                       t["long_seg"].data_ptr(), ws.data_ptr(), ws.numel(), stream),
+                                       t["long_seg"].data_ptr(), _lib.ptr(t["order"]), ws.data_ptr(), ws.numel(),
+                                       stream),
                    "gnn_split_build")
         torch.cuda.current_stream(dev).synchronize()  # ws is freed below
     t["c"] = _lib.GnnSplit(T, 0, n_long, n_pieces, t["ptr"].data_ptr(), t["nbr"].data_ptr(),
-                           t["piece0"].data_ptr(), t["piece_seg"].data_ptr(), t["long_seg"].data_ptr())
+                           t["piece0"].data_ptr(), t["piece_seg"].data_ptr(), t["long_seg"].data_ptr(),
+                           _lib.ptr(t["order"]))
     return t
 
 

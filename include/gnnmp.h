@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 14
+#define GNNMP_ABI_VERSION 15
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -71,6 +71,8 @@ typedef struct {
   const int32_t* piece0;      /* [N] partial-sum row of piece 0 of a long segment, -1 if short */
   const int32_t* piece_seg;   /* [num_pieces] segment of each piece */
   const int32_t* long_seg;    /* [num_long] the long segments */
+  const int32_t* order;       /* optional [N]: ptr/nbr position i holds segment order[i] (degree
+                                 order, longest first, stable); NULL: position i = segment i */
 } gnn_split;
 
 typedef struct {
@@ -112,14 +114,17 @@ gnn_status gnn_graph_build(const int64_t* edge_index, int64_t num_edges, int64_t
  * K0b  long-segment split of one direction (ptr/nbr = rowptr/col or colptr/row).
  * gnn_split_count writes {S_trunc, num_long, num_pieces} to device int64 counts[3] (the
  * caller reads them after the stream completes and sizes the outputs: tptr N+1, tnbr S_trunc,
- * piece0 N, piece_seg num_pieces, long_seg num_long).  gnn_split_build fills them.
+ * piece0 N, piece_seg num_pieces, long_seg num_long).  gnn_split_build fills them; with
+ * order (N entries, optional) the truncated tptr/tnbr are laid out in degree order (see
+ * gnn_split.order) — the lane-group gather (8 < F <= 32·vec) runs its main pass in that order.
  */
 gnn_status gnn_split_workspace_size(int64_t num_segs, size_t* bytes);
 gnn_status gnn_split_count(const int32_t* ptr, int64_t num_segs, int32_t seg_len, int64_t* counts,
                            gnn_stream_t stream);
 gnn_status gnn_split_build(const int32_t* ptr, const int32_t* nbr, int64_t num_segs, int32_t seg_len,
                            int32_t* tptr, int32_t* tnbr, int32_t* piece0, int32_t* piece_seg,
-                           int32_t* long_seg, void* workspace, size_t workspace_bytes, gnn_stream_t stream);
+                           int32_t* long_seg, int32_t* order, void* workspace, size_t workspace_bytes,
+                           gnn_stream_t stream);
 
 /* deg[i] = number of CSR slots of i as float (PyG `count` / `deg`, gnn.py:49 via SAGEConv mean). */
 gnn_status gnn_in_degree_f32(const gnn_graph* g, float* deg, gnn_stream_t stream);

@@ -87,7 +87,7 @@ def test_dropout_index_range_is_checked(lib):
 
 STRUCTS = {
     "gnn_split": ("GnnSplit", ["seg_len", "reserved", "num_long", "num_pieces", "ptr", "nbr", "piece0",
-                               "piece_seg", "long_seg"]),
+                               "piece_seg", "long_seg", "order"]),
     "gnn_graph": ("GnnGraph", ["num_nodes", "num_slots", "rowptr", "col", "colptr", "row", "csc2csr",
                                "csr_split", "csc_split"]),
     "gnn_agg_params": ("GnnAggParams", ["mode", "transpose", "nodew", "ew", "heads", "addend", "ld_add", "bias",
