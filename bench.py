@@ -226,7 +226,8 @@ def measured_traffic(tag):
     if tag[0] == "gemm_nt":
         M, N = tag[1], tag[3]
         grid = -(-M // 128) * 256 * -(-N // 128)
-        cand = [r for r in rows if "gemm_nt_ws" in r["kernel"]]  # the weight-stationary form
+        # the weight-stationary forms (split image / in-kernel split): one of them runs per build
+        cand = [r for r in rows if "gemm_nt_planes" in r["kernel"] or "gemm_nt_ws" in r["kernel"]]
         if len(cand) != 1:
             cand = [r for r in rows if "gemm_nt" in r["kernel"] and r["grid_threads"] == grid]
     elif tag[0] == "gemm_tn":

@@ -19,10 +19,12 @@ pytestmark = pytest.mark.gpu
 N_FULL, E_FULL = 203_769, 234_355
 
 
-def rel_l2(a, b):
+def rel_l2(a, b, floor=1e-30):
+    """Relative L2; ``floor`` bounds the divisor from below (the conv biases feeding BatchNorm have
+    an exactly-zero gradient, so both sides there are rounding noise: 1e-9 fp32 vs 1e-17 f64)."""
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()
-    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+    return float((a - b).norm() / max(float(b.norm()), floor))
 
 
 _CACHE = {}
@@ -67,7 +69,7 @@ def test_full_size_sage_train_step_gradients(device):
     torch.testing.assert_close(logits.detach().cpu().double(), ref_logits, rtol=1e-5, atol=1e-5)
     ref_loss, grads = pyg_ref.train_step_grads("sage", _f64(params), x64, data.edge_index, data.y, tm,
                                                cw.double(), **kw)
-    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
     for k, v in model.named_parameters():
         assert rel_l2(v.grad, grads[k]) < 1e-5, (k, rel_l2(v.grad, grads[k]))
 
@@ -136,9 +138,12 @@ def _resbn_step_vs_oracle(device, data):
     ref_loss, grads = pyg_ref.train_step_grads(
         "sage_resbn", p64, x64, data.edge_index, data.y, tm, cw.double(),
         bn_state={k: v.clone() for k, v in p64.items() if "running" in k}, **kw)
-    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
     for k, v in model.named_parameters():
-        assert rel_l2(v.grad, grads[k]) < 1e-5, (k, rel_l2(v.grad, grads[k]))
+        # a hidden conv's bias feeds BatchNorm: its true gradient is zero, so hold it to 1e-7 absolute
+        zero = k.startswith("convs.") and k.endswith("lin_l.bias") and int(k.split(".")[1]) < L - 1
+        e = rel_l2(v.grad, grads[k], floor=1e-2 if zero else 1e-30)
+        assert e < 1e-5, (k, e)
     assert int(model.state_dict()["bns.0.num_batches_tracked"]) == 1
 
 
@@ -194,7 +199,7 @@ def test_full_size_train_step_gradients(device, arch, hidden, heads):
     torch.testing.assert_close(logits.detach().cpu().double(), ref_logits, rtol=1e-5, atol=1e-5)
     ref_loss, grads = pyg_ref.train_step_grads(arch, _f64(params), x64, data.edge_index, data.y, tm,
                                                cw.double(), **kw)
-    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
     for k, v in model.named_parameters():
         assert rel_l2(v.grad, grads[k]) < 1e-5, (k, rel_l2(v.grad, grads[k]))
 
