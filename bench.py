@@ -441,8 +441,11 @@ def main():
             # launch latency between an event and its kernel as kernel time)
             torch.cuda._sleep(50_000_000)
             eager_step()
-        recs = KernelTimer.stop()
+        gap = KernelTimer.dispatch_gap_ms()
+        recs = KernelTimer.stop(gap)
         roof = roofline(recs)
+        if roof is not None:
+            roof["dispatch_gap_us"] = round(gap * 1e3, 2)  # taken off every bracket (rocprof excludes it)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -134,7 +134,10 @@ __device__ __forceinline__ void contrib(const AggArgs& a, int32_t n, int32_t r, 
 #pragma unroll
     for (int q = 0; q < VEC; ++q) v[q] = v[q] / d;
   } else if constexpr (MODE == GNN_AGG_GCN) {
-    float w = a.nodew[n] * a.nodew[r];
+    // PyG's message edge_weight * x_j, rounded, then summed (this file builds with
+    // -ffp-contract=off: an FMA with the accumulation would depend on the code path a walk step
+    // takes, and PyG rounds the message before the scatter-add)
+    const float w = a.nodew[n] * a.nodew[r];
 #pragma unroll
     for (int q = 0; q < VEC; ++q) v[q] = w * v[q];
   } else if constexpr (MODE == GNN_AGG_EDGE_W) {
@@ -179,7 +182,9 @@ __device__ __forceinline__ void finish(const AggArgs& a, int64_t r, int f0, floa
 
 constexpr int kU = 4;  // slots in flight per group (r11 lab: 8 measured 12-25 % slower on every F = 64 case)
 
-template <int MODE, int VEC, int LPS, int NCHMAX>
+// PF: the next kU neighbour ids are loaded behind this walk step's row loads (one dependent
+// round trip per step instead of two).
+template <int MODE, int VEC, int LPS, int NCHMAX, bool PF = false>
 __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
   const int gl = threadIdx.x & (LPS - 1);
   const int gbase = (threadIdx.x & 63) & ~(LPS - 1);
@@ -246,10 +251,17 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
   int j = 0;
   int32_t cend = ptr_at(1);
   int32_t crow = row_at(0);
-  for (int32_t s = ptr_at(0); s < send; s += kU) {
-    int32_t n[kU];
+  const int32_t sbeg = ptr_at(0);
+  int32_t n[kU];
+  if constexpr (PF) {
 #pragma unroll
-    for (int u = 0; u < kU; ++u) n[u] = a.nbr[s + u < send ? s + u : s];
+    for (int u = 0; u < kU; ++u) n[u] = a.nbr[sbeg + u < send ? sbeg + u : max(send - 1, sbeg)];
+  }
+  for (int32_t s = sbeg; s < send; s += kU) {
+    if constexpr (!PF) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) n[u] = a.nbr[s + u < send ? s + u : s];
+    }
     float v[kU][NCHMAX][VEC];
 #pragma unroll
     for (int u = 0; u < kU; ++u)
@@ -259,6 +271,11 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
           const int c = gl + LPS * i;
           vload<VEC>(a.x + (int64_t)n[u] * a.ldx + (c < nchunk ? c : 0) * VEC, v[u][i]);
         }
+    int32_t nn[kU];
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) nn[u] = a.nbr[min(s + kU + u, send - 1)];
+    }
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int32_t k = s + u;
@@ -276,6 +293,10 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
           for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];
         }
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) n[u] = nn[u];
     }
   }
   for (; j < nrow; ++j) flush(j);  // the last open row and any trailing empty rows
@@ -781,10 +802,20 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     // dropout 97.5 -> 89.2 us, CSC bwd 49.4 -> 41.3 us (profiles/lab_agg.py, r08; 4 rows: 91.5 /
     // 41.7, lps - 1 = 15 rows: 116.9 / 48.7).  Lab 5 / 6 / 8: 4 / 8 / lps - 1 rows.
     const int lv = g_agg_lab_variant;
-    const int rpg = lv == 5 ? 4 : lv == 6 ? 8 : lv == 8 ? lps - 1 : (lps == 8 ? 7 : lps == 16 ? 2 : 8);
+    // degree-ordered split main pass (a.order): ONE row per group — a wave's groups hold rows of
+    // the same length, so they walk in lockstep and nothing is gained by walking several rows
+    // flat; more, shorter-lived groups hide more latency (r14 lab, F = 64: SAGE mean fwd 59.7 ->
+    // 50.3 us, CSC mean bwd 80.0 -> 62.9, GCN fwd 73.5 -> 59.1; plan order at 2 rows: 71 / 98 / 84)
+    const int rpg = lv == 5 ? 4 : lv == 6 ? 8 : lv == 8 ? lps - 1 : (lv == 9 || lv == 11) ? 1
+                  : a.order ? 1 : (lps == 8 ? 7 : lps == 16 ? 2 : 8);
     const int64_t groups = ceil_div(a.nrows, rpg);
     const unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
-#define GNN_FLAT(V, L, NC) agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg)
+    const bool pf = lv == 10 || lv == 11;  // lab: neighbour-id prefetch (r14: 5-10 us slower)
+#define GNN_FLAT(V, L, NC)                                                      \
+  do {                                                                          \
+    if (pf) agg_flat_kernel<MODE, V, L, NC, true><<<blocks, 256, 0, st>>>(a, rpg); \
+    else agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg);         \
+  } while (0)
 #define GNN_FLAT_V(V)                      \
   do {                                     \
     if (lps == 64) GNN_FLAT(V, 64, 4);     \
