@@ -103,6 +103,9 @@ def _ld(x: torch.Tensor) -> int:
     return max(int(x.stride(0)), int(x.size(1)), 1)
 
 
+SPLIT_MAX_F = 128  # widest rows the long-segment split runs for (the lane-group gather)
+
+
 def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = False,
               nodew: torch.Tensor | None = None, ew: torch.Tensor | None = None, heads: int = 1,
               addend: torch.Tensor | None = None, bias: torch.Tensor | None = None,
@@ -124,7 +127,7 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
         addend = _as_f32_rows(addend)
     # partial-sum rows for the long-segment split (used by the lane-group gather, 8 < F <= 128;
     # the narrow F <= 4 kernels measured no faster with it on the bench graph)
-    npieces = plan.split_pieces(transpose) if (mode != _lib.AGG_EDGE_W and 8 < F <= 128) else 0
+    npieces = plan.split_pieces(transpose) if (mode != _lib.AGG_EDGE_W and 8 < F <= SPLIT_MAX_F) else 0
     part = torch.empty(npieces * F, dtype=torch.float32, device=x.device) if npieces else None
     p = _lib.GnnAggParams(
         mode, int(transpose), _lib.ptr(nodew), _lib.ptr(ew), int(heads),

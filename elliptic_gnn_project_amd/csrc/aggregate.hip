@@ -315,9 +315,11 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
   const int nchunk = a.F / VEC;
   const int32_t myptr = a.ptr[r0 + min(lane, nrow)];
+  const int32_t myrow = a.order ? a.order[r0 + min(lane, nrow - 1)] : (int32_t)(r0 + min(lane, nrow - 1));
   float mydeg = 1.0f;
-  if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[r0 + min(lane, nrow - 1)];
-  const int32_t mypiece = a.piece0 ? a.piece0[r0 + min(lane, nrow - 1)] : -1;
+  if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[myrow];
+  const int32_t mypiece = a.piece0 ? a.piece0[myrow] : -1;
+  auto row_at = [&](int j) { return a.order ? __builtin_amdgcn_readlane(myrow, j) : (int32_t)(r0 + j); };
   int coff[NCH];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
@@ -332,7 +334,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 
   const uint64_t dseed = a.dropout ? agg_seed(a) : 0;
   auto flush = [&](int j) {
-    const int64_t r = r0 + j;
+    const int64_t r = row_at(j);
     float d = 1.0f;
     if constexpr (MODE == GNN_AGG_MEAN) d = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mydeg), j)), 1.0f);
     const int32_t p0 = __builtin_amdgcn_readlane(mypiece, j);
@@ -394,6 +396,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   const int32_t send = __builtin_amdgcn_readlane(myptr, nrow);
   int j = 0;
   int32_t cend = __builtin_amdgcn_readlane(myptr, 1);
+  int32_t crow = row_at(0);
   int32_t n[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) n[u] = __builtin_amdgcn_readfirstlane(a.nbr[min(sbeg + u, max(send - 1, sbeg))]);
@@ -417,10 +420,11 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
         flush(j);
         ++j;
         cend = __builtin_amdgcn_readlane(myptr, j + 1);
+        crow = row_at(j);
       }
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
-        contrib<MODE, VEC>(a, n[u], (int32_t)(r0 + j), k, coff[i], v[u][i]);
+        contrib<MODE, VEC>(a, n[u], crow, k, coff[i], v[u][i]);
 #pragma unroll
         for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];
       }
@@ -829,7 +833,7 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
       // padded pitch (dwordx4, one load per row) 89.0 — the gather is not instruction-bound.
       // XCD-grouped block order (each XCD sweeping one contiguous eighth of the rows) measured
       // slower with cold caches (r10: 130.4 -> 138.5 us).  Lab 1 / 2 / 3: 8 / 4 / 32 rows.
-      const int rpw = lv == 1 ? 8 : lv == 2 ? 4 : lv == 3 ? 32 : 16;
+      const int rpw = (lv == 1 || lv == 14) ? 8 : (lv == 2 || lv == 13) ? 4 : lv == 3 ? 32 : 16;
       const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
       // (r13 lab: U = 16 neighbour rows in flight instead of 8, 98.5 -> 308.7 us warm — register
       // pressure; not kept)
@@ -983,7 +987,9 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
   // The split pays only for the lane-group gather (8..32 lanes per row, one row at a time per
   // group): r01 measurements — F=64 GCN fwd 72 -> 37 µs; the wave-wide gather (F/vec > 32) and
   // the narrow LDS/group kernels lose to the two extra launches.
-  if (sp && (F <= 8 || F / vec > 32 || g_agg_lab_variant == 7)) sp = nullptr;  // lab 7: no split
+  // (lab 12 / 13 / 14: the split, degree-ordered, for the wave-wide gather too, 16 / 4 / 8 rows per wave)
+  const bool lab_wsplit = g_agg_lab_variant >= 12 && g_agg_lab_variant <= 14;
+  if (sp && (F <= 8 || (F / vec > 32 && !lab_wsplit) || g_agg_lab_variant == 7)) sp = nullptr;  // lab 7: no split
   if (!sp) {
     a.ptr = p->transpose ? g->colptr : g->rowptr;
     a.nbr = p->transpose ? g->row : g->col;

@@ -34,6 +34,9 @@ def main():
                     help="evict L2 / Infinity Cache (write 1 GB) before every timed call, time calls one at a time")
     args = ap.parse_args()
     variants = [int(v) for v in args.variants.split(",")]
+    if any(12 <= v <= 14 for v in variants):  # wave-gather split variants need the partial buffer
+        import elliptic_gnn_project_amd.aggregation as agg_mod
+        agg_mod.SPLIT_MAX_F = 512
     lib = _lib.load()
     setv = lib.gnnx_set_agg_variant
     setv.argtypes = [ctypes.c_int]
