@@ -3,9 +3,21 @@
 #pragma once
 #include "common.hpp"
 
+#include <utility>
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 namespace gnnmp {
+
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 
 // Dropout keep decision for element `idx` of a call seeded with `seed`: murmur3's fmix32
@@ -175,8 +187,13 @@ void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st);
 // the split-image forms (gemm_ws.hip NT, gemm_planes.hip TN): shapes they take, launchers
 bool nt_planes_ok(const NTArgs& a);
 void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st);
+// the bf16 image form (gemm_ws.hip): bf16 storage, one product per MFMA, LDS-DMA staged
+bool nt_img16_ok(const NTArgs& a);
+void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st);
 bool tn_planes_ok(const TNArgs& a);
 void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st);
+bool tn_img16_ok(const TNArgs& a);
+void launch_tn_img16(const TNArgs& a, int nblk, hipStream_t st);
 // 3 planes of one f32 split: hi = RNE(v), mid = RNE(v - hi), lo = RNE(v - hi - mid), exact sum
 __device__ __forceinline__ void split3_pair(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
   typedef __bf16 bf16x2_ __attribute__((ext_vector_type(2)));

@@ -797,6 +797,13 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
     a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
     a.ap_ps = p->planes_stride;
     const size_t img_bytes = (size_t)(a.ap_ld / 16) * 3 * 256 * sizeof(uint4);
+    if (a.a_bf16) {  // a bf16 image (one plane): the bf16-storage form
+      if (p->math != GNN_MATH_F32 && !p->mask && nt_img16_ok(a) && p->workspace && p->workspace_bytes >= img_bytes) {
+        launch_nt_img16(a, static_cast<uint4*>(p->workspace), st);
+        return hip_check(hipGetLastError(), fn);
+      }
+      return fail(GNN_ERR_UNSUPPORTED, fn, "bf16 image A outside the image kernel's shapes");
+    }
     if (p->math != GNN_MATH_F32 && !p->mask && nt_planes_ok(a) && p->workspace &&
         p->workspace_bytes >= img_bytes) {
       launch_nt_ws_planes(a, static_cast<uint4*>(p->workspace), st);
@@ -905,6 +912,15 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
     a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
     a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
     a.ap_ps = p->planes_stride;
+    if (a.a_bf16) {  // a bf16 image (one plane): the bf16-storage form
+      if (p->math == GNN_MATH_F32 || !tn_img16_ok(a))
+        return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 image A outside the image kernel's shapes");
+      launch_tn_img16(a, nblk, st);
+      GNN_LAUNCH_CHECK();
+      slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+      GNN_LAUNCH_CHECK();
+      return GNN_OK;
+    }
     if (p->math != GNN_MATH_F32 && tn_planes_ok(a)) {
       launch_tn_planes(a, nblk, st);
       GNN_LAUNCH_CHECK();
@@ -960,7 +976,7 @@ extern "C" int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p) {
   a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
   a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
   a.ap_ps = p->planes_stride;
-  return nt_planes_ok(a) ? 1 : 0;
+  return (a.a_bf16 ? nt_img16_ok(a) : nt_planes_ok(a)) ? 1 : 0;
 }
 
 extern "C" int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p) {
@@ -973,5 +989,5 @@ extern "C" int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p) {
   a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
   a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
   a.ap_ps = p->planes_stride;
-  return tn_planes_ok(a) ? 1 : 0;
+  return (a.a_bf16 ? tn_img16_ok(a) : tn_planes_ok(a)) ? 1 : 0;
 }

@@ -24,6 +24,8 @@
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2v_t __attribute__((ext_vector_type(2)));
+typedef float f32x2v_t __attribute__((ext_vector_type(2)));
 
 namespace gnnmp {
 namespace {
@@ -391,6 +393,248 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
     slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
 }
 
+// ------------------------------------------------------------------ TN over a bf16 image
+// bf16 storage (BASELINE configs[4]): A = a one-plane bf16 image (planes.BfImage), h bf16, G
+// rounded to bf16 for the MFMA (one product), f32 accumulation.  One MFMA per k-tile per 16-row
+// chunk (11 per wave at K = 336) is far too short a phase to hide a chunk's loads behind, so the
+// loads run D chunks ahead in a register ring (slots indexed at compile time: the chunk loop is
+// unrolled by D):
+//   step c:  A(c+1) pieces -> LDS, G(c+1) formed from the ring slot and dz(c+1) -> LDS (bf16)
+//            | the slot refilled with chunk c+1+D | dz(c+2) -> the LDS dz ring, its slot refilled
+//            with dz(c+2+D) | the KT MFMAs of chunk c | barrier
+// Geometry, the G formation, masks, side sums and slab layout are the split-image kernel's above.
+template <bool PROJ, bool MASK, int KT, bool GOUT, int D>
+__global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
+  constexpr int NPA = 3;  // A pieces per thread per chunk (16 rows x <= 42 pieces <= 768)
+  __shared__ __attribute__((aligned(16))) uint16_t Gt[2][PT_GPL];
+  __shared__ __attribute__((aligned(16))) uint16_t At[2][PT_APL];
+  __shared__ float dzL[2][256];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int ld = a.ap_ld;
+  const int pr = ld >> 3;
+  const int64_t mbeg = (int64_t)blockIdx.x * a.rows_per_block;
+  const int64_t mend = min(a.M, mbeg + a.rows_per_block);
+  const int nch = mend > mbeg ? (int)((mend - mbeg + PT_ROWS - 1) / PT_ROWS) : 0;
+
+  floatx16 acc[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+
+  const __amdgpu_buffer_rsrc_t arsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.ap), 0, (int)(a.ap_ps * 2), 0x00020000);
+  uint32_t goff[NPA], loff[NPA];
+#pragma unroll
+  for (int j = 0; j < NPA; ++j) {
+    const int q = tid + 256 * j;
+    const bool ok = q < PT_ROWS * pr;
+    const int row = q / pr, c16 = q - row * pr;
+    goff[j] = ok ? (uint32_t)(((int64_t)row * ld + 8 * c16) * 2) : 0u;
+    loff[j] = ok ? (uint32_t)((row * PT_AP + 8 * c16) * 2)
+                 : (uint32_t)(((tid & 15) * PT_AP + PT_MAXLD + 8 * ((tid >> 4) & 1)) * 2);
+  }
+  // G slot: column gn, rows 8·go .. +8 of the chunk
+  const int gn = tid & 127, go = tid >> 7;
+  const bool gcol = gn < a.Nr;
+  const int gnc = gcol ? gn : 0;
+  const uint16_t* hbase = reinterpret_cast<const uint16_t*>(a.h) + gnc;
+  const float* gbase = a.g + gnc;
+  const int zr = (tid & 63) / MAXPROJ, zq = (tid & 63) % MAXPROJ;
+  const int zqc = PROJ ? min(zq, a.nproj - 1) : 0;
+  float pcol[MAXPROJ];
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (PROJ && q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
+
+  const int Mi = (int)a.M;
+  auto ldbase = [&](int c) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
+  const int clast = max(nch - 1, 0);
+  // the register ring (slot d: one chunk's A pieces, h / g column values, dz value)
+  u32x4 ra[D][NPA];
+  uint32_t rh[D][4];  // h: 8 bf16 of the slot's column, packed in pairs
+  float rg[D][8];
+  float rz[D];
+  auto load_chunk = [&](int d, int c) {  // c clamped by the caller
+    const int mb = ldbase(c);
+#pragma unroll
+    for (int j = 0; j < NPA; ++j) ra[d][j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], mb * ld * 2, 0);
+    if constexpr (MASK) {
+      uint32_t o = (uint32_t)((mb + 8 * go) * (int)a.ldh);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t lo = hbase[o], hi = hbase[o + (uint32_t)a.ldh];
+        rh[d][i] = lo | (hi << 16);
+        o += 2u * (uint32_t)a.ldh;
+      }
+    }
+    if constexpr (!PROJ) {
+      uint32_t o = (uint32_t)((mb + 8 * go) * (int)a.ldg);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        rg[d][i] = gbase[o];
+        o += (uint32_t)a.ldg;
+      }
+    }
+  };
+  auto load_z = [&](int d, int c) {
+    if constexpr (PROJ) rz[d] = a.dz[(uint32_t)((ldbase(c) + zr) * (int)a.lddz + zqc)];
+  };
+  auto put_z = [&](int d, int k) {  // dz of chunk k into its LDS ring slot (zero outside the block's rows)
+    if constexpr (PROJ) {
+      const int mb = ldbase(k);
+      const bool ok = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + k * PT_ROWS - mb && zr < (int)mend - mb;
+      dzL[k & 1][tid] = ok ? rz[d] : 0.0f;
+    }
+  };
+
+  float db = 0.f, dzs = 0.f;
+  float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
+  // chunk c's A pieces and G column (from ring slot d) into LDS buffer c & 1
+  auto put_chunk = [&](int d, int c) {
+    const int buf = c & 1;
+#pragma unroll
+    for (int j = 0; j < NPA; ++j) *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(At[buf]) + loff[j]) = ra[d][j];
+    const int mb = ldbase(c);
+    uint32_t w[4];
+#pragma unroll
+    for (int i2 = 0; i2 < 4; ++i2) {
+      float gv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = 2 * i2 + u;
+        const int r = 8 * go + i;
+        float e;
+        if constexpr (PROJ) {
+          const float4 z = *reinterpret_cast<const float4*>(&dzL[buf][r * MAXPROJ]);
+          e = z.x * pcol[0];
+          e = fmaf(z.y, pcol[1], e);
+          e = fmaf(z.z, pcol[2], e);
+          e = fmaf(z.w, pcol[3], e);
+          dzs += gn < MAXPROJ ? dzL[buf][r * MAXPROJ + (gn & (MAXPROJ - 1))] : 0.0f;
+          if constexpr (MASK) {
+            const float hv = __uint_as_float(u ? (rh[d][i2] & 0xffff0000u) : (rh[d][i2] << 16));
+            dw2[0] = fmaf(z.x, hv, dw2[0]);
+            dw2[1] = fmaf(z.y, hv, dw2[1]);
+            dw2[2] = fmaf(z.z, hv, dw2[2]);
+            dw2[3] = fmaf(z.w, hv, dw2[3]);
+          }
+        } else {
+          e = rg[d][i];
+        }
+        float g = e;
+        if constexpr (MASK) {
+          const float hv = __uint_as_float(u ? (rh[d][i2] & 0xffff0000u) : (rh[d][i2] << 16));
+          g = hv > 0.0f ? g * a.hscale : 0.0f;
+        }
+        const bool ok = r >= (int)mbeg + c * PT_ROWS - mb && r < (int)mend - mb && gcol;
+        if constexpr (!PROJ) g = ok ? g : 0.0f;
+        db += g;
+        if constexpr (GOUT) {
+          if (a.gout && ok) a.gout[(int64_t)(mb + r) * a.ldgout + gn] = g;
+        }
+        gv[u] = g;
+      }
+      w[i2] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v_t){gv[0], gv[1]}, bf16x2v_t));
+    }
+    *reinterpret_cast<uint4*>(Gt[buf] + gn * PT_GP + 8 * go) = make_uint4(w[0], w[1], w[2], w[3]);
+  };
+
+  const int gfo = (32 * wave + (lane & 31)) * PT_GP + 8 * (lane >> 5);
+  const int grp = lane >> 4, li = lane & 15;
+  const int afo = (8 * (grp >> 1) + (li >> 2)) * PT_AP + 16 * (grp & 1) + 4 * (li & 3);
+  auto compute = [&](int c) {
+    const int buf = c & 1;
+    const bf16x8 gf = *reinterpret_cast<const bf16x8*>(Gt[buf] + gfo);
+    const uint16_t* ab = At[buf] + afo;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const uint16_t* q = ab + t * 32;
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf, cat_frag(tr_read(q), tr_read(q + 4 * PT_AP)), acc[t], 0, 0, 0);
+    }
+  };
+
+  if (nch > 0) {
+    // prologue: ring slots d hold chunk d and dz(d); dz(0), dz(1) -> LDS; chunk 0 -> LDS
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      load_chunk(d, min(d, clast));
+      load_z(d, min(d, clast));
+    }
+    put_z(0, 0);
+    put_z(1, 1);
+    load_z(0, min(D, clast));
+    load_z(1, min(D + 1, clast));
+    __syncthreads();  // dzL
+    put_chunk(0, 0);
+    load_chunk(0, min(D, clast));
+    __syncthreads();
+    for (int c0 = 0; c0 < nch; c0 += D) {
+      static_for<D>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        const int c = c0 + d;
+        if (c < nch) {
+          constexpr int d1 = (d + 1) % D, d2 = (d + 2) % D;
+          put_chunk(d1, c + 1);                 // chunk c + 1 (rows past the block: zero G)
+          load_chunk(d1, min(c + 1 + D, clast));
+          put_z(d2, c + 2);
+          load_z(d2, min(c + 2 + D, clast));
+          compute(c);
+          __syncthreads();
+        }
+      });
+    }
+  }
+
+  // ---- this block's partial dW (segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2])
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
+  const int Kc = a.k1 + a.k2;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int kp = t * 32 + (lane & 31);
+    const bool s1 = kp < a.k1;
+    const bool s2 = kp >= a.ap_col2 && kp < a.ap_col2 + a.k2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int64_t idx = s1 ? (int64_t)row * a.k1 + kp : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (kp - a.ap_col2);
+      if (row < a.Nr && (s1 || s2)) slab[idx] = acc[t][r];
+    }
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(&At[0][0]);
+  constexpr int ns = 2 + MAXPROJ;
+  red[(go * 128 + gn) * ns + 0] = db;
+  red[(go * 128 + gn) * ns + 1] = dzs;
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
+  __syncthreads();
+  if (tid < 128 && tid < a.Nr) {
+    float* side = slab + (int64_t)a.Nr * Kc;
+    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
+    for (int q = 0; q < a.nproj; ++q)
+      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+  }
+  if (PROJ && tid < a.nproj)
+    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+}
+
+template <bool PROJ, bool MASK, int KT>
+void launch_tn_img16_k(const TNArgs& a, int nblk, hipStream_t st) {
+  if (a.gout) gemm_tn_img16_kernel<PROJ, MASK, KT, true, 4><<<nblk, 256, 0, st>>>(a);
+  else gemm_tn_img16_kernel<PROJ, MASK, KT, false, 4><<<nblk, 256, 0, st>>>(a);
+}
+
+template <int KT>
+void launch_tn_img16_kt(const TNArgs& a, int nblk, hipStream_t st) {
+  const bool proj = a.dz != nullptr, mask = a.h != nullptr;
+  if (proj && mask) launch_tn_img16_k<true, true, KT>(a, nblk, st);
+  else if (proj) launch_tn_img16_k<true, false, KT>(a, nblk, st);
+  else if (mask) launch_tn_img16_k<false, true, KT>(a, nblk, st);
+  else launch_tn_img16_k<false, false, KT>(a, nblk, st);
+}
+
 template <bool PROJ, bool MASK, int KT>
 void launch_tn_planes_k(const TNArgs& a, int nblk, hipStream_t st) {
   if (a.gout) gemm_tn_planes_kernel<PROJ, MASK, KT, true><<<nblk, 256, 0, st>>>(a);
@@ -407,6 +651,21 @@ void launch_tn_planes_kt(const TNArgs& a, int nblk, hipStream_t st) {
 }
 
 }  // namespace
+
+// the bf16 image form: one-plane bf16 image (ld 256 or 336), h bf16 when given
+bool tn_img16_ok(const TNArgs& a) {
+  if (!a.ap || !a.a_bf16 || (a.h && !a.h_bf16)) return false;
+  if ((a.ap_ld != 256 && a.ap_ld != 336) || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;
+  if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
+  if (a.ap_ps < a.M * (int64_t)a.ap_ld || a.ap_ps * 2 >= ((int64_t)1 << 31) || a.M < PT_ROWS) return false;
+  const int64_t ldmax = std::max({a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
+  return (a.M + 32) * ldmax < ((int64_t)1 << 31);
+}
+
+void launch_tn_img16(const TNArgs& a, int nblk, hipStream_t st) {
+  if (a.ap_ld == 256) launch_tn_img16_kt<8>(a, nblk, st);
+  else launch_tn_img16_kt<11>(a, nblk, st);
+}
 
 bool tn_planes_ok(const TNArgs& a) {
   if (!a.ap || a.a_bf16 || a.h_bf16) return false;

@@ -424,15 +424,6 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
   }
 }
 
-// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
 
 // ---------------------------------------------------------------- the split-image form (K7a-p)
 // A read from a split image (NTArgs::ap, gemm_planes.hip): every (plane, k-step) block of a
@@ -698,6 +689,195 @@ __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uin
   }
 }
 
+// ---------------------------------------------------------------- bf16 image form (K7a-b)
+// bf16 storage (BASELINE configs[4]): A is a bf16 image [M][ld] (one plane; ld = 16·NKS; A1 in
+// columns [0, k1), A2 in [col2, col2 + k2), zeros elsewhere), B the Linear weights rounded to bf16
+// (plane 0 of the ws B image: RNE(W)), C bf16.  One product per MFMA, so the kernel is HBM-bound
+// (A once, C once) and its staging is an LDS-DMA ring: every 1 KB k-step block of a 32-row tile is
+// ONE global_load_lds_dwordx4 (lane l: row l/2, k-half (l & 1) ^ bit 3 of the row — the fragment
+// layout above, lane-linear), NBUF tile buffers with NBUF - 1 tiles in flight across each raw
+// s_barrier (counted vmcnt: the DMA and the E2 stores are the loop's only vector-memory ops).
+// One 256-thread block per CU sweeps tiles t = blockIdx.x, += gridDim.x; wave w owns columns
+// 32w .. +32 with its B fragments stationary in VGPRs.  Per tile:
+//   wait for its DMA, barrier | E2 of the previous tile from its C tile: coalesced 16-byte bf16 C
+//   row stores and the projection z = h·Pᵀ of the ROUNDED h | DMA of tile + NBUF - 1 | NKS MFMAs
+//   | E1: bias, ReLU, counter-hash dropout, bf16 rounding -> this tile's C tile (two, alternating).
+// All LDS in one array (a second __shared__ object can make hipcc wait vmcnt(0) at ds_reads).
+template <int NKS, int EPI, int NBUF>
+__global__ __launch_bounds__(256) void gemm_nt_img16_kernel(NTArgs a, const uint4* __restrict__ bimg, int ntiles) {
+  constexpr int QW = (NKS + 3) / 4;             // DMA instructions per wave per tile (uniform count)
+  constexpr int ABUF = NKS * WS_KSB;
+  constexpr int SCR = NBUF * ABUF;              // 1 KB target of the count-padding DMAs
+  constexpr int CT0 = SCR + 1024;               // two C tiles [32][BN] f32
+  constexpr int CTB = WS_ROWS * BN * 4;
+  constexpr int LDSB = CT0 + 2 * CTB;
+  constexpr bool PROJ = (EPI & WS_PROJ) != 0;
+  constexpr int S = 2 + (PROJ ? 1 : 0);         // E2's stores per thread
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: the DMA targets are wave-uniform
+  const int64_t M = a.M;
+  const int Nc = a.Nc;
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  const int G = gridDim.x;
+
+  // ---- stationary B: columns 32·wave .. +32, all k-steps, plane 0
+  bf16x8 bw[NKS];
+  {
+    const int slot = 2 * (32 * wave + (lane & 31)) + (lane >> 5);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) bw[s] = __builtin_bit_cast(bf16x8, bimg[(s * 3) * 256 + slot]);
+  }
+  // ---- the LDS-DMA of one tile (rows clamped into the image: tail rows repeat row M - 1 and
+  //      their C rows are dropped by the store range)
+  const int ld = a.ap_ld;
+  const int prow = lane >> 1;
+  const int khalf = (lane & 1) ^ ((prow >> 3) & 1);
+  // The DMA is an asm statement (M0 written in the same statement): hipcc's waitcnt pass cannot
+  // tell DMA targets from the C-tile and fragment reads in the one LDS array and would drain every
+  // DMA (vmcnt(0)) at the first ds_read after each barrier; hidden from it, only the counted
+  // waits below order the ring.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  auto glds16 = [](const uint16_t* src, uint32_t dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+  };
+  auto dma = [&](int tt, int buf) {
+    const int tc = min(tt, ntiles - 1);
+    const int64_t row = min((int64_t)tc * WS_ROWS + prow, M - 1);
+    const uint16_t* src = a.ap + row * ld + 8 * khalf;
+#pragma unroll
+    for (int i = 0; i < QW; ++i) {
+      const int b = wave + 4 * i;
+      if (b < NKS) glds16(src + 16 * b, lds0 + (uint32_t)(buf * ABUF + b * WS_KSB));
+      else glds16(src, lds0 + (uint32_t)SCR);
+    }
+  };
+  // vmcnt(N) alone (expcnt / lgkmcnt at their maxima), gfx9 encoding
+  auto wait_vm = [](auto nc) {
+    constexpr int N = decltype(nc)::value;
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  };
+
+  const int frow = lane & 31;
+  const uint32_t foff = (uint32_t)(frow * 32 + (((lane >> 5) ^ ((frow >> 3) & 1)) << 4));
+  const int col = 32 * wave + (lane & 31);
+  const bool colok = col < Nc;
+  const uint32_t hstep = (uint32_t)Nc * kDropGolden;
+  // projection: this thread's row of the C tile and column slice, its P[q][slice] in registers
+  const int prow8 = tid >> 3, pcb = tid & 7;
+  float preg[MAXPROJ][16];
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int c = 16 * pcb + j;
+      preg[q][j] = (PROJ && q < a.nproj && c < Nc) ? a.proj[(int64_t)q * Nc + c] : 0.f;
+    }
+  float bv = 0.f;
+  if constexpr ((EPI & WS_BIAS) != 0) bv = colok ? a.bias[col] : 0.f;
+  const int64_t ldc = a.ldc;
+  const __amdgpu_buffer_rsrc_t crsrc = __builtin_amdgcn_make_buffer_rsrc(a.c, 0, (int)(M * ldc * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t zrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(a.z, 0, PROJ ? (int)(M * a.ldz * 4) : 0, 0x00020000);
+
+  // E1: the tile's accumulators -> C tile (bias, ReLU, dropout, bf16 rounding)
+  auto e1 = [&](const floatx16& acc, int tt, float* ct) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int rl = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+      float x = acc[j] + bv;
+      if constexpr ((EPI & WS_RELU) != 0) x = fmaxf(x, 0.f);
+      if constexpr ((EPI & WS_DROP) != 0) {  // == keep_elem(seed, row·Nc + col), bit for bit
+        const uint32_t h0 = ((uint32_t)(tt * WS_ROWS) * (uint32_t)Nc + (uint32_t)col) * kDropGolden + (uint32_t)seed;
+        x = keep_premixed(h0 + (uint32_t)rl * hstep, seed, a.keep_thresh) ? x * a.drop_scale : 0.f;
+      }
+      const uint32_t hb = ws_pk(x, 0.f) & 0xffffu;  // RNE to bf16: what C stores
+      ct[rl * BN + col] = colok ? __uint_as_float(hb << 16) : 0.f;
+    }
+  };
+  // E2: coalesced bf16 C rows (16 columns of 8 per row, 2 per thread) and the projection
+  auto e2 = [&](int tp, const float* ct) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int u = tid + 256 * q;
+      const int rl = u >> 4, c8 = (u & 15) * 8;
+      const float4 v0 = *reinterpret_cast<const float4*>(ct + rl * BN + c8);
+      const float4 v1 = *reinterpret_cast<const float4*>(ct + rl * BN + c8 + 4);
+      const u32x4 w = {ws_pk(v0.x, v0.y), ws_pk(v0.z, v0.w), ws_pk(v1.x, v1.y), ws_pk(v1.z, v1.w)};
+      const uint32_t off = (c8 < Nc && tp >= 0) ? (uint32_t)((((int64_t)tp * WS_ROWS + rl) * ldc + c8) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(w, crsrc, (int)off, 0, 0);
+    }
+    if constexpr (PROJ) {  // thread: row tid / 8, columns 16·(tid % 8) .. +16 (its P slice in registers)
+      const float* hr = ct + prow8 * BN + 16 * pcb;
+      float zq[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const float4 h = *reinterpret_cast<const float4*>(hr + 4 * c4);
+#pragma unroll
+        for (int q = 0; q < MAXPROJ; ++q) {
+          zq[q] = fmaf(h.x, preg[q][4 * c4 + 0], zq[q]);
+          zq[q] = fmaf(h.y, preg[q][4 * c4 + 1], zq[q]);
+          zq[q] = fmaf(h.z, preg[q][4 * c4 + 2], zq[q]);
+          zq[q] = fmaf(h.w, preg[q][4 * c4 + 3], zq[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < MAXPROJ; ++q) {  // the 8 column slices of the row: fixed xor tree
+        zq[q] += __shfl_xor(zq[q], 1);
+        zq[q] += __shfl_xor(zq[q], 2);
+        zq[q] += __shfl_xor(zq[q], 4);
+      }
+      const u32x4 zw = {__float_as_uint(zq[0]), __float_as_uint(zq[1]), __float_as_uint(zq[2]), __float_as_uint(zq[3])};
+      const uint32_t zoff = (pcb == 0 && tp >= 0) ? (uint32_t)((((int64_t)tp * WS_ROWS + prow8) * a.ldz) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(zw, zrsrc, (int)zoff, 0, 0);
+    }
+  };
+
+  // B, bias, projection and seed loads landed before the ring starts (hipcc would otherwise wait
+  // for them inside the loop with counts that also drain the DMAs)
+  wait_vm(std::integral_constant<int, 0>{});
+  // prologue: tiles t, t + G, .. in flight
+#pragma unroll
+  for (int b = 0; b < NBUF - 1; ++b) dma(t + b * G, b);
+  int tp = -1;
+  for (int i = 0;; ++i) {
+    // DMA(i) done: after it were issued the prologue's later DMAs and, per iteration since, S
+    // stores + one tile's DMA
+    if (i == 0) wait_vm(std::integral_constant<int, (NBUF - 2) * QW>{});
+    else if (NBUF == 3 || i == 1) wait_vm(std::integral_constant<int, (NBUF - 2) * QW + S>{});
+    else wait_vm(std::integral_constant<int, (NBUF - 2) * QW + (NBUF - 2) * S>{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous E1's C-tile writes
+    __builtin_amdgcn_s_barrier();
+    e2(tp, reinterpret_cast<const float*>(smem + CT0 + ((i + 1) & 1) * CTB));
+    dma(t + (NBUF - 1) * G, (i + NBUF - 1) % NBUF);
+    const char* cur = smem + (i % NBUF) * ABUF;
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const bf16x8 x = *reinterpret_cast<const bf16x8*>(cur + s * WS_KSB + foff);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, bw[s], acc, 0, 0, 0);
+    }
+    e1(acc, t, reinterpret_cast<float*>(smem + CT0 + (i & 1) * CTB));
+    tp = t;
+    t += G;
+    if (t >= ntiles) {
+      wait_vm(std::integral_constant<int, 0>{});  // no DMA may outlive the block's LDS
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      e2(tp, reinterpret_cast<const float*>(smem + CT0 + (i & 1) * CTB));
+      break;
+    }
+  }
+}
+
 int ws_num_cus() {
   static int cus = 0;
   if (!cus) {
@@ -832,6 +1012,47 @@ bool nt_planes_ok(const NTArgs& a) {
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
   if ((drop || proj || relu) && !(relu && bias)) return false;
   return true;
+}
+
+// The bf16 image form: bf16 A image (one plane, ld 256 or 336), bf16 C, the w1/w2 B form,
+// 8 <= N <= 128 (N % 8 == 0), M >= 32, the nt_ws_ok epilogues.
+bool nt_img16_ok(const NTArgs& a) {
+  if (!a.ap || !a.a_bf16 || !a.c_bf16 || !a.c || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc < 8 || a.Nc % 8)
+    return false;
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!al(a.ap) || (a.ap_ld != 256 && a.ap_ld != 336) || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 ||
+      a.ap_col2 + a.k2 > a.ap_ld)
+    return false;
+  if (!al(a.c) || a.ldc % 8 != 0 || a.ldc < a.Nc || a.M * a.ldc * 2 >= ((int64_t)1 << 31)) return false;
+  // the projection is stored as one 16-byte z row: all four products, 16-byte aligned rows
+  if (a.nproj > 0 && (a.nproj != MAXPROJ || a.ldz % 4 != 0 || !al(a.z) || a.M * a.ldz * 4 >= ((int64_t)1 << 31)))
+    return false;
+  if (a.M < WS_ROWS || ceil_div(a.M, WS_ROWS) >= INT32_MAX) return false;
+  const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
+  if ((drop || proj || relu) && !(relu && bias)) return false;
+  return true;
+}
+
+template <int NKS>
+void launch_nt_img16_k(const NTArgs& a, const uint4* img, hipStream_t st) {
+  const int ntiles = (int)ceil_div(a.M, WS_ROWS);
+  const int grid = std::min(ntiles, ws_num_cus());
+  const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
+#define GNN_I16(E) gemm_nt_img16_kernel<NKS, E, 4><<<grid, 256, 0, st>>>(a, img, ntiles)
+  if (proj && drop) GNN_I16(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
+  else if (proj) GNN_I16(WS_BIAS | WS_RELU | WS_PROJ);
+  else if (drop) GNN_I16(WS_BIAS | WS_RELU | WS_DROP);
+  else if (relu) GNN_I16(WS_BIAS | WS_RELU);
+  else if (bias) GNN_I16(WS_BIAS);
+  else GNN_I16(0);
+#undef GNN_I16
+}
+
+void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st) {
+  const int nks = a.ap_ld / 16;
+  ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // B image (plane 0 used)
+  if (nks == 16) launch_nt_img16_k<16>(a, img, st);
+  else launch_nt_img16_k<21>(a, img, st);
 }
 
 void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st) {

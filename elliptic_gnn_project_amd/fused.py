@@ -29,7 +29,7 @@ import torch
 from . import _lib
 from .aggregation import KernelTimer, aggregate, agg_bytes
 from .graph import GraphPlan, get_plan
-from .planes import mean_planes_ok, x_image
+from .planes import BfImage, bf_x_image, mean_planes_ok, x_image
 
 # The layer-1 operand [agg | x] as a split image (planes.py): on by default, GNNMP_PLANES=0 runs
 # the in-kernel split forms instead (same results within the split's error; A/B timing).
@@ -78,6 +78,11 @@ def _planes_fields(planes):
     return (planes.ptr, planes.ld, planes.ps, planes.col2)
 
 
+# bf16 storage: layer operands as one-plane bf16 images (planes.BfImage) for the weight-stationary
+# bf16 NT; GNNMP_BF_IMAGE=0 keeps the tiled bf16 NT over separate A1 / A2 (A/B timing)
+_BF_IMAGE = os.environ.get("GNNMP_BF_IMAGE", "1") != "0"
+
+
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
             out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None, mask=None, mask_scale=1.0,
             planes=None, check_planes=False):
@@ -90,7 +95,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
         M, k1, k2, dev = a1.size(0), a1.size(1), (a2.size(1) if a2 is not None else 0), a1.device
-    bf = a1 is not None and a1.dtype == torch.bfloat16
+    bf = getattr(planes, "bf16", False) or (a1 is not None and a1.dtype == torch.bfloat16)
     if out is None and want_c and not check_planes:
         out = torch.empty((M, n), dtype=torch.bfloat16 if bf else torch.float32, device=dev)
     ws = None
@@ -125,7 +130,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         # tag: kind, M, K, N, A element bytes, C element bytes, MFMA products per bf16 term
         # (6 split-bf16, 1 bf16 storage, 0 exact f32, -1 the VALU kernels of the skinny shapes).
         # A split image is priced at the algorithmic f32 bytes; it moves 6 B / element.
-        ea = 4 if a1 is None else a1.element_size()
+        ea = 2 if bf else (4 if a1 is None else a1.element_size())
         prod = 0 if (_math(math) == _lib.MATH_F32 or w1 is None) else (1 if ea == 2 else 6)
         if ea == 4 and proj is None and (n <= 8 or (k <= 8 and a2 is None)):
             prod = -1
@@ -142,6 +147,7 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
         M, k1, k2, dev = a1.size(0), a1.size(1), (a2.size(1) if a2 is not None else 0), a1.device
+    bf = getattr(planes, "bf16", False) or (a1 is not None and a1.dtype == torch.bfloat16)
     nproj = proj.size(0) if dz is not None else 0
     n_out = nr * (k1 + k2) + nr + nproj * nr + nproj
     p = _lib.GnnGemmTNParams(
@@ -154,7 +160,7 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         _lib.ptr(a1), _ld(a1) if a1 is not None else 0, k1,
         _lib.ptr(a2), _ld(a2) if a2 is not None else 0, k2,
         _math(math),
-        _lib.DTYPE_BF16 if (a1 is not None and a1.dtype == torch.bfloat16) else _lib.DTYPE_F32,
+        _lib.DTYPE_BF16 if bf else _lib.DTYPE_F32,
         _lib.DTYPE_BF16 if (h is not None and h.dtype == torch.bfloat16) else _lib.DTYPE_F32,
         *_planes_fields(planes),
     )
@@ -169,7 +175,7 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     _lib.call("gnn_gemm_tn_f32", p, out.data_ptr(), ws.data_ptr(), ws.numel() * 4, _lib.stream_handle(dev))
     if KernelTimer.active:
         e1.record()
-        ea = 4 if a1 is None else a1.element_size()
+        ea = 2 if bf else (4 if a1 is None else a1.element_size())
         prod = 0 if _math(math) == _lib.MATH_F32 else (1 if ea == 2 else 6)
         if ea == 4 and nr <= 8 and dz is None and h is None and gout is None:
             prod = -1
@@ -201,6 +207,24 @@ def _layer0_image(x: torch.Tensor, n_out: int, nt_kw):
     return im
 
 
+def _bf_image0(x: torch.Tensor, L: int, Wl):
+    """The cached layer-0 bf16 image when every hidden layer's NT can run on images (the shapes
+    nt_img16_ok takes: image rows of 256 or 336 columns, 8 <= F_out <= 128 with F_out % 8 == 0,
+    31-bit byte offsets), else None (the tiled bf16 NT over separate operands)."""
+    if not _BF_IMAGE or L < 2 or x.dim() != 2 or x.size(0) < 32 or x.stride(1) != 1:
+        return None
+    n, fi = x.size(0), x.size(1)
+    for l in range(L - 1):
+        fo = Wl[l].size(0)
+        ld = ((fi + 7) // 8 * 16 + 15) // 16 * 16
+        if ld not in (256, 336) or not (8 <= fo <= 128 and fo % 8 == 0):
+            return None
+        if n * max(ld, fo) * 2 >= 2 ** 31 or n * 4 * 4 >= 2 ** 31:
+            return None
+        fi = fo
+    return bf_x_image(x)
+
+
 class _FusedSAGE(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
@@ -219,6 +243,8 @@ class _FusedSAGE(torch.autograd.Function):
         P = torch.cat([Wl[-1], Wr[-1]], dim=0).contiguous()  # [2C, F_{L-1}]
         z = None
         ctx.image = None
+        bim = _bf_image0(x, L, Wl) if x.dtype == torch.bfloat16 else None
+        ctx.bimgs = [None] * (L - 1)
         for l in range(L - 1):
             h = hs[-1]
             last_hidden = l == L - 2
@@ -228,6 +254,18 @@ class _FusedSAGE(torch.autograd.Function):
             # the NT kernel's LDS image): no transposed copy
             nt_kw = dict(w1=Wl[l], w2=Wr[l], bias=bl[l], relu=True, dropout_p=train_drop, seed=seeds[l],
                          proj=P if last_hidden else None, z=z if last_hidden else None, seed_ptr=seed_ctr)
+            if bim is not None:  # bf16 storage on images: K1 into A1, the NT's C into the next image's A2
+                fo = Wl[l].size(0)
+                nxt = BfImage(h.size(0), fo, fo, h.device) if not last_hidden else None
+                out = nxt.a2 if nxt is not None else torch.empty((h.size(0), fo), dtype=torch.bfloat16,
+                                                                  device=h.device)
+                aggregate(plan, h, _lib.AGG_MEAN, nodew=plan.deg, out=bim.a1)
+                hn = gemm_nt(None, None, fo, planes=bim, out=out, **nt_kw)
+                ctx.bimgs[l] = bim
+                aggs.append(bim.a1)
+                hs.append(hn)
+                bim = nxt
+                continue
             im = _layer0_image(h, Wl[0].size(0), nt_kw) if l == 0 else None
             if im is not None:  # agg written straight into the split image by K1; A staged as planes
                 ctx.image = (im, im.fill_mean(plan, h))
@@ -276,6 +314,12 @@ class _FusedSAGE(torch.autograd.Function):
             need_g = l > 0 or need_x
             gout = torch.empty((N, fo), dtype=torch.float32, device=dz.device) if need_g else None
             a_l, im = aggs[l], None
+            bim = ctx.bimgs[l]
+            if bim is not None:  # bf16 storage: the TN reads the layer's bf16 image
+                tn_kw = dict(dz=dz, proj=P) if l == L - 2 else dict(g=g)
+                if gemm_tn(fo, None, None, h=hs[l + 1], hscale=hscale, gout=gout, planes=bim, check_planes=True,
+                           **tn_kw):
+                    im = bim
             if a_l is None:  # layer 0 on the split image (refreshed if another forward reused it)
                 im, gen = ctx.image
                 if im.gen != gen:

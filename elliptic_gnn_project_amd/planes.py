@@ -90,3 +90,54 @@ def x_image(x: torch.Tensor) -> SplitImage:
         im.fill_x(x)
         im.x_key = key
     return im
+
+
+# ----------------------------------------------------------------------------- bf16 images
+class BfImage:
+    """One-plane bf16 image [N, ld] of a bf16-storage layer operand [A1 | A2] (BASELINE configs[4]):
+    A1 (the layer's aggregate) in columns [0, k1), A2 (its input h) in [col2, col2 + k2), zeros
+    elsewhere, ld a multiple of 16 (whole MFMA k-steps).  The producers write straight into it —
+    the bf16 aggregation into ``a1`` (row pitch ld) and the previous layer's NT into ``a2`` — so
+    the weight-stationary bf16 NT (gemm_ws.hip gemm_nt_img16_kernel) stages whole 16-byte k-step
+    pieces with no gather or padding pass."""
+
+    bf16 = True
+
+    def __init__(self, n: int, k1: int, k2: int, device: torch.device, zero: bool = False):
+        self.n, self.k1, self.k2 = int(n), int(k1), int(k2)
+        self.col2 = _pad8(k1)
+        self.ld = (self.col2 + _pad8(k2) + 15) // 16 * 16
+        self.ps = self.n * self.ld
+        alloc = torch.zeros if (zero or self.col2 != self.k1 or self.col2 + self.k2 != self.ld) else torch.empty
+        self.img = alloc((self.n, self.ld), dtype=torch.bfloat16, device=device)
+        self.x_key = None
+
+    @property
+    def ptr(self) -> int:
+        return self.img.data_ptr()
+
+    @property
+    def a1(self) -> torch.Tensor:
+        return self.img[:, : self.k1]
+
+    @property
+    def a2(self) -> torch.Tensor:
+        return self.img[:, self.col2: self.col2 + self.k2]
+
+
+def bf_x_image(x: torch.Tensor) -> BfImage:
+    """The cached bf16 image of [agg | x] for a bf16 input x (its x half copied in once, like the
+    graph plan: rebuilt after an in-place edit of x); the agg half is rewritten every forward."""
+    key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
+    attr = _ATTR + "_bf16"
+    im = getattr(x, attr, None)
+    if im is None or im.n != x.size(0) or im.k2 != x.size(1):
+        im = BfImage(x.size(0), x.size(1), x.size(1), x.device, zero=True)
+        try:
+            setattr(x, attr, im)
+        except (AttributeError, RuntimeError):
+            pass
+    if im.x_key != key:
+        im.a2.copy_(x)  # one layout copy per input tensor (the padding columns stay zero)
+        im.x_key = key
+    return im

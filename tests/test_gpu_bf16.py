@@ -174,3 +174,104 @@ def test_fused_sage_bf16_train_step(device):
     grads = _ref_sage_bf16_grads(params, saved, w, data.edge_index, N, 3)
     for k, v in model.named_parameters():
         assert rel_l2(v.grad, grads[k]) < 2e-4, (k, rel_l2(v.grad, grads[k]))
+
+
+@pytest.mark.parametrize("M,k1,n,epi", [(3000, 166, 128, "bias_relu_drop_proj"), (777, 128, 128, "plain"),
+                                        (4133, 128, 64, "bias_relu_proj"), (64, 166, 8, "bias_relu")])
+def test_gemm_nt_bf16_image(device, M, k1, n, epi):
+    """The weight-stationary bf16 NT on a one-plane image (gemm_nt_img16_kernel, LDS-DMA ring):
+    C = epi([A1 | A2]·RNE([W1 | W2])ᵀ) stored bf16, every element within one bf16 ulp of the f64
+    reference, dropout masks bit-identical to the counter hash, z = h·Pᵀ of the stored h."""
+    from elliptic_gnn_project_amd.fused import gemm_nt
+    from elliptic_gnn_project_amd.planes import BfImage
+    from oracle.dropout_hash import keep_mask
+
+    g = torch.Generator().manual_seed(M + n)
+    im = BfImage(M, k1, k1, device, zero=True)
+    a1 = torch.randn(M, k1, generator=g).to(torch.bfloat16)
+    a2 = torch.randn(M, k1, generator=g).to(torch.bfloat16)
+    im.a1.copy_(a1.to(device))
+    im.a2.copy_(a2.to(device))
+    w1 = torch.randn(n, k1, generator=g) * 0.1
+    w2 = torch.randn(n, k1, generator=g) * 0.1
+    bias = torch.randn(n, generator=g)
+    proj = torch.randn(4, n, generator=g)
+    ref = torch.cat([a1, a2], 1).double() @ rb(torch.cat([w1, w2], 1)).double().t()
+    kw, z, p = {}, None, 0.0
+    if epi != "plain":
+        ref = torch.relu(ref + bias.double())
+        kw = dict(bias=bias.to(device), relu=True)
+    if "drop" in epi:
+        p = 0.3
+        kw.update(dropout_p=p, seed=1234)
+        ref = ref * torch.from_numpy(keep_mask(1234, M, n, p)).double() / (1 - p)
+    if "proj" in epi:
+        z = torch.empty(M, 4, device=device)
+        kw.update(proj=proj.to(device), z=z)
+    out = torch.empty(M, n, dtype=torch.bfloat16, device=device)
+    assert gemm_nt(None, None, n, planes=im, out=out, w1=w1.to(device), w2=w2.to(device), check_planes=True, **kw)
+    c = gemm_nt(None, None, n, planes=im, out=out, w1=w1.to(device), w2=w2.to(device), **kw)
+    d = (c.double().cpu() - ref).abs()
+    assert float(d.max()) <= float((BF_ULP * ref.abs() + 1e-5).max()), float(d.max())
+    assert rel_l2(c, ref) < 3e-3
+    if z is not None:
+        assert rel_l2(z, c.double().cpu() @ proj.double().t()) < 1e-5
+
+
+def test_fused_sage_bf16_image_equals_tiled(device, monkeypatch):
+    """The image path of the bf16-storage SAGE (BfImage operands, the image NT) and the tiled bf16
+    NT over separate operands give the same logits and gradients within the bf16 rounding
+    points' slack (both round the same products once; only accumulation order differs)."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=6000, num_edges=9000, seed=14),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+    x_bf = data.x.to(torch.bfloat16).to(device)
+    ei = data.edge_index.to(device)
+    res = []
+    for flag in (True, False):
+        monkeypatch.setattr(fused, "_BF_IMAGE", flag)
+        torch.manual_seed(3)
+        model = SAGENet(data.x.size(1), 128, layers=3, dropout=0.0).to(device)
+        logits = model(x_bf, ei)
+        logits.square().sum().backward()
+        res.append((logits.detach().cpu(), [p.grad.detach().cpu() for p in model.parameters()]))
+    assert rel_l2(res[0][0], res[1][0]) < 1e-3
+    for a, b in zip(res[0][1], res[1][1]):
+        assert rel_l2(a, b) < 5e-3
+
+
+@pytest.mark.parametrize("form,k1,M", [("dz_mask", 166, 5000), ("g_mask", 166, 4133), ("g_mask", 128, 3001),
+                                       ("dz_mask", 128, 40)])
+def test_gemm_tn_bf16_image(device, form, k1, M):
+    """The bf16 image TN (gemm_tn_img16_kernel, register ring D chunks ahead): dW = RNE(G)ᵀ·[A1 | A2]
+    from a one-plane image, G = (dz·P or g) ⊙ mask formed in f32 (and written to gout), db, dzᵀh."""
+    from elliptic_gnn_project_amd.fused import gemm_tn
+    from elliptic_gnn_project_amd.planes import BfImage
+
+    g_ = torch.Generator().manual_seed(M + k1)
+    nr = 128
+    im = BfImage(M, k1, k1, device, zero=True)
+    a1 = torch.randn(M, k1, generator=g_).to(torch.bfloat16)
+    a2 = torch.randn(M, k1, generator=g_).to(torch.bfloat16)
+    im.a1.copy_(a1.to(device))
+    im.a2.copy_(a2.to(device))
+    h = torch.relu(torch.randn(M, nr, generator=g_)).to(torch.bfloat16)
+    dz = torch.randn(M, 4, generator=g_) * 1e-3
+    proj = torch.randn(4, nr, generator=g_)
+    G = dz @ proj if form == "dz_mask" else torch.randn(M, nr, generator=g_) * 1e-3
+    kw = dict(dz=dz.to(device), proj=proj.to(device)) if form == "dz_mask" else dict(g=G.to(device))
+    Gm = torch.where(h.float() > 0, G * 2.0, torch.zeros_like(G))
+    gout = torch.empty(M, nr, device=device)
+    assert gemm_tn(nr, None, None, h=h.to(device), hscale=2.0, gout=gout, planes=im, check_planes=True, **kw)
+    dW, db, dW2, dzs = gemm_tn(nr, None, None, h=h.to(device), hscale=2.0, gout=gout, planes=im, **kw)
+    torch.testing.assert_close(gout.cpu(), Gm, rtol=1e-5, atol=1e-8)
+    A = torch.cat([a1, a2], 1).double()
+    ref = rb(Gm).double().t() @ A
+    assert rel_l2(torch.cat([dW[0], dW[1]], 1), ref) < 1e-5
+    assert rel_l2(db, Gm.sum(0)) < 1e-5
+    if form == "dz_mask":
+        assert rel_l2(dW2, dz.t().double() @ h.double()) < 1e-5
+        assert rel_l2(dzs, dz.sum(0)) < 1e-5
