@@ -436,46 +436,39 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
     loff[j] = ok ? (uint32_t)((row * PT_AP + 8 * c16) * 2)
                  : (uint32_t)(((tid & 15) * PT_AP + PT_MAXLD + 8 * ((tid >> 4) & 1)) * 2);
   }
-  // G slot: column gn, rows 8·go .. +8 of the chunk
-  const int gn = tid & 127, go = tid >> 7;
-  const bool gcol = gn < a.Nr;
-  const int gnc = gcol ? gn : 0;
-  const uint16_t* hbase = reinterpret_cast<const uint16_t*>(a.h) + gnc;
-  const float* gbase = a.g + gnc;
+  // G slot: columns n0 .. n0 + 4 (one vector load / store per row), rows 2·rp, 2·rp + 1 of the
+  // chunk.  Few, wide memory operations per chunk keep the ring's loads countable (vmcnt <= 63).
+  const int gc4 = tid & 31, rp = tid >> 5;
+  const int n0 = 4 * gc4;
+  const bool gcol = n0 < a.Nr;  // Nr % 4 == 0: all four columns or none
+  const int n0c = gcol ? n0 : 0;
+  const uint16_t* hbase = reinterpret_cast<const uint16_t*>(a.h) + n0c;
+  const float* gbase = a.g + n0c;
   const int zr = (tid & 63) / MAXPROJ, zq = (tid & 63) % MAXPROJ;
   const int zqc = PROJ ? min(zq, a.nproj - 1) : 0;
-  float pcol[MAXPROJ];
+  float pcol[4][MAXPROJ];
 #pragma unroll
-  for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (PROJ && q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int q = 0; q < MAXPROJ; ++q) pcol[j][q] = (PROJ && q < a.nproj && gcol) ? a.proj[q * a.Nr + n0 + j] : 0.0f;
 
   const int Mi = (int)a.M;
   auto ldbase = [&](int c) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
   const int clast = max(nch - 1, 0);
-  // the register ring (slot d: one chunk's A pieces, h / g column values, dz value)
+  // the register ring (slot d: one chunk's A pieces, the slot's h / g row vectors, a dz value)
   u32x4 ra[D][NPA];
-  uint32_t rh[D][4];  // h: 8 bf16 of the slot's column, packed in pairs
-  float rg[D][8];
+  uint2 rh[D][2];
+  float4 rg[D][2];
   float rz[D];
   auto load_chunk = [&](int d, int c) {  // c clamped by the caller
     const int mb = ldbase(c);
 #pragma unroll
     for (int j = 0; j < NPA; ++j) ra[d][j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], mb * ld * 2, 0);
-    if constexpr (MASK) {
-      uint32_t o = (uint32_t)((mb + 8 * go) * (int)a.ldh);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t lo = hbase[o], hi = hbase[o + (uint32_t)a.ldh];
-        rh[d][i] = lo | (hi << 16);
-        o += 2u * (uint32_t)a.ldh;
-      }
-    }
-    if constexpr (!PROJ) {
-      uint32_t o = (uint32_t)((mb + 8 * go) * (int)a.ldg);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        rg[d][i] = gbase[o];
-        o += (uint32_t)a.ldg;
-      }
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t row = (uint32_t)(mb + 2 * rp + i);
+      if constexpr (MASK) rh[d][i] = *reinterpret_cast<const uint2*>(hbase + row * (uint32_t)a.ldh);
+      if constexpr (!PROJ) rg[d][i] = *reinterpret_cast<const float4*>(gbase + row * (uint32_t)a.ldg);
     }
   };
   auto load_z = [&](int d, int c) {
@@ -489,56 +482,71 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
     }
   };
 
-  float db = 0.f, dzs = 0.f;
-  float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
-  // chunk c's A pieces and G column (from ring slot d) into LDS buffer c & 1
+  float db[4] = {0.f, 0.f, 0.f, 0.f};
+  float dzs[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
+  float dw2[4][MAXPROJ];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int q = 0; q < MAXPROJ; ++q) dw2[j][q] = 0.f;
+  // chunk c's A pieces and G block (from ring slot d) into LDS buffer c & 1
   auto put_chunk = [&](int d, int c) {
     const int buf = c & 1;
 #pragma unroll
     for (int j = 0; j < NPA; ++j) *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(At[buf]) + loff[j]) = ra[d][j];
     const int mb = ldbase(c);
-    uint32_t w[4];
+    float gv[2][4];
 #pragma unroll
-    for (int i2 = 0; i2 < 4; ++i2) {
-      float gv[2];
+    for (int i = 0; i < 2; ++i) {
+      const int r = 2 * rp + i;
+      const bool ok = r >= (int)mbeg + c * PT_ROWS - mb && r < (int)mend - mb && gcol;
+      float hv[4];
+      if constexpr (MASK) {
+        hv[0] = __uint_as_float(rh[d][i].x << 16);
+        hv[1] = __uint_as_float(rh[d][i].x & 0xffff0000u);
+        hv[2] = __uint_as_float(rh[d][i].y << 16);
+        hv[3] = __uint_as_float(rh[d][i].y & 0xffff0000u);
+      }
+      float4 z = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (PROJ) {
+        z = *reinterpret_cast<const float4*>(&dzL[buf][r * MAXPROJ]);
+        if (gc4 == 0) {  // Σ dz: the column-group-0 threads, one row each
+          dzs[0] += z.x; dzs[1] += z.y; dzs[2] += z.z; dzs[3] += z.w;
+        }
+      }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int i = 2 * i2 + u;
-        const int r = 8 * go + i;
+      for (int j = 0; j < 4; ++j) {
         float e;
         if constexpr (PROJ) {
-          const float4 z = *reinterpret_cast<const float4*>(&dzL[buf][r * MAXPROJ]);
-          e = z.x * pcol[0];
-          e = fmaf(z.y, pcol[1], e);
-          e = fmaf(z.z, pcol[2], e);
-          e = fmaf(z.w, pcol[3], e);
-          dzs += gn < MAXPROJ ? dzL[buf][r * MAXPROJ + (gn & (MAXPROJ - 1))] : 0.0f;
+          e = z.x * pcol[j][0];
+          e = fmaf(z.y, pcol[j][1], e);
+          e = fmaf(z.z, pcol[j][2], e);
+          e = fmaf(z.w, pcol[j][3], e);
           if constexpr (MASK) {
-            const float hv = __uint_as_float(u ? (rh[d][i2] & 0xffff0000u) : (rh[d][i2] << 16));
-            dw2[0] = fmaf(z.x, hv, dw2[0]);
-            dw2[1] = fmaf(z.y, hv, dw2[1]);
-            dw2[2] = fmaf(z.z, hv, dw2[2]);
-            dw2[3] = fmaf(z.w, hv, dw2[3]);
+            dw2[j][0] = fmaf(z.x, hv[j], dw2[j][0]);
+            dw2[j][1] = fmaf(z.y, hv[j], dw2[j][1]);
+            dw2[j][2] = fmaf(z.z, hv[j], dw2[j][2]);
+            dw2[j][3] = fmaf(z.w, hv[j], dw2[j][3]);
           }
         } else {
-          e = rg[d][i];
+          e = j == 0 ? rg[d][i].x : j == 1 ? rg[d][i].y : j == 2 ? rg[d][i].z : rg[d][i].w;
         }
         float g = e;
-        if constexpr (MASK) {
-          const float hv = __uint_as_float(u ? (rh[d][i2] & 0xffff0000u) : (rh[d][i2] << 16));
-          g = hv > 0.0f ? g * a.hscale : 0.0f;
-        }
-        const bool ok = r >= (int)mbeg + c * PT_ROWS - mb && r < (int)mend - mb && gcol;
+        if constexpr (MASK) g = hv[j] > 0.0f ? g * a.hscale : 0.0f;
         if constexpr (!PROJ) g = ok ? g : 0.0f;
-        db += g;
-        if constexpr (GOUT) {
-          if (a.gout && ok) a.gout[(int64_t)(mb + r) * a.ldgout + gn] = g;
-        }
-        gv[u] = g;
+        db[j] += g;
+        gv[i][j] = g;
       }
-      w[i2] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v_t){gv[0], gv[1]}, bf16x2v_t));
+      if constexpr (GOUT) {
+        if (a.gout && ok)
+          *reinterpret_cast<float4*>(a.gout + (int64_t)(mb + r) * a.ldgout + n0) =
+              make_float4(gv[i][0], gv[i][1], gv[i][2], gv[i][3]);
+      }
     }
-    *reinterpret_cast<uint4*>(Gt[buf] + gn * PT_GP + 8 * go) = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)  // Gt[n][rows]: the two rows of column n0 + j as one bf16 pair
+      *reinterpret_cast<uint32_t*>(Gt[buf] + (n0 + j) * PT_GP + 2 * rp) =
+          __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v_t){gv[0][j], gv[1][j]}, bf16x2v_t));
   };
 
   const int gfo = (32 * wave + (lane & 31)) * PT_GP + 8 * (lane >> 5);
@@ -602,22 +610,44 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
       if (row < a.Nr && (s1 || s2)) slab[idx] = acc[t][r];
     }
   }
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(&At[0][0]);
-  constexpr int ns = 2 + MAXPROJ;
-  red[(go * 128 + gn) * ns + 0] = db;
-  red[(go * 128 + gn) * ns + 1] = dzs;
+  // side sums: the two row pairs of a column group in a wave (lanes l, l + 32) by one exchange,
+  // then the four waves in order through LDS (At[0] is free after the last barrier)
+  constexpr int ns = 1 + MAXPROJ;
 #pragma unroll
-  for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
+  for (int j = 0; j < 4; ++j) {
+    db[j] += __shfl_xor(db[j], 32);
+#pragma unroll
+    for (int q = 0; q < MAXPROJ; ++q) dw2[j][q] += __shfl_xor(dw2[j][q], 32);
+  }
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) dzs[q] += __shfl_xor(dzs[q], 32);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(&At[0][0]);  // [4 waves][128 columns][ns] + [4 waves][4] dz sums
+  if (lane < 32) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[(wave * 128 + n0 + j) * ns] = db[j];
+#pragma unroll
+      for (int q = 0; q < MAXPROJ; ++q) red[(wave * 128 + n0 + j) * ns + 1 + q] = dw2[j][q];
+    }
+    if (gc4 == 0) {
+#pragma unroll
+      for (int q = 0; q < MAXPROJ; ++q) red[4 * 128 * ns + wave * MAXPROJ + q] = dzs[q];
+    }
+  }
   __syncthreads();
   if (tid < 128 && tid < a.Nr) {
     float* side = slab + (int64_t)a.Nr * Kc;
-    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
+    const float* rr = red + tid * ns;
+    side[tid] = ((rr[0] + rr[128 * ns]) + rr[2 * 128 * ns]) + rr[3 * 128 * ns];
     for (int q = 0; q < a.nproj; ++q)
-      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+      side[a.Nr + q * a.Nr + tid] = ((rr[1 + q] + rr[128 * ns + 1 + q]) + rr[2 * 128 * ns + 1 + q]) + rr[3 * 128 * ns + 1 + q];
   }
-  if (PROJ && tid < a.nproj)
-    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+  if (PROJ && tid < a.nproj) {
+    const float* rz4 = red + 4 * 128 * ns;
+    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] =
+        ((rz4[tid] + rz4[MAXPROJ + tid]) + rz4[2 * MAXPROJ + tid]) + rz4[3 * MAXPROJ + tid];
+  }
 }
 
 template <bool PROJ, bool MASK, int KT>
@@ -655,6 +685,11 @@ void launch_tn_planes_kt(const TNArgs& a, int nblk, hipStream_t st) {
 // the bf16 image form: one-plane bf16 image (ld 256 or 336), h bf16 when given
 bool tn_img16_ok(const TNArgs& a) {
   if (!a.ap || !a.a_bf16 || (a.h && !a.h_bf16)) return false;
+  // the G slot's vector accesses: 4 columns per row (8-byte h, 16-byte g / gout rows)
+  auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
+  if (a.Nr % 4 || (a.h && (a.ldh % 4 || !al(a.h, 8))) || (a.g && !a.dz && (a.ldg % 4 || !al(a.g, 16))) ||
+      (a.gout && (a.ldgout % 4 || !al(a.gout, 16))))
+    return false;
   if ((a.ap_ld != 256 && a.ap_ld != 336) || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;
   if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
   if (a.ap_ps < a.M * (int64_t)a.ap_ld || a.ap_ps * 2 >= ((int64_t)1 << 31) || a.M < PT_ROWS) return false;
