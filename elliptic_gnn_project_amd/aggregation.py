@@ -53,31 +53,12 @@ class KernelTimer:
         cls.records.append((tag, e0, e1, int(amount)))
 
     @classmethod
-    def dispatch_gap_ms(cls, n: int = 20) -> float:
-        """Median event-pair time around an (almost) empty kernel behind a busy stream: the
-        launch-boundary gap every bracket includes besides its kernel (~2 us on MI355X; rocprof's
-        kernel durations exclude it)."""
-        ts = []
-        torch.cuda._sleep(2_000_000)  # keep the stream busy while the pairs are enqueued
-        pairs = []
-        for _ in range(n):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            torch.cuda._sleep(1)
-            e1.record()
-            pairs.append((e0, e1))
-        torch.cuda.synchronize()
-        ts = sorted(a.elapsed_time(b) for a, b in pairs)
-        return ts[len(ts) // 2]
-
-    @classmethod
-    def stop(cls, gap_ms: float = 0.0):
-        """Per-tag totals; ``gap_ms`` (dispatch_gap_ms) is taken off every bracket."""
+    def stop(cls):
         cls.active = False
         torch.cuda.synchronize()
         out = {}
         for tag, a, b, amount in cls.records:
-            ms = max(a.elapsed_time(b) - gap_ms, 1e-6)
+            ms = a.elapsed_time(b)
             d = out.setdefault(tag, {"launches": 0, "ms": 0.0, "amount": 0})
             d["launches"] += 1
             d["ms"] += ms

@@ -83,7 +83,15 @@ struct GatArgs {
   // explain mode (generic kernels only): per-CSR-slot message multiplier and its gradient
   const float* ew;  // [S] or null
   float* dew;       // [S] or null
+  // the CSR group passes in the plan's degree order (K0b csr_split order: position -> row; rows
+  // of one wave then have nearly the same slot count and walk in lockstep), null: row order
+  const int32_t* order;
 };
+
+// the row of group position pos (pos < N)
+__device__ __forceinline__ int64_t gat_row(const GatArgs& a, int64_t pos) {
+  return (a.order && pos < a.N) ? (int64_t)a.order[pos] : pos;
+}
 
 // ---------------------------------------------------------------- forward (K5)
 __global__ __launch_bounds__(256) void gat_fwd_kernel(GatArgs a) {
@@ -620,7 +628,7 @@ __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g
   const bool writer = sl.ok && sl.fl == sl.hs * sl.L;
   const int64_t rpb = 4 * (int64_t)rpw;
   for (int64_t base = bid * rpb; base < a.N; base += nblk * rpb) {
-    const int64_t r = base + wave * rpw + (lane >> g.lgG);
+    const int64_t r = gat_row(a, base + wave * rpw + (lane >> g.lgG));
     int32_t beg = 0, end = 0;
     if (r < a.N) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
     const bool own = r < a.N && end - beg <= lg.T;
@@ -807,7 +815,7 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatG
   const float inv_h = a.concat ? 1.0f : 1.0f / (float)H;
   const int64_t rpb = 4 * (int64_t)rpw;
   for (int64_t base = bid * rpb; base < a.N; base += nblk * rpb) {
-    const int64_t r = base + wave * rpw + (lane >> g.lgG);
+    const int64_t r = gat_row(a, base + wave * rpw + (lane >> g.lgG));
     int32_t beg = 0, end = 0;
     if (r < a.N) { beg = a.rowptr[r]; end = a.rowptr[r + 1]; }
     const VecF<VEC> dO = load_dO<VEC>(a, sl, r, r < a.N);  // issued beside the rowptr loads
@@ -1028,6 +1036,12 @@ bool idx24_ok(const gnn_graph* g, int64_t ld_xh, int H) {
          g->num_nodes * ld_xh < ((int64_t)1 << 32) && g->num_slots * H < ((int64_t)1 << 32);
 }
 
+// Degree order of the plan's CSR split (K0b), or null (row order).
+const int32_t* csr_order(const gnn_graph* g) {
+  const gnn_split* sp = g->csr_split;
+  return (sp && sp->order && sp->num_long > 0) ? sp->order : nullptr;
+}
+
 // Long-row list of the plan's CSR split (K0b); none when the plan has no split.
 GatLong long_rows(const gnn_graph* g) {
   const gnn_split* sp = g->csr_split;
@@ -1093,6 +1107,7 @@ extern "C" gnn_status gnn_gat_fwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
     return fail(GNN_ERR_INVALID_ARG, __func__, "null");
   GatArgs a{};
   a.rowptr = g->rowptr; a.col = g->col; a.N = g->num_nodes;
+  a.order = csr_order(g);
   a.H = H; a.C = C; a.concat = concat; a.slope = slope;
   a.xh = xh; a.ld_xh = ld_xh; a.a_s = a_src; a.a_d = a_dst; a.bias = bias;
   a.alpha = alpha; a.out = out; a.ldo = ldo;
@@ -1128,6 +1143,7 @@ extern "C" gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fw
     return fail(GNN_ERR_INVALID_ARG, __func__, "null");
   GatArgs a{};
   a.rowptr = g->rowptr; a.col = g->col; a.N = g->num_nodes;
+  a.order = csr_order(g);
   a.H = H; a.C = C; a.concat = concat; a.slope = p->slope;
   a.xh = p->xh; a.ld_xh = p->ld_xh; a.a_s = p->a_src; a.a_d = p->a_dst; a.bias = p->bias;
   a.att_s = p->att_src; a.att_d = p->att_dst;
@@ -1216,6 +1232,7 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
   carve_bwd(c, g->num_nodes, g->num_slots, H, C, &a.dz, &a.dad, &a.das, &part);
   if (!c.ok) return fail(GNN_ERR_WORKSPACE, fn, "workspace too small");
   a.rowptr = g->rowptr; a.col = g->col; a.colptr = g->colptr; a.row = g->row; a.csc2csr = g->csc2csr;
+  a.order = csr_order(g);
   a.N = g->num_nodes; a.H = H; a.C = C; a.concat = concat; a.slope = slope;
   a.xh = xh; a.ld_xh = ld_xh; a.a_s = a_src; a.a_d = a_dst;
   a.att_s = att_src; a.att_d = att_dst; a.alpha = const_cast<float*>(alpha);
