@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -241,6 +241,12 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
          c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_gat_bwd_act_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+         c_i32, ctypes.c_float, ctypes.c_uint64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i64,
+         c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
     "gnn_gat_bwd_ew_f32": (
         ctypes.c_int,

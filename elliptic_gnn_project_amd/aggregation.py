@@ -386,12 +386,6 @@ class _GATAttention(torch.autograd.Function):
         dev = xh.device
         N = plan.num_nodes
         F = heads * chans
-        if out is not None:  # through dropout(act(.)) first: d pre
-            dpre = torch.empty_like(out)
-            _lib.call("gnn_gat_act_bwd_f32", N, out.size(1), act, dropout_p, seed & 0xFFFFFFFFFFFFFFFF,
-                      _lib.ptr(seed_ctr), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout), dpre.data_ptr(),
-                      _ld(dpre), _lib.stream_handle(dev))
-            dout = dpre
         dxh = torch.empty((N, F), dtype=torch.float32, device=dev)
         datt_s = torch.empty(F, dtype=torch.float32, device=dev)
         datt_d = torch.empty(F, dtype=torch.float32, device=dev)
@@ -399,10 +393,25 @@ class _GATAttention(torch.autograd.Function):
         _lib.call("gnn_gat_bwd_workspace_size", N, plan.num_slots, heads, chans, nb)
         ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
         t0 = KernelTimer.begin()
-        _lib.call("gnn_gat_bwd_f32", plan.c_graph, heads, chans, int(concat), slope, xh.data_ptr(), _ld(xh),
-                  a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
-                  dout.data_ptr(), _ld(dout), dxh.data_ptr(), _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(),
-                  ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+        if out is not None and concat:  # through dropout(act(.)): d pre formed inside the rows pass
+            dpre = torch.empty_like(out)
+            _lib.call("gnn_gat_bwd_act_f32", plan.c_graph, heads, chans, slope, xh.data_ptr(), _ld(xh),
+                      a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
+                      act, dropout_p, seed & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ctr), out.data_ptr(), _ld(out),
+                      dout.data_ptr(), _ld(dout), dpre.data_ptr(), _ld(dpre), dxh.data_ptr(), _ld(dxh),
+                      datt_s.data_ptr(), datt_d.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+            dout = dpre
+        else:
+            if out is not None:  # through dropout(act(.)) first: d pre
+                dpre = torch.empty_like(out)
+                _lib.call("gnn_gat_act_bwd_f32", N, out.size(1), act, dropout_p, seed & 0xFFFFFFFFFFFFFFFF,
+                          _lib.ptr(seed_ctr), out.data_ptr(), _ld(out), dout.data_ptr(), _ld(dout), dpre.data_ptr(),
+                          _ld(dpre), _lib.stream_handle(dev))
+                dout = dpre
+            _lib.call("gnn_gat_bwd_f32", plan.c_graph, heads, chans, int(concat), slope, xh.data_ptr(), _ld(xh),
+                      a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
+                      dout.data_ptr(), _ld(dout), dxh.data_ptr(), _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(),
+                      ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
         S = plan.num_slots
         fo = F if concat else chans
         # rows pass (dα, de per slot): id 4 + alpha 4H + xh row 4HC + de 4H, dout row 4·fo per node;

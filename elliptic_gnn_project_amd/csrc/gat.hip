@@ -86,6 +86,13 @@ struct GatArgs {
   // the CSR group passes in the plan's degree order (K0b csr_split order: position -> row; rows
   // of one wave then have nearly the same slot count and walk in lockstep), null: row order
   const int32_t* order;
+  // rows pass with the hidden layer's store backward fused (gnn_gat_bwd_act_f32): dout holds dy,
+  // d pre = dy * keep / (1-p) * elu'(pre) is formed from it and the stored y = dropout(elu(pre))
+  // as each row's slice is loaded, and written to dpre for the cols pass
+  const float* y; int64_t ld_y;
+  float* dpre; int64_t ld_dpre;
+  int32_t pe_act, pe_drop; uint32_t pe_thresh; float pe_scale, pe_keep;
+  uint64_t pe_seed; const uint64_t* pe_seed_ptr;
 };
 
 // the row of group position pos (pos < N)
@@ -768,7 +775,26 @@ __device__ __forceinline__ VecF<VEC> load_dO(const GatArgs& a, const SlotLane& s
 #pragma unroll
   for (int i = 0; i < VEC; ++i) d.v[i] = 0.0f;
   if (ok && sl.ok) d = ldv<VEC>(a.dout + r * a.ld_dout + (a.concat ? sl.f0 : sl.c0));
+  if (a.y && ok && sl.ok) {  // the store's backward (concat layers), as gat_act_bwd_kernel
+    const VecF<VEC> yv = ldv<VEC>(a.y + r * a.ld_y + sl.f0);
+    const uint64_t seed = a.pe_seed_ptr ? (*a.pe_seed_ptr) * 0x9E3779B97F4A7C15ull + a.pe_seed : a.pe_seed;
+    const int F = a.H * a.C;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float g = d.v[i];
+      if (a.pe_drop)
+        g = keep_elem(seed, (uint32_t)r * (uint32_t)F + (uint32_t)(sl.f0 + i), a.pe_thresh) ? g * a.pe_scale : 0.0f;
+      if (a.pe_act == GNN_ACT_ELU && !(yv.v[i] > 0.0f)) g = g * ((a.pe_drop ? yv.v[i] * a.pe_keep : yv.v[i]) + 1.0f);
+      d.v[i] = g;
+    }
+  }
   return d;
+}
+
+// the formed d pre of a row slice (one writer per feature slice: the phase-0 lane)
+template <int VEC>
+__device__ __forceinline__ void store_dpre(const GatArgs& a, const SlotLane& sl, int64_t r, const VecF<VEC>& d) {
+  if (a.dpre && sl.ok && sl.ep == 0) stv<VEC>(a.dpre + r * a.ld_dpre + sl.f0, d);
 }
 
 // One block, one long row: 256/FLp slot phases; t and d a_dst merged in the wave by xor
@@ -783,6 +809,7 @@ __device__ void gat_bwd_long_row(const GatArgs& a, const GatGeom& g, int64_t r, 
   const float adr = a.a_d[r * H + sl.hs];
   const float inv_h = a.concat ? 1.0f : 1.0f / (float)H;
   const VecF<VEC> dO = load_dO<VEC>(a, sl, r, true);
+  store_dpre<VEC>(a, sl, r, dO);
   BwdSlot q0{0.0f, 0.0f, false}, q1{0.0f, 0.0f, false};
   float t = sl.ok ? bwd_pass1<VEC>(a, sl, beg, end, adr, dO, inv_h, writer, q0, q1) : 0.0f;
   for (int off = 32; off >= g.FLp; off >>= 1) t += __shfl_xor(t, off);
@@ -823,6 +850,7 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatG
     const float adr = r < a.N ? adr_ : 0.0f;
     const bool own = r < a.N && end - beg <= lg.T;
     if (!own) end = beg;
+    if (own) store_dpre<VEC>(a, sl, r, dO);
     BwdSlot q0{0.0f, 0.0f, false}, q1{0.0f, 0.0f, false};
     float t = sl.ok ? bwd_pass1<VEC>(a, sl, beg, end, adr, dO, inv_h, writer, q0, q1) : 0.0f;
     for (int off = G >> 1; off >= g.FLp; off >>= 1) t += __shfl_xor(t, off);
@@ -1211,7 +1239,7 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
                         const float* xh, int64_t ld_xh, const float* a_src, const float* a_dst, const float* att_src,
                         const float* att_dst, const float* alpha, const float* dout, int64_t ld_dout, float* dxh,
                         int64_t ld_dxh, float* d_att_src, float* d_att_dst, const float* edge_w, float* d_edge_w,
-                        void* workspace, size_t workspace_bytes, gnn_stream_t stream) {
+                        void* workspace, size_t workspace_bytes, gnn_stream_t stream, const GatArgs* post = nullptr) {
   if (!g) return fail(GNN_ERR_INVALID_ARG, fn, "null graph");
   if (!pow2_heads(H)) return fail(GNN_ERR_UNSUPPORTED, fn, "heads must be a power of two <= 64");
   const int64_t F = (int64_t)H * C;
@@ -1240,15 +1268,27 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
   a.ew = edge_w; a.dew = d_edge_w;
   GatGeom gg;
   int vec = 1;
+  const bool fuse = post != nullptr;  // the store's backward rides in the rows pass
+  const int64_t F_ = (int64_t)H * C;
   if (!edge_w && idx24_ok(g, ld_xh, H) &&
-      gat_geom(H, C, concat, {{xh, ld_xh}, {dout, ld_dout}, {dxh, ld_dxh}, {att_src, 0}, {att_dst, 0}}, &gg, &vec)) {
+      gat_geom(H, C, concat, {{xh, ld_xh}, {dout, ld_dout}, {dxh, ld_dxh}, {att_src, 0}, {att_dst, 0},
+                              {fuse ? post->y : nullptr, fuse ? post->ld_y : 0},
+                              {fuse ? post->dpre : nullptr, fuse ? post->ld_dpre : 0}}, &gg, &vec)) {
     const GatLong lg = long_rows(g);
     const unsigned nbr = group_blocks(a.N, gg.G, (int64_t)1 << 20) + (unsigned)lg.n;
     const unsigned nbc = group_blocks(a.N, gg.G, kColsBlocks);
+    GatArgs ar = a;  // rows pass: dy in, d pre formed and written; cols pass reads d pre
+    if (fuse) {
+      ar.y = post->y; ar.ld_y = post->ld_y; ar.dpre = post->dpre; ar.ld_dpre = post->ld_dpre;
+      ar.pe_act = post->pe_act; ar.pe_drop = post->pe_drop; ar.pe_thresh = post->pe_thresh;
+      ar.pe_scale = post->pe_scale; ar.pe_keep = post->pe_keep; ar.pe_seed = post->pe_seed;
+      ar.pe_seed_ptr = post->pe_seed_ptr;
+      a.dout = post->dpre; a.ld_dout = post->ld_dpre;
+    }
     switch (vec) {
 #define GNN_GAT_BWD(V)                                                            \
   case V:                                                                         \
-    gat_bwd_rows_group_kernel<V><<<nbr, 256, 0, st>>>(a, gg, lg);                 \
+    gat_bwd_rows_group_kernel<V><<<nbr, 256, 0, st>>>(ar, gg, lg);                \
     GNN_LAUNCH_CHECK();                                                           \
     gat_bwd_cols_group_kernel<V><<<nbc, 256, 0, st>>>(a, gg, part);               \
     break;
@@ -1261,6 +1301,15 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
     gat_att_reduce_kernel<<<(unsigned)(2 * F), 256, 0, st>>>((int)F, (int)nbc, part, d_att_src, d_att_dst);
     GNN_LAUNCH_CHECK();
     return GNN_OK;
+  }
+  if (fuse) {  // generic geometry: the store's backward as its own pass first
+    GatEpi ep{};
+    ep.act = post->pe_act; ep.dropout = post->pe_drop; ep.keep_thresh = post->pe_thresh; ep.drop_scale = post->pe_scale;
+    ep.seed = post->pe_seed; ep.seed_ptr = post->pe_seed_ptr;
+    gat_act_bwd_kernel<<<elem_blocks(a.N * F_), 256, 0, st>>>(a.N, (int32_t)F_, ep, post->pe_keep, post->y, post->ld_y,
+                                                             dout, ld_dout, post->dpre, post->ld_dpre);
+    GNN_LAUNCH_CHECK();
+    a.dout = post->dpre; a.ld_dout = post->ld_dpre;
   }
   gat_bwd_rows_kernel<<<row_blocks(a.N), 256, 0, st>>>(a);
   GNN_LAUNCH_CHECK();
@@ -1287,6 +1336,29 @@ extern "C" gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, 
   return gat_bwd_impl(__func__, g, H, C, concat, slope, xh, ld_xh, a_src, a_dst, att_src, att_dst, alpha, dout,
                       ld_dout, dxh, ld_dxh, d_att_src, d_att_dst, nullptr, nullptr, workspace, workspace_bytes,
                       stream);
+}
+
+extern "C" gnn_status gnn_gat_bwd_act_f32(const gnn_graph* g, int32_t H, int32_t C, float slope, const float* xh,
+                                          int64_t ld_xh, const float* a_src, const float* a_dst, const float* att_src,
+                                          const float* att_dst, const float* alpha, gnn_act act, float dropout_p,
+                                          uint64_t seed, const uint64_t* seed_ptr, const float* y, int64_t ld_y,
+                                          const float* dy, int64_t ld_dy, float* dpre, int64_t ld_dpre, float* dxh,
+                                          int64_t ld_dxh, float* d_att_src, float* d_att_dst, void* workspace,
+                                          size_t workspace_bytes, gnn_stream_t stream) {
+  const int64_t F = (int64_t)H * C;
+  if (act != GNN_ACT_NONE && act != GNN_ACT_ELU) return fail(GNN_ERR_INVALID_ARG, __func__, "unknown act");
+  if (!(dropout_p >= 0.0f && dropout_p < 1.0f)) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout_p not in [0, 1)");
+  if (!g || (g->num_nodes > 0 && (!y || !dpre)) || ld_y < F || ld_dpre < F)
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad y / dpre");
+  if (dropout_p > 0.0f && g->num_nodes * F >= ((int64_t)1 << 32))
+    return fail(GNN_ERR_UNSUPPORTED, __func__, "dropout element index (rows x width) must be < 2^32");
+  GatArgs post{};
+  const GatEpi ep = make_epi(act, dropout_p, seed, seed_ptr);
+  post.y = y; post.ld_y = ld_y; post.dpre = dpre; post.ld_dpre = ld_dpre;
+  post.pe_act = ep.act; post.pe_drop = ep.dropout; post.pe_thresh = ep.keep_thresh; post.pe_scale = ep.drop_scale;
+  post.pe_keep = (float)(1.0 - (double)dropout_p); post.pe_seed = seed; post.pe_seed_ptr = seed_ptr;
+  return gat_bwd_impl(__func__, g, H, C, 1, slope, xh, ld_xh, a_src, a_dst, att_src, att_dst, alpha, dy, ld_dy, dxh,
+                      ld_dxh, d_att_src, d_att_dst, nullptr, nullptr, workspace, workspace_bytes, stream, &post);
 }
 
 extern "C" gnn_status gnn_gat_bwd_ew_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t concat, float slope,

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 15
+#define GNNMP_ABI_VERSION 16
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -264,6 +264,20 @@ gnn_status gnn_gat_bwd_f32(const gnn_graph* g, int32_t H, int32_t C, int32_t con
                            const float* dout, int64_t ld_dout, float* dxh, int64_t ld_dxh,
                            float* d_att_src, float* d_att_dst, void* workspace,
                            size_t workspace_bytes, gnn_stream_t stream);
+
+/* Backward of a hidden GATConv whose output went through dropout(act(.)) in the forward store
+ * (gnn_gat_fwd_fused_f32 with act / dropout_p; concat heads): dy is the gradient of the stored
+ * y; d pre = dy * keep / (1-p) * act'(pre) (gnn_gat_act_bwd_f32's formula) is formed inside the
+ * rows pass as each row is loaded and written to dpre [N, H*C] (the cols pass and the bias
+ * gradient read it); otherwise as gnn_gat_bwd_f32.  Replaces the act / dropout backward of
+ * GATNet's hidden layers (src/models/gnn.py:73-74) fused with GATConv's. */
+gnn_status gnn_gat_bwd_act_f32(const gnn_graph* g, int32_t H, int32_t C, float slope, const float* xh,
+                               int64_t ld_xh, const float* a_src, const float* a_dst, const float* att_src,
+                               const float* att_dst, const float* alpha, gnn_act act, float dropout_p,
+                               uint64_t seed, const uint64_t* seed_ptr, const float* y, int64_t ld_y,
+                               const float* dy, int64_t ld_dy, float* dpre, int64_t ld_dpre, float* dxh,
+                               int64_t ld_dxh, float* d_att_src, float* d_att_dst, void* workspace,
+                               size_t workspace_bytes, gnn_stream_t stream);
 
 /* Explain-mode backward (messages scaled by edge_w[s], see gnn_gat_fwd_params.edge_w): as
  * gnn_gat_bwd_f32, plus d_edge_w[s] = sum_h alpha[s,h] * <dout_i(h), xh[j,h,:]> for every CSR slot. */
