@@ -228,9 +228,10 @@ def _bf_image0(x: torch.Tensor, L: int, Wl):
 class _FusedSAGE(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, x, plan: GraphPlan, dropout_p: float, seeds: List[int], seed_ctr, *params):
+    def forward(ctx, x, plan: GraphPlan, dropout_p: float, seeds: List[int], seed_ctr, P, *params):
         # x bf16 selects the bf16-storage path: agg_l and h_l stored bf16, GEMMs on bf16 operands
         # (weights rounded to bf16) with f32 accumulation; z, logits and all gradients stay f32.
+        # P: [W_l ; W_r] of the output layer, [2C, F_{L-1}] (sage_forward's _output_weights)
         L = len(params) // 3
         Wl = params[0::3]
         bl = params[1::3]
@@ -240,7 +241,6 @@ class _FusedSAGE(torch.autograd.Function):
         train_drop = dropout_p if dropout_p > 0 else 0.0
         hs = [x]
         aggs = []
-        P = torch.cat([Wl[-1], Wr[-1]], dim=0).contiguous()  # [2C, F_{L-1}]
         z = None
         ctx.image = None
         bim = _bf_image0(x, L, Wl) if x.dtype == torch.bfloat16 else None
@@ -356,7 +356,7 @@ class _FusedSAGE(torch.autograd.Function):
                               addend=dA[:, fi:])
             # g: next (lower) layer's upstream gradient w.r.t. h_l, masked inside its TN
         dx = g.to(hs[0].dtype) if need_x else None
-        return (dx, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, *grads)
 
 
 class _FusedGCN(torch.autograd.Function):
@@ -496,6 +496,32 @@ def dropout_seeds(L: int, p: float, x: torch.Tensor):
     return [0] * L, None
 
 
+def _output_weights(conv):
+    """[W_l ; W_r] of the output conv as ONE tensor without a per-step copy.
+
+    The NT epilogue's projection and the TN read the stacked [2C, F] weights.  Instead of a
+    `torch.cat` every step (a launch on the critical path), the two Linear weights are re-pointed
+    (``.data``, once — parameters, optimizer state and state_dict keys are untouched) at the two
+    halves of one buffer, which then IS the stack.  A later ``.to()`` / ``load_state_dict`` that
+    separates them is noticed here and re-tied; under HIP-graph capture an untied pair falls back
+    to the copy (a re-tie must not be recorded)."""
+    wl, wr = conv.lin_l.weight, conv.lin_r.weight
+    buf = getattr(conv, "_gnnmp_out_w", None)
+    C = wl.size(0)
+    if (buf is not None and buf.device == wl.device and buf.dtype == wl.dtype and buf.shape == (2 * C, wl.size(1))
+            and wl.data_ptr() == buf.data_ptr() and wr.data_ptr() == buf[C:].data_ptr()
+            and wl.shape == wr.shape and wl.is_contiguous() and wr.is_contiguous()):
+        return buf
+    if wl.shape != wr.shape or torch.cuda.is_current_stream_capturing():
+        return torch.cat([wl, wr], dim=0).contiguous()
+    with torch.no_grad():
+        buf = torch.cat([wl.detach(), wr.detach()], dim=0).contiguous()
+        wl.data = buf[:C]
+        wr.data = buf[C:]
+    conv._gnnmp_out_w = buf
+    return buf
+
+
 def sage_forward(model, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
     plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
     L = len(model.convs)
@@ -504,7 +530,7 @@ def sage_forward(model, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tens
     params = []
     for c in model.convs:
         params += [c.lin_l.weight, c.lin_l.bias, c.lin_r.weight]
-    return _FusedSAGE.apply(x, plan, p, seeds, ctr, *params)
+    return _FusedSAGE.apply(x, plan, p, seeds, ctr, _output_weights(model.convs[-1]), *params)
 
 
 # --------------------------------------------------------------------------- SAGEResBNNet layer tail

@@ -30,10 +30,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--variants", default="0,1,2,3,4")
     ap.add_argument("--cases", default="sage,gcn")
+    ap.add_argument("--no-order", action="store_true", help="plans built with GNNMP_ORDER=0 (split tables in plan order)")
     ap.add_argument("--cold", action="store_true",
                     help="evict L2 / Infinity Cache (write 1 GB) before every timed call, time calls one at a time")
     args = ap.parse_args()
     variants = [int(v) for v in args.variants.split(",")]
+    if args.no_order:
+        os.environ["GNNMP_ORDER"] = "0"
     if any(12 <= v <= 14 for v in variants):  # wave-gather split variants need the partial buffer
         import elliptic_gnn_project_amd.aggregation as agg_mod
         agg_mod.SPLIT_MAX_F = 512
