@@ -514,12 +514,13 @@ __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
 // Narrow rows, slot-parallel (F <= 4; MEAN / MEAN_BWD / SUM): a wave owns 64 consecutive rows
 // (one per lane).  Their slots are staged through LDS with lanes over SLOTS — neighbour ids
 // and the F-wide neighbour rows of 64 slots per instruction, all in flight together — and then
-// each lane adds its own row's slots from LDS in edge order (sequential, deterministic).
+// each lane adds its own row's slots from LDS in edge order (sequential, deterministic; COOP: a
+// row's slots past the first 32 of a pass are summed by all 64 lanes, strided, in a fixed xor tree).
 // NF (2 or 4): compile-time bound on F.  The staging is branch-free: all neighbour ids of the
 // pass, then all their row values (clamped feature index) and weights, then the LDS writes — a
 // per-feature `f < F` branch had compiled to one dependent load + vmcnt(0) per value (r10: 16 us
 // warm, 21 us cold for ~11 MB).
-template <int MODE, int NF, int kNarrowCap = 256>  // kNarrowCap: slots staged per pass per wave
+template <int MODE, int NF, int kNarrowCap = 256, bool COOP = false>  // kNarrowCap: slots staged per pass per wave
 __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   __shared__ float sv[4][kNarrowCap * 4];
   const int lane = threadIdx.x & 63;
@@ -571,21 +572,23 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        float v = (f < NF && f < F) ? xv[i][f < NF ? f : 0] : 0.0f;
+      for (int f = 0; f < NF; ++f) {
+        float v = f < F ? xv[i][f] : 0.0f;
         if constexpr (MODE == GNN_AGG_MEAN_BWD) v = v / fmaxf(dd[i], 1.0f);
         buf[f * kNarrowCap + lane + 64 * i] = v;
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
-    const int32_t lo = max(pbeg, pb), hi = min(pend, pe);
+    const int32_t lo = max(pbeg, pb), hi0 = min(pend, pe);
+    constexpr int CAP = 32;  // COOP: a lane walks at most CAP slots of its row per pass
+    const int32_t hi = COOP ? min(hi0, lo + CAP) : hi0;
     // 4 interleaved partial sums: a hub lane's LDS reads pipeline instead of chaining
     float q1[4] = {0.f, 0.f, 0.f, 0.f}, q2[4] = {0.f, 0.f, 0.f, 0.f}, q3[4] = {0.f, 0.f, 0.f, 0.f};
     int32_t k = lo;
     for (; k + 3 < hi; k += 4) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < NF; ++f) {  // (features past NF are never staged: NF = 2 reads half)
         acc[f] += buf[f * kNarrowCap + (k - pb)];
         q1[f] += buf[f * kNarrowCap + (k + 1 - pb)];
         q2[f] += buf[f * kNarrowCap + (k + 2 - pb)];
@@ -594,10 +597,31 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
     }
     for (; k < hi; ++k) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) acc[f] += buf[f * kNarrowCap + (k - pb)];
+      for (int f = 0; f < NF; ++f) acc[f] += buf[f * kNarrowCap + (k - pb)];
     }
 #pragma unroll
-    for (int f = 0; f < 4; ++f) acc[f] += (q1[f] + q2[f]) + q3[f];
+    for (int f = 0; f < NF; ++f) acc[f] += (q1[f] + q2[f]) + q3[f];
+    if constexpr (COOP) {  // the rest of each long row: all 64 lanes, strided, then a fixed xor tree
+      uint64_t longm = __ballot(hi0 - lo > CAP);
+      while (longm) {
+        const int L = __builtin_ctzll(longm);
+        longm &= longm - 1;
+        const int32_t s0 = __builtin_amdgcn_readlane(lo, L) + CAP, s1 = __builtin_amdgcn_readlane(hi0, L);
+        float part[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) part[f] = 0.f;
+        for (int32_t k2 = s0 + lane; k2 < s1; k2 += 64) {
+#pragma unroll
+          for (int f = 0; f < NF; ++f) part[f] += buf[f * kNarrowCap + (k2 - pb)];
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) part[f] += __shfl_xor(part[f], off);
+          if (lane == L) acc[f] += part[f];
+        }
+      }
+    }
     __builtin_amdgcn_wave_barrier();
   }
   if (rok) {
@@ -785,8 +809,14 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
   if (sp) return launch_mode_split<MODE>(a, vec, st, sp);
   if (a.F <= 4 && (MODE == GNN_AGG_MEAN || MODE == GNN_AGG_MEAN_BWD || MODE == GNN_AGG_SUM)) {
     // slots staged per pass: 512 / 128 measured 15.3 / 17.2 us vs 16.1 at 256 (r10, warm)
-    if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2><<<(unsigned)ceil_div(a.nrows, 256), 256, 0, st>>>(a);
-    else agg_narrow_lds_kernel<MODE, 4><<<(unsigned)ceil_div(a.nrows, 256), 256, 0, st>>>(a);
+    const unsigned nb = (unsigned)ceil_div(a.nrows, 256);
+    // rows longer than 32 slots of a pass: the tail by the whole wave (r17 lab, SAGE preset F = 2:
+    // fwd 14.4 -> 13.2 us, CSC bwd 15.2 -> 14.4 cold); lab 15: each lane walks its whole row
+    if (g_agg_lab_variant == 15) {
+      if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2, 256, false><<<nb, 256, 0, st>>>(a);
+      else agg_narrow_lds_kernel<MODE, 4, 256, false><<<nb, 256, 0, st>>>(a);
+    } else if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2, 256, true><<<nb, 256, 0, st>>>(a);
+    else agg_narrow_lds_kernel<MODE, 4, 256, true><<<nb, 256, 0, st>>>(a);
   } else if (a.F <= 8) {
     int64_t blocks = ceil_div(a.nrows * kGroup, 256);
     if (blocks > ((int64_t)1 << 20)) blocks = (int64_t)1 << 20;

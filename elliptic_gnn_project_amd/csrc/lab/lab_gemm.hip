@@ -426,6 +426,10 @@ template <int LAB>
 void tnd(const TNArgs& a, const NTArgs&, const uint4*, int nblk, int) {
   gemm_tn_planes_dma_kernel<11, LAB><<<nblk, 256>>>(a);
 }
+template <int EPI>
+void nte(const TNArgs&, const NTArgs& a, const uint4* img, int, int ntiles) {
+  gemm_nt_planes_kernel<EPI, 0><<<256, 256>>>(a, img, ntiles);
+}
 template <int LAB>
 void nt(const TNArgs&, const NTArgs& a, const uint4* img, int, int ntiles) {
   gemm_nt_planes_kernel<WS_BIAS | WS_RELU | WS_DROP | WS_PROJ, LAB><<<256, 256>>>(a, img, ntiles);
@@ -475,7 +479,9 @@ int main(int argc, char** argv) {
       {"TN dma no frags", tnd<4>, {}}, {"TN dma DMA only", tnd<1 | 2 | 4>, {}},
       {"NT production", nt<0>, {}}, {"NT no MFMA", nt<1>, {}}, {"NT no epilogue", nt<2>, {}},
       {"NT no staging", nt<4>, {}}, {"NT no mid barrier", nt<8>, {}}, {"NT MFMA+frags only", nt<2 | 4 | 8>, {}},
-      {"NT epilogue only", nt<1 | 4>, {}}};
+      {"NT epilogue only", nt<1 | 4>, {}},
+      {"NT no dropout", nte<WS_BIAS | WS_RELU | WS_PROJ>, {}}, {"NT no projection", nte<WS_BIAS | WS_RELU | WS_DROP>, {}},
+      {"NT bias+relu only", nte<WS_BIAS | WS_RELU>, {}}};
   {
     std::vector<uint16_t> hb(512 * 8);  // random bf16 operands (truncated normal floats: no NaN)
     std::mt19937 g(9);

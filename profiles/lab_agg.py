@@ -99,8 +99,9 @@ def main():
         for v in variants:
             t = statistics.median(times[v])
             same = torch.equal(outs[v], ref)
+            rel = "" if same else f" (max rel diff {float(((outs[v] - ref).abs() / ref.abs().clamp_min(1e-6)).max()):.2e})"
             print(f"{name:38s} v{v}: {t:7.1f} us  {nb / t / 1e3:7.1f} GB/s  ({nb / t / 8e6 * 100:4.1f} % HBM)"
-                  f"  bitwise==v{variants[0]}: {same}", flush=True)
+                  f"  bitwise==v{variants[0]}: {same}{rel}", flush=True)
 
 
 if __name__ == "__main__":
