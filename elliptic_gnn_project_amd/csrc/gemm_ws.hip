@@ -445,12 +445,17 @@ __global__ __launch_bounds__(256 * KS) void gemm_nt_ws_kernel(NTArgs a, const ui
 // sets (two tiles per loop trip: static roles).
 // LAB (timing ablations, csrc/lab/lab_nt.hip only; the library instantiates 0): bit 1 no MFMAs,
 // bit 2 no epilogue slots, bit 4 no staging slots, bit 8 no mid-tile barrier.
-template <int EPI, int LAB = 0>
+template <int NKS, int EPI, int LAB = 0>
 __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uint4* __restrict__ bimg, int ntiles) {
-  constexpr int NKS = 21;
   constexpr int PLB = NKS * WS_KSB;  // bytes per plane of an A buffer
   constexpr int BUF = 3 * PLB;
-  constexpr int QP = 16;             // 1 KB blocks per wave per tile (63 real + 1 repeat)
+  constexpr int QP = (3 * NKS + 3) / 4;  // 1 KB blocks per wave per tile (NKS 21: 63 real + 1 repeat)
+  // slot schedule of a tile's chain (6·NKS MFMA slots; the rest run after the chain):
+  //   E1 [0, 48) | staging of QA pieces [48, SB] | barrier | E2 [60, 60 + NE2) | staging of QB
+  //   pieces [86, NSLOT)
+  constexpr int QA = QP < 6 ? QP : 6, QB = QP - QA;
+  constexpr int SB = 48 + 2 * QA - 1;  // the mid-tile barrier follows this slot
+  constexpr int NSLOT = 86 + 2 * QB;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) char A0[BUF];
   __shared__ __attribute__((aligned(16))) char A1[BUF];
@@ -598,9 +603,9 @@ __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uin
   auto slot = [&](int k, char* nxt, const floatx16& accp, int tp, int t) {
     if (k < 48) {
       if constexpr (!(LAB & 2)) e1(accp, k / 3, k % 3, tp);
-    } else if (k < 60 || (k >= 86 && k < 106)) {
+    } else if (k <= SB || (k >= 86 && k < NSLOT)) {
       if constexpr (!(LAB & 4)) {
-        const int i = k < 60 ? (k - 48) / 2 : 6 + (k - 86) / 2;
+        const int i = k <= SB ? (k - 48) / 2 : QA + (k - 86) / 2;
         if (k & 1) load_piece(i, t + 2 * (int)gridDim.x);
         else put_piece(nxt, i);
       }
@@ -635,10 +640,15 @@ __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uin
           if constexpr (m == 5) x[0] = frag(s + 1, 0);
         }
         slot(6 * s + m, nxt, accp, tp, t);
-        if constexpr (6 * s + m == 59 && !(LAB & 8)) __syncthreads();  // every wave's E1 is in the C tile
+        if constexpr (6 * s + m == SB && !(LAB & 8)) __syncthreads();  // every wave's E1 is in the C tile
       });
     });
     NTP_FENCE;
+    static_for<(NSLOT > 6 * NKS ? NSLOT - 6 * NKS : 0)>([&](auto kc) {  // short chains: the slots past it
+      constexpr int k = 6 * NKS + decltype(kc)::value;
+      slot(k, nxt, accp, tp, t);
+      if constexpr (k == SB && !(LAB & 8)) __syncthreads();
+    });
     if constexpr ((LAB & 1) != 0) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = x[0][r & 7];
@@ -1001,9 +1011,13 @@ namespace gnnmp {
 // (21 k-steps: the SAGE layer-1 [agg | x] of 166 + 166 features, each padded to 168),
 // 64 < N <= 128, M >= 32, the nt_ws_ok epilogues.
 bool nt_planes_ok(const NTArgs& a) {
-  if (!a.ap || a.a_bf16 || a.c_bf16 || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc <= 64) return false;
+  // 336-wide rows (the SAGE [agg | x]) for 64 < N <= 128; 176-wide rows (one 166-wide input, the
+  // GCN / GAT layer-1 x) for any N <= 128 (N <= 64 leaves half the MFMA columns zero: the kernel
+  // is bound by its A stream there, not by the MFMA chain)
+  if (!a.ap || a.a_bf16 || a.c_bf16 || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc < 1) return false;
+  if (!(a.ap_ld == 336 && a.Nc > 64) && a.ap_ld != 176) return false;
   auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  if (!al(a.ap) || a.ap_ld != 336 || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld)
+  if (!al(a.ap) || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld)
     return false;
   if (a.ap_ps < a.M * (int64_t)a.ap_ld || 3 * a.ap_ps * 2 >= ((int64_t)1 << 31)) return false;
   if (a.c && (!al(a.c) || a.ldc % 4 != 0 || a.M * a.ldc * 4 >= ((int64_t)1 << 31))) return false;
@@ -1055,13 +1069,12 @@ void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st) {
   else launch_nt_img16_k<21>(a, img, st);
 }
 
-void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st) {
-  const int nks = a.ap_ld / 16;
-  ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // the B image only
+template <int NKS>
+void launch_nt_ws_planes_k(const NTArgs& a, uint4* img, hipStream_t st) {
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
   const int grid = std::min(ntiles, ws_num_cus());
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
-#define GNN_WSP(E) gemm_nt_planes_kernel<E><<<grid, 256, 0, st>>>(a, img, ntiles)
+#define GNN_WSP(E) gemm_nt_planes_kernel<NKS, E><<<grid, 256, 0, st>>>(a, img, ntiles)
   if (proj && drop) GNN_WSP(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
   else if (proj) GNN_WSP(WS_BIAS | WS_RELU | WS_PROJ);
   else if (drop) GNN_WSP(WS_BIAS | WS_RELU | WS_DROP);
@@ -1069,6 +1082,13 @@ void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st) {
   else if (bias) GNN_WSP(WS_BIAS);
   else GNN_WSP(0);
 #undef GNN_WSP
+}
+
+void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st) {
+  const int nks = a.ap_ld / 16;
+  ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // the B image only
+  if (nks == 11) launch_nt_ws_planes_k<11>(a, img, st);
+  else launch_nt_ws_planes_k<21>(a, img, st);
 }
 
 }  // namespace gnnmp

@@ -428,11 +428,11 @@ void tnd(const TNArgs& a, const NTArgs&, const uint4*, int nblk, int) {
 }
 template <int EPI>
 void nte(const TNArgs&, const NTArgs& a, const uint4* img, int, int ntiles) {
-  gemm_nt_planes_kernel<EPI, 0><<<256, 256>>>(a, img, ntiles);
+  gemm_nt_planes_kernel<21, EPI, 0><<<256, 256>>>(a, img, ntiles);
 }
 template <int LAB>
 void nt(const TNArgs&, const NTArgs& a, const uint4* img, int, int ntiles) {
-  gemm_nt_planes_kernel<WS_BIAS | WS_RELU | WS_DROP | WS_PROJ, LAB><<<256, 256>>>(a, img, ntiles);
+  gemm_nt_planes_kernel<21, WS_BIAS | WS_RELU | WS_DROP | WS_PROJ, LAB><<<256, 256>>>(a, img, ntiles);
 }
 
 int main(int argc, char** argv) {

@@ -29,7 +29,7 @@ import torch
 from . import _lib
 from .aggregation import KernelTimer, aggregate, agg_bytes
 from .graph import GraphPlan, get_plan
-from .planes import BfImage, bf_x_image, mean_planes_ok, x_image
+from .planes import BfImage, bf_x_image, mean_planes_ok, x_image, x_only_image
 
 # The layer-1 operand [agg | x] as a split image (planes.py): on by default, GNNMP_PLANES=0 runs
 # the in-kernel split forms instead (same results within the split's error; A/B timing).
@@ -192,6 +192,24 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     o += nproj * nr
     dzs = out[o: o + nproj] if nproj else None
     return (dW1, dW2_), db, dW2, dzs
+
+
+def gemm_nt_input(x: torch.Tensor, n: int, **kw):
+    """gemm_nt(x, None, n, **kw) (w1 form, no a2) for a layer whose A operand is the model input x:
+    on the split-image NT over x's cached planes (planes.x_only_image) when it takes the shape."""
+    im = x_only_image(x)
+    if im is not None and gemm_nt(None, None, n, planes=im, check_planes=True, **kw):
+        return gemm_nt(None, None, n, planes=im, **kw)
+    return gemm_nt(x, None, n, **kw)
+
+
+def gemm_tn_input(nr: int, x: torch.Tensor, g: torch.Tensor):
+    """gemm_tn(nr, x, g=g) for a layer whose A operand is the model input x: on the split-image
+    TN over x's cached planes (planes.x_only_image) when it takes the shape, else the f32 form."""
+    im = x_only_image(x)
+    if im is not None and gemm_tn(nr, None, g=g, planes=im, check_planes=True):
+        return gemm_tn(nr, None, g=g, planes=im)
+    return gemm_tn(nr, x, g=g)
 
 
 def _layer0_image(x: torch.Tensor, n_out: int, nt_kw):
@@ -380,7 +398,7 @@ class _FusedGCN(torch.autograd.Function):
         hs = [x.contiguous()]
         dinv = plan.dinv
         for l in range(L - 1):
-            y = gemm_nt(hs[-1], None, W[l].size(0), w1=W[l])
+            y = gemm_nt_input(hs[0], W[0].size(0), w1=W[0]) if l == 0 else gemm_nt(hs[-1], None, W[l].size(0), w1=W[l])
             hs.append(aggregate(plan, y, _lib.AGG_GCN, nodew=dinv, bias=b[l], relu=True,
                                 dropout_p=dropout_p, seed=seeds[l], seed_ptr=seed_ctr))
         y = gemm_nt(hs[-1], None, W[-1].size(0), w1=W[-1])
@@ -408,7 +426,7 @@ class _FusedGCN(torch.autograd.Function):
         for l in range(L - 1, -1, -1):
             dy = aggregate(plan, g, _lib.AGG_GCN, transpose=True, nodew=dinv)
             grads[2 * l + 1] = colsum(g)
-            (dW, _), _, _, _ = gemm_tn(W[l].size(0), hs[l], g=dy)
+            (dW, _), _, _, _ = gemm_tn_input(W[l].size(0), hs[l], dy) if l == 0 else gemm_tn(W[l].size(0), hs[l], g=dy)
             grads[2 * l] = dW
             fo, fi = W[l].shape
             if l > 0:  # W [fo, fi] is the row-major [K, N] operand of dh = dy · W

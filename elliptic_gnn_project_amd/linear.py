@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .fused import gemm_nt, gemm_tn
+from .fused import gemm_nt, gemm_nt_input, gemm_tn, gemm_tn_input
 
 MAX_OUT = 128  # NT in-place weight form / TN dW rows
 MAX_IN = 384   # TN K extent
@@ -39,7 +39,10 @@ class _MfmaLinear(torch.autograd.Function):
         a2 = _rows(a2) if a2 is not None else None
         w1 = w1.contiguous()
         w2 = w2.contiguous() if w2 is not None else None
-        y = gemm_nt(a1, None, w1.size(0), a2=a2, bias=bias, w1=w1, w2=w2)
+        if a2 is None:  # a model input (GAT / GCN layer 1): on its cached split image
+            y = gemm_nt_input(a1, w1.size(0), bias=bias, w1=w1)
+        else:
+            y = gemm_nt(a1, None, w1.size(0), a2=a2, bias=bias, w1=w1, w2=w2)
         ctx.save_for_backward(a1, w1, a2, w2)
         ctx.has_bias = bias is not None
         return y
@@ -52,7 +55,10 @@ class _MfmaLinear(torch.autograd.Function):
         need = ctx.needs_input_grad
         dW1 = db = dW2 = None
         if need[1] or need[2] or need[4]:
-            (dW1, dW2), db, _, _ = gemm_tn(w1.size(0), a1, a2, g=dy)
+            if a2 is None:  # a model input (GAT / GCN layer 1) on its cached split image
+                (dW1, dW2), db, _, _ = gemm_tn_input(w1.size(0), a1, dy)
+            else:
+                (dW1, dW2), db, _, _ = gemm_tn(w1.size(0), a1, a2, g=dy)
         da1 = gemm_nt(dy, w1, w1.size(1)) if need[0] else None
         da2 = gemm_nt(dy, w2, w2.size(1)) if (a2 is not None and need[3]) else None
         return (da1, dW1 if need[1] else None, db if (ctx.has_bias and need[2]) else None,

@@ -92,6 +92,37 @@ def x_image(x: torch.Tensor) -> SplitImage:
     return im
 
 
+_ATTR_X = _ATTR + "_x"
+
+
+def x_only_image(x: torch.Tensor):
+    """The cached split image of x alone (x in columns [0, F), k2 = 0) for the GEMMs of a layer
+    whose A operand is a model input x (GCN / GAT layer 1: y = x·Wᵀ and dW = Gᵀ·x), or None.
+
+    Built on first use (one split pass, ~2/3 of one f32 read + write of x) and reused while x is
+    unmodified (data_ptr, _version), like the graph plan: a full-batch run splits its input once.
+    Every call over the same x takes the same kernels, so repeated forwards are bit-identical."""
+    if (x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1 or not x.is_cuda or x.requires_grad
+            or x.size(0) < 32 or x.size(1) > 328):
+        return None
+    key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
+    im = getattr(x, _ATTR_X, None)
+    if im is None or im.n != x.size(0) or im.k1 != x.size(1):
+        im = SplitImage(x.size(0), x.size(1), 0, x.device)
+        if 3 * im.ps * 2 >= 2 ** 31:
+            return None
+        try:
+            setattr(x, _ATTR_X, im)
+        except (AttributeError, RuntimeError):  # e.g. inference tensors: not cached, still used
+            pass
+    if im.x_key != key:
+        with torch.cuda.device(x.device):
+            _lib.call("gnn_split_planes_f32", x.data_ptr(), int(x.stride(0)), im.n, im.k1, im.ptr, im.ld, im.ps,
+                      0, im.ld, _lib.stream_handle(x.device))
+        im.x_key = key
+    return im
+
+
 # ----------------------------------------------------------------------------- bf16 images
 class BfImage:
     """One-plane bf16 image [N, ld] of a bf16-storage layer operand [A1 | A2] (BASELINE configs[4]):

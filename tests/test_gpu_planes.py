@@ -255,3 +255,57 @@ def test_x_image_follows_in_place_edit(device):
     im2 = x_image(x)
     hi = _planes_np(im2)[0][:, 168:334]
     assert np.array_equal(hi, split3(x.cpu().numpy())[0])
+
+
+@pytest.mark.parametrize("F,nr", [(166, 64), (166, 128), (40, 16)])
+def test_input_tn_on_x_only_image(device, F, nr):
+    """dW = Gᵀ·x for a model input x (GCN / GAT layer 1): the split-image TN over x's cached planes
+    (x in columns [0, F), k2 = 0) and the f32-operand TN both within the split's error of float64;
+    the planes are x's split bit for bit and follow an in-place edit of x."""
+    from elliptic_gnn_project_amd.fused import gemm_tn_input
+    from elliptic_gnn_project_amd.planes import x_only_image
+
+    N = 5000
+    g0 = torch.Generator().manual_seed(F + nr)
+    x = torch.randn(N, F, generator=g0).to(device)
+    G = torch.randn(N, nr, generator=g0).to(device)
+    ref = (G.double().t() @ x.double()).cpu()
+    from elliptic_gnn_project_amd.fused import gemm_tn
+
+    (dW1, _), db1, _, _ = gemm_tn(nr, x, g=G)  # the f32-operand TN
+    (dW2, _), db2, _, _ = gemm_tn_input(nr, x, G)  # x's cached planes
+    im = x_only_image(x)
+    assert getattr(x, "_gnnmp_split_image_x", None) is im
+    assert im is not None and im.k2 == 0 and im.ld == ((F + 7) // 8 * 8 + 15) // 16 * 16
+    hi, mid, lo = split3(x.cpu().numpy())
+    P = _planes_np(im)
+    assert np.array_equal(P[0, :, :F], hi) and np.array_equal(P[1, :, :F], mid) and np.array_equal(P[2, :, :F], lo)
+    assert not P[:, :, F:].any()
+    for dW, db in ((dW1, db1), (dW2, db2)):
+        assert rel_l2(dW, ref) < 1e-6
+        assert rel_l2(db, G.double().sum(0).cpu()) < 1e-6
+    x.add_(0.0)  # in-place edit: the planes are rebuilt from the new version
+    (dW3, _), _, _, _ = gemm_tn_input(nr, x, G)
+    assert rel_l2(dW3, ref) < 1e-6
+
+
+@pytest.mark.parametrize("F,n,bias", [(166, 64, False), (166, 128, True), (166, 2, True)])
+def test_input_nt_on_x_only_image(device, F, n, bias):
+    """y = x·Wᵀ (+ b) for a model input x (GCN / GAT layer 1): the split-image NT over x's cached
+    176-wide planes (N <= 128, N % 4 == 0) against float64, as the f32-operand NT is."""
+    from elliptic_gnn_project_amd.fused import gemm_nt, gemm_nt_input
+    from elliptic_gnn_project_amd.planes import x_only_image
+
+    N = 4099  # a ragged last row tile
+    g0 = torch.Generator().manual_seed(F + n)
+    x = torch.randn(N, F, generator=g0).to(device)
+    W = (torch.randn(n, F, generator=g0) * 0.1).to(device)
+    b = torch.randn(n, generator=g0).to(device) if bias else None
+    ref = x.double() @ W.double().t() + (b.double() if bias else 0)
+    y0 = gemm_nt(x, None, n, bias=b, w1=W)
+    im = x_only_image(x)
+    assert im is not None and x_only_image(x) is im  # cached on x
+    takes = gemm_nt(None, None, n, planes=im, check_planes=True, bias=b, w1=W)
+    assert takes == (n % 4 == 0)  # (N = 2 stays on the skinny VALU NT: 16-byte C row stores)
+    y1 = gemm_nt_input(x, n, bias=b, w1=W)
+    assert rel_l2(y0, ref) < 1e-6 and rel_l2(y1, ref) < 1e-6
