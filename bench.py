@@ -336,6 +336,7 @@ def main():
 
     from elliptic_gnn_project_amd import distributed as gdist
     from elliptic_gnn_project_amd.aggregation import KernelTimer
+    from elliptic_gnn_project_amd.planes import register_input
     from elliptic_gnn_project_amd.train_gnn import _make_loss_fn, build_model
 
     preset = PRESETS[args.arch]
@@ -347,6 +348,7 @@ def main():
     bf16 = preset.get("dtype") == "bf16"
     if bf16:  # bf16 storage of the node features (and, through the fused path, every activation)
         data.x = data.x.to(torch.bfloat16)
+    register_input(data.x)  # constant node features: GCN / GAT layer 1 read their split image
     torch.manual_seed(42)  # identical initial weights on every rank
     model = build_model(cfg["arch"], data.x.size(1), cfg).to(dev)
     if dist is not None:

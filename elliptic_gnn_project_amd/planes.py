@@ -95,15 +95,30 @@ def x_image(x: torch.Tensor) -> SplitImage:
 _ATTR_X = _ATTR + "_x"
 
 
-def x_only_image(x: torch.Tensor):
-    """The cached split image of x alone (x in columns [0, F), k2 = 0) for the GEMMs of a layer
-    whose A operand is a model input x (GCN / GAT layer 1: y = x·Wᵀ and dW = Gᵀ·x), or None.
+_CONST = "_gnnmp_const_input"
 
-    Built on first use (one split pass, ~2/3 of one f32 read + write of x) and reused while x is
-    unmodified (data_ptr, _version), like the graph plan: a full-batch run splits its input once.
-    Every call over the same x takes the same kernels, so repeated forwards are bit-identical."""
-    if (x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1 or not x.is_cuda or x.requires_grad
-            or x.size(0) < 32 or x.size(1) > 328):
+
+def register_input(x: torch.Tensor) -> torch.Tensor:
+    """Declare x a constant input of the run (the training loop's node features, prepared once,
+    src/train_gnn.py:315-350): layers whose A operand is x then read it from a split image built
+    once per (unmodified) x — a per-graph input layout, like the CSR plan.  Unregistered inputs
+    (a mini-batch's gathered rows, a per-step time-injected input) keep the f32-operand kernels,
+    so no call pays a split pass it cannot reuse.  Returns x."""
+    try:
+        setattr(x, _CONST, True)
+    except (AttributeError, RuntimeError):
+        pass
+    return x
+
+
+def x_only_image(x: torch.Tensor):
+    """The cached split image of a registered input x alone (x in columns [0, F), k2 = 0) for the
+    GEMMs of a layer whose A operand is x (GCN / GAT layer 1: y = x·Wᵀ and dW = Gᵀ·x), or None.
+
+    Built on first use (one split pass) and reused while x is unmodified (data_ptr, _version);
+    every call over a registered x takes the same kernels, so repeated forwards are bit-identical."""
+    if (not getattr(x, _CONST, False) or x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1
+            or not x.is_cuda or x.requires_grad or x.size(0) < 32 or x.size(1) > 328):
         return None
     key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
     im = getattr(x, _ATTR_X, None)

@@ -516,6 +516,10 @@ def main(cfg: Dict) -> Dict:
     n_train = int(full.n_train)
     local = shard_graph(full, world, rank) if dist is not None else full
     data = local.to(device)
+    if device.type == "cuda":
+        from .planes import register_input
+
+        register_input(data.x)  # constant node features: layer-1 GEMMs on its split image
     ei = data.edge_index
     model = build_model(cfg["arch"], data.x.size(1), cfg).to(device)
     bucket = None

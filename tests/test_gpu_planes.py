@@ -263,11 +263,13 @@ def test_input_tn_on_x_only_image(device, F, nr):
     (x in columns [0, F), k2 = 0) and the f32-operand TN both within the split's error of float64;
     the planes are x's split bit for bit and follow an in-place edit of x."""
     from elliptic_gnn_project_amd.fused import gemm_tn_input
-    from elliptic_gnn_project_amd.planes import x_only_image
+    from elliptic_gnn_project_amd.planes import register_input, x_only_image
 
     N = 5000
     g0 = torch.Generator().manual_seed(F + nr)
     x = torch.randn(N, F, generator=g0).to(device)
+    assert x_only_image(x) is None  # unregistered inputs keep the f32 operand
+    register_input(x)
     G = torch.randn(N, nr, generator=g0).to(device)
     ref = (G.double().t() @ x.double()).cpu()
     from elliptic_gnn_project_amd.fused import gemm_tn
@@ -294,11 +296,11 @@ def test_input_nt_on_x_only_image(device, F, n, bias):
     """y = x·Wᵀ (+ b) for a model input x (GCN / GAT layer 1): the split-image NT over x's cached
     176-wide planes (N <= 128, N % 4 == 0) against float64, as the f32-operand NT is."""
     from elliptic_gnn_project_amd.fused import gemm_nt, gemm_nt_input
-    from elliptic_gnn_project_amd.planes import x_only_image
+    from elliptic_gnn_project_amd.planes import register_input, x_only_image
 
     N = 4099  # a ragged last row tile
     g0 = torch.Generator().manual_seed(F + n)
-    x = torch.randn(N, F, generator=g0).to(device)
+    x = register_input(torch.randn(N, F, generator=g0).to(device))
     W = (torch.randn(n, F, generator=g0) * 0.1).to(device)
     b = torch.randn(n, generator=g0).to(device) if bias else None
     ref = x.double() @ W.double().t() + (b.double() if bias else 0)
