@@ -40,7 +40,9 @@ namespace {
 // DMAs are asm statements (M0 set in the statement), hidden from hipcc's waitcnt pass, which would
 // otherwise drain them at the first LDS read after each barrier.
 // LAB (csrc/lab/lab_gemm.hip only): bit 1 no MFMAs, bit 2 no G slots, bit 4 no fragment reads.
-template <int KT, int LAB = 0>
+// GF: the g form (G read from a.g rows, no projection, no h mask: the GCN / GAT layer-1 weight
+// gradient) — the h ring carries g's rows, no dz copy.
+template <int KT, int LAB = 0, bool GF = false>
 __global__ __launch_bounds__(256) void gemm_tn_planes_dma_kernel(TNArgs a) {
   constexpr int ACH = 3 * PT_APL * 2;          // one A chunk buffer: 33792 B = 33 x 1 KB
   constexpr int NA = ACH / 1024;
@@ -81,23 +83,25 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_dma_kernel(TNArgs a) {
     return (uint32_t)(((int64_t)p * a.ap_ps + (int64_t)row * ld) * 2) + (pc < pr ? 16u * pc : 0u);
   };
   const int hcol = min(4 * (lane & 31), (int)a.Nr - 4);
+  const int ldhg = GF ? (int)a.ldg : (int)a.ldh;  // the h ring's rows: h, or g in the g form
+  constexpr int NDUP0 = GF ? NA + NH : NA + NH + 1;  // first count-padding instruction
   uint32_t voff[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int I = wave + 4 * j;
     if (I < NA) voff[j] = a_off(I);
-    else if (I < NA + NH) voff[j] = (uint32_t)(((2 * (I - NA) + (lane >> 5)) * (int)a.ldh + hcol) * 4);
-    else if (I == NA + NH) voff[j] = (uint32_t)(((lane >> 2) * (int)a.lddz + min(lane & 3, a.nproj - 1)) * 4);
-    else voff[j] = a_off(I - NA - NH - 1);  // count padding: a duplicate of A instruction 0 / 1 (same bytes, same slot)
+    else if (I < NA + NH) voff[j] = (uint32_t)(((2 * (I - NA) + (lane >> 5)) * ldhg + hcol) * 4);
+    else if (!GF && I == NA + NH) voff[j] = (uint32_t)(((lane >> 2) * (int)a.lddz + min(lane & 3, a.nproj - 1)) * 4);
+    else voff[j] = a_off(I - NDUP0);  // count padding: a duplicate of an A instruction (same bytes, same slot)
   }
   // prologue group of h(0) / dz(0) alone: 3 per wave (I' = wave + 4j: h 0..7, dz 8, duplicates of h 0..2)
   uint32_t voff0[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int I = wave + 4 * j;
-    const int k = I < NH ? I : I == NH ? 0 : I - NH - 1;
-    voff0[j] = I == NH ? (uint32_t)(((lane >> 2) * (int)a.lddz + min(lane & 3, a.nproj - 1)) * 4)
-                       : (uint32_t)(((2 * k + (lane >> 5)) * (int)a.ldh + hcol) * 4);
+    const int k = I < NH ? I : (!GF && I == NH) ? 0 : I - NH - (GF ? 0 : 1);
+    voff0[j] = (!GF && I == NH) ? (uint32_t)(((lane >> 2) * (int)a.lddz + min(lane & 3, a.nproj - 1)) * 4)
+                                : (uint32_t)(((2 * k + (lane >> 5)) * ldhg + hcol) * 4);
   }
   auto glds16 = [](const void* src, uint32_t dst) __attribute__((always_inline)) {
     unsigned keep;
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_dma_kernel(TNArgs a) {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
   };
   const char* const apb = reinterpret_cast<const char*>(a.ap);
-  const char* const hb = reinterpret_cast<const char*>(a.h);
+  const char* const hb = reinterpret_cast<const char*>(GF ? a.g : a.h);
   const char* const zb = reinterpret_cast<const char*>(a.dz);
   // DMA j of group g(c) = {A(c + 2) -> A buffer (c + 2) % 3, h / dz(c + 3) -> buffers (c + 3) % 3}.
   // The instruction's operand is wave-uniform; its parameters are chosen here, at kernel scope (a
@@ -125,18 +129,18 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_dma_kernel(TNArgs a) {
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int I = wave + 4 * j;
-    const bool isA = I < NA || I > NA + NH, isZ = I == NA + NH;
+    const bool isA = I < NA || I >= NDUP0, isZ = !GF && I == NA + NH;
     sbase[j] = isA ? (uint64_t)(uintptr_t)apb : isZ ? (uint64_t)(uintptr_t)zb : (uint64_t)(uintptr_t)hb;
-    srb[j] = isA ? ld * 2 : isZ ? (int)a.lddz * 4 : (int)a.ldh * 4;
+    srb[j] = isA ? ld * 2 : isZ ? (int)a.lddz * 4 : ldhg * 4;
     sofs[j] = isA ? 2 : 3;
     sstr[j] = isA ? ACH : isZ ? 256 : HCH;
-    sdst[j] = isA ? OA + (I < NA ? I : I - NA - NH - 1) * 1024 : isZ ? OZ : OH + (I - NA) * 1024;
+    sdst[j] = isA ? OA + (I < NA ? I : I - NDUP0) * 1024 : isZ ? OZ : OH + (I - NA) * 1024;
   }
   const bool zwave = wave == (NA + NH) % 4;  // the wave whose last DMA is dz's dword copy
   auto dma = [&](int j, int c) __attribute__((always_inline)) {
     const char* src = reinterpret_cast<const char*>(sbase[j]) + (int64_t)ldbase(min(c + sofs[j], clast)) * srb[j] + voff[j];
     const uint32_t dst = lds0 + (uint32_t)(sdst[j] + ((c + sofs[j]) % 3) * sstr[j]);
-    if (j == (NA + NH) / 4 && zwave) glds4(src, dst);
+    if (!GF && j == (NA + NH) / 4 && zwave) glds4(src, dst);
     else glds16(src, dst);
   };
   auto sync = [&]() __attribute__((always_inline)) {  // the ring's barrier: own LDS writes done, then every wave's
@@ -168,6 +172,10 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_dma_kernel(TNArgs a) {
       const int r = 8 * go + i;
       const bool ok = r >= (int)mbeg + k * PT_ROWS - mb && r < (int)mend - mb;
       hv[i] = hs[r * 128 + (gcol ? gn : 0)];
+      if constexpr (GF) {  // g rows outside the block's range: zero G
+        hv[i] = ok && gcol ? hv[i] : 0.f;
+        continue;
+      }
       const float4 z = *reinterpret_cast<const float4*>(zs + r * MAXPROJ);
       const float zs1 = zs[r * MAXPROJ + (gn & (MAXPROJ - 1))];
       zv[i] = ok ? z : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -175,6 +183,11 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_dma_kernel(TNArgs a) {
     }
   };
   auto g_row = [&](int i, int half) __attribute__((always_inline)) {
+    if constexpr (GF) {
+      if (half == 0) e[i] = hv[i];
+      else db += e[i];
+      return;
+    }
     if (half == 0) {
       const float4 z = zv[i];
       float g = z.x * pcol[0];
@@ -276,8 +289,9 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_dma_kernel(TNArgs a) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int I = wave + 4 * j;
-        if (I == NH) glds4(zb + (int64_t)mb * a.lddz * 4 + voff0[j], lds0 + (uint32_t)OZ);
-        else glds16(hb + (int64_t)mb * a.ldh * 4 + voff0[j], lds0 + (uint32_t)(OH + (I < NH ? I : I - NH - 1) * 1024));
+        if (!GF && I == NH) glds4(zb + (int64_t)mb * a.lddz * 4 + voff0[j], lds0 + (uint32_t)OZ);
+        else glds16(hb + (int64_t)mb * ldhg * 4 + voff0[j],
+                    lds0 + (uint32_t)(OH + (I < NH ? I : I - NH - (GF ? 0 : 1)) * 1024));
       }
     }
 #pragma unroll
@@ -426,6 +440,15 @@ template <int LAB>
 void tnd(const TNArgs& a, const NTArgs&, const uint4*, int nblk, int) {
   gemm_tn_planes_dma_kernel<11, LAB><<<nblk, 256>>>(a);
 }
+static TNArgs g_gcn;  // the GCN layer-1 TN: dW = Gᵀ·x over x's 176-wide image, Nr = 64, g form
+template <int LAB>
+void tng(const TNArgs&, const NTArgs&, const uint4*, int nblk, int) {
+  gemm_tn_planes_kernel<false, false, 6, false, LAB><<<nblk, 256>>>(g_gcn);
+}
+template <int LAB>
+void tngd(const TNArgs&, const NTArgs&, const uint4*, int nblk, int) {
+  gemm_tn_planes_dma_kernel<6, LAB, true><<<nblk, 256>>>(g_gcn);
+}
 template <int EPI>
 void nte(const TNArgs&, const NTArgs& a, const uint4* img, int, int ntiles) {
   gemm_nt_planes_kernel<21, EPI, 0><<<256, 256>>>(a, img, ntiles);
@@ -470,11 +493,24 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&bimg, 21 * 3 * 256 * 16));
   ws_prep_kernel<<<21, 256>>>(n, bimg, 21, nullptr, 0, 168);
   const int ntiles = (int)ceil_div(M, 32);
+  {  // GCN layer 1: x alone at 176-wide rows, G [M, 64]
+    uint16_t* img2;
+    CK(hipMalloc(&img2, 3 * M * 176 * 2));
+    gnn_split_planes_f32(x, 2 * F, M, F, img2, 176, M * 176, 0, 176, nullptr);
+    g_gcn = TNArgs{};
+    g_gcn.M = M; g_gcn.Nr = 64; g_gcn.g = dev_rand(M * 64, 1.f, 11); g_gcn.ldg = 64;
+    g_gcn.k1 = F; g_gcn.k2 = 0; g_gcn.hscale = 1.f;
+    g_gcn.slab = slab; g_gcn.slab_stride = (64 * F + 64 + 63) / 64 * 64;
+    g_gcn.rows_per_block = a.rows_per_block;
+    g_gcn.ap = img2; g_gcn.ap_ld = 176; g_gcn.ap_col2 = 168; g_gcn.ap_ps = M * 176;
+  }
   struct V { const char* name; void (*f)(const TNArgs&, const NTArgs&, const uint4*, int, int); std::vector<float> t; };
   std::vector<V> vs = {
       {"TN production", tn<0>, {}}, {"TN no MFMA", tn<1>, {}}, {"TN no staging", tn<2>, {}},
       {"TN no frag reads", tn<4>, {}}, {"TN no barrier", tn<8>, {}}, {"TN MFMA+frags", tn<2 | 8>, {}},
       {"TN MFMA only", tn<2 | 4 | 8>, {}}, {"TN staging only", tn<1 | 4>, {}},
+      {"GCN TN production", tng<0>, {}}, {"GCN TN dma", tngd<0>, {}}, {"GCN TN staging only", tng<1 | 4>, {}},
+      {"GCN TN dma DMA only", tngd<1 | 2 | 4>, {}},
       {"TN dma", tnd<0>, {}}, {"TN dma no MFMA", tnd<1>, {}}, {"TN dma no G", tnd<2>, {}},
       {"TN dma no frags", tnd<4>, {}}, {"TN dma DMA only", tnd<1 | 2 | 4>, {}},
       {"NT production", nt<0>, {}}, {"NT no MFMA", nt<1>, {}}, {"NT no epilogue", nt<2>, {}},
@@ -524,6 +560,20 @@ int main(int argc, char** argv) {
         md = std::max(md, (double)std::fabs(r0[i] - r1[i]));
       }
     std::printf("TN dma vs production: %zu of %zu slab words differ (max |diff| %g)\n", ndiff, nsl, md);
+    CK(hipMemset(slab, 0, nsl * 4));
+    tng<0>(a, n, bimg, nblk, ntiles);
+    CK(hipMemcpy(r0.data(), slab, nsl * 4, hipMemcpyDeviceToHost));
+    CK(hipMemset(slab, 0, nsl * 4));
+    tngd<0>(a, n, bimg, nblk, ntiles);
+    CK(hipMemcpy(r1.data(), slab, nsl * 4, hipMemcpyDeviceToHost));
+    ndiff = 0;
+    md = 0;
+    for (size_t i = 0; i < nsl; ++i)
+      if (std::memcmp(&r0[i], &r1[i], 4)) {
+        ++ndiff;
+        md = std::max(md, (double)std::fabs(r0[i] - r1[i]));
+      }
+    std::printf("GCN TN dma vs production: %zu of %zu slab words differ (max |diff| %g)\n", ndiff, nsl, md);
   }
   for (int r = 0; r < rounds; ++r)
     for (auto& v : vs) {
