@@ -82,8 +82,13 @@ __device__ __forceinline__ bf16x8 cat_frag(s16x4 a, s16x4 b) {
 // SIMD the staging issues in the MFMAs' shadow instead of in a phase of its own.
 // LAB (timing ablations, csrc/lab/lab_tn.hip only; the library instantiates 0): bit 1 no MFMAs,
 // bit 2 no staging slots, bit 4 no fragment reads in the loop, bit 8 no per-chunk barrier.
-template <bool PROJ, bool MASK, int KT, bool GOUT, int LAB = 0>
+// KS = 2 (Nr <= 64): waves 0-1 own dW rows 0..63 over the first half of the k-tiles, waves 2-3
+// the same rows over the second half (each dW element still one wave's chain: same results), so
+// no wave multiplies the zero G columns 64..127 and the MFMA chain the staging hides behind halves.
+template <bool PROJ, bool MASK, int KT, bool GOUT, int LAB = 0, int KS = 1>
 __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
+  static_assert(KT % KS == 0, "k-tiles split evenly");
+  constexpr int KW = KT / KS;  // k-tiles per wave
   __shared__ __attribute__((aligned(16))) uint16_t Gt[2][3 * PT_GPL];
   __shared__ __attribute__((aligned(16))) uint16_t At[2][3 * PT_APL];
   __shared__ float dzL[2][256];  // dz rows of a chunk (16 x 4), threads 0..63 write theirs
@@ -97,9 +102,11 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   const int64_t mend = min(a.M, mbeg + a.rows_per_block);
   const int nch = mend > mbeg ? (int)((mend - mbeg + PT_ROWS - 1) / PT_ROWS) : 0;
 
-  floatx16 acc[KT];
+  const int wr = KS == 2 ? (wave & 1) : wave;  // the wave's 32 dW rows
+  const int t0 = KS == 2 ? (wave >> 1) * KW : 0;  // its first k-tile
+  floatx16 acc[KW];
 #pragma unroll
-  for (int t = 0; t < KT; ++t)
+  for (int t = 0; t < KW; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
 
@@ -282,7 +289,7 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
 
   // fragment addresses: G rows 32·wave + (lane & 31), k = 8·(lane >> 5); A (transposed reads)
   // lane 4q + p of 16-lane group g supplies row 8·(g >> 1) + q, columns 16·(g & 1) + 4p ..
-  const int gfo = (32 * wave + (lane & 31)) * PT_GP + 8 * (lane >> 5);
+  const int gfo = (32 * wr + (lane & 31)) * PT_GP + 8 * (lane >> 5);
   const int grp = lane >> 4, li = lane & 15;
   const int afo = (8 * (grp >> 1) + (li >> 2)) * PT_AP + 16 * (grp & 1) + 4 * (li & 3);
   auto afrag = [&](const uint16_t* base, int t, int p) {
@@ -297,15 +304,15 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
     for (int p = 0; p < 3; ++p) gf[p] = *reinterpret_cast<const bf16x8*>(Gt[buf] + p * PT_GPL + gfo);
     const uint16_t* ab = At[buf] + afo;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) af[0][p] = afrag(ab, 0, p);
+    for (int p = 0; p < 3; ++p) af[0][p] = afrag(ab, t0, p);
     // tile t+1's fragment reads are issued before tile t's MFMAs (in flight across them); one
     // staging slot after each MFMA (fences pin the order: the slot issues in the MFMA's shadow)
     constexpr int pa[6] = {1, 2, 0, 1, 0, 0}, pb[6] = {1, 0, 2, 0, 1, 0};  // small terms first
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-      if (t + 1 < KT && !(LAB & 4)) {
+    for (int t = 0; t < KW; ++t) {
+      if (t + 1 < KW && !(LAB & 4)) {
 #pragma unroll
-        for (int p = 0; p < 3; ++p) af[(t + 1) & 1][p] = afrag(ab, t + 1, p);
+        for (int p = 0; p < 3; ++p) af[(t + 1) & 1][p] = afrag(ab, t0 + t + 1, p);
       }
 #pragma unroll
       for (int m = 0; m < 6; ++m) {
@@ -318,11 +325,11 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
       PT_FENCE;
     }
 #pragma unroll
-    for (int u = 6 * KT; u < NU; ++u)  // narrow images: the slots past the MFMAs
+    for (int u = 6 * KW; u < NU; ++u)  // narrow images: the slots past the MFMAs
       if (!(LAB & 2)) unit(u, c);
     if constexpr ((LAB & 1) != 0) {  // keep the fragments live
 #pragma unroll
-      for (int t = 0; t < KT; ++t) acc[t][0] += (float)gf[0][0] + (float)af[0][0][0] + (float)af[1][1][1];
+      for (int t = 0; t < KW; ++t) acc[t][0] += (float)gf[0][0] + (float)af[0][0][0] + (float)af[1][1][1];
     }
   };
 #undef PT_FENCE
@@ -363,13 +370,13 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
   const int Kc = a.k1 + a.k2;
 #pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    const int kp = t * 32 + (lane & 31);  // image column
+  for (int t = 0; t < KW; ++t) {
+    const int kp = (t0 + t) * 32 + (lane & 31);  // image column
     const bool s1 = kp < a.k1;
     const bool s2 = kp >= a.ap_col2 && kp < a.ap_col2 + a.k2;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int row = 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       const int64_t idx = s1 ? (int64_t)row * a.k1 + kp : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (kp - a.ap_col2);
       if (row < a.Nr && (s1 || s2)) slab[idx] = acc[t][r];
     }
@@ -667,6 +674,13 @@ void launch_tn_img16_kt(const TNArgs& a, int nblk, hipStream_t st) {
 
 template <bool PROJ, bool MASK, int KT>
 void launch_tn_planes_k(const TNArgs& a, int nblk, hipStream_t st) {
+  if constexpr (KT % 2 == 0) {
+    if (a.Nr <= 64) {  // split K across the wave pairs (GCN / GAT layer 1, N = 64)
+      if (a.gout) gemm_tn_planes_kernel<PROJ, MASK, KT, true, 0, 2><<<nblk, 256, 0, st>>>(a);
+      else gemm_tn_planes_kernel<PROJ, MASK, KT, false, 0, 2><<<nblk, 256, 0, st>>>(a);
+      return;
+    }
+  }
   if (a.gout) gemm_tn_planes_kernel<PROJ, MASK, KT, true><<<nblk, 256, 0, st>>>(a);
   else gemm_tn_planes_kernel<PROJ, MASK, KT, false><<<nblk, 256, 0, st>>>(a);
 }

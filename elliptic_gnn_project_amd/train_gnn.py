@@ -314,12 +314,15 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(side)
         self.mid = mid
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread-local capture mode: the process group's watchdog thread keeps querying the events
+        # of earlier (eager) collectives while this thread captures; in the default global mode
+        # such a query from another thread invalidates the capture (hipErrorStreamCaptureUnsupported)
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = step_fn()
         self.tail_graph = None
         if tail is not None:
             self.tail_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.tail_graph, pool=self.graph.pool()):
+            with torch.cuda.graph(self.tail_graph, pool=self.graph.pool(), capture_error_mode="thread_local"):
                 tail()
 
     def __call__(self):
