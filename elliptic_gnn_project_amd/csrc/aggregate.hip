@@ -185,10 +185,10 @@ constexpr int kU = 4;  // slots in flight per group (r11 lab: 8 measured 12-25 %
 // PF: the next kU neighbour ids are loaded behind this walk step's row loads (one dependent
 // round trip per step instead of two).
 template <int MODE, int VEC, int LPS, int NCHMAX, bool PF = false>
-__global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
+__device__ __forceinline__ void agg_flat_body(const AggArgs& a, int32_t rpg, int64_t bid) {
   const int gl = threadIdx.x & (LPS - 1);
   const int gbase = (threadIdx.x & 63) & ~(LPS - 1);
-  const int64_t group = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPS;
+  const int64_t group = (bid * 256 + threadIdx.x) / LPS;
   const int64_t r0 = group * rpg;
   if (r0 >= a.nrows) return;  // group-uniform
   const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
@@ -300,6 +300,11 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
     }
   }
   for (; j < nrow; ++j) flush(j);  // the last open row and any trailing empty rows
+}
+
+template <int MODE, int VEC, int LPS, int NCHMAX, bool PF = false>
+__global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
+  agg_flat_body<MODE, VEC, LPS, NCHMAX, PF>(a, rpg, blockIdx.x);
 }
 
 // Wave-wide groups (LPS = 64, F/VEC > 32 chunks, e.g. the 166-wide layer-1 features):
@@ -648,10 +653,11 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
 // ---- long-segment split: pieces 1.. of every long segment, then the ordered combine.
 // Wide rows: one wave per piece, lanes over features, U neighbour rows in flight.
 template <int MODE, int VEC, int NCH>
-__global__ __launch_bounds__(256) void agg_piece_wide_kernel(AggArgs a, int64_t npieces, const int32_t* piece_seg) {
+__device__ __forceinline__ void agg_piece_wide_body(const AggArgs& a, int64_t npieces, const int32_t* piece_seg,
+                                                    int64_t bid) {
   constexpr int U = 8;
   const int lane = threadIdx.x & 63;
-  const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t p = (bid * 256 + threadIdx.x) >> 6;
   if (p >= npieces) return;
   const int32_t r = piece_seg[p];
   const int32_t k = (int32_t)p - a.piece0[r];
@@ -692,6 +698,21 @@ __global__ __launch_bounds__(256) void agg_piece_wide_kernel(AggArgs a, int64_t 
     const int c = lane + 64 * i;
     if (c < nchunk) vstore<VEC>(a.part + p * a.F + c * VEC, acc[i]);
   }
+}
+
+template <int MODE, int VEC, int NCH>
+__global__ __launch_bounds__(256) void agg_piece_wide_kernel(AggArgs a, int64_t npieces, const int32_t* piece_seg) {
+  agg_piece_wide_body<MODE, VEC, NCH>(a, npieces, piece_seg, blockIdx.x);
+}
+
+// The split main pass and the split pieces in ONE launch: blocks [0, pblocks) walk the long
+// segments' pieces (one wave each, launched first so the hubs start early), the rest the
+// degree-ordered main pass; both only write (partials / rows), the combine pass follows.
+template <int MODE, int VEC, int LPS, int NCHMAX>
+__global__ __launch_bounds__(256) void agg_flat_pieces_kernel(AggArgs a, int32_t rpg, int64_t npieces,
+                                                              const int32_t* piece_seg, uint32_t pblocks) {
+  if (blockIdx.x < pblocks) agg_piece_wide_body<MODE, VEC, 1>(a, npieces, piece_seg, blockIdx.x);
+  else agg_flat_body<MODE, VEC, LPS, NCHMAX>(a, rpg, (int64_t)blockIdx.x - pblocks);
 }
 
 // Narrow rows (F <= 8): one wave per piece, lanes over its <= 64 slots, fixed xor tree.
@@ -781,12 +802,21 @@ void launch_split_v(const AggArgs& a, const gnn_split* sp, hipStream_t st) {
 
 
 template <int MODE>
-gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp);
+gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp,
+                       const gnn_split* pieces = nullptr, bool* pieces_done = nullptr);
 
 template <int MODE>
 gnn_status launch_mode_split(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp) {
-  gnn_status s = launch_mode<MODE>(a, vec, st, nullptr);  // main pass over the truncated segments
+  bool pieces_done = false;  // the lane-group main pass takes the pieces into its own launch
+  gnn_status s = launch_mode<MODE>(a, vec, st, nullptr, sp, &pieces_done);  // main pass over the truncated segments
   if (s != GNN_OK || sp->num_long == 0) return s;
+  if (pieces_done) {
+    const int nch = (int)ceil_div(a.F / vec, 64);
+    if (vec == 4 && nch <= 1) agg_combine_kernel<MODE, 4, 1><<<(unsigned)ceil_div(sp->num_long * 64, 256), 256, 0, st>>>(a, sp->num_long, sp->long_seg);
+    else if (vec == 2 && nch <= 1) agg_combine_kernel<MODE, 2, 1><<<(unsigned)ceil_div(sp->num_long * 64, 256), 256, 0, st>>>(a, sp->num_long, sp->long_seg);
+    else agg_combine_kernel<MODE, 1, 1><<<(unsigned)ceil_div(sp->num_long * 64, 256), 256, 0, st>>>(a, sp->num_long, sp->long_seg);
+    return hip_check(hipGetLastError(), "gnn_aggregate_f32 (split combine)");
+  }
   if (a.F <= 8) {
     if (sp->num_pieces > sp->num_long)
       agg_piece_narrow_kernel<MODE><<<(unsigned)ceil_div(sp->num_pieces * 64, 256), 256, 0, st>>>(
@@ -804,7 +834,8 @@ gnn_status launch_mode_split(const AggArgs& a, int vec, hipStream_t st, const gn
 }
 
 template <int MODE>
-gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp) {
+gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_split* sp, const gnn_split* pieces,
+                       bool* pieces_done) {
   if (a.nrows == 0 || a.F == 0) return GNN_OK;
   if (sp) return launch_mode_split<MODE>(a, vec, st, sp);
   if (a.F <= 4 && (MODE == GNN_AGG_MEAN || MODE == GNN_AGG_MEAN_BWD || MODE == GNN_AGG_SUM)) {
@@ -845,10 +876,18 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     const int64_t groups = ceil_div(a.nrows, rpg);
     const unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
     const bool pf = lv == 10 || lv == 11;  // lab: neighbour-id prefetch (r14: 5-10 us slower)
-#define GNN_FLAT(V, L, NC)                                                      \
-  do {                                                                          \
-    if (pf) agg_flat_kernel<MODE, V, L, NC, true><<<blocks, 256, 0, st>>>(a, rpg); \
-    else agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg);         \
+    // split pieces (one wave each) folded into the main pass's launch when one wave covers F
+    const bool fold = pieces && pieces->num_pieces > pieces->num_long && !pf && nchunk <= 64 && lv != 16 &&
+                      !(lps == 64 && nchunk <= 128);  // (the wave-kernel path keeps its own passes)
+    const unsigned pblocks = fold ? (unsigned)ceil_div(pieces->num_pieces * 64, 256) : 0u;
+    if (fold && pieces_done) *pieces_done = true;
+#define GNN_FLAT(V, L, NC)                                                                                 \
+  do {                                                                                                     \
+    if (pf) agg_flat_kernel<MODE, V, L, NC, true><<<blocks, 256, 0, st>>>(a, rpg);                            \
+    else if (fold)                                                                                         \
+      agg_flat_pieces_kernel<MODE, V, L, NC><<<blocks + pblocks, 256, 0, st>>>(a, rpg, pieces->num_pieces,   \
+                                                                           pieces->piece_seg, pblocks);    \
+    else agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg);                                    \
   } while (0)
 #define GNN_FLAT_V(V)                      \
   do {                                     \
