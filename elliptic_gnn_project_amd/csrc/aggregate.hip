@@ -876,9 +876,10 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     const int64_t groups = ceil_div(a.nrows, rpg);
     const unsigned blocks = (unsigned)ceil_div(groups * lps, 256);
     const bool pf = lv == 10 || lv == 11;  // lab: neighbour-id prefetch (r14: 5-10 us slower)
-    // split pieces (one wave each) folded into the main pass's launch when one wave covers F
-    const bool fold = pieces && pieces->num_pieces > pieces->num_long && !pf && nchunk <= 64 && lv != 16 &&
-                      !(lps == 64 && nchunk <= 128);  // (the wave-kernel path keeps its own passes)
+    // split pieces (one wave each) folded into the main pass's launch: 16-lane groups only (r17:
+    // F = 64 passes 10-12 us faster; at F = 128 (32-lane groups) the scaled config's CSC pass
+    // measured 1463 -> 1679 us, the pieces' registers lowering the main pass's occupancy)
+    const bool fold = pieces && pieces->num_pieces > pieces->num_long && !pf && lps == 16 && lv != 16;
     const unsigned pblocks = fold ? (unsigned)ceil_div(pieces->num_pieces * 64, 256) : 0u;
     if (fold && pieces_done) *pieces_done = true;
 #define GNN_FLAT(V, L, NC)                                                                                 \
