@@ -98,6 +98,18 @@ __global__ void sample_fill_kernel(const int32_t* __restrict__ rowptr, const int
     for (int j = 0; j < d; ++j) emit(j, j);
     return;
   }
+  if (c > kMaxFanout) {  // more picks than the Floyd buffer: selection sampling (Knuth's
+    // algorithm S) — slot j kept with probability need / (d - j), one pass, already in CSR order
+    int32_t need = c, m = 0;
+    for (int32_t j = 0; j < d && need > 0; ++j) {
+      const uint64_t u = sample_hash(seed, hop, (uint32_t)v, (uint32_t)j);
+      if (((u * (uint64_t)(d - j)) >> 32) < (uint64_t)need) {
+        emit(m++, j);
+        --need;
+      }
+    }
+    return;
+  }
   int32_t sel[kMaxFanout];
   int m = 0;
   for (int32_t j = d - c; j < d; ++j) {
@@ -223,8 +235,8 @@ extern "C" gnn_status gnn_neighbor_sample(const gnn_graph* g, const int32_t* csr
   if (num_seeds > node_cap || (num_seeds > 0 && (!seeds || !n_id)))
     return fail(GNN_ERR_INVALID_ARG, fn, "node_cap smaller than the seed count");
   for (int h = 0; h < num_hops; ++h)
-    if (fanout[h] > kMaxFanout || fanout[h] == 0 || fanout[h] < -1)
-      return fail(GNN_ERR_INVALID_ARG, fn, "fanout must be -1 (all) or in [1, 256]");
+    if (fanout[h] == 0 || fanout[h] < -1)
+      return fail(GNN_ERR_INVALID_ARG, fn, "fanout must be -1 (all) or >= 1");
   const int64_t N = g->num_nodes;
   if (N >= INT_MAX || node_cap >= INT_MAX || edge_cap >= INT_MAX) return fail(GNN_ERR_INVALID_ARG, fn, "int32 sizes");
   WorkspaceCarver c(workspace, workspace_bytes);

@@ -42,8 +42,8 @@ class NeighborLoader:
             raise ValueError("batch_size must be >= 1")
         self.num_neighbors = [int(k) for k in num_neighbors]
         for k in self.num_neighbors:
-            if k == 0 or k < -1 or k > 256:
-                raise ValueError(f"num_neighbors entries must be -1 or in [1, 256], got {k}")
+            if k == 0 or k < -1:
+                raise ValueError(f"num_neighbors entries must be -1 or >= 1, got {k}")
         dev = torch.device(device) if device is not None else data.x.device
         if dev.type != "cuda":
             raise RuntimeError("NeighborLoader samples on the MI355X (HIP) device; pass device='cuda' "

@@ -478,7 +478,7 @@ gnn_status gnn_neighbor_sample_workspace_size(int64_t num_nodes, int64_t node_ca
 
 /* Sample one batch over the CSR-by-target direction of `g` (a GNN_LOOPS_KEEP plan of the
  * full graph's edge_index): seeds[num_seeds] (distinct, device int32) become local nodes
- * 0..B-1; hop h samples up to fanout[h] (host array; -1 = all, else 1..256) in-neighbours of
+ * 0..B-1; hop h samples up to fanout[h] (host array; -1 = all, else >= 1) in-neighbours of
  * every node first discovered in hop h-1, uniformly without replacement (all of them when the
  * in-degree is <= fanout), from a counter hash of (seed, hop, node, draw).  New nodes are
  * appended to n_id in order of first appearance in the hop's edge list (disjoint=False dedup).

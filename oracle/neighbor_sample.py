@@ -13,7 +13,8 @@ What is PyG's contract and what is ours:
   fanout = -1 everywhere the result is the deterministic k-hop in-neighbourhood, which
   ``khop_known_answer`` states independently (a BFS) — the PyG-semantics known answer.
 * Ours: WHICH fanout-subset is drawn comes from a counter hash of (seed, hop, node, draw) and
-  Floyd's algorithm (csrc/sample.hip), picks emitted in ascending CSR position; this module
+  Floyd's algorithm (csrc/sample.hip; selection sampling, Knuth's algorithm S, above 256 picks),
+  picks emitted in ascending CSR position; this module
   reproduces those draws bit for bit so the HIP sampler is checked exactly.  PyG's RNG stream
   (pyg-lib) is not reproducible: the choice of subset is "parity unpinned" against PyG.
 Pure Python loops: small graphs only.
@@ -52,6 +53,15 @@ def pick_positions(deg: int, k: int, seed: int, hop: int, node: int) -> List[int
     c = deg if k < 0 else min(deg, k)
     if c == deg:
         return list(range(deg))
+    if c > 256:  # more picks than the kernel's Floyd buffer: selection sampling (algorithm S)
+        out, need = [], c
+        for j in range(deg):
+            if need == 0:
+                break
+            if (sample_hash(seed, hop, node, j) * (deg - j)) >> 32 < need:
+                out.append(j)
+                need -= 1
+        return out
     sel: List[int] = []
     for j in range(deg - c, deg):
         t = (sample_hash(seed, hop, node, j) * (j + 1)) >> 32

@@ -1,7 +1,7 @@
 """GPU: K11 NeighborLoader sampling (csrc/sample.hip) through the C ABI.
 
 * bit-exact against the CPU restatement (oracle/neighbor_sample.py, same counter hash and
-  Floyd draws) on graphs with hubs, duplicate edges, self loops and isolated nodes, for the
+  Floyd draws; selection sampling above 256 picks) on graphs with hubs, duplicate edges, self loops and isolated nodes, for the
   reference's fan-out [10, 10] and others, including -1 (all: PyG's deterministic k-hop case,
   pinned in tests/test_sampler_oracle.py against a BFS statement of PyG's semantics);
 * at the Elliptic size (203,769 nodes, batch 8192, fan-out [10, 10], src/train_gnn.py:333-348)
@@ -48,7 +48,9 @@ def _loader_for(device, ei, n, fanout, bs):
     return NeighborLoader(data, num_neighbors=fanout, batch_size=bs)
 
 
-@pytest.mark.parametrize("fanout", [[10, 10], [2, 3], [-1, -1], [1], [25, 10, 5], [3, -1]])
+# [280]: more picks than the kernel's 256-entry Floyd buffer at the hub (in-degree ~300): the
+# selection-sampling path (algorithm S), checked against the oracle's restatement of it
+@pytest.mark.parametrize("fanout", [[10, 10], [2, 3], [-1, -1], [1], [25, 10, 5], [3, -1], [280], [280, 2]])
 def test_sampler_matches_oracle(device, fanout):
     n = 400
     ei = _graph(n, 1500, 1)
@@ -75,7 +77,9 @@ def test_sampler_errors(device):
     b = ld.sample(torch.tensor([], dtype=torch.int64), seed=0)
     assert b.n_id.numel() == 0 and b.edge_index.shape == (2, 0)
     with pytest.raises(ValueError):
-        _loader_for(device, ei, n, [300], 8)
+        _loader_for(device, ei, n, [0], 8)
+    with pytest.raises(ValueError):
+        _loader_for(device, ei, n, [3, -2], 8)
 
 
 def test_sampler_elliptic_size_contract(device):

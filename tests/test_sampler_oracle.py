@@ -63,6 +63,20 @@ def test_uniform_selection():
     assert np.all(np.abs(freq - 3 / 12) < 0.035), freq
 
 
+def test_uniform_selection_above_floyd_buffer():
+    """More than 256 picks (selection sampling): exactly k distinct positions, ascending, each
+    position of a degree-400 row drawn with p = k/deg."""
+    deg, k, trials = 400, 300, 400
+    counts = np.zeros(deg)
+    for s in range(trials):
+        picks = NS.pick_positions(deg, k, seed=s, hop=1, node=9)
+        assert len(picks) == k and picks == sorted(set(picks)) and 0 <= picks[0] and picks[-1] < deg
+        counts[picks] += 1
+    freq = counts / trials
+    assert abs(freq.mean() - k / deg) < 1e-12
+    assert np.all(np.abs(freq - k / deg) < 0.1), freq
+
+
 def test_duplicate_seeds_rejected():
     with pytest.raises(ValueError):
         NS.neighbor_sample(_graph(10, 20, 3), 10, [1, 1], [2], seed=0)
