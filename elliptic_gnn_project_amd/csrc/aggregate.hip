@@ -185,10 +185,10 @@ constexpr int kU = 4;  // slots in flight per group (r11 lab: 8 measured 12-25 %
 // PF: the next kU neighbour ids are loaded behind this walk step's row loads (one dependent
 // round trip per step instead of two).
 template <int MODE, int VEC, int LPS, int NCHMAX, bool PF = false>
-__device__ __forceinline__ void agg_flat_body(const AggArgs& a, int32_t rpg, int64_t bid) {
+__device__ __forceinline__ void agg_flat_body(const AggArgs& a, int32_t rpg, uint32_t bid) {
   const int gl = threadIdx.x & (LPS - 1);
   const int gbase = (threadIdx.x & 63) & ~(LPS - 1);
-  const int64_t group = (bid * 256 + threadIdx.x) / LPS;
+  const int64_t group = ((int64_t)bid * 256 + threadIdx.x) / LPS;
   const int64_t r0 = group * rpg;
   if (r0 >= a.nrows) return;  // group-uniform
   const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
@@ -302,9 +302,125 @@ __device__ __forceinline__ void agg_flat_body(const AggArgs& a, int32_t rpg, int
   for (; j < nrow; ++j) flush(j);  // the last open row and any trailing empty rows
 }
 
+// The standalone launch keeps its own copy of the walk (agg_flat_body below is the same code for
+// the pieces-folded launch): routed through the device function, hipcc scheduled the 32-lane
+// F = 128 pass differently and it measured 11 % slower (r17: 1473 -> 1641 us, scaled config).
 template <int MODE, int VEC, int LPS, int NCHMAX, bool PF = false>
 __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
-  agg_flat_body<MODE, VEC, LPS, NCHMAX, PF>(a, rpg, blockIdx.x);
+  const int gl = threadIdx.x & (LPS - 1);
+  const int gbase = (threadIdx.x & 63) & ~(LPS - 1);
+  const int64_t group = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPS;
+  const int64_t r0 = group * rpg;
+  if (r0 >= a.nrows) return;  // group-uniform
+  const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
+  const int nchunk = a.F / VEC;
+  const int nch = (nchunk + LPS - 1) / LPS;
+  const int32_t myptr = a.ptr[r0 + min(gl, nrow)];
+  // row of this lane's position (degree-ordered split main pass: positions are not rows)
+  const int32_t myrow = a.order ? a.order[r0 + min(gl, nrow - 1)] : (int32_t)(r0 + min(gl, nrow - 1));
+  float mydeg = 1.0f;
+  if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[myrow];
+  const int32_t mypiece = a.piece0 ? a.piece0[myrow] : -1;
+  auto ptr_at = [&](int j) { return __shfl(myptr, gbase + j); };
+  auto row_at = [&](int j) { return a.order ? __shfl(myrow, gbase + j) : (int32_t)(r0 + j); };
+
+  float acc[NCHMAX][VEC];
+#pragma unroll
+  for (int i = 0; i < NCHMAX; ++i)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+
+  const uint64_t dseed = a.dropout ? agg_seed(a) : 0;
+  auto flush = [&](int j) {
+    const int64_t r = row_at(j);
+    float d = 1.0f;
+    if constexpr (MODE == GNN_AGG_MEAN) d = fmaxf(__shfl(mydeg, gbase + j), 1.0f);
+    const int32_t p0 = __shfl(mypiece, gbase + j);
+#pragma unroll
+    for (int i = 0; i < NCHMAX; ++i) {
+      const int c = gl + LPS * i;
+      if (i < nch && c < nchunk && p0 >= 0) {  // long row: raw partial of piece 0
+        vstore<VEC>(a.part + (int64_t)p0 * a.F + c * VEC, acc[i]);
+      } else if (i < nch && c < nchunk) {
+        const int f0 = c * VEC;
+        float t[VEC];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) t[q] = (MODE == GNN_AGG_MEAN) ? acc[i][q] / d : acc[i][q];
+        if (a.add) {
+          float ad[VEC];
+          vload<VEC>(a.add + r * a.ld_add + f0, ad);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += ad[q];
+        }
+        if (a.bias) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += a.bias[f0 + q];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] = fmaxf(t[q], 0.0f);
+        }
+        if (a.dropout) agg_dropout<VEC>(a, dseed, r, f0, t);
+        vstore<VEC>(a.y + r * a.ldy + f0, t);
+      }
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+    }
+  };
+
+  const int32_t send = ptr_at(nrow);
+  int j = 0;
+  int32_t cend = ptr_at(1);
+  int32_t crow = row_at(0);
+  const int32_t sbeg = ptr_at(0);
+  int32_t n[kU];
+  if constexpr (PF) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) n[u] = a.nbr[sbeg + u < send ? sbeg + u : max(send - 1, sbeg)];
+  }
+  for (int32_t s = sbeg; s < send; s += kU) {
+    if constexpr (!PF) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) n[u] = a.nbr[s + u < send ? s + u : s];
+    }
+    float v[kU][NCHMAX][VEC];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int i = 0; i < NCHMAX; ++i)
+        if (i < nch) {
+          const int c = gl + LPS * i;
+          vload<VEC>(a.x + (int64_t)n[u] * a.ldx + (c < nchunk ? c : 0) * VEC, v[u][i]);
+        }
+    int32_t nn[kU];
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) nn[u] = a.nbr[min(s + kU + u, send - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int32_t k = s + u;
+      if (k >= send) break;
+      while (k >= cend) {  // passing one or more row ends (empty rows flush zeros)
+        flush(j);
+        ++j;
+        cend = ptr_at(j + 1);
+        crow = row_at(j);
+      }
+#pragma unroll
+      for (int i = 0; i < NCHMAX; ++i)
+        if (i < nch) {
+          contrib<MODE, VEC>(a, n[u], crow, k, (gl + LPS * i) * VEC, v[u][i]);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];
+        }
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) n[u] = nn[u];
+    }
+  }
+  for (; j < nrow; ++j) flush(j);  // the last open row and any trailing empty rows
 }
 
 // Wave-wide groups (LPS = 64, F/VEC > 32 chunks, e.g. the 166-wide layer-1 features):
@@ -654,10 +770,10 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
 // Wide rows: one wave per piece, lanes over features, U neighbour rows in flight.
 template <int MODE, int VEC, int NCH>
 __device__ __forceinline__ void agg_piece_wide_body(const AggArgs& a, int64_t npieces, const int32_t* piece_seg,
-                                                    int64_t bid) {
+                                                    uint32_t bid) {
   constexpr int U = 8;
   const int lane = threadIdx.x & 63;
-  const int64_t p = (bid * 256 + threadIdx.x) >> 6;
+  const int64_t p = ((int64_t)bid * 256 + threadIdx.x) >> 6;
   if (p >= npieces) return;
   const int32_t r = piece_seg[p];
   const int32_t k = (int32_t)p - a.piece0[r];
@@ -712,7 +828,7 @@ template <int MODE, int VEC, int LPS, int NCHMAX>
 __global__ __launch_bounds__(256) void agg_flat_pieces_kernel(AggArgs a, int32_t rpg, int64_t npieces,
                                                               const int32_t* piece_seg, uint32_t pblocks) {
   if (blockIdx.x < pblocks) agg_piece_wide_body<MODE, VEC, 1>(a, npieces, piece_seg, blockIdx.x);
-  else agg_flat_body<MODE, VEC, LPS, NCHMAX>(a, rpg, (int64_t)blockIdx.x - pblocks);
+  else agg_flat_body<MODE, VEC, LPS, NCHMAX>(a, rpg, blockIdx.x - pblocks);
 }
 
 // Narrow rows (F <= 8): one wave per piece, lanes over its <= 64 slots, fixed xor tree.
