@@ -98,3 +98,39 @@ def test_ordered_pass_bitwise_equals_plan_order(device, sym, loops_name, mode, t
         nodew = p.dinv if mode == "GCN" else p.deg
         outs.append(aggregate(p, x, getattr(_lib, f"AGG_{mode}"), transpose=transpose, nodew=nodew, **kw))
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("sym,loops_name,mode,transpose,F,epi", [c for c in CASES if c[4] == 64])
+def test_pieces_in_main_launch_bitwise(device, sym, loops_name, mode, transpose, F, epi):
+    """16-lane groups (F = 64): the split pieces walked inside the main pass's launch
+    (agg_flat_pieces_kernel) give the results of the separate piece launch bit for bit (lab knob
+    gnnx_set_agg_variant(16) keeps the pieces in their own launch)."""
+    import ctypes
+
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.aggregation import aggregate
+
+    loops = _lib.LOOPS_KEEP if loops_name == "keep" else _lib.LOOPS_REPLACE
+    g = _graph(sym)
+    N = g.x.size(0)
+    p = _plans(g.edge_index, N, loops, device)["1"]
+    if p.split_pieces(transpose) == 0:
+        pytest.skip("no long segments in this direction (the directed graph's out-degrees)")
+    gen = torch.Generator().manual_seed(F + 1)
+    x = torch.randn(N, F, generator=gen).to(device)
+    kw = dict(epi)
+    if kw.pop("addend", False):
+        kw["addend"] = torch.randn(N, F, generator=gen).to(device)
+    kw["bias"] = torch.randn(F, generator=gen).to(device)
+    nodew = p.dinv if mode == "GCN" else p.deg
+    setv = _lib.load().gnnx_set_agg_variant
+    setv.argtypes = [ctypes.c_int]
+    setv.restype = None
+    outs = []
+    try:
+        for v in (0, 16):
+            setv(v)
+            outs.append(aggregate(p, x, getattr(_lib, f"AGG_{mode}"), transpose=transpose, nodew=nodew, **kw))
+    finally:
+        setv(0)
+    assert torch.equal(outs[0], outs[1])
