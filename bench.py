@@ -85,7 +85,43 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only for multi-rank tests on one device")
     ap.add_argument("--cpu-1t-seconds", type=float, default=8.0, help="1-thread CPU baseline sample budget")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="CPU rehearsal of the N>1 launch (tests): ranks rendezvous, build and shard the global "
+                         "graph, time an empty step, reduce and report; no device work")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: this rank raises
     return ap.parse_args()
+
+
+def self_launch(args) -> int:
+    """`python bench.py --gpus N` without a launcher (N > 1, WORLD_SIZE unset): start N rank
+    processes through torch.distributed.run (127.0.0.1, a free port) as CHILD processes — this
+    process never touches the GPU and never exec()s — relay rank 0's JSON line on stdout (the
+    ranks' other output goes to stderr) and return non-zero if any rank failed."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / tensor sharing across ranks)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    line_out = None
+    for line in proc.stdout:
+        txt = line.strip()
+        if txt.startswith("{") and '"metric"' in txt and line_out is None:
+            line_out = txt
+            print(txt, flush=True)
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if rc == 0 and line_out is None:
+        sys.stderr.write("bench.py: the ranks exited without a result line\n")
+        return 1
+    return rc
 
 
 def make_global_graph(world: int, scale: str, degree: str, cfg, gen=None):
@@ -211,32 +247,45 @@ def cpu_baseline(data, state, cw, denom, cfg, budget_s: float, budget_1t: float)
 MFMA_F32_PEAK_TFS = 157.3  # gfx950 dense fp32 MFMA (= vector fp32) peak, MI355X_MICROARCH.md
 
 
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_latest.json")
+def traffic_file(arch):
+    """The PMC traffic summary of this workload: profiles/collect.sh (ARCH=<arch>) writes
+    traffic.json for the bench command of that arch; the committed copy is profiles/traffic_<arch>.json."""
+    return os.path.join(ROOT, "profiles", f"traffic_{arch}.json")
 
 
-def measured_traffic(tag):
-    """HBM bytes per launch of the bench's dominant kernel from the committed PMC summary
-    (profiles/pmc_summary.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same
-    command, gfx950-corrected).  None when no summary matches the kernel and shape."""
+def kernel_pattern(tag):
+    """Regex of the libgnnmp kernel a timed launch runs, keyed on its template signature (the tag
+    fixes the instantiation's leading parameters): NT k-steps = ceil(K/16), TN k-tiles = ceil(K/32),
+    the aggregation mode and its kernel family by width.  None when no family is known."""
+    import re
+
+    if tag[0] == "gemm_nt":
+        return re.compile(r"gemm_nt_(planes|ws|img16)_kernel<%d[,>]" % -(-tag[2] // 16))
+    if tag[0] == "gemm_tn":
+        return re.compile(r"gemm_tn_(planes|img16)_kernel<\w+, \w+, %d," % -(-tag[2] // 32))
+    if tag[0] == "agg":
+        mode, F = tag[1], tag[3]
+        fam = "agg_wave_kernel" if F > 128 else "agg_narrow_lds_kernel" if F <= 4 else "agg_flat(_pieces)?_kernel"
+        return re.compile(r"%s<%d," % (fam, mode))
+    return None
+
+
+def measured_traffic(tag, arch):
+    """(HBM bytes per launch, source) of the timed kernel from the committed PMC summary of this
+    same bench command (profiles/pmc_summary.py over separate rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes, gfx950-corrected), matched on the kernel's template signature; (None, None)
+    when the summary lacks it or the match is ambiguous."""
+    pat = kernel_pattern(tag)
+    path = traffic_file(arch)
     try:
-        with open(TRAFFIC_FILE) as fh:
+        with open(path) as fh:
             rows = json.load(fh)["kernels"]
     except (OSError, ValueError, KeyError):
-        return None
-    if tag[0] == "gemm_nt":
-        M, N = tag[1], tag[3]
-        grid = -(-M // 128) * 256 * -(-N // 128)
-        # the weight-stationary forms (split image / in-kernel split): one of them runs per build
-        cand = [r for r in rows if "gemm_nt_planes" in r["kernel"] or "gemm_nt_ws" in r["kernel"]]
-        if len(cand) != 1:
-            cand = [r for r in rows if "gemm_nt" in r["kernel"] and r["grid_threads"] == grid]
-    elif tag[0] == "gemm_tn":
-        cand = [r for r in rows if "gemm_tn" in r["kernel"]]
-    else:
-        return None
-    if len(cand) != 1 or cand[0]["traffic_bytes"] is None:
-        return None
-    return int(cand[0]["traffic_bytes"])
+        return None, None
+    cand = [r for r in rows if pat is not None and pat.search(r["kernel"]) and r.get("traffic_bytes")]
+    if len(cand) != 1:
+        return None, None
+    return int(cand[0]["traffic_bytes"]), f"{os.path.relpath(path, ROOT)}: {cand[0]['kernel']}"
 
 
 BF16_MFMA_PEAK_TFS = 2500.0  # gfx950 dense bf16 MFMA peak (MI355X_MICROARCH.md)
@@ -255,7 +304,7 @@ def gemm_floor(tag):
     return byts, byts / (HBM_PEAK_GBS * 1e9), 2.0 * M * K * N / (peak * 1e12), peak
 
 
-def roofline(recs):
+def roofline(recs, arch="sage"):
     """Dominant libgnnmp kernel (by total HIP-event time) against its roofline.
 
     Aggregations are HBM-bound: achieved = algorithmic bytes per launch / average duration.
@@ -295,9 +344,9 @@ def roofline(recs):
             ach = per / (avg_ms * 1e-3) / 1e12
             out = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
                    "frac": round(ach / peak, 4), "traffic": None}
-    out["traffic"] = measured_traffic(tag)
+    out["traffic"], src = measured_traffic(tag, arch)
     if out["traffic"] is not None:
-        out["traffic_source"] = os.path.relpath(TRAFFIC_FILE, ROOT)
+        out["traffic_source"] = src
     timed = {}
     for t, v in recs.items():
         us = v["ms"] / v["launches"] * 1e3
@@ -309,6 +358,9 @@ def roofline(recs):
             byts, t_hbm, t_mfma, peak = gemm_floor(t)
             e.update({"hbm_frac": round(t_hbm / (us * 1e-6), 4), "mfma_frac": round(t_mfma / (us * 1e-6), 4),
                       "floor_us": round(max(t_hbm, t_mfma) * 1e6, 1)})
+        tb = measured_traffic(t, arch)[0]
+        if tb is not None:
+            e["traffic"] = tb
         timed[label(t)] = e
     out.update({"kernel": label(tag), "avg_us": round(avg_ms * 1e3, 2), "per_launch": int(per),
                 "timed_kernels": timed})
@@ -317,15 +369,21 @@ def roofline(recs):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))  # before any GPU call: the parent only launches and relays
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if not (world == 1 and args.gpus == 1):
-            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch with torch.distributed.run")
-    ndev = torch.cuda.device_count()
-    torch.cuda.set_device(local % max(ndev, 1))
-    dev = torch.device("cuda", local % max(ndev, 1))
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    check = args.launch_check
+    if check:
+        dev = torch.device("cpu")
+        args.dist_backend = "gloo"
+    else:
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local % max(ndev, 1))
+        dev = torch.device("cuda", local % max(ndev, 1))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -333,6 +391,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    if rank == args.fail_rank:
+        raise RuntimeError(f"--fail-rank {rank}")
 
     from elliptic_gnn_project_amd import distributed as gdist
     from elliptic_gnn_project_amd.aggregation import KernelTimer
@@ -344,6 +404,9 @@ def main():
     full, key = make_global_graph(world, args.scale, args.degree, cfg, preset.get("gen"))
     E_global = full.edge_index.size(1)
     data_cpu = gdist.shard_graph(full, world, rank, key=key) if world > 1 else full
+    if check:
+        return report(args, preset, full, E_global, data_cpu, dist, world, rank, dev, lambda: None, False,
+                      None, None, launch_check=True)
     data = data_cpu.to(dev)
     bf16 = preset.get("dtype") == "bf16"
     if bf16:  # bf16 storage of the node features (and, through the fused path, every activation)
@@ -412,15 +475,49 @@ def main():
     else:
         step = eager_step
 
+    def extras(value):
+        """roofline (instrumented eager steps) and the CPU baseline, after the timed region."""
+        roof = None
+        if not args.no_roofline:
+            KernelTimer.start()
+            for _ in range(5):
+                # hold the stream in a spin kernel while Python enqueues the whole step, so each event
+                # pair brackets back-to-back GPU work only (an idle stream would count the host's
+                # launch latency between an event and its kernel as kernel time)
+                torch.cuda._sleep(50_000_000)
+                eager_step()
+            recs = KernelTimer.stop()
+            roof = roofline(recs, args.arch)
+            if roof is not None:  # an event pair also spans its kernel's launch boundary (~1.5-3 us)
+                roof["timing_note"] = ("HIP-event brackets behind a busy stream; each includes its kernel's launch "
+                                       "boundary (~1.5-3 us), which rocprofv3's kernel durations exclude")
+
+        cpu = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(data_cpu, state0, cw.cpu(), denom, cfg, args.cpu_seconds, args.cpu_1t_seconds)
+            cpu["speedup_gpu_over_cpu"] = round(value / cpu["value"], 1)
+        return roof, cpu
+
+    launch = ("eager" if not use_graph else "hip-graph replay of the whole step" if bucket is None
+              else "hip-graph replay of the whole step, RCCL collectives captured" if rccl
+              else "hip-graph replay of fwd+bwd and of the optimizer, eager all-reduce between")
+    return report(args, preset, full, E_global, data, dist, world, rank, dev, step, bf16, extras, launch)
+
+
+def report(args, preset, full, E_global, data, dist, world, rank, dev, step, bf16, extras, launch,
+           launch_check=False):
+    """Warm-up, the timed region (barrier + synchronize on both sides, max over ranks), and rank
+    0's JSON line."""
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     for _ in range(args.warmup):
         step()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -433,30 +530,10 @@ def main():
         dist.all_reduce(nl, op=dist.ReduceOp.MAX)
         n_local = nl.cpu()
     value = E_global * args.steps / el
-
-    roof = None
-    if not args.no_roofline:
-        KernelTimer.start()
-        for _ in range(5):
-            # hold the stream in a spin kernel while Python enqueues the whole step, so each event
-            # pair brackets back-to-back GPU work only (an idle stream would count the host's
-            # launch latency between an event and its kernel as kernel time)
-            torch.cuda._sleep(50_000_000)
-            eager_step()
-        recs = KernelTimer.stop()
-        roof = roofline(recs)
-        if roof is not None:  # an event pair also spans its kernel's launch boundary (~1.5-3 us)
-            roof["timing_note"] = ("HIP-event brackets behind a busy stream; each includes its kernel's launch "
-                                   "boundary (~1.5-3 us), which rocprofv3's kernel durations exclude")
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(data_cpu, state0, cw.cpu(), denom, cfg, args.cpu_seconds, args.cpu_1t_seconds)
-        cpu["speedup_gpu_over_cpu"] = round(value / cpu["value"], 1)
-
+    roof, cpu = extras(value) if extras is not None else (None, None)
     if rank == 0:
         scaling = "weak" if (world == 1 or args.scale == "weak") else "strong"
-        print(json.dumps({
+        line = {
             "metric": preset.get("metric") or (METRIC if args.arch == "sage" else METRIC.replace("SAGE", args.arch.upper())),
             "value": value,
             "unit": "edges/s",
@@ -475,13 +552,14 @@ def main():
                 "max_nodes_per_gpu": int(n_local[0]), "max_edges_per_gpu": int(n_local[1]),
                 "parallelism": f"dp{world} timestep-partitioned ({args.scale})" if world > 1 else "single",
                 "collective": f"{args.dist_backend} all-reduce of one flat fp32 gradient bucket per step" if world > 1 else None,
-                "launch": ("eager" if not use_graph else "hip-graph replay of the whole step" if bucket is None
-                           else "hip-graph replay of the whole step, RCCL collectives captured" if rccl
-                           else "hip-graph replay of fwd+bwd and of the optimizer, eager all-reduce between"),
+                "launch": launch,
             },
             "roofline": roof,
             "cpu_baseline": cpu,
-        }), flush=True)
+        }
+        if launch_check:
+            line["launch_check"] = "CPU rehearsal of the launch: empty step, no device work (not a measurement)"
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -894,8 +894,15 @@ __global__ __launch_bounds__(256) void agg_combine_kernel(AggArgs a, int64_t nlo
 
 bool aligned(const void* p, int bytes) { return p == nullptr || (reinterpret_cast<uintptr_t>(p) % bytes) == 0; }
 
-// Kernel-lab knob (gnnx_set_agg_variant, not part of the public ABI): 0 = production.
+// Kernel-lab knob: the constant 0 in libgnnmp.so (no global mutable state, no lab kernels
+// instantiated).  `make lab` compiles this file again with -DGNNMP_AGG_LAB into
+// _lab/libgnnmp_agglab.so, whose gnnx_set_agg_variant selects the lab launch shapes
+// (profiles/lab_agg.py, lab_order.py, tests/test_gpu_order.py).
+#ifdef GNNMP_AGG_LAB
 int g_agg_lab_variant = 0;
+#else
+constexpr int g_agg_lab_variant = 0;
+#endif
 
 template <int MODE, int VEC, int NCH>
 void launch_split_passes(const AggArgs& a, const gnn_split* sp, hipStream_t st) {
@@ -959,10 +966,13 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     const unsigned nb = (unsigned)ceil_div(a.nrows, 256);
     // rows longer than 32 slots of a pass: the tail by the whole wave (r17 lab, SAGE preset F = 2:
     // fwd 14.4 -> 13.2 us, CSC bwd 15.2 -> 14.4 cold); lab 15: each lane walks its whole row
+#ifdef GNNMP_AGG_LAB
     if (g_agg_lab_variant == 15) {
       if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2, 256, false><<<nb, 256, 0, st>>>(a);
       else agg_narrow_lds_kernel<MODE, 4, 256, false><<<nb, 256, 0, st>>>(a);
-    } else if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2, 256, true><<<nb, 256, 0, st>>>(a);
+    } else
+#endif
+    if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2, 256, true><<<nb, 256, 0, st>>>(a);
     else agg_narrow_lds_kernel<MODE, 4, 256, true><<<nb, 256, 0, st>>>(a);
   } else if (a.F <= 8) {
     int64_t blocks = ceil_div(a.nrows * kGroup, 256);
@@ -998,10 +1008,15 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     const bool fold = pieces && pieces->num_pieces > pieces->num_long && !pf && lps == 16 && lv != 16;
     const unsigned pblocks = fold ? (unsigned)ceil_div(pieces->num_pieces * 64, 256) : 0u;
     if (fold && pieces_done) *pieces_done = true;
+#ifdef GNNMP_AGG_LAB
+#define GNN_FLAT_PF(V, L, NC) if (pf) agg_flat_kernel<MODE, V, L, NC, true><<<blocks, 256, 0, st>>>(a, rpg); else
+#else
+#define GNN_FLAT_PF(V, L, NC)
+#endif
 #define GNN_FLAT(V, L, NC)                                                                                 \
   do {                                                                                                     \
-    if (pf) agg_flat_kernel<MODE, V, L, NC, true><<<blocks, 256, 0, st>>>(a, rpg);                            \
-    else if (fold)                                                                                         \
+    GNN_FLAT_PF(V, L, NC)                                                                                  \
+    if (fold)                                                                                              \
       agg_flat_pieces_kernel<MODE, V, L, NC><<<blocks + pblocks, 256, 0, st>>>(a, rpg, pieces->num_pieces,   \
                                                                            pieces->piece_seg, pblocks);    \
     else agg_flat_kernel<MODE, V, L, NC><<<blocks, 256, 0, st>>>(a, rpg);                                    \
@@ -1031,6 +1046,7 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
     else GNN_FLAT_V(1);
 #undef GNN_FLAT_V
 #undef GNN_FLAT
+#undef GNN_FLAT_PF
   }
   return hip_check(hipGetLastError(), "gnn_aggregate_f32");
 }
@@ -1105,8 +1121,10 @@ constexpr int64_t kColsumBlocks = 1024;
 
 using namespace gnnmp;
 
-// Tuning entry (not part of the public ABI): selects lab launch shapes of the wide gather.
+#ifdef GNNMP_AGG_LAB
+// Lab build only (not in libgnnmp.so): selects lab launch shapes of the gathers.
 extern "C" void gnnx_set_agg_variant(int v) { g_agg_lab_variant = v; }
+#endif
 
 extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params* p, const float* x,
                                         int64_t ldx, int64_t F, float* y, int64_t ldy,

@@ -22,6 +22,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-for
     -- python3 bench.py --arch $ARCH --steps 3 --warmup 2 --no-cpu-baseline --no-roofline > "$OUT/write.log" 2>&1
 python3 profiles/pmc_summary.py --fetch "$OUT/fetch" --write "$OUT/write" --out "$OUT/traffic.json" \
     > "$OUT/traffic.txt"
+cp "$OUT/traffic.json" "$OUT/traffic_${ARCH}.json"  # commit as profiles/traffic_<arch>.json (bench.py reads it)
 find "$OUT" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
 tail -1 "$OUT/bench.log"
 cat "$OUT/traffic.txt"

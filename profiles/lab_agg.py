@@ -40,10 +40,8 @@ def main():
     if any(12 <= v <= 14 for v in variants):  # wave-gather split variants need the partial buffer
         import elliptic_gnn_project_amd.aggregation as agg_mod
         agg_mod.SPLIT_MAX_F = 512
-    lib = _lib.load()
-    setv = lib.gnnx_set_agg_variant
-    setv.argtypes = [ctypes.c_int]
-    setv.restype = None
+    from agglab import route_to_agglab  # the lab build of aggregate.hip (make lab)
+    setv = route_to_agglab()
     dev = torch.device("cuda:0")
     cases = []
     want = set(args.cases.split(","))

@@ -40,10 +40,8 @@ def main():
     ap.add_argument("--variants", default="0,5,6")
     args = ap.parse_args()
     variants = [int(v) for v in args.variants.split(",")]
-    lib = _lib.load()
-    setv = lib.gnnx_set_agg_variant
-    setv.argtypes = [ctypes.c_int]
-    setv.restype = None
+    from agglab import route_to_agglab  # the lab build of aggregate.hip (make lab)
+    setv = route_to_agglab()
     dev = torch.device("cuda:0")
     sage = prepare_inputs(synthetic_elliptic(seed=42), dict(use_time_scalar=True, symmetrize_edges=True))
     ps = plans(sage.edge_index, sage.x.size(0), _lib.LOOPS_KEEP, dev)

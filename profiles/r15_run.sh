@@ -6,7 +6,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_bf16.py tests/test_gpu_planes.py tests/test_gpu_fused.py -q -x --timeout 240 --timeout-method thread > "$OUT/tests.txt" 2>&1 || { tail -30 "$OUT/tests.txt"; exit 1; }
 tail -1 "$OUT/tests.txt"
-timeout -k 10 200 elliptic_gnn_project_amd/_build/lab_gemm 7 > "$OUT/lab.txt" 2>&1
+timeout -k 10 200 elliptic_gnn_project_amd/_lab/lab_gemm 7 > "$OUT/lab.txt" 2>&1
 grep -E "TN production|NT production" "$OUT/lab.txt"
 bash profiles/arch_kt.sh "${1:-r15}" sage sage_scaled > /dev/null
 for a in sage sage_scaled; do

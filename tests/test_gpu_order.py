@@ -101,15 +101,21 @@ def test_ordered_pass_bitwise_equals_plan_order(device, sym, loops_name, mode, t
 
 
 @pytest.mark.parametrize("sym,loops_name,mode,transpose,F,epi", [c for c in CASES if c[4] == 64])
-def test_pieces_in_main_launch_bitwise(device, sym, loops_name, mode, transpose, F, epi):
+def test_pieces_in_main_launch_bitwise(device, monkeypatch, sym, loops_name, mode, transpose, F, epi):
     """16-lane groups (F = 64): the split pieces walked inside the main pass's launch
-    (agg_flat_pieces_kernel) give the results of the separate piece launch bit for bit (lab knob
-    gnnx_set_agg_variant(16) keeps the pieces in their own launch)."""
+    (agg_flat_pieces_kernel) give the results of the separate piece launch bit for bit.  The
+    separate-launch shape is selected on the LAB build of aggregate.hip (`make lab`:
+    _lab/libgnnmp_agglab.so, gnnx_set_agg_variant(16)); libgnnmp.so has no runtime knob, and its
+    own result (the product path) must equal both."""
     import ctypes
+    import os
 
     from elliptic_gnn_project_amd import _lib
     from elliptic_gnn_project_amd.aggregation import aggregate
 
+    lab_so = os.path.join(os.path.dirname(_lib.LIB_PATH), "_lab", "libgnnmp_agglab.so")
+    if not os.path.exists(lab_so):
+        pytest.skip("lab build missing (make -C elliptic_gnn_project_amd/csrc lab)")
     loops = _lib.LOOPS_KEEP if loops_name == "keep" else _lib.LOOPS_REPLACE
     g = _graph(sym)
     N = g.x.size(0)
@@ -123,14 +129,19 @@ def test_pieces_in_main_launch_bitwise(device, sym, loops_name, mode, transpose,
         kw["addend"] = torch.randn(N, F, generator=gen).to(device)
     kw["bias"] = torch.randn(F, generator=gen).to(device)
     nodew = p.dinv if mode == "GCN" else p.deg
-    setv = _lib.load().gnnx_set_agg_variant
-    setv.argtypes = [ctypes.c_int]
-    setv.restype = None
+    agg_mode = getattr(_lib, f"AGG_{mode}")
+    prod = aggregate(p, x, agg_mode, transpose=transpose, nodew=nodew, **kw)
+    lab = ctypes.CDLL(lab_so)
+    res, args = _lib.SIGNATURES["gnn_aggregate_f32"]
+    lab.gnn_aggregate_f32.restype, lab.gnn_aggregate_f32.argtypes = res, args
+    lab.gnnx_set_agg_variant.argtypes, lab.gnnx_set_agg_variant.restype = [ctypes.c_int], None
+    prod_call = _lib.call
+    monkeypatch.setattr(_lib, "call", lambda name, *a: _lib.check(lab.gnn_aggregate_f32(*a), name)
+                        if name == "gnn_aggregate_f32" else prod_call(name, *a))
     outs = []
-    try:
-        for v in (0, 16):
-            setv(v)
-            outs.append(aggregate(p, x, getattr(_lib, f"AGG_{mode}"), transpose=transpose, nodew=nodew, **kw))
-    finally:
-        setv(0)
+    for v in (0, 16):
+        lab.gnnx_set_agg_variant(v)
+        outs.append(aggregate(p, x, agg_mode, transpose=transpose, nodew=nodew, **kw))
+    lab.gnnx_set_agg_variant(0)
+    assert torch.equal(prod, outs[0])
     assert torch.equal(outs[0], outs[1])

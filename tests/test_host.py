@@ -45,6 +45,16 @@ def test_library_exports_every_header_symbol(lib):
         assert getattr(lib, fn) is not None
 
 
+def test_library_has_no_lab_exports_or_mutable_globals(lib):
+    """no global mutable state in the product library.  The lab launch-shape knob
+    (gnnx_*) exists only in the separate lab build (make lab), and the library exports no
+    writable data symbol of its own beyond the thread-local error string's machinery."""
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True, check=True).stdout
+    assert not re.findall(r" [TtDdBb] (gnnx_[a-z0-9_]+)", out)
+    syms = subprocess.run(["nm", "-C", str(LIB)], capture_output=True, text=True, check=True).stdout
+    assert "g_agg_lab_variant" not in syms
+
+
 def test_abi_and_status_strings(lib):
     from elliptic_gnn_project_amd import _lib
 
