@@ -95,25 +95,30 @@ struct AdamTable {
   int64_t off[GNN_ADAM_MAX_TENSORS + 1];  // element offsets of the flattened parameter list
 };
 
-// Σ g² over this block's slice of the flattened gradients; block 0 also keeps the step count
-// before this call in partial[kAdamBlocks] (clip_adam_kernel advances step[0] once it knows the
-// step is taken: no block reads step[0] while another may write it).
+// Σ g² over this block's slice of the flattened gradients, and the count of its non-finite
+// elements (partial[kAdamBlocks + 1 + block]); block 0 also keeps the step count before this
+// call in partial[kAdamBlocks] (clip_adam_kernel advances step[0] once it knows the step is
+// taken: no block reads step[0] while another may write it).
 __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, float* __restrict__ partial,
                                                                 const float* __restrict__ step) {
   __shared__ float sh[kAdamThreads / 64];
   const int64_t total = tb.off[tb.n];
   const int64_t per = (total + gridDim.x - 1) / gridDim.x;
   const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(total, e0 + per);
-  float s = 0.f;
+  float s = 0.f, nf = 0.f;
   int j = 0;
   for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamThreads) {
     while (e >= tb.off[j + 1]) ++j;
     const float g = tb.g[j][e - tb.off[j]];
     s = fmaf(g, g, s);
+    nf += isfinite(g) ? 0.f : 1.f;
   }
   const float t = block_sum(s, sh);
+  __syncthreads();  // sh reused
+  const float tn = block_sum(nf, sh);
   if (threadIdx.x == 0) {
     partial[blockIdx.x] = t;
+    partial[kAdamBlocks + 1 + blockIdx.x] = tn;
     if (blockIdx.x == 0) partial[kAdamBlocks] = step[0];
   }
 }
@@ -121,8 +126,9 @@ __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, flo
 // Mirrors torch.optim.Adam's default (foreach, non-capturable) update: bias corrections and
 // 1 - beta in double, as the Python scalars are; m.lerp_(g, 1 - b1); v = v·b2 + (1 - b2)·g·g;
 // p += -lr/bc1 · m / (sqrt(v)/sqrt(bc2) + eps).
-// skip_nonfinite (torch.amp.GradScaler.step's found_inf): a non-finite Σg² leaves parameters,
-// moments, gradients and the step count untouched.
+// skip_nonfinite (torch.amp.GradScaler.step's found_inf: some gradient ELEMENT is inf / NaN)
+// leaves parameters, moments, gradients and the step count untouched.  A finite gradient whose
+// Σg² overflows is not skipped: as in clip_grad_norm_, the norm is inf and the clip coefficient 0.
 __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, const float* __restrict__ partial,
                                                                   int nblk, float* __restrict__ step,
                                                                   double max_norm, double lr, double beta1,
@@ -136,7 +142,9 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
     const float norm = sqrtf(tot);
     float coef = 1.0f;
     if (max_norm > 0.0) coef = fminf((float)max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
-    const bool skip = skip_nonfinite && !isfinite(tot);
+    float nf = threadIdx.x < nblk ? partial[kAdamBlocks + 1 + threadIdx.x] : 0.f;
+    for (int o = 32; o > 0; o >>= 1) nf += __shfl_xor(nf, o);
+    const bool skip = skip_nonfinite && nf > 0.f;
     if (threadIdx.x == 0) {
       coef_sh = coef;
       skip_sh = skip;
@@ -211,7 +219,7 @@ extern "C" gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logit
 
 extern "C" gnn_status gnn_clip_adam_workspace_size(size_t* bytes) {
   if (!bytes) return fail(GNN_ERR_INVALID_ARG, __func__, "null");
-  *bytes = (kAdamBlocks + 1) * sizeof(float);
+  *bytes = (2 * kAdamBlocks + 1) * sizeof(float);
   return GNN_OK;
 }
 
@@ -219,7 +227,7 @@ extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, 
                                         size_t workspace_bytes, gnn_stream_t stream) {
   if (!grp || !step || grp->num_tensors < 0 || grp->num_tensors > GNN_ADAM_MAX_TENSORS)
     return fail(GNN_ERR_INVALID_ARG, __func__, "bad group");
-  if (!workspace || workspace_bytes < (kAdamBlocks + 1) * sizeof(float))
+  if (!workspace || workspace_bytes < (2 * kAdamBlocks + 1) * sizeof(float))
     return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
   AdamTable tb{};
   tb.n = grp->num_tensors;

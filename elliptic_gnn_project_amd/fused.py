@@ -29,7 +29,7 @@ import torch
 from . import _lib
 from .aggregation import KernelTimer, aggregate, agg_bytes
 from .graph import GraphPlan, get_plan
-from .planes import BfImage, bf_x_image, mean_planes_ok, x_image, x_only_image
+from .planes import BfImage, SplitImage, bf_x_image, is_registered, mean_planes_ok, x_image, x_only_image
 
 # The layer-1 operand [agg | x] as a split image (planes.py): on by default, GNNMP_PLANES=0 runs
 # the in-kernel split forms instead (same results within the split's error; A/B timing).
@@ -213,11 +213,12 @@ def gemm_tn_input(nr: int, x: torch.Tensor, g: torch.Tensor):
 
 
 def _layer0_image(x: torch.Tensor, n_out: int, nt_kw):
-    """The split image of [agg | x] when the planes path takes this layer (else None)."""
-    if not (_PLANES and mean_planes_ok(x)) or x.size(0) < 32:
+    """The split image of [agg | x] when the planes path takes this layer (else None): x must be a
+    registered constant input (planes.register_input) — its planes are built once and reused; a
+    per-batch or per-step input keeps the in-kernel split (gemm_nt over f32 [agg | x])."""
+    if not (_PLANES and is_registered(x) and mean_planes_ok(x)) or x.size(0) < 32:
         return None
-    ld = ((x.size(1) + 7) // 8 * 16 + 15) // 16 * 16  # [agg | x], each padded to 8 columns
-    if 3 * x.size(0) * ld * 2 >= 2 ** 31:  # the kernels address the planes with 31-bit offsets
+    if not SplitImage.addressable(x.size(0), x.size(1), x.size(1)):
         return None
     im = x_image(x)
     if not gemm_nt(None, None, n_out, planes=im, check_planes=True, **nt_kw):
@@ -514,30 +515,44 @@ def dropout_seeds(L: int, p: float, x: torch.Tensor):
     return [0] * L, None
 
 
-def _output_weights(conv):
-    """[W_l ; W_r] of the output conv as ONE tensor without a per-step copy.
-
-    The NT epilogue's projection and the TN read the stacked [2C, F] weights.  Instead of a
-    `torch.cat` every step (a launch on the critical path), the two Linear weights are re-pointed
-    (``.data``, once — parameters, optimizer state and state_dict keys are untouched) at the two
-    halves of one buffer, which then IS the stack.  A later ``.to()`` / ``load_state_dict`` that
-    separates them is noticed here and re-tied; under HIP-graph capture an untied pair falls back
-    to the copy (a re-tie must not be recorded)."""
+def tie_output_weights(conv) -> None:
+    """Lay the output conv's lin_l.weight and lin_r.weight out as the two halves of ONE [2C, F]
+    buffer, which then IS the stacked [W_l ; W_r] the NT epilogue's projection and the TN read
+    (no per-step torch.cat).  Called by SAGENet at construction and after every ``_apply``
+    (.to() / .cuda() / .float() ...), never from a forward: the Parameter objects, their values,
+    optimizer state and state_dict keys are untouched (load_state_dict copies in place and keeps
+    the tie; deepcopy keeps it too)."""
     wl, wr = conv.lin_l.weight, conv.lin_r.weight
-    buf = getattr(conv, "_gnnmp_out_w", None)
+    if (wl.shape != wr.shape or wl.device != wr.device or wl.dtype != wr.dtype or not wl.is_floating_point()
+            or (wl.is_cuda and torch.cuda.is_current_stream_capturing())):
+        return
+    if _tied_buffer(conv) is not None:
+        return
     C = wl.size(0)
-    if (buf is not None and buf.device == wl.device and buf.dtype == wl.dtype and buf.shape == (2 * C, wl.size(1))
-            and wl.data_ptr() == buf.data_ptr() and wr.data_ptr() == buf[C:].data_ptr()
-            and wl.shape == wr.shape and wl.is_contiguous() and wr.is_contiguous()):
-        return buf
-    if wl.shape != wr.shape or torch.cuda.is_current_stream_capturing():
-        return torch.cat([wl, wr], dim=0).contiguous()
     with torch.no_grad():
         buf = torch.cat([wl.detach(), wr.detach()], dim=0).contiguous()
         wl.data = buf[:C]
         wr.data = buf[C:]
-    conv._gnnmp_out_w = buf
-    return buf
+
+
+def _tied_buffer(conv):
+    """The [2C, F] tensor both output weights view (the tie of tie_output_weights), or None."""
+    wl, wr = conv.lin_l.weight, conv.lin_r.weight
+    C = wl.size(0)
+    if (wl.shape != wr.shape or not wl.is_contiguous() or not wr.is_contiguous() or wl.device != wr.device
+            or wl.dtype != wr.dtype or wl.untyped_storage().data_ptr() != wr.untyped_storage().data_ptr()
+            or wr.data_ptr() != wl.data_ptr() + wl.numel() * wl.element_size()):
+        return None
+    return torch.as_strided(wl.detach(), (2 * C, wl.size(1)), (wl.size(1), 1))
+
+
+def _output_weights(conv):
+    """[W_l ; W_r] of the output conv as ONE tensor: the tied buffer (tie_output_weights) when the
+    two weights are its halves, else a copy (torch.cat: e.g. after a Parameter was replaced)."""
+    buf = _tied_buffer(conv)
+    if buf is not None:
+        return buf
+    return torch.cat([conv.lin_l.weight, conv.lin_r.weight], dim=0).contiguous()
 
 
 def sage_forward(model, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:

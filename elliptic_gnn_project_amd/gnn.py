@@ -81,6 +81,23 @@ class SAGENet(_StackedConvNet):
 
     def __init__(self, in_dim, hidden_dim=128, layers=3, dropout=0.2, num_classes=2):
         super().__init__([SAGEConv(a, b) for a, b in _widths(in_dim, hidden_dim, layers, num_classes)], dropout)
+        _fused.tie_output_weights(self.convs[-1])
+
+    def _apply(self, fn, recurse=True):
+        # .to() / .cuda() / .float() give each weight new storage: re-tie the output conv's pair
+        # (the fused path reads [W_l ; W_r] as one buffer, fused.tie_output_weights)
+        out = super()._apply(fn, recurse)
+        _fused.tie_output_weights(self.convs[-1])
+        return out
+
+    def __deepcopy__(self, memo):
+        import copy
+
+        new = self.__class__.__new__(self.__class__)
+        memo[id(self)] = new
+        new.__setstate__(copy.deepcopy(self.__dict__, memo))
+        _fused.tie_output_weights(new.convs[-1])
+        return new
 
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor, t_idx: Optional[torch.Tensor] = None):
         if self.fused and x.is_cuda and _fused.fusable(self):

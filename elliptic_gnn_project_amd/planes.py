@@ -35,10 +35,20 @@ def _pad8(k: int) -> int:
 class SplitImage:
     """[3, N, ld] bf16 planes of [A1 | A2] with A1 at column 0 and A2 at column ``col2``."""
 
+    @staticmethod
+    def layout(k1: int, k2: int):
+        """(col2, ld) of an image of [A1 (k1 columns) | A2 (k2 columns)]."""
+        col2 = _pad8(k1)
+        return col2, (col2 + _pad8(k2) + 15) // 16 * 16
+
+    @staticmethod
+    def addressable(n: int, k1: int, k2: int) -> bool:
+        """The kernels address the three planes with 31-bit byte offsets."""
+        return 3 * int(n) * SplitImage.layout(k1, k2)[1] * 2 < 2 ** 31
+
     def __init__(self, n: int, k1: int, k2: int, device: torch.device):
         self.n, self.k1, self.k2 = int(n), int(k1), int(k2)
-        self.col2 = _pad8(k1)
-        self.ld = (self.col2 + _pad8(k2) + 15) // 16 * 16
+        self.col2, self.ld = self.layout(k1, k2)
         self.ps = self.n * self.ld
         self.img = torch.empty((3, self.n, self.ld), dtype=torch.bfloat16, device=device)
         self.gen = 0
@@ -98,12 +108,18 @@ _ATTR_X = _ATTR + "_x"
 _CONST = "_gnnmp_const_input"
 
 
+def is_registered(x: torch.Tensor) -> bool:
+    """Whether x was declared a constant input (register_input)."""
+    return bool(getattr(x, _CONST, False))
+
+
 def register_input(x: torch.Tensor) -> torch.Tensor:
     """Declare x a constant input of the run (the training loop's node features, prepared once,
     src/train_gnn.py:315-350): layers whose A operand is x then read it from a split image built
-    once per (unmodified) x — a per-graph input layout, like the CSR plan.  Unregistered inputs
-    (a mini-batch's gathered rows, a per-step time-injected input) keep the f32-operand kernels,
-    so no call pays a split pass it cannot reuse.  Returns x."""
+    once per (unmodified) x — a per-graph input layout, like the CSR plan: the SAGE layer-1
+    [agg | x] image (x half) and the GCN / GAT layer-1 x-only image.  Unregistered inputs (a
+    mini-batch's gathered rows, a per-step time-injected input) keep the f32-operand kernels, so
+    no call allocates an image or pays a split pass it cannot reuse.  Returns x."""
     try:
         setattr(x, _CONST, True)
     except (AttributeError, RuntimeError):
@@ -123,9 +139,9 @@ def x_only_image(x: torch.Tensor):
     key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
     im = getattr(x, _ATTR_X, None)
     if im is None or im.n != x.size(0) or im.k1 != x.size(1):
-        im = SplitImage(x.size(0), x.size(1), 0, x.device)
-        if 3 * im.ps * 2 >= 2 ** 31:
+        if not SplitImage.addressable(x.size(0), x.size(1), 0):  # checked before allocating
             return None
+        im = SplitImage(x.size(0), x.size(1), 0, x.device)
         try:
             setattr(x, _ATTR_X, im)
         except (AttributeError, RuntimeError):  # e.g. inference tensors: not cached, still used

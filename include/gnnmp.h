@@ -370,9 +370,12 @@ gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t Kc, int32_t
 gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* workspace, size_t workspace_bytes,
                            gnn_stream_t stream);
 /* 1 when the call would read A from p->a_planes (the f32 A operands are then not needed), else 0.
- * Split-image shapes: NT image rows of 336 (the SAGE layer-1 [agg | x], 166 + 166 padded to 168
- * each), 64 < N <= 128, f32 C; TN image rows of 32..336 (multiple of 16), f32 h; both need the
- * three planes to span < 2 GiB. */
+ * Split-image NT shapes (f32 C, the w1/w2 B form, N % 4 == 0, M >= 32; a ReLU, dropout or
+ * projection epilogue needs relu + bias):
+ *   image rows of 336 (the SAGE layer-1 [agg | x], 166 + 166 padded to 168 each), 64 < N <= 128;
+ *   image rows of 176 (one input of <= 176 columns: the GCN / GAT layer-1 x), 1 <= N <= 128.
+ * TN image rows of 32..336 (multiple of 16), f32 h.  Both need the three planes to span < 2 GiB
+ * and C / z below 2 GiB. */
 int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p);
 int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p);
 
@@ -460,8 +463,10 @@ typedef struct {
   int32_t num_tensors;
   double lr, beta1, beta2, eps, weight_decay, max_norm;  /* double, as torch's Python scalars */
   gnn_adam_tensor tensors[GNN_ADAM_MAX_TENSORS];
-  int32_t skip_nonfinite;  /* != 0: torch.amp.GradScaler.step semantics — a non-finite gradient norm
-                              skips the update (params, moments, grads and step count untouched) */
+  int32_t skip_nonfinite;  /* != 0: torch.amp.GradScaler.step semantics — any inf / NaN gradient
+                              ELEMENT skips the update (params, moments, grads and step count
+                              untouched); finite gradients whose Σg² overflows are clipped by
+                              coefficient 0, as clip_grad_norm_ does with an inf norm */
 } gnn_adam_group;
 gnn_status gnn_clip_adam_workspace_size(size_t* bytes);
 gnn_status gnn_clip_adam_f32(const gnn_adam_group* group, float* step, float* norm_out, void* workspace,

@@ -90,3 +90,47 @@ def test_captured_step_redraws_dropout(device, arch):
     l2 = float(cs().item())
     assert int(ctr.item()) == c0 + 2
     assert l1 != l2
+
+
+def test_captured_sage_reads_the_tied_output_weights(device):
+    """The SAGE output conv's [W_l ; W_r] is one buffer tied at construction / .to() (fused.
+    tie_output_weights), never re-pointed inside a forward: capture and replay keep the tie, the
+    optimizer's in-place updates are what the captured projection reads, and the result equals a
+    model whose weights were never tied (the torch.cat fallback)."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.train_gnn import CapturedStep
+
+    m_g, step_g, _, _ = _setup(device, "sage")
+    conv = m_g.convs[-1]
+    buf = fused._tied_buffer(conv)
+    assert buf is not None
+    ptrs = (conv.lin_l.weight.data_ptr(), conv.lin_r.weight.data_ptr())
+    cs = CapturedStep(step_g, warmup=2)
+    for _ in range(3):
+        cs()
+    torch.cuda.synchronize()
+    assert (conv.lin_l.weight.data_ptr(), conv.lin_r.weight.data_ptr()) == ptrs
+    assert torch.equal(fused._tied_buffer(conv), torch.cat([conv.lin_l.weight, conv.lin_r.weight]))
+    # untied twin: same steps eagerly through the cat fallback -> same parameters bit for bit
+    m_u, step_u, _, _ = _setup(device, "sage")
+    cu = m_u.convs[-1]
+    cu.lin_r.weight = torch.nn.Parameter(cu.lin_r.weight.detach().clone())
+    assert fused._tied_buffer(cu) is None
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+    # the optimizer of _setup holds the replaced Parameter's predecessor: rebuild the step around m_u
+    opt = ClipAdam(m_u.parameters(), lr=0.01, weight_decay=1e-4, max_norm=1.0)
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn
+    data = prepare_inputs(synthetic_elliptic(num_nodes=4000, num_edges=5000, seed=9),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10)).to(device)
+    cw = pyg_ref.class_weight(data.y[data.train_mask].cpu())
+    loss_fn = _make_loss_fn({}, cw, m_u, 1, 34)
+    denom = float(data.train_mask.sum())
+    for _ in range(5):
+        m_u.train()
+        opt.zero_grad(set_to_none=False)
+        loss_fn.full(m_u(data.x, data.edge_index), data.y, data.train_mask, denom=denom).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    for (k, a), b in zip(m_g.state_dict().items(), m_u.state_dict().values()):
+        assert torch.equal(a, b), k

@@ -43,9 +43,13 @@ def _f64(params):
     return {k: v.double() if v.is_floating_point() else v for k, v in params.items()}
 
 
-def test_full_size_sage_train_step_gradients(device):
-    """configs[1] at full size, train mode: logits and all 6 parameter gradients."""
+@pytest.mark.parametrize("registered", [True, False])
+def test_full_size_sage_train_step_gradients(device, registered):
+    """configs[1] at full size, train mode: logits and all 6 parameter gradients.  registered: x
+    declared constant as bench.py / train_gnn.main do — layer 1 on the [agg | x] split image (the
+    benched path: K1 into the agg planes, the planes NT / TN); else the in-kernel split forms."""
     from elliptic_gnn_project_amd.gnn import SAGENet
+    from elliptic_gnn_project_amd.planes import register_input
 
     data = _graph(True)
     assert data.edge_index.size(1) == 2 * E_FULL
@@ -54,8 +58,12 @@ def test_full_size_sage_train_step_gradients(device):
     model = SAGENet(166, 128, layers=2, dropout=0.5).to(device)
     params = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     model.train()
+    xd = data.x.to(device)
+    if registered:
+        register_input(xd)
     torch.manual_seed(123)
-    logits = model(data.x.to(device), data.edge_index.to(device))
+    logits = model(xd, data.edge_index.to(device))
+    assert (getattr(xd, "_gnnmp_split_image", None) is not None) == registered
     torch.manual_seed(123)
     seeds = torch.randint(0, 2 ** 62, (2,), dtype=torch.int64).tolist()
     masks = [torch.from_numpy(keep_mask(seeds[0], N, 128, 0.5))]
@@ -171,11 +179,15 @@ def test_full_size_sage_resbn_largest_shard(device):
 
 
 # ----------------------------------------------------------------------------- configs[0] / [2] train mode
+@pytest.mark.parametrize("registered", [True, False])
 @pytest.mark.parametrize("arch,hidden,heads", [("gcn", 64, 4), ("gat", 64, 4)])
-def test_full_size_train_step_gradients(device, arch, hidden, heads):
+def test_full_size_train_step_gradients(device, arch, hidden, heads, registered):
     """GCN 2L/64 (configs[0] preset) and GAT 2L 4x16 (configs[2]) train steps at full size with
     dropout 0.5: the fused dropout stores, GCN's mask epilogue and GAT's rows/cols backward over
-    the real hub rows, every parameter gradient vs the float64 oracle under the same masks."""
+    the real hub rows, every parameter gradient vs the float64 oracle under the same masks.
+    registered: x declared constant as bench.py does — layer 1's y = x·Wᵀ and dW = Gᵀ·x on x's
+    split image (the planes NT and the split-K TN the bench times); else the f32-operand forms."""
+    from elliptic_gnn_project_amd.planes import register_input
     from elliptic_gnn_project_amd.train_gnn import build_model
 
     data = _graph(False)
@@ -184,8 +196,12 @@ def test_full_size_train_step_gradients(device, arch, hidden, heads):
     model = build_model(arch, 166, dict(hidden_dim=hidden, layers=L, dropout=p, heads=heads)).to(device)
     params = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     model.train()
+    xd = data.x.to(device)
+    if registered:
+        register_input(xd)
     torch.manual_seed(321)
-    logits = model(data.x.to(device), data.edge_index.to(device))
+    logits = model(xd, data.edge_index.to(device))
+    assert (getattr(xd, "_gnnmp_split_image_x", None) is not None) == registered
     torch.manual_seed(321)
     seeds = torch.randint(0, 2 ** 62, (L,), dtype=torch.int64).tolist()
     masks = [torch.from_numpy(keep_mask(seeds[0], N, hidden, p))]

@@ -75,8 +75,11 @@ def _plan_and_x(n, e, seed, device):
 
     data = prepare_inputs(synthetic_elliptic(num_nodes=n, num_edges=e, seed=seed),
                           dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+    from elliptic_gnn_project_amd.planes import register_input
+
     ei = data.edge_index.to(device)
-    return data, get_plan(ei, data.x.size(0)), data.x.to(device)
+    # a registered constant input (as train_gnn.main / bench.py register x): the SAGE layer-1 [agg | x] image
+    return data, get_plan(ei, data.x.size(0)), register_input(data.x.to(device))
 
 
 @pytest.mark.parametrize("n,e", [(5000, 6000), (203_769, 234_355)])
@@ -227,6 +230,7 @@ def test_two_forwards_then_backward(device):
     """A second grad-enabled forward over the same x rewrites the image's agg half; the first
     forward's backward notices (generation stamp), refreshes it and gets the same gradients."""
     from elliptic_gnn_project_amd.gnn import SAGENet
+    from elliptic_gnn_project_amd.planes import register_input
 
     data, plan, x = _plan_and_x(3000, 4000, 8, device)
     ei = data.edge_index.to(device)
@@ -236,13 +240,37 @@ def test_two_forwards_then_backward(device):
     loss.backward()
     ref = {k: p.grad.clone() for k, p in model.named_parameters()}
     model.zero_grad()
-    x2 = x * 2.0  # another x: its own image
+    x2 = register_input(x * 2.0)  # another x: its own image
     out_a, loss_a = _sage_step(model, x, ei, 1)
     out_b, loss_b = _sage_step(model, x, ei, 1)  # same x: rewrites the agg half
     _ = model(x2, ei)
     loss_a.backward()
     for k, p in model.named_parameters():
         assert torch.equal(p.grad, ref[k]), k
+    assert getattr(x, "_gnnmp_split_image", None) is not None  # the planes path ran
+
+
+def test_unregistered_input_builds_no_image(device):
+    """A per-batch / per-step input (not registered) takes the in-kernel split: no [3, N, ld]
+    image is allocated for it, and the result equals the registered input's within 1e-5."""
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data, plan, x = _plan_and_x(3000, 4000, 9, device)
+    ei = data.edge_index.to(device)
+    xu = x.clone()  # same values, not registered
+    torch.manual_seed(5)
+    model = SAGENet(x.size(1), 128, layers=2, dropout=0.0).to(device).train()
+    outs = []
+    for inp in (x, xu):
+        model.zero_grad()
+        out, loss = _sage_step(model, inp, ei, 2)
+        loss.backward()
+        outs.append((out.detach(), {k: p.grad.clone() for k, p in model.named_parameters()}))
+    assert getattr(x, "_gnnmp_split_image", None) is not None
+    assert getattr(xu, "_gnnmp_split_image", None) is None
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-5)
+    for k in outs[0][1]:
+        assert rel_l2(outs[0][1][k], outs[1][1][k]) < 1e-5, k
 
 
 def test_x_image_follows_in_place_edit(device):

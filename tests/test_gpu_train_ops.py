@@ -64,6 +64,45 @@ def test_clip_adam_matches_torch(device, gscale, wd):
         torch.testing.assert_close(ob.state[q]["exp_avg_sq"], oa.state[p]["exp_avg_sq"], rtol=1e-6, atol=1e-12)
 
 
+@pytest.mark.parametrize("bad", ["none", "inf", "nan", "huge"])
+def test_clip_adam_skip_nonfinite_matches_grad_scaler(device, bad):
+    """ClipAdam(skip_nonfinite) against the reference's AMP step (src/train_gnn.py:202-207):
+    scaler.unscale_ -> clip_grad_norm_ -> scaler.step(Adam) -> scaler.update.  An inf / NaN
+    ELEMENT skips the update (found_inf); a finite 1e20 element is not skipped — its Σg²
+    overflows, so clip_grad_norm_ scales every gradient by 0 and Adam still steps (weight decay)."""
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+
+    pa, pb = _params(device, 5), _params(device, 5)
+    oa = torch.optim.Adam(pa, lr=0.01, weight_decay=1e-4)
+    scaler = torch.amp.GradScaler("cuda", init_scale=1.0, growth_interval=1_000_000)
+    ob = ClipAdam(pb, lr=0.01, weight_decay=1e-4, max_norm=1.0, skip_nonfinite=True)
+    g = torch.Generator().manual_seed(6)
+    for it in range(3):
+        grads = [torch.randn(p.shape, generator=g).to(device) for p in pa]
+        if it == 1 and bad != "none":
+            grads[2][5, 7] = {"inf": float("inf"), "nan": float("nan"), "huge": 1e20}[bad]
+        for p, q, gr in zip(pa, pb, grads):
+            p.grad = gr.clone()
+            q.grad = gr.clone()
+        scaler.scale(torch.zeros((), device=device))  # initialises the scaler's state (scale 1.0)
+        scaler.unscale_(oa)
+        torch.nn.utils.clip_grad_norm_(pa, 1.0)
+        scaler.step(oa)
+        scaler.update(1.0)
+        ob.step()
+        torch.cuda.synchronize()
+        for p, q in zip(pa, pb):
+            torch.testing.assert_close(q, p, rtol=1e-6, atol=1e-7)
+        for p, q in zip(pa, pb):
+            sa, sb = oa.state.get(p, {}), ob.state[q]
+            if sa:
+                torch.testing.assert_close(sb["exp_avg"], sa["exp_avg"], rtol=1e-6, atol=1e-9)
+                torch.testing.assert_close(sb["exp_avg_sq"], sa["exp_avg_sq"], rtol=1e-6, atol=1e-12)
+                assert float(sb["step"]) == float(sa["step"])
+            if it == 1 and bad in ("inf", "nan"):
+                assert float(sb["step"]) == 1.0  # the skipped update left the count
+
+
 def test_clip_adam_graph_replay(device):
     """Captured in a HIP graph, every replay advances the device step like an eager step."""
     from elliptic_gnn_project_amd.train_ops import ClipAdam
