@@ -319,7 +319,7 @@ def roofline(recs, arch="sage"):
             return f"{tag[0]}[{names[tag[1]]},{'csc' if tag[2] else 'csr'},F={tag[3]}]"
         if tag[0].startswith("gat"):
             return f"{tag[0]}[H={tag[1]},C={tag[2]},out={tag[3]}]"
-        math = {-1: "valu-f32", 0: "f32", 1: "bf16", 6: "split-bf16"}[tag[6]]
+        math = {-1: "valu-f32", 0: "f32", 1: "bf16", 3: "half-pair-f16", 6: "split-bf16"}[tag[6]]
         return f"{tag[0]}[M={tag[1]},K={tag[2]},N={tag[3]},{math}]"
 
     if not recs:

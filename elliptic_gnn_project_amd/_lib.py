@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -24,6 +24,10 @@ DTYPE_BF16 = 1
 # gnn_gemm_math
 MATH_SPLIT_BF16 = 0
 MATH_F32 = 1
+
+# gnn_planes_format
+PLANES_SPLIT_BF16 = 0
+PLANES_HALF_PAIR = 1
 
 # gnn_status
 GNN_OK = 0
@@ -119,6 +123,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("a_dtype", c_i32), ("c_dtype", c_i32),
         ("mask", c_ptr), ("ldmask", c_i64), ("mask_scale", ctypes.c_float),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
+        ("planes_format", c_i32),
     ]
 
 
@@ -135,6 +140,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("math", c_i32),
         ("a_dtype", c_i32), ("h_dtype", c_i32),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
+        ("planes_format", c_i32),
     ]
 
 
@@ -210,6 +216,11 @@ SIGNATURES = {
     ),
     "gnn_split_planes_f32": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr]),
     "gnn_sage_mean_fwd_planes": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr],
+    ),
+    "gnn_split_h2_f32": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr]),
+    "gnn_sage_mean_fwd_h2": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr],
     ),

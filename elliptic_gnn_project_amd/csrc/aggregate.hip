@@ -426,8 +426,9 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 // Wave-wide groups (LPS = 64, F/VEC > 32 chunks, e.g. the 166-wide layer-1 features):
 // every row boundary and neighbour id is wave-uniform, so they live in SGPRs (scalar loads,
 // v_readlane) and the next U neighbour ids are prefetched while the current U rows load.
-// PLN: y is written as a split image (3 bf16 planes, VEC even), no split partials.
-template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, bool PLN = false>  // BF: x and y hold bf16 (no split partials)
+// PLN: y is written as a split image, no split partials: 3 = split-bf16 planes (hi / mid / lo
+// bf16), 2 = half-pair planes (hi / lo f16, gemm_common.hpp split_h2_pair); VEC even.
+template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, int PLN = 0>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
@@ -462,7 +463,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int c = lane + 64 * i;
-      if constexpr (PLN) {
+      if constexpr (PLN != 0) {
         static_assert(VEC % 2 == 0, "planes are written in column pairs");
         if (c < nchunk || c * VEC < a.ywidth) {
           uint32_t w[VEC / 2][3];
@@ -470,11 +471,12 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
           for (int q = 0; q < VEC / 2; ++q) {
             const float t0 = c < nchunk ? acc[i][2 * q] / d : 0.0f;
             const float t1 = c < nchunk ? acc[i][2 * q + 1] / d : 0.0f;
-            split3_pair(t0, t1, w[q][0], w[q][1], w[q][2]);
+            if constexpr (PLN == 3) split3_pair(t0, t1, w[q][0], w[q][1], w[q][2]);
+            else split_h2_pair(t0, t1, w[q][0], w[q][1]);
           }
           uint16_t* dst = a.yp + r * a.ldy + c * VEC;
 #pragma unroll
-          for (int p = 0; p < 3; ++p) {
+          for (int p = 0; p < PLN; ++p) {
             if constexpr (VEC == 4) *reinterpret_cast<uint2*>(dst + p * a.yps) = make_uint2(w[0][p], w[1][p]);
             else *reinterpret_cast<uint32_t*>(dst + p * a.yps) = w[0][p];
           }
@@ -1295,16 +1297,18 @@ extern "C" gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg
 }
 
 // K1 with a split-image store: y = mean_{j->i} x[j] (MEAN over the CSR rows, PyG's order and
-// rounding) written as 3 bf16 planes (hi = RNE(y), mid = RNE(y - hi), lo = RNE(y - hi - mid)) at
-// img + p·plane_stride, row pitch ld, columns [F, width) zero.  Wide rows only (the wave gather).
-extern "C" gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
-                                               int64_t F, void* img, int64_t ld, int64_t plane_stride, int64_t width,
-                                               gnn_stream_t stream) {
-  if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, __func__, "null graph or deg");
+// rounding) written as 3 bf16 planes (hi = RNE(y), mid = RNE(y - hi), lo = RNE(y - hi - mid)) or,
+// PLN = 2, as 2 f16 planes (hi = RNE_f16(y), lo = RNE_f16((y - hi)·2^11)) at img + p·plane_stride,
+// row pitch ld, columns [F, width) zero.  Wide rows only (the wave gather).
+template <int PLN>
+static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
+                                      void* img, int64_t ld, int64_t plane_stride, int64_t width, gnn_stream_t stream,
+                                      const char* fn) {
+  if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or deg");
   if (F < 2 || ldx < F || width < F || width > ld || plane_stride < g->num_nodes * ld)
-    return fail(GNN_ERR_INVALID_ARG, __func__, "bad F / width / leading dimensions");
-  if (g->num_nodes > 0 && (!x || !img)) return fail(GNN_ERR_INVALID_ARG, __func__, "null x / image");
-  if (!g->rowptr || (g->num_slots > 0 && !g->col)) return fail(GNN_ERR_INVALID_ARG, __func__, "plan arrays null");
+    return fail(GNN_ERR_INVALID_ARG, fn, "bad F / width / leading dimensions");
+  if (g->num_nodes > 0 && (!x || !img)) return fail(GNN_ERR_INVALID_ARG, fn, "null x / image");
+  if (!g->rowptr || (g->num_slots > 0 && !g->col)) return fail(GNN_ERR_INVALID_ARG, fn, "plan arrays null");
   AggArgs a{};
   a.ptr = g->rowptr;
   a.nbr = g->col;
@@ -1322,14 +1326,26 @@ extern "C" gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* 
                   al(x, 8) && al(img, 4);
   const int vec = v4 ? 4 : 2;
   if (!v2 || F / vec <= 32 || ceil_div(width, vec) > 128)
-    return fail(GNN_ERR_UNSUPPORTED, __func__, "needs even F, 32 < F / vec, width / vec <= 128 and aligned rows");
+    return fail(GNN_ERR_UNSUPPORTED, fn, "needs even F, 32 < F / vec, width / vec <= 128 and aligned rows");
   if (a.nrows == 0) return GNN_OK;
   const int rpw = 16;
   const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
   hipStream_t st = (hipStream_t)stream;
-  if (vec == 4) agg_wave_kernel<GNN_AGG_MEAN, 4, 2, false, 8, true><<<wblocks, 256, 0, st>>>(a, rpw);
-  else agg_wave_kernel<GNN_AGG_MEAN, 2, 2, false, 8, true><<<wblocks, 256, 0, st>>>(a, rpw);
-  return hip_check(hipGetLastError(), __func__);
+  if (vec == 4) agg_wave_kernel<GNN_AGG_MEAN, 4, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
+  else agg_wave_kernel<GNN_AGG_MEAN, 2, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
+  return hip_check(hipGetLastError(), fn);
+}
+
+extern "C" gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
+                                               int64_t F, void* img, int64_t ld, int64_t plane_stride, int64_t width,
+                                               gnn_stream_t stream) {
+  return sage_mean_fwd_image<3>(g, deg, x, ldx, F, img, ld, plane_stride, width, stream, __func__);
+}
+
+extern "C" gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
+                                           int64_t F, void* img, int64_t ld, int64_t plane_stride, int64_t width,
+                                           gnn_stream_t stream) {
+  return sage_mean_fwd_image<2>(g, deg, x, ldx, F, img, ld, plane_stride, width, stream, __func__);
 }
 
 extern "C" gnn_status gnn_sage_mean_bwd_f32(const gnn_graph* g, const float* deg, const float* dout,

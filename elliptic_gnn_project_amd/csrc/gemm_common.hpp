@@ -69,6 +69,7 @@ struct NTArgs {
   // ap + p·ap_ps, row r at r·ap_ld; A1 in columns [0, k1), A2 in [ap_col2, ap_col2 + k2), zeros
   // elsewhere.  The weight-stationary kernel then stages A by plain copies (no split VALU).
   const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;
+  int32_t ap_h2;  // the image is a half-pair image (2 f16 planes hi / lo, gemm_ws.hip K7a-h)
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
@@ -170,6 +171,7 @@ struct TNArgs {
   int32_t a_bf16;  // A1/A2 hold bf16
   int32_t h_bf16;  // h holds bf16
   const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;  // split image of [A1 | A2] (as NTArgs)
+  int32_t ap_h2;  // half-pair image (2 f16 planes)
 };
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,
@@ -190,6 +192,11 @@ void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st);
 // the bf16 image form (gemm_ws.hip): bf16 storage, one product per MFMA, LDS-DMA staged
 bool nt_img16_ok(const NTArgs& a);
 void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st);
+// the half-pair forms (f16 hi / lo images, 3 products): gemm_ws.hip / gemm_planes.hip
+bool nt_h2_ok(const NTArgs& a);
+void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st);
+bool tn_h2_ok(const TNArgs& a);
+void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st);
 bool tn_planes_ok(const TNArgs& a);
 void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st);
 bool tn_img16_ok(const TNArgs& a);
@@ -205,6 +212,26 @@ __device__ __forceinline__ void split3_pair(float a, float b, uint32_t& h, uint3
   a -= __uint_as_float(m << 16);
   b -= __uint_as_float(m & 0xffff0000u);
   l = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{a, b}, bf16x2_));
+}
+
+// Half-pair split (gemm_ws.hip K7a-h): hi = RNE_f16(v), lo = RNE_f16((v - hi) · 2^11); the
+// remainder is exact in f32 and v = hi + 2^-11 lo to 2^-22 |v| (|v| < 2^14 assumed by the callers).
+__device__ __forceinline__ void split_h2_pair(float a, float b, uint32_t& h, uint32_t& l) {
+  typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
+  typedef float f32x2_ __attribute__((ext_vector_type(2)));
+  const h2_ hv = __builtin_convertvector(f32x2_{a, b}, h2_);
+  h = __builtin_bit_cast(uint32_t, hv);
+  const float ra = (a - (float)hv[0]) * 2048.0f;
+  const float rb = (b - (float)hv[1]) * 2048.0f;
+  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{ra, rb}, h2_));
+}
+
+// Two packed f16 values times a power of two (exact while the result stays in range).
+__device__ __forceinline__ uint32_t h2_scale_pair(uint32_t h, float s) {
+  typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
+  typedef float f32x2_ __attribute__((ext_vector_type(2)));
+  const h2_ v = __builtin_bit_cast(h2_, h);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_{(float)v[0] * s, (float)v[1] * s}, h2_));
 }
 
 // VALU kernels for the narrow output-layer shapes (gemm_skinny.hip).  launch_nt_skinny returns

@@ -792,11 +792,23 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
   a.mask = p->mask; a.ldmask = p->ldmask; a.mask_scale = p->mask_scale;
   if (p->mask && p->ldmask < p->N) return fail(GNN_ERR_INVALID_ARG, fn, "bad ldmask");
   if (p->a_planes) {
+    if (p->planes_format != GNN_PLANES_SPLIT_BF16 && p->planes_format != GNN_PLANES_HALF_PAIR)
+      return fail(GNN_ERR_INVALID_ARG, fn, "bad planes_format");
     a.ap = static_cast<const uint16_t*>(p->a_planes);
     a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
     a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
     a.ap_ps = p->planes_stride;
+    a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
     const size_t img_bytes = (size_t)(a.ap_ld / 16) * 3 * 256 * sizeof(uint4);
+    if (a.ap_h2) {  // the half-pair image: f16 hi / lo planes, 3 products
+      if (p->math != GNN_MATH_F32 && !p->mask && nt_h2_ok(a) && p->workspace &&
+          p->workspace_bytes >= img_bytes + BN * sizeof(float)) {
+        launch_nt_h2(a, static_cast<uint4*>(p->workspace), st);
+        return hip_check(hipGetLastError(), fn);
+      }
+      if (planes_only) return fail(GNN_ERR_UNSUPPORTED, fn, "half-pair image A outside the half-pair kernel's shapes");
+      a.ap = nullptr;
+    }
     if (a.a_bf16) {  // a bf16 image (one plane): the bf16-storage form
       if (p->math != GNN_MATH_F32 && !p->mask && nt_img16_ok(a) && p->workspace && p->workspace_bytes >= img_bytes) {
         launch_nt_img16(a, static_cast<uint4*>(p->workspace), st);
@@ -908,11 +920,25 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   // widest row pitch of any operand (the split kernel uses 32-bit element offsets)
   const int64_t ldmax = std::max({a.lda1, a.k2 > 0 ? a.lda2 : 0, a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
   if (p->a_planes) {
+    if (p->planes_format != GNN_PLANES_SPLIT_BF16 && p->planes_format != GNN_PLANES_HALF_PAIR)
+      return fail(GNN_ERR_INVALID_ARG, __fn, "bad planes_format");
     a.ap = static_cast<const uint16_t*>(p->a_planes);
     a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
     a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
     a.ap_ps = p->planes_stride;
-    if (a.a_bf16) {  // a bf16 image (one plane): the bf16-storage form
+    a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
+    if (a.ap_h2) {  // the half-pair image: f16 hi / lo planes, 3 products (dz form with the h mask)
+      if (p->math != GNN_MATH_F32 && tn_h2_ok(a)) {
+        launch_tn_h2(a, nblk, st);
+        GNN_LAUNCH_CHECK();
+        slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+        GNN_LAUNCH_CHECK();
+        return GNN_OK;
+      }
+      if (planes_only) return fail(GNN_ERR_UNSUPPORTED, __fn, "half-pair image A outside the half-pair kernel's shapes");
+      a.ap = nullptr;
+    }
+    if (a.ap && a.a_bf16) {  // a bf16 image (one plane): the bf16-storage form
       if (p->math == GNN_MATH_F32 || !tn_img16_ok(a))
         return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 image A outside the image kernel's shapes");
       launch_tn_img16(a, nblk, st);
@@ -921,7 +947,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
       GNN_LAUNCH_CHECK();
       return GNN_OK;
     }
-    if (p->math != GNN_MATH_F32 && tn_planes_ok(a)) {
+    if (a.ap && p->math != GNN_MATH_F32 && tn_planes_ok(a)) {
       launch_tn_planes(a, nblk, st);
       GNN_LAUNCH_CHECK();
       slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
@@ -976,6 +1002,8 @@ extern "C" int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p) {
   a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
   a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
   a.ap_ps = p->planes_stride;
+  a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
+  if (a.ap_h2) return nt_h2_ok(a) ? 1 : 0;
   return (a.a_bf16 ? nt_img16_ok(a) : nt_planes_ok(a)) ? 1 : 0;
 }
 
@@ -989,5 +1017,10 @@ extern "C" int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p) {
   a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
   a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
   a.ap_ps = p->planes_stride;
+  a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
+  if (a.ap_h2) {
+    a.proj = p->proj; a.nproj = p->dz ? p->nproj : 0;
+    return tn_h2_ok(a) ? 1 : 0;
+  }
   return (a.a_bf16 ? tn_img16_ok(a) : tn_planes_ok(a)) ? 1 : 0;
 }

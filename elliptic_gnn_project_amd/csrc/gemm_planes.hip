@@ -51,6 +51,25 @@ __global__ __launch_bounds__(256) void split_planes_kernel(const float* __restri
   d[ps] = l;
 }
 
+// half-pair image of an f32 matrix: one thread per column pair of one row (zeros at columns >= F)
+__global__ __launch_bounds__(256) void split_h2_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
+                                                       int32_t F, uint16_t* __restrict__ img, int64_t ld, int64_t ps,
+                                                       int32_t width) {
+  const int hw = width >> 1;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * hw) return;
+  const int64_t r = i / hw;
+  const int c = 2 * (int)(i - r * hw);
+  const float* xr = x + r * ldx;
+  const float a = c < F ? xr[c] : 0.0f;
+  const float b = c + 1 < F ? xr[c + 1] : 0.0f;
+  uint32_t h, l;
+  split_h2_pair(a, b, h, l);
+  uint32_t* d = reinterpret_cast<uint32_t*>(img + r * ld + c);
+  d[0] = h;
+  d[ps >> 1] = l;
+}
+
 // ------------------------------------------------------------------ TN over a split image
 constexpr int PT_ROWS = 16;               // rows per chunk = one MFMA k-step
 constexpr int PT_AP = 352;                // LDS row pitch of an A chunk (bf16): 704 B ≡ 48 dwords mod 64
@@ -400,6 +419,312 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
     slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
 }
 
+// ------------------------------------------------------------------ TN over a half-pair image
+// dW = Gᵀ·[A1 | A2] with A from a half-pair image (2 f16 planes hi / lo, gemm_ws.hip K7a-h) and
+// G — the dz form with the h mask, G = (dz·P) ⊙ [h > 0] / (1 - p), the SAGE preset's hidden
+// layer — formed on the fly, scaled by this block's power of two s_b (|G·s_b| < 16: the bound
+// hscale · max_rows Σ_q |dz_q| · max |P| over the block's rows, one pass over its dz rows before
+// the chunk loop) and held as three f16 planes hi' = 2^11 hi, hi, lo.  Three products per k-tile
+// into one accumulator (the split-image kernel above runs six):
+//     acc += G_hi'·A_hi + G_lo·A_hi + G_hi·A_lo  (= 2^11 s_b · Gᵀ·A up to 2^-22 relative)
+// and the slab gets acc · 2^-11 / s_b (exact).  The side sums (Σ G, dzᵀ·h, Σ dz) are f32 sums of
+// the unscaled values, as in the split-image kernel.  Geometry, the chunk pipeline and slab
+// layout are the split-image kernel's: 4 waves, wave w owns dW rows 32w .. +32 x all KT k-tiles,
+// 16-row chunks, one barrier per chunk, the staging of chunk c+1 spread over chunk c's 3·KT MFMA
+// gaps (several units per gap).  LAB as above (bit 1 no MFMAs, 2 no staging, 4 no fragment reads).
+template <int KT, bool GOUT, int LAB = 0>
+__global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
+  constexpr int NPA = (2 * PT_ROWS * (PT_MAXLD / 8) + 255) / 256;  // A pieces per thread per chunk (6)
+  __shared__ __attribute__((aligned(16))) uint16_t Gt[2][3 * PT_GPL];
+  __shared__ __attribute__((aligned(16))) uint16_t At[2][2 * PT_APL];
+  __shared__ float dzL[2][256];
+  __shared__ float redm[8];
+  constexpr int NU = 2 * NPA + 4 + 16 + 4 + 3;  // staging units per chunk
+  constexpr int NG = 3 * KT;                    // MFMA gaps per chunk
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int ld = a.ap_ld;
+  const int pr = ld >> 3;
+  const int64_t mbeg = (int64_t)blockIdx.x * a.rows_per_block;
+  const int64_t mend = min(a.M, mbeg + a.rows_per_block);
+  const int nch = mend > mbeg ? (int)((mend - mbeg + PT_ROWS - 1) / PT_ROWS) : 0;
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+  floatx16 acc[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+
+  const __amdgpu_buffer_rsrc_t arsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.ap), 0, (int)(2 * a.ap_ps * 2), 0x00020000);
+  uint32_t goff[NPA], loff[NPA];
+#pragma unroll
+  for (int j = 0; j < NPA; ++j) {
+    const int q = tid + 256 * j;
+    const int per_plane = PT_ROWS * pr;
+    const bool ok = q < 2 * per_plane;
+    const int p = q / per_plane, rr = q - p * per_plane;
+    const int row = rr / pr, c16 = rr - row * pr;
+    goff[j] = ok ? (uint32_t)(((int64_t)p * a.ap_ps + (int64_t)row * ld + 8 * c16) * 2) : 0u;
+    loff[j] = ok ? (uint32_t)((p * PT_APL + row * PT_AP + 8 * c16) * 2)
+                 : (uint32_t)(((tid & 15) * PT_AP + PT_MAXLD + 8 * ((tid >> 4) & 1)) * 2);
+  }
+
+  // ---- G slot: column gn, rows 8·go .. +8 of the chunk
+  const int gn = tid & 127, go = tid >> 7;
+  const bool gcol = gn < a.Nr;
+  const int gnc = gcol ? gn : 0;
+  const float* hb = a.h + gnc;
+  const int hld = (int)a.ldh;
+  const int zr = (tid & 63) / MAXPROJ, zq = (tid & 63) % MAXPROJ;
+  const int zqc = min(zq, a.nproj - 1);
+  float pcol[MAXPROJ];
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
+
+  // ---- the block's G scale s_b: |G| <= hscale · max_m Σ_q |dz[m][q]| · max |P|
+  float gsc, gunsc;
+  {
+    float zm = 0.f;
+    for (int64_t r = mbeg + tid; r < mend; r += 256) {
+      float s = 0.f;
+      for (int q = 0; q < a.nproj; ++q) s += fabsf(a.dz[r * a.lddz + q]);
+      zm = fmaxf(zm, s);
+    }
+    float pm = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXPROJ; ++q) pm = fmaxf(pm, fabsf(pcol[q]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      zm = fmaxf(zm, __shfl_xor(zm, o));
+      pm = fmaxf(pm, __shfl_xor(pm, o));
+    }
+    if (lane == 0) {
+      redm[wave] = zm;
+      redm[4 + wave] = pm;
+    }
+    __syncthreads();
+    zm = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+    pm = fmaxf(fmaxf(redm[4], redm[5]), fmaxf(redm[6], redm[7]));
+    const float bound = zm * pm * a.hscale;
+    int E = 0;
+    if (bound > 0.f && isfinite(bound)) frexpf(bound, &E);  // bound < 2^E
+    gsc = ldexpf(1.0f, 4 - E);                               // |G · gsc| < 16
+    gunsc = ldexpf(1.0f, E - 4 - 11);                        // slab = acc · 2^-11 / gsc
+  }
+
+  const int Mi = (int)a.M;
+  auto ldbase = [&](int c) __attribute__((always_inline)) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
+  const int clast = max(nch - 1, 0);
+  u32x4 ra[NPA];
+  float rg[8];
+  float rz = 0.f;
+  auto load_a = [&](int j, int c) __attribute__((always_inline)) {
+    ra[j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], ldbase(c) * ld * 2, 0);
+  };
+  auto load_g = [&](int c) __attribute__((always_inline)) {
+    uint32_t o = (uint32_t)((ldbase(c) + 8 * go) * hld);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      rg[i] = hb[o];
+      o += (uint32_t)hld;
+    }
+  };
+  auto load_z = [&](int c) __attribute__((always_inline)) { rz = a.dz[(uint32_t)((ldbase(c) + zr) * (int)a.lddz + zqc)]; };
+  auto put_z = [&](int k) __attribute__((always_inline)) {
+    const int mb = ldbase(k);
+    const bool ok = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + k * PT_ROWS - mb && zr < (int)mend - mb;
+    dzL[k & 1][tid] = ok ? rz : 0.0f;
+  };
+
+  float db = 0.f, dzs = 0.f;
+  float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
+  float e[8];
+  uint32_t w[4][3];
+  float4 zv[8];
+  float zsv[8];
+  auto z_read = [&](int c, int i0, int n) __attribute__((always_inline)) {
+    const int buf = c & 1;
+#pragma unroll
+    for (int i = i0; i < i0 + n; ++i) {
+      const int r = 8 * go + i;
+      zv[i] = *reinterpret_cast<const float4*>(&dzL[buf][r * MAXPROJ]);
+      zsv[i] = dzL[buf][r * MAXPROJ + (gn & (MAXPROJ - 1))];
+    }
+  };
+  auto put_a = [&](int j, int c) __attribute__((always_inline)) {
+    *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(At[c & 1]) + loff[j]) = ra[j];
+  };
+  auto g_row = [&](int i, int c, int half) __attribute__((always_inline)) {
+    if (half == 0) {
+      const float4 z = zv[i];
+      float g = z.x * pcol[0];
+      g = fmaf(z.y, pcol[1], g);
+      g = fmaf(z.z, pcol[2], g);
+      e[i] = fmaf(z.w, pcol[3], g);
+      dw2[0] = fmaf(z.x, rg[i], dw2[0]);
+      dw2[1] = fmaf(z.y, rg[i], dw2[1]);
+      dw2[2] = fmaf(z.z, rg[i], dw2[2]);
+      dw2[3] = fmaf(z.w, rg[i], dw2[3]);
+      return;
+    }
+    float g = e[i];
+    dzs += gn < MAXPROJ ? zsv[i] : 0.0f;
+    g = rg[i] > 0.0f ? g * a.hscale : 0.0f;
+    db += g;
+    if constexpr (GOUT) {
+      const int mb = ldbase(c);
+      const int r = 8 * go + i;
+      const bool ok = r >= (int)mbeg + c * PT_ROWS - mb && r < (int)mend - mb && gcol;
+      if (a.gout && ok) a.gout[(int64_t)(mb + r) * a.ldgout + gn] = g;
+    }
+    e[i] = g * gsc;  // exact (a power of two)
+  };
+  auto split_pair = [&](int j) __attribute__((always_inline)) {
+    split_h2_pair(e[2 * j], e[2 * j + 1], w[j][1], w[j][2]);
+    w[j][0] = h2_scale_pair(w[j][1], 2048.0f);
+  };
+  auto g_put = [&](int c) __attribute__((always_inline)) {
+    uint16_t* gd = Gt[c & 1] + gn * PT_GP + 8 * go;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      *reinterpret_cast<uint4*>(gd + p * PT_GPL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+  };
+  // staging unit k of chunk c + 1 (refills for chunks c + 2 / c + 3); same order as the
+  // split-image kernel: A pieces, dz reads, G rows, splits, G write, h loads, dz ring
+  auto unit = [&](int k, int c) __attribute__((always_inline)) {
+    constexpr int Z0 = 2 * NPA, G0 = Z0 + 4, S0 = G0 + 16, P0 = S0 + 4;
+    if (k < Z0) {
+      if (k & 1) load_a(k >> 1, min(c + 2, clast));
+      else put_a(k >> 1, c + 1);
+    } else if (k < G0) {
+      z_read(c + 1, 2 * (k - Z0), 2);
+    } else if (k < S0) {
+      g_row((k - G0) >> 1, c + 1, (k - G0) & 1);
+    } else if (k < P0) {
+      split_pair(k - S0);
+    } else if (k == P0) {
+      g_put(c + 1);
+    } else if (k == P0 + 1) {
+      load_g(min(c + 2, clast));
+    } else if (k == P0 + 2) {
+      put_z(c + 2);
+      load_z(min(c + 3, clast));
+    }
+  };
+
+  const int gfo = (32 * wave + (lane & 31)) * PT_GP + 8 * (lane >> 5);
+  const int grp = lane >> 4, li = lane & 15;
+  const int afo = (8 * (grp >> 1) + (li >> 2)) * PT_AP + 16 * (grp & 1) + 4 * (li & 3);
+  auto afrag = [&](const uint16_t* base, int t, int p) __attribute__((always_inline)) {
+    const uint16_t* q = base + p * PT_APL + t * 32;
+    return __builtin_bit_cast(f16x8, cat_frag(tr_read(q), tr_read(q + 4 * PT_AP)));
+  };
+#define TH_FENCE __builtin_amdgcn_sched_barrier(0)
+  auto compute = [&](int c) __attribute__((always_inline)) {
+    const int buf = c & 1;
+    f16x8 gf[3], af[2][2];  // G: hi', hi, lo; A: hi, lo
+#pragma unroll
+    for (int p = 0; p < 3; ++p) gf[p] = *reinterpret_cast<const f16x8*>(Gt[buf] + p * PT_GPL + gfo);
+    const uint16_t* ab = At[buf] + afo;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) af[0][p] = afrag(ab, 0, p);
+    constexpr int pg[3] = {2, 1, 0}, pa[3] = {0, 1, 0};  // G_lo·A_hi, G_hi·A_lo, G_hi'·A_hi
+    static_for<KT>([&](auto tc) __attribute__((always_inline)) {
+      constexpr int t = decltype(tc)::value;
+      if constexpr (t + 1 < KT && !(LAB & 4)) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) af[(t + 1) & 1][p] = afrag(ab, t + 1, p);
+      }
+      static_for<3>([&](auto mc) __attribute__((always_inline)) {
+        constexpr int m = decltype(mc)::value;
+        constexpr int gap = 3 * t + m;
+        TH_FENCE;
+        if constexpr (!(LAB & 1))
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gf[pg[m]], af[(LAB & 4) ? 0 : (t & 1)][pa[m]], acc[t], 0, 0, 0);
+        TH_FENCE;
+        if constexpr (!(LAB & 2)) {
+          static_for<(gap + 1) * NU / NG - gap * NU / NG>([&](auto uc) __attribute__((always_inline)) {
+            unit(gap * NU / NG + decltype(uc)::value, c);
+          });
+        }
+      });
+      TH_FENCE;
+    });
+    if constexpr (NU > NG) {}  // every unit is placed inside the chain (NU units over NG gaps)
+    if constexpr ((LAB & 1) != 0) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t) acc[t][0] += (float)gf[0][0] + (float)af[0][0][0] + (float)af[1][1][1];
+    }
+  };
+#undef TH_FENCE
+
+  if (nch > 0) {
+    rz = a.dz[(uint32_t)((ldbase(0) + zr) * (int)a.lddz + zqc)];
+    put_z(0);
+    load_z(min(1, clast));
+    put_z(1);
+    load_z(min(2, clast));
+#pragma unroll
+    for (int j = 0; j < NPA; ++j) load_a(j, 0);
+    load_g(0);
+    __syncthreads();  // dzL
+#pragma unroll
+    for (int j = 0; j < NPA; ++j) put_a(j, 0);
+    z_read(0, 0, 8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      g_row(i, 0, 0);
+      g_row(i, 0, 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_pair(j);
+    g_put(0);
+#pragma unroll
+    for (int j = 0; j < NPA; ++j) load_a(j, min(1, clast));
+    load_g(min(1, clast));
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      compute(c);
+      __syncthreads();
+    }
+  }
+
+  // ---- this block's partial dW (segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2])
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
+  const int Kc = a.k1 + a.k2;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int kp = t * 32 + (lane & 31);
+    const bool s1 = kp < a.k1;
+    const bool s2 = kp >= a.ap_col2 && kp < a.ap_col2 + a.k2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int64_t idx = s1 ? (int64_t)row * a.k1 + kp : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (kp - a.ap_col2);
+      if (row < a.Nr && (s1 || s2)) slab[idx] = acc[t][r] * gunsc;
+    }
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(&At[0][0]);
+  constexpr int ns = 2 + MAXPROJ;
+  red[(go * 128 + gn) * ns + 0] = db;
+  red[(go * 128 + gn) * ns + 1] = dzs;
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
+  __syncthreads();
+  if (tid < 128 && tid < a.Nr) {
+    float* side = slab + (int64_t)a.Nr * Kc;
+    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
+    for (int q = 0; q < a.nproj; ++q)
+      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+  }
+  if (tid < a.nproj)
+    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+}
+
 // ------------------------------------------------------------------ TN over a bf16 image
 // bf16 storage (BASELINE configs[4]): A = a one-plane bf16 image (planes.BfImage), h bf16, G
 // rounded to bf16 for the MFMA (one product), f32 accumulation.  One MFMA per k-tile per 16-row
@@ -698,7 +1023,7 @@ void launch_tn_planes_kt(const TNArgs& a, int nblk, hipStream_t st) {
 
 // the bf16 image form: one-plane bf16 image (ld 256 or 336), h bf16 when given
 bool tn_img16_ok(const TNArgs& a) {
-  if (!a.ap || !a.a_bf16 || (a.h && !a.h_bf16)) return false;
+  if (!a.ap || a.ap_h2 || !a.a_bf16 || (a.h && !a.h_bf16)) return false;
   // the G slot's vector accesses: 4 columns per row (8-byte h, 16-byte g / gout rows)
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
   if (a.Nr % 4 || (a.h && (a.ldh % 4 || !al(a.h, 8))) || (a.g && !a.dz && (a.ldg % 4 || !al(a.g, 16))) ||
@@ -716,8 +1041,23 @@ void launch_tn_img16(const TNArgs& a, int nblk, hipStream_t st) {
   else launch_tn_img16_kt<11>(a, nblk, st);
 }
 
+// the half-pair form: dz form with the h mask (the SAGE hidden layer), f32 h, 336-wide image rows
+bool tn_h2_ok(const TNArgs& a) {
+  if (!a.ap || !a.ap_h2 || a.a_bf16 || a.h_bf16 || !a.dz || !a.proj || !a.h || a.nproj < 1) return false;
+  if (a.ap_ld != 336 || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;
+  if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
+  if (a.ap_ps < a.M * (int64_t)a.ap_ld || 2 * a.ap_ps * 2 >= ((int64_t)1 << 31) || a.M < PT_ROWS) return false;
+  const int64_t ldmax = std::max({a.ldh, a.lddz});
+  return (a.M + 32) * ldmax < ((int64_t)1 << 31);
+}
+
+void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st) {
+  if (a.gout) gemm_tn_h2_kernel<11, true><<<nblk, 256, 0, st>>>(a);
+  else gemm_tn_h2_kernel<11, false><<<nblk, 256, 0, st>>>(a);
+}
+
 bool tn_planes_ok(const TNArgs& a) {
-  if (!a.ap || a.a_bf16 || a.h_bf16) return false;
+  if (!a.ap || a.ap_h2 || a.a_bf16 || a.h_bf16) return false;
   if (a.ap_ld % 16 || a.ap_ld > PT_MAXLD || a.ap_ld < 32) return false;
   if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
   if (a.ap_ps < a.M * (int64_t)a.ap_ld || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;
@@ -737,6 +1077,20 @@ void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st) {
 }  // namespace gnnmp
 
 using namespace gnnmp;
+
+extern "C" gnn_status gnn_split_h2_f32(const float* x, int64_t ldx, int64_t rows, int64_t F, void* img, int64_t ld,
+                                       int64_t plane_stride, int64_t col0, int64_t width, gnn_stream_t stream) {
+  if (rows < 0 || F < 0 || ldx < F || width < F || (width & 1) || (col0 & 1) || col0 < 0 || col0 + width > ld ||
+      plane_stride < rows * ld || (plane_stride & 1) || (ld & 1))
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad shapes (width >= F, even width / col0 / ld / plane_stride)");
+  if (rows == 0 || width == 0) return GNN_OK;
+  if (!x && F > 0) return fail(GNN_ERR_INVALID_ARG, __func__, "null x");
+  if (!img || (reinterpret_cast<uintptr_t>(img) & 3)) return fail(GNN_ERR_INVALID_ARG, __func__, "null or unaligned image");
+  const int64_t n = rows * (width / 2);
+  split_h2_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(
+      x, ldx, rows, (int32_t)F, static_cast<uint16_t*>(img) + col0, ld, plane_stride, (int32_t)width);
+  return hip_check(hipGetLastError(), __func__);
+}
 
 extern "C" gnn_status gnn_split_planes_f32(const float* x, int64_t ldx, int64_t rows, int64_t F, void* img, int64_t ld,
                                            int64_t plane_stride, int64_t col0, int64_t width, gnn_stream_t stream) {

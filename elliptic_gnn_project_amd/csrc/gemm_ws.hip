@@ -699,6 +699,362 @@ __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uin
   }
 }
 
+// ---------------------------------------------------------------- the half-pair form (K7a-h)
+// A read from a HALF-PAIR image (gemm_planes.hip, gnn_split_h2_f32): two f16 planes per f32
+// value v,
+//     hi = RNE_f16(v),   lo = RNE_f16((v - hi) · 2^11)      v = hi + 2^-11 lo + O(2^-22 |v|)
+// (the remainder v - hi is exact in f32; scaled by 2^11 it stays in f16's normal range, so small
+// values keep their relative precision).  B, from the Linear weights, each output column scaled
+// by the power of two 2^-e_n that brings its largest weight into [8, 16), is held as THREE
+// planes: hi' = 2^11·hi, hi, lo (hi' < 2^15 fits f16).  Three f16 products per k-step into ONE
+// accumulator (the split-bf16 form runs six):
+//     acc += A_hi · B_hi' + A_hi · B_lo + A_lo · B_hi   (= 2^11 · A·B, up to 2^-22 relative)
+//     C    = acc · 2^(e_n - 11)
+// The dropped A_lo·B_lo term is 2^-22 relative: products good to ~2^-21 (fp32 rounds at 2^-24;
+// the parity bar is 1e-5), on v_mfma_f32_32x32x16_f16 (the bf16 rate).  A moves 4 B per element
+// (the split-bf16 image's 6) and the MFMA chain halves.  Needs |A| < 2^14 (planes.py checks x
+// once per input; agg = mean of x rows stays inside).
+// Geometry and software pipeline as the split-image kernel (one 256-thread block per CU, wave w
+// owns columns 32w .. +32 with B stationary in AGPRs: NKS x 3 x 4 = 252 for NKS 21), 32-row tiles
+// t = blockIdx.x, += gridDim.x, two A buffers.  Slot schedule: the tile's 3·NKS MFMAs carry the
+// previous tile's E1 (bias, ReLU, dropout -> LDS C tile), the staging of tile t+G, a barrier, E2
+// (C stores, projection) and the rest of the staging, spread evenly (several actions per MFMA gap).
+// LAB (csrc/lab only; the library instantiates 0): bit 1 no MFMAs, 2 no epilogue, 4 no staging.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <int FIRST>
+__device__ __forceinline__ void h2_mfma(floatx16& acc, const f16x8& x, const f16x8& b) {
+  if constexpr (FIRST) asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=v"(acc) : "v"(x), "a"(b));
+  else asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(x), "a"(b));
+}
+__device__ __forceinline__ void h2_mfma_end(floatx16& a1) { asm volatile("s_nop 15\n\ts_nop 7" : "+v"(a1)); }
+
+namespace h2s {
+enum : int { E1 = 1, E2 = 2, SP = 3, SL = 4, BAR = 5 };
+constexpr int MAXA = 200;
+struct Sched {
+  int kind[MAXA], idx[MAXA];
+  int first[MAXA];  // first action of slot k; slot k runs actions [first[k], first[k + 1])
+  int n;
+};
+// actions: E1 (48: element j = i/3, part i%3) interleaved with the first staging pieces, the
+// barrier, E2 (ne2) interleaved with the rest; spread over nslot MFMA gaps
+constexpr Sched make(int QP, int ne2, int nslot) {
+  Sched s{};
+  int n = 0;
+  const int qa = QP / 2;  // staging pieces before the barrier
+  for (int e = 0, q = 0; e < 48; ++e) {
+    s.kind[n] = E1; s.idx[n++] = e;
+    if (q < qa && (e + 1) * qa / 48 > q) {
+      s.kind[n] = SP; s.idx[n++] = q;
+      s.kind[n] = SL; s.idx[n++] = q;
+      ++q;
+    }
+  }
+  s.kind[n] = BAR; s.idx[n++] = 0;
+  for (int e = 0, q = qa; e < ne2; ++e) {
+    s.kind[n] = E2; s.idx[n++] = e;
+    if (q < QP && qa + (e + 1) * (QP - qa) / ne2 > q) {
+      s.kind[n] = SP; s.idx[n++] = q;
+      s.kind[n] = SL; s.idx[n++] = q;
+      ++q;
+    }
+  }
+  s.n = n;
+  for (int k = 0; k <= nslot; ++k) s.first[k] = k * n / nslot;
+  return s;
+}
+}  // namespace h2s
+
+template <int NKS, int EPI, int LAB = 0>
+__global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* __restrict__ bimg,
+                                                         const float* __restrict__ colscale, int ntiles) {
+  constexpr int PLB = NKS * WS_KSB;  // bytes per plane of an A buffer
+  constexpr int BUF = 2 * PLB;
+  constexpr int QP = (2 * NKS + 3) / 4;  // 1 KB blocks per wave per tile (NKS 21: 42 -> 11, one repeat)
+  constexpr int NSL = 3 * NKS;           // MFMA gaps per tile
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) char A0[BUF];
+  __shared__ __attribute__((aligned(16))) char A1[BUF];
+  __shared__ __attribute__((aligned(16))) float CT[WS_ROWS * BN];
+  constexpr int PLP = BN + 16;
+  __shared__ __attribute__((aligned(16))) float PL[MAXPROJ * PLP];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int64_t M = a.M;
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+
+  f16x8 bw[NKS][3];  // hi' = 2^11 hi, hi, lo
+  {
+    const int slot = 2 * (32 * wave + (lane & 31)) + (lane >> 5);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bw[s][p] = __builtin_bit_cast(f16x8, bimg[(s * 3 + p) * 256 + slot]);
+  }
+
+  const int ld = a.ap_ld;
+  const int prow = lane >> 1;
+  const int pvoff = (prow * ld + 8 * ((lane & 1) ^ ((prow >> 3) & 1))) * 2;
+  const __amdgpu_buffer_rsrc_t prsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.ap), 0, (int)(2 * a.ap_ps * 2), 0x00020000);
+  u32x4 st[QP];
+  auto pblk = [&](int i) __attribute__((always_inline)) { return min(wave + 4 * i, 2 * NKS - 1); };
+  auto load_piece = [&](int i, int t) __attribute__((always_inline)) {
+    const int b = pblk(i), p = b / NKS, s = b - p * NKS;
+    const int tc = min(t, ntiles - 1);
+    st[i] = __builtin_amdgcn_raw_buffer_load_b128(prsrc, pvoff, (int)((p * a.ap_ps + 16 * s) * 2) + tc * WS_ROWS * ld * 2, 0);
+  };
+  auto put_piece = [&](char* buf, int i) __attribute__((always_inline)) {
+    const int b = pblk(i), p = b / NKS, s = b - p * NKS;
+    *reinterpret_cast<u32x4*>(buf + p * PLB + s * WS_KSB + 16 * lane) = st[i];
+  };
+
+  const int frow = lane & 31;
+  const uint32_t foff = (uint32_t)(frow * 32 + (((lane >> 5) ^ ((frow >> 3) & 1)) << 4));
+  const int col = 32 * wave + (lane & 31);
+  const int Nc = a.Nc;
+  const bool colok = col < Nc;
+  const uint32_t hstep = (uint32_t)Nc * kDropGolden;
+  if constexpr ((EPI & WS_PROJ) != 0) {
+    for (int i = tid; i < MAXPROJ * BN; i += 256) {
+      const int q = i / BN, c = i % BN;
+      PL[q * PLP + c] = (q < a.nproj && c < Nc) ? a.proj[(int64_t)q * Nc + c] : 0.f;
+    }
+  }
+  float bv = 0.f;
+  if constexpr ((EPI & WS_BIAS) != 0) bv = colok ? a.bias[col] : 0.f;
+  const float cs = colok ? colscale[col] : 0.f;  // 2^(e_n - 11)
+  float* const cptr = a.c;
+  const int64_t ldc = a.ldc;
+  const __amdgpu_buffer_rsrc_t crsrc =
+      __builtin_amdgcn_make_buffer_rsrc(cptr, 0, cptr ? (int)(M * ldc * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t zrsrc =
+      __builtin_amdgcn_make_buffer_rsrc(a.z, 0, (EPI & WS_PROJ) != 0 ? (int)(M * a.ldz * 4) : 0, 0x00020000);
+
+  float xv[16];
+  auto e1 = [&](const floatx16& p1, int j, int part, int tp) __attribute__((always_inline)) {
+    const int rl = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+    if (part == 0) {
+      float x = fmaf(p1[j], cs, bv);
+      if constexpr ((EPI & WS_RELU) != 0) x = fmaxf(x, 0.f);
+      xv[j] = x;
+    } else if (part == 1) {
+      if constexpr ((EPI & WS_DROP) != 0) {
+        const uint32_t h0 = ((uint32_t)(tp * WS_ROWS + 4 * (lane >> 5)) * (uint32_t)Nc + (uint32_t)col) * kDropGolden +
+                            (uint32_t)seed;
+        xv[j] = keep_premixed(h0 + (uint32_t)(rl - 4 * (lane >> 5)) * hstep, seed, a.keep_thresh) ? xv[j] * a.drop_scale
+                                                                                                  : 0.f;
+      }
+    } else {
+      CT[rl * BN + col] = colok ? xv[j] : 0.f;
+    }
+  };
+  float4 cv[4];
+  float4 ph[2][4];
+  float pacc0 = 0.f, pacc1 = 0.f;
+  constexpr int NP = 2;
+  const int ppart = tid % NP, pq = (tid / NP) % MAXPROJ, prl = tid / (NP * MAXPROJ);
+  auto c_read = [&](int i) __attribute__((always_inline)) {
+    const int u = tid + 256 * i;
+    cv[i] = *reinterpret_cast<const float4*>(CT + (u / (BN / 4)) * BN + (u % (BN / 4)) * 4);
+  };
+  auto c_store = [&](int i, int tp) __attribute__((always_inline)) {
+    const int u = tid + 256 * i;
+    const int rl = u / (BN / 4), c4 = (u % (BN / 4)) * 4;
+    const u32x4 xv4 = {__float_as_uint(cv[i].x), __float_as_uint(cv[i].y), __float_as_uint(cv[i].z),
+                       __float_as_uint(cv[i].w)};
+    const uint32_t off = (c4 < Nc && tp >= 0) ? (uint32_t)((((int64_t)tp * WS_ROWS + rl) * ldc + c4) * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b128(xv4, crsrc, (int)off, 0, 0);
+  };
+  auto p_read = [&](int tt) __attribute__((always_inline)) {
+    const float4* hrow = reinterpret_cast<const float4*>(CT + prl * BN);
+    const float4* prw = reinterpret_cast<const float4*>(PL + pq * PLP);
+    const int j = ppart + 2 * NP * tt;
+    ph[tt & 1][0] = hrow[j];
+    ph[tt & 1][1] = prw[j];
+    ph[tt & 1][2] = hrow[j + NP];
+    ph[tt & 1][3] = prw[j + NP];
+  };
+  auto p_fma = [&](int tt) __attribute__((always_inline)) {
+    const float4 h0_ = ph[tt & 1][0], p0 = ph[tt & 1][1], h1_ = ph[tt & 1][2], p1 = ph[tt & 1][3];
+    pacc0 = fmaf(h0_.x, p0.x, pacc0); pacc0 = fmaf(h0_.y, p0.y, pacc0);
+    pacc0 = fmaf(h0_.z, p0.z, pacc0); pacc0 = fmaf(h0_.w, p0.w, pacc0);
+    pacc1 = fmaf(h1_.x, p1.x, pacc1); pacc1 = fmaf(h1_.y, p1.y, pacc1);
+    pacc1 = fmaf(h1_.z, p1.z, pacc1); pacc1 = fmaf(h1_.w, p1.w, pacc1);
+  };
+  auto p_done = [&](int tp) __attribute__((always_inline)) {
+    float zsum = pacc0 + pacc1;
+    zsum += __shfl_xor(zsum, 1);
+    pacc0 = pacc1 = 0.f;
+    const int64_t row = (int64_t)tp * WS_ROWS + prl;
+    const uint32_t zoff = (ppart == 0 && pq < a.nproj && tp >= 0) ? (uint32_t)((row * a.ldz + pq) * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zsum), zrsrc, (int)zoff, 0, 0);
+  };
+  constexpr int PTRIPS = BN / 4 / (2 * NP);
+  constexpr int NE2 = 8 + 2 * PTRIPS + 1;
+  auto e2 = [&](int q, int tp) __attribute__((always_inline)) {
+    if (q < 4) c_read(q);
+    else if (q < 8) c_store(q - 4, tp);
+    else if constexpr ((EPI & WS_PROJ) != 0) {
+      const int k = q - 8;
+      if (k == 0) p_read(0);
+      else if (k < 2 * PTRIPS - 1) {
+        if (k & 1) p_read((k + 1) / 2);
+        else p_fma(k / 2 - 1);
+      } else if (k == 2 * PTRIPS - 1) {
+        p_fma(PTRIPS - 1);
+      } else if (k == 2 * PTRIPS) {
+        p_done(tp);
+      }
+    }
+  };
+
+  constexpr h2s::Sched SC = h2s::make(QP, NE2, NSL);
+  auto slot = [&](auto kc, char* nxt, const floatx16& p1, int tp, int t) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    static_for<SC.first[k + 1] - SC.first[k]>([&](auto ac) __attribute__((always_inline)) {
+      constexpr int ai = SC.first[k] + decltype(ac)::value;
+      constexpr int kind = SC.kind[ai], i = SC.idx[ai];
+      if constexpr (kind == h2s::E1) {
+        if constexpr (!(LAB & 2)) e1(p1, i / 3, i % 3, tp);
+      } else if constexpr (kind == h2s::E2) {
+        if constexpr (!(LAB & 2)) e2(i, tp);
+      } else if constexpr (kind == h2s::SP) {
+        if constexpr (!(LAB & 4)) put_piece(nxt, i);
+      } else if constexpr (kind == h2s::SL) {
+        if constexpr (!(LAB & 4)) load_piece(i, t + 2 * (int)gridDim.x);
+      } else if constexpr (kind == h2s::BAR) {
+        __syncthreads();  // every wave's E1 is in the C tile
+      }
+    });
+  };
+#define NTH_FENCE __builtin_amdgcn_sched_barrier(0)
+  auto kloop = [&](const char* cur, char* nxt, floatx16& c1, const floatx16& p1, int t, int tp) __attribute__((always_inline)) {
+    f16x8 x[2];
+    auto frag = [&](int s, int p) __attribute__((always_inline)) { return *reinterpret_cast<const f16x8*>(cur + p * PLB + s * WS_KSB + foff); };
+    x[0] = frag(0, 0);
+    x[1] = frag(0, 1);
+    static_for<NKS>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int s = decltype(sc)::value;
+      // small terms first: A_hi·B_lo, A_lo·B_hi, then A_hi·B_hi'
+      NTH_FENCE;
+      if constexpr (!(LAB & 1)) h2_mfma<s == 0>(c1, x[0], bw[s][2]);
+      NTH_FENCE;
+      slot(std::integral_constant<int, 3 * s>{}, nxt, p1, tp, t);
+      NTH_FENCE;
+      if constexpr (!(LAB & 1)) h2_mfma<0>(c1, x[1], bw[s][1]);
+      NTH_FENCE;
+      if constexpr (s + 1 < NKS) x[1] = frag(s + 1, 1);
+      slot(std::integral_constant<int, 3 * s + 1>{}, nxt, p1, tp, t);
+      NTH_FENCE;
+      if constexpr (!(LAB & 1)) h2_mfma<0>(c1, x[0], bw[s][0]);
+      NTH_FENCE;
+      if constexpr (s + 1 < NKS) x[0] = frag(s + 1, 0);
+      slot(std::integral_constant<int, 3 * s + 2>{}, nxt, p1, tp, t);
+    });
+    NTH_FENCE;
+    if constexpr ((LAB & 1) != 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) c1[r] = (float)x[0][r & 7];
+    }
+    h2_mfma_end(c1);
+  };
+#undef NTH_FENCE
+  auto finish = [&](const floatx16& p1, int tp) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 48; ++k) e1(p1, k / 3, k % 3, tp);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NE2; ++q) e2(q, tp);
+  };
+
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  const int G = gridDim.x;
+#pragma unroll
+  for (int i = 0; i < QP; ++i) load_piece(i, t);
+#pragma unroll
+  for (int i = 0; i < QP; ++i) put_piece(A0, i);
+#pragma unroll
+  for (int i = 0; i < QP; ++i) load_piece(i, t + G);
+  floatx16 aA, aB;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) aA[r] = aB[r] = 0.f;
+  __syncthreads();
+  int tp = -1;
+  while (true) {
+    kloop(A0, A1, aA, aB, t, tp);
+    __syncthreads();
+    tp = t;
+    t += G;
+    if (t >= ntiles) {
+      finish(aA, tp);
+      break;
+    }
+    kloop(A1, A0, aB, aA, t, tp);
+    __syncthreads();
+    tp = t;
+    t += G;
+    if (t >= ntiles) {
+      finish(aB, tp);
+      break;
+    }
+  }
+}
+
+// B image of the half-pair NT: per k-step s, plane p (hi' = 2^11 hi, hi, lo), slot 2n + khalf:
+// the 8 halves of column n, k = 16s + 8·khalf .. +8, of w_n · 2^-e_n, where 2^-e_n brings the
+// column's largest |w| into [8, 16) (a power of two: exact); colscale[n] = 2^(e_n - 11) (block 0).
+// Every block computes all column exponents (max |w_n| over the whole K, 2 threads per column).
+__device__ __forceinline__ float h2_col_exp2(float m) {  // 2^e with m · 2^-e in [8, 16); 1 for m = 0
+  if (!(m > 0.f) || !isfinite(m)) return 1.0f;
+  int E;
+  frexpf(m, &E);  // m in [2^(E-1), 2^E)
+  return ldexpf(1.0f, E - 4);
+}
+__global__ __launch_bounds__(256) void ws_prep_h2_kernel(NTArgs a, uint4* __restrict__ img, float* __restrict__ colscale,
+                                                         int col2) {
+  __shared__ float sc[BN];
+  const int tid = threadIdx.x;
+  {
+    const int n = tid >> 1, half = tid & 1;
+    float m = 0.f;
+    if (n < a.Nc) {
+      const float* w1 = a.w1 + (int64_t)n * a.ldw1;
+      for (int k = half; k < a.k1; k += 2) m = fmaxf(m, fabsf(w1[k]));
+      if (a.w2) {
+        const float* w2 = a.w2 + (int64_t)n * a.ldw2;
+        for (int k = half; k < a.k2; k += 2) m = fmaxf(m, fabsf(w2[k]));
+      }
+    }
+    m = fmaxf(m, __shfl_xor(m, 1));
+    if (half == 0) sc[n] = h2_col_exp2(m);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && tid < BN) colscale[tid] = sc[tid] * (1.0f / 2048.0f);
+  const int c = blockIdx.x, n = tid >> 1, kh = tid & 1;
+  const float inv = 1.0f / sc[n];  // a power of two: exact
+  uint32_t hw[4], lw[4], pw[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float v[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int k = 16 * c + 8 * kh + 2 * j + q;
+      float x = 0.f;
+      if (n < a.Nc && k < a.k1) x = a.w1[(int64_t)n * a.ldw1 + k];
+      else if (n < a.Nc && k >= col2 && k < col2 + a.k2) x = a.w2[(int64_t)n * a.ldw2 + (k - col2)];
+      v[q] = x * inv;
+    }
+    split_h2_pair(v[0], v[1], hw[j], lw[j]);
+    pw[j] = h2_scale_pair(hw[j], 2048.0f);
+  }
+  img[((int64_t)c * 3 + 0) * 256 + tid] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+  img[((int64_t)c * 3 + 1) * 256 + tid] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+  img[((int64_t)c * 3 + 2) * 256 + tid] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+}
+
 // ---------------------------------------------------------------- bf16 image form (K7a-b)
 // bf16 storage (BASELINE configs[4]): A is a bf16 image [M][ld] (one plane; ld = 16·NKS; A1 in
 // columns [0, k1), A2 in [col2, col2 + k2), zeros elsewhere), B the Linear weights rounded to bf16
@@ -1014,7 +1370,7 @@ bool nt_planes_ok(const NTArgs& a) {
   // 336-wide rows (the SAGE [agg | x]) for 64 < N <= 128; 176-wide rows (one 166-wide input, the
   // GCN / GAT layer-1 x) for any N <= 128 (N <= 64 leaves half the MFMA columns zero: the kernel
   // is bound by its A stream there, not by the MFMA chain)
-  if (!a.ap || a.a_bf16 || a.c_bf16 || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc < 1) return false;
+  if (!a.ap || a.ap_h2 || a.a_bf16 || a.c_bf16 || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc < 1) return false;
   if (!(a.ap_ld == 336 && a.Nc > 64) && a.ap_ld != 176) return false;
   auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al(a.ap) || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld)
@@ -1028,10 +1384,44 @@ bool nt_planes_ok(const NTArgs& a) {
   return true;
 }
 
+// The half-pair form: f32 C, the w1/w2 B form, a 336-wide half-pair image row (21 k-steps: the
+// SAGE layer-1 [agg | x]), 1 <= N <= 128 with N % 4 == 0, M >= 32, the nt_ws_ok epilogues.
+bool nt_h2_ok(const NTArgs& a) {
+  if (!a.ap || !a.ap_h2 || a.a_bf16 || a.c_bf16 || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc < 1) return false;
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (a.ap_ld != 336 || !al(a.ap) || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld)
+    return false;
+  if (a.ap_ps < a.M * (int64_t)a.ap_ld || 2 * a.ap_ps * 2 >= ((int64_t)1 << 31)) return false;
+  if (a.c && (!al(a.c) || a.ldc % 4 != 0 || a.M * a.ldc * 4 >= ((int64_t)1 << 31))) return false;
+  if (a.Nc % 4 != 0 || (a.nproj > 0 && a.M * a.ldz * 4 >= ((int64_t)1 << 31))) return false;
+  if (a.M < WS_ROWS) return false;
+  const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
+  if ((drop || proj || relu) && !(relu && bias)) return false;
+  return true;
+}
+
+// workspace: the B image (21 k-steps x 3 planes x 256 slots x 16 B), then the 128 column scales
+void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st) {
+  constexpr int NKS = 21;
+  float* colscale = reinterpret_cast<float*>(img + NKS * 3 * 256);
+  ws_prep_h2_kernel<<<NKS, 256, 0, st>>>(a, img, colscale, a.ap_col2);
+  const int ntiles = (int)ceil_div(a.M, WS_ROWS);
+  const int grid = std::min(ntiles, ws_num_cus());
+  const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
+#define GNN_NH(E) gemm_nt_h2_kernel<NKS, E><<<grid, 256, 0, st>>>(a, img, colscale, ntiles)
+  if (proj && drop) GNN_NH(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
+  else if (proj) GNN_NH(WS_BIAS | WS_RELU | WS_PROJ);
+  else if (drop) GNN_NH(WS_BIAS | WS_RELU | WS_DROP);
+  else if (relu) GNN_NH(WS_BIAS | WS_RELU);
+  else if (bias) GNN_NH(WS_BIAS);
+  else GNN_NH(0);
+#undef GNN_NH
+}
+
 // The bf16 image form: bf16 A image (one plane, ld 256 or 336), bf16 C, the w1/w2 B form,
 // 8 <= N <= 128 (N % 8 == 0), M >= 32, the nt_ws_ok epilogues.
 bool nt_img16_ok(const NTArgs& a) {
-  if (!a.ap || !a.a_bf16 || !a.c_bf16 || !a.c || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc < 8 || a.Nc % 8)
+  if (!a.ap || a.ap_h2 || !a.a_bf16 || !a.c_bf16 || !a.c || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc < 8 || a.Nc % 8)
     return false;
   auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al(a.ap) || (a.ap_ld != 256 && a.ap_ld != 336) || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 ||

@@ -29,11 +29,15 @@ import torch
 from . import _lib
 from .aggregation import KernelTimer, aggregate, agg_bytes
 from .graph import GraphPlan, get_plan
-from .planes import BfImage, SplitImage, bf_x_image, is_registered, mean_planes_ok, x_image, x_only_image
+from .planes import (BfImage, HalfPairImage, SplitImage, bf_x_image, h2_ok, is_registered, mean_planes_ok, x_image,
+                     x_only_image)
 
 # The layer-1 operand [agg | x] as a split image (planes.py): on by default, GNNMP_PLANES=0 runs
 # the in-kernel split forms instead (same results within the split's error; A/B timing).
 _PLANES = os.environ.get("GNNMP_PLANES", "1") != "0"
+# The 2-layer SAGE's layer-1 operand as a half-pair image (f16 hi / lo planes, 3 products: include/
+# gnnmp.h gnn_split_h2_f32) rather than the split-bf16 one; GNNMP_H2=0 keeps split-bf16 (A/B).
+_H2 = os.environ.get("GNNMP_H2", "1") != "0"
 
 MAX_PROJ = 4  # nproj = 2 * num_classes <= 4
 
@@ -74,8 +78,8 @@ def _nt_workspace(device, n, k1, k2):
 
 def _planes_fields(planes):
     if planes is None:
-        return (None, 0, 0, 0)
-    return (planes.ptr, planes.ld, planes.ps, planes.col2)
+        return (None, 0, 0, 0, _lib.PLANES_SPLIT_BF16)
+    return (planes.ptr, planes.ld, planes.ps, planes.col2, getattr(planes, "fmt", _lib.PLANES_SPLIT_BF16))
 
 
 # bf16 storage: layer operands as one-plane bf16 images (planes.BfImage) for the weight-stationary
@@ -132,6 +136,8 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         # A split image is priced at the algorithmic f32 bytes; it moves 6 B / element.
         ea = 2 if bf else (4 if a1 is None else a1.element_size())
         prod = 0 if (_math(math) == _lib.MATH_F32 or w1 is None) else (1 if ea == 2 else 6)
+        if getattr(planes, "fmt", None) == _lib.PLANES_HALF_PAIR:
+            prod = 3  # f16 half-pair: 3 products
         if ea == 4 and proj is None and (n <= 8 or (k <= 8 and a2 is None)):
             prod = -1
         KernelTimer.records.append((("gemm_nt", M, k, n, ea, out.element_size() if out is not None else 0, prod),
@@ -177,6 +183,8 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         e1.record()
         ea = 2 if bf else (4 if a1 is None else a1.element_size())
         prod = 0 if _math(math) == _lib.MATH_F32 else (1 if ea == 2 else 6)
+        if getattr(planes, "fmt", None) == _lib.PLANES_HALF_PAIR:
+            prod = 3
         if ea == 4 and nr <= 8 and dz is None and h is None and gout is None:
             prod = -1
         KernelTimer.records.append((("gemm_tn", M, k1 + k2, nr, ea, h.element_size() if h is not None else 4, prod),
@@ -212,12 +220,18 @@ def gemm_tn_input(nr: int, x: torch.Tensor, g: torch.Tensor):
     return gemm_tn(nr, x, g=g)
 
 
-def _layer0_image(x: torch.Tensor, n_out: int, nt_kw):
+def _layer0_image(x: torch.Tensor, n_out: int, nt_kw, h2: bool = False):
     """The split image of [agg | x] when the planes path takes this layer (else None): x must be a
     registered constant input (planes.register_input) — its planes are built once and reused; a
-    per-batch or per-step input keeps the in-kernel split (gemm_nt over f32 [agg | x])."""
+    per-batch or per-step input keeps the in-kernel split (gemm_nt over f32 [agg | x]).
+    h2: prefer the half-pair image (f16 hi / lo planes, 3 products) when x fits it (|x| < 2^14)
+    — the 2-layer net, whose layer-0 weight gradient is the TN's dz form."""
     if not (_PLANES and is_registered(x) and mean_planes_ok(x)) or x.size(0) < 32:
         return None
+    if h2 and _H2 and HalfPairImage.addressable(x.size(0), x.size(1), x.size(1)) and h2_ok(x):
+        im = x_image(x, HalfPairImage)
+        if gemm_nt(None, None, n_out, planes=im, check_planes=True, **nt_kw):
+            return im
     if not SplitImage.addressable(x.size(0), x.size(1), x.size(1)):
         return None
     im = x_image(x)
@@ -285,7 +299,7 @@ class _FusedSAGE(torch.autograd.Function):
                 hs.append(hn)
                 bim = nxt
                 continue
-            im = _layer0_image(h, Wl[0].size(0), nt_kw) if l == 0 else None
+            im = _layer0_image(h, Wl[0].size(0), nt_kw, h2=last_hidden) if l == 0 else None
             if im is not None:  # agg written straight into the split image by K1; A staged as planes
                 ctx.image = (im, im.fill_mean(plan, h))
                 hn = gemm_nt(None, None, Wl[l].size(0), planes=im, **nt_kw)

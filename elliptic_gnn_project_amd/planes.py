@@ -35,22 +35,28 @@ def _pad8(k: int) -> int:
 class SplitImage:
     """[3, N, ld] bf16 planes of [A1 | A2] with A1 at column 0 and A2 at column ``col2``."""
 
+    nplanes = 3
+    fmt = _lib.PLANES_SPLIT_BF16
+    _split_fn = "gnn_split_planes_f32"
+    _mean_fn = "gnn_sage_mean_fwd_planes"
+
     @staticmethod
     def layout(k1: int, k2: int):
         """(col2, ld) of an image of [A1 (k1 columns) | A2 (k2 columns)]."""
         col2 = _pad8(k1)
         return col2, (col2 + _pad8(k2) + 15) // 16 * 16
 
-    @staticmethod
-    def addressable(n: int, k1: int, k2: int) -> bool:
-        """The kernels address the three planes with 31-bit byte offsets."""
-        return 3 * int(n) * SplitImage.layout(k1, k2)[1] * 2 < 2 ** 31
+    @classmethod
+    def addressable(cls, n: int, k1: int, k2: int) -> bool:
+        """The kernels address the planes with 31-bit byte offsets."""
+        return cls.nplanes * int(n) * SplitImage.layout(k1, k2)[1] * 2 < 2 ** 31
 
     def __init__(self, n: int, k1: int, k2: int, device: torch.device):
         self.n, self.k1, self.k2 = int(n), int(k1), int(k2)
         self.col2, self.ld = self.layout(k1, k2)
         self.ps = self.n * self.ld
-        self.img = torch.empty((3, self.n, self.ld), dtype=torch.bfloat16, device=device)
+        dt = torch.bfloat16 if self.nplanes == 3 else torch.float16
+        self.img = torch.empty((self.nplanes, self.n, self.ld), dtype=dt, device=device)
         self.gen = 0
         self.x_key = None
 
@@ -61,7 +67,7 @@ class SplitImage:
     def fill_x(self, x: torch.Tensor) -> None:
         """Planes of x into columns [col2, ld) (zeros past k2)."""
         with torch.cuda.device(x.device):
-            _lib.call("gnn_split_planes_f32", x.data_ptr(), int(x.stride(0)), self.n, self.k2, self.ptr, self.ld,
+            _lib.call(self._split_fn, x.data_ptr(), int(x.stride(0)), self.n, self.k2, self.ptr, self.ld,
                       self.ps, self.col2, self.ld - self.col2, _lib.stream_handle(x.device))
 
     def fill_mean(self, plan, x: torch.Tensor) -> int:
@@ -69,12 +75,27 @@ class SplitImage:
         from .aggregation import KernelTimer, agg_bytes
 
         e0 = KernelTimer.begin()
-        _lib.call("gnn_sage_mean_fwd_planes", plan.c_graph, plan.deg.data_ptr(), x.data_ptr(), int(x.stride(0)),
+        _lib.call(self._mean_fn, plan.c_graph, plan.deg.data_ptr(), x.data_ptr(), int(x.stride(0)),
                   self.k1, self.ptr, self.ld, self.ps, self.col2, _lib.stream_handle(x.device))
         # algorithmic bytes of K1 as SURVEY §8(d) counts them (f32 output); the planes store 6 B
         KernelTimer.end(e0, ("agg", _lib.AGG_MEAN, False, self.k1), agg_bytes(plan, self.k1, _lib.AGG_MEAN, False, False))
         self.gen += 1
         return self.gen
+
+
+class HalfPairImage(SplitImage):
+    """[2, N, ld] f16 half-pair planes of [A1 | A2] (include/gnnmp.h gnn_split_h2_f32): hi =
+    RNE_f16(v), lo = RNE_f16((v - hi)·2^11).  The half-pair GEMMs read them with 3 f16 products
+    per product (the split-bf16 image needs 6) and 4 B per element (6).  Values must stay below
+    2^14 in magnitude: h2_image checks x once per input; the mean half is a mean of x's rows."""
+
+    nplanes = 2
+    fmt = _lib.PLANES_HALF_PAIR
+    _split_fn = "gnn_split_h2_f32"
+    _mean_fn = "gnn_sage_mean_fwd_h2"
+
+
+H2_LIMIT = 2.0 ** 14
 
 
 def mean_planes_ok(x: torch.Tensor) -> bool:
@@ -86,20 +107,37 @@ def mean_planes_ok(x: torch.Tensor) -> bool:
     return F % 2 == 0 and x.stride(0) % 2 == 0 and F // vec > 32 and _pad8(F) // vec <= 128
 
 
-def x_image(x: torch.Tensor) -> SplitImage:
-    """The cached split image of [agg | x] for x (its x half filled), rebuilt after in-place edits."""
+def x_image(x: torch.Tensor, cls=SplitImage) -> SplitImage:
+    """The cached split image of [agg | x] for x (its x half filled), rebuilt after in-place edits.
+    cls: SplitImage (split-bf16) or HalfPairImage."""
     key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
-    im = getattr(x, _ATTR, None)
+    attr = _ATTR if cls is SplitImage else _ATTR + "_h2"
+    im = getattr(x, attr, None)
     if im is None or im.n != x.size(0) or im.k2 != x.size(1):
-        im = SplitImage(x.size(0), x.size(1), x.size(1), x.device)
+        im = cls(x.size(0), x.size(1), x.size(1), x.device)
         try:
-            setattr(x, _ATTR, im)
+            setattr(x, attr, im)
         except (AttributeError, RuntimeError):  # e.g. inference tensors: no caching
             pass
     if im.x_key != key:
         im.fill_x(x)
         im.x_key = key
     return im
+
+
+def h2_ok(x: torch.Tensor) -> bool:
+    """Whether x's values fit a half-pair image (|x| < 2^14; finite): one reduction per x (cached
+    with the same (data_ptr, _version) key as the image)."""
+    key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
+    got = getattr(x, _ATTR + "_h2ok", None)
+    if got is not None and got[0] == key:
+        return got[1]
+    ok = bool(torch.isfinite(x).all()) and float(x.abs().max()) < H2_LIMIT if x.numel() else True
+    try:
+        setattr(x, _ATTR + "_h2ok", (key, ok))
+    except (AttributeError, RuntimeError):
+        pass
+    return ok
 
 
 _ATTR_X = _ATTR + "_x"

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 16
+#define GNNMP_ABI_VERSION 17
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -190,6 +190,21 @@ gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* deg, const 
                                     void* img, int64_t ld, int64_t plane_stride, int64_t width,
                                     gnn_stream_t stream);
 
+/* Half-pair images: an f32 matrix held as TWO f16 planes, hi = RNE_f16(v) and
+ * lo = RNE_f16((v - hi) * 2^11), so v = hi + 2^-11 lo to 2^-22 |v| (the remainder is exact in f32;
+ * scaled by 2^11 it keeps small values' relative precision).  Needs |v| < 2^14.  The half-pair
+ * GEMMs (planes_format = GNN_PLANES_HALF_PAIR) run 3 f16 products per product instead of the
+ * split-bf16 form's 6 and move 4 B per element instead of 6.  Same layout and arguments as the
+ * split-bf16 functions above. */
+gnn_status gnn_split_h2_f32(const float* x, int64_t ldx, int64_t rows, int64_t F, void* img, int64_t ld,
+                            int64_t plane_stride, int64_t col0, int64_t width, gnn_stream_t stream);
+gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
+                                void* img, int64_t ld, int64_t plane_stride, int64_t width, gnn_stream_t stream);
+typedef enum {
+  GNN_PLANES_SPLIT_BF16 = 0,  /* 3 bf16 planes hi / mid / lo (gnn_split_planes_f32) */
+  GNN_PLANES_HALF_PAIR = 1    /* 2 f16 planes hi / lo (gnn_split_h2_f32) */
+} gnn_planes_format;
+
 /* Named forms of the above (what an FFI binding of SAGEConv would call). */
 gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
                                  int64_t F, float* out, int64_t ldo, gnn_stream_t stream);
@@ -340,6 +355,9 @@ typedef struct {
                                             takes (gnn_gemm_nt_planes_ok) A is read from it and a1 / a2 may
                                             be NULL; otherwise a1 / a2 are used (UNSUPPORTED if NULL). */
   int64_t planes_ld, planes_stride, planes_col2;
+  int32_t planes_format;                 /* gnn_planes_format of a_planes (HALF_PAIR: 336-wide rows,
+                                            1 <= N <= 128, N % 4 == 0; B per output column scaled by
+                                            a power of two into f16 range, 3 f16 products) */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
@@ -361,6 +379,8 @@ typedef struct {
   int32_t h_dtype;                       /* gnn_dtype of h */
   const void* a_planes;                  /* optional split image of [A1 | A2], as gnn_gemm_nt_params */
   int64_t planes_ld, planes_stride, planes_col2;
+  int32_t planes_format;                 /* gnn_planes_format (HALF_PAIR: the dz form with h, 336-wide
+                                            rows; G scaled per row block by a power of two, 3 products) */
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).
@@ -373,8 +393,10 @@ gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* worksp
  * Split-image NT shapes (f32 C, the w1/w2 B form, N % 4 == 0, M >= 32; a ReLU, dropout or
  * projection epilogue needs relu + bias):
  *   image rows of 336 (the SAGE layer-1 [agg | x], 166 + 166 padded to 168 each), 64 < N <= 128;
- *   image rows of 176 (one input of <= 176 columns: the GCN / GAT layer-1 x), 1 <= N <= 128.
- * TN image rows of 32..336 (multiple of 16), f32 h.  Both need the three planes to span < 2 GiB
+ *   image rows of 176 (one input of <= 176 columns: the GCN / GAT layer-1 x), 1 <= N <= 128;
+ *   a half-pair image (planes_format HALF_PAIR) of 336-wide rows, 1 <= N <= 128.
+ * TN image rows of 32..336 (multiple of 16), f32 h; half-pair: the dz form with h, 336-wide rows
+ * (gnn_gemm_tn_planes_ok).  Both need the planes to span < 2 GiB
  * and C / z below 2 GiB. */
 int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p);
 int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p);

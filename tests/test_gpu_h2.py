@@ -1,0 +1,228 @@
+"""GPU: half-pair images (include/gnnmp.h gnn_split_h2_f32: f16 hi = RNE(v), lo = RNE((v - hi)·2^11))
+and the 3-product f16 GEMMs that read them — the 2-layer SAGE's layer-1 [agg | x] operand.
+
+* gnn_split_h2_f32 and K1's half-pair store (gnn_sage_mean_fwd_h2) are rounding work: bit-exact
+  against a numpy restatement (numpy's float32 -> float16 cast is RNE), and K1's planes are the
+  split of the f32 K1 output bit for bit.
+* The NT / TN kernels are floating point: within relL2 1e-6 of a float64 reference (the bound the
+  split-bf16 image kernels are held to; the dropped lo·lo term is 2^-22 relative), also for
+  weights / gradients far outside [1/16, 16] (the per-column / per-block power-of-two scales),
+  and the fused SAGE step with half-pair planes within 1e-5 of the split-bf16 planes.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_l2(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def split_h2(v):
+    """hi / lo f16 words of float32 v (|v| < 2^14)."""
+    v = np.asarray(v, dtype=np.float32)
+    hi = v.astype(np.float16)
+    r = ((v - hi.astype(np.float32)) * np.float32(2048.0)).astype(np.float32)
+    lo = r.astype(np.float16)
+    return hi.view(np.uint16), lo.view(np.uint16)
+
+
+def _planes_np(im):
+    return im.img.view(torch.int16).cpu().numpy().view(np.uint16)
+
+
+def _plan_and_x(n, e, seed, device):
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.graph import get_plan
+    from elliptic_gnn_project_amd.planes import register_input
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=n, num_edges=e, seed=seed),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+    ei = data.edge_index.to(device)
+    return data, get_plan(ei, data.x.size(0)), register_input(data.x.to(device))
+
+
+def test_split_h2_bit_exact(device):
+    from elliptic_gnn_project_amd.planes import HalfPairImage
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(777, 166, generator=g) * torch.exp(torch.randn(777, 1, generator=g) * 3)
+    x[0, :8] = torch.tensor([0.0, -0.0, 1.0, -1.0, 16383.0, -2.5e-30, 1.0 + 2 ** -23, 6.0e-8])
+    x = x.clamp(-16383.0, 16383.0)
+    im = HalfPairImage(777, 166, 166, device)
+    im.img.fill_(1.0)
+    im.fill_x(x.to(device))
+    got = _planes_np(im)
+    hi, lo = split_h2(x.numpy())
+    assert np.array_equal(got[0][:, 168:334], hi)
+    assert np.array_equal(got[1][:, 168:334], lo)
+    assert not got[0][:, 334:].any() and not got[1][:, 334:].any()
+    # hi + 2^-11 lo reproduces v to 2^-22 relative
+    rec = got[0][:, 168:334].view(np.float16).astype(np.float64) + got[1][:, 168:334].view(np.float16) / 2048.0
+    xd = x.double().numpy()
+    assert np.all(np.abs(rec - xd) <= 2.0 ** -22 * np.abs(xd) + 2.0 ** -36)
+
+
+@pytest.mark.parametrize("n,e", [(5000, 6000), (203_769, 234_355)])
+def test_mean_h2_equals_split_of_k1(device, n, e):
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.aggregation import aggregate
+    from elliptic_gnn_project_amd.planes import HalfPairImage
+
+    data, plan, x = _plan_and_x(n, e, 31, device)
+    agg = aggregate(plan, x, _lib.AGG_MEAN, nodew=plan.deg).cpu().numpy()
+    im = HalfPairImage(x.size(0), x.size(1), x.size(1), device)
+    im.img.fill_(1.0)
+    assert im.fill_mean(plan, x) == 1
+    got = _planes_np(im)
+    for p, want in enumerate(split_h2(agg)):
+        assert np.array_equal(got[p][:, :166], want), p
+        assert not got[p][:, 166:168].any()
+
+
+def _operands(M, F, n, seed, wscale=0.08):
+    g = torch.Generator().manual_seed(seed)
+    agg = torch.randn(M, F, generator=g) * 0.7
+    x = torch.randn(M, F, generator=g)
+    w1 = torch.randn(n, F, generator=g) * wscale
+    w2 = torch.randn(n, F, generator=g) * wscale
+    return agg, x, w1, w2
+
+
+def _image(agg, x, device):
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.planes import HalfPairImage
+
+    im = HalfPairImage(agg.size(0), agg.size(1), x.size(1), device)
+    im.fill_x(x.to(device))
+    _lib.call("gnn_split_h2_f32", agg.to(device).data_ptr(), agg.size(1), im.n, im.k1, im.ptr, im.ld, im.ps, 0,
+              im.col2, _lib.stream_handle(device))
+    return im
+
+
+@pytest.mark.parametrize("M", [32, 1000, 4097, 20000, 203_769])
+@pytest.mark.parametrize("epi", ["plain", "relu_drop_proj"])
+def test_nt_h2_vs_f64(device, M, epi):
+    from oracle.dropout_hash import keep_mask
+    from elliptic_gnn_project_amd.fused import gemm_nt
+
+    F, n = 166, 128
+    agg, x, w1, w2 = _operands(M, F, n, M)
+    bias = torch.randn(n) * 0.1
+    proj = torch.randn(4, n)
+    ref = torch.cat([agg, x], 1).double() @ torch.cat([w1, w2], 1).double().t()
+    kw = dict(w1=w1.to(device), w2=w2.to(device))
+    z = None
+    if epi != "plain":
+        p = 0.5
+        m = torch.from_numpy(keep_mask(99, M, n, p)).double()
+        ref = torch.relu(ref + bias.double()) * m * 2.0
+        z = torch.empty(M, 4, device=device)
+        kw.update(bias=bias.to(device), relu=True, dropout_p=p, seed=99, proj=proj.to(device), z=z)
+    im = _image(agg, x, device)
+    assert gemm_nt(None, None, n, planes=im, check_planes=True, **kw)
+    c = gemm_nt(None, None, n, planes=im, **kw)
+    assert rel_l2(c, ref) < 1e-6
+    if z is not None:
+        assert rel_l2(z, c.double().cpu() @ proj.double().t()) < 1e-6
+
+
+@pytest.mark.parametrize("wscale", [3e4, 1e-6, 0.5])
+def test_nt_h2_column_scales(device, wscale):
+    """Weights far outside f16's comfortable range: every output column is scaled by its own
+    power of two (largest weight into [8, 16)), so big and tiny columns stay accurate."""
+    from elliptic_gnn_project_amd.fused import gemm_nt
+
+    M, F, n = 4097, 166, 96
+    agg, x, w1, w2 = _operands(M, F, n, 7, wscale)
+    w1[3] *= 1e4  # one column much larger than the rest
+    w2[5] *= 1e-4  # and one much smaller
+    ref = torch.cat([agg, x], 1).double() @ torch.cat([w1, w2], 1).double().t()
+    im = _image(agg, x, device)
+    c = gemm_nt(None, None, n, planes=im, w1=w1.to(device), w2=w2.to(device))
+    for j in range(n):
+        assert rel_l2(c[:, j], ref[:, j]) < 1e-6, j
+
+
+@pytest.mark.parametrize("M", [16, 1000, 20001, 203_769])
+@pytest.mark.parametrize("dzscale,gout", [(1e-3, False), (1e-3, True), (1e-9, False), (1e4, False)])
+def test_tn_h2_vs_f64(device, M, dzscale, gout):
+    """dW = Gᵀ·[agg | x] with G = (dz·P) ⊙ [h > 0]·2: the dz form of the SAGE hidden layer, with
+    tiny and large gradients (each row block's power-of-two G scale)."""
+    from elliptic_gnn_project_amd.fused import gemm_tn
+
+    F, nr = 166, 128
+    agg, x, _, _ = _operands(M, F, 1, M + 1)
+    g_ = torch.Generator().manual_seed(M)
+    h = torch.relu(torch.randn(M, nr, generator=g_))
+    dz = torch.randn(M, 4, generator=g_) * dzscale
+    proj = torch.randn(4, nr, generator=g_)
+    G = torch.where(h > 0, (dz @ proj) * 2.0, torch.zeros(M, nr))
+    kw = dict(dz=dz.to(device), proj=proj.to(device), h=h.to(device), hscale=2.0)
+    go = torch.empty(M, nr, device=device) if gout else None
+    im = _image(agg, x, device)
+    assert gemm_tn(nr, None, None, planes=im, check_planes=True, **kw)
+    dW, db, dW2, dzs = gemm_tn(nr, None, None, planes=im, gout=go, **kw)
+    A = torch.cat([agg, x], 1).double()
+    Gd = torch.where(h > 0, (dz.double() @ proj.double()) * 2.0, torch.zeros(M, nr, dtype=torch.float64))
+    assert rel_l2(torch.cat([dW[0], dW[1]], 1), Gd.t() @ A) < 1e-6
+    assert rel_l2(db, Gd.sum(0)) < 1e-6
+    assert rel_l2(dW2, dz.double().t() @ h.double()) < 1e-6
+    assert rel_l2(dzs, dz.double().sum(0)) < 1e-6
+    if go is not None:
+        torch.testing.assert_close(go.cpu(), G, rtol=1e-6, atol=1e-30)
+
+
+def _sage_step(model, x, ei, seed):
+    torch.manual_seed(seed)
+    out = model(x, ei)
+    loss = out.square().mean()
+    return out, loss
+
+
+@pytest.mark.parametrize("n,e", [(5000, 6000), (203_769, 234_355)])
+def test_fused_sage_h2_vs_split_bf16(device, n, e):
+    """The fused SAGE train step (dropout 0.5) on the half-pair image vs the split-bf16 image:
+    logits and every gradient within 1e-5 (same dropout masks)."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data, plan, x = _plan_and_x(n, e, 5, device)
+    ei = data.edge_index.to(device)
+    torch.manual_seed(3)
+    model = SAGENet(x.size(1), 128, layers=2, dropout=0.5).to(device).train()
+    res = []
+    for on in (True, False):
+        fused._H2 = on
+        try:
+            model.zero_grad()
+            out, loss = _sage_step(model, x, ei, 123)
+            loss.backward()
+            res.append((out.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()}))
+        finally:
+            fused._H2 = True
+    assert getattr(x, "_gnnmp_split_image_h2", None) is not None  # the half-pair path ran
+    (o1, g1), (o2, g2) = res
+    torch.testing.assert_close(o1, o2, rtol=1e-5, atol=1e-5)
+    for k in g1:
+        assert rel_l2(g1[k], g2[k]) < 1e-5, k
+
+
+def test_large_input_keeps_split_bf16(device):
+    """|x| >= 2^14 does not fit a half-pair image: the layer takes the split-bf16 image."""
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data, plan, x = _plan_and_x(3000, 4000, 6, device)
+    x = x.clone()
+    x[0, 0] = 2.0 ** 15
+    from elliptic_gnn_project_amd.planes import register_input
+    register_input(x)
+    torch.manual_seed(4)
+    model = SAGENet(x.size(1), 128, layers=2, dropout=0.0).to(device).train()
+    model(x, data.edge_index.to(device)).sum().backward()
+    assert getattr(x, "_gnnmp_split_image_h2", None) is None
+    assert getattr(x, "_gnnmp_split_image", None) is not None
