@@ -123,7 +123,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("a_dtype", c_i32), ("c_dtype", c_i32),
         ("mask", c_ptr), ("ldmask", c_i64), ("mask_scale", ctypes.c_float),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
-        ("planes_format", c_i32),
+        ("planes_format", c_i32), ("keep_mask", c_ptr),
     ]
 
 
@@ -222,7 +222,8 @@ SIGNATURES = {
     "gnn_split_h2_f32": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr]),
     "gnn_sage_mean_fwd_h2": (
         ctypes.c_int,
-        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr],
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64,
+         c_ptr, c_i64, ctypes.c_float, ctypes.c_uint64, c_ptr, c_ptr],
     ),
     "gnn_sage_mean_bwd_f32": (
         ctypes.c_int,

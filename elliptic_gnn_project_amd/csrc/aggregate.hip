@@ -108,6 +108,10 @@ struct AggArgs {
   // split-image output (gnn_sage_mean_fwd_planes): hi / mid / lo bf16 planes at yp + p·yps, row
   // pitch ldy, columns [F, ywidth) zero
   uint16_t* yp; int64_t yps; int32_t ywidth;
+  // K1 of the half-pair path: the dropout keep bits of the NEXT GEMM's output rows (the NT that
+  // consumes this image, N = kcols <= 128 columns), bit c of kmask[r·4 + c/32] = keep_elem(seed,
+  // r·kcols + c), computed here where the gather leaves the VALU idle
+  uint32_t* kmask; int32_t kcols;
 };
 
 __device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
@@ -483,6 +487,15 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
         }
 #pragma unroll
         for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+        if (i == NCH - 1 && a.kmask) {  // once per row, after its planes
+          const uint32_t e0 = (uint32_t)r * (uint32_t)a.kcols;
+          const bool k0 = lane < a.kcols && keep_elem(dseed, e0 + (uint32_t)lane, a.keep_thresh);
+          const bool k1 = lane + 64 < a.kcols && keep_elem(dseed, e0 + (uint32_t)(lane + 64), a.keep_thresh);
+          const uint64_t b0 = __ballot(k0), b1 = __ballot(k1);
+          if (lane == 0)
+            *reinterpret_cast<uint4*>(a.kmask + r * 4) =
+                make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
+        }
         continue;
       }
       if (!BF && c < nchunk && p0 >= 0) {  // long row: raw partial of piece 0
@@ -1303,7 +1316,8 @@ extern "C" gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg
 template <int PLN>
 static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
                                       void* img, int64_t ld, int64_t plane_stride, int64_t width, gnn_stream_t stream,
-                                      const char* fn) {
+                                      const char* fn, uint32_t* keep_mask = nullptr, int64_t mask_cols = 0,
+                                      float dropout_p = 0.f, uint64_t seed = 0, const uint64_t* seed_ptr = nullptr) {
   if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or deg");
   if (F < 2 || ldx < F || width < F || width > ld || plane_stride < g->num_nodes * ld)
     return fail(GNN_ERR_INVALID_ARG, fn, "bad F / width / leading dimensions");
@@ -1319,6 +1333,16 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
   a.yp = static_cast<uint16_t*>(img); a.ldy = ld; a.yps = plane_stride; a.ywidth = (int32_t)width;
   a.nrows = g->num_nodes;
   a.F = (int32_t)F;
+  if (keep_mask) {
+    if (mask_cols < 1 || mask_cols > 128 || !(dropout_p > 0.f && dropout_p < 1.f) ||
+        (reinterpret_cast<uintptr_t>(keep_mask) & 15) || g->num_nodes * mask_cols >= ((int64_t)1 << 32))
+      return fail(GNN_ERR_INVALID_ARG, fn, "keep mask: 1 <= mask_cols <= 128, 0 < p < 1, 16-byte aligned, rows x cols < 2^32");
+    a.kmask = keep_mask; a.kcols = (int32_t)mask_cols;
+    a.dropout = 1;
+    a.keep_thresh = (uint32_t)((1.0 - (double)dropout_p) * 16777216.0);
+    a.seed = seed;
+    a.seed_ptr = reinterpret_cast<const int64_t*>(seed_ptr);
+  }
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
   const bool v4 = F % 4 == 0 && ldx % 4 == 0 && width % 4 == 0 && ld % 4 == 0 && plane_stride % 4 == 0 &&
                   al(x, 16) && al(img, 8);
@@ -1344,8 +1368,10 @@ extern "C" gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* 
 
 extern "C" gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
                                            int64_t F, void* img, int64_t ld, int64_t plane_stride, int64_t width,
-                                           gnn_stream_t stream) {
-  return sage_mean_fwd_image<2>(g, deg, x, ldx, F, img, ld, plane_stride, width, stream, __func__);
+                                           uint32_t* keep_mask, int64_t mask_cols, float dropout_p, uint64_t seed,
+                                           const uint64_t* seed_ptr, gnn_stream_t stream) {
+  return sage_mean_fwd_image<2>(g, deg, x, ldx, F, img, ld, plane_stride, width, stream, __func__, keep_mask,
+                                mask_cols, dropout_p, seed, seed_ptr);
 }
 
 extern "C" gnn_status gnn_sage_mean_bwd_f32(const gnn_graph* g, const float* deg, const float* dout,

@@ -70,6 +70,7 @@ struct NTArgs {
   // elsewhere.  The weight-stationary kernel then stages A by plain copies (no split VALU).
   const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;
   int32_t ap_h2;  // the image is a half-pair image (2 f16 planes hi / lo, gemm_ws.hip K7a-h)
+  const uint32_t* kmask;  // optional dropout keep bits (half-pair NT): bit c of kmask[r·4 + c/32]
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }

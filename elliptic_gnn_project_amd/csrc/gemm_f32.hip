@@ -800,6 +800,11 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
     a.ap_ps = p->planes_stride;
     a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
     const size_t img_bytes = (size_t)(a.ap_ld / 16) * 3 * 256 * sizeof(uint4);
+    if (p->keep_mask) {
+      if (!a.ap_h2 || !a.dropout || (reinterpret_cast<uintptr_t>(p->keep_mask) & 3))
+        return fail(GNN_ERR_INVALID_ARG, fn, "keep_mask needs a half-pair image A and dropout_p > 0");
+      a.kmask = p->keep_mask;
+    }
     if (a.ap_h2) {  // the half-pair image: f16 hi / lo planes, 3 products
       if (p->math != GNN_MATH_F32 && !p->mask && nt_h2_ok(a) && p->workspace &&
           p->workspace_bytes >= img_bytes + BN * sizeof(float)) {

@@ -69,6 +69,7 @@ __device__ __forceinline__ uint32_t ws_off(int row, int kk) {
 
 // Flags of the fused epilogue (compile-time: the interleaved loop must stay one basic block).
 constexpr int WS_BIAS = 1, WS_RELU = 2, WS_DROP = 4, WS_PROJ = 8;
+constexpr int WS_KMASK = 16;  // half-pair NT: dropout from precomputed keep bits (NTArgs::kmask)
 
 // KS = 1: 4 waves (one per SIMD), every wave holds all NKS k-steps of its columns (≤ 264 VGPRs
 //         of B; 512-register waves).  KS = 2: 8 waves (two per SIMD), each holds half the
@@ -833,6 +834,11 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
       __builtin_amdgcn_make_buffer_rsrc(a.z, 0, (EPI & WS_PROJ) != 0 ? (int)(M * a.ldz * 4) : 0, 0x00020000);
 
   float xv[16];
+  uint32_t mk[2] = {0u, 0u};  // keep-bit words: the tile being computed (loaded) / the tile in E1 (used)
+  uint32_t mku = 0u;
+  auto load_mk = [&](uint32_t& m, int t) __attribute__((always_inline)) {
+    if constexpr ((EPI & WS_KMASK) != 0) m = a.kmask[((int64_t)t * WS_ROWS + (lane & 31)) * 4 + wave];
+  };
   auto e1 = [&](const floatx16& p1, int j, int part, int tp) __attribute__((always_inline)) {
     const int rl = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
     if (part == 0) {
@@ -840,7 +846,12 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
       if constexpr ((EPI & WS_RELU) != 0) x = fmaxf(x, 0.f);
       xv[j] = x;
     } else if (part == 1) {
-      if constexpr ((EPI & WS_DROP) != 0) {
+      if constexpr ((EPI & WS_DROP) != 0 && (EPI & WS_KMASK) != 0) {
+        // the keep bits K1 computed for this tile's rows: lane r < 32 holds row r's word of this
+        // wave's 32 columns (== keep_elem(seed, row·Nc + col), bit for bit)
+        const uint32_t bits = (uint32_t)__shfl((int)mku, rl);
+        xv[j] = ((bits >> (lane & 31)) & 1u) ? xv[j] * a.drop_scale : 0.f;
+      } else if constexpr ((EPI & WS_DROP) != 0) {
         const uint32_t h0 = ((uint32_t)(tp * WS_ROWS + 4 * (lane >> 5)) * (uint32_t)Nc + (uint32_t)col) * kDropGolden +
                             (uint32_t)seed;
         xv[j] = keep_premixed(h0 + (uint32_t)(rl - 4 * (lane >> 5)) * hstep, seed, a.keep_thresh) ? xv[j] * a.drop_scale
@@ -930,7 +941,10 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
     });
   };
 #define NTH_FENCE __builtin_amdgcn_sched_barrier(0)
-  auto kloop = [&](const char* cur, char* nxt, floatx16& c1, const floatx16& p1, int t, int tp) __attribute__((always_inline)) {
+  auto kloop = [&](const char* cur, char* nxt, floatx16& c1, const floatx16& p1, int t, int tp, uint32_t& mkl,
+                   uint32_t mkp) __attribute__((always_inline)) {
+    mku = mkp;       // E1 of tile tp reads its keep bits
+    load_mk(mkl, t);  // and tile t's are loaded for its E1 one tile later
     f16x8 x[2];
     auto frag = [&](int s, int p) __attribute__((always_inline)) { return *reinterpret_cast<const f16x8*>(cur + p * PLB + s * WS_KSB + foff); };
     x[0] = frag(0, 0);
@@ -984,19 +998,21 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
   __syncthreads();
   int tp = -1;
   while (true) {
-    kloop(A0, A1, aA, aB, t, tp);
+    kloop(A0, A1, aA, aB, t, tp, mk[0], mk[1]);
     __syncthreads();
     tp = t;
     t += G;
     if (t >= ntiles) {
+      mku = mk[0];
       finish(aA, tp);
       break;
     }
-    kloop(A1, A0, aB, aA, t, tp);
+    kloop(A1, A0, aB, aA, t, tp, mk[1], mk[0]);
     __syncthreads();
     tp = t;
     t += G;
     if (t >= ntiles) {
+      mku = mk[1];
       finish(aB, tp);
       break;
     }
@@ -1409,7 +1425,9 @@ void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st) {
   const int grid = std::min(ntiles, ws_num_cus());
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
 #define GNN_NH(E) gemm_nt_h2_kernel<NKS, E><<<grid, 256, 0, st>>>(a, img, colscale, ntiles)
-  if (proj && drop) GNN_NH(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
+  if (proj && drop && a.kmask) GNN_NH(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ | WS_KMASK);
+  else if (drop && a.kmask) GNN_NH(WS_BIAS | WS_RELU | WS_DROP | WS_KMASK);
+  else if (proj && drop) GNN_NH(WS_BIAS | WS_RELU | WS_DROP | WS_PROJ);
   else if (proj) GNN_NH(WS_BIAS | WS_RELU | WS_PROJ);
   else if (drop) GNN_NH(WS_BIAS | WS_RELU | WS_DROP);
   else if (relu) GNN_NH(WS_BIAS | WS_RELU);

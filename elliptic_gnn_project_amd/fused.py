@@ -89,12 +89,13 @@ _BF_IMAGE = os.environ.get("GNNMP_BF_IMAGE", "1") != "0"
 
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
             out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None, mask=None, mask_scale=1.0,
-            planes=None, check_planes=False):
+            planes=None, check_planes=False, keep_mask=None):
     """C = epilogue([a1 | a2] · B) on the NT kernels; B = bt ([K, n] row-major) or, with bt None,
     [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2].
     bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too.
     ``planes`` (planes.SplitImage): A read from the split image; a1 / a2 may then be None.
-    ``check_planes``: only report whether the call would take the split-image kernel (no launch)."""
+    ``check_planes``: only report whether the call would take the split-image kernel (no launch).
+    ``keep_mask`` (half-pair planes with dropout): the keep bits K1 wrote for this call's seed."""
     if planes is not None:
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
@@ -119,7 +120,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.DTYPE_BF16 if bf else _lib.DTYPE_F32,
         _lib.DTYPE_BF16 if (out is not None and out.dtype == torch.bfloat16) else _lib.DTYPE_F32,
         _lib.ptr(mask), _ld(mask) if mask is not None else 0, float(mask_scale),
-        *_planes_fields(planes),
+        *_planes_fields(planes), _lib.ptr(keep_mask),
     )
     if check_planes:
         return bool(_lib.load().gnn_gemm_nt_planes_ok(p))
@@ -301,7 +302,12 @@ class _FusedSAGE(torch.autograd.Function):
                 continue
             im = _layer0_image(h, Wl[0].size(0), nt_kw, h2=last_hidden) if l == 0 else None
             if im is not None:  # agg written straight into the split image by K1; A staged as planes
-                ctx.image = (im, im.fill_mean(plan, h))
+                keep = None
+                if isinstance(im, HalfPairImage) and train_drop > 0:  # K1 also writes the NT's keep bits
+                    kb = im.keep_buffer()
+                    keep = (kb, Wl[l].size(0), train_drop, seeds[l], seed_ctr)
+                    nt_kw = dict(nt_kw, keep_mask=kb)
+                ctx.image = (im, im.fill_mean(plan, h, keep))
                 hn = gemm_nt(None, None, Wl[l].size(0), planes=im, **nt_kw)
                 agg = None
             else:

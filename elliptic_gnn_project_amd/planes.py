@@ -70,13 +70,19 @@ class SplitImage:
             _lib.call(self._split_fn, x.data_ptr(), int(x.stride(0)), self.n, self.k2, self.ptr, self.ld,
                       self.ps, self.col2, self.ld - self.col2, _lib.stream_handle(x.device))
 
-    def fill_mean(self, plan, x: torch.Tensor) -> int:
-        """K1: planes of mean_{j->i} x[j] into columns [0, col2); returns the new generation."""
+    def fill_mean(self, plan, x: torch.Tensor, keep=None) -> int:
+        """K1: planes of mean_{j->i} x[j] into columns [0, col2); returns the new generation.
+        keep (half-pair images only): (mask [N, 4] int32, cols, p, seed, seed_ptr) — K1 also writes
+        the dropout keep bits of the NT that reads this image (include/gnnmp.h gnn_sage_mean_fwd_h2)."""
         from .aggregation import KernelTimer, agg_bytes
 
         e0 = KernelTimer.begin()
-        _lib.call(self._mean_fn, plan.c_graph, plan.deg.data_ptr(), x.data_ptr(), int(x.stride(0)),
-                  self.k1, self.ptr, self.ld, self.ps, self.col2, _lib.stream_handle(x.device))
+        args = (plan.c_graph, plan.deg.data_ptr(), x.data_ptr(), int(x.stride(0)), self.k1, self.ptr, self.ld,
+                self.ps, self.col2)
+        if self.nplanes == 2:
+            km, cols, p, seed, sptr = keep if keep is not None else (None, 0, 0.0, 0, None)
+            args += (_lib.ptr(km), int(cols), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(sptr))
+        _lib.call(self._mean_fn, *args, _lib.stream_handle(x.device))
         # algorithmic bytes of K1 as SURVEY §8(d) counts them (f32 output); the planes store 6 B
         KernelTimer.end(e0, ("agg", _lib.AGG_MEAN, False, self.k1), agg_bytes(plan, self.k1, _lib.AGG_MEAN, False, False))
         self.gen += 1
@@ -93,6 +99,13 @@ class HalfPairImage(SplitImage):
     fmt = _lib.PLANES_HALF_PAIR
     _split_fn = "gnn_split_h2_f32"
     _mean_fn = "gnn_sage_mean_fwd_h2"
+
+    def keep_buffer(self) -> torch.Tensor:
+        """[N, 4] int32 keep bits of the dropout that follows this image's NT (written by K1)."""
+        kb = getattr(self, "_keep", None)
+        if kb is None:
+            kb = self._keep = torch.empty((self.n, 4), dtype=torch.int32, device=self.img.device)
+        return kb
 
 
 H2_LIMIT = 2.0 ** 14

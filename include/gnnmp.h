@@ -198,8 +198,14 @@ gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* deg, const 
  * split-bf16 functions above. */
 gnn_status gnn_split_h2_f32(const float* x, int64_t ldx, int64_t rows, int64_t F, void* img, int64_t ld,
                             int64_t plane_stride, int64_t col0, int64_t width, gnn_stream_t stream);
+/* gnn_sage_mean_fwd_h2 optionally also writes the dropout keep bits of the NT that consumes the
+ * image (keep_mask != NULL, [num_nodes][4] uint32, 16-byte aligned): bit c of keep_mask[r*4 + c/32]
+ * = keep_elem(seed', r*mask_cols + c) with seed' the NT's (seed, seed_ptr) rule — the mask the NT
+ * would hash itself, computed where the gather leaves the VALU idle (gnn_gemm_nt_params.keep_mask). */
 gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
-                                void* img, int64_t ld, int64_t plane_stride, int64_t width, gnn_stream_t stream);
+                                void* img, int64_t ld, int64_t plane_stride, int64_t width, uint32_t* keep_mask,
+                                int64_t mask_cols, float dropout_p, uint64_t seed, const uint64_t* seed_ptr,
+                                gnn_stream_t stream);
 typedef enum {
   GNN_PLANES_SPLIT_BF16 = 0,  /* 3 bf16 planes hi / mid / lo (gnn_split_planes_f32) */
   GNN_PLANES_HALF_PAIR = 1    /* 2 f16 planes hi / lo (gnn_split_h2_f32) */
@@ -358,6 +364,9 @@ typedef struct {
   int32_t planes_format;                 /* gnn_planes_format of a_planes (HALF_PAIR: 336-wide rows,
                                             1 <= N <= 128, N % 4 == 0; B per output column scaled by
                                             a power of two into f16 range, 3 f16 products) */
+  const uint32_t* keep_mask;             /* optional (HALF_PAIR with dropout): the keep bits written by
+                                            gnn_sage_mean_fwd_h2 for this call's seed / p / N; used
+                                            instead of hashing every element in the epilogue */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */

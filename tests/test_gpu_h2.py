@@ -226,3 +226,28 @@ def test_large_input_keeps_split_bf16(device):
     model(x, data.edge_index.to(device)).sum().backward()
     assert getattr(x, "_gnnmp_split_image_h2", None) is None
     assert getattr(x, "_gnnmp_split_image", None) is not None
+
+
+@pytest.mark.parametrize("use_ptr", [False, True])
+def test_k1_keep_bits_equal_the_dropout_hash(device, use_ptr):
+    """K1 of the half-pair path writes the keep bits of the NT's dropout (bit c of word r·4 + c/32
+    = keep_elem(seed, r·128 + c)) — bit for bit the oracle's mask, with a plain seed and with the
+    HIP-graph device counter (seed' = counter · golden + salt)."""
+    from oracle.dropout_hash import keep_mask
+    from elliptic_gnn_project_amd.planes import HalfPairImage
+
+    data, plan, x = _plan_and_x(5000, 6000, 12, device)
+    im = HalfPairImage(x.size(0), x.size(1), x.size(1), device)
+    kb = im.keep_buffer()
+    kb.fill_(-1)
+    if use_ptr:
+        ctr = torch.tensor([12345], dtype=torch.int64, device=device)
+        seed = ((12345 * 0x9E3779B97F4A7C15) + 3) & 0xFFFFFFFFFFFFFFFF
+        im.fill_mean(plan, x, (kb, 128, 0.5, 3, ctr))
+    else:
+        seed = 987654321987
+        im.fill_mean(plan, x, (kb, 128, 0.5, seed, None))
+    want = keep_mask(seed, x.size(0), 128, 0.5)
+    got = kb.cpu().numpy().view(np.uint32)
+    bits = (got[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1
+    assert np.array_equal(bits.reshape(x.size(0), 128).astype(bool), want)
