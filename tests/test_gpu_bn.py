@@ -193,3 +193,23 @@ def test_time_inject_sin_matches_torch(device, dim, T, Fin):
     torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
     assert torch.equal(out[:, :Fin], x)
     assert torch.equal(m._inject_time(x, t), out)
+
+
+def test_time_inject_cached_for_registered_input(device):
+    """K13's [x | sin(t)] is a function of constants for a registered x: computed once, cached on
+    x, registered itself (layer 1's GEMMs read its image); an in-place edit of x recomputes it."""
+    from elliptic_gnn_project_amd.fused import time_inject_sin
+    from elliptic_gnn_project_amd.planes import is_registered, register_input
+
+    g = torch.Generator().manual_seed(5)
+    x = register_input(torch.randn(3000, 165, generator=g).to(device))
+    t = torch.randint(1, 50, (3000,), generator=g).to(device)
+    a = time_inject_sin(x, t, 2, 49)
+    b = time_inject_sin(x, t, 2, 49)
+    assert a is b and is_registered(a)
+    x.mul_(2.0)
+    c = time_inject_sin(x, t, 2, 49)
+    assert c is not a
+    torch.testing.assert_close(c[:, :165], x)
+    u = torch.randn(100, 165, generator=g).to(device)  # unregistered: no cache, fresh each call
+    assert time_inject_sin(u, t[:100], 2, 49) is not time_inject_sin(u, t[:100], 2, 49)

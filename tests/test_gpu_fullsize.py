@@ -113,10 +113,13 @@ def _resbn_data():
     return _CACHE["resbn"]
 
 
-def _resbn_step_vs_oracle(device, data):
+def _resbn_step_vs_oracle(device, data, registered=False):
     """One SAGE-ResBN train step (K13 time input, K12 BN tails with the f64 batch statistics over
     every row, dropout 0.2) vs the float64 oracle under the same masks: logits, loss, all
-    parameter gradients and both layers' BN running statistics (src/models/gnn.py:168-194)."""
+    parameter gradients and both layers' BN running statistics (src/models/gnn.py:168-194).
+    registered: x declared constant (as bench.py / train_gnn.main do) — K13's output is cached and
+    registered, so layer 1's conv and residual GEMMs read its split image."""
+    from elliptic_gnn_project_amd.planes import register_input
     from elliptic_gnn_project_amd.train_gnn import build_model
 
     L, H, p = RESBN["layers"], RESBN["hidden_dim"], RESBN["dropout"]
@@ -125,8 +128,14 @@ def _resbn_step_vs_oracle(device, data):
     model = build_model("sage_resbn", data.x.size(1), RESBN).to(device)
     params = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
     model.train()
+    xd = data.x.to(device)
+    if registered:
+        register_input(xd)
     torch.manual_seed(11)
-    logits = model(data.x.to(device), data.edge_index.to(device), data.timestep.to(device))
+    logits = model(xd, data.edge_index.to(device), data.timestep.to(device))
+    if registered:
+        h0 = xd._gnnmp_time_inject[1]  # the cached [x | sin(t)], registered: its image served layer 1
+        assert getattr(h0, "_gnnmp_split_image_x", None) is not None
     torch.manual_seed(11)
     seeds = torch.randint(0, 2 ** 62, (L,), dtype=torch.int64).tolist()
     masks = [torch.from_numpy(keep_mask(seeds[l], N, H, p)) for l in range(L - 1)]
@@ -155,13 +164,14 @@ def _resbn_step_vs_oracle(device, data):
     assert int(model.state_dict()["bns.0.num_batches_tracked"]) == 1
 
 
-def test_full_size_sage_resbn_train_step(device):
+@pytest.mark.parametrize("registered", [True, False])
+def test_full_size_sage_resbn_train_step(device, registered):
     """BASELINE configs[3] (rec_k8 SAGE-ResBN 3L/64 + sin2) on the full 203,769-node graph: the
     K12 statistics merge over all its row blocks, K13 over every row, F = 64 split pieces at the
     real hub degrees, against the float64 oracle."""
     data = _resbn_data()
     assert data.edge_index.size(1) == 2 * E_FULL and data.x.size(1) == 165
-    _resbn_step_vs_oracle(device, data)
+    _resbn_step_vs_oracle(device, data, registered)
 
 
 def test_full_size_sage_resbn_largest_shard(device):
