@@ -18,6 +18,321 @@ namespace gnnmp {
 void set_last_error(const std::string&) {}
 }
 
+namespace gnnmp {
+namespace {
+// Half-pair TN with every chunk operand copied into LDS rings by global_load_lds (the lab's
+// split-bf16 DMA TN, gemm_tn_planes_dma_kernel in lab_gemm.hip, on 2 f16 A planes and 3 G planes):
+// A two chunks ahead, h / dz three, so more bytes are in flight per CU than one register-staged
+// chunk (a half-pair chunk's MFMA phase is 33 MFMAs, shorter than a load's latency).
+template <int KT, int LAB = 0>
+__global__ __launch_bounds__(256) void gemm_tn_h2_dma_kernel(TNArgs a) {
+  constexpr int ACH = 2 * PT_APL * 2;          // one A chunk buffer: 22528 B = 22 x 1 KB
+  constexpr int NA = ACH / 1024;
+  constexpr int HCH = PT_ROWS * 128 * 4;       // one h chunk: 16 rows x 128 f32
+  constexpr int NH = HCH / 1024;
+  constexpr int NI = (NA + NH + 1 + 3) / 4;    // DMA instructions per wave per group (8)
+  constexpr int GCH = 3 * PT_GPL * 2;          // one G buffer (3 planes [n][m])
+  constexpr int OA = 0, OH = OA + 3 * ACH, OZ = OH + 3 * HCH, OG = OZ + 3 * 256;
+  constexpr int LDSB = OG + 2 * GCH;
+  static_assert(ACH % 1024 == 0 && HCH % 1024 == 0 && LDSB <= 160 * 1024, "LDS layout");
+  static_assert(3 * KT >= NI, "the DMA group issues in the chain's first slots");
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
+  __shared__ float redm[8];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ld = a.ap_ld;
+  const int pr = ld >> 3;
+  const int64_t mbeg = (int64_t)blockIdx.x * a.rows_per_block;
+  const int64_t mend = min(a.M, mbeg + a.rows_per_block);
+  const int nch = mend > mbeg ? (int)((mend - mbeg + PT_ROWS - 1) / PT_ROWS) : 0;
+  const int Mi = (int)a.M;
+  auto ldbase = [&](int c) __attribute__((always_inline)) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
+  const int clast = max(nch - 1, 0);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+
+  floatx16 acc[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+
+  auto a_off = [&](int I) __attribute__((always_inline)) {
+    const int q = 64 * I + lane;
+    const int p = q / (PT_ROWS * (PT_AP / 8)), rr = q - p * (PT_ROWS * (PT_AP / 8));
+    const int row = rr / (PT_AP / 8), pc = rr - row * (PT_AP / 8);
+    return (uint32_t)(((int64_t)p * a.ap_ps + (int64_t)row * ld) * 2) + (pc < pr ? 16u * pc : 0u);
+  };
+  const int hcol = min(4 * (lane & 31), (int)a.Nr - 4);
+  const int ldhg = (int)a.ldh;
+  constexpr int NDUP0 = NA + NH + 1;  // first count-padding instruction
+  uint32_t voff[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int I = wave + 4 * j;
+    if (I < NA) voff[j] = a_off(I);
+    else if (I < NA + NH) voff[j] = (uint32_t)(((2 * (I - NA) + (lane >> 5)) * ldhg + hcol) * 4);
+    else if (I == NA + NH) voff[j] = (uint32_t)(((lane >> 2) * (int)a.lddz + min(lane & 3, a.nproj - 1)) * 4);
+    else voff[j] = a_off(I - NDUP0);
+  }
+  uint32_t voff0[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int I = wave + 4 * j;
+    const int k = I < NH ? I : I == NH ? 0 : I - NH - 1;
+    voff0[j] = (I == NH) ? (uint32_t)(((lane >> 2) * (int)a.lddz + min(lane & 3, a.nproj - 1)) * 4)
+                         : (uint32_t)(((2 * k + (lane >> 5)) * ldhg + hcol) * 4);
+  }
+  auto glds16 = [](const void* src, uint32_t dst) __attribute__((always_inline)) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst)));
+  };
+  auto glds4 = [](const void* src, uint32_t dst) __attribute__((always_inline)) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst)));
+  };
+  auto wait_vm = [](auto nc) __attribute__((always_inline)) {
+    constexpr int N = decltype(nc)::value;
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  };
+  const char* const apb = reinterpret_cast<const char*>(a.ap);
+  const char* const hb = reinterpret_cast<const char*>(a.h);
+  const char* const zb = reinterpret_cast<const char*>(a.dz);
+  uint64_t sbase[NI];
+  int srb[NI], sofs[NI], sstr[NI], sdst[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int I = wave + 4 * j;
+    const bool isA = I < NA || I >= NDUP0, isZ = I == NA + NH;
+    sbase[j] = isA ? (uint64_t)(uintptr_t)apb : isZ ? (uint64_t)(uintptr_t)zb : (uint64_t)(uintptr_t)hb;
+    srb[j] = isA ? ld * 2 : isZ ? (int)a.lddz * 4 : ldhg * 4;
+    sofs[j] = isA ? 2 : 3;
+    sstr[j] = isA ? ACH : isZ ? 256 : HCH;
+    sdst[j] = isA ? OA + (I < NA ? I : I - NDUP0) * 1024 : isZ ? OZ : OH + (I - NA) * 1024;
+  }
+  const bool zwave = wave == (NA + NH) % 4;
+  auto dma = [&](int j, int c) __attribute__((always_inline)) {
+    const char* src = reinterpret_cast<const char*>(sbase[j]) + (int64_t)ldbase(min(c + sofs[j], clast)) * srb[j] + voff[j];
+    const uint32_t dst = lds0 + (uint32_t)(sdst[j] + ((c + sofs[j]) % 3) * sstr[j]);
+    if (j == (NA + NH) / 4 && zwave) glds4(src, dst);
+    else glds16(src, dst);
+  };
+  auto sync = [&]() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  const int gn = tid & 127, go = tid >> 7;
+  const bool gcol = gn < a.Nr;
+  float pcol[MAXPROJ];
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
+  // the block's G scale (as gemm_tn_h2_kernel)
+  float gsc, gunsc;
+  {
+    float zm = 0.f;
+    for (int64_t r = mbeg + tid; r < mend; r += 256) {
+      float s = 0.f;
+      for (int q = 0; q < a.nproj; ++q) s += fabsf(a.dz[r * a.lddz + q]);
+      zm = fmaxf(zm, s);
+    }
+    float pm = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXPROJ; ++q) pm = fmaxf(pm, fabsf(pcol[q]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      zm = fmaxf(zm, __shfl_xor(zm, o));
+      pm = fmaxf(pm, __shfl_xor(pm, o));
+    }
+    if (lane == 0) {
+      redm[wave] = zm;
+      redm[4 + wave] = pm;
+    }
+    __syncthreads();
+    zm = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
+    pm = fmaxf(fmaxf(redm[4], redm[5]), fmaxf(redm[6], redm[7]));
+    const float bound = zm * pm * a.hscale;
+    int E = 0;
+    if (bound > 0.f && isfinite(bound)) frexpf(bound, &E);
+    gsc = ldexpf(1.0f, 4 - E);
+    gunsc = ldexpf(1.0f, E - 4 - 11);
+  }
+  float db = 0.f, dzs = 0.f;
+  float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
+  float e[8], hv[8];
+  uint32_t w[4][3];
+  float4 zv[8];
+  float zsv[8];
+  auto hz_read = [&](int k, int i0) __attribute__((always_inline)) {
+    const int mb = ldbase(k);
+    const float* hs = reinterpret_cast<const float*>(smem + OH + (k % 3) * HCH);
+    const float* zs = reinterpret_cast<const float*>(smem + OZ + (k % 3) * 256);
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i) {
+      const int r = 8 * go + i;
+      const bool ok = r >= (int)mbeg + k * PT_ROWS - mb && r < (int)mend - mb;
+      hv[i] = hs[r * 128 + (gcol ? gn : 0)];
+      const float4 z = *reinterpret_cast<const float4*>(zs + r * MAXPROJ);
+      const float zs1 = zs[r * MAXPROJ + (gn & (MAXPROJ - 1))];
+      zv[i] = ok ? z : make_float4(0.f, 0.f, 0.f, 0.f);
+      zsv[i] = ok ? zs1 : 0.f;
+    }
+  };
+  auto g_row = [&](int i, int half) __attribute__((always_inline)) {
+    if (half == 0) {
+      const float4 z = zv[i];
+      float g = z.x * pcol[0];
+      g = fmaf(z.y, pcol[1], g);
+      g = fmaf(z.z, pcol[2], g);
+      e[i] = fmaf(z.w, pcol[3], g);
+      dw2[0] = fmaf(z.x, hv[i], dw2[0]);
+      dw2[1] = fmaf(z.y, hv[i], dw2[1]);
+      dw2[2] = fmaf(z.z, hv[i], dw2[2]);
+      dw2[3] = fmaf(z.w, hv[i], dw2[3]);
+      return;
+    }
+    dzs += gn < MAXPROJ ? zsv[i] : 0.0f;
+    const float g = hv[i] > 0.0f ? e[i] * a.hscale : 0.0f;
+    db += g;
+    e[i] = g * gsc;
+  };
+  auto split_pair = [&](int j) __attribute__((always_inline)) {
+    split_h2_pair(e[2 * j], e[2 * j + 1], w[j][1], w[j][2]);
+    w[j][0] = h2_scale_pair(w[j][1], 2048.0f);
+  };
+  auto g_put = [&](int k) __attribute__((always_inline)) {
+    uint16_t* gd = reinterpret_cast<uint16_t*>(smem + OG + (k & 1) * GCH) + gn * PT_GP + 8 * go;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      *reinterpret_cast<uint4*>(gd + p * PT_GPL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+  };
+  constexpr int U_HZ = NI, U_G = U_HZ + 4, U_S = U_G + 16, U_P = U_S + 4, NU = U_P + 1;
+  auto unit = [&](int k, int c) __attribute__((always_inline)) {
+    if (k < U_HZ) return;
+    if (LAB & 2) return;
+    else if (k < U_G) hz_read(c + 1, 2 * (k - U_HZ));
+    else if (k < U_S) g_row((k - U_G) >> 1, (k - U_G) & 1);
+    else if (k < U_P) split_pair(k - U_S);
+    else g_put(c + 1);
+  };
+
+  const int gfo = (32 * wave + (lane & 31)) * PT_GP + 8 * (lane >> 5);
+  const int grp = lane >> 4, li = lane & 15;
+  const int afo = (8 * (grp >> 1) + (li >> 2)) * PT_AP + 16 * (grp & 1) + 4 * (li & 3);
+  auto afrag = [&](const uint16_t* base, int t, int p) __attribute__((always_inline)) {
+    const uint16_t* q = base + p * PT_APL + t * 32;
+    return __builtin_bit_cast(f16x8, cat_frag(tr_read(q), tr_read(q + 4 * PT_AP)));
+  };
+#define PD_FENCE __builtin_amdgcn_sched_barrier(0)
+  auto compute = [&](int c) __attribute__((always_inline)) {
+    const uint16_t* gt = reinterpret_cast<const uint16_t*>(smem + OG + (c & 1) * GCH);
+    f16x8 gf[3], af[2][2];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) gf[p] = *reinterpret_cast<const f16x8*>(gt + p * PT_GPL + gfo);
+    const uint16_t* ab = reinterpret_cast<const uint16_t*>(smem + OA + (c % 3) * ACH) + afo;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) af[0][p] = afrag(ab, 0, p);
+    constexpr int pg[3] = {2, 1, 0}, pa[3] = {0, 1, 0};
+    static_for<KT>([&](auto tc) __attribute__((always_inline)) {
+      constexpr int t = decltype(tc)::value;
+      if constexpr (t + 1 < KT && !(LAB & 4)) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) af[(t + 1) & 1][p] = afrag(ab, t + 1, p);
+      }
+      static_for<3>([&](auto mc) __attribute__((always_inline)) {
+        constexpr int m = decltype(mc)::value;
+        PD_FENCE;
+        if constexpr (!(LAB & 1))
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gf[pg[m]], af[(LAB & 4) ? 0 : (t & 1)][pa[m]], acc[t], 0, 0, 0);
+        PD_FENCE;
+        if constexpr (3 * t + m < U_HZ) dma(3 * t + m, c);
+        else if constexpr (3 * t + m < NU) unit(3 * t + m, c);
+      });
+      PD_FENCE;
+    });
+#pragma unroll
+    for (int u = max(3 * KT, U_HZ); u < NU; ++u) unit(u, c);
+    if constexpr ((LAB & 1) != 0) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t) acc[t][0] += (float)gf[0][0] + (float)af[0][0][0] + (float)af[1][1][1];
+    }
+  };
+#undef PD_FENCE
+
+  if (nch > 0) {
+    wait_vm(std::integral_constant<int, 0>{});
+    {
+      const int mb = ldbase(0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int I = wave + 4 * j;
+        if (I == NH) glds4(zb + (int64_t)mb * a.lddz * 4 + voff0[j], lds0 + (uint32_t)OZ);
+        else glds16(hb + (int64_t)mb * ldhg * 4 + voff0[j], lds0 + (uint32_t)(OH + (I < NH ? I : I - NH - 1) * 1024));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) dma(j, -2);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) dma(j, -1);
+    wait_vm(std::integral_constant<int, 2 * NI>{});
+    sync();
+    hz_read(0, 0); hz_read(0, 2); hz_read(0, 4); hz_read(0, 6);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      g_row(i, 0);
+      g_row(i, 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_pair(j);
+    g_put(0);
+    wait_vm(std::integral_constant<int, NI>{});
+    sync();
+    for (int c = 0; c < nch; ++c) {
+      compute(c);
+      wait_vm(std::integral_constant<int, NI>{});
+      sync();
+    }
+    wait_vm(std::integral_constant<int, 0>{});
+    sync();
+  }
+
+  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
+  const int Kc = a.k1 + a.k2;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int kp = t * 32 + (lane & 31);
+    const bool s1 = kp < a.k1;
+    const bool s2 = kp >= a.ap_col2 && kp < a.ap_col2 + a.k2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int64_t idx = s1 ? (int64_t)row * a.k1 + kp : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (kp - a.ap_col2);
+      if (row < a.Nr && (s1 || s2)) slab[idx] = acc[t][r] * gunsc;
+    }
+  }
+  float* red = reinterpret_cast<float*>(smem + OA);
+  constexpr int ns = 2 + MAXPROJ;
+  red[(go * 128 + gn) * ns + 0] = db;
+  red[(go * 128 + gn) * ns + 1] = dzs;
+#pragma unroll
+  for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
+  __syncthreads();
+  if (tid < 128 && tid < a.Nr) {
+    float* side = slab + (int64_t)a.Nr * Kc;
+    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
+    for (int q = 0; q < a.nproj; ++q)
+      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+  }
+  if (tid < a.nproj)
+    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+}
+}  // namespace
+}  // namespace gnnmp
+
 #define CK(x)                                                                         \
   do {                                                                                \
     hipError_t e_ = (x);                                                              \
@@ -60,6 +375,10 @@ void tnp(const NTArgs&, const uint4*, int) {
 template <int LAB>
 void tnh(const NTArgs&, const uint4*, int) {
   gemm_tn_h2_kernel<11, false, LAB><<<256, 256>>>(g_th);
+}
+template <int LAB>
+void tnd(const NTArgs&, const uint4*, int) {
+  gemm_tn_h2_dma_kernel<11, LAB><<<256, 256>>>(g_th);
 }
 
 int main(int argc, char** argv) {
@@ -199,9 +518,10 @@ int main(int argc, char** argv) {
           ref[NR * F + n2 * F + k] += gg * hx[m * LD + 168 + k];
         }
       }
-    auto run = [&](const char* name, bool h2) {
+    auto run = [&](const char* name, int h2) {
       CK(hipMemset(slab, 0, nblk * stride * 4));
-      if (h2) gemm_tn_h2_kernel<11, false, 0><<<nblk, 256>>>(ha);
+      if (h2 == 2) gemm_tn_h2_dma_kernel<11, 0><<<nblk, 256>>>(ha);
+      else if (h2) gemm_tn_h2_kernel<11, false, 0><<<nblk, 256>>>(ha);
       else gemm_tn_planes_kernel<true, true, 11, false, 0><<<nblk, 256>>>(pa);
       CK(hipDeviceSynchronize());
       std::vector<float> hs(nblk * stride);
@@ -215,8 +535,9 @@ int main(int argc, char** argv) {
       }
       std::printf("TN %s: dW relL2 vs f64 %.3g\n", name, std::sqrt(e / nn));
     };
-    run("split-bf16 planes", false);
-    run("half-pair", true);
+    run("split-bf16 planes", 0);
+    run("half-pair", 1);
+    run("half-pair dma", 2);
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -229,7 +550,8 @@ int main(int argc, char** argv) {
       {"NT half-pair MFMA only", nth<2 | 4>, {}}, {"NT half-pair no MFMA", nth<1>, {}},
       {"NT half-pair no dropout", nth<0, EPIN>, {}},
       {"TN planes (bf16 x6)", tnp<0>, {}}, {"TN planes MFMA only", tnp<2 | 8>, {}},
-      {"TN half-pair", tnh<0>, {}}, {"TN half-pair no staging", tnh<2>, {}}, {"TN half-pair no MFMA", tnh<1>, {}}};
+      {"TN half-pair", tnh<0>, {}}, {"TN half-pair no staging", tnh<2>, {}}, {"TN half-pair no MFMA", tnh<1>, {}},
+      {"TN half-pair dma", tnd<0>, {}}, {"TN half-pair dma no MFMA", tnd<1>, {}}, {"TN half-pair dma no G", tnd<2>, {}}};
   for (int r = 0; r < rounds; ++r)
     for (auto& v : vs) {
       v.f(n, bimg, ntiles);
