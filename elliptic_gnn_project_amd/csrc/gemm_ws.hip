@@ -1400,12 +1400,13 @@ bool nt_planes_ok(const NTArgs& a) {
   return true;
 }
 
-// The half-pair form: f32 C, the w1/w2 B form, a 336-wide half-pair image row (21 k-steps: the
-// SAGE layer-1 [agg | x]), 1 <= N <= 128 with N % 4 == 0, M >= 32, the nt_ws_ok epilogues.
+// The half-pair form: f32 C, the w1/w2 B form, a half-pair image row of 336 (21 k-steps: the
+// SAGE layer-1 [agg | x]) or 176 (11: one input, the GCN / GAT layer-1 x), 1 <= N <= 128 with
+// N % 4 == 0, M >= 32, the nt_ws_ok epilogues.
 bool nt_h2_ok(const NTArgs& a) {
   if (!a.ap || !a.ap_h2 || a.a_bf16 || a.c_bf16 || !a.w1 || (a.k2 > 0 && !a.w2) || a.Nc > BN || a.Nc < 1) return false;
   auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  if (a.ap_ld != 336 || !al(a.ap) || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld)
+  if ((a.ap_ld != 336 && a.ap_ld != 176) || !al(a.ap) || a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld)
     return false;
   if (a.ap_ps < a.M * (int64_t)a.ap_ld || 2 * a.ap_ps * 2 >= ((int64_t)1 << 31)) return false;
   if (a.c && (!al(a.c) || a.ldc % 4 != 0 || a.M * a.ldc * 4 >= ((int64_t)1 << 31))) return false;
@@ -1416,9 +1417,9 @@ bool nt_h2_ok(const NTArgs& a) {
   return true;
 }
 
-// workspace: the B image (21 k-steps x 3 planes x 256 slots x 16 B), then the 128 column scales
-void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st) {
-  constexpr int NKS = 21;
+// workspace: the B image (NKS k-steps x 3 planes x 256 slots x 16 B), then the 128 column scales
+template <int NKS>
+void launch_nt_h2_k(const NTArgs& a, uint4* img, hipStream_t st) {
   float* colscale = reinterpret_cast<float*>(img + NKS * 3 * 256);
   ws_prep_h2_kernel<<<NKS, 256, 0, st>>>(a, img, colscale, a.ap_col2);
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
@@ -1434,6 +1435,11 @@ void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st) {
   else if (bias) GNN_NH(WS_BIAS);
   else GNN_NH(0);
 #undef GNN_NH
+}
+
+void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st) {
+  if (a.ap_ld == 176) launch_nt_h2_k<11>(a, img, st);
+  else launch_nt_h2_k<21>(a, img, st);
 }
 
 // The bf16 image form: bf16 A image (one plane, ld 256 or 336), bf16 C, the w1/w2 B form,

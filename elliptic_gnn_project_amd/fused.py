@@ -206,6 +206,10 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
 def gemm_nt_input(x: torch.Tensor, n: int, **kw):
     """gemm_nt(x, None, n, **kw) (w1 form, no a2) for a layer whose A operand is the model input x:
     on the split-image NT over x's cached planes (planes.x_only_image) when it takes the shape."""
+    if _H2:  # the half-pair image (3 products) when x fits it
+        im = x_only_image(x, HalfPairImage)
+        if im is not None and gemm_nt(None, None, n, planes=im, check_planes=True, **kw):
+            return gemm_nt(None, None, n, planes=im, **kw)
     im = x_only_image(x)
     if im is not None and gemm_nt(None, None, n, planes=im, check_planes=True, **kw):
         return gemm_nt(None, None, n, planes=im, **kw)

@@ -178,28 +178,32 @@ def register_input(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
-def x_only_image(x: torch.Tensor):
+def x_only_image(x: torch.Tensor, cls=SplitImage):
     """The cached split image of a registered input x alone (x in columns [0, F), k2 = 0) for the
     GEMMs of a layer whose A operand is x (GCN / GAT layer 1: y = x·Wᵀ and dW = Gᵀ·x), or None.
+    cls: SplitImage (split-bf16, both GEMMs) or HalfPairImage (the forward NT; x must fit it).
 
     Built on first use (one split pass) and reused while x is unmodified (data_ptr, _version);
     every call over a registered x takes the same kernels, so repeated forwards are bit-identical."""
     if (not getattr(x, _CONST, False) or x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1
             or not x.is_cuda or x.requires_grad or x.size(0) < 32 or x.size(1) > 328):
         return None
+    if cls is HalfPairImage and not h2_ok(x):
+        return None
     key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
-    im = getattr(x, _ATTR_X, None)
+    attr = _ATTR_X if cls is SplitImage else _ATTR_X + "_h2"
+    im = getattr(x, attr, None)
     if im is None or im.n != x.size(0) or im.k1 != x.size(1):
-        if not SplitImage.addressable(x.size(0), x.size(1), 0):  # checked before allocating
+        if not cls.addressable(x.size(0), x.size(1), 0):  # checked before allocating
             return None
-        im = SplitImage(x.size(0), x.size(1), 0, x.device)
+        im = cls(x.size(0), x.size(1), 0, x.device)
         try:
-            setattr(x, _ATTR_X, im)
+            setattr(x, attr, im)
         except (AttributeError, RuntimeError):  # e.g. inference tensors: not cached, still used
             pass
     if im.x_key != key:
         with torch.cuda.device(x.device):
-            _lib.call("gnn_split_planes_f32", x.data_ptr(), int(x.stride(0)), im.n, im.k1, im.ptr, im.ld, im.ps,
+            _lib.call(cls._split_fn, x.data_ptr(), int(x.stride(0)), im.n, im.k1, im.ptr, im.ld, im.ps,
                       0, im.ld, _lib.stream_handle(x.device))
         im.x_key = key
     return im

@@ -251,3 +251,26 @@ def test_k1_keep_bits_equal_the_dropout_hash(device, use_ptr):
     got = kb.cpu().numpy().view(np.uint32)
     bits = (got[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1
     assert np.array_equal(bits.reshape(x.size(0), 128).astype(bool), want)
+
+
+@pytest.mark.parametrize("F,n,bias", [(166, 64, True), (166, 128, False), (40, 16, True)])
+def test_input_nt_h2(device, F, n, bias):
+    """y = x·Wᵀ (+ b) for a registered model input (GCN / GAT layer 1) on x's half-pair image
+    (176-wide rows): within relL2 1e-6 of float64, and equal to the split-bf16 image's result
+    within 1e-5."""
+    from elliptic_gnn_project_amd.fused import gemm_nt, gemm_nt_input
+    from elliptic_gnn_project_amd.planes import HalfPairImage, register_input, x_only_image
+
+    M = 20000
+    g = torch.Generator().manual_seed(F + n)
+    x = register_input(torch.randn(M, F, generator=g).to(device))
+    w = torch.randn(n, F, generator=g) * 0.1
+    b = torch.randn(n, generator=g) if bias else None
+    kw = dict(w1=w.to(device), bias=b.to(device) if bias else None)
+    y = gemm_nt_input(x, n, **kw)
+    assert getattr(x, "_gnnmp_split_image_x_h2", None) is not None
+    ref = x.double().cpu() @ w.double().t() + (b.double() if bias else 0.0)
+    assert rel_l2(y, ref) < 1e-6
+    im = x_only_image(x)
+    y2 = gemm_nt(None, None, n, planes=im, **kw)
+    torch.testing.assert_close(y.cpu(), y2.cpu(), rtol=1e-5, atol=1e-5)
