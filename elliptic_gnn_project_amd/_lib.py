@@ -140,7 +140,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("math", c_i32),
         ("a_dtype", c_i32), ("h_dtype", c_i32),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
-        ("planes_format", c_i32),
+        ("planes_format", c_i32), ("g_dtype", c_i32),
     ]
 
 

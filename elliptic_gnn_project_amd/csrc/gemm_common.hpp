@@ -171,6 +171,7 @@ struct TNArgs {
   int32_t want_db;
   int32_t a_bf16;  // A1/A2 hold bf16
   int32_t h_bf16;  // h holds bf16
+  int32_t g_bf16;  // g (input) and gout (output) hold bf16 (the bf16-image TN)
   const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;  // split image of [A1 | A2] (as NTArgs)
   int32_t ap_h2;  // half-pair image (2 f16 planes)
 };

@@ -919,8 +919,12 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   const bool proj = a.dz != nullptr, mask = a.h != nullptr;
   a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16;
   a.h_bf16 = p->h_dtype == GNN_DTYPE_BF16;
-  if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->h_dtype != GNN_DTYPE_F32 && p->h_dtype != GNN_DTYPE_BF16))
+  a.g_bf16 = p->g_dtype == GNN_DTYPE_BF16;
+  if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->h_dtype != GNN_DTYPE_F32 && p->h_dtype != GNN_DTYPE_BF16) ||
+      (p->g_dtype != GNN_DTYPE_F32 && p->g_dtype != GNN_DTYPE_BF16))
     return fail(GNN_ERR_INVALID_ARG, __fn, "bad dtype");
+  if (a.g_bf16 && !(p->a_planes && a.a_bf16))
+    return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 g / gout need the bf16-image TN (a bf16 a_planes)");
   if (a.h_bf16 && !a.a_bf16) return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 h needs bf16 A");
   // widest row pitch of any operand (the split kernel uses 32-bit element offsets)
   const int64_t ldmax = std::max({a.lda1, a.k2 > 0 ? a.lda2 : 0, a.h ? a.ldh : 0, a.g ? a.ldg : 0, a.dz ? a.lddz : 0});
@@ -1018,6 +1022,7 @@ extern "C" int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p) {
   a.M = p->M; a.Nr = (int32_t)p->Nr; a.g = p->g; a.ldg = p->ldg; a.dz = p->dz; a.lddz = p->lddz;
   a.h = p->h; a.ldh = p->ldh; a.k1 = (int32_t)p->k1; a.k2 = (int32_t)p->k2;
   a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16; a.h_bf16 = p->h_dtype == GNN_DTYPE_BF16;
+  a.g_bf16 = p->g_dtype == GNN_DTYPE_BF16;
   a.ap = static_cast<const uint16_t*>(p->a_planes);
   a.ap_ld = (int32_t)std::min<int64_t>(p->planes_ld, INT32_MAX);
   a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);

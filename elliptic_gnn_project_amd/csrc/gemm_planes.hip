@@ -735,7 +735,9 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
 //            | the slot refilled with chunk c+1+D | dz(c+2) -> the LDS dz ring, its slot refilled
 //            with dz(c+2+D) | the KT MFMAs of chunk c | barrier
 // Geometry, the G formation, masks, side sums and slab layout are the split-image kernel's above.
-template <bool PROJ, bool MASK, int KT, bool GOUT, int D>
+// GB: g (the g form's input) and gout are bf16 rows — the bf16-storage backward keeps the hidden
+// layers' input gradients in bf16 (autocast's rounding points: G and dh stored bf16).
+template <bool PROJ, bool MASK, int KT, bool GOUT, int D, bool GB = false>
 __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
   constexpr int NPA = 3;  // A pieces per thread per chunk (16 rows x <= 42 pieces <= 768)
   __shared__ __attribute__((aligned(16))) uint16_t Gt[2][PT_GPL];
@@ -776,6 +778,7 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
   const int n0c = gcol ? n0 : 0;
   const uint16_t* hbase = reinterpret_cast<const uint16_t*>(a.h) + n0c;
   const float* gbase = a.g + n0c;
+  const uint16_t* gbase16 = reinterpret_cast<const uint16_t*>(a.g) + n0c;
   const int zr = (tid & 63) / MAXPROJ, zq = (tid & 63) % MAXPROJ;
   const int zqc = PROJ ? min(zq, a.nproj - 1) : 0;
   float pcol[4][MAXPROJ];
@@ -791,6 +794,7 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
   u32x4 ra[D][NPA];
   uint2 rh[D][2];
   float4 rg[D][2];
+  uint2 rgb[D][2];
   float rz[D];
   auto load_chunk = [&](int d, int c) {  // c clamped by the caller
     const int mb = ldbase(c);
@@ -800,7 +804,8 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
     for (int i = 0; i < 2; ++i) {
       const uint32_t row = (uint32_t)(mb + 2 * rp + i);
       if constexpr (MASK) rh[d][i] = *reinterpret_cast<const uint2*>(hbase + row * (uint32_t)a.ldh);
-      if constexpr (!PROJ) rg[d][i] = *reinterpret_cast<const float4*>(gbase + row * (uint32_t)a.ldg);
+      if constexpr (!PROJ && GB) rgb[d][i] = *reinterpret_cast<const uint2*>(gbase16 + row * (uint32_t)a.ldg);
+      else if constexpr (!PROJ) rg[d][i] = *reinterpret_cast<const float4*>(gbase + row * (uint32_t)a.ldg);
     }
   };
   auto load_z = [&](int d, int c) {
@@ -860,6 +865,9 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
             dw2[j][2] = fmaf(z.z, hv[j], dw2[j][2]);
             dw2[j][3] = fmaf(z.w, hv[j], dw2[j][3]);
           }
+        } else if constexpr (GB) {
+          const uint32_t wd = j < 2 ? rgb[d][i].x : rgb[d][i].y;
+          e = __uint_as_float((j & 1) ? (wd & 0xffff0000u) : (wd << 16));
         } else {
           e = j == 0 ? rg[d][i].x : j == 1 ? rg[d][i].y : j == 2 ? rg[d][i].z : rg[d][i].w;
         }
@@ -869,7 +877,12 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
         db[j] += g;
         gv[i][j] = g;
       }
-      if constexpr (GOUT) {
+      if constexpr (GOUT && GB) {  // the rounded G the MFMA uses, as bf16 rows
+        if (a.gout && ok)
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.gout) + (int64_t)(mb + r) * a.ldgout + n0) = make_uint2(
+              __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v_t){gv[i][0], gv[i][1]}, bf16x2v_t)),
+              __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v_t){gv[i][2], gv[i][3]}, bf16x2v_t)));
+      } else if constexpr (GOUT) {
         if (a.gout && ok)
           *reinterpret_cast<float4*>(a.gout + (int64_t)(mb + r) * a.ldgout + n0) =
               make_float4(gv[i][0], gv[i][1], gv[i][2], gv[i][3]);
@@ -984,6 +997,11 @@ __global__ __launch_bounds__(256) void gemm_tn_img16_kernel(TNArgs a) {
 
 template <bool PROJ, bool MASK, int KT>
 void launch_tn_img16_k(const TNArgs& a, int nblk, hipStream_t st) {
+  if (a.g_bf16) {
+    if (a.gout) gemm_tn_img16_kernel<PROJ, MASK, KT, true, 4, true><<<nblk, 256, 0, st>>>(a);
+    else gemm_tn_img16_kernel<PROJ, MASK, KT, false, 4, true><<<nblk, 256, 0, st>>>(a);
+    return;
+  }
   if (a.gout) gemm_tn_img16_kernel<PROJ, MASK, KT, true, 4><<<nblk, 256, 0, st>>>(a);
   else gemm_tn_img16_kernel<PROJ, MASK, KT, false, 4><<<nblk, 256, 0, st>>>(a);
 }
@@ -1024,10 +1042,11 @@ void launch_tn_planes_kt(const TNArgs& a, int nblk, hipStream_t st) {
 // the bf16 image form: one-plane bf16 image (ld 256 or 336), h bf16 when given
 bool tn_img16_ok(const TNArgs& a) {
   if (!a.ap || a.ap_h2 || !a.a_bf16 || (a.h && !a.h_bf16)) return false;
-  // the G slot's vector accesses: 4 columns per row (8-byte h, 16-byte g / gout rows)
+  // the G slot's vector accesses: 4 columns per row (8-byte h, 16-byte f32 / 8-byte bf16 g and gout rows)
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
-  if (a.Nr % 4 || (a.h && (a.ldh % 4 || !al(a.h, 8))) || (a.g && !a.dz && (a.ldg % 4 || !al(a.g, 16))) ||
-      (a.gout && (a.ldgout % 4 || !al(a.gout, 16))))
+  const int gb = a.g_bf16 ? 8 : 16;
+  if (a.Nr % 4 || (a.h && (a.ldh % 4 || !al(a.h, 8))) || (a.g && !a.dz && (a.ldg % 4 || !al(a.g, gb))) ||
+      (a.gout && (a.ldgout % 4 || !al(a.gout, gb))))
     return false;
   if ((a.ap_ld != 256 && a.ap_ld != 336) || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;
   if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
@@ -1043,7 +1062,7 @@ void launch_tn_img16(const TNArgs& a, int nblk, hipStream_t st) {
 
 // the half-pair form: dz form with the h mask (the SAGE hidden layer), f32 h, 336-wide image rows
 bool tn_h2_ok(const TNArgs& a) {
-  if (!a.ap || !a.ap_h2 || a.a_bf16 || a.h_bf16 || !a.dz || !a.proj || !a.h || a.nproj < 1) return false;
+  if (!a.ap || !a.ap_h2 || a.a_bf16 || a.h_bf16 || a.g_bf16 || !a.dz || !a.proj || !a.h || a.nproj < 1) return false;
   if (a.ap_ld != 336 || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;
   if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
   if (a.ap_ps < a.M * (int64_t)a.ap_ld || 2 * a.ap_ps * 2 >= ((int64_t)1 << 31) || a.M < PT_ROWS) return false;
@@ -1057,7 +1076,7 @@ void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st) {
 }
 
 bool tn_planes_ok(const TNArgs& a) {
-  if (!a.ap || a.ap_h2 || a.a_bf16 || a.h_bf16) return false;
+  if (!a.ap || a.ap_h2 || a.a_bf16 || a.h_bf16 || a.g_bf16) return false;
   if (a.ap_ld % 16 || a.ap_ld > PT_MAXLD || a.ap_ld < 32) return false;
   if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
   if (a.ap_ps < a.M * (int64_t)a.ap_ld || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;

@@ -170,6 +170,7 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         _lib.DTYPE_BF16 if bf else _lib.DTYPE_F32,
         _lib.DTYPE_BF16 if (h is not None and h.dtype == torch.bfloat16) else _lib.DTYPE_F32,
         *_planes_fields(planes),
+        _lib.DTYPE_BF16 if any(t is not None and t.dtype == torch.bfloat16 for t in (g, gout)) else _lib.DTYPE_F32,
     )
     if check_planes:
         return bool(_lib.load().gnn_gemm_tn_planes_ok(p))
@@ -355,9 +356,18 @@ class _FusedSAGE(torch.autograd.Function):
         for l in range(L - 2, -1, -1):
             fo, fi = Wl[l].shape
             need_g = l > 0 or need_x
-            gout = torch.empty((N, fo), dtype=torch.float32, device=dz.device) if need_g else None
-            a_l, im = aggs[l], None
             bim = ctx.bimgs[l]
+            # bf16 storage: G and the input gradient dh stay bf16 between the layers (autocast's
+            # rounding points): the TN writes the rounded G into the right half of a [meanᵀ(G) | G]
+            # bf16 image, whose left half the bf16 transposed aggregation fills; dh is then ONE
+            # one-product bf16 image NT.  (Needs fo <= 128 and fi <= 128 with the image's widths.)
+            gimg = None
+            if bim is not None and need_g and fi <= 128 and 8 <= fi and fi % 8 == 0 and 2 * fo in (256,) and _BF_IMAGE:
+                gimg = BfImage(N, fo, fo, dz.device)
+                gout = gimg.a2
+            else:
+                gout = torch.empty((N, fo), dtype=torch.float32, device=dz.device) if need_g else None
+            a_l, im = aggs[l], None
             if bim is not None:  # bf16 storage: the TN reads the layer's bf16 image
                 tn_kw = dict(dz=dz, proj=P) if l == L - 2 else dict(g=g)
                 if gemm_tn(fo, None, None, h=hs[l + 1], hscale=hscale, gout=gout, planes=bim, check_planes=True,
@@ -382,7 +392,11 @@ class _FusedSAGE(torch.autograd.Function):
             grads[3 * l + 0] = dW[0]
             grads[3 * l + 1] = db
             grads[3 * l + 2] = dW[1]
-            if need_g and fi <= 128:
+            if gimg is not None:
+                aggregate(plan, gout, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=gimg.a1)
+                g = gemm_nt(None, None, fi, planes=gimg, w1=Wl[l].t().contiguous(), w2=Wr[l].t().contiguous(),
+                            out=torch.empty((N, fi), dtype=torch.bfloat16, device=dz.device))
+            elif need_g and fi <= 128:
                 # dh_l = meanᵀ(G · W_l) + G · W_r = [meanᵀ(G) | G] · [W_l; W_r]  (G = dL/dpre_{l+1}):
                 # reassociated so one transposed aggregation of G (width fo) and ONE GEMM
                 # (K = 2·fo, split-bf16, W read as the [fi, fo] transposes) replace two GEMMs

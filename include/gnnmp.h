@@ -390,6 +390,8 @@ typedef struct {
   int64_t planes_ld, planes_stride, planes_col2;
   int32_t planes_format;                 /* gnn_planes_format (HALF_PAIR: the dz form with h, 336-wide
                                             rows; G scaled per row block by a power of two, 3 products) */
+  int32_t g_dtype;                       /* gnn_dtype of g and gout (BF16: the bf16-image TN only; gout
+                                            then holds the bf16-rounded G its MFMAs use) */
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).

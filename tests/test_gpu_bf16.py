@@ -120,15 +120,17 @@ def _ref_sage_bf16(params, x_bf, ei, N, layers):
 
 
 def _ref_sage_bf16_grads(params, saved, dlogits, ei, N, layers):
-    """Backward of _ref_sage_bf16 in float64 with the kernels' one backward rounding point: the
-    TN's MFMA operand G = dL/dpre (f32 in the kernel) is rounded to bf16 for the weight gradients;
-    db = ΣG and the input gradients dh = [meanᵀ(G) | G]·[W_l; W_r] use G and the f32 weights
-    unrounded (split-bf16 NT), as fused._FusedSAGE.backward does."""
+    """Backward of _ref_sage_bf16 in float64 with the kernels' backward rounding points (bf16
+    storage keeps the hidden layers' gradients in bf16, as autocast would): the TN's MFMA operand
+    G = dL/dpre is rounded to bf16 for the weight gradients and stored so (gout); meanᵀ of the
+    stored G is rounded to bf16 (the bf16 aggregation); dh = [meanᵀ(G) | G]·[W_l; W_r] runs with
+    bf16-rounded weights and is stored bf16 (the one-product bf16 image NT); db = ΣG sums the
+    unrounded G of the top hidden layer (formed in f32 from dz) and the bf16 G below it."""
     P = {k: v.double() for k, v in params.items()}
     deg = torch.bincount(ei[1], minlength=N).double().clamp_min(1.0)
 
     def mean_t(g):  # meanᵀ: dst-row gradient / in-degree, summed onto the sources
-        return torch.zeros(N, g.size(1), dtype=g.dtype).index_add_(0, ei[0], (g / deg[:, None])[ei[1]])
+        return torch.zeros(N, g.size(1), dtype=g.dtype, device=g.device).index_add_(0, ei[0], (g / deg[:, None])[ei[1]])
 
     out = {}
     l = layers - 1
@@ -142,10 +144,12 @@ def _ref_sage_bf16_grads(params, saved, dlogits, ei, N, layers):
     for l in range(layers - 2, -1, -1):
         agg, hin = saved[l]
         G = dh * (saved[l + 1][1] > 0).double()
-        out[f"convs.{l}.lin_l.weight"] = rb(G).t() @ agg
-        out[f"convs.{l}.lin_r.weight"] = rb(G).t() @ hin
+        Gb = rb(G)
+        out[f"convs.{l}.lin_l.weight"] = Gb.t() @ agg
+        out[f"convs.{l}.lin_r.weight"] = Gb.t() @ hin
         out[f"convs.{l}.lin_l.bias"] = G.sum(0)
-        dh = mean_t(G) @ P[f"convs.{l}.lin_l.weight"] + G @ P[f"convs.{l}.lin_r.weight"]
+        if l > 0:
+            dh = rb(rb(mean_t(Gb)) @ rb(P[f"convs.{l}.lin_l.weight"]) + Gb @ rb(P[f"convs.{l}.lin_r.weight"]))
     return out
 
 

@@ -115,7 +115,7 @@ STRUCTS = {
     "gnn_gemm_tn_params": ("GnnGemmTNParams", ["M", "Nr", "g", "ldg", "dz", "lddz", "proj", "nproj", "h", "ldh",
                                                "hscale", "gout", "ldgout", "a1", "lda1", "k1", "a2", "lda2", "k2",
                                                "math", "a_dtype", "h_dtype", "a_planes", "planes_ld",
-                                               "planes_stride", "planes_col2", "planes_format"]),
+                                               "planes_stride", "planes_col2", "planes_format", "g_dtype"]),
 }
 
 
