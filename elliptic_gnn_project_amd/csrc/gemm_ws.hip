@@ -943,8 +943,9 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
 #define NTH_FENCE __builtin_amdgcn_sched_barrier(0)
   auto kloop = [&](const char* cur, char* nxt, floatx16& c1, const floatx16& p1, int t, int tp, uint32_t& mkl,
                    uint32_t mkp) __attribute__((always_inline)) {
-    mku = mkp;       // E1 of tile tp reads its keep bits
-    load_mk(mkl, t);  // and tile t's are loaded for its E1 one tile later
+    mku = mkp;  // E1 of tile tp reads its keep bits
+    uint32_t mkraw = 0u;
+    load_mk(mkraw, t);  // tile t's, for its E1 one tile later
     f16x8 x[2];
     auto frag = [&](int s, int p) __attribute__((always_inline)) { return *reinterpret_cast<const f16x8*>(cur + p * PLB + s * WS_KSB + foff); };
     x[0] = frag(0, 0);
@@ -968,6 +969,12 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
       slot(std::integral_constant<int, 3 * s + 2>{}, nxt, p1, tp, t);
     });
     NTH_FENCE;
+    if constexpr ((EPI & WS_KMASK) != 0) {
+      // consume the keep-bit load HERE, at the end of the chain that issued it: the wait hipcc
+      // places before this copy counts only the loads issued after it (landed long since); a
+      // first use in the next tile's E1 made it wait for the A prefetches issued in between
+      asm volatile("v_mov_b32 %0, %1" : "=v"(mkl) : "v"(mkraw));
+    }
     if constexpr ((LAB & 1) != 0) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) c1[r] = (float)x[0][r & 7];

@@ -38,6 +38,9 @@ _PLANES = os.environ.get("GNNMP_PLANES", "1") != "0"
 # The 2-layer SAGE's layer-1 operand as a half-pair image (f16 hi / lo planes, 3 products: include/
 # gnnmp.h gnn_split_h2_f32) rather than the split-bf16 one; GNNMP_H2=0 keeps split-bf16 (A/B).
 _H2 = os.environ.get("GNNMP_H2", "1") != "0"
+# K1 writes the half-pair NT's dropout keep bits (the NT then skips the hash); GNNMP_KEEP_MASK=0
+# hashes in the NT epilogue instead (A/B)
+_KEEP_MASK = os.environ.get("GNNMP_KEEP_MASK", "1") != "0"
 
 MAX_PROJ = 4  # nproj = 2 * num_classes <= 4
 
@@ -308,7 +311,7 @@ class _FusedSAGE(torch.autograd.Function):
             im = _layer0_image(h, Wl[0].size(0), nt_kw, h2=last_hidden) if l == 0 else None
             if im is not None:  # agg written straight into the split image by K1; A staged as planes
                 keep = None
-                if isinstance(im, HalfPairImage) and train_drop > 0:  # K1 also writes the NT's keep bits
+                if isinstance(im, HalfPairImage) and train_drop > 0 and _KEEP_MASK:  # K1 also writes the NT's keep bits
                     kb = im.keep_buffer()
                     keep = (kb, Wl[l].size(0), train_drop, seeds[l], seed_ctr)
                     nt_kw = dict(nt_kw, keep_mask=kb)

@@ -47,13 +47,15 @@ class SplitImage:
         return col2, (col2 + _pad8(k2) + 15) // 16 * 16
 
     @classmethod
-    def addressable(cls, n: int, k1: int, k2: int) -> bool:
+    def addressable(cls, n: int, k1: int, k2: int, ld: int | None = None) -> bool:
         """The kernels address the planes with 31-bit byte offsets."""
-        return cls.nplanes * int(n) * SplitImage.layout(k1, k2)[1] * 2 < 2 ** 31
+        return cls.nplanes * int(n) * max(SplitImage.layout(k1, k2)[1], ld or 0) * 2 < 2 ** 31
 
-    def __init__(self, n: int, k1: int, k2: int, device: torch.device):
+    def __init__(self, n: int, k1: int, k2: int, device: torch.device, ld: int | None = None):
         self.n, self.k1, self.k2 = int(n), int(k1), int(k2)
         self.col2, self.ld = self.layout(k1, k2)
+        if ld is not None:  # a wider row (zeros past the operand): the kernels' fixed image widths
+            self.ld = max(self.ld, int(ld))
         self.ps = self.n * self.ld
         dt = torch.bfloat16 if self.nplanes == 3 else torch.float16
         self.img = torch.empty((self.nplanes, self.n, self.ld), dtype=dt, device=device)
@@ -178,6 +180,9 @@ def register_input(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+X_ONLY_LD = 176
+
+
 def x_only_image(x: torch.Tensor, cls=SplitImage):
     """The cached split image of a registered input x alone (x in columns [0, F), k2 = 0) for the
     GEMMs of a layer whose A operand is x (GCN / GAT layer 1: y = x·Wᵀ and dW = Gᵀ·x), or None.
@@ -193,10 +198,12 @@ def x_only_image(x: torch.Tensor, cls=SplitImage):
     key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
     attr = _ATTR_X if cls is SplitImage else _ATTR_X + "_h2"
     im = getattr(x, attr, None)
+    # rows of 176 (the input GEMMs' image width) for any x of <= 176 columns, zeros past x
+    ld = X_ONLY_LD if x.size(1) <= X_ONLY_LD else None
     if im is None or im.n != x.size(0) or im.k1 != x.size(1):
-        if not cls.addressable(x.size(0), x.size(1), 0):  # checked before allocating
+        if not cls.addressable(x.size(0), x.size(1), 0, ld):  # checked before allocating
             return None
-        im = cls(x.size(0), x.size(1), 0, x.device)
+        im = cls(x.size(0), x.size(1), 0, x.device, ld)
         try:
             setattr(x, attr, im)
         except (AttributeError, RuntimeError):  # e.g. inference tensors: not cached, still used

@@ -62,7 +62,7 @@ def test_split_h2_bit_exact(device):
     assert np.array_equal(got[1][:, 168:334], lo)
     assert not got[0][:, 334:].any() and not got[1][:, 334:].any()
     # hi + 2^-11 lo reproduces v to 2^-22 relative
-    rec = got[0][:, 168:334].view(np.float16).astype(np.float64) + got[1][:, 168:334].view(np.float16) / 2048.0
+    rec = got[0][:, 168:334].view(np.float16).astype(np.float64) + got[1][:, 168:334].view(np.float16).astype(np.float64) / 2048.0
     xd = x.double().numpy()
     assert np.all(np.abs(rec - xd) <= 2.0 ** -22 * np.abs(xd) + 2.0 ** -36)
 

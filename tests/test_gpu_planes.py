@@ -210,6 +210,7 @@ def test_fused_sage_planes_on_off(device, n, e):
     torch.manual_seed(3)
     model = SAGENet(x.size(1), 128, layers=2, dropout=0.5).to(device).train()
     res = []
+    fused._H2 = False  # the split-bf16 image (the half-pair one: tests/test_gpu_h2.py)
     for on in (True, False):
         fused._PLANES = on
         try:
@@ -219,11 +220,13 @@ def test_fused_sage_planes_on_off(device, n, e):
             res.append((out.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()}))
         finally:
             fused._PLANES = True
+            fused._H2 = True
     (o1, g1), (o2, g2) = res
     torch.testing.assert_close(o1, o2, rtol=1e-5, atol=1e-5)
     for k in g1:
         assert rel_l2(g1[k], g2[k]) < 1e-5, k
-    assert getattr(x, "_gnnmp_split_image", None) is not None  # the planes path ran
+    assert any(getattr(x, a, None) is not None  # the planes path ran (half-pair or split-bf16 image)
+               for a in ("_gnnmp_split_image", "_gnnmp_split_image_h2"))
 
 
 def test_two_forwards_then_backward(device):
@@ -247,7 +250,8 @@ def test_two_forwards_then_backward(device):
     loss_a.backward()
     for k, p in model.named_parameters():
         assert torch.equal(p.grad, ref[k]), k
-    assert getattr(x, "_gnnmp_split_image", None) is not None  # the planes path ran
+    assert any(getattr(x, a, None) is not None  # the planes path ran (half-pair or split-bf16 image)
+               for a in ("_gnnmp_split_image", "_gnnmp_split_image_h2"))
 
 
 def test_unregistered_input_builds_no_image(device):
@@ -266,8 +270,8 @@ def test_unregistered_input_builds_no_image(device):
         out, loss = _sage_step(model, inp, ei, 2)
         loss.backward()
         outs.append((out.detach(), {k: p.grad.clone() for k, p in model.named_parameters()}))
-    assert getattr(x, "_gnnmp_split_image", None) is not None
-    assert getattr(xu, "_gnnmp_split_image", None) is None
+    assert any(getattr(x, a, None) is not None for a in ("_gnnmp_split_image", "_gnnmp_split_image_h2"))
+    assert all(getattr(xu, a, None) is None for a in ("_gnnmp_split_image", "_gnnmp_split_image_h2"))
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-5)
     for k in outs[0][1]:
         assert rel_l2(outs[0][1][k], outs[1][1][k]) < 1e-5, k
