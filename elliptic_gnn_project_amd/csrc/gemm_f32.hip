@@ -849,7 +849,9 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
 
 extern "C" gnn_status gnn_gemm_nt_workspace_size(int64_t N, int64_t k1, int64_t k2, size_t* bytes) {
   if (!bytes || N < 1 || k1 < 1 || k2 < 0) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
-  *bytes = N <= BN ? nt_x3_workspace(k1, k2) : 0;
+  // the image-A kernels (a_planes) size their B image by the image's row width (<= 336 columns,
+  // 21 k-steps), not by k1 + k2: a narrow input on a 176-wide image runs 11 k-steps
+  *bytes = N <= BN ? std::max(nt_x3_workspace(k1, k2), (size_t)21 * 3 * 256 * 16 + BN * sizeof(float)) : 0;
   return GNN_OK;
 }
 

@@ -1029,33 +1029,56 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
 // B image of the half-pair NT: per k-step s, plane p (hi' = 2^11 hi, hi, lo), slot 2n + khalf:
 // the 8 halves of column n, k = 16s + 8·khalf .. +8, of w_n · 2^-e_n, where 2^-e_n brings the
 // column's largest |w| into [8, 16) (a power of two: exact); colscale[n] = 2^(e_n - 11) (block 0).
-// Every block computes all column exponents (max |w_n| over the whole K, 2 threads per column).
+// Every block computes all column exponents (max |w_n| over the whole K): 16 waves, 8 columns
+// each, a wave's lanes across k so the loads coalesce and all of them (8 columns x 2 segments x
+// <= 6 per lane, K <= 336) are in flight at once -- one round trip instead of a per-thread walk
+// down the row (the first form spent ~33 us here on dependent load latency).
 __device__ __forceinline__ float h2_col_exp2(float m) {  // 2^e with m · 2^-e in [8, 16); 1 for m = 0
   if (!(m > 0.f) || !isfinite(m)) return 1.0f;
   int E;
   frexpf(m, &E);  // m in [2^(E-1), 2^E)
   return ldexpf(1.0f, E - 4);
 }
-__global__ __launch_bounds__(256) void ws_prep_h2_kernel(NTArgs a, uint4* __restrict__ img, float* __restrict__ colscale,
-                                                         int col2) {
+constexpr int WS_PREP_THREADS = 1024;
+__global__ __launch_bounds__(WS_PREP_THREADS) void ws_prep_h2_kernel(NTArgs a, uint4* __restrict__ img,
+                                                                     float* __restrict__ colscale, int col2) {
   __shared__ float sc[BN];
   const int tid = threadIdx.x;
   {
-    const int n = tid >> 1, half = tid & 1;
-    float m = 0.f;
-    if (n < a.Nc) {
-      const float* w1 = a.w1 + (int64_t)n * a.ldw1;
-      for (int k = half; k < a.k1; k += 2) m = fmaxf(m, fabsf(w1[k]));
-      if (a.w2) {
-        const float* w2 = a.w2 + (int64_t)n * a.ldw2;
-        for (int k = half; k < a.k2; k += 2) m = fmaxf(m, fabsf(w2[k]));
+    const int wave = tid >> 6, lane = tid & 63;
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = wave * 8 + j;
+      m[j] = 0.f;
+      if (n < a.Nc) {
+        const float* w1 = a.w1 + (int64_t)n * a.ldw1;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+          if (lane + 64 * i < a.k1) m[j] = fmaxf(m[j], fabsf(w1[lane + 64 * i]));
+        if (a.w2) {
+          const float* w2 = a.w2 + (int64_t)n * a.ldw2;
+#pragma unroll
+          for (int i = 0; i < 6; ++i)
+            if (lane + 64 * i < a.k2) m[j] = fmaxf(m[j], fabsf(w2[lane + 64 * i]));
+        }
       }
     }
-    m = fmaxf(m, __shfl_xor(m, 1));
-    if (half == 0) sc[n] = h2_col_exp2(m);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], __shfl_xor(m[j], o));
+    if (lane < 8) {
+      float v = m[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j)
+        if (lane == j) v = m[j];
+      sc[wave * 8 + lane] = h2_col_exp2(v);
+    }
   }
   __syncthreads();
   if (blockIdx.x == 0 && tid < BN) colscale[tid] = sc[tid] * (1.0f / 2048.0f);
+  if (tid >= 256) return;
   const int c = blockIdx.x, n = tid >> 1, kh = tid & 1;
   const float inv = 1.0f / sc[n];  // a power of two: exact
   uint32_t hw[4], lw[4], pw[4];
@@ -1428,7 +1451,7 @@ bool nt_h2_ok(const NTArgs& a) {
 template <int NKS>
 void launch_nt_h2_k(const NTArgs& a, uint4* img, hipStream_t st) {
   float* colscale = reinterpret_cast<float*>(img + NKS * 3 * 256);
-  ws_prep_h2_kernel<<<NKS, 256, 0, st>>>(a, img, colscale, a.ap_col2);
+  ws_prep_h2_kernel<<<NKS, WS_PREP_THREADS, 0, st>>>(a, img, colscale, a.ap_col2);
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
   const int grid = std::min(ntiles, ws_num_cus());
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;

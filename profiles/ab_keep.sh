@@ -13,4 +13,11 @@ t=d['roofline']['timed_kernels']; print('$f', round(d['ms_per_step'],4), {k: v['
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
     -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/kt.log" 2>&1
 find "$OUT/kt" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats.csv" \;
-head -14 "$OUT/kernel_stats.csv" | cut -c1-150
+
+GNNMP_KEEP_MASK=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt_hash" -o run --output-format csv \
+    -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/kt_hash.log" 2>&1
+find "$OUT/kt_hash" -name "*kernel_stats.csv" -exec cp {} "$OUT/kernel_stats_hash.csv" \;
+for f in kernel_stats kernel_stats_hash; do python3 -c "
+import csv
+for r in csv.DictReader(open('$OUT/$f.csv')):
+    if 'gnnmp' in r['Name']: print('$f', r['Name'][:60], r['Calls'], round(float(r['AverageNs'])/1000,1))"; done

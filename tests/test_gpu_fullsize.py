@@ -310,5 +310,6 @@ def test_scaled_bf16_train_step_gradients(device):
         assert rel_l2(logits, ref) < 1e-3, rel_l2(logits, ref)
         del ref
         grads = _ref_sage_bf16_grads(params, saved, w, ei, N, 3)
-    for k, v in model.named_parameters():
-        assert rel_l2(v.grad, grads[k]) < 2e-4, (k, rel_l2(v.grad, grads[k]))
+    errs = {k: rel_l2(v.grad, grads[k]) for k, v in model.named_parameters()}
+    print("scaled bf16 gradient relL2:", errs)
+    assert all(e < 2e-4 for e in errs.values()), errs

@@ -310,7 +310,7 @@ def test_input_tn_on_x_only_image(device, F, nr):
     (dW2, _), db2, _, _ = gemm_tn_input(nr, x, G)  # x's cached planes
     im = x_only_image(x)
     assert getattr(x, "_gnnmp_split_image_x", None) is im
-    assert im is not None and im.k2 == 0 and im.ld == ((F + 7) // 8 * 8 + 15) // 16 * 16
+    assert im is not None and im.k2 == 0 and im.ld == 176  # planes.X_ONLY_LD: every x-only image
     hi, mid, lo = split3(x.cpu().numpy())
     P = _planes_np(im)
     assert np.array_equal(P[0, :, :F], hi) and np.array_equal(P[1, :, :F], mid) and np.array_equal(P[2, :, :F], lo)
