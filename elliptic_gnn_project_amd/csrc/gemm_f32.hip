@@ -1006,7 +1006,8 @@ extern "C" int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p) {
   if (!p || !p->a_planes || p->math == GNN_MATH_F32 || p->mask || p->M < 1) return 0;
   NTArgs a{};
   a.M = p->M; a.Nc = (int32_t)p->N; a.k1 = (int32_t)p->k1; a.k2 = (int32_t)p->k2;
-  a.w1 = p->w1; a.w2 = p->w2; a.c = p->c; a.ldc = p->ldc; a.bias = p->bias; a.relu = p->relu;
+  a.w1 = p->w1; a.w2 = p->w2; a.ldw1 = p->ldw1; a.ldw2 = p->ldw2;
+  a.c = p->c; a.ldc = p->ldc; a.bias = p->bias; a.relu = p->relu;
   a.dropout = p->dropout_p > 0.f; a.nproj = p->nproj; a.ldz = p->ldz;
   a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16; a.c_bf16 = p->c_dtype == GNN_DTYPE_BF16;
   a.ap = static_cast<const uint16_t*>(p->a_planes);

@@ -1029,10 +1029,12 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
 // B image of the half-pair NT: per k-step s, plane p (hi' = 2^11 hi, hi, lo), slot 2n + khalf:
 // the 8 halves of column n, k = 16s + 8·khalf .. +8, of w_n · 2^-e_n, where 2^-e_n brings the
 // column's largest |w| into [8, 16) (a power of two: exact); colscale[n] = 2^(e_n - 11) (block 0).
-// Every block computes all column exponents (max |w_n| over the whole K): 16 waves, 8 columns
-// each, a wave's lanes across k so the loads coalesce and all of them (8 columns x 2 segments x
-// <= 6 per lane, K <= 336) are in flight at once -- one round trip instead of a per-thread walk
-// down the row (the first form spent ~33 us here on dependent load latency).
+// Every block computes all column exponents (max |w_n| over the whole K): 16 waves x 8 columns, a
+// wave's lanes across k (coalesced), in two passes of 4 columns whose 48 loads per lane are all
+// issued before the first use (indices clamped into the operand, the excess masked to 0: no load
+// sits behind a branch), then a wave max per column.  (A per-thread walk down each row spent
+// ~30 us on dependent load latency; a linear sweep into LDS atomics ~40 us on same-address
+// ds_max conflicts.)
 __device__ __forceinline__ float h2_col_exp2(float m) {  // 2^e with m · 2^-e in [8, 16); 1 for m = 0
   if (!(m > 0.f) || !isfinite(m)) return 1.0f;
   int E;
@@ -1043,56 +1045,65 @@ constexpr int WS_PREP_THREADS = 1024;
 __global__ __launch_bounds__(WS_PREP_THREADS) void ws_prep_h2_kernel(NTArgs a, uint4* __restrict__ img,
                                                                      float* __restrict__ colscale, int col2) {
   __shared__ float sc[BN];
+  __shared__ float slice[BN][17];  // this block's k-step of the image, [column][16 k] (+1: banks)
   const int tid = threadIdx.x;
+  const int c = blockIdx.x;
+  const int k2m = a.k2 > 0 ? a.k2 - 1 : 0;
+  const float* w2b = a.w2 ? a.w2 : a.w1;
+  const int64_t ld2 = a.w2 ? a.ldw2 : a.ldw1;
+  for (int i = tid; i < BN * 17; i += WS_PREP_THREADS) (&slice[0][0])[i] = 0.f;
+  __syncthreads();
   {
     const int wave = tid >> 6, lane = tid & 63;
-    float m[8];
+    const int k1m = a.k1 - 1;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = wave * 8 + j;
-      m[j] = 0.f;
-      if (n < a.Nc) {
-        const float* w1 = a.w1 + (int64_t)n * a.ldw1;
+    for (int pass = 0; pass < 2; ++pass) {
+      float v[4][12];
 #pragma unroll
-        for (int i = 0; i < 6; ++i)
-          if (lane + 64 * i < a.k1) m[j] = fmaxf(m[j], fabsf(w1[lane + 64 * i]));
-        if (a.w2) {
-          const float* w2 = a.w2 + (int64_t)n * a.ldw2;
+      for (int j = 0; j < 4; ++j) {
+        const int nc = min(wave * 8 + pass * 4 + j, a.Nc - 1);
+        const float* w1 = a.w1 + (int64_t)nc * a.ldw1;
+        const float* w2 = w2b + (int64_t)nc * ld2;
 #pragma unroll
-          for (int i = 0; i < 6; ++i)
-            if (lane + 64 * i < a.k2) m[j] = fmaxf(m[j], fabsf(w2[lane + 64 * i]));
+        for (int i = 0; i < 6; ++i) {
+          v[j][i] = w1[min(lane + 64 * i, k1m)];
+          v[j][6 + i] = w2[min(lane + 64 * i, k2m)];
         }
       }
-    }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1)
+      for (int j = 0; j < 4; ++j) {
+        float m = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], __shfl_xor(m[j], o));
-    if (lane < 8) {
-      float v = m[0];
+        for (int i = 0; i < 6; ++i) {
+          m = fmaxf(m, lane + 64 * i < a.k1 ? fabsf(v[j][i]) : 0.f);
+          m = fmaxf(m, lane + 64 * i < a.k2 ? fabsf(v[j][6 + i]) : 0.f);
+        }
 #pragma unroll
-      for (int j = 1; j < 8; ++j)
-        if (lane == j) v = m[j];
-      sc[wave * 8 + lane] = h2_col_exp2(v);
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const int n = wave * 8 + pass * 4 + j;
+        if (lane == 0) sc[n] = n < a.Nc ? h2_col_exp2(m) : 1.0f;
+        if (n < a.Nc) {  // the block's k-step: image column kk = 16c + t holds w1[kk] or w2[kk - col2]
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            const int k = lane + 64 * i, t1 = k - 16 * c, t2 = col2 + k - 16 * c;
+            if (k < a.k1 && t1 >= 0 && t1 < 16) slice[n][t1] = v[j][i];
+            if (k < a.k2 && t2 >= 0 && t2 < 16) slice[n][t2] = v[j][6 + i];
+          }
+        }
+      }
     }
   }
   __syncthreads();
   if (blockIdx.x == 0 && tid < BN) colscale[tid] = sc[tid] * (1.0f / 2048.0f);
   if (tid >= 256) return;
-  const int c = blockIdx.x, n = tid >> 1, kh = tid & 1;
+  const int n = tid >> 1, kh = tid & 1;
   const float inv = 1.0f / sc[n];  // a power of two: exact
   uint32_t hw[4], lw[4], pw[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float v[2];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int k = 16 * c + 8 * kh + 2 * j + q;
-      float x = 0.f;
-      if (n < a.Nc && k < a.k1) x = a.w1[(int64_t)n * a.ldw1 + k];
-      else if (n < a.Nc && k >= col2 && k < col2 + a.k2) x = a.w2[(int64_t)n * a.ldw2 + (k - col2)];
-      v[q] = x * inv;
-    }
+    for (int q = 0; q < 2; ++q) v[q] = slice[n][8 * kh + 2 * j + q] * inv;
     split_h2_pair(v[0], v[1], hw[j], lw[j]);
     pw[j] = h2_scale_pair(hw[j], 2048.0f);
   }
@@ -1442,6 +1453,9 @@ bool nt_h2_ok(const NTArgs& a) {
   if (a.c && (!al(a.c) || a.ldc % 4 != 0 || a.M * a.ldc * 4 >= ((int64_t)1 << 31))) return false;
   if (a.Nc % 4 != 0 || (a.nproj > 0 && a.M * a.ldz * 4 >= ((int64_t)1 << 31))) return false;
   if (a.M < WS_ROWS) return false;
+  // the prep kernel's linear sweep indexes the weights with 32-bit element offsets
+  if (a.ldw1 < a.k1 || a.Nc * a.ldw1 >= ((int64_t)1 << 30) || (a.w2 && a.k2 > 0 && (a.ldw2 < a.k2 || a.Nc * a.ldw2 >= ((int64_t)1 << 30))))
+    return false;
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
   if ((drop || proj || relu) && !(relu && bias)) return false;
   return true;

@@ -32,14 +32,20 @@ for nn, ne in [(6000, 9000), (200_000, 400_000), (2_000_000, 4_000_000)]:
     x_bf = data.x.to(torch.bfloat16).to(dev)
     logits = model(x_bf, ei)
     w = torch.randn(N, 2, generator=torch.Generator().manual_seed(1)).to(dev)
+    st = [t.detach().clone() for t in logits.grad_fn.saved_tensors[:5]]  # hs (L), aggs (L - 1): the kernels' own
     (logits * w).sum().backward()
+    own = [(st[3 + l].double() if l < 2 else None, st[l].double()) for l in range(3)]
     with torch.no_grad():
         ref, saved = _ref_sage_bf16(params, x_bf, ei, N, 3)
         le = rel(logits, ref)
+        fd = {f"h{l}": rel(st[l], saved[l][1]) for l in range(3)}
+        fd.update({f"agg{l}": rel(st[3 + l], saved[l][0]) for l in range(2)})
         grads = _ref_sage_bf16_grads(params, saved, w, ei, N, 3)
-    errs = {k: f"{rel(v.grad, grads[k]):.2e}" for k, v in model.named_parameters()}
+        grads_own = _ref_sage_bf16_grads(params, own, w, ei, N, 3)
+    errs = {k: f"{rel(v.grad, grads[k]):.2e}/{rel(v.grad, grads_own[k]):.2e}" for k, v in model.named_parameters()}
+    print("forward stores relL2", {k: f"{v:.2e}" for k, v in fd.items()})
     deg = torch.bincount(ei[1], minlength=N)
     print(f"N={N} E={ei.size(1)} maxdeg={int(deg.max())} logits {le:.2e} grads {errs} ({time.time() - t0:.0f}s)",
           flush=True)
-    del data, ei, model, params, x_bf, logits, ref, saved, grads, w
+    del data, ei, model, params, x_bf, logits, ref, saved, grads, grads_own, own, st, w
     torch.cuda.empty_cache()

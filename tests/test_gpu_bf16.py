@@ -247,9 +247,11 @@ def test_fused_sage_bf16_image_equals_tiled(device, monkeypatch):
         assert rel_l2(a, b) < 5e-3
 
 
-@pytest.mark.parametrize("form,k1,M", [("dz_mask", 166, 5000), ("g_mask", 166, 4133), ("g_mask", 128, 3001),
-                                       ("dz_mask", 128, 40)])
-def test_gemm_tn_bf16_image(device, form, k1, M):
+@pytest.mark.parametrize("form,k1,M,gdt", [("dz_mask", 166, 5000, "f32"), ("g_mask", 166, 4133, "f32"),
+                                           ("g_mask", 128, 3001, "f32"), ("dz_mask", 128, 40, "f32"),
+                                           ("dz_mask", 128, 200_000, "bf16"), ("g_mask", 128, 200_000, "bf16"),
+                                           ("dz_mask", 128, 6000, "bf16"), ("g_mask", 128, 5000, "bf16")])
+def test_gemm_tn_bf16_image(device, form, k1, M, gdt):
     """The bf16 image TN (gemm_tn_img16_kernel, register ring D chunks ahead): dW = RNE(G)ᵀ·[A1 | A2]
     from a one-plane image, G = (dz·P or g) ⊙ mask formed in f32 (and written to gout), db, dzᵀh."""
     from elliptic_gnn_project_amd.fused import gemm_tn
@@ -266,16 +268,21 @@ def test_gemm_tn_bf16_image(device, form, k1, M):
     dz = torch.randn(M, 4, generator=g_) * 1e-3
     proj = torch.randn(4, nr, generator=g_)
     G = dz @ proj if form == "dz_mask" else torch.randn(M, nr, generator=g_) * 1e-3
-    kw = dict(dz=dz.to(device), proj=proj.to(device)) if form == "dz_mask" else dict(g=G.to(device))
+    if gdt == "bf16" and form == "g_mask":
+        G = G.to(torch.bfloat16).float()  # the lower layers' g arrives bf16 (the dh NT's output)
+    gin = G.to(torch.bfloat16) if gdt == "bf16" else G
+    kw = dict(dz=dz.to(device), proj=proj.to(device)) if form == "dz_mask" else dict(g=gin.to(device))
     Gm = torch.where(h.float() > 0, G * 2.0, torch.zeros_like(G))
-    gout = torch.empty(M, nr, device=device)
+    odt = torch.bfloat16 if gdt == "bf16" else torch.float32
+    gout = torch.empty(M, nr, device=device, dtype=odt)
     assert gemm_tn(nr, None, None, h=h.to(device), hscale=2.0, gout=gout, planes=im, check_planes=True, **kw)
     dW, db, dW2, dzs = gemm_tn(nr, None, None, h=h.to(device), hscale=2.0, gout=gout, planes=im, **kw)
-    torch.testing.assert_close(gout.cpu(), Gm, rtol=1e-5, atol=1e-8)
+    torch.testing.assert_close(gout.cpu().float(), Gm.to(odt).float(), rtol=1e-5 if gdt == "f32" else 2.0 ** -8,
+                               atol=1e-8)
     A = torch.cat([a1, a2], 1).double()
     ref = rb(Gm).double().t() @ A
     assert rel_l2(torch.cat([dW[0], dW[1]], 1), ref) < 1e-5
-    assert rel_l2(db, Gm.sum(0)) < 1e-5
+    assert rel_l2(db, Gm.sum(0)) < 1e-5, rel_l2(db, Gm.sum(0))
     if form == "dz_mask":
         assert rel_l2(dW2, dz.t().double() @ h.double()) < 1e-5
         assert rel_l2(dzs, dz.sum(0)) < 1e-5

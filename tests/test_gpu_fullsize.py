@@ -283,9 +283,10 @@ def test_scaled_bf16_train_step_gradients(device):
     edges, SAGE 166->128->128->2 on bf16 storage): logits and every parameter gradient vs the
     float64 reference with the kernels' rounding points in both directions (tests/test_gpu_bf16.py
     _ref_sage_bf16 / _ref_sage_bf16_grads: forward stores, the TN's bf16 G), evaluated in float64
-    on the device.  Bounds as the 6,000-node test: logits relL2 < 1e-3, gradients < 2e-4 — at this
-    size the bf16 image TN, the f32 meanᵀ(G) at F = 128 and the reassociated dh GEMM run over the
-    real 2 M-row operands (dropout 0: the reference has no mask)."""
+    on the device.  Bounds: logits relL2 < 1e-3; the backward, evaluated on the kernels' own forward
+    stores, < 2e-4 as in the 6,000-node test; end to end < 2e-3 (see below).  At this size the bf16
+    image TN, the bf16 [meanᵀ(G) | G] image and its one-product dh NT run over the real 2 M-row
+    operands (dropout 0: the reference has no mask)."""
     from test_gpu_bf16 import _ref_sage_bf16, _ref_sage_bf16_grads
 
     from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
@@ -303,13 +304,28 @@ def test_scaled_bf16_train_step_gradients(device):
     del data
     logits = model(x_bf, ei)
     assert logits.dtype == torch.float32
+    # the kernels' own forward stores (hs = x, h1, h2; aggs = agg0, agg1), kept before the backward
+    st = [t.detach().clone() for t in logits.grad_fn.saved_tensors[:5]]
+    own = [(st[3].double(), st[0].double()), (st[4].double(), st[1].double()), (None, st[2].double())]
+    del st
     w = torch.randn(N, 2, generator=torch.Generator().manual_seed(1)).to(device)
     (logits * w).sum().backward()
     with torch.no_grad():
         ref, saved = _ref_sage_bf16(params, x_bf, ei, N, 3)
         assert rel_l2(logits, ref) < 1e-3, rel_l2(logits, ref)
         del ref
+        fwd = {f"h{l}": rel_l2(own[l][1], saved[l][1]) for l in (1, 2)}
+        fwd["agg1"] = rel_l2(own[1][0], saved[1][0])
+        assert all(e < 2e-4 for e in fwd.values()), fwd  # measured ~2e-5 (h1, agg1), ~5e-5 (h2)
         grads = _ref_sage_bf16_grads(params, saved, w, ei, N, 3)
-    errs = {k: rel_l2(v.grad, grads[k]) for k, v in model.named_parameters()}
-    print("scaled bf16 gradient relL2:", errs)
-    assert all(e < 2e-4 for e in errs.values()), errs
+        errs = {k: rel_l2(v.grad, grads[k]) for k, v in model.named_parameters()}
+        del grads, saved
+        grads = _ref_sage_bf16_grads(params, own, w, ei, N, 3)
+        errs_own = {k: rel_l2(v.grad, grads[k]) for k, v in model.named_parameters()}
+    print("scaled bf16 gradient relL2 vs the reference forward / vs the kernels' forward stores:", errs, errs_own)
+    # the backward proper, on the same forward stores: every gradient within 2e-4 (as at 6,000 nodes)
+    assert all(e < 2e-4 for e in errs_own.values()), errs_own
+    # end to end: the forward's one-ulp store flips (~5e-5 of h2) reach the gradients through the
+    # ReLU masks and the high-degree rows' meanᵀ sums; measured 6.5e-4 .. 8.7e-4 for the two hidden
+    # layers at 200 k and 2 M nodes (diagnostic: profiles/bf16_grad_diag.py), top layer ~1e-4
+    assert all(e < 2e-3 for e in errs.values()), errs
