@@ -260,9 +260,10 @@ def kernel_pattern(tag):
     import re
 
     if tag[0] == "gemm_nt":
-        return re.compile(r"gemm_nt_(planes|ws|img16)_kernel<%d[,>]" % -(-tag[2] // 16))
+        return re.compile(r"gemm_nt_(planes|ws|img16|h2)_kernel<%d[,>]" % -(-tag[2] // 16))
     if tag[0] == "gemm_tn":
-        return re.compile(r"gemm_tn_(planes|img16)_kernel<\w+, \w+, %d," % -(-tag[2] // 32))
+        kt = -(-tag[2] // 32)
+        return re.compile(r"gemm_tn_(planes|img16)_kernel<\w+, \w+, %d,|gemm_tn_h2_kernel<%d," % (kt, kt))
     if tag[0] == "agg":
         mode, F = tag[1], tag[3]
         fam = "agg_wave_kernel" if F > 128 else "agg_narrow_lds_kernel" if F <= 4 else "agg_flat(_pieces)?_kernel"

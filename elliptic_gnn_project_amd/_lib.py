@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -123,7 +123,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("a_dtype", c_i32), ("c_dtype", c_i32),
         ("mask", c_ptr), ("ldmask", c_i64), ("mask_scale", ctypes.c_float),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
-        ("planes_format", c_i32), ("keep_mask", c_ptr),
+        ("planes_format", c_i32), ("keep_mask", c_ptr), ("b_ready", c_i32),
     ]
 
 
@@ -267,6 +267,7 @@ SIGNATURES = {
     ),
     "gnn_gemm_nt_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_size)]),
     "gnn_gemm_nt_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),
+    "gnn_gemm_nt_prep_b": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),
     "gnn_gemm_tn_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32, ctypes.POINTER(c_size)]),
     "gnn_gemm_tn_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams), c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_gemm_nt_planes_ok": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams)]),

@@ -190,13 +190,15 @@ size_t nt_ws_tail_offset(int64_t k1, int64_t k2);
 void launch_nt_ws(const NTArgs& a, uint4* img, hipStream_t st);
 // the split-image forms (gemm_ws.hip NT, gemm_planes.hip TN): shapes they take, launchers
 bool nt_planes_ok(const NTArgs& a);
-void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st);
+// Image-A NT launch phases: the B-image prep, the GEMM, or both (gnn_gemm_nt_prep_b / b_ready)
+constexpr int NT_PHASE_PREP = 1, NT_PHASE_RUN = 2, NT_PHASE_ALL = 3;
+void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st, int phase = NT_PHASE_ALL);
 // the bf16 image form (gemm_ws.hip): bf16 storage, one product per MFMA, LDS-DMA staged
 bool nt_img16_ok(const NTArgs& a);
-void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st);
+void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st, int phase = NT_PHASE_ALL);
 // the half-pair forms (f16 hi / lo images, 3 products): gemm_ws.hip / gemm_planes.hip
 bool nt_h2_ok(const NTArgs& a);
-void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st);
+void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st, int phase = NT_PHASE_ALL);
 bool tn_h2_ok(const TNArgs& a);
 void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st);
 bool tn_planes_ok(const TNArgs& a);

@@ -740,8 +740,9 @@ int tn_blocks(int64_t M) {
 
 using namespace gnnmp;
 
-static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t stream, const char* fn) {
+static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t stream, const char* fn, int phase) {
   if (!p) return fail(GNN_ERR_INVALID_ARG, fn, "null params");
+  if (phase == NT_PHASE_ALL && p->b_ready) phase = NT_PHASE_RUN;
   const bool planes_only = p->a_planes && !p->a1;  // A given only as a split image
   if (p->M < 0 || p->N < 1 || p->k1 < 1 || p->k2 < 0 || (!p->a1 && !p->a_planes) ||
       (p->k2 > 0 && !p->a2 && !planes_only))
@@ -761,7 +762,7 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
   if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, fn, "bad math mode");
   if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->c_dtype != GNN_DTYPE_F32 && p->c_dtype != GNN_DTYPE_BF16))
     return fail(GNN_ERR_INVALID_ARG, fn, "bad dtype");
-  if (p->M == 0) return GNN_OK;
+  if (p->M == 0 && phase != NT_PHASE_PREP) return GNN_OK;
   NTArgs a{};
   a.M = p->M; a.Nc = (int32_t)p->N;
   a.a1 = p->a1; a.lda1 = p->lda1; a.k1 = (int32_t)p->k1;
@@ -808,7 +809,7 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
     if (a.ap_h2) {  // the half-pair image: f16 hi / lo planes, 3 products
       if (p->math != GNN_MATH_F32 && !p->mask && nt_h2_ok(a) && p->workspace &&
           p->workspace_bytes >= img_bytes + BN * sizeof(float)) {
-        launch_nt_h2(a, static_cast<uint4*>(p->workspace), st);
+        launch_nt_h2(a, static_cast<uint4*>(p->workspace), st, phase);
         return hip_check(hipGetLastError(), fn);
       }
       if (planes_only) return fail(GNN_ERR_UNSUPPORTED, fn, "half-pair image A outside the half-pair kernel's shapes");
@@ -816,19 +817,22 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
     }
     if (a.a_bf16) {  // a bf16 image (one plane): the bf16-storage form
       if (p->math != GNN_MATH_F32 && !p->mask && nt_img16_ok(a) && p->workspace && p->workspace_bytes >= img_bytes) {
-        launch_nt_img16(a, static_cast<uint4*>(p->workspace), st);
+        launch_nt_img16(a, static_cast<uint4*>(p->workspace), st, phase);
         return hip_check(hipGetLastError(), fn);
       }
       return fail(GNN_ERR_UNSUPPORTED, fn, "bf16 image A outside the image kernel's shapes");
     }
     if (p->math != GNN_MATH_F32 && !p->mask && nt_planes_ok(a) && p->workspace &&
         p->workspace_bytes >= img_bytes) {
-      launch_nt_ws_planes(a, static_cast<uint4*>(p->workspace), st);
+      launch_nt_ws_planes(a, static_cast<uint4*>(p->workspace), st, phase);
       return hip_check(hipGetLastError(), fn);
     }
     if (planes_only) return fail(GNN_ERR_UNSUPPORTED, fn, "split-image A outside the planes kernel's shapes");
     a.ap = nullptr;  // the f32 operands serve
   }
+  if (phase != NT_PHASE_ALL)  // prep_b / b_ready: only the image-A kernels have a separate B image
+    return fail(phase == NT_PHASE_PREP ? GNN_ERR_UNSUPPORTED : GNN_ERR_INVALID_ARG, fn,
+                "a separate B prep (prep_b / b_ready) needs an image-A kernel (gnn_gemm_nt_planes_ok)");
   if (launch_nt_skinny(a, st)) return hip_check(hipGetLastError(), fn);  // Nc <= 8 or K <= 8
   if (p->mask) return fail(GNN_ERR_UNSUPPORTED, fn, "the mask epilogue needs a skinny shape (K <= 8 or N <= 8)");
   if (a.a_bf16 || a.c_bf16) {
@@ -856,7 +860,11 @@ extern "C" gnn_status gnn_gemm_nt_workspace_size(int64_t N, int64_t k1, int64_t 
 }
 
 extern "C" gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream) {
-  return gemm_nt_dispatch(p, stream, __func__);
+  return gemm_nt_dispatch(p, stream, __func__, NT_PHASE_ALL);
+}
+
+extern "C" gnn_status gnn_gemm_nt_prep_b(const gnn_gemm_nt_params* p, gnn_stream_t stream) {
+  return gemm_nt_dispatch(p, stream, __func__, NT_PHASE_PREP);
 }
 
 

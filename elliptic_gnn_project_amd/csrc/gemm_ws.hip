@@ -1463,9 +1463,10 @@ bool nt_h2_ok(const NTArgs& a) {
 
 // workspace: the B image (NKS k-steps x 3 planes x 256 slots x 16 B), then the 128 column scales
 template <int NKS>
-void launch_nt_h2_k(const NTArgs& a, uint4* img, hipStream_t st) {
+void launch_nt_h2_k(const NTArgs& a, uint4* img, hipStream_t st, int phase) {
   float* colscale = reinterpret_cast<float*>(img + NKS * 3 * 256);
-  ws_prep_h2_kernel<<<NKS, WS_PREP_THREADS, 0, st>>>(a, img, colscale, a.ap_col2);
+  if (phase & NT_PHASE_PREP) ws_prep_h2_kernel<<<NKS, WS_PREP_THREADS, 0, st>>>(a, img, colscale, a.ap_col2);
+  if (!(phase & NT_PHASE_RUN)) return;
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
   const int grid = std::min(ntiles, ws_num_cus());
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
@@ -1481,9 +1482,9 @@ void launch_nt_h2_k(const NTArgs& a, uint4* img, hipStream_t st) {
 #undef GNN_NH
 }
 
-void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st) {
-  if (a.ap_ld == 176) launch_nt_h2_k<11>(a, img, st);
-  else launch_nt_h2_k<21>(a, img, st);
+void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st, int phase) {
+  if (a.ap_ld == 176) launch_nt_h2_k<11>(a, img, st, phase);
+  else launch_nt_h2_k<21>(a, img, st, phase);
 }
 
 // The bf16 image form: bf16 A image (one plane, ld 256 or 336), bf16 C, the w1/w2 B form,
@@ -1520,9 +1521,10 @@ void launch_nt_img16_k(const NTArgs& a, const uint4* img, hipStream_t st) {
 #undef GNN_I16
 }
 
-void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st) {
+void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st, int phase) {
   const int nks = a.ap_ld / 16;
-  ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // B image (plane 0 used)
+  if (phase & NT_PHASE_PREP) ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // B image (plane 0 used)
+  if (!(phase & NT_PHASE_RUN)) return;
   if (nks == 16) launch_nt_img16_k<16>(a, img, st);
   else launch_nt_img16_k<21>(a, img, st);
 }
@@ -1542,9 +1544,10 @@ void launch_nt_ws_planes_k(const NTArgs& a, uint4* img, hipStream_t st) {
 #undef GNN_WSP
 }
 
-void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st) {
+void launch_nt_ws_planes(const NTArgs& a, uint4* img, hipStream_t st, int phase) {
   const int nks = a.ap_ld / 16;
-  ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // the B image only
+  if (phase & NT_PHASE_PREP) ws_prep_kernel<<<(unsigned)nks, 256, 0, st>>>(a, img, nks, nullptr, 0, a.ap_col2);  // the B image only
+  if (!(phase & NT_PHASE_RUN)) return;
   if (nks == 11) launch_nt_ws_planes_k<11>(a, img, st);
   else launch_nt_ws_planes_k<21>(a, img, st);
 }

@@ -38,9 +38,22 @@ _PLANES = os.environ.get("GNNMP_PLANES", "1") != "0"
 # The 2-layer SAGE's layer-1 operand as a half-pair image (f16 hi / lo planes, 3 products: include/
 # gnnmp.h gnn_split_h2_f32) rather than the split-bf16 one; GNNMP_H2=0 keeps split-bf16 (A/B).
 _H2 = os.environ.get("GNNMP_H2", "1") != "0"
-# K1 writes the half-pair NT's dropout keep bits (the NT then skips the hash); GNNMP_KEEP_MASK=0
-# hashes in the NT epilogue instead (A/B)
-_KEEP_MASK = os.environ.get("GNNMP_KEEP_MASK", "1") != "0"
+# GNNMP_KEEP_MASK=1: K1 also writes the half-pair NT's dropout keep bits and the NT reads them
+# instead of hashing.  Off by default: measured (profiles/r18f, rocprofv3) the NT at 88.8 us with the
+# bits vs 89.6 us hashing, while writing them costs K1 6.5 us (110.0 vs 103.5 us).
+_KEEP_MASK = os.environ.get("GNNMP_KEEP_MASK", "0") == "1"
+# The SAGE layer-0 NT's weight prep (the B image: ~11 us of latency-bound work over the weights
+# only) runs on a side stream beside K1 (the aggregation that writes the NT's A image), joined
+# before the NT; GNNMP_SIDE_PREP=0 keeps it in line, inside the NT call (A/B)
+_SIDE_PREP = os.environ.get("GNNMP_SIDE_PREP", "1") != "0"
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = torch.cuda.Stream(device=key)
+    return _SIDE_STREAMS[key]
 
 MAX_PROJ = 4  # nproj = 2 * num_classes <= 4
 
@@ -92,22 +105,25 @@ _BF_IMAGE = os.environ.get("GNNMP_BF_IMAGE", "1") != "0"
 
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
             out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None, mask=None, mask_scale=1.0,
-            planes=None, check_planes=False, keep_mask=None):
+            planes=None, check_planes=False, keep_mask=None, workspace=None, b_stage=None):
     """C = epilogue([a1 | a2] · B) on the NT kernels; B = bt ([K, n] row-major) or, with bt None,
     [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2].
     bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too.
     ``planes`` (planes.SplitImage): A read from the split image; a1 / a2 may then be None.
     ``check_planes``: only report whether the call would take the split-image kernel (no launch).
-    ``keep_mask`` (half-pair planes with dropout): the keep bits K1 wrote for this call's seed."""
+    ``keep_mask`` (half-pair planes with dropout): the keep bits K1 wrote for this call's seed.
+    ``b_stage`` (image-A forms, with an explicit ``workspace``): "prep" launches only the B-image
+    prep (gnn_gemm_nt_prep_b; returns None), "ready" only the GEMM over the image a "prep" call of
+    the same weights left in ``workspace``."""
     if planes is not None:
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
         M, k1, k2, dev = a1.size(0), a1.size(1), (a2.size(1) if a2 is not None else 0), a1.device
     bf = getattr(planes, "bf16", False) or (a1 is not None and a1.dtype == torch.bfloat16)
-    if out is None and want_c and not check_planes:
+    if out is None and want_c and not check_planes and b_stage != "prep":
         out = torch.empty((M, n), dtype=torch.bfloat16 if bf else torch.float32, device=dev)
-    ws = None
-    if w1 is not None:  # B pre-split image for the streaming split-bf16 kernel (≈24 KB per 32 of K)
+    ws = workspace
+    if ws is None and w1 is not None:  # B pre-split image for the streaming split-bf16 kernel (≈24 KB per 32 of K)
         ws = _nt_workspace(dev, n, k1, k2)
     p = _lib.GnnGemmNTParams(
         M, n,
@@ -123,10 +139,13 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.DTYPE_BF16 if bf else _lib.DTYPE_F32,
         _lib.DTYPE_BF16 if (out is not None and out.dtype == torch.bfloat16) else _lib.DTYPE_F32,
         _lib.ptr(mask), _ld(mask) if mask is not None else 0, float(mask_scale),
-        *_planes_fields(planes), _lib.ptr(keep_mask),
+        *_planes_fields(planes), _lib.ptr(keep_mask), int(b_stage == "ready"),
     )
     if check_planes:
         return bool(_lib.load().gnn_gemm_nt_planes_ok(p))
+    if b_stage == "prep":
+        _lib.call("gnn_gemm_nt_prep_b", p, _lib.stream_handle(dev))
+        return None
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
@@ -315,8 +334,17 @@ class _FusedSAGE(torch.autograd.Function):
                     kb = im.keep_buffer()
                     keep = (kb, Wl[l].size(0), train_drop, seeds[l], seed_ctr)
                     nt_kw = dict(nt_kw, keep_mask=kb)
+                n_out = Wl[l].size(0)
+                ws, side = _nt_workspace(h.device, n_out, im.k1, im.k2), None
+                if _SIDE_PREP:  # the B prep beside K1 (it reads only the weights)
+                    side, cur = _side_stream(h.device), torch.cuda.current_stream(h.device)
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="prep", **nt_kw)
                 ctx.image = (im, im.fill_mean(plan, h, keep))
-                hn = gemm_nt(None, None, Wl[l].size(0), planes=im, **nt_kw)
+                if side is not None:
+                    cur.wait_stream(side)
+                hn = gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="ready" if side else None, **nt_kw)
                 agg = None
             else:
                 agg = aggregate(plan, h, _lib.AGG_MEAN, nodew=plan.deg)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 17
+#define GNNMP_ABI_VERSION 18
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -367,11 +367,20 @@ typedef struct {
   const uint32_t* keep_mask;             /* optional (HALF_PAIR with dropout): the keep bits written by
                                             gnn_sage_mean_fwd_h2 for this call's seed / p / N; used
                                             instead of hashing every element in the epilogue */
+  int32_t b_ready;                       /* image-A forms only: nonzero = workspace already holds the B
+                                            image gnn_gemm_nt_prep_b wrote for these weights and shapes
+                                            (the call launches only the GEMM) */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
 gnn_status gnn_gemm_nt_workspace_size(int64_t N, int64_t k1, int64_t k2, size_t* bytes);
 gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream);
+/* The image-A forms' weight prep alone: writes the B image (split / half-pair / bf16 planes of
+ * [w1 | w2]ᵀ, with the half-pair column scales) into p->workspace, for a later gnn_gemm_nt_f32 of
+ * the same params with b_ready = 1.  Lets a caller run the prep on a second stream beside the
+ * producer of A (it reads only the weights).  UNSUPPORTED (nothing launched) when the params do
+ * not select an image-A kernel (gnn_gemm_nt_planes_ok). */
+gnn_status gnn_gemm_nt_prep_b(const gnn_gemm_nt_params* p, gnn_stream_t stream);
 
 typedef struct {
   int64_t M, Nr;                         /* dW is [Nr, k1+k2], Nr <= 128, k1+k2 <= 384 */

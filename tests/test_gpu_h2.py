@@ -131,6 +131,63 @@ def test_nt_h2_vs_f64(device, M, epi):
         assert rel_l2(z, c.double().cpu() @ proj.double().t()) < 1e-6
 
 
+@pytest.mark.parametrize("fmt", ["h2", "split"])
+def test_nt_prep_b_then_ready_equals_one_call(device, fmt):
+    """gnn_gemm_nt_prep_b on a side stream, then gnn_gemm_nt_f32 with b_ready over the same
+    workspace (the SAGE layer-0 schedule): bit-identical to the one-call form, for the half-pair
+    and the split-bf16 image."""
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.fused import _nt_workspace, gemm_nt
+    from elliptic_gnn_project_amd.planes import SplitImage
+
+    M, F, n = 5000, 166, 128
+    agg, x, w1, w2 = _operands(M, F, n, 7)
+    if fmt == "h2":
+        im = _image(agg, x, device)
+    else:
+        im = SplitImage(M, F, F, device)
+        im.fill_x(x.to(device))
+        _lib.call("gnn_split_planes_f32", agg.to(device).data_ptr(), F, M, F, im.ptr, im.ld, im.ps, 0, im.col2,
+                  _lib.stream_handle(device))
+    kw = dict(w1=w1.to(device), w2=w2.to(device), bias=torch.randn(n).to(device), relu=True, dropout_p=0.5, seed=5)
+    one = gemm_nt(None, None, n, planes=im, **kw)
+    ws = _nt_workspace(device, n, im.k1, im.k2)
+    side, cur = torch.cuda.Stream(device=device), torch.cuda.current_stream(device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        assert gemm_nt(None, None, n, planes=im, workspace=ws, b_stage="prep", **kw) is None
+    cur.wait_stream(side)
+    two = gemm_nt(None, None, n, planes=im, workspace=ws, b_stage="ready", **kw)
+    assert torch.equal(one, two)
+
+
+def test_fused_sage_side_prep_equals_inline(device):
+    """The SAGE train step with the layer-0 B prep on the side stream (default) and in line
+    (GNNMP_SIDE_PREP=0): bit-identical logits and gradients."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data, plan, x = _plan_and_x(20_000, 30_000, 5, device)
+    ei = data.edge_index.to(device)
+    torch.manual_seed(3)
+    model = SAGENet(x.size(1), 128, layers=2, dropout=0.5).to(device).train()
+    res = []
+    saved = fused._SIDE_PREP
+    for on in (True, False):
+        fused._SIDE_PREP = on
+        try:
+            model.zero_grad()
+            out, loss = _sage_step(model, x, ei, 78)
+            loss.backward()
+            res.append((out.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()}))
+        finally:
+            fused._SIDE_PREP = saved
+    (o1, g1), (o2, g2) = res
+    assert torch.equal(o1, o2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+
+
 @pytest.mark.parametrize("wscale", [3e4, 1e-6, 0.5])
 def test_nt_h2_column_scales(device, wscale):
     """Weights far outside f16's comfortable range: every output column is scaled by its own
@@ -210,6 +267,33 @@ def test_fused_sage_h2_vs_split_bf16(device, n, e):
     torch.testing.assert_close(o1, o2, rtol=1e-5, atol=1e-5)
     for k in g1:
         assert rel_l2(g1[k], g2[k]) < 1e-5, k
+
+
+def test_fused_sage_keep_bits_equal_hash(device):
+    """GNNMP_KEEP_MASK=1 (K1 writes the NT's keep bits, the NT reads them) against the default
+    (the NT hashes): the same masks, so logits and gradients are bit-identical."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data, plan, x = _plan_and_x(20_000, 30_000, 5, device)
+    ei = data.edge_index.to(device)
+    torch.manual_seed(3)
+    model = SAGENet(x.size(1), 128, layers=2, dropout=0.5).to(device).train()
+    res = []
+    saved = fused._KEEP_MASK
+    for on in (True, False):
+        fused._KEEP_MASK = on
+        try:
+            model.zero_grad()
+            out, loss = _sage_step(model, x, ei, 77)
+            loss.backward()
+            res.append((out.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()}))
+        finally:
+            fused._KEEP_MASK = saved
+    (o1, g1), (o2, g2) = res
+    assert torch.equal(o1, o2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
 
 
 def test_large_input_keeps_split_bf16(device):

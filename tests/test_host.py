@@ -95,6 +95,21 @@ def test_dropout_index_range_is_checked(lib):
     assert lib.gnn_gat_act_bwd_f32(1 << 26, F, 1, 0.5, 1, None, fake, F, fake, F, fake, F, None) == 5
 
 
+def test_prep_b_needs_an_image_form(lib):
+    """gnn_gemm_nt_prep_b / b_ready apply only to the image-A kernels: an f32-operand call is refused
+    before any launch (UNSUPPORTED for the prep, INVALID_ARG for b_ready; pointers never read)."""
+    from elliptic_gnn_project_amd import _lib
+
+    fake = 1 << 20
+    p = _lib.GnnGemmNTParams(1000, 128, fake, 166, 166, None, 0, 0, None, 0, fake, None, 166, 0, fake, 128)
+    p.math = _lib.MATH_SPLIT_BF16
+    p.a_dtype = p.c_dtype = _lib.DTYPE_F32
+    assert lib.gnn_gemm_nt_prep_b(p, None) == 5
+    assert b"image-A" in lib.gnn_last_error()
+    p.b_ready = 1
+    assert lib.gnn_gemm_nt_f32(p, None) == 1
+
+
 STRUCTS = {
     "gnn_split": ("GnnSplit", ["seg_len", "reserved", "num_long", "num_pieces", "ptr", "nbr", "piece0",
                                "piece_seg", "long_seg", "order"]),
@@ -108,7 +123,8 @@ STRUCTS = {
                                                "nproj", "z", "ldz", "math", "workspace",
                                                "workspace_bytes", "a_dtype", "c_dtype", "mask", "ldmask",
                                                "mask_scale", "a_planes", "planes_ld", "planes_stride",
-                                               "planes_col2", "planes_format", "keep_mask"]),
+                                               "planes_col2", "planes_format", "keep_mask",
+                                               "b_ready"]),
     "gnn_adam_tensor": ("GnnAdamTensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel"]),
     "gnn_adam_group": ("GnnAdamGroup", ["num_tensors", "lr", "beta1", "beta2", "eps", "weight_decay", "max_norm",
                                         "tensors", "skip_nonfinite"]),
