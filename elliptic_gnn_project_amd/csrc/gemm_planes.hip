@@ -441,6 +441,9 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   __shared__ float redm[8];
   constexpr int NU = 2 * NPA + 4 + 16 + 4 + 3;  // staging units per chunk
   constexpr int NG = 3 * KT;                    // MFMA gaps per chunk
+  // A's register ring: RING sets of the NPA pieces, so a chunk's loads are issued RING chunks
+  // before its LDS put (LAB 16: one set, one chunk ahead — the round-3 form)
+  constexpr int RING = (LAB & 16) ? 1 : 2;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -484,14 +487,28 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
 #pragma unroll
   for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
 
-  // ---- the block's G scale s_b: |G| <= hscale · max_m Σ_q |dz[m][q]| · max |P|
-  float gsc, gunsc;
-  {
+  // ---- the block's G scale s_b: |G| <= hscale · max_m Σ_q |dz[m][q]| · max |P|.  The dz rows are
+  // read 4 per thread per pass with clamped indices and no branch around a load, so a pass is one
+  // round trip (the first form's per-row loop waited on every row: ~5 us of the prologue)
+  float gsc = 1.f, gunsc = 1.f;
+  auto scan_scale = [&]() __attribute__((always_inline)) {  // run in the prologue, behind chunk 0's loads
     float zm = 0.f;
-    for (int64_t r = mbeg + tid; r < mend; r += 256) {
-      float s = 0.f;
-      for (int q = 0; q < a.nproj; ++q) s += fabsf(a.dz[r * a.lddz + q]);
-      zm = fmaxf(zm, s);
+    const int nq = a.nproj;
+    for (int64_t r0 = mbeg + tid; r0 < mend; r0 += 4 * 256) {
+      float v[4][MAXPROJ];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = min(r0 + 256 * u, mend - 1);
+#pragma unroll
+        for (int q = 0; q < MAXPROJ; ++q) v[u][q] = a.dz[r * a.lddz + min(q, nq - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < MAXPROJ; ++q) s += q < nq ? fabsf(v[u][q]) : 0.f;
+        zm = fmaxf(zm, r0 + 256 * u < mend ? s : 0.f);
+      }
     }
     float pm = 0.f;
 #pragma unroll
@@ -513,16 +530,16 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     if (bound > 0.f && isfinite(bound)) frexpf(bound, &E);  // bound < 2^E
     gsc = ldexpf(1.0f, 4 - E);                               // |G · gsc| < 16
     gunsc = ldexpf(1.0f, E - 4 - 11);                        // slab = acc · 2^-11 / gsc
-  }
+  };
 
   const int Mi = (int)a.M;
   auto ldbase = [&](int c) __attribute__((always_inline)) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
   const int clast = max(nch - 1, 0);
-  u32x4 ra[NPA];
+  u32x4 ra[RING][NPA];
   float rg[8];
   float rz = 0.f;
-  auto load_a = [&](int j, int c) __attribute__((always_inline)) {
-    ra[j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], ldbase(c) * ld * 2, 0);
+  auto load_a = [&](int s, int j, int c) __attribute__((always_inline)) {
+    ra[s][j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], ldbase(c) * ld * 2, 0);
   };
   auto load_g = [&](int c) __attribute__((always_inline)) {
     uint32_t o = (uint32_t)((ldbase(c) + 8 * go) * hld);
@@ -554,8 +571,8 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
       zsv[i] = dzL[buf][r * MAXPROJ + (gn & (MAXPROJ - 1))];
     }
   };
-  auto put_a = [&](int j, int c) __attribute__((always_inline)) {
-    *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(At[c & 1]) + loff[j]) = ra[j];
+  auto put_a = [&](int s, int j, int c) __attribute__((always_inline)) {
+    *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(At[c & 1]) + loff[j]) = ra[s][j];
   };
   auto g_row = [&](int i, int c, int half) __attribute__((always_inline)) {
     if (half == 0) {
@@ -594,11 +611,14 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   };
   // staging unit k of chunk c + 1 (refills for chunks c + 2 / c + 3); same order as the
   // split-image kernel: A pieces, dz reads, G rows, splits, G write, h loads, dz ring
-  auto unit = [&](int k, int c) __attribute__((always_inline)) {
+  // (par: c's parity, a compile-time constant after inlining — chunk c + 1's pieces sit in set
+  // (c + 1) % RING, refilled with chunk c + 1 + RING)
+  auto unit = [&](int k, int c, int par) __attribute__((always_inline)) {
     constexpr int Z0 = 2 * NPA, G0 = Z0 + 4, S0 = G0 + 16, P0 = S0 + 4;
+    const int sa = RING == 1 ? 0 : (par ^ 1);
     if (k < Z0) {
-      if (k & 1) load_a(k >> 1, min(c + 2, clast));
-      else put_a(k >> 1, c + 1);
+      if (k & 1) load_a(sa, k >> 1, min(c + 1 + RING, clast));
+      else put_a(sa, k >> 1, c + 1);
     } else if (k < G0) {
       z_read(c + 1, 2 * (k - Z0), 2);
     } else if (k < S0) {
@@ -623,7 +643,8 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     return __builtin_bit_cast(f16x8, cat_frag(tr_read(q), tr_read(q + 4 * PT_AP)));
   };
 #define TH_FENCE __builtin_amdgcn_sched_barrier(0)
-  auto compute = [&](int c) __attribute__((always_inline)) {
+  auto compute = [&](int c, auto parc) __attribute__((always_inline)) {
+    constexpr int par = decltype(parc)::value;
     const int buf = c & 1;
     f16x8 gf[3], af[2][2];  // G: hi', hi, lo; A: hi, lo
 #pragma unroll
@@ -647,7 +668,7 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
         TH_FENCE;
         if constexpr (!(LAB & 2)) {
           static_for<(gap + 1) * NU / NG - gap * NU / NG>([&](auto uc) __attribute__((always_inline)) {
-            unit(gap * NU / NG + decltype(uc)::value, c);
+            unit(gap * NU / NG + decltype(uc)::value, c, par);
           });
         }
       });
@@ -668,11 +689,15 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     put_z(1);
     load_z(min(2, clast));
 #pragma unroll
-    for (int j = 0; j < NPA; ++j) load_a(j, 0);
-    load_g(0);
-    __syncthreads();  // dzL
+    for (int j = 0; j < NPA; ++j) load_a(0, j, 0);
+    if constexpr (RING == 2) {
 #pragma unroll
-    for (int j = 0; j < NPA; ++j) put_a(j, 0);
+      for (int j = 0; j < NPA; ++j) load_a(1, j, min(1, clast));
+    }
+    load_g(0);
+    scan_scale();     // (its barrier also publishes dzL)
+#pragma unroll
+    for (int j = 0; j < NPA; ++j) put_a(0, j, 0);
     z_read(0, 0, 8);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -683,12 +708,16 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     for (int j = 0; j < 4; ++j) split_pair(j);
     g_put(0);
 #pragma unroll
-    for (int j = 0; j < NPA; ++j) load_a(j, min(1, clast));
+    for (int j = 0; j < NPA; ++j) load_a(0, j, min(RING, clast));  // set 0: chunk RING (1 or 2)
     load_g(min(1, clast));
     __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-      compute(c);
+    for (int c = 0; c < nch; c += 2) {  // unrolled by 2: the ring's set indices are static
+      compute(c, std::integral_constant<int, 0>{});
       __syncthreads();
+      if (c + 1 < nch) {
+        compute(c + 1, std::integral_constant<int, 1>{});
+        __syncthreads();
+      }
     }
   }
 

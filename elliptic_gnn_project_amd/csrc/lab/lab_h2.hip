@@ -551,6 +551,7 @@ int main(int argc, char** argv) {
       {"NT half-pair no dropout", nth<0, EPIN>, {}},
       {"TN planes (bf16 x6)", tnp<0>, {}}, {"TN planes MFMA only", tnp<2 | 8>, {}},
       {"TN half-pair", tnh<0>, {}}, {"TN half-pair no staging", tnh<2>, {}}, {"TN half-pair no MFMA", tnh<1>, {}},
+      {"TN half-pair ring1", tnh<16>, {}}, {"TN half-pair ring1 no MFMA", tnh<17>, {}},
       {"TN half-pair dma", tnd<0>, {}}, {"TN half-pair dma no MFMA", tnd<1>, {}}, {"TN half-pair dma no G", tnd<2>, {}}};
   for (int r = 0; r < rounds; ++r)
     for (auto& v : vs) {
