@@ -223,7 +223,7 @@ SIGNATURES = {
     "gnn_sage_mean_fwd_h2": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64,
-         c_ptr, c_i64, ctypes.c_float, ctypes.c_uint64, c_ptr, c_ptr],
+         c_ptr, c_i64, ctypes.c_float, ctypes.c_uint64, c_ptr, ctypes.POINTER(GnnGemmNTParams), c_ptr],
     ),
     "gnn_sage_mean_bwd_f32": (
         ctypes.c_int,

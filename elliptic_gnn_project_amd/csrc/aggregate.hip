@@ -112,6 +112,9 @@ struct AggArgs {
   // consumes this image, N = kcols <= 128 columns), bit c of kmask[r·4 + c/32] = keep_elem(seed,
   // r·kcols + c), computed here where the gather leaves the VALU idle
   uint32_t* kmask; int32_t kcols;
+  // K1 of the half-pair path may also carry the consuming NT's B-image prep (gnn_sage_mean_fwd_h2
+  // prep_b): hp.blocks extra blocks at the front of the grid run ws_prep_h2_body, one per k-step
+  H2Prep hp;
 };
 
 __device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
@@ -434,8 +437,15 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 // bf16), 2 = half-pair planes (hi / lo f16, gemm_common.hpp split_h2_pair); VEC even.
 template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, int PLN = 0>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
+  if constexpr (PLN == 2) {  // the NT's B prep rides along (blocks [0, hp.blocks), launched first)
+    if ((int)blockIdx.x < a.hp.blocks) {
+      ws_prep_h2_body<256>(a.hp, (int)blockIdx.x);
+      return;
+    }
+  }
   const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t bid = (int64_t)blockIdx.x - (PLN == 2 ? a.hp.blocks : 0);
+  const int64_t wave = (bid * 256 + threadIdx.x) >> 6;
   const int64_t r0 = wave * rpg;
   if (r0 >= a.nrows) return;
   const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
@@ -1317,7 +1327,8 @@ template <int PLN>
 static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
                                       void* img, int64_t ld, int64_t plane_stride, int64_t width, gnn_stream_t stream,
                                       const char* fn, uint32_t* keep_mask = nullptr, int64_t mask_cols = 0,
-                                      float dropout_p = 0.f, uint64_t seed = 0, const uint64_t* seed_ptr = nullptr) {
+                                      float dropout_p = 0.f, uint64_t seed = 0, const uint64_t* seed_ptr = nullptr,
+                                      const gnn_gemm_nt_params* prep_b = nullptr) {
   if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or deg");
   if (F < 2 || ldx < F || width < F || width > ld || plane_stride < g->num_nodes * ld)
     return fail(GNN_ERR_INVALID_ARG, fn, "bad F / width / leading dimensions");
@@ -1343,6 +1354,11 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
     a.seed = seed;
     a.seed_ptr = reinterpret_cast<const int64_t*>(seed_ptr);
   }
+  if (prep_b) {  // the half-pair NT that reads this image: its B prep joins this launch
+    if (PLN != 2 || prep_b->a_planes != img) return fail(GNN_ERR_INVALID_ARG, fn, "prep_b: the NT must read this half-pair image");
+    const gnn_status s = nt_h2_prep_from_params(prep_b, &a.hp, fn);
+    if (s != GNN_OK) return s;
+  }
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
   const bool v4 = F % 4 == 0 && ldx % 4 == 0 && width % 4 == 0 && ld % 4 == 0 && plane_stride % 4 == 0 &&
                   al(x, 16) && al(img, 8);
@@ -1353,7 +1369,7 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
     return fail(GNN_ERR_UNSUPPORTED, fn, "needs even F, 32 < F / vec, width / vec <= 128 and aligned rows");
   if (a.nrows == 0) return GNN_OK;
   const int rpw = 16;
-  const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
+  const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256) + (unsigned)a.hp.blocks;
   hipStream_t st = (hipStream_t)stream;
   if (vec == 4) agg_wave_kernel<GNN_AGG_MEAN, 4, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
   else agg_wave_kernel<GNN_AGG_MEAN, 2, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
@@ -1369,9 +1385,10 @@ extern "C" gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* 
 extern "C" gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
                                            int64_t F, void* img, int64_t ld, int64_t plane_stride, int64_t width,
                                            uint32_t* keep_mask, int64_t mask_cols, float dropout_p, uint64_t seed,
-                                           const uint64_t* seed_ptr, gnn_stream_t stream) {
+                                           const uint64_t* seed_ptr, const gnn_gemm_nt_params* prep_b,
+                                           gnn_stream_t stream) {
   return sage_mean_fwd_image<2>(g, deg, x, ldx, F, img, ld, plane_stride, width, stream, __func__, keep_mask,
-                                mask_cols, dropout_p, seed, seed_ptr);
+                                mask_cols, dropout_p, seed, seed_ptr, prep_b);
 }
 
 extern "C" gnn_status gnn_sage_mean_bwd_f32(const gnn_graph* g, const float* deg, const float* dout,

@@ -73,6 +73,15 @@ struct NTArgs {
   const uint32_t* kmask;  // optional dropout keep bits (half-pair NT): bit c of kmask[r·4 + c/32]
 };
 
+// the half-pair NT's B-image prep (ws_prep_h2_body below)
+struct H2Prep {
+  const float* w1; const float* w2;  // w2 may be null (k2 = 0)
+  int64_t ldw1, ldw2;
+  int32_t k1, k2, Nc, col2;
+  int32_t blocks;                    // k-steps (= blocks of the prep)
+  uint4* img; float* colscale;
+};
+
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {  // RNE (v_cvt_pk_bf16_f32), NaN stays NaN
   return __builtin_bit_cast(uint16_t, (__bf16)f);
@@ -198,6 +207,10 @@ bool nt_img16_ok(const NTArgs& a);
 void launch_nt_img16(const NTArgs& a, uint4* img, hipStream_t st, int phase = NT_PHASE_ALL);
 // the half-pair forms (f16 hi / lo images, 3 products): gemm_ws.hip / gemm_planes.hip
 bool nt_h2_ok(const NTArgs& a);
+H2Prep h2_prep_of(const NTArgs& a, uint4* img);  // the prep of the half-pair NT a over workspace img
+// the half-pair NT's prep for a caller's NT params (gnn_sage_mean_fwd_h2's prep_b): GNN_OK and
+// *out filled when p selects the half-pair NT with a large enough workspace, else UNSUPPORTED
+gnn_status nt_h2_prep_from_params(const gnn_gemm_nt_params* p, H2Prep* out, const char* fn);
 void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st, int phase = NT_PHASE_ALL);
 bool tn_h2_ok(const TNArgs& a);
 void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st);
@@ -244,5 +257,93 @@ bool launch_nt_skinny(const NTArgs& a, hipStream_t st);
 int tn_skinny_blocks(int64_t M);
 bool tn_skinny_ok(const TNArgs& a);
 void launch_tn_skinny(const TNArgs& a, int nblk, hipStream_t st);
+
+
+// ---- the half-pair NT's B image (K7a-h).  Per k-step s, plane p (hi' = 2^11 hi, hi, lo), slot
+// 2n + khalf: the 8 halves of column n, k = 16s + 8·khalf .. +8, of w_n · 2^-e_n, where 2^-e_n
+// brings the column's largest |w| into [8, 16) (a power of two: exact); colscale[n] = 2^(e_n - 11)
+// (written by the k-step-0 block).  One block per k-step; every block computes all column
+// exponents (max |w_n| over the whole K): NTH/64 waves, a wave's lanes across k (coalesced), in
+// passes of 4 columns whose 48 loads per lane are all issued before the first use (indices
+// clamped into the operand, the excess masked to 0: no load sits behind a branch), then a wave
+// max per column; the block's own k-step is staged in LDS on the way.  (A per-thread walk down
+// each row spent ~30 us on dependent load latency; a linear sweep into LDS atomics ~40 us on
+// same-address ds_max conflicts.)  Needs k1, k2 <= 384 (nt_h2_ok: <= 336).
+__device__ __forceinline__ float h2_col_exp2(float m) {  // 2^e with m · 2^-e in [8, 16); 1 for m = 0
+  if (!(m > 0.f) || !isfinite(m)) return 1.0f;
+  int E;
+  frexpf(m, &E);  // m in [2^(E-1), 2^E)
+  return ldexpf(1.0f, E - 4);
+}
+template <int NTH>
+__device__ __forceinline__ void ws_prep_h2_body(const H2Prep& a, int c) {
+  static_assert(NTH >= 256 && NTH % 256 == 0, "the write phase uses 256 threads");
+  constexpr int NW = NTH / 64, CPW = BN / NW;  // waves, columns per wave
+  __shared__ float sc[BN];
+  __shared__ float slice[BN][17];  // this block's k-step of the image, [column][16 k] (+1: banks)
+  const int tid = threadIdx.x;
+  const int k1m = a.k1 - 1, k2m = a.k2 > 0 ? a.k2 - 1 : 0;
+  const float* w2b = a.w2 ? a.w2 : a.w1;
+  const int64_t ld2 = a.w2 ? a.ldw2 : a.ldw1;
+  for (int i = tid; i < BN * 17; i += NTH) (&slice[0][0])[i] = 0.f;
+  __syncthreads();
+  {
+    const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll 1
+    for (int pass = 0; pass < CPW / 4; ++pass) {
+      float v[4][12];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int nc = min(wave * CPW + pass * 4 + j, a.Nc - 1);
+        const float* w1 = a.w1 + (int64_t)nc * a.ldw1;
+        const float* w2 = w2b + (int64_t)nc * ld2;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          v[j][i] = w1[min(lane + 64 * i, k1m)];
+          v[j][6 + i] = w2[min(lane + 64 * i, k2m)];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float m = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          m = fmaxf(m, lane + 64 * i < a.k1 ? fabsf(v[j][i]) : 0.f);
+          m = fmaxf(m, lane + 64 * i < a.k2 ? fabsf(v[j][6 + i]) : 0.f);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const int n = wave * CPW + pass * 4 + j;
+        if (lane == 0) sc[n] = n < a.Nc ? h2_col_exp2(m) : 1.0f;
+        if (n < a.Nc) {  // the block's k-step: image column kk = 16c + t holds w1[kk] or w2[kk - col2]
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            const int k = lane + 64 * i, t1 = k - 16 * c, t2 = a.col2 + k - 16 * c;
+            if (k < a.k1 && t1 >= 0 && t1 < 16) slice[n][t1] = v[j][i];
+            if (k < a.k2 && t2 >= 0 && t2 < 16) slice[n][t2] = v[j][6 + i];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (c == 0 && tid < BN) a.colscale[tid] = sc[tid] * (1.0f / 2048.0f);
+  if (tid >= 256) return;
+  const int n = tid >> 1, kh = tid & 1;
+  const float inv = 1.0f / sc[n];  // a power of two: exact
+  uint32_t hw[4], lw[4], pw[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float v[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) v[q] = slice[n][8 * kh + 2 * j + q] * inv;
+    split_h2_pair(v[0], v[1], hw[j], lw[j]);
+    pw[j] = h2_scale_pair(hw[j], 2048.0f);
+  }
+  a.img[((int64_t)c * 3 + 0) * 256 + tid] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+  a.img[((int64_t)c * 3 + 1) * 256 + tid] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+  a.img[((int64_t)c * 3 + 2) * 256 + tid] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+}
+constexpr int WS_PREP_THREADS = 1024;
 
 }  // namespace gnnmp

@@ -1010,8 +1010,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
 }
 
 // Whether a call would run the split-image kernels (the caller then needs no f32 A).
-extern "C" int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p) {
-  if (!p || !p->a_planes || p->math == GNN_MATH_F32 || p->mask || p->M < 1) return 0;
+static NTArgs nt_image_args(const gnn_gemm_nt_params* p) {  // the fields the image-A predicates read
   NTArgs a{};
   a.M = p->M; a.Nc = (int32_t)p->N; a.k1 = (int32_t)p->k1; a.k2 = (int32_t)p->k2;
   a.w1 = p->w1; a.w2 = p->w2; a.ldw1 = p->ldw1; a.ldw2 = p->ldw2;
@@ -1023,9 +1022,29 @@ extern "C" int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p) {
   a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
   a.ap_ps = p->planes_stride;
   a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
+  return a;
+}
+
+extern "C" int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p) {
+  if (!p || !p->a_planes || p->math == GNN_MATH_F32 || p->mask || p->M < 1) return 0;
+  const NTArgs a = nt_image_args(p);
   if (a.ap_h2) return nt_h2_ok(a) ? 1 : 0;
   return (a.a_bf16 ? nt_img16_ok(a) : nt_planes_ok(a)) ? 1 : 0;
 }
+
+namespace gnnmp {
+gnn_status nt_h2_prep_from_params(const gnn_gemm_nt_params* p, H2Prep* out, const char* fn) {
+  if (!p || !p->a_planes || p->math == GNN_MATH_F32 || p->mask || p->M < 1 || p->planes_format != GNN_PLANES_HALF_PAIR)
+    return fail(GNN_ERR_UNSUPPORTED, fn, "prep_b needs NT params that select the half-pair NT");
+  const NTArgs a = nt_image_args(p);
+  const size_t img_bytes = (size_t)(a.ap_ld / 16) * 3 * 256 * sizeof(uint4);
+  if (!nt_h2_ok(a) || !p->workspace || p->workspace_bytes < img_bytes + BN * sizeof(float) ||
+      (reinterpret_cast<uintptr_t>(p->workspace) & 15))
+    return fail(GNN_ERR_UNSUPPORTED, fn, "prep_b needs NT params that select the half-pair NT (and its workspace)");
+  *out = h2_prep_of(a, static_cast<uint4*>(p->workspace));
+  return GNN_OK;
+}
+}  // namespace gnnmp
 
 extern "C" int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p) {
   if (!p || !p->a_planes || p->math == GNN_MATH_F32 || p->M < 1 || p->Nr < 1 || p->Nr > 128) return 0;

@@ -441,9 +441,10 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   __shared__ float redm[8];
   constexpr int NU = 2 * NPA + 4 + 16 + 4 + 3;  // staging units per chunk
   constexpr int NG = 3 * KT;                    // MFMA gaps per chunk
-  // A's register ring: RING sets of the NPA pieces, so a chunk's loads are issued RING chunks
-  // before its LDS put (LAB 16: one set, one chunk ahead — the round-3 form)
-  constexpr int RING = (LAB & 16) ? 1 : 2;
+  // A's register ring: RING sets of the NPA pieces, a chunk's loads issued RING chunks before
+  // its LDS put.  LAB 16: two sets — measured slower (lab 104.2 vs 100.6 us, r18h: the second
+  // set's 24 VGPRs cost more in the chunk loop than the extra lead buys)
+  constexpr int RING = (LAB & 16) ? 2 : 1;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;

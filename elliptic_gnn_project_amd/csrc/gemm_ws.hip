@@ -1026,90 +1026,10 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
   }
 }
 
-// B image of the half-pair NT: per k-step s, plane p (hi' = 2^11 hi, hi, lo), slot 2n + khalf:
-// the 8 halves of column n, k = 16s + 8·khalf .. +8, of w_n · 2^-e_n, where 2^-e_n brings the
-// column's largest |w| into [8, 16) (a power of two: exact); colscale[n] = 2^(e_n - 11) (block 0).
-// Every block computes all column exponents (max |w_n| over the whole K): 16 waves x 8 columns, a
-// wave's lanes across k (coalesced), in two passes of 4 columns whose 48 loads per lane are all
-// issued before the first use (indices clamped into the operand, the excess masked to 0: no load
-// sits behind a branch), then a wave max per column.  (A per-thread walk down each row spent
-// ~30 us on dependent load latency; a linear sweep into LDS atomics ~40 us on same-address
-// ds_max conflicts.)
-__device__ __forceinline__ float h2_col_exp2(float m) {  // 2^e with m · 2^-e in [8, 16); 1 for m = 0
-  if (!(m > 0.f) || !isfinite(m)) return 1.0f;
-  int E;
-  frexpf(m, &E);  // m in [2^(E-1), 2^E)
-  return ldexpf(1.0f, E - 4);
-}
-constexpr int WS_PREP_THREADS = 1024;
-__global__ __launch_bounds__(WS_PREP_THREADS) void ws_prep_h2_kernel(NTArgs a, uint4* __restrict__ img,
-                                                                     float* __restrict__ colscale, int col2) {
-  __shared__ float sc[BN];
-  __shared__ float slice[BN][17];  // this block's k-step of the image, [column][16 k] (+1: banks)
-  const int tid = threadIdx.x;
-  const int c = blockIdx.x;
-  const int k2m = a.k2 > 0 ? a.k2 - 1 : 0;
-  const float* w2b = a.w2 ? a.w2 : a.w1;
-  const int64_t ld2 = a.w2 ? a.ldw2 : a.ldw1;
-  for (int i = tid; i < BN * 17; i += WS_PREP_THREADS) (&slice[0][0])[i] = 0.f;
-  __syncthreads();
-  {
-    const int wave = tid >> 6, lane = tid & 63;
-    const int k1m = a.k1 - 1;
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      float v[4][12];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int nc = min(wave * 8 + pass * 4 + j, a.Nc - 1);
-        const float* w1 = a.w1 + (int64_t)nc * a.ldw1;
-        const float* w2 = w2b + (int64_t)nc * ld2;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          v[j][i] = w1[min(lane + 64 * i, k1m)];
-          v[j][6 + i] = w2[min(lane + 64 * i, k2m)];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float m = 0.f;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          m = fmaxf(m, lane + 64 * i < a.k1 ? fabsf(v[j][i]) : 0.f);
-          m = fmaxf(m, lane + 64 * i < a.k2 ? fabsf(v[j][6 + i]) : 0.f);
-        }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        const int n = wave * 8 + pass * 4 + j;
-        if (lane == 0) sc[n] = n < a.Nc ? h2_col_exp2(m) : 1.0f;
-        if (n < a.Nc) {  // the block's k-step: image column kk = 16c + t holds w1[kk] or w2[kk - col2]
-#pragma unroll
-          for (int i = 0; i < 6; ++i) {
-            const int k = lane + 64 * i, t1 = k - 16 * c, t2 = col2 + k - 16 * c;
-            if (k < a.k1 && t1 >= 0 && t1 < 16) slice[n][t1] = v[j][i];
-            if (k < a.k2 && t2 >= 0 && t2 < 16) slice[n][t2] = v[j][6 + i];
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (blockIdx.x == 0 && tid < BN) colscale[tid] = sc[tid] * (1.0f / 2048.0f);
-  if (tid >= 256) return;
-  const int n = tid >> 1, kh = tid & 1;
-  const float inv = 1.0f / sc[n];  // a power of two: exact
-  uint32_t hw[4], lw[4], pw[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float v[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) v[q] = slice[n][8 * kh + 2 * j + q] * inv;
-    split_h2_pair(v[0], v[1], hw[j], lw[j]);
-    pw[j] = h2_scale_pair(hw[j], 2048.0f);
-  }
-  img[((int64_t)c * 3 + 0) * 256 + tid] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
-  img[((int64_t)c * 3 + 1) * 256 + tid] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-  img[((int64_t)c * 3 + 2) * 256 + tid] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+// B image of the half-pair NT (gemm_common.hpp ws_prep_h2_body): the standalone launch, one
+// 1024-thread block per k-step.  (K1 can also carry it: gnn_sage_mean_fwd_h2's prep_b.)
+__global__ __launch_bounds__(WS_PREP_THREADS) void ws_prep_h2_kernel(H2Prep p) {
+  ws_prep_h2_body<WS_PREP_THREADS>(p, (int)blockIdx.x);
 }
 
 // ---------------------------------------------------------------- bf16 image form (K7a-b)
@@ -1461,11 +1381,21 @@ bool nt_h2_ok(const NTArgs& a) {
   return true;
 }
 
+H2Prep h2_prep_of(const NTArgs& a, uint4* img) {
+  H2Prep p{};
+  p.w1 = a.w1; p.w2 = a.w2; p.ldw1 = a.ldw1; p.ldw2 = a.ldw2;
+  p.k1 = a.k1; p.k2 = a.k2; p.Nc = a.Nc; p.col2 = a.ap_col2;
+  p.blocks = a.ap_ld / 16;
+  p.img = img;
+  p.colscale = reinterpret_cast<float*>(img + p.blocks * 3 * 256);
+  return p;
+}
+
 // workspace: the B image (NKS k-steps x 3 planes x 256 slots x 16 B), then the 128 column scales
 template <int NKS>
 void launch_nt_h2_k(const NTArgs& a, uint4* img, hipStream_t st, int phase) {
   float* colscale = reinterpret_cast<float*>(img + NKS * 3 * 256);
-  if (phase & NT_PHASE_PREP) ws_prep_h2_kernel<<<NKS, WS_PREP_THREADS, 0, st>>>(a, img, colscale, a.ap_col2);
+  if (phase & NT_PHASE_PREP) ws_prep_h2_kernel<<<NKS, WS_PREP_THREADS, 0, st>>>(h2_prep_of(a, img));
   if (!(phase & NT_PHASE_RUN)) return;
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
   const int grid = std::min(ntiles, ws_num_cus());

@@ -431,10 +431,10 @@ int main(int argc, char** argv) {
   uint4* bimg;
   CK(hipMalloc(&bimg, 21 * 3 * 256 * 16));
   ws_prep_kernel<<<21, 256>>>(n, bimg, 21, nullptr, 0, 168);
-  CK(hipMalloc(&g_bh, 21 * 3 * 256 * 16));
-  CK(hipMalloc(&g_cs, 128 * 4));
+  CK(hipMalloc(&g_bh, 21 * 3 * 256 * 16 + 128 * 4));
+  g_cs = reinterpret_cast<float*>(g_bh + 21 * 3 * 256);  // the column scales follow the image (h2_prep_of)
   g_h = n; g_h.ap = imh; g_h.c = c2; g_h.z = z2;
-  ws_prep_h2_kernel<<<21, 256>>>(g_h, g_bh, g_cs, 168);
+  ws_prep_h2_kernel<<<21, WS_PREP_THREADS>>>(h2_prep_of(g_h, g_bh));
   const int ntiles = (int)ceil_div(M, 32);
 
   // accuracy: no dropout (deterministic), C vs float64 on sampled rows
@@ -551,7 +551,7 @@ int main(int argc, char** argv) {
       {"NT half-pair no dropout", nth<0, EPIN>, {}},
       {"TN planes (bf16 x6)", tnp<0>, {}}, {"TN planes MFMA only", tnp<2 | 8>, {}},
       {"TN half-pair", tnh<0>, {}}, {"TN half-pair no staging", tnh<2>, {}}, {"TN half-pair no MFMA", tnh<1>, {}},
-      {"TN half-pair ring1", tnh<16>, {}}, {"TN half-pair ring1 no MFMA", tnh<17>, {}},
+      {"TN half-pair ring2", tnh<16>, {}}, {"TN half-pair ring2 no MFMA", tnh<17>, {}},
       {"TN half-pair dma", tnd<0>, {}}, {"TN half-pair dma no MFMA", tnd<1>, {}}, {"TN half-pair dma no G", tnd<2>, {}}};
   for (int r = 0; r < rounds; ++r)
     for (auto& v : vs) {

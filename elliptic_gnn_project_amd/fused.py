@@ -42,10 +42,14 @@ _H2 = os.environ.get("GNNMP_H2", "1") != "0"
 # instead of hashing.  Off by default: measured (profiles/r18f, rocprofv3) the NT at 88.8 us with the
 # bits vs 89.6 us hashing, while writing them costs K1 6.5 us (110.0 vs 103.5 us).
 _KEEP_MASK = os.environ.get("GNNMP_KEEP_MASK", "0") == "1"
-# The SAGE layer-0 NT's weight prep (the B image: ~11 us of latency-bound work over the weights
-# only) runs on a side stream beside K1 (the aggregation that writes the NT's A image), joined
-# before the NT; GNNMP_SIDE_PREP=0 keeps it in line, inside the NT call (A/B)
-_SIDE_PREP = os.environ.get("GNNMP_SIDE_PREP", "1") != "0"
+# The SAGE layer-0 half-pair NT's weight prep (its B image) rides in K1's launch on extra blocks
+# beside the gather (gnn_sage_mean_fwd_h2 prep_b); GNNMP_K1_PREP=0 leaves it to the NT call (A/B)
+_K1_PREP = os.environ.get("GNNMP_K1_PREP", "1") != "0"
+# GNNMP_SIDE_PREP=1: the SAGE layer-0 NT's weight prep (the B image, latency-bound work over the
+# weights only) on a side stream beside K1, joined before the NT.  Off by default: measured
+# (profiles/r18h) 0.3692 vs 0.3637 ms per step in line — the captured fork / join costs more than
+# the prep it hides, as in round 3
+_SIDE_PREP = os.environ.get("GNNMP_SIDE_PREP", "0") == "1"
 _SIDE_STREAMS = {}
 
 
@@ -114,13 +118,14 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
     ``keep_mask`` (half-pair planes with dropout): the keep bits K1 wrote for this call's seed.
     ``b_stage`` (image-A forms, with an explicit ``workspace``): "prep" launches only the B-image
     prep (gnn_gemm_nt_prep_b; returns None), "ready" only the GEMM over the image a "prep" call of
-    the same weights left in ``workspace``."""
+    the same weights left in ``workspace``; "params" launches nothing and returns the call's
+    GnnGemmNTParams (K1's prep_b: HalfPairImage.fill_mean)."""
     if planes is not None:
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
         M, k1, k2, dev = a1.size(0), a1.size(1), (a2.size(1) if a2 is not None else 0), a1.device
     bf = getattr(planes, "bf16", False) or (a1 is not None and a1.dtype == torch.bfloat16)
-    if out is None and want_c and not check_planes and b_stage != "prep":
+    if out is None and want_c and not check_planes and b_stage not in ("prep", "params"):
         out = torch.empty((M, n), dtype=torch.bfloat16 if bf else torch.float32, device=dev)
     ws = workspace
     if ws is None and w1 is not None:  # B pre-split image for the streaming split-bf16 kernel (≈24 KB per 32 of K)
@@ -143,6 +148,8 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
     )
     if check_planes:
         return bool(_lib.load().gnn_gemm_nt_planes_ok(p))
+    if b_stage == "params":
+        return p
     if b_stage == "prep":
         _lib.call("gnn_gemm_nt_prep_b", p, _lib.stream_handle(dev))
         return None
@@ -335,16 +342,21 @@ class _FusedSAGE(torch.autograd.Function):
                     keep = (kb, Wl[l].size(0), train_drop, seeds[l], seed_ctr)
                     nt_kw = dict(nt_kw, keep_mask=kb)
                 n_out = Wl[l].size(0)
-                ws, side = _nt_workspace(h.device, n_out, im.k1, im.k2), None
-                if _SIDE_PREP:  # the B prep beside K1 (it reads only the weights)
+                ws, side, ready = _nt_workspace(h.device, n_out, im.k1, im.k2), None, False
+                prep_b = None
+                if _K1_PREP and isinstance(im, HalfPairImage):  # the B prep inside K1's launch
+                    prep_b = gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="params", **nt_kw)
+                    ready = True
+                elif _SIDE_PREP:  # the B prep beside K1 on a side stream (it reads only the weights)
                     side, cur = _side_stream(h.device), torch.cuda.current_stream(h.device)
                     side.wait_stream(cur)
                     with torch.cuda.stream(side):
                         gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="prep", **nt_kw)
-                ctx.image = (im, im.fill_mean(plan, h, keep))
+                    ready = True
+                ctx.image = (im, im.fill_mean(plan, h, keep, prep_b=prep_b))
                 if side is not None:
                     cur.wait_stream(side)
-                hn = gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="ready" if side else None, **nt_kw)
+                hn = gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="ready" if ready else None, **nt_kw)
                 agg = None
             else:
                 agg = aggregate(plan, h, _lib.AGG_MEAN, nodew=plan.deg)

@@ -72,10 +72,12 @@ class SplitImage:
             _lib.call(self._split_fn, x.data_ptr(), int(x.stride(0)), self.n, self.k2, self.ptr, self.ld,
                       self.ps, self.col2, self.ld - self.col2, _lib.stream_handle(x.device))
 
-    def fill_mean(self, plan, x: torch.Tensor, keep=None) -> int:
+    def fill_mean(self, plan, x: torch.Tensor, keep=None, prep_b=None) -> int:
         """K1: planes of mean_{j->i} x[j] into columns [0, col2); returns the new generation.
         keep (half-pair images only): (mask [N, 4] int32, cols, p, seed, seed_ptr) — K1 also writes
-        the dropout keep bits of the NT that reads this image (include/gnnmp.h gnn_sage_mean_fwd_h2)."""
+        the dropout keep bits of the NT that reads this image (include/gnnmp.h gnn_sage_mean_fwd_h2).
+        prep_b (half-pair images only): the GnnGemmNTParams of that NT (fused.gemm_nt b_stage
+        "params"); its B-image prep runs inside K1's launch, the NT then runs with b_ready."""
         from .aggregation import KernelTimer, agg_bytes
 
         e0 = KernelTimer.begin()
@@ -83,7 +85,9 @@ class SplitImage:
                 self.ps, self.col2)
         if self.nplanes == 2:
             km, cols, p, seed, sptr = keep if keep is not None else (None, 0, 0.0, 0, None)
-            args += (_lib.ptr(km), int(cols), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(sptr))
+            args += (_lib.ptr(km), int(cols), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(sptr), prep_b)
+        elif prep_b is not None:
+            raise ValueError("prep_b needs a half-pair image")
         _lib.call(self._mean_fn, *args, _lib.stream_handle(x.device))
         # algorithmic bytes of K1 as SURVEY §8(d) counts them (f32 output); the planes store 6 B
         KernelTimer.end(e0, ("agg", _lib.AGG_MEAN, False, self.k1), agg_bytes(plan, self.k1, _lib.AGG_MEAN, False, False))

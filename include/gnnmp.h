@@ -201,11 +201,16 @@ gnn_status gnn_split_h2_f32(const float* x, int64_t ldx, int64_t rows, int64_t F
 /* gnn_sage_mean_fwd_h2 optionally also writes the dropout keep bits of the NT that consumes the
  * image (keep_mask != NULL, [num_nodes][4] uint32, 16-byte aligned): bit c of keep_mask[r*4 + c/32]
  * = keep_elem(seed', r*mask_cols + c) with seed' the NT's (seed, seed_ptr) rule — the mask the NT
- * would hash itself, computed where the gather leaves the VALU idle (gnn_gemm_nt_params.keep_mask). */
+ * would hash itself, computed where the gather leaves the VALU idle (gnn_gemm_nt_params.keep_mask).
+ * prep_b (optional): the params of the half-pair NT that reads this image (a_planes == img); its
+ * B-image prep (gnn_gemm_nt_prep_b) runs inside this launch, on extra blocks beside the gather,
+ * for a later gnn_gemm_nt_f32 of the same params with b_ready = 1.  UNSUPPORTED when the params
+ * do not select the half-pair NT. */
+struct gnn_gemm_nt_params;
 gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
                                 void* img, int64_t ld, int64_t plane_stride, int64_t width, uint32_t* keep_mask,
                                 int64_t mask_cols, float dropout_p, uint64_t seed, const uint64_t* seed_ptr,
-                                gnn_stream_t stream);
+                                const struct gnn_gemm_nt_params* prep_b, gnn_stream_t stream);
 typedef enum {
   GNN_PLANES_SPLIT_BF16 = 0,  /* 3 bf16 planes hi / mid / lo (gnn_split_planes_f32) */
   GNN_PLANES_HALF_PAIR = 1    /* 2 f16 planes hi / lo (gnn_split_h2_f32) */
@@ -328,7 +333,7 @@ typedef enum {
  * gnn.py:23,66,124): NT with N <= 8 (K <= 384) or with K <= 8 (one A segment), f32 A/C and no
  * projection; TN with Nr <= 8 in the plain g form (no dz/proj, h or gout) and f32 A. */
 
-typedef struct {
+typedef struct gnn_gemm_nt_params {
   int64_t M, N;                          /* C is [M, N] */
   const float* a1; int64_t lda1; int64_t k1;
   const float* a2; int64_t lda2; int64_t k2;   /* optional 2nd K segment: A = [A1 | A2] (k2 = 0: none) */

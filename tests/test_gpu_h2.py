@@ -161,6 +161,59 @@ def test_nt_prep_b_then_ready_equals_one_call(device, fmt):
     assert torch.equal(one, two)
 
 
+def test_k1_prep_b_then_ready_equals_one_call(device):
+    """The half-pair NT's B prep carried by K1's launch (gnn_sage_mean_fwd_h2 prep_b), then the NT
+    with b_ready: the image and C bit-identical to K1 alone + the one-call NT."""
+    from elliptic_gnn_project_amd.fused import _nt_workspace, gemm_nt
+
+    data, plan, x = _plan_and_x(20_000, 30_000, 5, device)
+    n = 128
+    g = torch.Generator().manual_seed(11)
+    w1 = (torch.randn(n, x.size(1), generator=g) * 0.08).to(device)
+    w2 = (torch.randn(n, x.size(1), generator=g) * 0.08).to(device)
+    kw = dict(w1=w1, w2=w2, bias=torch.randn(n, generator=g).to(device), relu=True, dropout_p=0.5, seed=9)
+    from elliptic_gnn_project_amd.planes import HalfPairImage
+
+    im = HalfPairImage(x.size(0), x.size(1), x.size(1), device)
+    im.fill_x(x)
+    im.fill_mean(plan, x)
+    img0 = im.img.clone()
+    one = gemm_nt(None, None, n, planes=im, **kw)
+    ws = _nt_workspace(device, n, im.k1, im.k2)
+    p = gemm_nt(None, None, n, planes=im, workspace=ws, b_stage="params", **kw)
+    im.fill_mean(plan, x, prep_b=p)
+    assert torch.equal(im.img, img0)
+    two = gemm_nt(None, None, n, planes=im, workspace=ws, b_stage="ready", **kw)
+    assert torch.equal(one, two)
+
+
+def test_fused_sage_k1_prep_equals_nt_prep(device):
+    """The SAGE train step with the layer-0 B prep inside K1's launch (default) and inside the NT
+    call (GNNMP_K1_PREP=0): bit-identical logits and gradients."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data, plan, x = _plan_and_x(20_000, 30_000, 5, device)
+    ei = data.edge_index.to(device)
+    torch.manual_seed(3)
+    model = SAGENet(x.size(1), 128, layers=2, dropout=0.5).to(device).train()
+    res = []
+    saved = fused._K1_PREP
+    for on in (True, False):
+        fused._K1_PREP = on
+        try:
+            model.zero_grad()
+            out, loss = _sage_step(model, x, ei, 79)
+            loss.backward()
+            res.append((out.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()}))
+        finally:
+            fused._K1_PREP = saved
+    (o1, g1), (o2, g2) = res
+    assert torch.equal(o1, o2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+
+
 def test_fused_sage_side_prep_equals_inline(device):
     """The SAGE train step with the layer-0 B prep on the side stream (default) and in line
     (GNNMP_SIDE_PREP=0): bit-identical logits and gradients."""
@@ -172,7 +225,8 @@ def test_fused_sage_side_prep_equals_inline(device):
     torch.manual_seed(3)
     model = SAGENet(x.size(1), 128, layers=2, dropout=0.5).to(device).train()
     res = []
-    saved = fused._SIDE_PREP
+    saved, saved_k1 = fused._SIDE_PREP, fused._K1_PREP
+    fused._K1_PREP = False
     for on in (True, False):
         fused._SIDE_PREP = on
         try:
@@ -182,6 +236,7 @@ def test_fused_sage_side_prep_equals_inline(device):
             res.append((out.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()}))
         finally:
             fused._SIDE_PREP = saved
+    fused._K1_PREP = saved_k1
     (o1, g1), (o2, g2) = res
     assert torch.equal(o1, o2)
     for k in g1:

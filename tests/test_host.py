@@ -110,6 +110,27 @@ def test_prep_b_needs_an_image_form(lib):
     assert lib.gnn_gemm_nt_f32(p, None) == 1
 
 
+def test_k1_prep_b_needs_the_half_pair_nt(lib):
+    """gnn_sage_mean_fwd_h2's prep_b is refused before any launch unless the NT params select the
+    half-pair NT over this very image (pointers never read)."""
+    import ctypes
+
+    from elliptic_gnn_project_amd import _lib
+
+    fake, N, F, ld = 1 << 20, 1000, 166, 336
+    g = _lib.GnnGraph(N, 2000, fake, fake, fake, fake, fake, None, None)
+    p = _lib.GnnGemmNTParams(N, 128, None, 0, 166, None, 0, 166, None, 0, fake, fake, 166, 166, fake, 128)
+    p.math = _lib.MATH_SPLIT_BF16
+    p.a_planes, p.planes_ld, p.planes_stride, p.planes_col2 = fake, ld, N * ld, 168
+    args = (ctypes.byref(g), fake, fake, F, F, fake, ld, N * ld, 168, None, 0, 0.0, 0, None)
+    p.planes_format = _lib.PLANES_SPLIT_BF16  # not the half-pair NT
+    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 5
+    p.planes_format = _lib.PLANES_HALF_PAIR  # no workspace
+    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 5
+    p.a_planes = fake + 4096  # another image
+    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 1
+
+
 STRUCTS = {
     "gnn_split": ("GnnSplit", ["seg_len", "reserved", "num_long", "num_pieces", "ptr", "nbr", "piece0",
                                "piece_seg", "long_seg", "order"]),
