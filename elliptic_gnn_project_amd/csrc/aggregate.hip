@@ -439,7 +439,7 @@ template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, int PLN = 0>  
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   if constexpr (PLN == 2) {  // the NT's B prep rides along (blocks [0, hp.blocks), launched first)
     if ((int)blockIdx.x < a.hp.blocks) {
-      ws_prep_h2_body<256>(a.hp, (int)blockIdx.x);
+      ws_prep_h2_body<256, 1>(a.hp, (int)blockIdx.x);
       return;
     }
   }

@@ -275,10 +275,13 @@ __device__ __forceinline__ float h2_col_exp2(float m) {  // 2^e with m · 2^-e i
   frexpf(m, &E);  // m in [2^(E-1), 2^E)
   return ldexpf(1.0f, E - 4);
 }
-template <int NTH>
+// CPP: columns per pass (12·CPP loads in flight per lane; K1's copy runs CPP = 1 so the gather
+// kernel it rides in keeps its register budget and occupancy)
+template <int NTH, int CPP = 4>
 __device__ __forceinline__ void ws_prep_h2_body(const H2Prep& a, int c) {
   static_assert(NTH >= 256 && NTH % 256 == 0, "the write phase uses 256 threads");
   constexpr int NW = NTH / 64, CPW = BN / NW;  // waves, columns per wave
+  static_assert(CPW % CPP == 0, "whole passes");
   __shared__ float sc[BN];
   __shared__ float slice[BN][17];  // this block's k-step of the image, [column][16 k] (+1: banks)
   const int tid = threadIdx.x;
@@ -290,11 +293,11 @@ __device__ __forceinline__ void ws_prep_h2_body(const H2Prep& a, int c) {
   {
     const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll 1
-    for (int pass = 0; pass < CPW / 4; ++pass) {
-      float v[4][12];
+    for (int pass = 0; pass < CPW / CPP; ++pass) {
+      float v[CPP][12];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int nc = min(wave * CPW + pass * 4 + j, a.Nc - 1);
+      for (int j = 0; j < CPP; ++j) {
+        const int nc = min(wave * CPW + pass * CPP + j, a.Nc - 1);
         const float* w1 = a.w1 + (int64_t)nc * a.ldw1;
         const float* w2 = w2b + (int64_t)nc * ld2;
 #pragma unroll
@@ -304,7 +307,7 @@ __device__ __forceinline__ void ws_prep_h2_body(const H2Prep& a, int c) {
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < CPP; ++j) {
         float m = 0.f;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -313,7 +316,7 @@ __device__ __forceinline__ void ws_prep_h2_body(const H2Prep& a, int c) {
         }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        const int n = wave * CPW + pass * 4 + j;
+        const int n = wave * CPW + pass * CPP + j;
         if (lane == 0) sc[n] = n < a.Nc ? h2_col_exp2(m) : 1.0f;
         if (n < a.Nc) {  // the block's k-step: image column kk = 16c + t holds w1[kk] or w2[kk - col2]
 #pragma unroll
