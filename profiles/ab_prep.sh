@@ -7,8 +7,8 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_k1prep.log" 2>&1 || { tail -5 "$OUT/bench_k1prep.log"; exit 1; }
 GNNMP_K1_PREP=0 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_ntprep.log" 2>&1 || exit 1
-GNNMP_K1_PREP=0 GNNMP_SIDE_PREP=1 timeout -k 10 300 python bench.py --no-cpu-baseline > "$OUT/bench_sideprep.log" 2>&1 || exit 1
-for f in k1prep ntprep sideprep; do python3 -c "
+
+for f in k1prep ntprep; do python3 -c "
 import json; d=json.loads(open('$OUT/bench_$f.log').read().strip().splitlines()[-1])
 t=d['roofline']['timed_kernels']; print('$f', round(d['ms_per_step'],4), d['roofline']['frac'], {k: v['us_per_launch'] for k,v in t.items()})"; done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv \
