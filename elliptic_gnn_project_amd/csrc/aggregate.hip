@@ -155,10 +155,17 @@ __device__ __forceinline__ void contrib(const AggArgs& a, int32_t n, int32_t r, 
   }
 }
 
-// contrib with the neighbour's node weight already loaded (wn = nodew[n]): same arithmetic
-template <int MODE, int VEC>
+// contrib with the neighbour's node weight already loaded (wn = nodew[n]): same arithmetic.
+// BF (bf16 storage, the result rounded to bf16): MEAN_BWD multiplies by one correctly rounded
+// reciprocal per slot (<= 1 f32 ulp from the quotient, far below the bf16 store's rounding) — the
+// per-element IEEE division's ~10 VALU ops bound the F = 128 meanᵀ of configs[4]
+template <int MODE, int VEC, bool BF = false>
 __device__ __forceinline__ void contrib_w(const AggArgs& a, float wn, int32_t r, float (&v)[VEC]) {
-  if constexpr (MODE == GNN_AGG_MEAN_BWD) {
+  if constexpr (MODE == GNN_AGG_MEAN_BWD && BF) {
+    const float rd = 1.0f / fmaxf(wn, 1.0f);
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) v[q] = v[q] * rd;
+  } else if constexpr (MODE == GNN_AGG_MEAN_BWD) {
     const float d = fmaxf(wn, 1.0f);
 #pragma unroll
     for (int q = 0; q < VEC; ++q) v[q] = v[q] / d;
@@ -592,7 +599,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
       }
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
-        if constexpr (SW) contrib_w<MODE, VEC>(a, dn[u], crow, v[u][i]);
+        if constexpr (SW) contrib_w<MODE, VEC, BF>(a, dn[u], crow, v[u][i]);
         else contrib<MODE, VEC>(a, n[u], crow, k, coff[i], v[u][i]);
 #pragma unroll
         for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];

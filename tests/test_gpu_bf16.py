@@ -42,6 +42,29 @@ def test_aggregate_bf16_mean(device, F):
     assert float((d <= BF_ULP * ref.abs() + 1e-30).double().mean()) == 1.0, float(d.max())
 
 
+@pytest.mark.parametrize("F", [128, 166])
+def test_aggregate_bf16_mean_bwd(device, F):
+    """The bf16 transposed mean (meanᵀ of the bf16-storage backward, one reciprocal per slot):
+    every output within one bf16 ulp of the float64 meanᵀ, on a graph with hub rows."""
+    from elliptic_gnn_project_amd import _lib
+    from elliptic_gnn_project_amd.aggregation import aggregate
+    from elliptic_gnn_project_amd.graph import get_plan
+
+    g = torch.Generator().manual_seed(F + 1)
+    N, E = 4000, 12000
+    ei = torch.randint(0, N, (2, E), generator=g)
+    ei[1, :600] = 7  # a hub destination (in-degree >= 600)
+    x = torch.randn(N, F, generator=g).to(torch.bfloat16)
+    deg = torch.bincount(ei[1], minlength=N).double().clamp_min(1.0)
+    ref = torch.zeros(N, F, dtype=torch.float64).index_add_(0, ei[0], (x.double() / deg[:, None])[ei[1]])
+    plan = get_plan(ei.to(device), N, _lib.LOOPS_KEEP)
+    y = aggregate(plan, x.to(device), _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg)
+    assert y.dtype == torch.bfloat16
+    d = (y.double().cpu() - ref).abs()
+    assert float((d <= 2 * BF_ULP * ref.abs() + 1e-30).double().mean()) == 1.0, float(d.max())  # 1 ulp
+    assert float((d <= BF_ULP * ref.abs() + 1e-30).double().mean()) > 0.999  # RNE's half ulp, but for ties
+
+
 @pytest.mark.parametrize("M,k1,k2,n", [(3000, 166, 166, 128), (777, 128, 128, 64), (129, 30, 0, 2)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu_proj"])
 def test_gemm_nt_bf16(device, M, k1, k2, n, epi):
