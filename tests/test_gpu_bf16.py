@@ -61,7 +61,8 @@ def test_aggregate_bf16_mean_bwd(device, F):
     y = aggregate(plan, x.to(device), _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg)
     assert y.dtype == torch.bfloat16
     d = (y.double().cpu() - ref).abs()
-    assert float((d <= 2 * BF_ULP * ref.abs() + 1e-30).double().mean()) == 1.0, float(d.max())  # 1 ulp
+    mag = torch.maximum(ref.abs(), y.double().cpu().abs())  # one ulp of the larger: a flip may cross a binade
+    assert float((d <= 2 * BF_ULP * mag + 1e-30).double().mean()) == 1.0, float(d.max())
     assert float((d <= BF_ULP * ref.abs() + 1e-30).double().mean()) > 0.999  # RNE's half ulp, but for ties
 
 
