@@ -99,19 +99,66 @@ struct AdamTable {
 // elements (partial[kAdamBlocks + 1 + block]); block 0 also keeps the step count before this
 // call in partial[kAdamBlocks] (clip_adam_kernel advances step[0] once it knows the step is
 // taken: no block reads step[0] while another may write it).
+// The block's tensor table staged in LDS once (the kernel-argument table indexed by a run-time
+// tensor id compiled to a dependent load of the pointer per element), and a thread's elements of
+// the block's slice (<= kAdamUnroll of them: all parameter lists of the path fit one pass at 64
+// blocks) located by a walk in LDS, so every value load is issued before the first use.
+constexpr int kAdamUnroll = 4;
+struct AdamLds {
+  int64_t off[GNN_ADAM_MAX_TENSORS + 1];
+  float* p[GNN_ADAM_MAX_TENSORS];
+  float* g[GNN_ADAM_MAX_TENSORS];
+  float* m[GNN_ADAM_MAX_TENSORS];
+  float* v[GNN_ADAM_MAX_TENSORS];
+};
+__device__ __forceinline__ void adam_stage(const AdamTable& tb, AdamLds& L) {
+  const int t = threadIdx.x;
+  if (t <= tb.n) L.off[t] = tb.off[t];
+  if (t < tb.n) {
+    L.p[t] = tb.p[t];
+    L.g[t] = tb.g[t];
+    L.m[t] = tb.m[t];
+    L.v[t] = tb.v[t];
+  }
+  __syncthreads();
+}
+// tensor ids and in-tensor offsets of elements e, e + T, ... (clamped into [e0, e1); valid[u] marks real ones)
+__device__ __forceinline__ void adam_locate(const AdamLds& L, int n, int64_t e, int64_t e1, int (&j)[kAdamUnroll],
+                                            int64_t (&i)[kAdamUnroll], bool (&valid)[kAdamUnroll]) {
+  int jj = 0;
+#pragma unroll
+  for (int u = 0; u < kAdamUnroll; ++u) {
+    const int64_t eu = e + (int64_t)u * kAdamThreads;
+    valid[u] = eu < e1;
+    const int64_t ec = valid[u] ? eu : e;
+    while (jj + 1 < n && ec >= L.off[jj + 1]) ++jj;
+    j[u] = jj;
+    i[u] = ec - L.off[jj];
+  }
+}
+
 __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, float* __restrict__ partial,
                                                                 const float* __restrict__ step) {
   __shared__ float sh[kAdamThreads / 64];
-  const int64_t total = tb.off[tb.n];
+  __shared__ AdamLds L;
+  adam_stage(tb, L);
+  const int64_t total = L.off[tb.n];
   const int64_t per = (total + gridDim.x - 1) / gridDim.x;
   const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(total, e0 + per);
   float s = 0.f, nf = 0.f;
-  int j = 0;
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamThreads) {
-    while (e >= tb.off[j + 1]) ++j;
-    const float g = tb.g[j][e - tb.off[j]];
-    s = fmaf(g, g, s);
-    nf += isfinite(g) ? 0.f : 1.f;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamUnroll * kAdamThreads) {
+    int j[kAdamUnroll];
+    int64_t i[kAdamUnroll];
+    bool ok[kAdamUnroll];
+    adam_locate(L, tb.n, e, e1, j, i, ok);
+    float g[kAdamUnroll];
+#pragma unroll
+    for (int u = 0; u < kAdamUnroll; ++u) g[u] = L.g[j[u]][i[u]];
+#pragma unroll
+    for (int u = 0; u < kAdamUnroll; ++u) {  // in element order, as the one-at-a-time loop summed
+      s = ok[u] ? fmaf(g[u], g[u], s) : s;
+      nf += (ok[u] && !isfinite(g[u])) ? 1.f : 0.f;
+    }
   }
   const float t = block_sum(s, sh);
   __syncthreads();  // sh reused
@@ -136,6 +183,8 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
                                                                   float* __restrict__ norm_out, int skip_nonfinite) {
   __shared__ float coef_sh;
   __shared__ int skip_sh;
+  __shared__ AdamLds L;
+  adam_stage(tb, L);
   if (threadIdx.x < 64) {  // the nblk <= 64 partials: one per lane, fixed butterfly (same in every block)
     float tot = threadIdx.x < nblk ? partial[threadIdx.x] : 0.f;
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
@@ -162,23 +211,34 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
   const float neg_step = (float)(-lr / bc1), bc2s = (float)sqrt(bc2);
   const float b2 = (float)beta2, omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
   const float epsf = (float)eps, wdf = (float)wd;
-  const int64_t total = tb.off[tb.n];
+  const int64_t total = L.off[tb.n];
   const int64_t per = (total + gridDim.x - 1) / gridDim.x;
   const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(total, e0 + per);
-  int j = 0;
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamThreads) {
-    while (e >= tb.off[j + 1]) ++j;
-    const int64_t i = e - tb.off[j];
-    float g = tb.g[j][i] * coef;
-    tb.g[j][i] = g;  // clip_grad_norm_ scales .grad in place
-    const float p = tb.p[j][i];
-    if (wdf != 0.f) g = g + wdf * p;  // Adam (not AdamW) weight decay: grad.add(param, alpha=wd)
-    const float m0 = tb.m[j][i];
-    const float m = fmaf(omb1, g - m0, m0);  // exp_avg.lerp_(grad, 1 - beta1)
-    const float v = tb.v[j][i] * b2 + omb2 * g * g;
-    tb.m[j][i] = m;
-    tb.v[j][i] = v;
-    tb.p[j][i] = p + neg_step * (m / (sqrtf(v) / bc2s + epsf));
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamUnroll * kAdamThreads) {
+    int j[kAdamUnroll];
+    int64_t i[kAdamUnroll];
+    bool ok[kAdamUnroll];
+    adam_locate(L, tb.n, e, e1, j, i, ok);
+    float g0[kAdamUnroll], p[kAdamUnroll], m0[kAdamUnroll], v0[kAdamUnroll];
+#pragma unroll
+    for (int u = 0; u < kAdamUnroll; ++u) {  // every load of the pass issued first
+      g0[u] = L.g[j[u]][i[u]];
+      p[u] = L.p[j[u]][i[u]];
+      m0[u] = L.m[j[u]][i[u]];
+      v0[u] = L.v[j[u]][i[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < kAdamUnroll; ++u) {
+      if (!ok[u]) continue;
+      float g = g0[u] * coef;
+      L.g[j[u]][i[u]] = g;  // clip_grad_norm_ scales .grad in place
+      if (wdf != 0.f) g = g + wdf * p[u];  // Adam (not AdamW) weight decay: grad.add(param, alpha=wd)
+      const float m = fmaf(omb1, g - m0[u], m0[u]);  // exp_avg.lerp_(grad, 1 - beta1)
+      const float v = v0[u] * b2 + omb2 * g * g;
+      L.m[j[u]][i[u]] = m;
+      L.v[j[u]][i[u]] = v;
+      L.p[j[u]][i[u]] = p[u] + neg_step * (m / (sqrtf(v) / bc2s + epsf));
+    }
   }
 }
 
