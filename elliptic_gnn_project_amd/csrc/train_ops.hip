@@ -122,7 +122,9 @@ __device__ __forceinline__ void adam_stage(const AdamTable& tb, AdamLds& L) {
   }
   __syncthreads();
 }
-// tensor ids and in-tensor offsets of elements e, e + T, ... (clamped into [e0, e1); valid[u] marks real ones)
+// tensor ids and in-tensor offsets of elements e, e + T, ... (valid[u] marks real ones; the others
+// are clamped to the slice's LAST element, e1 - 1 >= every real one, so the walk only moves
+// forward and every load stays inside a tensor)
 __device__ __forceinline__ void adam_locate(const AdamLds& L, int n, int64_t e, int64_t e1, int (&j)[kAdamUnroll],
                                             int64_t (&i)[kAdamUnroll], bool (&valid)[kAdamUnroll]) {
   int jj = 0;
@@ -130,7 +132,7 @@ __device__ __forceinline__ void adam_locate(const AdamLds& L, int n, int64_t e, 
   for (int u = 0; u < kAdamUnroll; ++u) {
     const int64_t eu = e + (int64_t)u * kAdamThreads;
     valid[u] = eu < e1;
-    const int64_t ec = valid[u] ? eu : e;
+    const int64_t ec = valid[u] ? eu : e1 - 1;
     while (jj + 1 < n && ec >= L.off[jj + 1]) ++jj;
     j[u] = jj;
     i[u] = ec - L.off[jj];
