@@ -180,6 +180,7 @@ class GnnAdamGroup(ctypes.Structure):
         ("weight_decay", ctypes.c_double), ("max_norm", ctypes.c_double),
         ("tensors", GnnAdamTensor * ADAM_MAX_TENSORS),
         ("skip_nonfinite", c_i32),
+        ("bump_counter", c_ptr),
     ]
 
 

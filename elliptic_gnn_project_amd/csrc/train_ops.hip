@@ -182,7 +182,8 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
                                                                   int nblk, float* __restrict__ step,
                                                                   double max_norm, double lr, double beta1,
                                                                   double beta2, double eps, double wd,
-                                                                  float* __restrict__ norm_out, int skip_nonfinite) {
+                                                                  float* __restrict__ norm_out, int skip_nonfinite,
+                                                                  int64_t* __restrict__ bump) {
   __shared__ float coef_sh;
   __shared__ int skip_sh;
   __shared__ AdamLds L;
@@ -202,6 +203,7 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
       if (blockIdx.x == 0) {
         if (norm_out) norm_out[0] = norm;
         step[0] = partial[nblk] + (skip ? 0.0f : 1.0f);
+        if (bump) bump[0] = bump[0] + 1;  // no kernel of this launch reads it
       }
     }
   }
@@ -307,7 +309,7 @@ extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, 
   GNN_LAUNCH_CHECK();
   clip_adam_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, kAdamBlocks, step, grp->max_norm, grp->lr,
                                                          grp->beta1, grp->beta2, grp->eps, grp->weight_decay, norm_out,
-                                                         grp->skip_nonfinite);
+                                                         grp->skip_nonfinite, grp->bump_counter);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }

@@ -581,13 +581,52 @@ def _graph_seed_counter(device: torch.device) -> torch.Tensor:
     return c
 
 
+# Inside train_gnn.CapturedStep the counter's per-step bump is deferred to the step's end: ClipAdam's
+# launch carries it (gnn_adam_group.bump_counter) — one launch fewer per replayed step — or, with
+# another optimizer, CapturedStep records the add itself at the end of the capture.
+_BUMP_DEFER = [False]
+_PENDING_BUMP = {}
+
+
+class deferred_seed_bumps:
+    """Context of a step capture whose dropout counter bumps run at the step's end."""
+
+    def __enter__(self):
+        _BUMP_DEFER[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _BUMP_DEFER[0] = False
+        _PENDING_BUMP.clear()
+        return False
+
+
+def take_seed_bump(device: torch.device):
+    """The counter whose bump this step still owes (the optimizer's launch performs it), or None."""
+    if not _BUMP_DEFER[0] or not torch.cuda.is_current_stream_capturing():
+        return None
+    return _PENDING_BUMP.pop(device, None)
+
+
+def flush_seed_bumps() -> None:
+    """Record the owed bumps (an add per counter) into the capture in progress."""
+    for ctr in _PENDING_BUMP.values():
+        ctr.add_(1)
+    _PENDING_BUMP.clear()
+
+
 def dropout_seeds(L: int, p: float, x: torch.Tensor):
     """(per-layer seeds, device counter or None) for the counter-hash dropout of one forward:
-    L seeds from torch's CPU generator when eager; per-layer salts plus the bumped device
-    counter under HIP-graph capture (see _graph_seed_counter)."""
+    L seeds from torch's CPU generator when eager; per-layer salts plus the device counter,
+    bumped once per forward, under HIP-graph capture (see _graph_seed_counter)."""
     if p > 0 and torch.cuda.is_current_stream_capturing():
         ctr = _graph_seed_counter(x.device)
-        ctr.add_(1)
+        if _BUMP_DEFER[0]:
+            if x.device in _PENDING_BUMP:  # a second forward in the step: its own counter value
+                ctr.add_(1)
+            _PENDING_BUMP[x.device] = ctr
+        else:
+            ctr.add_(1)
         return [l + 1 for l in range(L)], ctr
     if p > 0:
         if x.is_cuda:

@@ -30,6 +30,7 @@ import yaml
 
 from .dataset_elliptic import GraphData, load_graph, prepare_inputs, synthetic_elliptic
 from .distributed import GradBucket, convert_sync_batchnorm, gather_rows, shard_graph
+from . import fused
 from .gnn import GATNet, GCNNet, SAGENet, SAGEResBNNet
 
 
@@ -314,16 +315,22 @@ class CapturedStep:
         torch.cuda.current_stream().wait_stream(side)
         self.mid = mid
         self.graph = torch.cuda.CUDAGraph()
-        # thread-local capture mode: the process group's watchdog thread keeps querying the events
-        # of earlier (eager) collectives while this thread captures; in the default global mode
-        # such a query from another thread invalidates the capture (hipErrorStreamCaptureUnsupported)
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.out = step_fn()
         self.tail_graph = None
-        if tail is not None:
-            self.tail_graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.tail_graph, pool=self.graph.pool(), capture_error_mode="thread_local"):
-                tail()
+        # the dropout counter's per-step bump runs at the step's end (fused.deferred_seed_bumps):
+        # inside ClipAdam's launch when the step has one, else as an add recorded here
+        with fused.deferred_seed_bumps():
+            # thread-local capture mode: the process group's watchdog thread keeps querying the events
+            # of earlier (eager) collectives while this thread captures; in the default global mode
+            # such a query from another thread invalidates the capture (hipErrorStreamCaptureUnsupported)
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                self.out = step_fn()
+                if tail is None:
+                    fused.flush_seed_bumps()
+            if tail is not None:
+                self.tail_graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.tail_graph, pool=self.graph.pool(), capture_error_mode="thread_local"):
+                    tail()
+                    fused.flush_seed_bumps()
 
     def __call__(self):
         self.graph.replay()

@@ -139,8 +139,13 @@ class ClipAdam(torch.optim.Optimizer):
             if cached is None or cached[0] != key:
                 cached = (key, self._build(group, ps))
                 self._groups[gi] = cached
+            from .fused import take_seed_bump
+
+            bump = take_seed_bump(dev)  # a captured step's dropout counter, advanced by this launch
+            cached[1].bump_counter = bump.data_ptr() if bump is not None else None
             _lib.call("gnn_clip_adam_f32", cached[1], group["step_t"].data_ptr(), self.last_norm.data_ptr(),
                       self._ws.data_ptr(), self._ws.numel() * 4, _lib.stream_handle(dev))
+            cached[1].bump_counter = None
         return loss
 
     @staticmethod

@@ -514,6 +514,9 @@ typedef struct {
                               ELEMENT skips the update (params, moments, grads and step count
                               untouched); finite gradients whose Σg² overflows are clipped by
                               coefficient 0, as clip_grad_norm_ does with an inf norm */
+  int64_t* bump_counter;   /* optional (ABI 18): a device int64 the call increments by one (the
+                              dropout seed counter of a captured step — gnn_gemm_nt_params.seed_ptr
+                              — advanced at the step's end instead of by a launch of its own) */
 } gnn_adam_group;
 gnn_status gnn_clip_adam_workspace_size(size_t* bytes);
 gnn_status gnn_clip_adam_f32(const gnn_adam_group* group, float* step, float* norm_out, void* workspace,

@@ -92,6 +92,36 @@ def test_captured_step_redraws_dropout(device, arch):
     assert l1 != l2
 
 
+@pytest.mark.parametrize("form", ["split", "torch_adam"])
+def test_captured_step_bumps_the_counter_once_per_replay(device, form):
+    """The dropout counter's bump runs at the captured step's end: in ClipAdam's launch (the one-
+    graph form, above), in the optimizer graph of the split form, or — with an optimizer that
+    cannot carry it — as an add CapturedStep records itself; one bump per replay either way."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.train_gnn import CapturedStep
+
+    m, step, fwd_bwd, opt = _setup(device, "sage", dropout=0.5)
+    if form == "split":
+        cs = CapturedStep(fwd_bwd, warmup=1, mid=lambda: None, tail=opt.step)
+    else:
+        topt = torch.optim.Adam(m.parameters(), lr=0.01, capturable=True)
+
+        def step2():
+            loss = fwd_bwd()
+            topt.step()
+            return loss
+
+        cs = CapturedStep(step2, warmup=1)
+    ctr = fused._SEED_CTR[device]
+    c0 = int(ctr.item())
+    l1 = float(cs().item())
+    l2 = float(cs().item())
+    l3 = float(cs().item())
+    assert int(ctr.item()) == c0 + 3
+    assert l1 != l2 and l2 != l3
+    assert not fused._PENDING_BUMP and not fused._BUMP_DEFER[0]
+
+
 def test_captured_sage_reads_the_tied_output_weights(device):
     """The SAGE output conv's [W_l ; W_r] is one buffer tied at construction / .to() (fused.
     tie_output_weights), never re-pointed inside a forward: capture and replay keep the tie, the
