@@ -432,15 +432,22 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
 // layout are the split-image kernel's: 4 waves, wave w owns dW rows 32w .. +32 x all KT k-tiles,
 // 16-row chunks, one barrier per chunk, the staging of chunk c+1 spread over chunk c's 3·KT MFMA
 // gaps (several units per gap).  LAB as above (bit 1 no MFMAs, 2 no staging, 4 no fragment reads).
-template <int KT, bool GOUT, int LAB = 0>
-__global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
-  constexpr int NPA = (2 * PT_ROWS * (PT_MAXLD / 8) + 255) / 256;  // A pieces per thread per chunk (6)
+// NW = 8 (r19): two waves per SIMD — waves w and w + 4 share dW rows 32(w & 3) .. +32 and split the
+// k-tiles (the first (KT + 1) / 2 and the rest), so each holds half the accumulators and the block
+// twice the staging threads (twice the chunk loads in flight per CU).
+template <int KT, bool GOUT, int LAB = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int T = 64 * NW;
+  constexpr int NPA = (2 * PT_ROWS * (PT_MAXLD / 8) + T - 1) / T;  // A pieces per thread per chunk (6 / 3)
+  constexpr int RP = PT_ROWS / (T / 128);                           // G rows per thread per chunk (8 / 4)
+  constexpr int KTW = NW == 4 ? KT : (KT + 1) / 2;                  // k-tiles per wave
   __shared__ __attribute__((aligned(16))) uint16_t Gt[2][3 * PT_GPL];
   __shared__ __attribute__((aligned(16))) uint16_t At[2][2 * PT_APL];
   __shared__ float dzL[2][256];
-  __shared__ float redm[8];
-  constexpr int NU = 2 * NPA + 4 + 16 + 4 + 3;  // staging units per chunk
-  constexpr int NG = 3 * KT;                    // MFMA gaps per chunk
+  __shared__ float redm[2 * NW];
+  constexpr int NU = 2 * NPA + RP / 2 + 2 * RP + RP / 2 + 3;  // staging units per chunk
+  constexpr int NG = 3 * KTW;                                 // MFMA gaps per chunk
   // A's register ring: RING sets of the NPA pieces, a chunk's loads issued RING chunks before
   // its LDS put.  LAB 16: two sets — measured slower (lab 104.2 vs 100.6 us, r18h: the second
   // set's 24 VGPRs cost more in the chunk loop than the extra lead buys)
@@ -454,10 +461,13 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   const int64_t mend = min(a.M, mbeg + a.rows_per_block);
   const int nch = mend > mbeg ? (int)((mend - mbeg + PT_ROWS - 1) / PT_ROWS) : 0;
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  const int wrow = 32 * (wave & 3);                             // this wave's dW rows
+  const int tbase = NW == 4 ? 0 : (wave >> 2) * KTW;            // and k-tiles [tbase, tbase + ntl)
+  const int ntl = NW == 4 ? KT : min(KTW, KT - tbase);
 
-  floatx16 acc[KT];
+  floatx16 acc[KTW];
 #pragma unroll
-  for (int t = 0; t < KT; ++t)
+  for (int t = 0; t < KTW; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
 
@@ -466,7 +476,7 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   uint32_t goff[NPA], loff[NPA];
 #pragma unroll
   for (int j = 0; j < NPA; ++j) {
-    const int q = tid + 256 * j;
+    const int q = tid + T * j;
     const int per_plane = PT_ROWS * pr;
     const bool ok = q < 2 * per_plane;
     const int p = q / per_plane, rr = q - p * per_plane;
@@ -476,7 +486,7 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
                  : (uint32_t)(((tid & 15) * PT_AP + PT_MAXLD + 8 * ((tid >> 4) & 1)) * 2);
   }
 
-  // ---- G slot: column gn, rows 8·go .. +8 of the chunk
+  // ---- G slot: column gn, rows RP·go .. +RP of the chunk
   const int gn = tid & 127, go = tid >> 7;
   const bool gcol = gn < a.Nr;
   const int gnc = gcol ? gn : 0;
@@ -495,11 +505,11 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   auto scan_scale = [&]() __attribute__((always_inline)) {  // run in the prologue, behind chunk 0's loads
     float zm = 0.f;
     const int nq = a.nproj;
-    for (int64_t r0 = mbeg + tid; r0 < mend; r0 += 4 * 256) {
+    for (int64_t r0 = mbeg + tid; r0 < mend; r0 += 4 * T) {
       float v[4][MAXPROJ];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int64_t r = min(r0 + 256 * u, mend - 1);
+        const int64_t r = min(r0 + (int64_t)T * u, mend - 1);
 #pragma unroll
         for (int q = 0; q < MAXPROJ; ++q) v[u][q] = a.dz[r * a.lddz + min(q, nq - 1)];
       }
@@ -508,7 +518,7 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
         float s = 0.f;
 #pragma unroll
         for (int q = 0; q < MAXPROJ; ++q) s += q < nq ? fabsf(v[u][q]) : 0.f;
-        zm = fmaxf(zm, r0 + 256 * u < mend ? s : 0.f);
+        zm = fmaxf(zm, r0 + (int64_t)T * u < mend ? s : 0.f);
       }
     }
     float pm = 0.f;
@@ -521,11 +531,16 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     }
     if (lane == 0) {
       redm[wave] = zm;
-      redm[4 + wave] = pm;
+      redm[NW + wave] = pm;
     }
     __syncthreads();
-    zm = fmaxf(fmaxf(redm[0], redm[1]), fmaxf(redm[2], redm[3]));
-    pm = fmaxf(fmaxf(redm[4], redm[5]), fmaxf(redm[6], redm[7]));
+    zm = redm[0];
+    pm = redm[NW];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      zm = fmaxf(zm, redm[w]);
+      pm = fmaxf(pm, redm[NW + w]);
+    }
     const float bound = zm * pm * a.hscale;
     int E = 0;
     if (bound > 0.f && isfinite(bound)) frexpf(bound, &E);  // bound < 2^E
@@ -537,15 +552,15 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   auto ldbase = [&](int c) __attribute__((always_inline)) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
   const int clast = max(nch - 1, 0);
   u32x4 ra[RING][NPA];
-  float rg[8];
+  float rg[RP];
   float rz = 0.f;
   auto load_a = [&](int s, int j, int c) __attribute__((always_inline)) {
     ra[s][j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], ldbase(c) * ld * 2, 0);
   };
   auto load_g = [&](int c) __attribute__((always_inline)) {
-    uint32_t o = (uint32_t)((ldbase(c) + 8 * go) * hld);
+    uint32_t o = (uint32_t)((ldbase(c) + RP * go) * hld);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < RP; ++i) {
       rg[i] = hb[o];
       o += (uint32_t)hld;
     }
@@ -554,20 +569,20 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   auto put_z = [&](int k) __attribute__((always_inline)) {
     const int mb = ldbase(k);
     const bool ok = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + k * PT_ROWS - mb && zr < (int)mend - mb;
-    dzL[k & 1][tid] = ok ? rz : 0.0f;
+    if (T == 256 || tid < 256) dzL[k & 1][tid] = ok ? rz : 0.0f;
   };
 
   float db = 0.f, dzs = 0.f;
   float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
-  float e[8];
-  uint32_t w[4][3];
-  float4 zv[8];
-  float zsv[8];
+  float e[RP];
+  uint32_t w[RP / 2][3];
+  float4 zv[RP];
+  float zsv[RP];
   auto z_read = [&](int c, int i0, int n) __attribute__((always_inline)) {
     const int buf = c & 1;
 #pragma unroll
     for (int i = i0; i < i0 + n; ++i) {
-      const int r = 8 * go + i;
+      const int r = RP * go + i;
       zv[i] = *reinterpret_cast<const float4*>(&dzL[buf][r * MAXPROJ]);
       zsv[i] = dzL[buf][r * MAXPROJ + (gn & (MAXPROJ - 1))];
     }
@@ -594,7 +609,7 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     db += g;
     if constexpr (GOUT) {
       const int mb = ldbase(c);
-      const int r = 8 * go + i;
+      const int r = RP * go + i;
       const bool ok = r >= (int)mbeg + c * PT_ROWS - mb && r < (int)mend - mb && gcol;
       if (a.gout && ok) a.gout[(int64_t)(mb + r) * a.ldgout + gn] = g;
     }
@@ -605,17 +620,19 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     w[j][0] = h2_scale_pair(w[j][1], 2048.0f);
   };
   auto g_put = [&](int c) __attribute__((always_inline)) {
-    uint16_t* gd = Gt[c & 1] + gn * PT_GP + 8 * go;
+    uint16_t* gd = Gt[c & 1] + gn * PT_GP + RP * go;
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-      *reinterpret_cast<uint4*>(gd + p * PT_GPL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+    for (int p = 0; p < 3; ++p) {
+      if constexpr (RP == 8) *reinterpret_cast<uint4*>(gd + p * PT_GPL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+      else *reinterpret_cast<uint2*>(gd + p * PT_GPL) = make_uint2(w[0][p], w[1][p]);
+    }
   };
   // staging unit k of chunk c + 1 (refills for chunks c + 2 / c + 3); same order as the
   // split-image kernel: A pieces, dz reads, G rows, splits, G write, h loads, dz ring
   // (par: c's parity, a compile-time constant after inlining — chunk c + 1's pieces sit in set
   // (c + 1) % RING, refilled with chunk c + 1 + RING)
   auto unit = [&](int k, int c, int par) __attribute__((always_inline)) {
-    constexpr int Z0 = 2 * NPA, G0 = Z0 + 4, S0 = G0 + 16, P0 = S0 + 4;
+    constexpr int Z0 = 2 * NPA, G0 = Z0 + RP / 2, S0 = G0 + 2 * RP, P0 = S0 + RP / 2;
     const int sa = RING == 1 ? 0 : (par ^ 1);
     if (k < Z0) {
       if (k & 1) load_a(sa, k >> 1, min(c + 1 + RING, clast));
@@ -636,7 +653,7 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     }
   };
 
-  const int gfo = (32 * wave + (lane & 31)) * PT_GP + 8 * (lane >> 5);
+  const int gfo = (wrow + (lane & 31)) * PT_GP + 8 * (lane >> 5);
   const int grp = lane >> 4, li = lane & 15;
   const int afo = (8 * (grp >> 1) + (li >> 2)) * PT_AP + 16 * (grp & 1) + 4 * (li & 3);
   auto afrag = [&](const uint16_t* base, int t, int p) __attribute__((always_inline)) {
@@ -652,20 +669,22 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     for (int p = 0; p < 3; ++p) gf[p] = *reinterpret_cast<const f16x8*>(Gt[buf] + p * PT_GPL + gfo);
     const uint16_t* ab = At[buf] + afo;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) af[0][p] = afrag(ab, 0, p);
+    for (int p = 0; p < 2; ++p) af[0][p] = afrag(ab, tbase, p);
     constexpr int pg[3] = {2, 1, 0}, pa[3] = {0, 1, 0};  // G_lo·A_hi, G_hi·A_lo, G_hi'·A_hi
-    static_for<KT>([&](auto tc) __attribute__((always_inline)) {
-      constexpr int t = decltype(tc)::value;
-      if constexpr (t + 1 < KT && !(LAB & 4)) {
+    static_for<KTW>([&](auto tc) __attribute__((always_inline)) {
+      constexpr int t = decltype(tc)::value;  // this wave's t-th k-tile: tbase + t
+      if constexpr (t + 1 < KTW && !(LAB & 4)) {
 #pragma unroll
-        for (int p = 0; p < 2; ++p) af[(t + 1) & 1][p] = afrag(ab, t + 1, p);
+        for (int p = 0; p < 2; ++p) af[(t + 1) & 1][p] = afrag(ab, tbase + t + 1, p);  // (past ntl: unused)
       }
       static_for<3>([&](auto mc) __attribute__((always_inline)) {
         constexpr int m = decltype(mc)::value;
         constexpr int gap = 3 * t + m;
         TH_FENCE;
-        if constexpr (!(LAB & 1))
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gf[pg[m]], af[(LAB & 4) ? 0 : (t & 1)][pa[m]], acc[t], 0, 0, 0);
+        if constexpr (!(LAB & 1)) {
+          if (NW == 4 || t < ntl)  // wave-uniform
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gf[pg[m]], af[(LAB & 4) ? 0 : (t & 1)][pa[m]], acc[t], 0, 0, 0);
+        }
         TH_FENCE;
         if constexpr (!(LAB & 2)) {
           static_for<(gap + 1) * NU / NG - gap * NU / NG>([&](auto uc) __attribute__((always_inline)) {
@@ -678,7 +697,7 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     if constexpr (NU > NG) {}  // every unit is placed inside the chain (NU units over NG gaps)
     if constexpr ((LAB & 1) != 0) {
 #pragma unroll
-      for (int t = 0; t < KT; ++t) acc[t][0] += (float)gf[0][0] + (float)af[0][0][0] + (float)af[1][1][1];
+      for (int t = 0; t < KTW; ++t) acc[t][0] += (float)gf[0][0] + (float)af[0][0][0] + (float)af[1][1][1];
     }
   };
 #undef TH_FENCE
@@ -699,14 +718,14 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
     scan_scale();     // (its barrier also publishes dzL)
 #pragma unroll
     for (int j = 0; j < NPA; ++j) put_a(0, j, 0);
-    z_read(0, 0, 8);
+    z_read(0, 0, RP);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < RP; ++i) {
       g_row(i, 0, 0);
       g_row(i, 0, 1);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) split_pair(j);
+    for (int j = 0; j < RP / 2; ++j) split_pair(j);
     g_put(0);
 #pragma unroll
     for (int j = 0; j < NPA; ++j) load_a(0, j, min(RING, clast));  // set 0: chunk RING (1 or 2)
@@ -726,13 +745,14 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
   float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
   const int Kc = a.k1 + a.k2;
 #pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    const int kp = t * 32 + (lane & 31);
+  for (int t = 0; t < KTW; ++t) {
+    if (NW == 8 && t >= ntl) break;  // wave-uniform
+    const int kp = (tbase + t) * 32 + (lane & 31);
     const bool s1 = kp < a.k1;
     const bool s2 = kp >= a.ap_col2 && kp < a.ap_col2 + a.k2;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int row = wrow + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       const int64_t idx = s1 ? (int64_t)row * a.k1 + kp : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (kp - a.ap_col2);
       if (row < a.Nr && (s1 || s2)) slab[idx] = acc[t][r] * gunsc;
     }
@@ -745,14 +765,19 @@ __global__ __launch_bounds__(256) void gemm_tn_h2_kernel(TNArgs a) {
 #pragma unroll
   for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
   __syncthreads();
+  constexpr int NGO = T / 128;  // row groups of a column, combined in order
+  auto comb = [&](int col, int f) __attribute__((always_inline)) {
+    float v = red[col * ns + f];
+#pragma unroll
+    for (int o = 1; o < NGO; ++o) v += red[(o * 128 + col) * ns + f];
+    return v;
+  };
   if (tid < 128 && tid < a.Nr) {
     float* side = slab + (int64_t)a.Nr * Kc;
-    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
-    for (int q = 0; q < a.nproj; ++q)
-      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+    side[tid] = comb(tid, 0);
+    for (int q = 0; q < a.nproj; ++q) side[a.Nr + q * a.Nr + tid] = comb(tid, 2 + q);
   }
-  if (tid < a.nproj)
-    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+  if (tid < a.nproj) slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = comb(tid, 1);
 }
 
 // ------------------------------------------------------------------ TN over a bf16 image
@@ -1100,9 +1125,11 @@ bool tn_h2_ok(const TNArgs& a) {
   return (a.M + 32) * ldmax < ((int64_t)1 << 31);
 }
 
+// 8 waves (two per SIMD, the k-tiles split between them): lab 102.3 -> 95.2 us on the headline
+// shape (profiles/r19_lab_h2.txt), the staging alone 93.4 — the kernel now runs at its stream
 void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st) {
-  if (a.gout) gemm_tn_h2_kernel<11, true><<<nblk, 256, 0, st>>>(a);
-  else gemm_tn_h2_kernel<11, false><<<nblk, 256, 0, st>>>(a);
+  if (a.gout) gemm_tn_h2_kernel<11, true, 0, 8><<<nblk, 512, 0, st>>>(a);
+  else gemm_tn_h2_kernel<11, false, 0, 8><<<nblk, 512, 0, st>>>(a);
 }
 
 bool tn_planes_ok(const TNArgs& a) {

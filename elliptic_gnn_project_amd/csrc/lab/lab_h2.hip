@@ -377,6 +377,10 @@ void tnh(const NTArgs&, const uint4*, int) {
   gemm_tn_h2_kernel<11, false, LAB><<<256, 256>>>(g_th);
 }
 template <int LAB>
+void tnh8(const NTArgs&, const uint4*, int) {
+  gemm_tn_h2_kernel<11, false, LAB, 8><<<256, 512>>>(g_th);
+}
+template <int LAB>
 void tnd(const NTArgs&, const uint4*, int) {
   gemm_tn_h2_dma_kernel<11, LAB><<<256, 256>>>(g_th);
 }
@@ -520,7 +524,8 @@ int main(int argc, char** argv) {
       }
     auto run = [&](const char* name, int h2) {
       CK(hipMemset(slab, 0, nblk * stride * 4));
-      if (h2 == 2) gemm_tn_h2_dma_kernel<11, 0><<<nblk, 256>>>(ha);
+      if (h2 == 3) gemm_tn_h2_kernel<11, false, 0, 8><<<nblk, 512>>>(ha);
+      else if (h2 == 2) gemm_tn_h2_dma_kernel<11, 0><<<nblk, 256>>>(ha);
       else if (h2) gemm_tn_h2_kernel<11, false, 0><<<nblk, 256>>>(ha);
       else gemm_tn_planes_kernel<true, true, 11, false, 0><<<nblk, 256>>>(pa);
       CK(hipDeviceSynchronize());
@@ -538,6 +543,7 @@ int main(int argc, char** argv) {
     run("split-bf16 planes", 0);
     run("half-pair", 1);
     run("half-pair dma", 2);
+    run("half-pair 8 waves", 3);
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -552,6 +558,8 @@ int main(int argc, char** argv) {
       {"TN planes (bf16 x6)", tnp<0>, {}}, {"TN planes MFMA only", tnp<2 | 8>, {}},
       {"TN half-pair", tnh<0>, {}}, {"TN half-pair no staging", tnh<2>, {}}, {"TN half-pair no MFMA", tnh<1>, {}},
       {"TN half-pair ring2", tnh<16>, {}}, {"TN half-pair ring2 no MFMA", tnh<17>, {}},
+      {"TN half-pair 8 waves", tnh8<0>, {}}, {"TN half-pair 8 waves no MFMA", tnh8<1>, {}},
+      {"TN half-pair 8 waves no staging", tnh8<2>, {}},
       {"TN half-pair dma", tnd<0>, {}}, {"TN half-pair dma no MFMA", tnd<1>, {}}, {"TN half-pair dma no G", tnd<2>, {}}};
   for (int r = 0; r < rounds; ++r)
     for (auto& v : vs) {
