@@ -1029,7 +1029,7 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
 // B image of the half-pair NT (gemm_common.hpp ws_prep_h2_body): the standalone launch, one
 // 1024-thread block per k-step.  (K1 can also carry it: gnn_sage_mean_fwd_h2's prep_b.)
 __global__ __launch_bounds__(WS_PREP_THREADS) void ws_prep_h2_kernel(H2Prep p) {
-  ws_prep_h2_body<WS_PREP_THREADS, 8>(p, (int)blockIdx.x);  // one pass: 96 loads per lane in flight
+  ws_prep_h2_body<WS_PREP_THREADS>(p, (int)blockIdx.x);  // (one 8-column pass: 9.5 vs 8.8 us, r19g)
 }
 
 // ---------------------------------------------------------------- bf16 image form (K7a-b)
