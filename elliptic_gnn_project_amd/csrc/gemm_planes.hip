@@ -76,7 +76,7 @@ constexpr int PT_AP = 352;                // LDS row pitch of an A chunk (bf16):
 constexpr int PT_APL = PT_ROWS * PT_AP;   // one plane of a chunk
 constexpr int PT_GP = 24;                 // G row pitch ([n][m], 12 dwords: conflict-free b128 reads)
 constexpr int PT_GPL = 128 * PT_GP;
-constexpr int PT_NP = 8;                  // 16-byte A pieces per thread per chunk (3·16·42 = 2016 <= 2048)
+// 16-byte A pieces per thread per chunk: 8 at 256 threads, 4 at 512 (3·16·42 = 2016 <= 2048)
 constexpr int PT_MAXLD = 336;             // widest image row the chunk layout holds (42 pieces)
 
 // one transposed 4-row x 16-column read (lane i of each 16-lane group gets column i)
@@ -104,14 +104,21 @@ __device__ __forceinline__ bf16x8 cat_frag(s16x4 a, s16x4 b) {
 // KS = 2 (Nr <= 64): waves 0-1 own dW rows 0..63 over the first half of the k-tiles, waves 2-3
 // the same rows over the second half (each dW element still one wave's chain: same results), so
 // no wave multiplies the zero G columns 64..127 and the MFMA chain the staging hides behind halves.
-template <bool PROJ, bool MASK, int KT, bool GOUT, int LAB = 0, int KS = 1>
-__global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
-  static_assert(KT % KS == 0, "k-tiles split evenly");
-  constexpr int KW = KT / KS;  // k-tiles per wave
+// NW = 8 (r19): two waves per SIMD, the k-tiles split KS ways over RG = NW / KS row groups (as
+// evenly as KT allows: wave group kg owns tiles [kg·KT/KS, (kg+1)·KT/KS)), twice the staging threads.
+template <bool PROJ, bool MASK, int KT, bool GOUT, int LAB = 0, int KS = 1, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_tn_planes_kernel(TNArgs a) {
+  constexpr int RG = NW / KS;  // row groups of 32 dW rows
+  static_assert((NW == 4 || NW == 8) && (RG == 2 || RG == 4) && RG * KS == NW, "wave layout");
+  constexpr bool EVEN = KT % KS == 0;
+  constexpr int KW = (KT + KS - 1) / KS;  // k-tiles per wave (at most)
+  constexpr int T = 64 * NW;
+  constexpr int NP = (3 * PT_ROWS * (PT_MAXLD / 8) + T - 1) / T;  // A pieces per thread (8 / 4)
+  constexpr int RP = PT_ROWS / (T / 128);                          // G rows per thread (8 / 4)
   __shared__ __attribute__((aligned(16))) uint16_t Gt[2][3 * PT_GPL];
   __shared__ __attribute__((aligned(16))) uint16_t At[2][3 * PT_APL];
   __shared__ float dzL[2][256];  // dz rows of a chunk (16 x 4), threads 0..63 write theirs
-  constexpr int NU = 2 * PT_NP + 31;  // staging slots per chunk (<= 6·KT for the MFMA shadow)
+  constexpr int NU = 2 * NP + RP / 2 + 2 * RP + RP + 3;  // staging slots per chunk (47 / 25)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -121,8 +128,10 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   const int64_t mend = min(a.M, mbeg + a.rows_per_block);
   const int nch = mend > mbeg ? (int)((mend - mbeg + PT_ROWS - 1) / PT_ROWS) : 0;
 
-  const int wr = KS == 2 ? (wave & 1) : wave;  // the wave's 32 dW rows
-  const int t0 = KS == 2 ? (wave >> 1) * KW : 0;  // its first k-tile
+  const int wr = wave % RG;                          // the wave's 32 dW rows
+  const int kg = wave / RG;                          // its k-tile group
+  const int t0 = kg * KT / KS;                       // first k-tile
+  const int ntl = (kg + 1) * KT / KS - t0;           // and count (KW when EVEN)
   floatx16 acc[KW];
 #pragma unroll
   for (int t = 0; t < KW; ++t)
@@ -134,10 +143,10 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   //      (columns 336.. of plane 0, never part of a written dW column).
   const __amdgpu_buffer_rsrc_t arsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.ap), 0, (int)(3 * a.ap_ps * 2), 0x00020000);
-  uint32_t goff[PT_NP], loff[PT_NP];
+  uint32_t goff[NP], loff[NP];
 #pragma unroll
-  for (int j = 0; j < PT_NP; ++j) {
-    const int q = tid + 256 * j;
+  for (int j = 0; j < NP; ++j) {
+    const int q = tid + T * j;
     const int per_plane = PT_ROWS * pr;
     const bool ok = q < 3 * per_plane;
     const int p = q / per_plane, rr = q - p * per_plane;
@@ -147,7 +156,7 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
                  : (uint32_t)(((tid & 15) * PT_AP + PT_MAXLD + 8 * ((tid >> 4) & 1)) * 2);
   }
 
-  // ---- G slot: column gn, rows 8·go .. +8 of the chunk
+  // ---- G slot: column gn, rows RP·go .. +RP of the chunk
   const int gn = tid & 127, go = tid >> 7;
   const bool gcol = gn < a.Nr;
   const int gnc = gcol ? gn : 0;
@@ -164,8 +173,8 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   const int Mi = (int)a.M;
   auto ldbase = [&](int c) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
   const int clast = max(nch - 1, 0);
-  u32x4 ra[PT_NP];
-  float rg[8], rg2[8];
+  u32x4 ra[NP];
+  float rg[RP], rg2[RP];
   float rz = 0.f;
   // loads of chunk c into the stage registers (c clamped by the callers: always in bounds)
   auto load_a = [&](int j, int c) {
@@ -174,17 +183,17 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   auto load_g = [&](int c) {
     const int mb = ldbase(c);
     if constexpr (MASK || !PROJ) {  // the dz form without a mask reads no G column
-      uint32_t o = (uint32_t)((mb + 8 * go) * gld);
+      uint32_t o = (uint32_t)((mb + RP * go) * gld);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < RP; ++i) {
         rg[i] = gbase[o];
         o += (uint32_t)gld;
       }
     }
     if constexpr (MASK && !PROJ) {
-      uint32_t o2 = (uint32_t)((mb + 8 * go) * g2ld);
+      uint32_t o2 = (uint32_t)((mb + RP * go) * g2ld);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < RP; ++i) {
         rg2[i] = g2base[o2];
         o2 += (uint32_t)g2ld;
       }
@@ -199,22 +208,22 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
       const int mb = ldbase(k);
       const bool ok = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + k * PT_ROWS - mb &&
                       zr < (int)mend - mb;
-      dzL[k & 1][tid] = ok ? rz : 0.0f;
+      if (T == 256 || tid < 256) dzL[k & 1][tid] = ok ? rz : 0.0f;
     }
   };
 
   float db = 0.f, dzs = 0.f;
   float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
-  float e[8];
-  uint32_t w[4][3];
-  float4 zv[8];  // dz rows of the G slot (read in one unit, ahead of their use)
-  float zsv[8];
+  float e[RP];
+  uint32_t w[RP / 2][3];
+  float4 zv[RP];  // dz rows of the G slot (read in one unit, ahead of their use)
+  float zsv[RP];
   auto z_read = [&](int c, int i0, int n) {  // rows i0 .. i0 + n of the G slot
     if constexpr (PROJ) {
       const int buf = c & 1;
 #pragma unroll
       for (int i = i0; i < i0 + n; ++i) {
-        const int r = 8 * go + i;
+        const int r = RP * go + i;
         zv[i] = *reinterpret_cast<const float4*>(&dzL[buf][r * MAXPROJ]);
         zsv[i] = dzL[buf][r * MAXPROJ + (gn & (MAXPROJ - 1))];
       }
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
       return;
     }
     const int mb = ldbase(c);
-    const int r = 8 * go + i;
+    const int r = RP * go + i;
     const bool ok = r >= (int)mbeg + c * PT_ROWS - mb && r < (int)mend - mb && gcol;
     float g = e[i];
     if constexpr (PROJ) dzs += gn < MAXPROJ ? zsv[i] : 0.0f;  // unconditional read + select: no branch
@@ -276,15 +285,17 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
     }
   };
   auto g_put = [&](int c) {
-    uint16_t* gd = Gt[c & 1] + gn * PT_GP + 8 * go;
+    uint16_t* gd = Gt[c & 1] + gn * PT_GP + RP * go;
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-      *reinterpret_cast<uint4*>(gd + p * PT_GPL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+    for (int p = 0; p < 3; ++p) {
+      if constexpr (RP == 8) *reinterpret_cast<uint4*>(gd + p * PT_GPL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+      else *reinterpret_cast<uint2*>(gd + p * PT_GPL) = make_uint2(w[0][p], w[1][p]);
+    }
   };
   // staging slot k of chunk c + 1, issued right after one MFMA of chunk c (a few instructions in
   // the MFMA's shadow); refills for chunks c + 2 / c + 3
   auto unit = [&](int k, int c) {
-    constexpr int A0 = 0, Z0 = 2 * PT_NP, G0 = Z0 + 4, S0 = G0 + 16, P0 = S0 + 8;
+    constexpr int A0 = 0, Z0 = 2 * NP, G0 = Z0 + RP / 2, S0 = G0 + 2 * RP, P0 = S0 + RP;
     if (k < Z0) {
       if (k & 1) load_a(k >> 1, min(c + 2, clast));
       else put_a(k >> 1, c + 1);
@@ -304,7 +315,7 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
     }
     (void)A0;
   };
-  static_assert(2 * PT_NP + 4 + 16 + 8 + 3 == NU, "slot count");
+  static_assert(2 * NP + RP / 2 + 2 * RP + RP + 3 == NU, "slot count");
 
   // fragment addresses: G rows 32·wave + (lane & 31), k = 8·(lane >> 5); A (transposed reads)
   // lane 4q + p of 16-lane group g supplies row 8·(g >> 1) + q, columns 16·(g & 1) + 4p ..
@@ -336,8 +347,10 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
 #pragma unroll
       for (int m = 0; m < 6; ++m) {
         PT_FENCE;
-        if constexpr (!(LAB & 1))
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[pa[m]], af[(LAB & 4) ? 0 : (t & 1)][pb[m]], acc[t], 0, 0, 0);
+        if constexpr (!(LAB & 1)) {
+          if (EVEN || t < ntl)  // wave-uniform
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gf[pa[m]], af[(LAB & 4) ? 0 : (t & 1)][pb[m]], acc[t], 0, 0, 0);
+        }
         PT_FENCE;
         if (6 * t + m < NU && !(LAB & 2)) unit(6 * t + m, c);
       }
@@ -361,22 +374,22 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
     put_z(1);
     load_z(min(2, clast));
 #pragma unroll
-    for (int j = 0; j < PT_NP; ++j) load_a(j, 0);
+    for (int j = 0; j < NP; ++j) load_a(j, 0);
     load_g(0);
     __syncthreads();  // dzL
 #pragma unroll
-    for (int j = 0; j < PT_NP; ++j) put_a(j, 0);
-    z_read(0, 0, 8);
+    for (int j = 0; j < NP; ++j) put_a(j, 0);
+    z_read(0, 0, RP);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < RP; ++i) {
       g_row(i, 0, 0);
       g_row(i, 0, 1);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) split3_pair(e[2 * j], e[2 * j + 1], w[j][0], w[j][1], w[j][2]);
+    for (int j = 0; j < RP / 2; ++j) split3_pair(e[2 * j], e[2 * j + 1], w[j][0], w[j][1], w[j][2]);
     g_put(0);
 #pragma unroll
-    for (int j = 0; j < PT_NP; ++j) load_a(j, min(1, clast));
+    for (int j = 0; j < NP; ++j) load_a(j, min(1, clast));
     load_g(min(1, clast));
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
@@ -390,6 +403,7 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
   const int Kc = a.k1 + a.k2;
 #pragma unroll
   for (int t = 0; t < KW; ++t) {
+    if (!EVEN && t >= ntl) break;  // wave-uniform
     const int kp = (t0 + t) * 32 + (lane & 31);  // image column
     const bool s1 = kp < a.k1;
     const bool s2 = kp >= a.ap_col2 && kp < a.ap_col2 + a.k2;
@@ -409,14 +423,19 @@ __global__ __launch_bounds__(256) void gemm_tn_planes_kernel(TNArgs a) {
 #pragma unroll
   for (int q = 0; q < MAXPROJ; ++q) red[(go * 128 + gn) * ns + 2 + q] = dw2[q];
   __syncthreads();
+  constexpr int NGO = T / 128;  // row groups of a column, combined in order
+  auto comb = [&](int col, int f) {
+    float v = red[col * ns + f];
+#pragma unroll
+    for (int o = 1; o < NGO; ++o) v += red[(o * 128 + col) * ns + f];
+    return v;
+  };
   if (tid < 128 && tid < a.Nr) {
     float* side = slab + (int64_t)a.Nr * Kc;
-    side[tid] = red[tid * ns] + red[(128 + tid) * ns];
-    for (int q = 0; q < a.nproj; ++q)
-      side[a.Nr + q * a.Nr + tid] = red[tid * ns + 2 + q] + red[(128 + tid) * ns + 2 + q];
+    side[tid] = comb(tid, 0);
+    for (int q = 0; q < a.nproj; ++q) side[a.Nr + q * a.Nr + tid] = comb(tid, 2 + q);
   }
-  if (PROJ && tid < a.nproj)
-    slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = red[tid * ns + 1] + red[(128 + tid) * ns + 1];
+  if (PROJ && tid < a.nproj) slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = comb(tid, 1);
 }
 
 // ------------------------------------------------------------------ TN over a half-pair image

@@ -450,6 +450,10 @@ void tngk(const TNArgs&, const NTArgs&, const uint4*, int nblk, int) {
   gemm_tn_planes_kernel<false, false, 6, false, LAB, 2><<<nblk, 256>>>(g_gcn);
 }
 template <int LAB>
+void tngk8(const TNArgs&, const NTArgs&, const uint4*, int nblk, int) {  // 8 waves: 2 row groups x 4 k-groups
+  gemm_tn_planes_kernel<false, false, 6, false, LAB, 4, 8><<<nblk, 512>>>(g_gcn);
+}
+template <int LAB>
 void tngd(const TNArgs&, const NTArgs&, const uint4*, int nblk, int) {
   gemm_tn_planes_dma_kernel<6, LAB, true><<<nblk, 256>>>(g_gcn);
 }
@@ -513,7 +517,8 @@ int main(int argc, char** argv) {
       {"TN production", tn<0>, {}}, {"TN no MFMA", tn<1>, {}}, {"TN no staging", tn<2>, {}},
       {"TN no frag reads", tn<4>, {}}, {"TN no barrier", tn<8>, {}}, {"TN MFMA+frags", tn<2 | 8>, {}},
       {"TN MFMA only", tn<2 | 4 | 8>, {}}, {"TN staging only", tn<1 | 4>, {}},
-      {"GCN TN production", tng<0>, {}}, {"GCN TN split-K", tngk<0>, {}}, {"GCN TN dma", tngd<0>, {}}, {"GCN TN staging only", tng<1 | 4>, {}},
+      {"GCN TN production", tng<0>, {}}, {"GCN TN split-K", tngk<0>, {}}, {"GCN TN 8 waves", tngk8<0>, {}},
+      {"GCN TN 8w staging", tngk8<1 | 4>, {}}, {"GCN TN dma", tngd<0>, {}}, {"GCN TN staging only", tng<1 | 4>, {}},
       {"GCN TN dma DMA only", tngd<1 | 2 | 4>, {}},
       {"TN dma", tnd<0>, {}}, {"TN dma no MFMA", tnd<1>, {}}, {"TN dma no G", tnd<2>, {}},
       {"TN dma no frags", tnd<4>, {}}, {"TN dma DMA only", tnd<1 | 2 | 4>, {}},
@@ -584,6 +589,18 @@ int main(int argc, char** argv) {
     ndiff = 0;
     for (size_t i = 0; i < nsl; ++i) ndiff += std::memcmp(&r0[i], &r1[i], 4) != 0;
     std::printf("GCN TN split-K vs production: %zu of %zu slab words differ\n", ndiff, nsl);
+    CK(hipMemset(slab, 0, nsl * 4));
+    tngk8<0>(a, n, bimg, nblk, ntiles);
+    CK(hipMemcpy(r1.data(), slab, nsl * 4, hipMemcpyDeviceToHost));
+    ndiff = 0;
+    md = 0;
+    for (size_t i = 0; i < nsl; ++i)
+      if (std::memcmp(&r0[i], &r1[i], 4)) {
+        ++ndiff;
+        md = std::max(md, (double)std::fabs(r0[i] - r1[i]));
+      }
+    std::printf("GCN TN 8 waves vs production: %zu of %zu slab words differ (max |diff| %g; dW bit-exact, the side sums' order)\n",
+                ndiff, nsl, md);
   }
   for (int r = 0; r < rounds; ++r)
     for (auto& v : vs) {

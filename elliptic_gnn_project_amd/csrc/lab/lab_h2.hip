@@ -373,6 +373,10 @@ void tnp(const NTArgs&, const uint4*, int) {
   gemm_tn_planes_kernel<true, true, 11, false, LAB><<<256, 256>>>(g_tp);
 }
 template <int LAB>
+void tnp8(const NTArgs&, const uint4*, int) {
+  gemm_tn_planes_kernel<true, true, 11, false, LAB, 2, 8><<<256, 512>>>(g_tp);
+}
+template <int LAB>
 void tnh(const NTArgs&, const uint4*, int) {
   gemm_tn_h2_kernel<11, false, LAB><<<256, 256>>>(g_th);
 }
@@ -524,7 +528,8 @@ int main(int argc, char** argv) {
       }
     auto run = [&](const char* name, int h2) {
       CK(hipMemset(slab, 0, nblk * stride * 4));
-      if (h2 == 3) gemm_tn_h2_kernel<11, false, 0, 8><<<nblk, 512>>>(ha);
+      if (h2 == 4) gemm_tn_planes_kernel<true, true, 11, false, 0, 2, 8><<<nblk, 512>>>(pa);
+      else if (h2 == 3) gemm_tn_h2_kernel<11, false, 0, 8><<<nblk, 512>>>(ha);
       else if (h2 == 2) gemm_tn_h2_dma_kernel<11, 0><<<nblk, 256>>>(ha);
       else if (h2) gemm_tn_h2_kernel<11, false, 0><<<nblk, 256>>>(ha);
       else gemm_tn_planes_kernel<true, true, 11, false, 0><<<nblk, 256>>>(pa);
@@ -544,6 +549,7 @@ int main(int argc, char** argv) {
     run("half-pair", 1);
     run("half-pair dma", 2);
     run("half-pair 8 waves", 3);
+    run("split-bf16 planes 8 waves", 4);
   }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -556,6 +562,7 @@ int main(int argc, char** argv) {
       {"NT half-pair MFMA only", nth<2 | 4>, {}}, {"NT half-pair no MFMA", nth<1>, {}},
       {"NT half-pair no dropout", nth<0, EPIN>, {}},
       {"TN planes (bf16 x6)", tnp<0>, {}}, {"TN planes MFMA only", tnp<2 | 8>, {}},
+      {"TN planes 8 waves", tnp8<0>, {}},
       {"TN half-pair", tnh<0>, {}}, {"TN half-pair no staging", tnh<2>, {}}, {"TN half-pair no MFMA", tnh<1>, {}},
       {"TN half-pair ring2", tnh<16>, {}}, {"TN half-pair ring2 no MFMA", tnh<17>, {}},
       {"TN half-pair 8 waves", tnh8<0>, {}}, {"TN half-pair 8 waves no MFMA", tnh8<1>, {}},
