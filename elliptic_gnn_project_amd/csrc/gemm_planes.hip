@@ -1091,12 +1091,11 @@ void launch_tn_img16_kt(const TNArgs& a, int nblk, hipStream_t st) {
 
 template <bool PROJ, bool MASK, int KT>
 void launch_tn_planes_k(const TNArgs& a, int nblk, hipStream_t st) {
-  if constexpr (KT % 2 == 0) {
-    if (a.Nr <= 64) {  // split K across the wave pairs (GCN / GAT layer 1, N = 64)
-      if (a.gout) gemm_tn_planes_kernel<PROJ, MASK, KT, true, 0, 2><<<nblk, 256, 0, st>>>(a);
-      else gemm_tn_planes_kernel<PROJ, MASK, KT, false, 0, 2><<<nblk, 256, 0, st>>>(a);
-      return;
-    }
+  if (a.Nr <= 64) {  // K split 4 ways over 8 waves (GCN / GAT layer 1, N = 64): lab GCN shape 57.2 ->
+    // 53.8 us vs the 4-wave split-K (profiles/r19_lab_gemm.txt; dW bit-identical)
+    if (a.gout) gemm_tn_planes_kernel<PROJ, MASK, KT, true, 0, 4, 8><<<nblk, 512, 0, st>>>(a);
+    else gemm_tn_planes_kernel<PROJ, MASK, KT, false, 0, 4, 8><<<nblk, 512, 0, st>>>(a);
+    return;
   }
   if (a.gout) gemm_tn_planes_kernel<PROJ, MASK, KT, true><<<nblk, 256, 0, st>>>(a);
   else gemm_tn_planes_kernel<PROJ, MASK, KT, false><<<nblk, 256, 0, st>>>(a);
