@@ -1097,6 +1097,11 @@ void launch_tn_planes_k(const TNArgs& a, int nblk, hipStream_t st) {
     else gemm_tn_planes_kernel<PROJ, MASK, KT, false, 0, 4, 8><<<nblk, 512, 0, st>>>(a);
     return;
   }
+  if constexpr (KT <= 8) {  // narrower images at N > 64 (the SAGE-ResBN layer-0 conv over x): K split 2 ways
+    if (a.gout) gemm_tn_planes_kernel<PROJ, MASK, KT, true, 0, 2, 8><<<nblk, 512, 0, st>>>(a);
+    else gemm_tn_planes_kernel<PROJ, MASK, KT, false, 0, 2, 8><<<nblk, 512, 0, st>>>(a);
+    return;
+  }
   if (a.gout) gemm_tn_planes_kernel<PROJ, MASK, KT, true><<<nblk, 256, 0, st>>>(a);
   else gemm_tn_planes_kernel<PROJ, MASK, KT, false><<<nblk, 256, 0, st>>>(a);
 }
