@@ -181,6 +181,7 @@ class GnnAdamGroup(ctypes.Structure):
         ("tensors", GnnAdamTensor * ADAM_MAX_TENSORS),
         ("skip_nonfinite", c_i32),
         ("bump_counter", c_ptr),
+        ("loss_partial", c_ptr), ("loss_nblk", c_i32), ("loss_scale", ctypes.c_float), ("loss_out", c_ptr),
     ]
 
 
@@ -269,6 +270,7 @@ SIGNATURES = {
     "gnn_gemm_nt_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_size)]),
     "gnn_gemm_nt_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),
     "gnn_gemm_nt_prep_b": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),
+    "gnn_masked_ce_finish": (ctypes.c_int, [c_ptr, c_i32, ctypes.c_float, c_ptr, c_ptr]),
     "gnn_gemm_tn_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32, ctypes.POINTER(c_size)]),
     "gnn_gemm_tn_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams), c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_gemm_nt_planes_ok": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams)]),

@@ -139,8 +139,11 @@ __device__ __forceinline__ void adam_locate(const AdamLds& L, int n, int64_t e, 
   }
 }
 
+struct LossFinish {  // a deferred gnn_masked_ce_f32 loss (gnn_adam_group.loss_partial)
+  const float* partial; int32_t n; float scale; float* out;
+};
 __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, float* __restrict__ partial,
-                                                                const float* __restrict__ step) {
+                                                                const float* __restrict__ step, LossFinish lf) {
   __shared__ float sh[kAdamThreads / 64];
   __shared__ AdamLds L;
   adam_stage(tb, L);
@@ -169,6 +172,13 @@ __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, flo
     partial[blockIdx.x] = t;
     partial[kAdamBlocks + 1 + blockIdx.x] = tn;
     if (blockIdx.x == 0) partial[kAdamBlocks] = step[0];
+  }
+  if (lf.partial && blockIdx.x == gridDim.x - 1) {  // sum_partials_kernel's loop and reduction, exactly
+    __syncthreads();  // sh reused
+    float v = 0.f;
+    for (int i = threadIdx.x; i < lf.n; i += kAdamThreads) v += lf.partial[i];
+    const float tl = block_sum(v, sh);
+    if (threadIdx.x == 0) lf.out[0] = tl * lf.scale;
   }
 }
 
@@ -261,14 +271,17 @@ extern "C" gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logit
                                         const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
                                         int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,
                                         gnn_stream_t stream) {
-  if (N < 0 || C < 1 || C > kMaxClasses || ldx < C || ld_d < C || !loss || (N > 0 && (!logits || !y || !mask ||
-                                                                                        !class_w || !dlogits)))
+  if (N < 0 || C < 1 || C > kMaxClasses || ldx < C || ld_d < C || (N > 0 && (!logits || !y || !mask ||
+                                                                               !class_w || !dlogits)))
     return fail(GNN_ERR_INVALID_ARG, __func__, "bad args (1 <= C <= 16)");
   const int nblk = (int)std::max<int64_t>(1, ceil_div(N, kCeThreads));
   if (!workspace || workspace_bytes < nblk * sizeof(float)) return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
   hipStream_t st = (hipStream_t)stream;
   float* partial = static_cast<float*>(workspace);
-  if (N == 0) return hip_check(hipMemsetAsync(loss, 0, sizeof(float), st), __func__);
+  if (N == 0) {
+    if (!loss) return hip_check(hipMemsetAsync(partial, 0, sizeof(float), st), __func__);  // one zero partial
+    return hip_check(hipMemsetAsync(loss, 0, sizeof(float), st), __func__);
+  }
   if (C == 2)
     masked_ce_kernel<2><<<nblk, kCeThreads, 0, st>>>(N, C, logits, ldx, y, mask, class_w, inv_denom, dlogits, ld_d,
                                                      partial);
@@ -276,7 +289,16 @@ extern "C" gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logit
     masked_ce_kernel<0><<<nblk, kCeThreads, 0, st>>>(N, C, logits, ldx, y, mask, class_w, inv_denom, dlogits, ld_d,
                                                      partial);
   GNN_LAUNCH_CHECK();
+  if (!loss) return GNN_OK;  // the partials stay in the workspace (gnn_masked_ce_finish / ClipAdam)
   sum_partials_kernel<<<1, 256, 0, st>>>(partial, nblk, inv_denom, loss);
+  GNN_LAUNCH_CHECK();
+  return GNN_OK;
+}
+
+extern "C" gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, float inv_denom, float* loss,
+                                           gnn_stream_t stream) {
+  if (!partial || !loss || nblk < 1) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
+  sum_partials_kernel<<<1, 256, 0, (hipStream_t)stream>>>(partial, nblk, inv_denom, loss);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }
@@ -305,7 +327,9 @@ extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, 
   }
   hipStream_t st = (hipStream_t)stream;
   float* partial = static_cast<float*>(workspace);
-  grad_sq_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, step);
+  LossFinish lf{grp->loss_partial, grp->loss_nblk, grp->loss_scale, grp->loss_out};
+  if (lf.partial && (!lf.out || lf.n < 1)) return fail(GNN_ERR_INVALID_ARG, __func__, "loss_partial needs loss_out and loss_nblk >= 1");
+  grad_sq_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, step, lf);
   GNN_LAUNCH_CHECK();
   clip_adam_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, kAdamBlocks, step, grp->max_norm, grp->lr,
                                                          grp->beta1, grp->beta2, grp->eps, grp->weight_decay, norm_out,

@@ -581,11 +581,14 @@ def _graph_seed_counter(device: torch.device) -> torch.Tensor:
     return c
 
 
-# Inside train_gnn.CapturedStep the counter's per-step bump is deferred to the step's end: ClipAdam's
-# launch carries it (gnn_adam_group.bump_counter) — one launch fewer per replayed step — or, with
-# another optimizer, CapturedStep records the add itself at the end of the capture.
+# Inside train_gnn.CapturedStep two pieces of end-of-step work are deferred to the step's end: the
+# dropout counter's per-step bump and the fused CE's loss scalar (nothing reads either before the
+# optimizer in a training step).  ClipAdam's launch carries both (gnn_adam_group.bump_counter /
+# loss_partial) — two launches fewer per replayed step — or, with another optimizer, CapturedStep
+# records them itself at the end of the capture.
 _BUMP_DEFER = [False]
 _PENDING_BUMP = {}
+_PENDING_LOSS = {}  # device -> (partials workspace, nblk, inv_denom, loss tensor)
 
 
 class deferred_seed_bumps:
@@ -598,7 +601,25 @@ class deferred_seed_bumps:
     def __exit__(self, *exc):
         _BUMP_DEFER[0] = False
         _PENDING_BUMP.clear()
+        _PENDING_LOSS.clear()
         return False
+
+
+def defer_loss_sum(device: torch.device, ws: torch.Tensor, nblk: int, inv_denom: float, loss: torch.Tensor) -> bool:
+    """Called by the fused CE: True when its loss scalar is left to the step's end (then the CE
+    launched with loss = NULL and ``ws`` holds its partials until then)."""
+    if not _BUMP_DEFER[0] or not torch.cuda.is_current_stream_capturing() or device in _PENDING_LOSS:
+        return False
+    _PENDING_LOSS[device] = (ws, int(nblk), float(inv_denom), loss)
+    return True
+
+
+def take_loss_sum(device: torch.device):
+    """The deferred CE loss of this step ((ws, nblk, inv_denom, loss) — the optimizer's launch
+    finishes it), or None."""
+    if not _BUMP_DEFER[0] or not torch.cuda.is_current_stream_capturing():
+        return None
+    return _PENDING_LOSS.pop(device, None)
 
 
 def take_seed_bump(device: torch.device):
@@ -609,10 +630,13 @@ def take_seed_bump(device: torch.device):
 
 
 def flush_seed_bumps() -> None:
-    """Record the owed bumps (an add per counter) into the capture in progress."""
+    """Record the owed end-of-step work (a counter add, a loss sum) into the capture in progress."""
     for ctr in _PENDING_BUMP.values():
         ctr.add_(1)
     _PENDING_BUMP.clear()
+    for dev, (ws, nblk, inv_denom, loss) in _PENDING_LOSS.items():
+        _lib.call("gnn_masked_ce_finish", ws.data_ptr(), nblk, inv_denom, loss.data_ptr(), _lib.stream_handle(dev))
+    _PENDING_LOSS.clear()
 
 
 def dropout_seeds(L: int, p: float, x: torch.Tensor):

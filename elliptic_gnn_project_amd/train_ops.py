@@ -54,9 +54,14 @@ class _MaskedCE(torch.autograd.Function):
         dl = buf[:, C:]
         loss = torch.empty((), dtype=torch.float32, device=logits.device)
         ws = _ws(_ce_ws_bytes(N), logits.device)
+        from .fused import defer_loss_sum
+
+        nblk = max(1, -(-N // 256))  # gnn_masked_ce_f32's partials (256-row blocks)
+        deferred = defer_loss_sum(logits.device, ws, nblk, float(inv_denom), loss)  # captured step: at its end
         _lib.call("gnn_masked_ce_f32", N, C, logits.data_ptr(), C, y.data_ptr(), mask_u8.data_ptr(),
-                  class_w.data_ptr(), float(inv_denom), dl.data_ptr(), 2 * C, loss.data_ptr(), ws.data_ptr(),
-                  ws.numel() * 4, _lib.stream_handle(logits.device))
+                  class_w.data_ptr(), float(inv_denom), dl.data_ptr(), 2 * C,
+                  None if deferred else loss.data_ptr(), ws.data_ptr(), ws.numel() * 4,
+                  _lib.stream_handle(logits.device))
         ctx.save_for_backward(buf)
         ctx.C = C
         return loss
@@ -139,13 +144,22 @@ class ClipAdam(torch.optim.Optimizer):
             if cached is None or cached[0] != key:
                 cached = (key, self._build(group, ps))
                 self._groups[gi] = cached
-            from .fused import take_seed_bump
+            from .fused import take_loss_sum, take_seed_bump
 
-            bump = take_seed_bump(dev)  # a captured step's dropout counter, advanced by this launch
-            cached[1].bump_counter = bump.data_ptr() if bump is not None else None
-            _lib.call("gnn_clip_adam_f32", cached[1], group["step_t"].data_ptr(), self.last_norm.data_ptr(),
+            # a captured step's end-of-step work rides in this launch: the dropout counter's bump and
+            # the fused CE's loss sum
+            g = cached[1]
+            bump = take_seed_bump(dev)
+            g.bump_counter = bump.data_ptr() if bump is not None else None
+            ls = take_loss_sum(dev) if gi == 0 else None
+            if ls is not None:
+                g.loss_partial, g.loss_nblk, g.loss_scale, g.loss_out = ls[0].data_ptr(), ls[1], ls[2], ls[3].data_ptr()
+            _lib.call("gnn_clip_adam_f32", g, group["step_t"].data_ptr(), self.last_norm.data_ptr(),
                       self._ws.data_ptr(), self._ws.numel() * 4, _lib.stream_handle(dev))
-            cached[1].bump_counter = None
+            g.bump_counter = g.loss_partial = g.loss_out = None
+            g.loss_nblk, g.loss_scale = 0, 0.0
+            if ls is not None:
+                self._held_loss_ws = ls[0]  # the partials stay allocated with the graph
         return loss
 
     @staticmethod

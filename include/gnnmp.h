@@ -493,6 +493,10 @@ gnn_status gnn_time_inject_sin_f32(const float* x, int64_t ldx, int64_t N, int64
  * loss_vec.mean() with inv_denom = 1 / n_train, src/train_gnn.py:175); dlogits = d(*loss)/dx
  * (zero on every other row).  C <= 16.  Deterministic fixed-order reduction. */
 gnn_status gnn_masked_ce_workspace_size(int64_t N, size_t* bytes);
+/* loss = NULL (ABI 18): the per-block partial sums stay in the workspace (its first ceil(N / 256)
+ * floats) and the loss is finished later — by gnn_masked_ce_finish, or inside a gnn_clip_adam_f32
+ * call (gnn_adam_group.loss_partial) when nothing reads it before the optimizer (a captured step). */
+gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, float inv_denom, float* loss, gnn_stream_t stream);
 gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logits, int64_t ldx, const int64_t* y,
                              const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
                              int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,
@@ -517,6 +521,10 @@ typedef struct {
   int64_t* bump_counter;   /* optional (ABI 18): a device int64 the call increments by one (the
                               dropout seed counter of a captured step — gnn_gemm_nt_params.seed_ptr
                               — advanced at the step's end instead of by a launch of its own) */
+  const float* loss_partial; int32_t loss_nblk; float loss_scale; float* loss_out;
+                           /* optional (ABI 18): *loss_out = loss_scale · Σ loss_partial[0 .. loss_nblk)
+                              in gnn_masked_ce_f32's order — the loss of a gnn_masked_ce_f32 call made
+                              with loss = NULL, finished in this call's first launch */
 } gnn_adam_group;
 gnn_status gnn_clip_adam_workspace_size(size_t* bytes);
 gnn_status gnn_clip_adam_f32(const gnn_adam_group* group, float* step, float* norm_out, void* workspace,

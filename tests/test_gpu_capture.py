@@ -58,8 +58,7 @@ def test_captured_step_matches_eager(device, arch, split):
     from elliptic_gnn_project_amd.train_gnn import CapturedStep
 
     m_e, step_e, _, _ = _setup(device, arch)
-    for _ in range(5):
-        step_e()
+    losses_e = [float(step_e().item()) for _ in range(5)]
     m_g, step_g, fwd_bwd, opt = _setup(device, arch)
     mids = []
     if split:  # the N>1 form with a stand-in for the all-reduce (identity: x * 1)
@@ -69,8 +68,10 @@ def test_captured_step_matches_eager(device, arch, split):
     else:
         cs = CapturedStep(step_g, warmup=3)
     cs()
-    cs()
+    out = cs()
     torch.cuda.synchronize()
+    # the replayed step's loss (finished at the step's end, in ClipAdam's launch) == the eager one
+    assert float(out.item()) == losses_e[-1]
     if split:
         assert len(mids) == 5  # 3 warm-up + 2 replays ran the eager middle
     for (k, a), b in zip(m_e.state_dict().items(), m_g.state_dict().values()):

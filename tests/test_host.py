@@ -148,7 +148,8 @@ STRUCTS = {
                                                "b_ready"]),
     "gnn_adam_tensor": ("GnnAdamTensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel"]),
     "gnn_adam_group": ("GnnAdamGroup", ["num_tensors", "lr", "beta1", "beta2", "eps", "weight_decay", "max_norm",
-                                        "tensors", "skip_nonfinite", "bump_counter"]),
+                                        "tensors", "skip_nonfinite", "bump_counter", "loss_partial", "loss_nblk",
+                                        "loss_scale", "loss_out"]),
     "gnn_gemm_tn_params": ("GnnGemmTNParams", ["M", "Nr", "g", "ldg", "dz", "lddz", "proj", "nproj", "h", "ldh",
                                                "hscale", "gout", "ldgout", "a1", "lda1", "k1", "a2", "lda2", "k2",
                                                "math", "a_dtype", "h_dtype", "a_planes", "planes_ld",
