@@ -1404,7 +1404,9 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
   const int rpw = 16;
   const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256) + (unsigned)a.hp.blocks;
   hipStream_t st = (hipStream_t)stream;
-  if (vec == 4) agg_wave_kernel<GNN_AGG_MEAN, 4, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
+  if (vec == 4 && ceil_div(width, 4) <= 64)  // one pass per row (e.g. a 168-wide padded x: 42 lanes)
+    agg_wave_kernel<GNN_AGG_MEAN, 4, 1, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
+  else if (vec == 4) agg_wave_kernel<GNN_AGG_MEAN, 4, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
   else agg_wave_kernel<GNN_AGG_MEAN, 2, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
   return hip_check(hipGetLastError(), fn);
 }

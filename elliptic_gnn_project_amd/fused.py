@@ -29,7 +29,7 @@ import torch
 from . import _lib
 from .aggregation import KernelTimer, aggregate, agg_bytes
 from .graph import GraphPlan, get_plan
-from .planes import (BfImage, HalfPairImage, SplitImage, bf_x_image, h2_ok, is_registered, mean_planes_ok,
+from .planes import (BfImage, HalfPairImage, SplitImage, bf_x_image, h2_ok, is_registered, mean_planes_ok, x_padded,
                      register_input, x_image, x_only_image)
 
 # The layer-1 operand [agg | x] as a split image (planes.py): on by default, GNNMP_PLANES=0 runs
@@ -45,6 +45,9 @@ _KEEP_MASK = os.environ.get("GNNMP_KEEP_MASK", "0") == "1"
 # The SAGE layer-0 half-pair NT's weight prep (its B image) rides in K1's launch on extra blocks
 # beside the gather (gnn_sage_mean_fwd_h2 prep_b); GNNMP_K1_PREP=0 leaves it to the NT call (A/B)
 _K1_PREP = os.environ.get("GNNMP_K1_PREP", "1") != "0"
+# K1 gathers a zero-padded copy of the registered x (rows of col2 = 168 floats, 16-byte pieces);
+# GNNMP_K1_PAD=0 gathers x itself (8-byte pieces, two passes per row) (A/B)
+_K1_PAD = os.environ.get("GNNMP_K1_PAD", "1") != "0"
 # GNNMP_SIDE_PREP=1: the SAGE layer-0 NT's weight prep (the B image, latency-bound work over the
 # weights only) on a side stream beside K1, joined before the NT.  Off by default: measured
 # (profiles/r18h) 0.3692 vs 0.3637 ms per step in line — the captured fork / join costs more than
@@ -353,7 +356,8 @@ class _FusedSAGE(torch.autograd.Function):
                     with torch.cuda.stream(side):
                         gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="prep", **nt_kw)
                     ready = True
-                ctx.image = (im, im.fill_mean(plan, h, keep, prep_b=prep_b))
+                xp = x_padded(h, im.col2) if _K1_PAD and im.col2 % 4 == 0 and im.col2 > h.size(1) else None
+                ctx.image = (im, im.fill_mean(plan, h, keep, prep_b=prep_b, x_pad=xp))
                 if side is not None:
                     cur.wait_stream(side)
                 hn = gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="ready" if ready else None, **nt_kw)

@@ -72,16 +72,19 @@ class SplitImage:
             _lib.call(self._split_fn, x.data_ptr(), int(x.stride(0)), self.n, self.k2, self.ptr, self.ld,
                       self.ps, self.col2, self.ld - self.col2, _lib.stream_handle(x.device))
 
-    def fill_mean(self, plan, x: torch.Tensor, keep=None, prep_b=None) -> int:
+    def fill_mean(self, plan, x: torch.Tensor, keep=None, prep_b=None, x_pad=None) -> int:
         """K1: planes of mean_{j->i} x[j] into columns [0, col2); returns the new generation.
         keep (half-pair images only): (mask [N, 4] int32, cols, p, seed, seed_ptr) — K1 also writes
         the dropout keep bits of the NT that reads this image (include/gnnmp.h gnn_sage_mean_fwd_h2).
         prep_b (half-pair images only): the GnnGemmNTParams of that NT (fused.gemm_nt b_stage
-        "params"); its B-image prep runs inside K1's launch, the NT then runs with b_ready."""
+        "params"); its B-image prep runs inside K1's launch, the NT then runs with b_ready.
+        x_pad: x padded with zero columns to the image's col2 (planes.x_padded): K1 gathers it
+        (16-byte pieces) and writes the agg half at full width, padding columns zero."""
         from .aggregation import KernelTimer, agg_bytes
 
         e0 = KernelTimer.begin()
-        args = (plan.c_graph, plan.deg.data_ptr(), x.data_ptr(), int(x.stride(0)), self.k1, self.ptr, self.ld,
+        src, F = (x_pad, int(x_pad.size(1))) if x_pad is not None else (x, self.k1)
+        args = (plan.c_graph, plan.deg.data_ptr(), src.data_ptr(), int(src.stride(0)), F, self.ptr, self.ld,
                 self.ps, self.col2)
         if self.nplanes == 2:
             km, cols, p, seed, sptr = keep if keep is not None else (None, 0, 0.0, 0, None)
@@ -142,6 +145,24 @@ def x_image(x: torch.Tensor, cls=SplitImage) -> SplitImage:
         im.fill_x(x)
         im.x_key = key
     return im
+
+
+def x_padded(x: torch.Tensor, width: int) -> torch.Tensor:
+    """x with its rows padded by zero columns to ``width`` (a multiple of 4: 16-byte rows), cached
+    on x with the image key: K1's gather then reads one 16-byte piece per lane (VEC 4, one pass
+    over the row) instead of two 8-byte ones.  The padding columns aggregate to the zeros the
+    image holds there anyway."""
+    key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), int(width))
+    got = getattr(x, _ATTR + "_pad", None)
+    if got is not None and got[0] == key:
+        return got[1]
+    xp = torch.zeros((x.size(0), width), dtype=x.dtype, device=x.device)
+    xp[:, : x.size(1)].copy_(x)
+    try:
+        setattr(x, _ATTR + "_pad", (key, xp))
+    except (AttributeError, RuntimeError):
+        pass
+    return xp
 
 
 def h2_ok(x: torch.Tensor) -> bool:

@@ -187,6 +187,26 @@ def test_k1_prep_b_then_ready_equals_one_call(device):
     assert torch.equal(one, two)
 
 
+@pytest.mark.parametrize("cls", ["h2", "split"])
+def test_k1_padded_x_equals_x(device, cls):
+    """K1 over x padded with zero columns to the image's col2 (16-byte pieces, one pass per row)
+    writes the image bit for bit as K1 over x itself."""
+    from elliptic_gnn_project_amd.planes import HalfPairImage, SplitImage, x_padded
+
+    data, plan, x = _plan_and_x(20_000, 30_000, 5, device)
+    C = HalfPairImage if cls == "h2" else SplitImage
+    im = C(x.size(0), x.size(1), x.size(1), device)
+    im.fill_x(x)
+    im.fill_mean(plan, x)
+    img0 = im.img.clone()
+    im.img.fill_(7)
+    im.fill_x(x)
+    xp = x_padded(x, im.col2)
+    assert xp.shape == (x.size(0), im.col2) and x_padded(x, im.col2) is xp  # cached
+    im.fill_mean(plan, x, x_pad=xp)
+    assert torch.equal(im.img, img0)
+
+
 def test_fused_sage_k1_prep_equals_nt_prep(device):
     """The SAGE train step with the layer-0 B prep inside K1's launch (default) and inside the NT
     call (GNNMP_K1_PREP=0): bit-identical logits and gradients."""
@@ -198,16 +218,17 @@ def test_fused_sage_k1_prep_equals_nt_prep(device):
     torch.manual_seed(3)
     model = SAGENet(x.size(1), 128, layers=2, dropout=0.5).to(device).train()
     res = []
-    saved = fused._K1_PREP
+    saved, saved_pad = fused._K1_PREP, fused._K1_PAD
     for on in (True, False):
         fused._K1_PREP = on
+        fused._K1_PAD = on  # (also: K1 over the padded x vs x itself)
         try:
             model.zero_grad()
             out, loss = _sage_step(model, x, ei, 79)
             loss.backward()
             res.append((out.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()}))
         finally:
-            fused._K1_PREP = saved
+            fused._K1_PREP, fused._K1_PAD = saved, saved_pad
     (o1, g1), (o2, g2) = res
     assert torch.equal(o1, o2)
     for k in g1:
