@@ -45,10 +45,10 @@ _KEEP_MASK = os.environ.get("GNNMP_KEEP_MASK", "0") == "1"
 # The SAGE layer-0 half-pair NT's weight prep (its B image) rides in K1's launch on extra blocks
 # beside the gather (gnn_sage_mean_fwd_h2 prep_b); GNNMP_K1_PREP=0 leaves it to the NT call (A/B)
 _K1_PREP = os.environ.get("GNNMP_K1_PREP", "1") != "0"
-# GNNMP_K1_PAD=1: K1 gathers a zero-padded copy of the registered x (rows of col2 = 168 floats,
-# 16-byte pieces, one pass per row) instead of x itself (8-byte pieces, two passes) — an A/B knob,
-# off until measured on the headline step
-_K1_PAD = os.environ.get("GNNMP_K1_PAD", "0") == "1"
+# K1 gathers a zero-padded copy of the registered x (rows of col2 = 168 floats, 16-byte pieces,
+# one pass per row, cached on x) instead of x itself (8-byte pieces, two passes): K1 107.0 ->
+# 92.5 us, the headline step 0.3426 -> 0.3299 ms (profiles/r19n_ab.txt).  GNNMP_K1_PAD=0: A/B
+_K1_PAD = os.environ.get("GNNMP_K1_PAD", "1") != "0"
 # GNNMP_SIDE_PREP=1: the SAGE layer-0 NT's weight prep (the B image, latency-bound work over the
 # weights only) on a side stream beside K1, joined before the NT.  Off by default: measured
 # (profiles/r18h) 0.3692 vs 0.3637 ms per step in line — the captured fork / join costs more than
