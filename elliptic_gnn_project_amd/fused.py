@@ -331,7 +331,14 @@ class _FusedSAGE(torch.autograd.Function):
                 nxt = BfImage(h.size(0), fo, fo, h.device) if not last_hidden else None
                 out = nxt.a2 if nxt is not None else torch.empty((h.size(0), fo), dtype=torch.bfloat16,
                                                                   device=h.device)
-                aggregate(plan, h, _lib.AGG_MEAN, nodew=plan.deg, out=bim.a1)
+                if _K1_PAD and bim.k2 == bim.k1 < bim.col2 and bim.col2 % 4 == 0 and bim.ld >= 2 * bim.col2:
+                    # h is the image's A2 half, zero columns up to ld (a padded image is zero-
+                    # allocated): gather it there at the padded width, 8-byte pieces in one pass
+                    # per row; the padding columns aggregate to the zeros already in A1's
+                    aggregate(plan, bim.img[:, bim.col2: 2 * bim.col2], _lib.AGG_MEAN, nodew=plan.deg,
+                              out=bim.img[:, : bim.col2])
+                else:
+                    aggregate(plan, h, _lib.AGG_MEAN, nodew=plan.deg, out=bim.a1)
                 hn = gemm_nt(None, None, fo, planes=bim, out=out, **nt_kw)
                 ctx.bimgs[l] = bim
                 aggs.append(bim.a1)

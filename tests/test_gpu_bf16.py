@@ -273,6 +273,31 @@ def test_fused_sage_bf16_image_equals_tiled(device, monkeypatch):
         assert rel_l2(a, b) < 5e-3
 
 
+def test_fused_sage_bf16_k1_padded_equals_unpadded(device, monkeypatch):
+    """Layer 0 of the bf16-storage SAGE gathers x from the image's zero-padded A2 half at the padded
+    width (168 columns, 8-byte pieces) instead of x itself (166, 4-byte): logits and gradients are
+    bit for bit the same (same slot order, same f32 sums; the padding columns aggregate to zero)."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.gnn import SAGENet
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=6000, num_edges=9000, seed=15),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+    x_bf = data.x.to(torch.bfloat16).to(device)
+    ei = data.edge_index.to(device)
+    res = []
+    for flag in (True, False):
+        monkeypatch.setattr(fused, "_K1_PAD", flag)
+        torch.manual_seed(3)
+        model = SAGENet(data.x.size(1), 128, layers=3, dropout=0.0).to(device)
+        logits = model(x_bf, ei)
+        logits.square().sum().backward()
+        res.append((logits.detach().cpu(), [p.grad.detach().cpu() for p in model.parameters()]))
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("form,k1,M,gdt", [("dz_mask", 166, 5000, "f32"), ("g_mask", 166, 4133, "f32"),
                                            ("g_mask", 128, 3001, "f32"), ("dz_mask", 128, 40, "f32"),
                                            ("dz_mask", 128, 200_000, "bf16"), ("g_mask", 128, 200_000, "bf16"),
