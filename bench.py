@@ -12,10 +12,11 @@ N > 1 (launched by torch.distributed.run, one rank per GPU): ONE global graph is
 by whole timesteps over the ranks (distributed.shard_graph: LPT bin-packing, no cross-timestep
 edges, so no halo exchange); gradients are summed with one flat RCCL all-reduce per step, the
 loss is normalised by the global train count and BatchNorm (SAGE-ResBN) is SyncBN.
-  --scale weak   (default) the global graph is N Elliptic-shaped blocks (seeds 42..42+N-1,
-                 49 timesteps each), partitioned by (block, timestep): per-GPU work fixed.
-  --scale strong the global graph is the ONE 203,769-node Elliptic graph split N ways
-                 (BASELINE configs[3], rec_k8: --arch sage_resbn --scale strong).
+  --scale strong (default) the global graph is the ONE 203,769-node Elliptic graph split N
+                 ways — the metric's named workload ("Elliptic 203k/234k/166-feat, 1->8 MI355X"),
+                 so the 1/2/4/8 lines form a strong-scaling curve over it.
+  --scale weak   the global graph is N Elliptic-shaped blocks (seeds 42..42+N-1, 49 timesteps
+                 each), partitioned by (block, timestep): per-GPU work fixed.
 value = edges of the global graph x steps / max-over-ranks wall time.
 
 Extra fields: ``roofline`` (dominant libgnnmp kernel: algorithmic bytes per launch / its
@@ -80,8 +81,9 @@ def parse():
     ap.add_argument("--arch", default="sage", choices=sorted(PRESETS), help="workload (sage = headline)")
     ap.add_argument("--aten-step", action="store_true",
                     help="loss/clip/Adam with the ATen ops instead of the fused libgnnmp step ops")
-    ap.add_argument("--scale", default="weak", choices=["weak", "strong"],
-                    help="N>1: weak = one Elliptic block per rank; strong = the one Elliptic graph split N ways")
+    ap.add_argument("--scale", default="strong", choices=["weak", "strong"],
+                    help="N>1: strong (default) = the one Elliptic graph split N ways; weak = one Elliptic "
+                         "block per rank")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only for multi-rank tests on one device")
     ap.add_argument("--cpu-1t-seconds", type=float, default=8.0, help="1-thread CPU baseline sample budget")
@@ -89,6 +91,13 @@ def parse():
                     help="CPU rehearsal of the N>1 launch (tests): ranks rendezvous, build and shard the global "
                          "graph, time an empty step, reduce and report; no device work")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # tests: this rank raises
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="before the warm-up: hold the GPU busy this long with a device-to-device copy loop (no "
+                         "step work) so the timed steps do not run on clocks still ramping up from the idle "
+                         "setup phase; 0 disables")
+    ap.add_argument("--step-trace", action="store_true",
+                    help="diagnostic: record a HIP event between the timed steps and print each step's GPU "
+                         "time (and the host's enqueue time) to stderr")
     return ap.parse_args()
 
 
@@ -469,10 +478,11 @@ def main():
 
     if use_graph:
         from elliptic_gnn_project_amd.train_gnn import CapturedStep
+        # defer_loss: the loss is read only after the step (returned, never used inside it)
         if bucket is None or rccl:
-            step = CapturedStep(eager_step)
+            step = CapturedStep(eager_step, defer_loss=True)
         else:
-            step = CapturedStep(fwd_bwd, mid=allreduce, tail=opt_step)
+            step = CapturedStep(fwd_bwd, mid=allreduce, tail=opt_step, defer_loss=True)
     else:
         step = eager_step
 
@@ -505,20 +515,60 @@ def main():
     return report(args, preset, full, E_global, data, dist, world, rank, dev, step, bf16, extras, launch)
 
 
+def settle(dev, ms: float):
+    """Bring the GPU out of its idle clock state before the warm-up: the setup phase (graph build,
+    capture) leaves it idle for seconds, and the first ~30 replayed steps then run 5-10 % slow
+    while the clocks ramp (profiles/r22_timing.txt: per-step events 0.34-0.37 ms for the first
+    15 steps, 0.32 ms after).  A device-to-device copy loop over two 256 MiB scratch buffers — no
+    model, graph or optimizer state is touched, nothing of the step runs — for ``ms`` of wall
+    time.  Returns the description the JSON line carries, or None."""
+    if dev.type != "cuda" or ms <= 0:
+        return None
+    a = torch.empty(64 << 20, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    a.zero_()
+    t0 = time.perf_counter()
+    n = 0
+    while 1e3 * (time.perf_counter() - t0) < ms:
+        for _ in range(8):
+            b.copy_(a)
+            a.copy_(b)
+        n += 16
+        torch.cuda.synchronize(dev)
+    del a, b
+    return f"{n} device copies of 256 MiB ({1e3 * (time.perf_counter() - t0):.0f} ms) before the warm-up: clock ramp, no step work"
+
+
 def report(args, preset, full, E_global, data, dist, world, rank, dev, step, bf16, extras, launch,
            launch_check=False):
     """Warm-up, the timed region (barrier + synchronize on both sides, max over ranks), and rank
     0's JSON line."""
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+    settled = settle(dev, args.settle_ms)
     for _ in range(args.warmup):
         step()
     if dist is not None:
         dist.barrier()
     sync()
+    trace = args.step_trace and dev.type == "cuda"
+    evs, host = [], []
+    if trace:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if trace:
+            evs[i].record()
+            host.append(time.perf_counter())
         step()
+    if trace:
+        evs[-1].record()
     sync()
+    if trace:
+        gpu = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+        hst = [1e3 * (b - a) for a, b in zip(host, host[1:])]
+        sys.stderr.write("step-trace gpu ms: " + " ".join(f"{g:.4f}" for g in gpu) + "\n")
+        sys.stderr.write("step-trace host enqueue ms: " + " ".join(f"{h:.4f}" for h in hst) + "\n")
+        sys.stderr.write(f"step-trace first-event lag ms: {1e3 * (host[0] - t0):.4f}\n")
     if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -558,6 +608,8 @@ def report(args, preset, full, E_global, data, dist, world, rank, dev, step, bf1
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if settled:
+            line["settle"] = settled
         if launch_check:
             line["launch_check"] = "CPU rehearsal of the launch: empty step, no device work (not a measurement)"
         print(json.dumps(line), flush=True)

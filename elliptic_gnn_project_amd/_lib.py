@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libgnnmp.so"
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -123,7 +123,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("a_dtype", c_i32), ("c_dtype", c_i32),
         ("mask", c_ptr), ("ldmask", c_i64), ("mask_scale", ctypes.c_float),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
-        ("planes_format", c_i32), ("keep_mask", c_ptr), ("b_ready", c_i32),
+        ("planes_format", c_i32), ("keep_mask", c_ptr), ("b_ready", c_i32), ("planes_exp", c_i32),
     ]
 
 
@@ -140,7 +140,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("math", c_i32),
         ("a_dtype", c_i32), ("h_dtype", c_i32),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
-        ("planes_format", c_i32), ("g_dtype", c_i32),
+        ("planes_format", c_i32), ("g_dtype", c_i32), ("planes_exp", c_i32),
     ]
 
 
@@ -221,10 +221,10 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr],
     ),
-    "gnn_split_h2_f32": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_ptr]),
+    "gnn_split_h2_f32": (ctypes.c_int, [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i64, c_i32, c_ptr]),
     "gnn_sage_mean_fwd_h2": (
         ctypes.c_int,
-        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64,
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32,
          c_ptr, c_i64, ctypes.c_float, ctypes.c_uint64, c_ptr, ctypes.POINTER(GnnGemmNTParams), c_ptr],
     ),
     "gnn_sage_mean_bwd_f32": (

@@ -108,6 +108,7 @@ struct AggArgs {
   // split-image output (gnn_sage_mean_fwd_planes): hi / mid / lo bf16 planes at yp + p·yps, row
   // pitch ldy, columns [F, ywidth) zero
   uint16_t* yp; int64_t yps; int32_t ywidth;
+  float yscale;  // half-pair store: the image's pre-scale 2^scale_exp (exact), 1 otherwise
   // K1 of the half-pair path: the dropout keep bits of the NEXT GEMM's output rows (the NT that
   // consumes this image, N = kcols <= 128 columns), bit c of kmask[r·4 + c/32] = keep_elem(seed,
   // r·kcols + c), computed here where the gather leaves the VALU idle
@@ -507,7 +508,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
             const float t0 = c < nchunk ? acc[i][2 * q] / d : 0.0f;
             const float t1 = c < nchunk ? acc[i][2 * q + 1] / d : 0.0f;
             if constexpr (PLN == 3) split3_pair(t0, t1, w[q][0], w[q][1], w[q][2]);
-            else split_h2_pair(t0, t1, w[q][0], w[q][1]);
+            else split_h2_pair(t0 * a.yscale, t1 * a.yscale, w[q][0], w[q][1]);  // PyG's mean, then 2^exp
           }
           uint16_t* dst = a.yp + r * a.ldy + c * VEC;
 #pragma unroll
@@ -1361,8 +1362,9 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
                                       void* img, int64_t ld, int64_t plane_stride, int64_t width, gnn_stream_t stream,
                                       const char* fn, uint32_t* keep_mask = nullptr, int64_t mask_cols = 0,
                                       float dropout_p = 0.f, uint64_t seed = 0, const uint64_t* seed_ptr = nullptr,
-                                      const gnn_gemm_nt_params* prep_b = nullptr) {
+                                      const gnn_gemm_nt_params* prep_b = nullptr, int32_t scale_exp = 0) {
   if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or deg");
+  if (scale_exp < -100 || scale_exp > 100) return fail(GNN_ERR_INVALID_ARG, fn, "scale_exp outside [-100, 100]");
   if (F < 2 || ldx < F || width < F || width > ld || plane_stride < g->num_nodes * ld)
     return fail(GNN_ERR_INVALID_ARG, fn, "bad F / width / leading dimensions");
   if (g->num_nodes > 0 && (!x || !img)) return fail(GNN_ERR_INVALID_ARG, fn, "null x / image");
@@ -1375,6 +1377,7 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
   a.chan = (int32_t)F;
   a.x = x; a.ldx = ldx;
   a.yp = static_cast<uint16_t*>(img); a.ldy = ld; a.yps = plane_stride; a.ywidth = (int32_t)width;
+  a.yscale = ldexpf(1.0f, scale_exp);
   a.nrows = g->num_nodes;
   a.F = (int32_t)F;
   if (keep_mask) {
@@ -1388,7 +1391,8 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
     a.seed_ptr = reinterpret_cast<const int64_t*>(seed_ptr);
   }
   if (prep_b) {  // the half-pair NT that reads this image: its B prep joins this launch
-    if (PLN != 2 || prep_b->a_planes != img) return fail(GNN_ERR_INVALID_ARG, fn, "prep_b: the NT must read this half-pair image");
+    if (PLN != 2 || prep_b->a_planes != img || prep_b->planes_exp != scale_exp)
+      return fail(GNN_ERR_INVALID_ARG, fn, "prep_b: the NT must read this half-pair image (same planes_exp)");
     const gnn_status s = nt_h2_prep_from_params(prep_b, &a.hp, fn);
     if (s != GNN_OK) return s;
   }
@@ -1419,11 +1423,11 @@ extern "C" gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* 
 
 extern "C" gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
                                            int64_t F, void* img, int64_t ld, int64_t plane_stride, int64_t width,
-                                           uint32_t* keep_mask, int64_t mask_cols, float dropout_p, uint64_t seed,
-                                           const uint64_t* seed_ptr, const gnn_gemm_nt_params* prep_b,
+                                           int32_t scale_exp, uint32_t* keep_mask, int64_t mask_cols, float dropout_p,
+                                           uint64_t seed, const uint64_t* seed_ptr, const gnn_gemm_nt_params* prep_b,
                                            gnn_stream_t stream) {
   return sage_mean_fwd_image<2>(g, deg, x, ldx, F, img, ld, plane_stride, width, stream, __func__, keep_mask,
-                                mask_cols, dropout_p, seed, seed_ptr, prep_b);
+                                mask_cols, dropout_p, seed, seed_ptr, prep_b, scale_exp);
 }
 
 extern "C" gnn_status gnn_sage_mean_bwd_f32(const gnn_graph* g, const float* deg, const float* dout,

@@ -70,6 +70,7 @@ struct NTArgs {
   // elsewhere.  The weight-stationary kernel then stages A by plain copies (no split VALU).
   const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;
   int32_t ap_h2;  // the image is a half-pair image (2 f16 planes hi / lo, gemm_ws.hip K7a-h)
+  int32_t ap_exp; // half-pair: the image holds A · 2^ap_exp (undone in the epilogue's column scale)
   const uint32_t* kmask;  // optional dropout keep bits (half-pair NT): bit c of kmask[r·4 + c/32]
 };
 
@@ -80,6 +81,7 @@ struct H2Prep {
   int32_t k1, k2, Nc, col2;
   int32_t blocks;                    // k-steps (= blocks of the prep)
   uint4* img; float* colscale;
+  float a_unscale;                   // 2^-ap_exp of the A image (folded into colscale)
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
@@ -183,6 +185,7 @@ struct TNArgs {
   int32_t g_bf16;  // g (input) and gout (output) hold bf16 (the bf16-image TN)
   const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;  // split image of [A1 | A2] (as NTArgs)
   int32_t ap_h2;  // half-pair image (2 f16 planes)
+  int32_t ap_exp; // half-pair: the image holds A · 2^ap_exp (undone in the slab scale)
 };
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,
@@ -232,7 +235,9 @@ __device__ __forceinline__ void split3_pair(float a, float b, uint32_t& h, uint3
 }
 
 // Half-pair split (gemm_ws.hip K7a-h): hi = RNE_f16(v), lo = RNE_f16((v - hi) · 2^11); the
-// remainder is exact in f32 and v = hi + 2^-11 lo to 2^-22 |v| (|v| < 2^14 assumed by the callers).
+// remainder is exact in f32 and v = hi + 2^-11 lo to 2^-22 |v| while hi and the scaled remainder
+// are f16 normals (|v| >= 2^-13; below, an absolute 2^-36): the callers pre-scale A into
+// [2^13, 2^14) (gnn_split_h2_f32 scale_exp) and G per block into [8, 16), and need |v| < 2^15.
 __device__ __forceinline__ void split_h2_pair(float a, float b, uint32_t& h, uint32_t& l) {
   typedef _Float16 h2_ __attribute__((ext_vector_type(2)));
   typedef float f32x2_ __attribute__((ext_vector_type(2)));
@@ -261,10 +266,10 @@ void launch_tn_skinny(const TNArgs& a, int nblk, hipStream_t st);
 
 // ---- the half-pair NT's B image (K7a-h).  Per k-step s, plane p (hi' = 2^11 hi, hi, lo), slot
 // 2n + khalf: the 8 halves of column n, k = 16s + 8·khalf .. +8, of w_n · 2^-e_n, where 2^-e_n
-// brings the column's largest |w| into [8, 16) (a power of two: exact); colscale[n] = 2^(e_n - 11)
-// (written by the k-step-0 block).  One block per k-step; every block computes all column
-// exponents (max |w_n| over the whole K): NTH/64 waves, a wave's lanes across k (coalesced), in
-// passes of 4 columns whose 48 loads per lane are all issued before the first use (indices
+// brings the column's largest |w| into [8, 16) (a power of two: exact); colscale[n] =
+// 2^(e_n - 11 - ap_exp), which also undoes the A image's pre-scale (written by the k-step-0
+// block).  One block per k-step; every block computes all column exponents (max |w_n| over the
+// whole K): NTH/64 waves, a wave's lanes across k (coalesced), in passes of 4 columns whose 48 loads per lane are all issued before the first use (indices
 // clamped into the operand, the excess masked to 0: no load sits behind a branch), then a wave
 // max per column; the block's own k-step is staged in LDS on the way.  (A per-thread walk down
 // each row spent ~30 us on dependent load latency; a linear sweep into LDS atomics ~40 us on
@@ -330,7 +335,7 @@ __device__ __forceinline__ void ws_prep_h2_body(const H2Prep& a, int c) {
     }
   }
   __syncthreads();
-  if (c == 0 && tid < BN) a.colscale[tid] = sc[tid] * (1.0f / 2048.0f);
+  if (c == 0 && tid < BN) a.colscale[tid] = sc[tid] * (1.0f / 2048.0f) * a.a_unscale;  // powers of two: exact
   if (tid >= 256) return;
   const int n = tid >> 1, kh = tid & 1;
   const float inv = 1.0f / sc[n];  // a power of two: exact

@@ -800,6 +800,8 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
     a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
     a.ap_ps = p->planes_stride;
     a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
+    a.ap_exp = a.ap_h2 ? p->planes_exp : 0;
+    if (a.ap_exp < -100 || a.ap_exp > 100) return fail(GNN_ERR_INVALID_ARG, fn, "planes_exp outside [-100, 100]");
     const size_t img_bytes = (size_t)(a.ap_ld / 16) * 3 * 256 * sizeof(uint4);
     if (p->keep_mask) {
       if (!a.ap_h2 || !a.dropout || (reinterpret_cast<uintptr_t>(p->keep_mask) & 3))
@@ -946,7 +948,9 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
     a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
     a.ap_ps = p->planes_stride;
     a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
-    if (a.ap_h2) {  // the half-pair image: f16 hi / lo planes, 3 products (dz form with the h mask)
+    a.ap_exp = a.ap_h2 ? p->planes_exp : 0;
+    if (a.ap_exp < -100 || a.ap_exp > 100) return fail(GNN_ERR_INVALID_ARG, __fn, "planes_exp outside [-100, 100]");
+    if (a.ap_h2) {  // the half-pair image: f16 hi / lo planes, 3 products
       if (p->math != GNN_MATH_F32 && tn_h2_ok(a)) {
         launch_tn_h2(a, nblk, st);
         GNN_LAUNCH_CHECK();
@@ -1022,6 +1026,7 @@ static NTArgs nt_image_args(const gnn_gemm_nt_params* p) {  // the fields the im
   a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
   a.ap_ps = p->planes_stride;
   a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
+  a.ap_exp = a.ap_h2 ? p->planes_exp : 0;
   return a;
 }
 
@@ -1038,6 +1043,7 @@ gnn_status nt_h2_prep_from_params(const gnn_gemm_nt_params* p, H2Prep* out, cons
     return fail(GNN_ERR_UNSUPPORTED, fn, "prep_b needs NT params that select the half-pair NT");
   const NTArgs a = nt_image_args(p);
   const size_t img_bytes = (size_t)(a.ap_ld / 16) * 3 * 256 * sizeof(uint4);
+  if (a.ap_exp < -100 || a.ap_exp > 100) return fail(GNN_ERR_INVALID_ARG, fn, "planes_exp outside [-100, 100]");
   if (!nt_h2_ok(a) || !p->workspace || p->workspace_bytes < img_bytes + BN * sizeof(float) ||
       (reinterpret_cast<uintptr_t>(p->workspace) & 15))
     return fail(GNN_ERR_UNSUPPORTED, fn, "prep_b needs NT params that select the half-pair NT (and its workspace)");

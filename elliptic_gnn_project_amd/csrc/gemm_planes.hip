@@ -51,18 +51,19 @@ __global__ __launch_bounds__(256) void split_planes_kernel(const float* __restri
   d[ps] = l;
 }
 
-// half-pair image of an f32 matrix: one thread per column pair of one row (zeros at columns >= F)
+// half-pair image of an f32 matrix pre-scaled by the power of two s (exact): one thread per column
+// pair of one row (zeros at columns >= F)
 __global__ __launch_bounds__(256) void split_h2_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
                                                        int32_t F, uint16_t* __restrict__ img, int64_t ld, int64_t ps,
-                                                       int32_t width) {
+                                                       int32_t width, float s) {
   const int hw = width >> 1;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * hw) return;
   const int64_t r = i / hw;
   const int c = 2 * (int)(i - r * hw);
   const float* xr = x + r * ldx;
-  const float a = c < F ? xr[c] : 0.0f;
-  const float b = c + 1 < F ? xr[c + 1] : 0.0f;
+  const float a = c < F ? xr[c] * s : 0.0f;
+  const float b = c + 1 < F ? xr[c + 1] * s : 0.0f;
   uint32_t h, l;
   split_h2_pair(a, b, h, l);
   uint32_t* d = reinterpret_cast<uint32_t*>(img + r * ld + c);
@@ -446,7 +447,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_planes_kernel(TNArgs a) {
 // the chunk loop) and held as three f16 planes hi' = 2^11 hi, hi, lo.  Three products per k-tile
 // into one accumulator (the split-image kernel above runs six):
 //     acc += G_hi'·A_hi + G_lo·A_hi + G_hi·A_lo  (= 2^11 s_b · Gᵀ·A up to 2^-22 relative)
-// and the slab gets acc · 2^-11 / s_b (exact).  The side sums (Σ G, dzᵀ·h, Σ dz) are f32 sums of
+// and the slab gets acc · 2^-11 / s_b (exact; also / 2^ap_exp, the A image's pre-scale).  The side sums (Σ G, dzᵀ·h, Σ dz) are f32 sums of
 // the unscaled values, as in the split-image kernel.  Geometry, the chunk pipeline and slab
 // layout are the split-image kernel's: 4 waves, wave w owns dW rows 32w .. +32 x all KT k-tiles,
 // 16-row chunks, one barrier per chunk, the staging of chunk c+1 spread over chunk c's 3·KT MFMA
@@ -564,7 +565,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
     int E = 0;
     if (bound > 0.f && isfinite(bound)) frexpf(bound, &E);  // bound < 2^E
     gsc = ldexpf(1.0f, 4 - E);                               // |G · gsc| < 16
-    gunsc = ldexpf(1.0f, E - 4 - 11);                        // slab = acc · 2^-11 / gsc
+    gunsc = ldexpf(1.0f, E - 4 - 11 - a.ap_exp);             // slab = acc · 2^-11 / gsc / 2^ap_exp
   };
 
   const int Mi = (int)a.M;
@@ -1178,7 +1179,9 @@ void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st) {
 using namespace gnnmp;
 
 extern "C" gnn_status gnn_split_h2_f32(const float* x, int64_t ldx, int64_t rows, int64_t F, void* img, int64_t ld,
-                                       int64_t plane_stride, int64_t col0, int64_t width, gnn_stream_t stream) {
+                                       int64_t plane_stride, int64_t col0, int64_t width, int32_t scale_exp,
+                                       gnn_stream_t stream) {
+  if (scale_exp < -100 || scale_exp > 100) return fail(GNN_ERR_INVALID_ARG, __func__, "scale_exp outside [-100, 100]");
   if (rows < 0 || F < 0 || ldx < F || width < F || (width & 1) || (col0 & 1) || col0 < 0 || col0 + width > ld ||
       plane_stride < rows * ld || (plane_stride & 1) || (ld & 1))
     return fail(GNN_ERR_INVALID_ARG, __func__, "bad shapes (width >= F, even width / col0 / ld / plane_stride)");
@@ -1187,7 +1190,8 @@ extern "C" gnn_status gnn_split_h2_f32(const float* x, int64_t ldx, int64_t rows
   if (!img || (reinterpret_cast<uintptr_t>(img) & 3)) return fail(GNN_ERR_INVALID_ARG, __func__, "null or unaligned image");
   const int64_t n = rows * (width / 2);
   split_h2_kernel<<<(unsigned)ceil_div(n, 256), 256, 0, (hipStream_t)stream>>>(
-      x, ldx, rows, (int32_t)F, static_cast<uint16_t*>(img) + col0, ld, plane_stride, (int32_t)width);
+      x, ldx, rows, (int32_t)F, static_cast<uint16_t*>(img) + col0, ld, plane_stride, (int32_t)width,
+      ldexpf(1.0f, scale_exp));
   return hip_check(hipGetLastError(), __func__);
 }
 

@@ -702,19 +702,20 @@ __global__ __launch_bounds__(256) void gemm_nt_planes_kernel(NTArgs a, const uin
 
 // ---------------------------------------------------------------- the half-pair form (K7a-h)
 // A read from a HALF-PAIR image (gemm_planes.hip, gnn_split_h2_f32): two f16 planes per f32
-// value v,
-//     hi = RNE_f16(v),   lo = RNE_f16((v - hi) · 2^11)      v = hi + 2^-11 lo + O(2^-22 |v|)
-// (the remainder v - hi is exact in f32; scaled by 2^11 it stays in f16's normal range, so small
-// values keep their relative precision).  B, from the Linear weights, each output column scaled
-// by the power of two 2^-e_n that brings its largest weight into [8, 16), is held as THREE
-// planes: hi' = 2^11·hi, hi, lo (hi' < 2^15 fits f16).  Three f16 products per k-step into ONE
-// accumulator (the split-bf16 form runs six):
-//     acc += A_hi · B_hi' + A_hi · B_lo + A_lo · B_hi   (= 2^11 · A·B, up to 2^-22 relative)
-//     C    = acc · 2^(e_n - 11)
+// value v, pre-scaled per image by 2^ap_exp so the image's largest |u| sits in [2^13, 2^14):
+//     u = v · 2^ap_exp,   hi = RNE_f16(u),   lo = RNE_f16((u - hi) · 2^11)
+// (the remainder u - hi is exact in f32; u = hi + 2^-11 lo to 2^-22 |u| while hi and the scaled
+// remainder are f16 normals, |u| >= 2^-13 — every value within 2^-26 of the image's largest,
+// whatever the input's magnitude; below f16's normal floor only an absolute 2^-36 would remain,
+// which is why the image is pre-scaled rather than stored as is).  B, from the Linear weights,
+// each output column scaled by the power of two 2^-e_n that brings its largest weight into
+// [8, 16), is held as THREE planes: hi' = 2^11·hi, hi, lo (hi' < 2^15 fits f16).  Three f16
+// products per k-step into ONE accumulator (the split-bf16 form runs six):
+//     acc += A_hi · B_hi' + A_hi · B_lo + A_lo · B_hi   (= 2^(11 + ap_exp) · A·B, up to 2^-22 relative)
+//     C    = acc · 2^(e_n - 11 - ap_exp)                 (colscale: powers of two, exact)
 // The dropped A_lo·B_lo term is 2^-22 relative: products good to ~2^-21 (fp32 rounds at 2^-24;
 // the parity bar is 1e-5), on v_mfma_f32_32x32x16_f16 (the bf16 rate).  A moves 4 B per element
-// (the split-bf16 image's 6) and the MFMA chain halves.  Needs |A| < 2^14 (planes.py checks x
-// once per input; agg = mean of x rows stays inside).
+// (the split-bf16 image's 6) and the MFMA chain halves.
 // Geometry and software pipeline as the split-image kernel (one 256-thread block per CU, wave w
 // owns columns 32w .. +32 with B stationary in AGPRs: NKS x 3 x 4 = 252 for NKS 21), 32-row tiles
 // t = blockIdx.x, += gridDim.x, two A buffers.  Slot schedule: the tile's 3·NKS MFMAs carry the
@@ -837,7 +838,8 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
   uint32_t mk[2] = {0u, 0u};  // keep-bit words: the tile being computed (loaded) / the tile in E1 (used)
   uint32_t mku = 0u;
   auto load_mk = [&](uint32_t& m, int t) __attribute__((always_inline)) {
-    if constexpr ((EPI & WS_KMASK) != 0) m = a.kmask[((int64_t)t * WS_ROWS + (lane & 31)) * 4 + wave];
+    if constexpr ((EPI & WS_KMASK) != 0)  // row clamped: the last tile's rows past M read row M - 1's word
+      m = a.kmask[min((int64_t)t * WS_ROWS + (lane & 31), M - 1) * 4 + wave];
   };
   auto e1 = [&](const floatx16& p1, int j, int part, int tp) __attribute__((always_inline)) {
     const int rl = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
@@ -1388,6 +1390,7 @@ H2Prep h2_prep_of(const NTArgs& a, uint4* img) {
   p.blocks = a.ap_ld / 16;
   p.img = img;
   p.colscale = reinterpret_cast<float*>(img + p.blocks * 3 * 256);
+  p.a_unscale = ldexpf(1.0f, -a.ap_exp);  // |ap_exp| <= 100 (gemm_nt_dispatch): a normal float
   return p;
 }
 

@@ -149,6 +149,7 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         _lib.DTYPE_BF16 if (out is not None and out.dtype == torch.bfloat16) else _lib.DTYPE_F32,
         _lib.ptr(mask), _ld(mask) if mask is not None else 0, float(mask_scale),
         *_planes_fields(planes), _lib.ptr(keep_mask), int(b_stage == "ready"),
+        int(getattr(planes, "exp", 0)),
     )
     if check_planes:
         return bool(_lib.load().gnn_gemm_nt_planes_ok(p))
@@ -204,6 +205,7 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         _lib.DTYPE_BF16 if (h is not None and h.dtype == torch.bfloat16) else _lib.DTYPE_F32,
         *_planes_fields(planes),
         _lib.DTYPE_BF16 if any(t is not None and t.dtype == torch.bfloat16 for t in (g, gout)) else _lib.DTYPE_F32,
+        int(getattr(planes, "exp", 0)),
     )
     if check_planes:
         return bool(_lib.load().gnn_gemm_tn_planes_ok(p))
@@ -263,7 +265,7 @@ def _layer0_image(x: torch.Tensor, n_out: int, nt_kw, h2: bool = False):
     """The split image of [agg | x] when the planes path takes this layer (else None): x must be a
     registered constant input (planes.register_input) — its planes are built once and reused; a
     per-batch or per-step input keeps the in-kernel split (gemm_nt over f32 [agg | x]).
-    h2: prefer the half-pair image (f16 hi / lo planes, 3 products) when x fits it (|x| < 2^14)
+    h2: prefer the half-pair image (f16 hi / lo planes, 3 products) when x fits it (finite)
     — the 2-layer net, whose layer-0 weight gradient is the TN's dz form."""
     if not (_PLANES and is_registered(x) and mean_planes_ok(x)) or x.size(0) < 32:
         return None
@@ -593,50 +595,66 @@ def _graph_seed_counter(device: torch.device) -> torch.Tensor:
     return c
 
 
-# Inside train_gnn.CapturedStep two pieces of end-of-step work are deferred to the step's end: the
-# dropout counter's per-step bump and the fused CE's loss scalar (nothing reads either before the
-# optimizer in a training step).  ClipAdam's launch carries both (gnn_adam_group.bump_counter /
-# loss_partial) — two launches fewer per replayed step — or, with another optimizer, CapturedStep
-# records them itself at the end of the capture.
-_BUMP_DEFER = [False]
+# Inside train_gnn.CapturedStep two pieces of end-of-step work can be deferred to the step's end:
+# the dropout counter's per-step bump (always: nothing in a step reads the counter after its
+# forward) and — only with CapturedStep(defer_loss=True) — the fused CE's loss scalar.  ClipAdam's
+# launch carries both (gnn_adam_group.bump_counter / loss_partial) — two launches fewer per
+# replayed step — or, with another optimizer, CapturedStep records them itself at the end of the
+# capture.  The loss deferral is opt-in because a step_fn that reads the loss before the optimizer
+# (a `loss + reg` term, a NaN guard, a running total, scaler.scale(loss)) would read the previous
+# replay's value; bench.py and train_epoch read it only after the step.
+_BUMP_DEFER = [None]  # the active deferred_seed_bumps context (or None)
 _PENDING_BUMP = {}
 _PENDING_LOSS = {}  # device -> (partials workspace, nblk, inv_denom, loss tensor)
 
 
 class deferred_seed_bumps:
-    """Context of a step capture whose dropout counter bumps run at the step's end."""
+    """Context of a step capture whose dropout counter bumps (and, with ``defer_loss``, the fused
+    CE's loss sum) run at the step's end.  ``held``: the CE partials workspaces a deferred loss
+    reads at the step's end — the capturing CapturedStep keeps them for the graph's lifetime, so
+    no later allocation from the graph's pool can take them over (whichever launch finishes the
+    loss: ClipAdam's or the gnn_masked_ce_finish flush_seed_bumps records)."""
+
+    def __init__(self, defer_loss: bool = False):
+        self.defer_loss = bool(defer_loss)
+        self.held = []
 
     def __enter__(self):
-        _BUMP_DEFER[0] = True
+        _BUMP_DEFER[0] = self
         return self
 
     def __exit__(self, *exc):
-        _BUMP_DEFER[0] = False
+        _BUMP_DEFER[0] = None
         _PENDING_BUMP.clear()
         _PENDING_LOSS.clear()
         return False
 
 
+def _deferring() -> bool:
+    return _BUMP_DEFER[0] is not None and torch.cuda.is_current_stream_capturing()
+
+
 def defer_loss_sum(device: torch.device, ws: torch.Tensor, nblk: int, inv_denom: float, loss: torch.Tensor) -> bool:
     """Called by the fused CE: True when its loss scalar is left to the step's end (then the CE
     launched with loss = NULL and ``ws`` holds its partials until then)."""
-    if not _BUMP_DEFER[0] or not torch.cuda.is_current_stream_capturing() or device in _PENDING_LOSS:
+    if not _deferring() or not _BUMP_DEFER[0].defer_loss or device in _PENDING_LOSS:
         return False
     _PENDING_LOSS[device] = (ws, int(nblk), float(inv_denom), loss)
+    _BUMP_DEFER[0].held.append(ws)
     return True
 
 
 def take_loss_sum(device: torch.device):
     """The deferred CE loss of this step ((ws, nblk, inv_denom, loss) — the optimizer's launch
     finishes it), or None."""
-    if not _BUMP_DEFER[0] or not torch.cuda.is_current_stream_capturing():
+    if not _deferring():
         return None
     return _PENDING_LOSS.pop(device, None)
 
 
 def take_seed_bump(device: torch.device):
     """The counter whose bump this step still owes (the optimizer's launch performs it), or None."""
-    if not _BUMP_DEFER[0] or not torch.cuda.is_current_stream_capturing():
+    if not _deferring():
         return None
     return _PENDING_BUMP.pop(device, None)
 
@@ -657,7 +675,7 @@ def dropout_seeds(L: int, p: float, x: torch.Tensor):
     bumped once per forward, under HIP-graph capture (see _graph_seed_counter)."""
     if p > 0 and torch.cuda.is_current_stream_capturing():
         ctr = _graph_seed_counter(x.device)
-        if _BUMP_DEFER[0]:
+        if _BUMP_DEFER[0] is not None:
             if x.device in _PENDING_BUMP:  # a second forward in the step: its own counter value
                 ctr.add_(1)
             _PENDING_BUMP[x.device] = ctr

@@ -61,6 +61,7 @@ class SplitImage:
         self.img = torch.empty((self.nplanes, self.n, self.ld), dtype=dt, device=device)
         self.gen = 0
         self.x_key = None
+        self.exp = 0  # half-pair images: the pre-scale exponent of the image's values (h2_exp)
 
     @property
     def ptr(self) -> int:
@@ -70,7 +71,10 @@ class SplitImage:
         """Planes of x into columns [col2, ld) (zeros past k2)."""
         with torch.cuda.device(x.device):
             _lib.call(self._split_fn, x.data_ptr(), int(x.stride(0)), self.n, self.k2, self.ptr, self.ld,
-                      self.ps, self.col2, self.ld - self.col2, _lib.stream_handle(x.device))
+                      self.ps, self.col2, self.ld - self.col2, *self._exp_arg(), _lib.stream_handle(x.device))
+
+    def _exp_arg(self):
+        return ()
 
     def fill_mean(self, plan, x: torch.Tensor, keep=None, prep_b=None, x_pad=None) -> int:
         """K1: planes of mean_{j->i} x[j] into columns [0, col2); returns the new generation.
@@ -88,7 +92,7 @@ class SplitImage:
                 self.ps, self.col2)
         if self.nplanes == 2:
             km, cols, p, seed, sptr = keep if keep is not None else (None, 0, 0.0, 0, None)
-            args += (_lib.ptr(km), int(cols), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(sptr), prep_b)
+            args += (int(self.exp), _lib.ptr(km), int(cols), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(sptr), prep_b)
         elif prep_b is not None:
             raise ValueError("prep_b needs a half-pair image")
         _lib.call(self._mean_fn, *args, _lib.stream_handle(x.device))
@@ -99,15 +103,27 @@ class SplitImage:
 
 
 class HalfPairImage(SplitImage):
-    """[2, N, ld] f16 half-pair planes of [A1 | A2] (include/gnnmp.h gnn_split_h2_f32): hi =
-    RNE_f16(v), lo = RNE_f16((v - hi)·2^11).  The half-pair GEMMs read them with 3 f16 products
-    per product (the split-bf16 image needs 6) and 4 B per element (6).  Values must stay below
-    2^14 in magnitude: h2_image checks x once per input; the mean half is a mean of x's rows."""
+    """[2, N, ld] f16 half-pair planes of [A1 | A2] · 2^exp (include/gnnmp.h gnn_split_h2_f32):
+    u = v·2^exp, hi = RNE_f16(u), lo = RNE_f16((u - hi)·2^11).  The half-pair GEMMs read them with
+    3 f16 products per product (the split-bf16 image needs 6) and 4 B per element (6), and undo
+    the power-of-two pre-scale exactly in their epilogues.  ``exp`` (h2_exp of x) brings x's
+    largest magnitude into [2^13, 2^14), so every value within 2^-26 of it keeps hi and lo f16
+    normals — full 2^-22 relative precision whatever x's magnitude; the mean half is a mean of
+    x's rows and stays inside the same range."""
 
     nplanes = 2
     fmt = _lib.PLANES_HALF_PAIR
     _split_fn = "gnn_split_h2_f32"
     _mean_fn = "gnn_sage_mean_fwd_h2"
+
+    def _exp_arg(self):
+        return (int(self.exp),)
+
+    def fill_x(self, x: torch.Tensor) -> None:
+        self.exp = h2_exp(x)
+        if self.exp is None:
+            raise ValueError("a half-pair image needs finite x (h2_ok)")
+        super().fill_x(x)
 
     def keep_buffer(self) -> torch.Tensor:
         """[N, 4] int32 keep bits of the dropout that follows this image's NT (written by K1)."""
@@ -117,7 +133,7 @@ class HalfPairImage(SplitImage):
         return kb
 
 
-H2_LIMIT = 2.0 ** 14
+H2_TOP = 14  # a half-pair image's largest magnitude is pre-scaled into [2^(H2_TOP-1), 2^H2_TOP)
 
 
 def mean_planes_ok(x: torch.Tensor) -> bool:
@@ -165,19 +181,38 @@ def x_padded(x: torch.Tensor, width: int) -> torch.Tensor:
     return xp
 
 
-def h2_ok(x: torch.Tensor) -> bool:
-    """Whether x's values fit a half-pair image (|x| < 2^14; finite): one reduction per x (cached
-    with the same (data_ptr, _version) key as the image)."""
+def h2_exp(x: torch.Tensor):
+    """The half-pair pre-scale exponent of x — e = 14 - E for max|x| in [2^(E-1), 2^E), so the
+    image holds x·2^e with its largest magnitude in [2^13, 2^14) (0 for an all-zero x; clamped to
+    the ABI's [-100, 100]) — or None when x has a non-finite value (such inputs keep the split-bf16
+    image).  One reduction per x, cached with the image key (data_ptr, _version)."""
+    import math
+
     key = (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()))
-    got = getattr(x, _ATTR + "_h2ok", None)
+    got = getattr(x, _ATTR + "_h2exp", None)
     if got is not None and got[0] == key:
         return got[1]
-    ok = bool(torch.isfinite(x).all()) and float(x.abs().max()) < H2_LIMIT if x.numel() else True
+    if x.numel() == 0:
+        e = 0
+    else:
+        amax = float(x.detach().abs().amax())  # inf / nan propagate
+        if not math.isfinite(amax):
+            e = None
+        elif amax == 0.0:
+            e = 0
+        else:
+            e = max(-100, min(100, H2_TOP - math.frexp(amax)[1]))
     try:
-        setattr(x, _ATTR + "_h2ok", (key, ok))
+        setattr(x, _ATTR + "_h2exp", (key, e))
     except (AttributeError, RuntimeError):
         pass
-    return ok
+    return e
+
+
+def h2_ok(x: torch.Tensor) -> bool:
+    """Whether x fits a half-pair image: every value finite (the power-of-two pre-scale, h2_exp,
+    takes any finite magnitude)."""
+    return h2_exp(x) is not None
 
 
 _ATTR_X = _ATTR + "_x"
@@ -211,7 +246,7 @@ X_ONLY_LD = 176
 def x_only_image(x: torch.Tensor, cls=SplitImage):
     """The cached split image of a registered input x alone (x in columns [0, F), k2 = 0) for the
     GEMMs of a layer whose A operand is x (GCN / GAT layer 1: y = x·Wᵀ and dW = Gᵀ·x), or None.
-    cls: SplitImage (split-bf16, both GEMMs) or HalfPairImage (the forward NT; x must fit it).
+    cls: SplitImage (split-bf16, both GEMMs) or HalfPairImage (x must be finite: h2_ok).
 
     Built on first use (one split pass) and reused while x is unmodified (data_ptr, _version);
     every call over a registered x takes the same kernels, so repeated forwards are bit-identical."""
@@ -234,9 +269,11 @@ def x_only_image(x: torch.Tensor, cls=SplitImage):
         except (AttributeError, RuntimeError):  # e.g. inference tensors: not cached, still used
             pass
     if im.x_key != key:
+        if cls is HalfPairImage:
+            im.exp = h2_exp(x)
         with torch.cuda.device(x.device):
             _lib.call(cls._split_fn, x.data_ptr(), int(x.stride(0)), im.n, im.k1, im.ptr, im.ld, im.ps,
-                      0, im.ld, _lib.stream_handle(x.device))
+                      0, im.ld, *im._exp_arg(), _lib.stream_handle(x.device))
         im.x_key = key
     return im
 

@@ -300,9 +300,16 @@ class CapturedStep:
     and ``tail`` given), for CPU-side collectives (gloo): ``step_fn`` (forward + backward) is
     graph A, ``mid`` runs eagerly (the gradient all-reduce) and ``tail`` (the optimizer step) is
     graph B.
+
+    ``defer_loss`` (off by default): the fused CE's loss scalar is finished at the step's end —
+    inside ClipAdam's launch, or by a launch recorded at the end of the capture — one launch fewer
+    per replay.  Only for a ``step_fn`` that reads the loss after the optimizer step (returns it,
+    as bench.py and train_epoch do): read before it, the loss tensor still holds the previous
+    replay's value.  The CE partials such a loss reads at the step's end are held here
+    (``self._held``) for the graph's lifetime.
     """
 
-    def __init__(self, step_fn, warmup: int = 3, mid=None, tail=None):
+    def __init__(self, step_fn, warmup: int = 3, mid=None, tail=None, defer_loss: bool = False):
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -318,7 +325,7 @@ class CapturedStep:
         self.tail_graph = None
         # the dropout counter's per-step bump runs at the step's end (fused.deferred_seed_bumps):
         # inside ClipAdam's launch when the step has one, else as an add recorded here
-        with fused.deferred_seed_bumps():
+        with fused.deferred_seed_bumps(defer_loss=defer_loss) as dctx:
             # thread-local capture mode: the process group's watchdog thread keeps querying the events
             # of earlier (eager) collectives while this thread captures; in the default global mode
             # such a query from another thread invalidates the capture (hipErrorStreamCaptureUnsupported)
@@ -331,6 +338,7 @@ class CapturedStep:
                 with torch.cuda.graph(self.tail_graph, pool=self.graph.pool(), capture_error_mode="thread_local"):
                     tail()
                     fused.flush_seed_bumps()
+        self._held = list(dctx.held)  # buffers a replay still reads at its end (deferred loss partials)
 
     def __call__(self):
         self.graph.replay()

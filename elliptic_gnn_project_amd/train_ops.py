@@ -157,9 +157,7 @@ class ClipAdam(torch.optim.Optimizer):
             _lib.call("gnn_clip_adam_f32", g, group["step_t"].data_ptr(), self.last_norm.data_ptr(),
                       self._ws.data_ptr(), self._ws.numel() * 4, _lib.stream_handle(dev))
             g.bump_counter = g.loss_partial = g.loss_out = None
-            g.loss_nblk, g.loss_scale = 0, 0.0
-            if ls is not None:
-                self._held_loss_ws = ls[0]  # the partials stay allocated with the graph
+            g.loss_nblk, g.loss_scale = 0, 0.0  # (the partials workspace is held by the capturing CapturedStep)
         return loss
 
     @staticmethod

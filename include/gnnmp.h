@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 18
+#define GNNMP_ABI_VERSION 19
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -190,27 +190,41 @@ gnn_status gnn_sage_mean_fwd_planes(const gnn_graph* g, const float* deg, const 
                                     void* img, int64_t ld, int64_t plane_stride, int64_t width,
                                     gnn_stream_t stream);
 
-/* Half-pair images: an f32 matrix held as TWO f16 planes, hi = RNE_f16(v) and
- * lo = RNE_f16((v - hi) * 2^11), so v = hi + 2^-11 lo to 2^-22 |v| (the remainder is exact in f32;
- * scaled by 2^11 it keeps small values' relative precision).  Needs |v| < 2^14.  The half-pair
- * GEMMs (planes_format = GNN_PLANES_HALF_PAIR) run 3 f16 products per product instead of the
- * split-bf16 form's 6 and move 4 B per element instead of 6.  Same layout and arguments as the
- * split-bf16 functions above. */
+/* Half-pair images: an f32 matrix held as TWO f16 planes of its PRE-SCALED values
+ * u = v * 2^scale_exp:  hi = RNE_f16(u), lo = RNE_f16((u - hi) * 2^11), so u = hi + 2^-11 lo to
+ * 2^-22 |u| while hi and (u - hi) * 2^11 are f16 normals, i.e. |u| >= 2^-13 (below that the pair
+ * holds u to an absolute 2^-36).  The caller picks scale_exp per matrix so that its largest
+ * magnitude lands in [2^13, 2^14): scale_exp = 14 - E with max|v| in [2^(E-1), 2^E) (0 for an
+ * all-zero matrix; |scale_exp| <= 100).  Every value within 2^-26 of the matrix's largest then
+ * keeps the full 2^-22 relative precision, whatever the matrix's overall magnitude (ABI 19: the
+ * unscaled images of ABI 18 lost it below |v| ~ 2^-13).  |u| must stay below 2^15 (f16 range with
+ * headroom for the agg half, a mean of the x rows).  The consuming GEMMs undo the scale exactly
+ * (gnn_gemm_nt_params / gnn_gemm_tn_params .planes_exp, a power of two in their epilogues).  The
+ * half-pair GEMMs (planes_format = GNN_PLANES_HALF_PAIR) run 3 f16 products per product instead
+ * of the split-bf16 form's 6 and move 4 B per element instead of 6.  Otherwise the same layout and
+ * arguments as the split-bf16 functions above. */
 gnn_status gnn_split_h2_f32(const float* x, int64_t ldx, int64_t rows, int64_t F, void* img, int64_t ld,
-                            int64_t plane_stride, int64_t col0, int64_t width, gnn_stream_t stream);
-/* gnn_sage_mean_fwd_h2 optionally also writes the dropout keep bits of the NT that consumes the
- * image (keep_mask != NULL, [num_nodes][4] uint32, 16-byte aligned): bit c of keep_mask[r*4 + c/32]
- * = keep_elem(seed', r*mask_cols + c) with seed' the NT's (seed, seed_ptr) rule — the mask the NT
- * would hash itself, computed where the gather leaves the VALU idle (gnn_gemm_nt_params.keep_mask).
- * prep_b (optional): the params of the half-pair NT that reads this image (a_planes == img); its
- * B-image prep (gnn_gemm_nt_prep_b) runs inside this launch, on extra blocks beside the gather,
- * for a later gnn_gemm_nt_f32 of the same params with b_ready = 1.  UNSUPPORTED when the params
- * do not select the half-pair NT. */
+                            int64_t plane_stride, int64_t col0, int64_t width, int32_t scale_exp,
+                            gnn_stream_t stream);
+/* gnn_sage_mean_fwd_h2: K1 with a half-pair store of mean_{j->i} x[j] * 2^scale_exp (the mean
+ * rounded as gnn_sage_mean_fwd_f32 rounds it, then scaled exactly; scale_exp = the exponent of
+ * the image's x half, so |agg * 2^scale_exp| <= max|x * 2^scale_exp|).  It optionally also writes
+ * the dropout keep bits of the NT that consumes the
+ * image (keep_mask != NULL, [num_nodes][4] uint32, 16-byte aligned; the NT reads the words of
+ * ceil(num_nodes / 32) * 32 rows, clamping the row index into [0, num_nodes)): bit c of
+ * keep_mask[r*4 + c/32] = keep_elem(seed', r*mask_cols + c) with seed' the NT's (seed, seed_ptr)
+ * rule — the mask the NT would hash itself, computed where the gather leaves the VALU idle
+ * (gnn_gemm_nt_params.keep_mask).
+ * prep_b (optional): the params of the half-pair NT that reads this image (a_planes == img and
+ * planes_exp == scale_exp); its B-image prep (gnn_gemm_nt_prep_b) runs inside this launch, on
+ * extra blocks beside the gather, for a later gnn_gemm_nt_f32 of the same params with
+ * b_ready = 1.  UNSUPPORTED when the params do not select the half-pair NT. */
 struct gnn_gemm_nt_params;
 gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
-                                void* img, int64_t ld, int64_t plane_stride, int64_t width, uint32_t* keep_mask,
-                                int64_t mask_cols, float dropout_p, uint64_t seed, const uint64_t* seed_ptr,
-                                const struct gnn_gemm_nt_params* prep_b, gnn_stream_t stream);
+                                void* img, int64_t ld, int64_t plane_stride, int64_t width, int32_t scale_exp,
+                                uint32_t* keep_mask, int64_t mask_cols, float dropout_p, uint64_t seed,
+                                const uint64_t* seed_ptr, const struct gnn_gemm_nt_params* prep_b,
+                                gnn_stream_t stream);
 typedef enum {
   GNN_PLANES_SPLIT_BF16 = 0,  /* 3 bf16 planes hi / mid / lo (gnn_split_planes_f32) */
   GNN_PLANES_HALF_PAIR = 1    /* 2 f16 planes hi / lo (gnn_split_h2_f32) */
@@ -375,6 +389,8 @@ typedef struct gnn_gemm_nt_params {
   int32_t b_ready;                       /* image-A forms only: nonzero = workspace already holds the B
                                             image gnn_gemm_nt_prep_b wrote for these weights and shapes
                                             (the call launches only the GEMM) */
+  int32_t planes_exp;                    /* HALF_PAIR (ABI 19): the image holds A * 2^planes_exp
+                                            (gnn_split_h2_f32 scale_exp); C is unscaled exactly */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
@@ -406,6 +422,8 @@ typedef struct {
                                             rows; G scaled per row block by a power of two, 3 products) */
   int32_t g_dtype;                       /* gnn_dtype of g and gout (BF16: the bf16-image TN only; gout
                                             then holds the bf16-rounded G its MFMAs use) */
+  int32_t planes_exp;                    /* HALF_PAIR (ABI 19): the image holds A * 2^planes_exp; dW is
+                                            unscaled exactly */
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).

@@ -26,12 +26,27 @@ def _one_line(stdout):
 
 
 def test_self_launch_two_ranks_cpu_rehearsal():
+    """The default N > 1 line measures the metric's own workload: the ONE 203,769-node Elliptic
+    graph split over the ranks (strong scaling)."""
     r = _run(["--gpus", "2", "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--launch-check"])
     assert r.returncode == 0, r.stderr[-3000:]
     line = _one_line(r.stdout)
     assert line["n_gpus"] == 2 and line["steps"] == 2 and line["value"] > 0
+    assert line["scaling"] == "strong"
+    assert line["config"]["parallelism"] == "dp2 timestep-partitioned (strong)"
+    assert line["config"]["global_nodes"] == 203_769 and line["config"]["global_edges"] == 468_710
+    assert line["config"]["max_nodes_per_gpu"] < 203_769  # each rank holds about half
+    assert line["launch_check"]
+
+
+def test_self_launch_two_ranks_weak_scaling_option():
+    r = _run(["--gpus", "2", "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--launch-check",
+              "--scale", "weak"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _one_line(r.stdout)
+    assert line["scaling"] == "weak"
     assert line["config"]["parallelism"] == "dp2 timestep-partitioned (weak)"
-    assert line["config"]["global_nodes"] > 2 * 200_000  # two Elliptic-shaped blocks (weak scaling)
+    assert line["config"]["global_nodes"] > 2 * 200_000  # two Elliptic-shaped blocks
     assert line["launch_check"]
 
 

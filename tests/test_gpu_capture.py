@@ -54,7 +54,8 @@ def _setup(device, arch, dropout=0.0):
 
 @pytest.mark.parametrize("arch", list(ARCHS))
 @pytest.mark.parametrize("split", [False, True])
-def test_captured_step_matches_eager(device, arch, split):
+@pytest.mark.parametrize("defer_loss", [False, True])
+def test_captured_step_matches_eager(device, arch, split, defer_loss):
     from elliptic_gnn_project_amd.train_gnn import CapturedStep
 
     m_e, step_e, _, _ = _setup(device, arch)
@@ -64,18 +65,45 @@ def test_captured_step_matches_eager(device, arch, split):
     if split:  # the N>1 form with a stand-in for the all-reduce (identity: x * 1)
         params = [p for p in m_g.parameters()]
         cs = CapturedStep(fwd_bwd, warmup=3, mid=lambda: mids.append([p.grad.mul_(1.0) for p in params]),
-                          tail=opt.step)
+                          tail=opt.step, defer_loss=defer_loss)
     else:
-        cs = CapturedStep(step_g, warmup=3)
+        cs = CapturedStep(step_g, warmup=3, defer_loss=defer_loss)
+    # a deferred loss's CE partials are held by the step for the graph's lifetime
+    assert bool(cs._held) == defer_loss
     cs()
     out = cs()
     torch.cuda.synchronize()
-    # the replayed step's loss (finished at the step's end, in ClipAdam's launch) == the eager one
+    # the replayed step's loss (deferred: finished at the step's end, in ClipAdam's launch) == the eager one
     assert float(out.item()) == losses_e[-1]
     if split:
         assert len(mids) == 5  # 3 warm-up + 2 replays ran the eager middle
     for (k, a), b in zip(m_e.state_dict().items(), m_g.state_dict().values()):
         assert torch.equal(a, b), k
+
+
+def test_captured_step_loss_read_before_the_optimizer(device):
+    """A step_fn that reads the loss before opt.step() (here: a copy of it, as a NaN guard or a
+    running total would) sees THIS replay's loss under the default CapturedStep (defer_loss off):
+    the CE finishes its loss in its own launch (the deferral is opt-in)."""
+    from elliptic_gnn_project_amd.train_gnn import CapturedStep
+
+    m_e, step_e, _, _ = _setup(device, "sage")
+    losses_e = [float(step_e().item()) for _ in range(5)]
+    _, _, fwd_bwd, opt = _setup(device, "sage")
+    snap = torch.zeros((), device=device)
+
+    def step():
+        loss = fwd_bwd()
+        snap.copy_(loss)  # read before the optimizer
+        opt.step()
+        return loss
+
+    cs = CapturedStep(step, warmup=3)
+    got = []
+    for _ in range(2):
+        cs()
+        got.append(float(snap.item()))
+    assert got == losses_e[3:5]
 
 
 @pytest.mark.parametrize("arch", ["sage", "gat"])

@@ -1,13 +1,16 @@
-"""GPU: half-pair images (include/gnnmp.h gnn_split_h2_f32: f16 hi = RNE(v), lo = RNE((v - hi)·2^11))
-and the 3-product f16 GEMMs that read them — the 2-layer SAGE's layer-1 [agg | x] operand.
+"""GPU: half-pair images (include/gnnmp.h gnn_split_h2_f32: u = v·2^e, f16 hi = RNE(u),
+lo = RNE((u - hi)·2^11), e the per-image pre-scale putting max|u| in [2^13, 2^14)) and the
+3-product f16 GEMMs that read them — the 2-layer SAGE's layer-1 [agg | x] operand.
 
 * gnn_split_h2_f32 and K1's half-pair store (gnn_sage_mean_fwd_h2) are rounding work: bit-exact
   against a numpy restatement (numpy's float32 -> float16 cast is RNE), and K1's planes are the
   split of the f32 K1 output bit for bit.
 * The NT / TN kernels are floating point: within relL2 1e-6 of a float64 reference (the bound the
   split-bf16 image kernels are held to; the dropped lo·lo term is 2^-22 relative), also for
-  weights / gradients far outside [1/16, 16] (the per-column / per-block power-of-two scales),
-  and the fused SAGE step with half-pair planes within 1e-5 of the split-bf16 planes.
+  weights / gradients far outside [1/16, 16] (the per-column / per-block power-of-two scales)
+  and for inputs of any magnitude (1e-7 .. 3e4: the image's pre-scale; ABI 18's unscaled image
+  lost 9e-5 relL2 at 1e-7), and the fused SAGE step with half-pair planes within 1e-5 of the
+  split-bf16 planes and of the float64 oracle.
 """
 import numpy as np
 import pytest
@@ -16,15 +19,15 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def rel_l2(a, b):
+def rel_l2(a, b, floor=1e-30):
     a = a.detach().double().cpu()
     b = b.detach().double().cpu()
-    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+    return float((a - b).norm() / max(float(b.norm()), floor))
 
 
-def split_h2(v):
-    """hi / lo f16 words of float32 v (|v| < 2^14)."""
-    v = np.asarray(v, dtype=np.float32)
+def split_h2(v, e=0):
+    """hi / lo f16 words of float32 v · 2^e (|v · 2^e| < 2^15)."""
+    v = np.asarray(v, dtype=np.float32) * np.float32(2.0 ** e)  # exact: a power of two
     hi = v.astype(np.float16)
     r = ((v - hi.astype(np.float32)) * np.float32(2048.0)).astype(np.float32)
     lo = r.astype(np.float16)
@@ -53,18 +56,22 @@ def test_split_h2_bit_exact(device):
     x = torch.randn(777, 166, generator=g) * torch.exp(torch.randn(777, 1, generator=g) * 3)
     x[0, :8] = torch.tensor([0.0, -0.0, 1.0, -1.0, 16383.0, -2.5e-30, 1.0 + 2 ** -23, 6.0e-8])
     x = x.clamp(-16383.0, 16383.0)
-    im = HalfPairImage(777, 166, 166, device)
-    im.img.fill_(1.0)
-    im.fill_x(x.to(device))
-    got = _planes_np(im)
-    hi, lo = split_h2(x.numpy())
-    assert np.array_equal(got[0][:, 168:334], hi)
-    assert np.array_equal(got[1][:, 168:334], lo)
-    assert not got[0][:, 334:].any() and not got[1][:, 334:].any()
-    # hi + 2^-11 lo reproduces v to 2^-22 relative
-    rec = got[0][:, 168:334].view(np.float16).astype(np.float64) + got[1][:, 168:334].view(np.float16).astype(np.float64) / 2048.0
-    xd = x.double().numpy()
-    assert np.all(np.abs(rec - xd) <= 2.0 ** -22 * np.abs(xd) + 2.0 ** -36)
+    for scale, e in ((1.0, 0), (2.0 ** -30, 30), (2.0 ** 40, -40), (3e-7, 21)):  # max|x| = 16383
+        xs = x * scale
+        im = HalfPairImage(777, 166, 166, device)
+        im.img.fill_(1.0)
+        im.fill_x(xs.to(device))
+        assert im.exp == e, (scale, im.exp)
+        got = _planes_np(im)
+        hi, lo = split_h2(xs.numpy(), e)
+        assert np.array_equal(got[0][:, 168:334], hi)
+        assert np.array_equal(got[1][:, 168:334], lo)
+        assert not got[0][:, 334:].any() and not got[1][:, 334:].any()
+        # (hi + 2^-11 lo) · 2^-e reproduces v to 2^-22 relative, or 2^-36 of the image's top
+        rec = (got[0][:, 168:334].view(np.float16).astype(np.float64)
+               + got[1][:, 168:334].view(np.float16).astype(np.float64) / 2048.0) * 2.0 ** -e
+        xd = xs.double().numpy()
+        assert np.all(np.abs(rec - xd) <= 2.0 ** -22 * np.abs(xd) + 2.0 ** -36 * 2.0 ** -e)
 
 
 @pytest.mark.parametrize("n,e", [(5000, 6000), (203_769, 234_355)])
@@ -77,11 +84,13 @@ def test_mean_h2_equals_split_of_k1(device, n, e):
     agg = aggregate(plan, x, _lib.AGG_MEAN, nodew=plan.deg).cpu().numpy()
     im = HalfPairImage(x.size(0), x.size(1), x.size(1), device)
     im.img.fill_(1.0)
-    assert im.fill_mean(plan, x) == 1
-    got = _planes_np(im)
-    for p, want in enumerate(split_h2(agg)):
-        assert np.array_equal(got[p][:, :166], want), p
-        assert not got[p][:, 166:168].any()
+    for gen, ex in enumerate((0, 9, -3), start=1):  # K1 stores mean · 2^exp (the image's pre-scale)
+        im.exp = ex
+        assert im.fill_mean(plan, x) == gen
+        got = _planes_np(im)
+        for p, want in enumerate(split_h2(agg, ex)):
+            assert np.array_equal(got[p][:, :166], want), (p, ex)
+            assert not got[p][:, 166:168].any()
 
 
 def _operands(M, F, n, seed, wscale=0.08):
@@ -98,9 +107,9 @@ def _image(agg, x, device):
     from elliptic_gnn_project_amd.planes import HalfPairImage
 
     im = HalfPairImage(agg.size(0), agg.size(1), x.size(1), device)
-    im.fill_x(x.to(device))
+    im.fill_x(x.to(device))  # sets im.exp from x; agg must stay within 2x of max|x| (as a mean does)
     _lib.call("gnn_split_h2_f32", agg.to(device).data_ptr(), agg.size(1), im.n, im.k1, im.ptr, im.ld, im.ps, 0,
-              im.col2, _lib.stream_handle(device))
+              im.col2, im.exp, _lib.stream_handle(device))
     return im
 
 
@@ -372,20 +381,112 @@ def test_fused_sage_keep_bits_equal_hash(device):
         assert torch.equal(g1[k], g2[k]), k
 
 
-def test_large_input_keeps_split_bf16(device):
-    """|x| >= 2^14 does not fit a half-pair image: the layer takes the split-bf16 image."""
+def test_nonfinite_input_keeps_split_bf16(device):
+    """A non-finite x has no half-pair pre-scale (h2_exp None): the layer takes the split-bf16
+    image.  Any finite magnitude takes the half-pair image (the scaled-input tests below)."""
     from elliptic_gnn_project_amd.gnn import SAGENet
+    from elliptic_gnn_project_amd.planes import h2_exp, register_input
 
     data, plan, x = _plan_and_x(3000, 4000, 6, device)
     x = x.clone()
-    x[0, 0] = 2.0 ** 15
-    from elliptic_gnn_project_amd.planes import register_input
+    x[0, 0] = float("inf")
     register_input(x)
+    assert h2_exp(x) is None
     torch.manual_seed(4)
     model = SAGENet(x.size(1), 128, layers=2, dropout=0.0).to(device).train()
-    model(x, data.edge_index.to(device)).sum().backward()
+    with torch.no_grad():
+        model(x, data.edge_index.to(device))
     assert getattr(x, "_gnnmp_split_image_h2", None) is None
     assert getattr(x, "_gnnmp_split_image", None) is not None
+
+
+SCALES = [1e-7, 1e-5, 1e-3, 3e4]
+
+
+@pytest.mark.parametrize("scale", SCALES)
+def test_h2_scaled_inputs_nt_tn_vs_f64(device, scale):
+    """The headline NT and TN on a half-pair image of inputs of any magnitude: [agg | x] scaled by
+    1e-7 .. 3e4 (ABI 18 kept no pre-scale: 9e-5 relL2 at 1e-7, split-bf16 above 2^14) within relL2
+    1e-6 of float64 — the image's power-of-two pre-scale keeps every value's f16 planes normal."""
+    from elliptic_gnn_project_amd.fused import gemm_nt, gemm_tn
+
+    M, F, n = 20001, 166, 128
+    agg, x, w1, w2 = _operands(M, F, n, 17)
+    agg, x = agg * scale, x * scale
+    im = _image(agg, x, device)
+    A = torch.cat([agg, x], 1).double()
+    ref = A @ torch.cat([w1, w2], 1).double().t()
+    c = gemm_nt(None, None, n, planes=im, w1=w1.to(device), w2=w2.to(device))
+    assert rel_l2(c, ref) < 1e-6, rel_l2(c, ref)
+    g_ = torch.Generator().manual_seed(3)
+    h = torch.relu(torch.randn(M, n, generator=g_))
+    dz = torch.randn(M, 4, generator=g_) * 1e-3
+    proj = torch.randn(4, n, generator=g_)
+    kw = dict(dz=dz.to(device), proj=proj.to(device), h=h.to(device), hscale=2.0)
+    assert gemm_tn(n, None, None, planes=im, check_planes=True, **kw)
+    dW, db, dW2, dzs = gemm_tn(n, None, None, planes=im, **kw)
+    Gd = torch.where(h > 0, (dz.double() @ proj.double()) * 2.0, torch.zeros(M, n, dtype=torch.float64))
+    assert rel_l2(torch.cat([dW[0], dW[1]], 1), Gd.t() @ A) < 1e-6
+    assert rel_l2(db, Gd.sum(0)) < 1e-6
+
+
+def test_h2_power_of_two_scaling_is_exact(device):
+    """x · 2^-24 and x give bitwise the same GEMM results up to the factor: the pre-scale is an
+    exact power of two on both sides (image split and epilogue), so no input magnitude changes
+    the rounding."""
+    from elliptic_gnn_project_amd.fused import gemm_nt, gemm_tn
+
+    M, F, n = 5000, 166, 128
+    agg, x, w1, w2 = _operands(M, F, n, 23)
+    g_ = torch.Generator().manual_seed(4)
+    h = torch.relu(torch.randn(M, n, generator=g_))
+    dz = torch.randn(M, 4, generator=g_) * 1e-2
+    proj = torch.randn(4, n, generator=g_)
+    kw = dict(dz=dz.to(device), proj=proj.to(device), h=h.to(device), hscale=2.0)
+    out = []
+    for s in (1.0, 2.0 ** -24):
+        im = _image(agg * s, x * s, device)
+        c = gemm_nt(None, None, n, planes=im, w1=w1.to(device), w2=w2.to(device))
+        dW, _, _, _ = gemm_tn(n, None, None, planes=im, **kw)
+        out.append((c / s, torch.cat([dW[0], dW[1]], 1) / s))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("arch", ["sage", "gcn"])
+@pytest.mark.parametrize("scale", [1e-7, 1e-3, 3e4])
+def test_fused_step_scaled_input_vs_f64(device, arch, scale):
+    """The registered-input train step (SAGE: K1 into the half-pair [agg | x] image, the NT and TN
+    over it; GCN: layer 1's NT on x's half-pair image) with the node features scaled by 1e-7 ..
+    3e4: logits and every parameter gradient within relL2 1e-5 of the float64 oracle."""
+    from oracle import pyg_ref
+    from elliptic_gnn_project_amd.planes import register_input
+    from elliptic_gnn_project_amd.train_gnn import build_model
+
+    data, plan, _ = _plan_and_x(5000, 6000, 5, device)
+    xs = data.x * scale
+    x = register_input(xs.to(device))
+    ei = data.edge_index if arch == "sage" else data.edge_index
+    torch.manual_seed(6)
+    model = build_model(arch, x.size(1), dict(hidden_dim=128 if arch == "sage" else 64, layers=2,
+                                              dropout=0.0)).to(device).train()
+    params = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    logits = model(x, ei.to(device))
+    img = "_gnnmp_split_image_h2" if arch == "sage" else "_gnnmp_split_image_x_h2"
+    assert getattr(x, img, None) is not None  # the half-pair path ran
+    tm = data.train_mask
+    cw = pyg_ref.class_weight(data.y[tm])
+    loss = pyg_ref.ce_loss(logits[tm.to(device)], data.y[tm].to(device), cw.to(device))
+    loss.backward()
+    p64 = {k: v.double() if v.is_floating_point() else v for k, v in params.items()}
+    ref = pyg_ref.model_forward(arch, p64, xs.double(), ei, layers=2)
+    assert rel_l2(logits, ref) < 1e-5
+    _, grads = pyg_ref.train_step_grads(arch, p64, xs.double(), ei, data.y, tm, cw.double(), layers=2)
+    for k, v in model.named_parameters():
+        # at 1e-7 every node's logits are the bias: the class-weighted dlogits cancel in the output
+        # bias gradient (true value ~1e-8, fp32 noise ~1e-8), so biases are held to 1e-7 absolute
+        e = rel_l2(v.grad, grads[k], floor=1e-2 if k.endswith("bias") else 1e-30)
+        assert e < 1e-5, (k, e)
 
 
 @pytest.mark.parametrize("use_ptr", [False, True])

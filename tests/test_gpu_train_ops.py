@@ -163,3 +163,74 @@ def test_unit_gradient_paths_match_plain_backward(device):
     logits.grad = None
     masked_cross_entropy(logits, yy, mm, w, denom=float(mm.sum())).backward()
     assert torch.equal(g1, logits.grad)
+
+
+def _sized_params(device, sizes, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(n, generator=g).to(device).requires_grad_(True) for n in sizes]
+
+
+def _boundary_tables():
+    """Parameter tables whose tensor starts fall exactly on ClipAdam's block-slice boundaries
+    (per = ceil(total / 64) elements per block, train_ops.hip grad_sq_kernel / clip_adam_kernel),
+    with slices ending mid-pass (per not a multiple of the 4 x 256 elements a pass covers) and
+    zero-size tensors between them — the shapes of the round-4 fault (gpurun_out/r19a: adam_locate
+    walked a past-the-slice lane back to a negative in-tensor offset when a tensor began a slice)."""
+    out = []
+    for per in (1000, 1537, 1024, 3):
+        k = [1, 2, 5, 7, 3, 9, 1, 4, 6, 2, 8, 11, 5]  # 64 slices in 13 tensors
+        assert sum(k) == 64
+        sizes = [per * m for m in k]
+        sizes.insert(3, 0)   # zero-size tensors: one inside, one at the end
+        sizes.append(0)
+        out.append(sizes)
+    out.append([1000 * 64 - 1, 1, 0, 999])  # total not a multiple of 64: a start one before a boundary
+    out.append([3, 0, 5, 1])                # fewer elements than blocks: most slices empty
+    return out
+
+
+@pytest.mark.parametrize("sizes", _boundary_tables(), ids=lambda s: f"n{len(s)}_t{sum(s)}")
+@pytest.mark.parametrize("captured", [False, True])
+def test_clip_adam_slice_boundaries(device, sizes, captured):
+    """ClipAdam over tensors starting on block-slice boundaries, eager and replayed from a captured
+    HIP graph, against clip_grad_norm_ + torch.optim.Adam (src/train_gnn.py:203-206)."""
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+
+    pa, pb = _sized_params(device, sizes, 3), _sized_params(device, sizes, 3)
+    oa = torch.optim.Adam(pa, lr=0.01, weight_decay=1e-4)
+    ob = ClipAdam(pb, lr=0.01, weight_decay=1e-4, max_norm=1.0)
+    g = torch.Generator().manual_seed(4)
+    steps = [[torch.randn(n, generator=g).to(device) * 0.05 for n in sizes] for _ in range(4)]
+    for q, gr in zip(pb, steps[0]):
+        q.grad = gr.clone()
+    graph = None
+    if captured:  # warm-up (allocates the state), then capture one step and replay the rest
+        ob.step()
+        for p, gr in zip(pa, steps[0]):
+            p.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(pa, 1.0)
+        oa.step()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s), torch.cuda.graph(graph):
+            ob.step()
+        torch.cuda.current_stream().wait_stream(s)
+        todo = steps[1:]
+    else:
+        todo = steps
+    for gr_list in todo:
+        for p, q, gr in zip(pa, pb, gr_list):
+            p.grad = gr.clone()
+            q.grad.copy_(gr)
+        norm = torch.nn.utils.clip_grad_norm_(pa, 1.0)
+        oa.step()
+        if graph is not None:
+            graph.replay()
+        else:
+            ob.step()
+        torch.testing.assert_close(ob.last_norm[0], norm, rtol=1e-5, atol=0)
+        for p, q in zip(pa, pb):
+            torch.testing.assert_close(q.grad, p.grad, rtol=1e-6, atol=1e-9)
+            torch.testing.assert_close(q, p, rtol=1e-6, atol=1e-7)
+    torch.cuda.synchronize()

@@ -122,13 +122,20 @@ def test_k1_prep_b_needs_the_half_pair_nt(lib):
     p = _lib.GnnGemmNTParams(N, 128, None, 0, 166, None, 0, 166, None, 0, fake, fake, 166, 166, fake, 128)
     p.math = _lib.MATH_SPLIT_BF16
     p.a_planes, p.planes_ld, p.planes_stride, p.planes_col2 = fake, ld, N * ld, 168
-    args = (ctypes.byref(g), fake, fake, F, F, fake, ld, N * ld, 168, None, 0, 0.0, 0, None)
+    args = (ctypes.byref(g), fake, fake, F, F, fake, ld, N * ld, 168, 3, None, 0, 0.0, 0, None)
     p.planes_format = _lib.PLANES_SPLIT_BF16  # not the half-pair NT
+    p.planes_exp = 3
     assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 5
     p.planes_format = _lib.PLANES_HALF_PAIR  # no workspace
     assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 5
+    p.planes_exp = 4  # the NT would undo another pre-scale than K1 applies
+    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 1
+    assert b"planes_exp" in lib.gnn_last_error()
+    p.planes_exp = 3
     p.a_planes = fake + 4096  # another image
     assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 1
+    bad = args[:9] + (101,) + args[10:]  # the pre-scale exponent's range
+    assert lib.gnn_sage_mean_fwd_h2(*bad, None, None) == 1
 
 
 STRUCTS = {
@@ -145,7 +152,7 @@ STRUCTS = {
                                                "workspace_bytes", "a_dtype", "c_dtype", "mask", "ldmask",
                                                "mask_scale", "a_planes", "planes_ld", "planes_stride",
                                                "planes_col2", "planes_format", "keep_mask",
-                                               "b_ready"]),
+                                               "b_ready", "planes_exp"]),
     "gnn_adam_tensor": ("GnnAdamTensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel"]),
     "gnn_adam_group": ("GnnAdamGroup", ["num_tensors", "lr", "beta1", "beta2", "eps", "weight_decay", "max_norm",
                                         "tensors", "skip_nonfinite", "bump_counter", "loss_partial", "loss_nblk",
@@ -153,7 +160,8 @@ STRUCTS = {
     "gnn_gemm_tn_params": ("GnnGemmTNParams", ["M", "Nr", "g", "ldg", "dz", "lddz", "proj", "nproj", "h", "ldh",
                                                "hscale", "gout", "ldgout", "a1", "lda1", "k1", "a2", "lda2", "k2",
                                                "math", "a_dtype", "h_dtype", "a_planes", "planes_ld",
-                                               "planes_stride", "planes_col2", "planes_format", "g_dtype"]),
+                                               "planes_stride", "planes_col2", "planes_format", "g_dtype",
+                                               "planes_exp"]),
 }
 
 
