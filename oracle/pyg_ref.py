@@ -206,8 +206,13 @@ def model_forward(arch: str, p: Dict[str, Tensor], x: Tensor, edge_index: Tensor
                   layers: int, dropout: float = 0.0, training: bool = False, heads: int = 4,
                   t_idx: Optional[Tensor] = None, time_embed_dim: int = 0, time_embed_type: str = "none",
                   max_timestep: int = 49, use_bn: bool = True, dropout_masks=None,
-                  bn_state: Optional[Dict[str, Tensor]] = None) -> Tensor:
-    """Forward of GCNNet / SAGENet / GATNet / SAGEResBNNet with PyG-keyed parameters ``p``."""
+                  bn_state: Optional[Dict[str, Tensor]] = None, relu_force=None, trace=None) -> Tensor:
+    """Forward of GCNNet / SAGENet / GATNet / SAGEResBNNet with PyG-keyed parameters ``p``.
+
+    Test hooks (SAGE-ResBN): ``trace`` (a list) receives each hidden layer's pre-ReLU BatchNorm
+    output; ``relu_force`` ({layer: (flat indices, bool keep)}) fixes the ReLU decision of those
+    elements — ties (|BN(z)| at the fp32 rounding of z) that an fp32 device may resolve either way,
+    so a parity test can check the device against the oracle for the tie resolution it took."""
     masks = list(dropout_masks) if dropout_masks is not None else [None] * layers
     h = x
     if arch == "sage":
@@ -250,7 +255,15 @@ def model_forward(arch: str, p: Dict[str, Tensor], x: Tensor, edge_index: Tensor
                 rv = bn_state.get(f"bns.{i}.running_var") if bn_state else None
                 z = F.batch_norm(z, rm, rv, p[f"bns.{i}.weight"], p[f"bns.{i}.bias"], training or rm is None,
                                  0.1, 1e-5)
-            z = _dropout(F.relu(z), dropout, training, masks[i])
+            if trace is not None:
+                trace.append(z.detach())
+            if relu_force is not None and i in relu_force:
+                idx, keep = relu_force[i]
+                on = (z > 0).flatten().clone()
+                on[idx] = keep
+                z = _dropout(z * on.view_as(z).to(z.dtype), dropout, training, masks[i])
+            else:
+                z = _dropout(F.relu(z), dropout, training, masks[i])
             rp = p.get(f"res_projs.{i}.weight")
             h = z + (F.linear(h_in, rp) if rp is not None else h_in)
         i = layers - 1

@@ -18,6 +18,7 @@ their inputs — which test_gpu_train_main.py covers; here the step runs fp32 di
 import pytest
 import torch
 
+import relu_ties
 from oracle import pyg_ref
 from oracle.dropout_hash import keep_mask
 
@@ -64,8 +65,12 @@ def _step_vs_oracle(device, cfg, data, registered):
     if registered:
         register_input(xd)
     t_idx = data.timestep.to(device) if te else None
+    bn = cfg["arch"] == "sage_resbn"
+    zs, hooks = relu_ties.capture_hidden_z(model) if bn else ([], [])
     torch.manual_seed(11)
     logits = model(xd, data.edge_index.to(device), t_idx)
+    for hk in hooks:
+        hk.remove()
     torch.manual_seed(11)
     seeds = torch.randint(0, 2 ** 62, (L,), dtype=torch.int64).tolist()
     masks = [torch.from_numpy(keep_mask(seeds[l], N, H, p)) for l in range(L - 1)]
@@ -75,20 +80,23 @@ def _step_vs_oracle(device, cfg, data, registered):
     loss.backward()
     p64 = {k: v.double() if v.is_floating_point() else v for k, v in params.items()}
     kw = dict(layers=L, dropout=p, training=True, dropout_masks=masks)
-    bn = cfg["arch"] == "sage_resbn"
     if te:
         kw.update(t_idx=data.timestep, time_embed_dim=te, time_embed_type=cfg["time_embed_type"],
                   max_timestep=cfg["max_timestep"])
     bn_state = {k: v.clone() for k, v in p64.items() if "running" in k} if bn else None
     x64 = data.x.double()
-    ref = pyg_ref.model_forward(cfg["arch"], p64, x64, data.edge_index, bn_state=bn_state, **kw)
+    trace = []
+    ref = pyg_ref.model_forward(cfg["arch"], p64, x64, data.edge_index, bn_state=bn_state, trace=trace, **kw)
     torch.testing.assert_close(logits.detach().cpu().double(), ref, rtol=1e-5, atol=1e-5)
+    force = None
     if bn:
         for k in bn_state:  # the running statistics K12 updated, vs F.batch_norm's in-place update
             torch.testing.assert_close(model.state_dict()[k].cpu().double(), bn_state[k], rtol=1e-5, atol=1e-6)
+        force = relu_ties.relu_force(zs, p64, trace)  # the device's resolution of ReLU ties (relu_ties.py)
+        assert sum(int(v[0].numel()) for v in force.values()) <= 8, force
     ref_loss, grads = pyg_ref.train_step_grads(
         cfg["arch"], p64, x64, data.edge_index, data.y, tm, cw.double(),
-        bn_state={k: v.clone() for k, v in p64.items() if "running" in k} if bn else None, **kw)
+        bn_state={k: v.clone() for k, v in p64.items() if "running" in k} if bn else None, relu_force=force, **kw)
     assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
     if te and cfg["time_embed_type"] == "learned":
         assert "time_emb.weight" in grads  # the learned embedding is trained through the step

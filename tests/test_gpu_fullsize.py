@@ -11,6 +11,7 @@ result is held to (fp32 CPU and GPU differ from it by their own rounding).
 import pytest
 import torch
 
+import relu_ties
 from oracle import pyg_ref
 from oracle.dropout_hash import keep_mask
 
@@ -132,8 +133,11 @@ def _resbn_step_vs_oracle(device, data, registered=False):
     xd = data.x.to(device)
     if registered:
         register_input(xd)
+    zs, hooks = relu_ties.capture_hidden_z(model)
     torch.manual_seed(11)
     logits = model(xd, data.edge_index.to(device), data.timestep.to(device))
+    for hk in hooks:
+        hk.remove()
     if registered:
         h0 = xd._gnnmp_time_inject[1]  # the cached [x | sin(t)], registered: its image served layer 1
         assert any(getattr(h0, a, None) is not None for a in ("_gnnmp_split_image_x_h2", "_gnnmp_split_image_x"))
@@ -149,13 +153,17 @@ def _resbn_step_vs_oracle(device, data, registered=False):
     kw = dict(layers=L, dropout=p, training=True, dropout_masks=masks, t_idx=data.timestep, time_embed_dim=2,
               time_embed_type="sin", max_timestep=49)
     x64 = data.x.double()
-    ref = pyg_ref.model_forward("sage_resbn", p64, x64, data.edge_index, bn_state=bn_state, **kw)
+    trace = []
+    ref = pyg_ref.model_forward("sage_resbn", p64, x64, data.edge_index, bn_state=bn_state, trace=trace, **kw)
     torch.testing.assert_close(logits.detach().cpu().double(), ref, rtol=1e-5, atol=1e-5)
     for k in bn_state:  # F.batch_norm updated the oracle's copies in place
         torch.testing.assert_close(model.state_dict()[k].cpu().double(), bn_state[k], rtol=1e-5, atol=1e-6)
+    # the device's own resolution of the (few) ReLU ties at fp32 rounding level (tests/relu_ties.py)
+    force = relu_ties.relu_force(zs, p64, trace)
+    assert sum(int(v[0].numel()) for v in force.values()) <= 8, force
     ref_loss, grads = pyg_ref.train_step_grads(
         "sage_resbn", p64, x64, data.edge_index, data.y, tm, cw.double(),
-        bn_state={k: v.clone() for k, v in p64.items() if "running" in k}, **kw)
+        bn_state={k: v.clone() for k, v in p64.items() if "running" in k}, relu_force=force, **kw)
     assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
     for k, v in model.named_parameters():
         # a hidden conv's bias feeds BatchNorm: its true gradient is zero, so hold it to 1e-7 absolute
