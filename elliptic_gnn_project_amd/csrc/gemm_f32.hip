@@ -1056,7 +1056,7 @@ extern "C" int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p) {
   if (!p || !p->a_planes || p->math == GNN_MATH_F32 || p->M < 1 || p->Nr < 1 || p->Nr > 128) return 0;
   TNArgs a{};
   a.M = p->M; a.Nr = (int32_t)p->Nr; a.g = p->g; a.ldg = p->ldg; a.dz = p->dz; a.lddz = p->lddz;
-  a.h = p->h; a.ldh = p->ldh; a.k1 = (int32_t)p->k1; a.k2 = (int32_t)p->k2;
+  a.h = p->h; a.ldh = p->ldh; a.gout = p->gout; a.ldgout = p->ldgout; a.k1 = (int32_t)p->k1; a.k2 = (int32_t)p->k2;
   a.a_bf16 = p->a_dtype == GNN_DTYPE_BF16; a.h_bf16 = p->h_dtype == GNN_DTYPE_BF16;
   a.g_bf16 = p->g_dtype == GNN_DTYPE_BF16;
   a.ap = static_cast<const uint16_t*>(p->a_planes);

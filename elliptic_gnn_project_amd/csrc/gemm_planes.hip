@@ -455,7 +455,11 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_planes_kernel(TNArgs a) {
 // NW = 8 (r19): two waves per SIMD — waves w and w + 4 share dW rows 32(w & 3) .. +32 and split the
 // k-tiles (the first (KT + 1) / 2 and the rest), so each holds half the accumulators and the block
 // twice the staging threads (twice the chunk loads in flight per CU).
-template <int KT, bool GOUT, int LAB = 0, int NW = 4>
+// GF (round 5): the plain g form — G = g read as is ([M, Nr] f32: the input layer's weight
+// gradient of GCN / GAT layer 1 and of SAGE-ResBN layer 0's conv and residual projection, dW =
+// Gᵀ·x over x's half-pair image), block scale from max |g| over the block's rows (one pass over
+// them before the chunk loop, behind chunk 0's loads), side sums: db = Σ G only.
+template <int KT, bool GOUT, int LAB = 0, int NW = 4, bool GF = false>
 __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int T = 64 * NW;
@@ -472,6 +476,9 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   // its LDS put.  LAB 16: two sets — measured slower (lab 104.2 vs 100.6 us, r18h: the second
   // set's 24 VGPRs cost more in the chunk loop than the extra lead buys)
   constexpr int RING = (LAB & 16) ? 2 : 1;
+  // RGN: register sets of G rows (2: two chunks ahead; measured no faster on the g form, r27: 70.0
+  // vs 66.9 us on the GCN layer-1 shape, so one set)
+  constexpr int RGN = 1;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -510,13 +517,13 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   const int gn = tid & 127, go = tid >> 7;
   const bool gcol = gn < a.Nr;
   const int gnc = gcol ? gn : 0;
-  const float* hb = a.h + gnc;
-  const int hld = (int)a.ldh;
+  const float* hb = GF ? a.g + gnc : a.h + gnc;  // the g form loads G itself where the dz form loads h
+  const int hld = GF ? (int)a.ldg : (int)a.ldh;
   const int zr = (tid & 63) / MAXPROJ, zq = (tid & 63) % MAXPROJ;
   const int zqc = min(zq, a.nproj - 1);
   float pcol[MAXPROJ];
 #pragma unroll
-  for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
+  for (int q = 0; q < MAXPROJ; ++q) pcol[q] = (!GF && q < a.nproj && gcol) ? a.proj[q * a.Nr + gn] : 0.0f;
 
   // ---- the block's G scale s_b: |G| <= hscale · max_m Σ_q |dz[m][q]| · max |P|.  The dz rows are
   // read 4 per thread per pass with clamped indices and no branch around a load, so a pass is one
@@ -525,7 +532,32 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   auto scan_scale = [&]() __attribute__((always_inline)) {  // run in the prologue, behind chunk 0's loads
     float zm = 0.f;
     const int nq = a.nproj;
-    for (int64_t r0 = mbeg + tid; r0 < mend; r0 += 4 * T) {
+    if constexpr (GF) {  // max |g| over the block's rows: float4 pieces, 16 in flight per thread
+      constexpr int SU = 16;  // (the block's ~800 rows in two round trips: the scan is latency-bound)
+      const int n4 = (a.Nr + 3) >> 2;
+      const int64_t npc = (mend - mbeg) * n4;
+      for (int64_t q0 = tid; q0 < npc; q0 += SU * T) {
+        float4 v[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int64_t q = min(q0 + (int64_t)T * u, npc - 1);
+          const int64_t r = mbeg + q / n4;
+          const int c4 = (int)(q - (q / n4) * n4) * 4;
+          v[u] = *reinterpret_cast<const float4*>(a.g + r * a.ldg + c4);
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int64_t q = q0 + (int64_t)T * u;
+          const int c4 = (int)(min(q, npc - 1) % n4) * 4;  // columns past Nr (the last piece) masked
+          float m = fabsf(v[u].x);
+          m = fmaxf(m, c4 + 1 < a.Nr ? fabsf(v[u].y) : 0.f);
+          m = fmaxf(m, c4 + 2 < a.Nr ? fabsf(v[u].z) : 0.f);
+          m = fmaxf(m, c4 + 3 < a.Nr ? fabsf(v[u].w) : 0.f);
+          zm = fmaxf(zm, q < npc ? m : 0.f);
+        }
+      }
+    }
+    for (int64_t r0 = mbeg + tid; !GF && r0 < mend; r0 += 4 * T) {
       float v[4][MAXPROJ];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -561,7 +593,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
       zm = fmaxf(zm, redm[w]);
       pm = fmaxf(pm, redm[NW + w]);
     }
-    const float bound = zm * pm * a.hscale;
+    const float bound = GF ? zm : zm * pm * a.hscale;
     int E = 0;
     if (bound > 0.f && isfinite(bound)) frexpf(bound, &E);  // bound < 2^E
     gsc = ldexpf(1.0f, 4 - E);                               // |G · gsc| < 16
@@ -572,21 +604,24 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   auto ldbase = [&](int c) __attribute__((always_inline)) { return min((int)mbeg + c * PT_ROWS, Mi - PT_ROWS); };
   const int clast = max(nch - 1, 0);
   u32x4 ra[RING][NPA];
-  float rg[RP];
+  float rg[RGN][RP];
   float rz = 0.f;
   auto load_a = [&](int s, int j, int c) __attribute__((always_inline)) {
     ra[s][j] = __builtin_amdgcn_raw_buffer_load_b128(arsrc, (int)goff[j], ldbase(c) * ld * 2, 0);
   };
-  auto load_g = [&](int c) __attribute__((always_inline)) {
+  auto load_g = [&](int sg, int c) __attribute__((always_inline)) {
     uint32_t o = (uint32_t)((ldbase(c) + RP * go) * hld);
 #pragma unroll
     for (int i = 0; i < RP; ++i) {
-      rg[i] = hb[o];
+      rg[sg][i] = hb[o];
       o += (uint32_t)hld;
     }
   };
-  auto load_z = [&](int c) __attribute__((always_inline)) { rz = a.dz[(uint32_t)((ldbase(c) + zr) * (int)a.lddz + zqc)]; };
+  auto load_z = [&](int c) __attribute__((always_inline)) {
+    if constexpr (!GF) rz = a.dz[(uint32_t)((ldbase(c) + zr) * (int)a.lddz + zqc)];
+  };
   auto put_z = [&](int k) __attribute__((always_inline)) {
+    if constexpr (GF) return;
     const int mb = ldbase(k);
     const bool ok = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + k * PT_ROWS - mb && zr < (int)mend - mb;
     if (T == 256 || tid < 256) dzL[k & 1][tid] = ok ? rz : 0.0f;
@@ -599,6 +634,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   float4 zv[RP];
   float zsv[RP];
   auto z_read = [&](int c, int i0, int n) __attribute__((always_inline)) {
+    if constexpr (GF) return;
     const int buf = c & 1;
 #pragma unroll
     for (int i = i0; i < i0 + n; ++i) {
@@ -610,22 +646,32 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   auto put_a = [&](int s, int j, int c) __attribute__((always_inline)) {
     *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(At[c & 1]) + loff[j]) = ra[s][j];
   };
-  auto g_row = [&](int i, int c, int half) __attribute__((always_inline)) {
+  auto g_row = [&](int i, int c, int half, int sg) __attribute__((always_inline)) {
+    if constexpr (GF) {  // G itself (rows past the block's end: zero)
+      if (half == 0) return;
+      const int mb = ldbase(c);
+      const int r = RP * go + i;
+      const bool ok = r >= (int)mbeg + c * PT_ROWS - mb && r < (int)mend - mb && gcol;
+      const float g = ok ? rg[sg][i] : 0.0f;
+      db += g;
+      e[i] = g * gsc;  // exact (a power of two)
+      return;
+    }
     if (half == 0) {
       const float4 z = zv[i];
       float g = z.x * pcol[0];
       g = fmaf(z.y, pcol[1], g);
       g = fmaf(z.z, pcol[2], g);
       e[i] = fmaf(z.w, pcol[3], g);
-      dw2[0] = fmaf(z.x, rg[i], dw2[0]);
-      dw2[1] = fmaf(z.y, rg[i], dw2[1]);
-      dw2[2] = fmaf(z.z, rg[i], dw2[2]);
-      dw2[3] = fmaf(z.w, rg[i], dw2[3]);
+      dw2[0] = fmaf(z.x, rg[sg][i], dw2[0]);
+      dw2[1] = fmaf(z.y, rg[sg][i], dw2[1]);
+      dw2[2] = fmaf(z.z, rg[sg][i], dw2[2]);
+      dw2[3] = fmaf(z.w, rg[sg][i], dw2[3]);
       return;
     }
     float g = e[i];
     dzs += gn < MAXPROJ ? zsv[i] : 0.0f;
-    g = rg[i] > 0.0f ? g * a.hscale : 0.0f;
+    g = rg[sg][i] > 0.0f ? g * a.hscale : 0.0f;
     db += g;
     if constexpr (GOUT) {
       const int mb = ldbase(c);
@@ -654,19 +700,20 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   auto unit = [&](int k, int c, int par) __attribute__((always_inline)) {
     constexpr int Z0 = 2 * NPA, G0 = Z0 + RP / 2, S0 = G0 + 2 * RP, P0 = S0 + RP / 2;
     const int sa = RING == 1 ? 0 : (par ^ 1);
+    const int sg = RGN == 1 ? 0 : (par ^ 1);  // chunk c + 1's G rows
     if (k < Z0) {
       if (k & 1) load_a(sa, k >> 1, min(c + 1 + RING, clast));
       else put_a(sa, k >> 1, c + 1);
     } else if (k < G0) {
       z_read(c + 1, 2 * (k - Z0), 2);
     } else if (k < S0) {
-      g_row((k - G0) >> 1, c + 1, (k - G0) & 1);
+      g_row((k - G0) >> 1, c + 1, (k - G0) & 1, sg);
     } else if (k < P0) {
       split_pair(k - S0);
     } else if (k == P0) {
       g_put(c + 1);
     } else if (k == P0 + 1) {
-      load_g(min(c + 2, clast));
+      load_g(sg, min(c + 1 + RGN, clast));
     } else if (k == P0 + 2) {
       put_z(c + 2);
       load_z(min(c + 3, clast));
@@ -723,7 +770,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
 #undef TH_FENCE
 
   if (nch > 0) {
-    rz = a.dz[(uint32_t)((ldbase(0) + zr) * (int)a.lddz + zqc)];
+    if constexpr (!GF) rz = a.dz[(uint32_t)((ldbase(0) + zr) * (int)a.lddz + zqc)];
     put_z(0);
     load_z(min(1, clast));
     put_z(1);
@@ -734,22 +781,23 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
 #pragma unroll
       for (int j = 0; j < NPA; ++j) load_a(1, j, min(1, clast));
     }
-    load_g(0);
+    load_g(0, 0);
+    if constexpr (RGN == 2) load_g(1, min(1, clast));
     scan_scale();     // (its barrier also publishes dzL)
 #pragma unroll
     for (int j = 0; j < NPA; ++j) put_a(0, j, 0);
     z_read(0, 0, RP);
 #pragma unroll
     for (int i = 0; i < RP; ++i) {
-      g_row(i, 0, 0);
-      g_row(i, 0, 1);
+      g_row(i, 0, 0, 0);
+      g_row(i, 0, 1, 0);
     }
 #pragma unroll
     for (int j = 0; j < RP / 2; ++j) split_pair(j);
     g_put(0);
 #pragma unroll
     for (int j = 0; j < NPA; ++j) load_a(0, j, min(RING, clast));  // set 0: chunk RING (1 or 2)
-    load_g(min(1, clast));
+    load_g(0, min(RGN, clast));  // set 0: chunk RGN (1 or 2)
     __syncthreads();
     for (int c = 0; c < nch; c += 2) {  // unrolled by 2: the ring's set indices are static
       compute(c, std::integral_constant<int, 0>{});
@@ -1139,19 +1187,31 @@ void launch_tn_img16(const TNArgs& a, int nblk, hipStream_t st) {
   else launch_tn_img16_kt<11>(a, nblk, st);
 }
 
-// the half-pair form: dz form with the h mask (the SAGE hidden layer), f32 h, 336-wide image rows
+// the half-pair forms: the dz form with the h mask (the SAGE hidden layer), f32 h, 336-wide image
+// rows; the plain g form (no dz / h / gout: G read as is, 16-byte aligned rows) over 336- or
+// 176-wide images (x's x-only image: GCN / GAT layer 1, SAGE-ResBN layer 0)
 bool tn_h2_ok(const TNArgs& a) {
-  if (!a.ap || !a.ap_h2 || a.a_bf16 || a.h_bf16 || a.g_bf16 || !a.dz || !a.proj || !a.h || a.nproj < 1) return false;
-  if (a.ap_ld != 336 || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;
+  if (!a.ap || !a.ap_h2 || a.a_bf16 || a.h_bf16 || a.g_bf16 || (reinterpret_cast<uintptr_t>(a.ap) & 15)) return false;
+  const bool gf = !a.dz && a.g && !a.h && !a.gout;
+  if (gf) {
+    if ((a.ap_ld != 336 && a.ap_ld != 176) || a.ldg % 4 || (reinterpret_cast<uintptr_t>(a.g) & 15)) return false;
+  } else if (!a.dz || !a.proj || !a.h || a.nproj < 1 || a.ap_ld != 336) {
+    return false;
+  }
   if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
   if (a.ap_ps < a.M * (int64_t)a.ap_ld || 2 * a.ap_ps * 2 >= ((int64_t)1 << 31) || a.M < PT_ROWS) return false;
-  const int64_t ldmax = std::max({a.ldh, a.lddz});
+  const int64_t ldmax = gf ? a.ldg : std::max({a.ldh, a.lddz});
   return (a.M + 32) * ldmax < ((int64_t)1 << 31);
 }
 
 // 8 waves (two per SIMD, the k-tiles split between them): lab 102.3 -> 95.2 us on the headline
 // shape (profiles/r19_lab_h2.txt), the staging alone 93.4 — the kernel now runs at its stream
 void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st) {
+  if (!a.dz) {  // the g form
+    if (a.ap_ld == 176) gemm_tn_h2_kernel<6, false, 0, 8, true><<<nblk, 512, 0, st>>>(a);
+    else gemm_tn_h2_kernel<11, false, 0, 8, true><<<nblk, 512, 0, st>>>(a);
+    return;
+  }
   if (a.gout) gemm_tn_h2_kernel<11, true, 0, 8><<<nblk, 512, 0, st>>>(a);
   else gemm_tn_h2_kernel<11, false, 0, 8><<<nblk, 512, 0, st>>>(a);
 }

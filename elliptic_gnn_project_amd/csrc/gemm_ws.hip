@@ -1313,7 +1313,7 @@ bool nt_ws_ok(const NTArgs& a) {
   if (a.M < WS_ROWS || a.M * (int64_t)std::max(a.k1, a.k2) >= ((int64_t)1 << 40)) return false;
   // the block always computes 128 columns: at N <= 64 half its MFMAs are wasted and the tiled
   // x3 kernel wins (r07: GAT/GCN layer 1, K = 166, N = 64: 104 vs 80 us)
-  if (a.Nc <= 64) return false;
+  if (a.Nc <= 64) return false;  // (r22: also slower on SAGE-ResBN's K = 128, N = 64 GEMMs: 1.070 vs 1.053 ms/step)
   const bool drop = a.dropout != 0, relu = a.relu != 0, bias = a.bias != nullptr, proj = a.nproj > 0;
   if ((drop || proj || relu) && !(relu && bias)) return false;
   return true;

@@ -253,8 +253,13 @@ def gemm_nt_input(x: torch.Tensor, n: int, **kw):
 
 
 def gemm_tn_input(nr: int, x: torch.Tensor, g: torch.Tensor):
-    """gemm_tn(nr, x, g=g) for a layer whose A operand is the model input x: on the split-image
-    TN over x's cached planes (planes.x_only_image) when it takes the shape, else the f32 form."""
+    """gemm_tn(nr, x, g=g) for a layer whose A operand is the model input x: on the half-pair TN
+    over x's cached half-pair image (the one the forward NT read: 4 B per element, 3 products)
+    when it takes the shape, else the split-image TN over x's split-bf16 planes, else the f32 form."""
+    if _H2:
+        im = x_only_image(x, HalfPairImage)
+        if im is not None and gemm_tn(nr, None, g=g, planes=im, check_planes=True):
+            return gemm_tn(nr, None, g=g, planes=im)
     im = x_only_image(x)
     if im is not None and gemm_tn(nr, None, g=g, planes=im, check_planes=True):
         return gemm_tn(nr, None, g=g, planes=im)

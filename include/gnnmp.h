@@ -419,7 +419,8 @@ typedef struct {
   const void* a_planes;                  /* optional split image of [A1 | A2], as gnn_gemm_nt_params */
   int64_t planes_ld, planes_stride, planes_col2;
   int32_t planes_format;                 /* gnn_planes_format (HALF_PAIR: the dz form with h, 336-wide
-                                            rows; G scaled per row block by a power of two, 3 products) */
+                                            rows, or the plain g form over 336- / 176-wide rows; G scaled
+                                            per row block by a power of two, 3 products) */
   int32_t g_dtype;                       /* gnn_dtype of g and gout (BF16: the bf16-image TN only; gout
                                             then holds the bf16-rounded G its MFMAs use) */
   int32_t planes_exp;                    /* HALF_PAIR (ABI 19): the image holds A * 2^planes_exp; dW is
@@ -438,8 +439,9 @@ gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* worksp
  *   image rows of 336 (the SAGE layer-1 [agg | x], 166 + 166 padded to 168 each), 64 < N <= 128;
  *   image rows of 176 (one input of <= 176 columns: the GCN / GAT layer-1 x), 1 <= N <= 128;
  *   a half-pair image (planes_format HALF_PAIR) of 336-wide rows, 1 <= N <= 128.
- * TN image rows of 32..336 (multiple of 16), f32 h; half-pair: the dz form with h, 336-wide rows
- * (gnn_gemm_tn_planes_ok).  Both need the planes to span < 2 GiB
+ * TN image rows of 32..336 (multiple of 16), f32 h; half-pair: the dz form with h, 336-wide rows,
+ * or (ABI 19) the plain g form — g given, no dz / h / gout, 16-byte aligned g rows — over 336- or
+ * 176-wide rows (gnn_gemm_tn_planes_ok).  Both need the planes to span < 2 GiB
  * and C / z below 2 GiB. */
 int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p);
 int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p);
