@@ -95,6 +95,10 @@ def parse():
                     help="before the warm-up: hold the GPU busy this long with a device-to-device copy loop (no "
                          "step work) so the timed steps do not run on clocks still ramping up from the idle "
                          "setup phase; 0 disables")
+    ap.add_argument("--rehearse-shard", type=int, default=0, metavar="N",
+                    help="diagnostic (N=1 only): time the largest shard of the N-way timestep partition of "
+                         "the global graph on this one GPU, without collectives — the per-GPU compute of a "
+                         "strong-scaling N-GPU run (the line's value is then that shard's edges/s)")
     ap.add_argument("--step-trace", action="store_true",
                     help="diagnostic: record a HIP event between the timed steps and print each step's GPU "
                          "time (and the host's enqueue time) to stderr")
@@ -414,6 +418,12 @@ def main():
     full, key = make_global_graph(world, args.scale, args.degree, cfg, preset.get("gen"))
     E_global = full.edge_index.size(1)
     data_cpu = gdist.shard_graph(full, world, rank, key=key) if world > 1 else full
+    if args.rehearse_shard > 1 and world == 1:  # diagnostic: one GPU runs the largest shard alone
+        parts = gdist.partition_timesteps(key, full.edge_index, args.rehearse_shard)
+        e_t = torch.bincount(key[full.edge_index[1]], minlength=int(key.max()) + 1)
+        big = max(range(args.rehearse_shard), key=lambda i: int(sum(int(e_t[t]) for t in parts[i])))
+        data_cpu = gdist.shard_graph(full, args.rehearse_shard, big, parts=parts, key=key)
+        E_global = data_cpu.edge_index.size(1)
     if check:
         return report(args, preset, full, E_global, data_cpu, dist, world, rank, dev, lambda: None, False,
                       None, None, launch_check=True)
@@ -610,6 +620,9 @@ def report(args, preset, full, E_global, data, dist, world, rank, dev, step, bf1
         }
         if settled:
             line["settle"] = settled
+        if args.rehearse_shard > 1 and world == 1:
+            line["rehearsal"] = (f"largest shard of a {args.rehearse_shard}-way timestep partition on one GPU, "
+                                 "no collectives (diagnostic, not the metric's workload)")
         if launch_check:
             line["launch_check"] = "CPU rehearsal of the launch: empty step, no device work (not a measurement)"
         print(json.dumps(line), flush=True)
