@@ -99,6 +99,8 @@ def parse():
                     help="diagnostic (N=1 only): time the largest shard of the N-way timestep partition of "
                          "the global graph on this one GPU, without collectives — the per-GPU compute of a "
                          "strong-scaling N-GPU run (the line's value is then that shard's edges/s)")
+    ap.add_argument("--separate-ce", action="store_true",
+                    help="A/B: launch the masked CE on its own instead of in the output layer's mean")
     ap.add_argument("--step-trace", action="store_true",
                     help="diagnostic: record a HIP event between the timed steps and print each step's GPU "
                          "time (and the host's enqueue time) to stderr")
@@ -463,7 +465,11 @@ def main():
     def fwd_bwd():
         model.train()
         opt.zero_grad(set_to_none=bucket is None)
-        logits = model(data.x, data.edge_index, t_idx)
+        if args.aten_step or args.separate_ce:
+            logits = model(data.x, data.edge_index, t_idx)
+        else:  # the fused SAGE output layer computes the step's masked CE in its mean's launch
+            with loss_fn.target(data.y, data.train_mask, denom):
+                logits = model(data.x, data.edge_index, t_idx)
         if args.aten_step:
             loss = loss_fn(logits.index_select(0, tidx), ytr, denom=denom)
         else:  # the same masked weighted CE, one fused kernel (fwd + dlogits)

@@ -116,6 +116,10 @@ struct AggArgs {
   // K1 of the half-pair path may also carry the consuming NT's B-image prep (gnn_sage_mean_fwd_h2
   // prep_b): hp.blocks extra blocks at the front of the grid run ws_prep_h2_body, one per k-step
   H2Prep hp;
+  // gnn_sage_out_mean_ce_f32: the masked weighted CE of the finished rows (gnn_masked_ce_f32's
+  // arithmetic) in the narrow kernel's epilogue: dlogits into ce_dl, per-256-row loss partials
+  const int64_t* ce_y; const uint8_t* ce_mask; const float* ce_w; float ce_inv;
+  float* ce_dl; int64_t ce_ldd; float* ce_part;
 };
 
 __device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
@@ -700,13 +704,21 @@ __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
 // pass, then all their row values (clamped feature index) and weights, then the LDS writes — a
 // per-feature `f < F` branch had compiled to one dependent load + vmcnt(0) per value (r10: 16 us
 // warm, 21 us cold for ~11 MB).
-template <int MODE, int NF, int kNarrowCap = 256, bool COOP = false>  // kNarrowCap: slots staged per pass per wave
+// CE (gnn_sage_out_mean_ce_f32): each finished row's masked weighted cross entropy in the
+// epilogue (masked_ce_kernel's arithmetic, bit for bit: a block's 4 waves x 64 rows are that
+// kernel's 256-row block, its loss partial summed in the same order); waves past the last row
+// then stay for the block's one barrier instead of returning.
+template <int MODE, int NF, int kNarrowCap = 256, bool COOP = false, bool CE = false>  // kNarrowCap: slots staged per pass per wave
 __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   __shared__ float sv[4][kNarrowCap * 4];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + w) * 64;
-  if (r0 >= a.nrows) return;  // wave-uniform; no block barriers below
+  float lg[4] = {0.f, 0.f, 0.f, 0.f};  // CE: the row's logits
+  if constexpr (!CE) {
+    if (r0 >= a.nrows) return;  // wave-uniform; no block barriers below
+  }
+  if (r0 < a.nrows) {  // (CE: the block's barrier follows)
   const int64_t r = r0 + lane;
   const bool rok = r < a.nrows;
   const int32_t pbeg = a.ptr[rok ? r : a.nrows];
@@ -819,8 +831,29 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
           if (a.relu) t[0] = fmaxf(t[0], 0.0f);
           if (a.dropout) agg_dropout<1>(a, agg_seed(a), r, f, t);
           a.y[r * a.ldy + f] = t[0];
+          lg[f] = t[0];
         }
       }
+    }
+  }
+  }  // r0 < nrows
+  if constexpr (CE) {
+    const int64_t r = r0 + lane;
+    const int C = a.F;
+    float l = 0.f;
+    if (r < a.nrows) {  // masked_ce_kernel<C>: loss_r = -w[y]·log_softmax[y], dl = w[y]/n·(softmax - onehot)
+      const int64_t tg = a.ce_y[r];
+      const bool on = a.ce_mask[r] != 0 && tg >= 0 && tg < C;
+      l = masked_ce_row<4>(lg, C, tg, on, on ? a.ce_w[tg] : 0.f, a.ce_inv, a.ce_dl + r * a.ce_ldd);
+    }
+    __shared__ float cesh[4];
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);  // train_ops.hip block_sum, same order
+    if (lane == 0) cesh[w] = l;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int i = 0; i < 4; ++i) t += cesh[i];
+      a.ce_part[blockIdx.x] = t;
     }
   }
 }
@@ -1428,6 +1461,42 @@ extern "C" gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg,
                                            gnn_stream_t stream) {
   return sage_mean_fwd_image<2>(g, deg, x, ldx, F, img, ld, plane_stride, width, stream, __func__, keep_mask,
                                 mask_cols, dropout_p, seed, seed_ptr, prep_b, scale_exp);
+}
+
+extern "C" gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, float inv_denom, float* loss,
+                                           gnn_stream_t stream);
+
+extern "C" gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* deg, const float* z, int64_t ldz,
+                                               int32_t C, const float* bias, float* logits, int64_t ldo,
+                                               const int64_t* y, const uint8_t* mask, const float* class_w,
+                                               float inv_denom, float* dlogits, int64_t ld_d, float* loss,
+                                               void* workspace, size_t workspace_bytes, gnn_stream_t stream) {
+  const char* fn = __func__;
+  if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or deg");
+  if (C < 1 || C > 4 || ldz < 2 * C || ldo < C || ld_d < C) return fail(GNN_ERR_INVALID_ARG, fn, "needs 1 <= C <= 4, ldz >= 2C");
+  const int64_t N = g->num_nodes;
+  if (N > 0 && (!z || !logits || !y || !mask || !class_w || !dlogits)) return fail(GNN_ERR_INVALID_ARG, fn, "null operand");
+  if (!g->rowptr || (g->num_slots > 0 && !g->col)) return fail(GNN_ERR_INVALID_ARG, fn, "plan arrays null");
+  const int nblk = (int)std::max<int64_t>(1, ceil_div(N, 256));
+  if (!workspace || workspace_bytes < (size_t)nblk * sizeof(float)) return fail(GNN_ERR_WORKSPACE, fn, "workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* partial = static_cast<float*>(workspace);
+  if (N == 0) {
+    if (!loss) return hip_check(hipMemsetAsync(partial, 0, sizeof(float), st), fn);
+    return hip_check(hipMemsetAsync(loss, 0, sizeof(float), st), fn);
+  }
+  AggArgs a{};
+  a.ptr = g->rowptr; a.nbr = g->col; a.nodew = deg; a.heads = 1; a.chan = C;
+  a.x = z; a.ldx = ldz; a.y = logits; a.ldy = ldo;
+  a.add = z + C; a.ld_add = ldz; a.bias = bias;
+  a.nrows = N; a.F = C;
+  a.ce_y = y; a.ce_mask = mask; a.ce_w = class_w; a.ce_inv = inv_denom; a.ce_dl = dlogits; a.ce_ldd = ld_d;
+  a.ce_part = partial;
+  if (C <= 2) agg_narrow_lds_kernel<GNN_AGG_MEAN, 2, 256, true, true><<<(unsigned)nblk, 256, 0, st>>>(a);
+  else agg_narrow_lds_kernel<GNN_AGG_MEAN, 4, 256, true, true><<<(unsigned)nblk, 256, 0, st>>>(a);
+  const gnn_status s = hip_check(hipGetLastError(), fn);
+  if (s != GNN_OK || !loss) return s;  // loss NULL: the partials stay in the workspace (ClipAdam / finish)
+  return gnn_masked_ce_finish(partial, nblk, inv_denom, loss, stream);
 }
 
 extern "C" gnn_status gnn_sage_mean_bwd_f32(const gnn_graph* g, const float* deg, const float* dout,

@@ -46,27 +46,9 @@ __global__ __launch_bounds__(kCeThreads) void masked_ce_kernel(int64_t N, int Cr
     const int64_t t = y[row];
     const bool on = mask[row] != 0 && t >= 0 && t < C;
     float v[CM];
-    float mx = -INFINITY;
 #pragma unroll
-    for (int c = 0; c < CM; ++c)
-      if (c < C) {
-        v[c] = x[row * ldx + c];
-        mx = fmaxf(mx, v[c]);
-      }
-    float s = 0.f, xt = 0.f;
-#pragma unroll
-    for (int c = 0; c < CM; ++c)
-      if (c < C) {
-        if (c == t) xt = v[c];
-        v[c] = expf(v[c] - mx);
-        s += v[c];
-      }
-    const float wt = on ? w[t] : 0.f;
-    if (on) l = -wt * (xt - mx - logf(s));
-    const float g = wt * inv_denom, rs = 1.0f / s;
-#pragma unroll
-    for (int c = 0; c < CM; ++c)
-      if (c < C) dx[row * ldd + c] = on ? g * (v[c] * rs - (c == t ? 1.f : 0.f)) : 0.f;
+    for (int c = 0; c < CM; ++c) v[c] = c < C ? x[row * ldx + c] : 0.f;
+    l = masked_ce_row<CM>(v, C, t, on, on ? w[t] : 0.f, inv_denom, dx + row * ldd);
   }
   const float t = block_sum(l, sh);
   if (threadIdx.x == 0) partial[blockIdx.x] = t;

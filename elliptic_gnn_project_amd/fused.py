@@ -382,7 +382,17 @@ class _FusedSAGE(torch.autograd.Function):
                 hn = gemm_nt(agg, None, Wl[l].size(0), a2=h, **nt_kw)
             aggs.append(agg)
             hs.append(hn)
-        logits = aggregate(plan, z[:, :C], _lib.AGG_MEAN, nodew=plan.deg, addend=z[:, C:], bias=bl[-1])
+        from .train_ops import ce_target, sage_out_mean_ce
+
+        tgt = ce_target()
+        if tgt is not None and any(ctx.needs_input_grad) and z.dtype == torch.float32 and C <= 4:
+            # the step's masked CE in the output mean's launch (train_ops.fused_ce_target)
+            e0 = KernelTimer.begin()
+            logits, ce = sage_out_mean_ce(plan, z, C, bl[-1], tgt)
+            KernelTimer.end(e0, ("agg", _lib.AGG_MEAN, False, C), agg_bytes(plan, C, _lib.AGG_MEAN, False, False))
+            logits._gnnmp_ce = ce
+        else:
+            logits = aggregate(plan, z[:, :C], _lib.AGG_MEAN, nodew=plan.deg, addend=z[:, C:], bias=bl[-1])
         ctx.plan = plan
         ctx.meta = (L, C, float(dropout_p))
         ctx.P = P  # the output layer's stacked weights, reused by the backward (no second cat)

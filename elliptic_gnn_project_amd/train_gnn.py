@@ -17,6 +17,7 @@ The mini-batch path (:212-245, :260-276, :329-348) runs on loader.NeighborLoader
 from __future__ import annotations
 
 import argparse
+import contextlib
 import csv
 import json
 import os
@@ -141,8 +142,22 @@ def _make_loss_fn(cfg: Dict, cw: torch.Tensor, model, t_min: int, t_max: int, wo
         t_sel = t_idx_all.index_select(0, idx) if t_idx_all is not None else None
         return loss_fn(logits.index_select(0, idx), y_all.index_select(0, idx), t_sel, denom=denom)
 
+    def target(y_all, mask, denom):
+        """Context for the training forward whose loss is ``full(logits, y_all, mask, denom)``:
+        the forward may compute that masked CE itself (train_ops.fused_ce_target — the fused SAGE
+        output layer does, in its aggregation's launch); a no-op for the other loss variants."""
+        if not (loss_fn.plain and y_all.is_cuda and denom is not None):
+            return contextlib.nullcontext()
+        from .train_ops import fused_ce_target
+
+        w = cw_dev.get(y_all.device)
+        if w is None:
+            w = cw_dev[y_all.device] = cw.to(y_all.device)
+        return fused_ce_target(y_all, mask, w, denom)
+
     loss_fn.plain = not focal and scheme == "none" and embed_l2 == 0.0
     loss_fn.full = full
+    loss_fn.target = target
     return loss_fn
 
 
@@ -208,8 +223,10 @@ def train_epoch(model, data, edge_index, optimizer, loss_fn, scaler, use_amp, cf
     # AMP on an fp32 libgnnmp model (amp_is_exact): the fused step, GradScaler's scale / unscale
     # left out (exact on fp32 gradients) and its skip of a non-finite update done by ClipAdam
     amp_fused = use_amp and getattr(optimizer, "skip_nonfinite", False)
+    fused_ce = getattr(loss_fn, "plain", False) and (not use_amp or amp_fused) and denom is not None
     with _autocast(device, use_amp):
-        logits = model(data.x, edge_index, data.timestep if _model_uses_time_embed(model) else None)
+        with (loss_fn.target(data.y, data.train_mask, denom) if fused_ce else contextlib.nullcontext()):
+            logits = model(data.x, edge_index, data.timestep if _model_uses_time_embed(model) else None)
         t_idx = _rows(data.timestep, data, "train") if cfg.get("time_loss_weighting", "none") != "none" else None
         if (getattr(loss_fn, "plain", False) and logits.is_cuda and logits.dtype == torch.float32
                 and (not use_amp or amp_fused)):

@@ -77,6 +77,90 @@ class _MaskedCE(torch.autograd.Function):
         return dl * g, None, None, None, None
 
 
+class _PrecomputedCE(torch.autograd.Function):
+    """The masked CE a forward already computed (fused_ce_target: gnn_sage_out_mean_ce_f32 ran it
+    in the output layer's aggregation): the loss as is, dlogits from its [N, 2C] buffer — the
+    same tensors and tags _MaskedCE produces."""
+
+    @staticmethod
+    def forward(ctx, logits, ce):
+        _, loss, buf, ws = ce
+        ctx.save_for_backward(buf)
+        ctx.C = buf.size(1) // 2
+        ctx.ws = ws  # the loss partials (a deferred loss reads them at the step's end)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (buf,) = ctx.saved_tensors
+        dl = buf[:, ctx.C:]
+        ones = _ONES.get(g.device)
+        if ones is not None and g.data_ptr() == ones.data_ptr():
+            dl._gnnmp_dz = buf
+            return dl, None
+        return dl * g, None
+
+
+_CE_TARGET = [None]  # (key, y, mask_u8, class_w, inv_denom) of the active fused_ce_target
+
+
+def _ce_operands(y, mask, class_w, denom, device):
+    m8 = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)
+    w = class_w.to(device=device, dtype=torch.float32).contiguous()
+    y = y.contiguous()
+    m8 = m8.contiguous()
+    inv = 1.0 / float(denom)
+    return (y.data_ptr(), m8.data_ptr(), w.data_ptr(), inv), y, m8, w, inv
+
+
+class fused_ce_target:
+    """Context of a training forward whose loss will be ``masked_cross_entropy(logits, y, mask,
+    class_w, denom)`` with exactly these operands: a forward that can compute it on the way does
+    (the fused SAGE output layer's mean runs gnn_sage_out_mean_ce_f32 — the F = 2 aggregation and
+    the CE in one launch, bit for bit the two launches' results) and masked_cross_entropy then
+    returns that result instead of launching the CE.  Every other consumer of the logits sees the
+    same logits; a loss with other operands falls back to its own launch.  ``denom`` must be given
+    (no host sync)."""
+
+    def __init__(self, y: torch.Tensor, mask: torch.Tensor, class_w: torch.Tensor, denom: float):
+        self.args = (y, mask, class_w, denom)
+
+    def __enter__(self):
+        y, mask, class_w, denom = self.args
+        if y.is_cuda and float(denom) != 0.0:
+            _CE_TARGET[0] = _ce_operands(y, mask, class_w, denom, y.device)
+        return self
+
+    def __exit__(self, *exc):
+        _CE_TARGET[0] = None
+        return False
+
+
+def ce_target():
+    """The active fused_ce_target's (key, y, mask_u8, class_w, inv_denom), or None."""
+    return _CE_TARGET[0]
+
+
+def sage_out_mean_ce(plan, z: torch.Tensor, C: int, bias, target):
+    """logits = mean_{j->i} z[j, :C] + z[i, C:] + bias and the target's masked CE in one launch
+    (include/gnnmp.h gnn_sage_out_mean_ce_f32).  Returns (logits, ce) — ce for _PrecomputedCE."""
+    from .fused import defer_loss_sum
+
+    key, y, m8, w, inv = target
+    N, dev = z.size(0), z.device
+    logits = torch.empty((N, C), dtype=torch.float32, device=dev)
+    buf = torch.empty((N, 2 * C), dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    ws = _ws(_ce_ws_bytes(N), dev)
+    nblk = max(1, -(-N // 256))
+    deferred = defer_loss_sum(dev, ws, nblk, inv, loss)  # captured step with defer_loss: at its end
+    _lib.call("gnn_sage_out_mean_ce_f32", plan.c_graph, plan.deg.data_ptr(), z.data_ptr(), int(z.stride(0)), int(C),
+              _lib.ptr(bias), logits.data_ptr(), C, y.data_ptr(), m8.data_ptr(), w.data_ptr(), float(inv),
+              buf.data_ptr() + C * 4, 2 * C, None if deferred else loss.data_ptr(), ws.data_ptr(), ws.numel() * 4,
+              _lib.stream_handle(dev))
+    return logits, (key, loss, buf, ws)
+
+
 def masked_cross_entropy(logits: torch.Tensor, y: torch.Tensor, mask: torch.Tensor, class_w: torch.Tensor,
                          denom: float | None = None) -> torch.Tensor:
     """Σ_{i: mask_i} CE_w(logits_i, y_i) / denom (denom defaults to mask.sum(): the reference's .mean()).
@@ -92,9 +176,11 @@ def masked_cross_entropy(logits: torch.Tensor, y: torch.Tensor, mask: torch.Tens
     if float(denom) == 0.0:
         # empty selection: the reference's loss_vec.mean() is NaN and its gradient is zero
         return logits.sum() * 0.0 + float("nan")
-    m8 = mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)  # bool: no copy
-    w = class_w.to(device=logits.device, dtype=torch.float32).contiguous()
-    return _MaskedCE.apply(logits, y.contiguous(), m8.contiguous(), w, 1.0 / float(denom))
+    key, y, m8, w, inv = _ce_operands(y, mask, class_w, denom, logits.device)  # bool mask: no copy
+    ce = getattr(logits, "_gnnmp_ce", None)
+    if ce is not None and ce[0] == key:  # the forward already computed it (fused_ce_target)
+        return _PrecomputedCE.apply(logits, ce)
+    return _MaskedCE.apply(logits, y, m8, w, inv)
 
 
 class ClipAdam(torch.optim.Optimizer):

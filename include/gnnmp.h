@@ -230,6 +230,20 @@ typedef enum {
   GNN_PLANES_HALF_PAIR = 1    /* 2 f16 planes hi / lo (gnn_split_h2_f32) */
 } gnn_planes_format;
 
+/* The SAGE output layer's mean and the training loss in ONE pass (ABI 19): logits = mean_{j->i}
+ * z[j, 0:C] + z[i, C:2C] + bias (SAGEConv transform-first: z = h·[W_l ; W_r]ᵀ, gnn.py:49-53) —
+ * gnn_aggregate_f32(MEAN, addend, bias)'s arithmetic — and, in the same kernel's epilogue, the
+ * masked class-weighted cross entropy of those logits (gnn_masked_ce_f32: dlogits, per-256-row loss
+ * partials in `workspace`, `loss` = Σ partials · inv_denom or left to gnn_masked_ce_finish /
+ * gnn_adam_group.loss_partial when NULL), bit for bit as the two calls produce them.  Replaces
+ * the F = 2 aggregation + the CE launch of the training step (src/train_gnn.py:192-199).
+ * 1 <= C <= 4, ldz >= 2C; workspace: gnn_masked_ce_workspace_size(num_nodes). */
+gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* deg, const float* z, int64_t ldz, int32_t C,
+                                    const float* bias, float* logits, int64_t ldo, const int64_t* y,
+                                    const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
+                                    int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,
+                                    gnn_stream_t stream);
+
 /* Named forms of the above (what an FFI binding of SAGEConv would call). */
 gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,
                                  int64_t F, float* out, int64_t ldo, gnn_stream_t stream);
