@@ -14,7 +14,7 @@ from pathlib import Path
 import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "libgnnmp.so"
+LIB_PATH = Path(os.environ["GNNMP_LIB"]) if os.environ.get("GNNMP_LIB") else PKG_DIR / "libgnnmp.so"  # (GNNMP_LIB: A/B builds)
 ABI_VERSION = 19
 
 # gnn_dtype

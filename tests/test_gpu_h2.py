@@ -539,11 +539,14 @@ def test_input_nt_h2(device, F, n, bias):
 
 @pytest.mark.parametrize("F,nr", [(166, 64), (166, 128), (167, 64), (40, 16)])
 @pytest.mark.parametrize("scale", [1.0, 1e-6, 3e4])
-def test_input_tn_h2_g_form(device, F, nr, scale):
+@pytest.mark.parametrize("prof", ["rand", "ramp", "late"])
+def test_input_tn_h2_g_form(device, F, nr, scale, prof):
     """dW = Gᵀ·x, db = ΣG for a registered model input (GCN / GAT layer 1, SAGE-ResBN layer 0) on
     x's half-pair image (the plain g form of the half-pair TN, round 5): within relL2 1e-6 of
     float64 for inputs and gradients of any magnitude, and equal to the split-bf16 image's TN
-    within 1e-5."""
+    within 1e-5.  ``prof`` shapes |G| along the rows for the kernel's running block scale: ramp —
+    growing 1e-4 -> 1e4 down the rows (the scale drops chunk after chunk, the accumulators are
+    rescaled); late — rows zero except the last of every 800 (the scale is set by one chunk)."""
     from elliptic_gnn_project_amd.fused import gemm_tn, gemm_tn_input
     from elliptic_gnn_project_amd.planes import HalfPairImage, register_input, x_only_image
 
@@ -551,6 +554,10 @@ def test_input_tn_h2_g_form(device, F, nr, scale):
     g_ = torch.Generator().manual_seed(F + nr)
     x = register_input((torch.randn(M, F, generator=g_) * scale).to(device))
     G = torch.randn(M, nr, generator=g_) * torch.exp(torch.randn(M, 1, generator=g_) * 2) * 1e-3
+    if prof == "ramp":
+        G = G * torch.logspace(-4, 4, M).view(M, 1)
+    elif prof == "late":
+        G = G * (torch.arange(M).view(M, 1) % 800 == 799)
     im = x_only_image(x, HalfPairImage)
     assert gemm_tn(nr, None, g=G.to(device), planes=im, check_planes=True)
     (dW, _), db, _, _ = gemm_tn_input(nr, x, G.to(device))
