@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["GNNMP_LIB"]) if os.environ.get("GNNMP_LIB") else PKG_DIR / "libgnnmp.so"  # (GNNMP_LIB: A/B builds)
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -101,6 +101,8 @@ class GnnAggParams(ctypes.Structure):
         ("dropout_p", ctypes.c_float),
         ("seed", ctypes.c_uint64),
         ("seed_ptr", c_ptr),
+        ("addend2", c_ptr),
+        ("ld_add2", c_i64),
     ]
 
 
@@ -141,6 +143,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("a_dtype", c_i32), ("h_dtype", c_i32),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
         ("planes_format", c_i32), ("g_dtype", c_i32), ("planes_exp", c_i32),
+        ("sq_partial", c_ptr), ("sq_step", c_ptr), ("sq_skip_lo", c_i64), ("sq_skip_hi", c_i64), ("sq_cap", c_i64),
     ]
 
 
@@ -182,6 +185,7 @@ class GnnAdamGroup(ctypes.Structure):
         ("skip_nonfinite", c_i32),
         ("bump_counter", c_ptr),
         ("loss_partial", c_ptr), ("loss_nblk", c_i32), ("loss_scale", ctypes.c_float), ("loss_out", c_ptr),
+        ("grad_sq_partial", c_ptr), ("grad_sq_nblk", c_i32),
     ]
 
 
@@ -277,6 +281,7 @@ SIGNATURES = {
     "gnn_gemm_nt_prep_b": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), c_ptr]),
     "gnn_masked_ce_finish": (ctypes.c_int, [c_ptr, c_i32, ctypes.c_float, c_ptr, c_ptr]),
     "gnn_gemm_tn_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32, ctypes.POINTER(c_size)]),
+    "gnn_gemm_tn_sq_blocks": (ctypes.c_int, [c_i64, ctypes.POINTER(c_i32)]),
     "gnn_gemm_tn_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams), c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_gemm_nt_planes_ok": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams)]),
     "gnn_gemm_tn_planes_ok": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams)]),

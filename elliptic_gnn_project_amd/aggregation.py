@@ -91,12 +91,13 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
               nodew: torch.Tensor | None = None, ew: torch.Tensor | None = None, heads: int = 1,
               addend: torch.Tensor | None = None, bias: torch.Tensor | None = None,
               relu: bool = False, out: torch.Tensor | None = None, dropout_p: float = 0.0, seed: int = 0,
-              seed_ptr: torch.Tensor | None = None) -> torch.Tensor:
+              seed_ptr: torch.Tensor | None = None, addend2: torch.Tensor | None = None) -> torch.Tensor:
     """Raw call of gnn_aggregate_f32 (no autograd); bf16 rows go to gnn_aggregate_bf16 (bf16 out).
-    ``dropout_p`` > 0: counter-hash dropout of element r·F + f after bias / ReLU (fp32 path)."""
+    ``dropout_p`` > 0: counter-hash dropout of element r·F + f after bias / ReLU (fp32 path).
+    ``addend2``: a second [N, F] term summed after ``addend`` (fp32 path, ABI 20)."""
     if x.dtype == torch.bfloat16:
-        if dropout_p > 0:
-            raise NotImplementedError("dropout epilogue on the bf16-storage aggregation")
+        if dropout_p > 0 or addend2 is not None:
+            raise NotImplementedError("dropout / addend2 epilogue on the bf16-storage aggregation")
         return _aggregate_bf16(plan, x, mode, transpose, nodew, addend, bias, relu, out)
     x = _as_f32_rows(x)
     N, F = plan.num_nodes, x.size(1)
@@ -106,6 +107,8 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
         out = torch.empty((N, F), dtype=torch.float32, device=x.device)
     if addend is not None:
         addend = _as_f32_rows(addend)
+    if addend2 is not None:
+        addend2 = _as_f32_rows(addend2)
     # partial-sum rows for the long-segment split (used by the lane-group gather, 8 < F <= 128;
     # the narrow F <= 4 kernels measured no faster with it on the bench graph)
     npieces = plan.split_pieces(transpose) if (mode != _lib.AGG_EDGE_W and 8 < F <= SPLIT_MAX_F) else 0
@@ -115,6 +118,7 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
         _lib.ptr(addend), _ld(addend) if addend is not None else 0,
         _lib.ptr(bias), int(relu), _lib.ptr(part), part.numel() * 4 if part is not None else 0,
         float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ptr),
+        _lib.ptr(addend2), _ld(addend2) if addend2 is not None else 0,
     )
     if KernelTimer.active:
         a = torch.cuda.Event(enable_timing=True)
@@ -125,7 +129,7 @@ def aggregate(plan: GraphPlan, x: torch.Tensor, mode: int, transpose: bool = Fal
     if KernelTimer.active:
         b.record()
         KernelTimer.records.append((("agg", int(mode), bool(transpose), int(F)), a, b,
-                                    agg_bytes(plan, F, mode, transpose, addend is not None)))
+                                    agg_bytes(plan, F, mode, transpose, int(addend is not None) + int(addend2 is not None))))
     return out
 
 
@@ -159,7 +163,7 @@ def _aggregate_bf16(plan, x, mode, transpose, nodew, addend, bias, relu, out):
     return out
 
 
-def agg_bytes(plan: GraphPlan, F: int, mode: int, transpose: bool, has_addend: bool, elem: int = 4) -> int:
+def agg_bytes(plan: GraphPlan, F: int, mode: int, transpose: bool, has_addend, elem: int = 4) -> int:
     """Algorithmic HBM bytes of one aggregation launch (fp32, int32 plan).
 
     rowptr/colptr 4(N+1) + neighbour ids 4S + one F-row gather per slot 4·S·F + output
@@ -172,8 +176,7 @@ def agg_bytes(plan: GraphPlan, F: int, mode: int, transpose: bool, has_addend: b
         b += 4 * N
     elif mode in (_lib.AGG_MEAN_BWD, _lib.AGG_GCN):
         b += 4 * S
-    if has_addend:
-        b += 4 * N * F
+    b += 4 * N * F * int(has_addend)  # (the number of fused [N, F] addends: 0, 1 or 2)
     return b
 
 

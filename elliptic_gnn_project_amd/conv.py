@@ -77,11 +77,15 @@ class _SAGEAggregateFirst(torch.autograd.Function):
     """out = [mean_{j->i} x_j | x_i] · [W_l | W_r]ᵀ + b (PyG's order) with a one-pass backward for
     the input: [dG_l | dG_r] = dout · [W_l | W_r] as ONE split-bf16 NT GEMM (dout read once), then
     dx = meanᵀ(dG_l) + dG_r with dG_r added in the transposed aggregation's epilogue — instead of
-    two NT GEMMs and an add kernel.  dW_l, dW_r, db from one TN over [agg | x] as linear2."""
+    two NT GEMMs and an add kernel.  dW_l, dW_r, db from one TN over [agg | x] as linear2.
+    ``res``: also return x itself (an alias) for an identity residual branch that consumes it
+    (SAGE-ResBN's hidden layers, gnn.py:187-194); its gradient dr is then summed in the same
+    transposed aggregation's store, dx = meanᵀ(dG_l) + dG_r + dr (gnn_agg_params.addend2),
+    instead of autograd adding the two branches' gradients in a separate pass."""
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-    def forward(ctx, x, wl, wr, bias, plan: GraphPlan):
+    def forward(ctx, x, wl, wr, bias, plan: GraphPlan, res: bool = False):
         from .fused import gemm_nt
         from .linear import _rows
         x = _rows(x)
@@ -92,11 +96,12 @@ class _SAGEAggregateFirst(torch.autograd.Function):
         ctx.save_for_backward(agg, x, wl, wr)
         ctx.plan = plan
         ctx.has_bias = bias is not None
-        return y
+        ctx.res = bool(res)
+        return (y, x.view_as(x)) if res else y
 
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
-    def backward(ctx, dy):
+    def backward(ctx, dy, dr=None):
         from .fused import gemm_nt, gemm_tn
         from .linear import _rows
         agg, x, wl, wr = ctx.saved_tensors
@@ -110,9 +115,10 @@ class _SAGEAggregateFirst(torch.autograd.Function):
             fi = wl.size(1)
             wt = torch.cat([wl, wr], dim=1).t().contiguous()  # [2·F_in, F_out]: Linear-weight form
             d = gemm_nt(dy, None, 2 * fi, w1=wt)
-            dx = aggregate(plan, d[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, addend=d[:, fi:])
+            dx = aggregate(plan, d[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, addend=d[:, fi:],
+                           addend2=dr if (ctx.res and dr is not None) else None)
         return (dx, dWl if need[1] else None, dWr if need[2] else None,
-                db if (ctx.has_bias and need[3]) else None, None)
+                db if (ctx.has_bias and need[3]) else None, None, None)
 
 
 class SAGEConv(nn.Module):
@@ -151,6 +157,20 @@ class SAGEConv(nn.Module):
             return self.out_channels < self.in_channels
         return self.order == "transform_first"
 
+    def _aggregate_first_ok(self, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dim() == 2 and x.size(0) > 0 and x.dtype != torch.bfloat16
+                and 2 * self.in_channels <= 128 and self.out_channels <= 128)
+
+    def forward_with_residual(self, x: torch.Tensor, edge_index: torch.Tensor):
+        """(forward(x, edge_index), r) with r == x for an identity residual branch: on the fused
+        aggregate-first path r is an alias whose gradient the conv's backward sums into dx in its
+        own aggregation store (internal to SAGEResBNNet.forward; not part of PyG's API)."""
+        if (not getattr(self, "explain", False) and not self._transform_first()
+                and self._aggregate_first_ok(x) and torch.is_grad_enabled()):
+            plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
+            return _SAGEAggregateFirst.apply(x, self.lin_l.weight, self.lin_r.weight, self.lin_l.bias, plan, True)
+        return self.forward(x, edge_index), x
+
     def forward(self, x: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
         if getattr(self, "explain", False) and getattr(self, "_edge_mask", None) is not None:
             # PyG explain mode (set_masks): messages x_j scaled by the (sigmoided) edge mask
@@ -163,8 +183,7 @@ class SAGEConv(nn.Module):
             y = linear(x, w)  # [N, 2*F_out]: MFMA GEMM (K7)
             plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
             return _MeanAggRootBias.apply(y, self.lin_l.bias, plan, fo)
-        if (x.is_cuda and x.dim() == 2 and x.size(0) > 0 and x.dtype != torch.bfloat16
-                and 2 * self.in_channels <= 128 and self.out_channels <= 128):
+        if self._aggregate_first_ok(x):
             plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
             return _SAGEAggregateFirst.apply(x, self.lin_l.weight, self.lin_r.weight, self.lin_l.bias, plan)
         agg = mean_aggregate(x, edge_index)

@@ -91,6 +91,7 @@ struct AggArgs {
   const float* x; int64_t ldx;
   float* y; int64_t ldy;
   const float* add; int64_t ld_add;
+  const float* add2; int64_t ld_add2;  // a second addend, summed after add (ABI 20)
   const float* bias;
   int32_t relu;
   int64_t nrows;
@@ -194,6 +195,12 @@ __device__ __forceinline__ void finish(const AggArgs& a, int64_t r, int f0, floa
 #pragma unroll
     for (int q = 0; q < VEC; ++q) acc[q] += t[q];
   }
+  if (a.add2) {
+    float t[VEC];
+    vload<VEC>(a.add2 + r * a.ld_add2 + f0, t);
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) acc[q] += t[q];
+  }
   if (a.bias) {
 #pragma unroll
     for (int q = 0; q < VEC; ++q) acc[q] += a.bias[f0 + q];
@@ -261,6 +268,12 @@ __device__ __forceinline__ void agg_flat_body(const AggArgs& a, int32_t rpg, uin
         if (a.add) {
           float ad[VEC];
           vload<VEC>(a.add + r * a.ld_add + f0, ad);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += ad[q];
+        }
+        if (a.add2) {
+          float ad[VEC];
+          vload<VEC>(a.add2 + r * a.ld_add2 + f0, ad);
 #pragma unroll
           for (int q = 0; q < VEC; ++q) t[q] += ad[q];
         }
@@ -382,6 +395,12 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
         if (a.add) {
           float ad[VEC];
           vload<VEC>(a.add + r * a.ld_add + f0, ad);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += ad[q];
+        }
+        if (a.add2) {
+          float ad[VEC];
+          vload<VEC>(a.add2 + r * a.ld_add2 + f0, ad);
 #pragma unroll
           for (int q = 0; q < VEC; ++q) t[q] += ad[q];
         }
@@ -547,6 +566,12 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
 #pragma unroll
           for (int q = 0; q < VEC; ++q) t[q] += ad[q];
         }
+        if (a.add2) {
+          float ad[VEC];
+          vload<VEC>(a.add2 + r * a.ld_add2 + f0, ad);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) t[q] += ad[q];
+        }
         if (a.bias) {
 #pragma unroll
           for (int q = 0; q < VEC; ++q) t[q] += a.bias[f0 + q];
@@ -667,11 +692,12 @@ __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
       // epilogue operands loaded together (clamped indices) — finish<MODE, 1>'s arithmetic
       const int32_t p0 = a.piece0 ? a.piece0[r] : -1;
       const float dr = MODE == GNN_AGG_MEAN ? fmaxf(a.nodew[r], 1.0f) : 1.0f;
-      float addv[NF], bv[NF];
+      float addv[NF], add2v[NF], bv[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         const int fc = f < a.F ? f : 0;
         addv[f] = a.add ? a.add[r * a.ld_add + fc] : 0.0f;
+        add2v[f] = a.add2 ? a.add2[r * a.ld_add2 + fc] : 0.0f;
         bv[f] = a.bias ? a.bias[fc] : 0.0f;
       }
       const uint64_t dseed = a.dropout ? agg_seed(a) : 0;
@@ -684,6 +710,7 @@ __global__ __launch_bounds__(256) void agg_group_kernel(AggArgs a) {
           } else {
             if constexpr (MODE == GNN_AGG_MEAN) t[0] = t[0] / dr;
             if (a.add) t[0] += addv[f];
+            if (a.add2) t[0] += add2v[f];
             if (a.bias) t[0] += bv[f];
             if (a.relu) t[0] = fmaxf(t[0], 0.0f);
             if (a.dropout) agg_dropout<1>(a, dseed, r, f, t);
@@ -731,11 +758,15 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   // the gather instead of one more dependent round trip after it
   // (clamped row / feature indices, no per-value branch: the epilogue reads only f < F)
   const int64_t rr = rok ? r : r0;
-  float pdeg = 1.0f, padd[4] = {0.f, 0.f, 0.f, 0.f}, pbias[4] = {0.f, 0.f, 0.f, 0.f};
+  float pdeg = 1.0f, padd[4] = {0.f, 0.f, 0.f, 0.f}, padd2[4] = {0.f, 0.f, 0.f, 0.f}, pbias[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (MODE == GNN_AGG_MEAN) pdeg = fmaxf(a.nodew[rr], 1.0f);
   if (a.add) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) padd[f] = a.add[rr * a.ld_add + (f < F ? f : 0)];
+  }
+  if (a.add2) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) padd2[f] = a.add2[rr * a.ld_add2 + (f < F ? f : 0)];
   }
   if (a.bias) {
 #pragma unroll
@@ -827,6 +858,7 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
         } else {  // finish<MODE, 1> with the preloaded operands (same operation order)
           if constexpr (MODE == GNN_AGG_MEAN) t[0] = t[0] / pdeg;
           if (a.add) t[0] += padd[f];
+          if (a.add2) t[0] += padd2[f];
           if (a.bias) t[0] += pbias[f];
           if (a.relu) t[0] = fmaxf(t[0], 0.0f);
           if (a.dropout) agg_dropout<1>(a, agg_seed(a), r, f, t);
@@ -1226,6 +1258,7 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
     return fail(GNN_ERR_INVALID_ARG, __func__, "bad F / leading dimensions");
   if (g->num_nodes > 0 && F > 0 && (!x || !y)) return fail(GNN_ERR_INVALID_ARG, __func__, "null x/y");
   if (p->addend && p->ld_add < F) return fail(GNN_ERR_INVALID_ARG, __func__, "bad ld_add");
+  if (p->addend2 && p->ld_add2 < F) return fail(GNN_ERR_INVALID_ARG, __func__, "bad ld_add2");
   AggArgs a{};
   a.ptr = p->transpose ? g->colptr : g->rowptr;
   a.nbr = p->transpose ? g->row : g->col;
@@ -1235,6 +1268,7 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
   a.heads = p->heads > 0 ? p->heads : 1;
   a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy;
   a.add = p->addend; a.ld_add = p->ld_add;
+  a.add2 = p->addend2; a.ld_add2 = p->ld_add2;
   a.bias = p->bias; a.relu = p->relu;
   if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout p in [0,1)");
   if (p->dropout_p > 0.f && (int64_t)g->num_nodes * (int64_t)F >= ((int64_t)1 << 32))
@@ -1258,9 +1292,10 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
   auto ok_vec = [&](int v) {
     if (F % v || ldx % v || ldy % v) return false;
     if (p->addend && p->ld_add % v) return false;
+    if (p->addend2 && p->ld_add2 % v) return false;
     if (p->mode == GNN_AGG_EDGE_W && a.chan % v) return false;
     int b = 4 * v;
-    return aligned(x, b) && aligned(y, b) && aligned(p->addend, b);
+    return aligned(x, b) && aligned(y, b) && aligned(p->addend, b) && aligned(p->addend2, b);
   };
   // Long-segment split (not for EDGE_W: its weights are indexed by the untruncated slot).
   const gnn_split* sp = p->transpose ? g->csc_split : g->csr_split;
@@ -1339,6 +1374,7 @@ extern "C" gnn_status gnn_aggregate_bf16(const gnn_graph* g, const gnn_agg_param
     return fail(GNN_ERR_INVALID_ARG, __func__, "mode needs nodew");
   if (g->num_nodes > 0 && F > 0 && (!x || !y)) return fail(GNN_ERR_INVALID_ARG, __func__, "null x/y");
   if (p->addend && p->ld_add < F) return fail(GNN_ERR_INVALID_ARG, __func__, "bad ld_add");
+  if (p->addend2) return fail(GNN_ERR_UNSUPPORTED, __func__, "addend2 is f32-only");
   AggArgs a{};
   a.ptr = p->transpose ? g->colptr : g->rowptr;
   a.nbr = p->transpose ? g->row : g->col;

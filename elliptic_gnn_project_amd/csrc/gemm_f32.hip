@@ -687,9 +687,14 @@ __global__ __launch_bounds__(TN_THREADS) void gemm_tn_kernel(TNArgs a) {
 // thread rows each sum a fixed 1/16 of the slabs (4 independent loads in flight), and the 16
 // partials are combined through LDS in slab order.  ~700 blocks: the whole chip streams the
 // slabs instead of one thread per output walking all of them.
+// SqOut (ABI 20): the clip + Adam norm partials of this block's outputs (Σ out² and the count of
+// non-finite outputs, outside [skip_lo, skip_hi)), and block 0 snapshots the optimizer's step count.
+struct SqOut {
+  float* part; const float* step; int64_t skip_lo, skip_hi;
+};
 constexpr int kRedOut = 16, kRedGrp = 16;
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, int64_t stride, int nblk,
-                                                          float* __restrict__ out, int64_t n) {
+                                                          float* __restrict__ out, int64_t n, SqOut sq = SqOut{}) {
   __shared__ float4 part[kRedGrp][kRedOut];
   const int o = threadIdx.x & (kRedOut - 1);
   const int g = threadIdx.x / kRedOut;
@@ -716,8 +721,10 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   }
   part[g][o] = s;
   __syncthreads();
-  if (g == 0 && j < n) {
-    float4 t = part[0][o];
+  if (g != 0) return;  // threads 0..15 (wave 0) finish the block's 16 float4 outputs
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (j < n) {
+    t = part[0][o];
     for (int q = 1; q < kRedGrp; ++q) {
       float4 v = part[q][o];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
@@ -726,6 +733,27 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     if (j + 1 < n) out[j + 1] = t.y;
     if (j + 2 < n) out[j + 2] = t.z;
     if (j + 3 < n) out[j + 3] = t.w;
+  }
+  if (sq.part) {  // this block's norm partials: its 64 outputs in a fixed order (ABI 20)
+    float s2 = 0.f, nf = 0.f;
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t je = j + e;
+      const bool use = je < n && (je < sq.skip_lo || je >= sq.skip_hi);
+      s2 = use ? fmaf(tv[e], tv[e], s2) : s2;
+      nf += (use && !isfinite(tv[e])) ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) {
+      s2 += __shfl_xor(s2, off, 16);
+      nf += __shfl_xor(nf, off, 16);
+    }
+    if (o == 0) {
+      sq.part[blockIdx.x] = s2;
+      sq.part[gridDim.x + blockIdx.x] = nf;
+      if (blockIdx.x == 0) sq.part[2 * gridDim.x] = sq.step[0];
+    }
   }
 }
 
@@ -883,6 +911,14 @@ extern "C" gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t 
 static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void* workspace,
                                    size_t workspace_bytes, gnn_stream_t stream);
 
+static unsigned red_blocks(int64_t n_out) { return (unsigned)ceil_div(ceil_div(n_out, 4), kRedOut); }
+
+extern "C" gnn_status gnn_gemm_tn_sq_blocks(int64_t n_out, int32_t* nb) {
+  if (!nb || n_out < 1) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
+  *nb = (int32_t)red_blocks(n_out);
+  return GNN_OK;
+}
+
 extern "C" gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* workspace,
                                       size_t workspace_bytes, gnn_stream_t stream) {
   return gemm_tn_dispatch(p, out, workspace, workspace_bytes, stream);
@@ -915,7 +951,17 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   if (!workspace || workspace_bytes < (size_t)nblk * stride * sizeof(float))
     return fail(GNN_ERR_WORKSPACE, __fn, "workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  if (p->M == 0) return hip_check(hipMemsetAsync(out, 0, n_out * sizeof(float), st), __fn);
+  SqOut sqo{};
+  if (p->sq_partial) {
+    if (!p->sq_step || p->sq_cap < 2 * (int64_t)red_blocks(n_out) + 1 || p->sq_skip_lo > p->sq_skip_hi)
+      return fail(GNN_ERR_INVALID_ARG, __fn, "sq_partial needs sq_step, sq_cap >= 2 nb + 1, skip_lo <= skip_hi");
+    sqo = SqOut{p->sq_partial, p->sq_step, p->sq_skip_lo, p->sq_skip_hi};
+  }
+  if (p->M == 0) {
+    if (!p->sq_partial) return hip_check(hipMemsetAsync(out, 0, n_out * sizeof(float), st), __fn);
+    slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(static_cast<float*>(workspace), stride, 0, out, n_out, sqo);
+    return hip_check(hipGetLastError(), __fn);  // zero slabs: out = 0, partials 0, the step snapshot
+  }
   TNArgs a{};
   a.M = p->M; a.Nr = (int32_t)p->Nr;
   a.g = p->g; a.ldg = p->ldg; a.dz = p->dz; a.lddz = p->lddz; a.proj = p->proj; a.nproj = nproj;
@@ -954,7 +1000,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
       if (p->math != GNN_MATH_F32 && tn_h2_ok(a)) {
         launch_tn_h2(a, nblk, st);
         GNN_LAUNCH_CHECK();
-        slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+        slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nblk, out, n_out, sqo);
         GNN_LAUNCH_CHECK();
         return GNN_OK;
       }
@@ -966,14 +1012,14 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
         return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 image A outside the image kernel's shapes");
       launch_tn_img16(a, nblk, st);
       GNN_LAUNCH_CHECK();
-      slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+      slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nblk, out, n_out, sqo);
       GNN_LAUNCH_CHECK();
       return GNN_OK;
     }
     if (a.ap && p->math != GNN_MATH_F32 && tn_planes_ok(a)) {
       launch_tn_planes(a, nblk, st);
       GNN_LAUNCH_CHECK();
-      slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+      slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nblk, out, n_out, sqo);
       GNN_LAUNCH_CHECK();
       return GNN_OK;
     }
@@ -986,7 +1032,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
       return fail(GNN_ERR_WORKSPACE, __fn, "workspace too small");
     launch_tn_skinny(a, nblk, st);
     GNN_LAUNCH_CHECK();
-    slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+    slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nblk, out, n_out, sqo);
     GNN_LAUNCH_CHECK();
     return GNN_OK;
   }
@@ -996,7 +1042,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31) && a.M >= 16) {
     launch_tn_x3(a, nblk, st);  // split-bf16 MFMA (gemm_x3.hip)
     GNN_LAUNCH_CHECK();
-    slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+    slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nblk, out, n_out, sqo);
     GNN_LAUNCH_CHECK();
     return GNN_OK;
   }
@@ -1008,7 +1054,7 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   else { if (v2) GNN_TN(false, false, 2, 32); else GNN_TN(false, false, 1, 32); }
 #undef GNN_TN
   GNN_LAUNCH_CHECK();
-  slab_reduce_kernel<<<(unsigned)ceil_div(ceil_div(n_out, 4), kRedOut), 256, 0, st>>>(a.slab, stride, nblk, out, n_out);
+  slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nblk, out, n_out, sqo);
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }

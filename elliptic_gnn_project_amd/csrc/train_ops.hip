@@ -124,6 +124,14 @@ __device__ __forceinline__ void adam_locate(const AdamLds& L, int n, int64_t e, 
 struct LossFinish {  // a deferred gnn_masked_ce_f32 loss (gnn_adam_group.loss_partial)
   const float* partial; int32_t n; float scale; float* out;
 };
+// *lf.out = lf.scale · Σ lf.partial: sum_partials_kernel's loop and reduction, exactly (one block)
+__device__ __forceinline__ void finish_loss(const LossFinish& lf, float* sh) {
+  float v = 0.f;
+  for (int i = threadIdx.x; i < lf.n; i += kAdamThreads) v += lf.partial[i];
+  const float tl = block_sum(v, sh);
+  if (threadIdx.x == 0) lf.out[0] = tl * lf.scale;
+}
+
 __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, float* __restrict__ partial,
                                                                 const float* __restrict__ step, LossFinish lf) {
   __shared__ float sh[kAdamThreads / 64];
@@ -155,12 +163,9 @@ __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, flo
     partial[kAdamBlocks + 1 + blockIdx.x] = tn;
     if (blockIdx.x == 0) partial[kAdamBlocks] = step[0];
   }
-  if (lf.partial && blockIdx.x == gridDim.x - 1) {  // sum_partials_kernel's loop and reduction, exactly
+  if (lf.partial && blockIdx.x == gridDim.x - 1) {
     __syncthreads();  // sh reused
-    float v = 0.f;
-    for (int i = threadIdx.x; i < lf.n; i += kAdamThreads) v += lf.partial[i];
-    const float tl = block_sum(v, sh);
-    if (threadIdx.x == 0) lf.out[0] = tl * lf.scale;
+    finish_loss(lf, sh);
   }
 }
 
@@ -170,31 +175,72 @@ __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, flo
 // skip_nonfinite (torch.amp.GradScaler.step's found_inf: some gradient ELEMENT is inf / NaN)
 // leaves parameters, moments, gradients and the step count untouched.  A finite gradient whose
 // Σg² overflows is not skipped: as in clip_grad_norm_, the norm is inf and the clip coefficient 0.
+// partial: Σg² of block b at [b], its non-finite count at [nf_off + b], the step count before the
+// update at [step_off]: grad_sq_kernel's layout (nblk = 64, nf_off = 65, step_off = 64) or the TN
+// reduce's (ABI 20: nblk = nb, nf_off = nb, step_off = 2 nb).  Every block sums them in the same
+// fixed order (lane-strided, then a butterfly per wave, then the 4 waves in order): for nblk <= 64
+// that is grad_sq's one-wave butterfly exactly.
 __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, const float* __restrict__ partial,
-                                                                  int nblk, float* __restrict__ step,
+                                                                  int nblk, int nf_off, int step_off,
+                                                                  float* __restrict__ step,
                                                                   double max_norm, double lr, double beta1,
                                                                   double beta2, double eps, double wd,
                                                                   float* __restrict__ norm_out, int skip_nonfinite,
-                                                                  int64_t* __restrict__ bump) {
+                                                                  int64_t* __restrict__ bump, LossFinish lf) {
   __shared__ float coef_sh;
   __shared__ int skip_sh;
+  __shared__ float red_sh[2][kAdamThreads / 64];
   __shared__ AdamLds L;
+  if (lf.partial && blockIdx.x == kAdamBlocks) {  // the extra block: a deferred CE loss, beside the update
+    finish_loss(lf, &red_sh[0][0]);
+    return;
+  }
   adam_stage(tb, L);
-  if (threadIdx.x < 64) {  // the nblk <= 64 partials: one per lane, fixed butterfly (same in every block)
-    float tot = threadIdx.x < nblk ? partial[threadIdx.x] : 0.f;
-    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
-    const float norm = sqrtf(tot);
-    float coef = 1.0f;
-    if (max_norm > 0.0) coef = fminf((float)max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
-    float nf = threadIdx.x < nblk ? partial[kAdamBlocks + 1 + threadIdx.x] : 0.f;
-    for (int o = 32; o > 0; o >>= 1) nf += __shfl_xor(nf, o);
-    const bool skip = skip_nonfinite && nf > 0.f;
+  {
+    float tot = 0.f, nf = 0.f;
+    constexpr int U = 4;  // every load of the first U·256 partials issued before the sums (clamped, no branch)
+    float pv[U], nv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = threadIdx.x + u * kAdamThreads, ic = min(i, nblk - 1);
+      pv[u] = partial[ic];
+      nv[u] = partial[nf_off + ic];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = threadIdx.x + u * kAdamThreads < nblk;
+      tot += ok ? pv[u] : 0.f;
+      nf += ok ? nv[u] : 0.f;
+    }
+    for (int i = threadIdx.x + U * kAdamThreads; i < nblk; i += kAdamThreads) {
+      tot += partial[i];
+      nf += partial[nf_off + i];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      tot += __shfl_xor(tot, o);
+      nf += __shfl_xor(nf, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      red_sh[0][threadIdx.x >> 6] = tot;
+      red_sh[1][threadIdx.x >> 6] = nf;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
+      tot = red_sh[0][0];
+      nf = red_sh[1][0];
+      for (int w = 1; w < kAdamThreads / 64; ++w) {
+        tot += red_sh[0][w];
+        nf += red_sh[1][w];
+      }
+      const float norm = sqrtf(tot);
+      float coef = 1.0f;
+      if (max_norm > 0.0) coef = fminf((float)max_norm / (norm + 1e-6f), 1.0f);  // torch clip_grad_norm_
+      const bool skip = skip_nonfinite && nf > 0.f;
       coef_sh = coef;
       skip_sh = skip;
       if (blockIdx.x == 0) {
         if (norm_out) norm_out[0] = norm;
-        step[0] = partial[nblk] + (skip ? 0.0f : 1.0f);
+        step[0] = partial[step_off] + (skip ? 0.0f : 1.0f);
         if (bump) bump[0] = bump[0] + 1;  // no kernel of this launch reads it
       }
     }
@@ -202,13 +248,13 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
   __syncthreads();
   if (skip_sh) return;  // block-uniform
   const float coef = coef_sh;
-  const double t = (double)partial[nblk] + 1.0;
+  const double t = (double)partial[step_off] + 1.0;
   const double bc1 = 1.0 - pow(beta1, t), bc2 = 1.0 - pow(beta2, t);
   const float neg_step = (float)(-lr / bc1), bc2s = (float)sqrt(bc2);
   const float b2 = (float)beta2, omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
   const float epsf = (float)eps, wdf = (float)wd;
   const int64_t total = L.off[tb.n];
-  const int64_t per = (total + gridDim.x - 1) / gridDim.x;
+  const int64_t per = (total + kAdamBlocks - 1) / kAdamBlocks;  // (an extra loss block: no slice)
   const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(total, e0 + per);
   for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamUnroll * kAdamThreads) {
     int j[kAdamUnroll];
@@ -311,11 +357,22 @@ extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, 
   float* partial = static_cast<float*>(workspace);
   LossFinish lf{grp->loss_partial, grp->loss_nblk, grp->loss_scale, grp->loss_out};
   if (lf.partial && (!lf.out || lf.n < 1)) return fail(GNN_ERR_INVALID_ARG, __func__, "loss_partial needs loss_out and loss_nblk >= 1");
+  if (grp->grad_sq_partial) {  // ABI 20: the norm partials came with the gradients (the TN's reduce)
+    if (grp->grad_sq_nblk < 1) return fail(GNN_ERR_INVALID_ARG, __func__, "grad_sq_partial needs grad_sq_nblk >= 1");
+    const int nb = grp->grad_sq_nblk;
+    clip_adam_kernel<<<kAdamBlocks + (lf.partial ? 1 : 0), kAdamThreads, 0, st>>>(tb, grp->grad_sq_partial, nb, nb, 2 * nb, step,
+                                                           grp->max_norm, grp->lr, grp->beta1, grp->beta2, grp->eps,
+                                                           grp->weight_decay, norm_out, grp->skip_nonfinite,
+                                                           grp->bump_counter, lf);
+    GNN_LAUNCH_CHECK();
+    return GNN_OK;
+  }
   grad_sq_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, step, lf);
   GNN_LAUNCH_CHECK();
-  clip_adam_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, kAdamBlocks, step, grp->max_norm, grp->lr,
-                                                         grp->beta1, grp->beta2, grp->eps, grp->weight_decay, norm_out,
-                                                         grp->skip_nonfinite, grp->bump_counter);
+  clip_adam_kernel<<<kAdamBlocks, kAdamThreads, 0, st>>>(tb, partial, kAdamBlocks, kAdamBlocks + 1, kAdamBlocks, step,
+                                                         grp->max_norm, grp->lr, grp->beta1, grp->beta2, grp->eps,
+                                                         grp->weight_decay, norm_out, grp->skip_nonfinite,
+                                                         grp->bump_counter, LossFinish{});
   GNN_LAUNCH_CHECK();
   return GNN_OK;
 }

@@ -20,6 +20,7 @@ kept values by 1/(1-p).
 """
 from __future__ import annotations
 
+import ctypes
 import functools
 import os
 from typing import List
@@ -181,9 +182,12 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
 
 
 def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gout=None, math=None,
-            planes=None, check_planes=False):
+            planes=None, check_planes=False, sq=None, sq_skip=(0, 0)):
     """((Gᵀ·a1, Gᵀ·a2), db, dzᵀ·h, dzsum) from one flat fp32 buffer — the MFMA TN kernel.
-    ``planes``: A read from a split image (a1 / a2 may be None); ``check_planes`` as gemm_nt."""
+    ``planes``: A read from a split image (a1 / a2 may be None); ``check_planes`` as gemm_nt.
+    ``sq`` = (partials buffer, step tensor) of train_ops.grad_sq_request: the reduce also writes
+    the clip + Adam norm partials of the output outside ``sq_skip`` (indices into the flat output,
+    negative ones from its end), recorded by train_ops.grad_sq_produced."""
     if planes is not None:
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
@@ -210,12 +214,20 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     if check_planes:
         return bool(_lib.load().gnn_gemm_tn_planes_ok(p))
     out = torch.empty(n_out, dtype=torch.float32, device=dev)
+    if sq is not None:
+        lo, hi = (int(v) + n_out if v < 0 else int(v) for v in sq_skip)
+        p.sq_partial, p.sq_step = sq[0].data_ptr(), sq[1].data_ptr()
+        p.sq_skip_lo, p.sq_skip_hi, p.sq_cap = lo, hi, sq[0].numel()
     ws = torch.empty(max(_tn_ws_bytes(M, nr, k1 + k2, nproj) // 4, 1), dtype=torch.float32, device=dev)
     if KernelTimer.active:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
     _lib.call("gnn_gemm_tn_f32", p, out.data_ptr(), ws.data_ptr(), ws.numel() * 4, _lib.stream_handle(dev))
+    if sq is not None:
+        from .train_ops import grad_sq_produced
+
+        grad_sq_produced(dev, (out, n_out, (lo, hi), _sq_blocks(n_out), sq[0], sq[1]))
     if KernelTimer.active:
         e1.record()
         ea = 2 if bf else (4 if a1 is None else a1.element_size())
@@ -237,6 +249,13 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     o += nproj * nr
     dzs = out[o: o + nproj] if nproj else None
     return (dW1, dW2_), db, dW2, dzs
+
+
+@functools.lru_cache(maxsize=64)
+def _sq_blocks(n_out: int) -> int:
+    nb = _lib.c_i32(0)
+    _lib.call("gnn_gemm_tn_sq_blocks", n_out, ctypes.byref(nb))
+    return int(nb.value)
 
 
 def gemm_nt_input(x: torch.Tensor, n: int, **kw):
@@ -424,6 +443,12 @@ class _FusedSAGE(torch.autograd.Function):
         P = ctx.P
         grads = [None] * (3 * L)
         need_x = ctx.needs_input_grad[0]
+        from .train_ops import grad_sq_produced, grad_sq_request
+
+        grad_sq_produced(dz.device, None)
+        # 2 layers: the one TN below writes every parameter's gradient (dzsum[:C], Σ meanᵀ(dlogits),
+        # is not one of them) — Σg² for clip_grad_norm_ comes with its reduce
+        sq = grad_sq_request(dz.device) if L == 2 else None
         g = None
         for l in range(L - 2, -1, -1):
             fo, fi = Wl[l].shape
@@ -455,7 +480,7 @@ class _FusedSAGE(torch.autograd.Function):
                     a_l, im = aggregate(plan, hs[0], _lib.AGG_MEAN, nodew=plan.deg), None
             if l == L - 2:
                 dW, db, dW2, dzs = gemm_tn(fo, a_l, hs[l], dz=dz, proj=P, h=hs[l + 1], hscale=hscale,
-                                           gout=gout, planes=im)
+                                           gout=gout, planes=im, sq=sq, sq_skip=(-2 * C, -C))
                 grads[3 * (L - 1) + 0] = dW2[:C]
                 grads[3 * (L - 1) + 1] = dzs[C:]
                 grads[3 * (L - 1) + 2] = dW2[C:]

@@ -13,6 +13,7 @@ train/eval callers (src/train_gnn.py:67-104, src/analysis/*) work unchanged.
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Optional
 
 import torch
@@ -130,6 +131,9 @@ class GATNet(_StackedConvNet):
         return last(h, edge_index)
 
 
+_RES_FOLD = os.environ.get("GNNMP_RES_FOLD", "1") != "0"  # A/B: 0 = autograd adds the residual's gradient
+
+
 class SAGEResBNNet(nn.Module):
     """SAGE + BatchNorm + residual, optional timestep embedding concatenated to the input.
 
@@ -204,11 +208,14 @@ class SAGEResBNNet(nn.Module):
         fuse = self.fused_bn and self.use_bn and self.training and x.is_cuda
         seeds, ctr = (_fused.dropout_seeds(len(self.convs), self.dropout, h) if fuse else (None, None))
         for li, conv in enumerate(hidden):
-            z = conv(h, edge_index)
             if fuse and _fused.bn_fusable(self.bns[li]):
-                h = _fused.bn_relu_dropout_residual(z, self.res_projs[li](h), self.bns[li], self.dropout,
-                                                    seeds[li], ctr)
+                if isinstance(self.res_projs[li], nn.Identity) and _RES_FOLD:  # the residual's gradient in conv's dx
+                    z, r = conv.forward_with_residual(h, edge_index)
+                else:
+                    z, r = conv(h, edge_index), self.res_projs[li](h)
+                h = _fused.bn_relu_dropout_residual(z, r, self.bns[li], self.dropout, seeds[li], ctr)
                 continue
+            z = conv(h, edge_index)
             if self.use_bn:
                 z = self.bns[li](z)
             z = F.dropout(F.relu(z), p=self.dropout, training=self.training)

@@ -183,6 +183,52 @@ def masked_cross_entropy(logits: torch.Tensor, y: torch.Tensor, mask: torch.Tens
     return _MaskedCE.apply(logits, y, m8, w, inv)
 
 
+# Σg² folded into the gradients' producer (ABI 20).  A ClipAdam registers (partials buffer, step
+# counter) per device; a backward whose ONE weight-gradient TN writes every gradient of the model
+# (the fused 2-layer SAGE) passes them to that TN, whose ordered reduce then also writes the norm
+# partials and the step snapshot, and records what it wrote; the next ClipAdam.step takes the
+# record when its gradients are exactly views of that output — then its launch pair is one launch.
+_GRAD_SQ_REQ: dict = {}   # device -> (partials buffer, step tensor)
+_GRAD_SQ_DONE: dict = {}  # device -> (out, n_out, (skip_lo, skip_hi), nb, partials buffer, step tensor)
+_GRAD_SQ_CAP = 2048       # >= 2 nb + 1 for every TN output (Nr <= 128, K <= 384: nb <= 779)
+
+
+def grad_sq_request(device):
+    """(partials buffer, step tensor) of the ClipAdam on ``device`` that takes Σg² from the producer."""
+    return _GRAD_SQ_REQ.get(device)
+
+
+def grad_sq_produced(device, rec) -> None:
+    """Record (or clear, rec None) the norm partials this step's gradient producer wrote."""
+    if rec is None:
+        _GRAD_SQ_DONE.pop(device, None)
+    else:
+        _GRAD_SQ_DONE[device] = rec
+
+
+def _tiles(rec, ps) -> bool:
+    """The grads of ``ps`` are views of rec's out that tile [0, n_out) minus the skipped range."""
+    out, n_out, (lo, hi) = rec[0], rec[1], rec[2]
+    base, sto, spans = out.data_ptr(), out.untyped_storage().data_ptr(), []
+    for p in ps:
+        g = p.grad  # (AccumulateGrad adopts the backward's views detached: same storage, no _base)
+        if (g is None or g.untyped_storage().data_ptr() != sto or not g.is_contiguous()
+                or g.dtype != torch.float32):
+            return False
+        off = (g.data_ptr() - base) // 4
+        spans.append((off, off + g.numel()))
+    pos = 0
+    for a, b in sorted(spans):
+        if pos == lo:
+            pos = hi
+        if a != pos:
+            return False
+        pos = b
+    if pos == lo:
+        pos = hi
+    return pos == n_out
+
+
 class ClipAdam(torch.optim.Optimizer):
     """``clip_grad_norm_(max_norm)`` + ``Adam`` (L2 weight decay, amsgrad off) in two kernels.
 
@@ -202,6 +248,8 @@ class ClipAdam(torch.optim.Optimizer):
             raise ValueError("ClipAdam clips over one parameter group (as clip_grad_norm_ over model.parameters())")
         self.max_norm = max_norm
         self._ws = None
+        self._sq = None  # norm partials written by the gradients' producer (grad_sq_request)
+        self.last_folded = False  # the last step took them (one launch instead of two)
         self._groups = {}
         self.last_norm = None
 
@@ -240,10 +288,19 @@ class ClipAdam(torch.optim.Optimizer):
             ls = take_loss_sum(dev) if gi == 0 else None
             if ls is not None:
                 g.loss_partial, g.loss_nblk, g.loss_scale, g.loss_out = ls[0].data_ptr(), ls[1], ls[2], ls[3].data_ptr()
+            rec = _GRAD_SQ_DONE.pop(dev, None) if gi == 0 else None
+            self.last_folded = (rec is not None and len(self.param_groups) == 1 and rec[5] is group["step_t"]
+                                and _tiles(rec, ps))
+            if self.last_folded:  # one launch: Σg² came with the gradients
+                g.grad_sq_partial, g.grad_sq_nblk = rec[4].data_ptr(), rec[3]
             _lib.call("gnn_clip_adam_f32", g, group["step_t"].data_ptr(), self.last_norm.data_ptr(),
                       self._ws.data_ptr(), self._ws.numel() * 4, _lib.stream_handle(dev))
-            g.bump_counter = g.loss_partial = g.loss_out = None
-            g.loss_nblk, g.loss_scale = 0, 0.0  # (the partials workspace is held by the capturing CapturedStep)
+            g.bump_counter = g.loss_partial = g.loss_out = g.grad_sq_partial = None
+            g.loss_nblk, g.loss_scale, g.grad_sq_nblk = 0, 0.0, 0  # (the partials workspace is held by the capturing CapturedStep)
+            if len(self.param_groups) == 1:  # the next backward's producer may fold Σg²
+                if self._sq is None:
+                    self._sq = torch.zeros(_GRAD_SQ_CAP, dtype=torch.float32, device=dev)
+                _GRAD_SQ_REQ[dev] = (self._sq, group["step_t"])
         return loss
 
     @staticmethod

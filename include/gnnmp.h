@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 19
+#define GNNMP_ABI_VERSION 20
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -163,6 +163,10 @@ typedef struct {
                              scaled by 1/(1-p) — GCNNet's hidden layers (src/models/gnn.py:29-30) */
   uint64_t seed;
   const int64_t* seed_ptr; /* optional device counter: seed = *seed_ptr * 0x9E3779B97F4A7C15 + seed */
+  const float* addend2;   /* optional (ABI 20, f32 only): a second [rows, F] term added after addend
+                             (ld_add2) — a residual branch's gradient summed in the same store
+                             (SAGE-ResBN's identity residual: dx = meanᵀ(dG_l) + dG_r + dr) */
+  int64_t ld_add2;
 } gnn_agg_params;
 
 /* Generic fp32 aggregation: y[r, 0:F] for r in [0, N). */
@@ -439,6 +443,16 @@ typedef struct {
                                             then holds the bf16-rounded G its MFMAs use) */
   int32_t planes_exp;                    /* HALF_PAIR (ABI 19): the image holds A * 2^planes_exp; dW is
                                             unscaled exactly */
+  float* sq_partial;                     /* optional (ABI 20): the clip + Adam norm partials of `out`, for a
+                                            call whose out holds every gradient of an optimizer group —
+                                            per block b < nb of the ordered reduce (nb =
+                                            gnn_gemm_tn_sq_blocks), over the out[j] with j outside
+                                            [sq_skip_lo, sq_skip_hi): sq_partial[b] = Σ out[j]², sq_partial[nb + b]
+                                            = the count of non-finite out[j]; sq_partial[2 nb] = *sq_step (the
+                                            step count before the update).  Capacity sq_cap floats >= 2 nb + 1;
+                                            hand them to gnn_clip_adam_f32 (gnn_adam_group.grad_sq_partial) */
+  const float* sq_step;
+  int64_t sq_skip_lo, sq_skip_hi, sq_cap;
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).
@@ -447,6 +461,8 @@ typedef struct {
 gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t Kc, int32_t nproj, size_t* bytes);
 gnn_status gnn_gemm_tn_f32(const gnn_gemm_tn_params* p, float* out, void* workspace, size_t workspace_bytes,
                            gnn_stream_t stream);
+/* The number nb of norm partials a call with sq_partial writes for an out of n_out floats (ABI 20). */
+gnn_status gnn_gemm_tn_sq_blocks(int64_t n_out, int32_t* nb);
 /* 1 when the call would read A from p->a_planes (the f32 A operands are then not needed), else 0.
  * Split-image NT shapes (f32 C, the w1/w2 B form, N % 4 == 0, M >= 32; a ReLU, dropout or
  * projection epilogue needs relu + bias):
@@ -558,7 +574,12 @@ typedef struct {
   const float* loss_partial; int32_t loss_nblk; float loss_scale; float* loss_out;
                            /* optional (ABI 18): *loss_out = loss_scale · Σ loss_partial[0 .. loss_nblk)
                               in gnn_masked_ce_f32's order — the loss of a gnn_masked_ce_f32 call made
-                              with loss = NULL, finished in this call's first launch */
+                              with loss = NULL, finished in this call */
+  const float* grad_sq_partial; int32_t grad_sq_nblk;
+                           /* optional (ABI 20): the norm partials a gnn_gemm_tn_f32 call wrote
+                              (gnn_gemm_tn_params.sq_partial, nb = grad_sq_nblk) for EXACTLY these
+                              tensors' gradients, with *step as sq_step: the call then launches only the
+                              clip + Adam kernel (its Σg² pass is folded into the TN's reduce) */
 } gnn_adam_group;
 gnn_status gnn_clip_adam_workspace_size(size_t* bytes);
 gnn_status gnn_clip_adam_f32(const gnn_adam_group* group, float* step, float* norm_out, void* workspace,

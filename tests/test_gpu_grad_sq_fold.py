@@ -1,0 +1,156 @@
+"""GPU: clip_grad_norm_'s Σg² folded into the weight-gradient TN's ordered reduce (ABI 20,
+gnn_gemm_tn_params.sq_partial -> gnn_adam_group.grad_sq_partial): the reduce's norm partials, the
+non-finite counts and the step snapshot; ClipAdam taking them (one launch instead of two) equal to
+torch's clip_grad_norm_ + Adam (src/train_gnn.py:203-206), with GradScaler's skip of non-finite
+steps; the fused 2-layer SAGE step folded vs not folded; no fold when the gradients do not tile
+the TN's output."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _tn(device, M, nr, k1, k2, seed, sq=None, skip=(0, 0), bad=None):
+    from elliptic_gnn_project_amd.fused import gemm_tn
+
+    g = torch.Generator().manual_seed(seed)
+    a1 = torch.randn(M, k1, generator=g).to(device)
+    a2 = torch.randn(M, k2, generator=g).to(device)
+    G = (torch.randn(M, nr, generator=g) * 0.05).to(device)
+    if bad is not None:
+        G[7, 3] = bad
+    (dW1, dW2), db, _, _ = gemm_tn(nr, a1, a2, g=G, sq=sq, sq_skip=skip)
+    return dW1, dW2, db
+
+
+@pytest.mark.parametrize("skip", [(0, 0), (5, 17), (-3, -1)])
+def test_tn_reduce_writes_norm_partials(device, skip):
+    from elliptic_gnn_project_amd import train_ops
+
+    buf = torch.full((train_ops._GRAD_SQ_CAP,), -1.0, device=device)
+    step = torch.tensor([7.0], device=device)
+    dW1, dW2, db = _tn(device, 5000, 64, 40, 24, 1, sq=(buf, step), skip=skip)
+    rec = train_ops._GRAD_SQ_DONE.pop(device)
+    out, n_out, (lo, hi), nb = rec[0], rec[1], rec[2], rec[3]
+    assert n_out == 64 * 64 + 64 and dW1.data_ptr() == out.data_ptr()
+    keep = torch.ones(n_out, dtype=torch.bool, device=device)
+    keep[lo:hi] = False
+    ref = float((out.double()[keep] ** 2).sum())
+    got = float(buf[:nb].double().sum())
+    assert abs(got - ref) <= 1e-6 * ref
+    assert float(buf[nb: 2 * nb].sum()) == 0.0
+    assert float(buf[2 * nb]) == 7.0
+    assert float(buf[2 * nb + 1]) == -1.0  # nothing past the 2 nb + 1 floats
+
+
+def _tiled_params(device, nr, k1, k2, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(*s, generator=g).to(device).requires_grad_(True) for s in ((nr, k1), (nr, k2), (nr,))]
+
+
+@pytest.mark.parametrize("bad", [None, float("inf"), float("nan")])
+@pytest.mark.parametrize("scale", [1.0, 100.0])
+def test_clip_adam_takes_the_tn_partials(device, bad, scale):
+    """ClipAdam over the three gradients one TN call wrote (views of its output): the folded step
+    (last_folded) equals torch's clip_grad_norm_ + Adam on the same gradients — GradScaler's
+    skip when a gradient element is inf / NaN."""
+    from elliptic_gnn_project_amd import train_ops
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+
+    nr, k1, k2 = 32, 48, 16
+    pa, pb = _tiled_params(device, nr, k1, k2, 3), _tiled_params(device, nr, k1, k2, 3)
+    oa = torch.optim.Adam(pa, lr=0.01, weight_decay=1e-4)
+    ob = ClipAdam(pb, lr=0.01, weight_decay=1e-4, max_norm=1.0, skip_nonfinite=True)
+    scaler = torch.amp.GradScaler("cuda", init_scale=1.0, growth_interval=1_000_000)
+    for it in range(3):
+        req = train_ops.grad_sq_request(device) if it > 0 else None
+        dW1, dW2, db = _tn(device, 3000, nr, k1, k2, 10 + it, sq=req, bad=bad if it == 1 else None)
+        grads = [dW1 * scale, dW2 * scale, db * scale] if scale != 1.0 else [dW1, dW2, db]
+        if scale != 1.0 and req is not None:  # scaled copies do not tile the output: no fold
+            train_ops._GRAD_SQ_DONE.pop(device, None)
+        for p, q, gr in zip(pa, pb, grads):
+            p.grad = gr.clone()
+            q.grad = gr
+        scaler.scale(torch.zeros((), device=device))
+        scaler.unscale_(oa)
+        norm = torch.nn.utils.clip_grad_norm_(pa, 1.0)
+        scaler.step(oa)
+        scaler.update(1.0)
+        ob.step()
+        torch.cuda.synchronize()
+        assert ob.last_folded == (it > 0 and scale == 1.0)
+        if torch.isfinite(norm):
+            torch.testing.assert_close(ob.last_norm[0], norm, rtol=1e-5, atol=0)
+        for p, q in zip(pa, pb):
+            torch.testing.assert_close(q, p, rtol=1e-6, atol=1e-7)
+        if it == 1 and bad is not None:
+            assert float(ob.param_groups[0]["step_t"]) == 1.0  # the skipped update left the count
+    assert not train_ops._GRAD_SQ_DONE
+
+
+def _sage(device, seed=11):
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn, build_model
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+    from oracle import pyg_ref
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=6000, num_edges=7000, seed=4),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10)).to(device)
+    torch.manual_seed(seed)
+    model = build_model("sage", data.x.size(1), dict(hidden_dim=128, layers=2, dropout=0.5)).to(device)
+    opt = ClipAdam(model.parameters(), lr=0.01, weight_decay=1e-4, max_norm=1.0)
+    cw = pyg_ref.class_weight(data.y[data.train_mask].cpu())
+    return data, model, opt, _make_loss_fn({}, cw, model, 1, 34), float(data.train_mask.sum())
+
+
+def test_sage_step_folded_matches_unfolded(device):
+    """The fused 2-layer SAGE train step: with the fold (every step after the first) and with the
+    request withdrawn before each backward — same losses, parameters within 1e-6 (the norm's Σ runs
+    in another fixed order), the folded run really folded."""
+    from elliptic_gnn_project_amd import train_ops
+    from elliptic_gnn_project_amd.train_ops import unit_gradient
+
+    runs = []
+    for fold in (True, False):
+        data, model, opt, loss_fn, denom = _sage(device)
+        folded, losses = [], []
+        for it in range(5):
+            model.train()
+            opt.zero_grad(set_to_none=True)
+            if not fold:
+                train_ops._GRAD_SQ_REQ.pop(device, None)
+            torch.manual_seed(100 + it)
+            with loss_fn.target(data.y, data.train_mask, denom):
+                logits = model(data.x, data.edge_index)
+            loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
+            loss.backward(unit_gradient(device))
+            opt.step()
+            folded.append(opt.last_folded)
+            losses.append(float(loss))
+        runs.append((model, folded, losses, float(opt.last_norm[0])))
+    (ma, fa, la, na), (mb, fb, lb, nb) = runs
+    assert fa == [False, True, True, True, True] and not any(fb)
+    for x, y in zip(la, lb):
+        assert abs(x - y) <= 1e-6 * abs(y)
+    assert abs(na - nb) <= 1e-6 * nb
+    for (k, a), b in zip(ma.state_dict().items(), mb.state_dict().values()):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7, msg=k)
+
+
+def test_no_fold_when_the_optimizer_holds_other_parameters(device):
+    """An optimizer over the model's parameters plus one more: its gradients do not tile the TN's
+    output, so the Σg² pass runs — and the step is still clip + Adam over all of them."""
+    from elliptic_gnn_project_amd.train_ops import ClipAdam, unit_gradient
+
+    data, model, _, loss_fn, denom = _sage(device)
+    extra = torch.nn.Parameter(torch.ones(3, device=device))
+    opt = ClipAdam(list(model.parameters()) + [extra], lr=0.01, max_norm=1.0)
+    for it in range(3):
+        model.train()
+        opt.zero_grad(set_to_none=True)
+        with loss_fn.target(data.y, data.train_mask, denom):
+            logits = model(data.x, data.edge_index)
+        loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom) + extra.sum() * 0.1
+        loss.backward(unit_gradient(device))
+        opt.step()
+        assert not opt.last_folded

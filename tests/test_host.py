@@ -144,7 +144,8 @@ STRUCTS = {
     "gnn_graph": ("GnnGraph", ["num_nodes", "num_slots", "rowptr", "col", "colptr", "row", "csc2csr",
                                "csr_split", "csc_split"]),
     "gnn_agg_params": ("GnnAggParams", ["mode", "transpose", "nodew", "ew", "heads", "addend", "ld_add", "bias",
-                                        "relu", "part", "part_bytes", "dropout_p", "seed", "seed_ptr"]),
+                                        "relu", "part", "part_bytes", "dropout_p", "seed", "seed_ptr",
+                                        "addend2", "ld_add2"]),
     "gnn_gemm_nt_params": ("GnnGemmNTParams", ["M", "N", "a1", "lda1", "k1", "a2", "lda2", "k2", "bt", "ldb",
                                                "w1", "w2", "ldw1", "ldw2", "c",
                                                "ldc", "bias", "relu", "dropout_p", "seed", "seed_ptr", "proj",
@@ -156,12 +157,13 @@ STRUCTS = {
     "gnn_adam_tensor": ("GnnAdamTensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel"]),
     "gnn_adam_group": ("GnnAdamGroup", ["num_tensors", "lr", "beta1", "beta2", "eps", "weight_decay", "max_norm",
                                         "tensors", "skip_nonfinite", "bump_counter", "loss_partial", "loss_nblk",
-                                        "loss_scale", "loss_out"]),
+                                        "loss_scale", "loss_out", "grad_sq_partial", "grad_sq_nblk"]),
     "gnn_gemm_tn_params": ("GnnGemmTNParams", ["M", "Nr", "g", "ldg", "dz", "lddz", "proj", "nproj", "h", "ldh",
                                                "hscale", "gout", "ldgout", "a1", "lda1", "k1", "a2", "lda2", "k2",
                                                "math", "a_dtype", "h_dtype", "a_planes", "planes_ld",
                                                "planes_stride", "planes_col2", "planes_format", "g_dtype",
-                                               "planes_exp"]),
+                                               "planes_exp", "sq_partial", "sq_step", "sq_skip_lo", "sq_skip_hi",
+                                               "sq_cap"]),
 }
 
 
