@@ -24,7 +24,7 @@ from . import _lib
 from .aggregation import (aggregate, colsum, gat_attention, gcn_aggregate, masked_gat_attention, masked_gcn_aggregate,
                           masked_mean_aggregate, mean_aggregate)
 from .graph import GraphPlan, get_plan
-from .linear import Linear, linear, linear2
+from .linear import Linear, linear, linear2, linear_stacked
 
 __all__ = ["SAGEConv", "GCNConv", "GATConv"]
 
@@ -113,7 +113,7 @@ class _SAGEAggregateFirst(torch.autograd.Function):
             (dWl, dWr), db, _, _ = gemm_tn(wl.size(0), agg, x, g=dy)
         if need[0]:
             fi = wl.size(1)
-            wt = torch.cat([wl, wr], dim=1).t().contiguous()  # [2·F_in, F_out]: Linear-weight form
+            wt = torch.cat([wl.t(), wr.t()], dim=0)  # [2·F_in, F_out]: Linear-weight form, one copy kernel
             d = gemm_nt(dy, None, 2 * fi, w1=wt)
             dx = aggregate(plan, d[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, addend=d[:, fi:],
                            addend2=dr if (ctx.res and dr is not None) else None)
@@ -147,6 +147,20 @@ class SAGEConv(nn.Module):
         self.order = order
         self.lin_l = Linear(self.in_channels, self.out_channels, bias=bias)
         self.lin_r = Linear(self.in_channels, self.out_channels, bias=False)
+        self._tie()
+
+    def _tie(self) -> None:
+        # transform first: lin_l.weight and lin_r.weight laid out as the halves of ONE [2·F_out,
+        # F_in] buffer, the stacked weight of its GEMM (no per-step torch.cat; fused.tie_output_weights)
+        if self._transform_first():
+            from .fused import tie_output_weights
+
+            tie_output_weights(self)
+
+    def _apply(self, fn, recurse=True):
+        out = super()._apply(fn, recurse)
+        self._tie()  # .to() / .cuda() / .float() give new tensors: lay them out again
+        return out
 
     def reset_parameters(self) -> None:
         self.lin_l.reset_parameters()
@@ -179,8 +193,7 @@ class SAGEConv(nn.Module):
             return linear2(agg, x, self.lin_l.weight, self.lin_r.weight, self.lin_l.bias)
         if self._transform_first():
             fo = self.out_channels
-            w = torch.cat([self.lin_l.weight, self.lin_r.weight], dim=0)
-            y = linear(x, w)  # [N, 2*F_out]: MFMA GEMM (K7)
+            y = linear_stacked(x, self.lin_l.weight, self.lin_r.weight)  # [N, 2*F_out]: MFMA GEMM (K7)
             plan = get_plan(edge_index, x.size(0), _lib.LOOPS_KEEP)
             return _MeanAggRootBias.apply(y, self.lin_l.bias, plan, fo)
         if self._aggregate_first_ok(x):

@@ -751,7 +751,11 @@ def tie_output_weights(conv) -> None:
 
 def _tied_buffer(conv):
     """The [2C, F] tensor both output weights view (the tie of tie_output_weights), or None."""
-    wl, wr = conv.lin_l.weight, conv.lin_r.weight
+    return _tied_buffer_of(conv.lin_l.weight, conv.lin_r.weight)
+
+
+def _tied_buffer_of(wl, wr):
+    """[wl ; wr] as one [2C, F] tensor when wr directly follows wl in one storage, else None."""
     C = wl.size(0)
     if (wl.shape != wr.shape or not wl.is_contiguous() or not wr.is_contiguous() or wl.device != wr.device
             or wl.dtype != wr.dtype or wl.untyped_storage().data_ptr() != wr.untyped_storage().data_ptr()

@@ -65,6 +65,50 @@ class _MfmaLinear(torch.autograd.Function):
                 da2, dW2 if need[4] else None)
 
 
+class _StackedLinear(torch.autograd.Function):
+    """x · [W_l ; W_r]ᵀ — SAGEConv's transform-first GEMM (conv.py) — from the two weights with no
+    per-step torch.cat when they are the halves of one buffer (fused.tie_output_weights): the same
+    NT / TN kernels as _MfmaLinear over the stacked weight, whose TN output rows are the two
+    weights' gradients (views, adopted by autograd)."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, x, wl, wr):
+        from .fused import _tied_buffer_of
+
+        w = _tied_buffer_of(wl, wr)
+        if w is None:
+            w = torch.cat([wl, wr], dim=0)
+        x = _rows(x)
+        y = gemm_nt_input(x, w.size(0), w1=w)
+        ctx.save_for_backward(x, w)
+        ctx.fo = wl.size(0)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = _rows(dy)
+        need = ctx.needs_input_grad
+        dWl = dWr = dx = None
+        if need[1] or need[2]:
+            (dW, _), _, _, _ = gemm_tn_input(w.size(0), x, dy)
+            dWl, dWr = dW[:ctx.fo], dW[ctx.fo:]
+        if need[0]:
+            dx = gemm_nt(dy, w, w.size(1))
+        return dx, dWl if need[1] else None, dWr if need[2] else None
+
+
+def linear_stacked(x: torch.Tensor, wl: torch.Tensor, wr: torch.Tensor) -> torch.Tensor:
+    """``x · [wl ; wr]ᵀ`` (= F.linear(x, torch.cat([wl, wr]))) on the MFMA kernels."""
+    if not x.is_cuda:
+        raise RuntimeError("elliptic_gnn_project_amd.linear_stacked runs on the HIP device only")
+    if x.dim() != 2 or x.size(0) == 0 or wl.shape != wr.shape or not fits(wl.size(1), 2 * wl.size(0)):
+        return F.linear(x, torch.cat([wl, wr], dim=0))
+    return _StackedLinear.apply(x, wl, wr)
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """``F.linear`` on the MFMA kernels (HIP device, fp32 compute, 2-D input)."""
     if not x.is_cuda:
