@@ -121,6 +121,7 @@ struct AggArgs {
   // arithmetic) in the narrow kernel's epilogue: dlogits into ce_dl, per-256-row loss partials
   const int64_t* ce_y; const uint8_t* ce_mask; const float* ce_w; float ce_inv;
   float* ce_dl; int64_t ce_ldd; float* ce_part;
+  float* ce_u; int64_t ce_ldu;  // optional: dl / max(deg, 1) per row (the transposed mean's per-slot term)
 };
 
 __device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
@@ -742,6 +743,10 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   const int w = threadIdx.x >> 6;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + w) * 64;
   float lg[4] = {0.f, 0.f, 0.f, 0.f};  // CE: the row's logits
+  int64_t ce_t = -1;                   // CE: its label, mask byte and the class weights (prefetched)
+  float ce_deg = 1.0f;                 // CE: max(deg, 1) of the row (the u output's divisor)
+  uint8_t ce_m = 0;
+  float ce_w[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (!CE) {
     if (r0 >= a.nrows) return;  // wave-uniform; no block barriers below
   }
@@ -771,6 +776,13 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   if (a.bias) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) pbias[f] = a.bias[f < F ? f : 0];
+  }
+  if constexpr (CE) {  // the CE's row operands too (label, mask, the C class weights): no round trip after the sum
+    ce_deg = pdeg;
+    ce_t = a.ce_y[rr];
+    ce_m = a.ce_mask[rr];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) ce_w[c] = a.ce_w[c < F ? c : 0];
   }
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float* buf = sv[w];
@@ -874,9 +886,16 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
     const int C = a.F;
     float l = 0.f;
     if (r < a.nrows) {  // masked_ce_kernel<C>: loss_r = -w[y]·log_softmax[y], dl = w[y]/n·(softmax - onehot)
-      const int64_t tg = a.ce_y[r];
-      const bool on = a.ce_mask[r] != 0 && tg >= 0 && tg < C;
-      l = masked_ce_row<4>(lg, C, tg, on, on ? a.ce_w[tg] : 0.f, a.ce_inv, a.ce_dl + r * a.ce_ldd);
+      const int64_t tg = ce_t;
+      const bool on = ce_m != 0 && tg >= 0 && tg < C;
+      const float wt = tg == 0 ? ce_w[0] : tg == 1 ? ce_w[1] : tg == 2 ? ce_w[2] : ce_w[3];
+      float dlv[4] = {0.f, 0.f, 0.f, 0.f};
+      l = masked_ce_row<4>(lg, C, tg, on, on ? wt : 0.f, a.ce_inv, a.ce_dl + r * a.ce_ldd, dlv);
+      if (a.ce_u) {  // MEAN_BWD's v / max(deg, 1) of this row, the same division (deg is MEAN's nodew)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c < C) a.ce_u[r * a.ce_ldu + c] = dlv[c] / ce_deg;
+      }
     }
     __shared__ float cesh[4];
     for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);  // train_ops.hip block_sum, same order
@@ -1505,8 +1524,9 @@ extern "C" gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, f
 extern "C" gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* deg, const float* z, int64_t ldz,
                                                int32_t C, const float* bias, float* logits, int64_t ldo,
                                                const int64_t* y, const uint8_t* mask, const float* class_w,
-                                               float inv_denom, float* dlogits, int64_t ld_d, float* loss,
-                                               void* workspace, size_t workspace_bytes, gnn_stream_t stream) {
+                                               float inv_denom, float* dlogits, int64_t ld_d, float* u, int64_t ldu,
+                                               float* loss, void* workspace, size_t workspace_bytes,
+                                               gnn_stream_t stream) {
   const char* fn = __func__;
   if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or deg");
   if (C < 1 || C > 4 || ldz < 2 * C || ldo < C || ld_d < C) return fail(GNN_ERR_INVALID_ARG, fn, "needs 1 <= C <= 4, ldz >= 2C");
@@ -1528,6 +1548,8 @@ extern "C" gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* 
   a.nrows = N; a.F = C;
   a.ce_y = y; a.ce_mask = mask; a.ce_w = class_w; a.ce_inv = inv_denom; a.ce_dl = dlogits; a.ce_ldd = ld_d;
   a.ce_part = partial;
+  if (u && ldu < C) return fail(GNN_ERR_INVALID_ARG, fn, "ldu < C");
+  a.ce_u = u; a.ce_ldu = ldu;
   if (C <= 2) agg_narrow_lds_kernel<GNN_AGG_MEAN, 2, 256, true, true><<<(unsigned)nblk, 256, 0, st>>>(a);
   else agg_narrow_lds_kernel<GNN_AGG_MEAN, 4, 256, true, true><<<(unsigned)nblk, 256, 0, st>>>(a);
   const gnn_status s = hip_check(hipGetLastError(), fn);

@@ -110,7 +110,7 @@ __device__ __forceinline__ float ce_logf(float x) {
 
 template <int CM>
 __device__ __forceinline__ float masked_ce_row(float (&v)[CM], int C, int64_t t, bool on, float wt, float inv,
-                                               float* __restrict__ dl) {
+                                               float* __restrict__ dl, float* dlv = nullptr) {
 #pragma clang fp contract(off)
   float mx = -INFINITY;
 #pragma unroll
@@ -128,7 +128,11 @@ __device__ __forceinline__ float masked_ce_row(float (&v)[CM], int C, int64_t t,
   const float g = wt * inv, rs = 1.0f / s;
 #pragma unroll
   for (int c = 0; c < CM; ++c)
-    if (c < C) dl[c] = on ? g * fmaf(v[c], rs, c == t ? -1.f : 0.f) : 0.f;
+    if (c < C) {
+      const float d = on ? g * fmaf(v[c], rs, c == t ? -1.f : 0.f) : 0.f;
+      dl[c] = d;
+      if (dlv) dlv[c] = d;  // (the caller's copy: aggregate.hip's per-row term of the transposed mean)
+    }
   return l;
 }
 

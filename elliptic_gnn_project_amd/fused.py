@@ -434,7 +434,11 @@ class _FusedSAGE(torch.autograd.Function):
         if (buf is not None and buf.shape == (N, 2 * C) and dlogits.stride() == (2 * C, 1)
                 and dlogits.data_ptr() == buf.data_ptr() + C * buf.element_size()):
             dz = buf
-            aggregate(plan, dlogits, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dz[:, :C])
+            u = getattr(dlogits, "_gnnmp_u", None)  # dlogits / max(deg, 1) from the forward's CE launch
+            if u is not None:  # meanᵀ as a plain CSC sum: MEAN_BWD's per-slot terms precomputed, same bits
+                aggregate(plan, u, _lib.AGG_SUM, transpose=True, out=dz[:, :C])
+            else:
+                aggregate(plan, dlogits, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dz[:, :C])
         else:
             dlogits = dlogits.contiguous()
             dz = torch.empty((N, 2 * C), dtype=torch.float32, device=dlogits.device)
@@ -557,7 +561,9 @@ class _FusedGCN(torch.autograd.Function):
         scale = 1.0 / (1.0 - p) if p > 0 else 1.0
         dinv = plan.dinv
         grads = [None] * (2 * L)
-        g = dlogits.contiguous()
+        # the fused CE's dlogits is the right half of its [N, 2C] buffer: read in place (row stride 2C)
+        g = dlogits if (dlogits.dim() == 2 and dlogits.stride(1) == 1 and dlogits.stride(0) >= dlogits.size(1)) \
+            else dlogits.contiguous()
         dx = None
         for l in range(L - 1, -1, -1):
             dy = aggregate(plan, g, _lib.AGG_GCN, transpose=True, nodew=dinv)

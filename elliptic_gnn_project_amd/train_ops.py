@@ -88,6 +88,7 @@ class _PrecomputedCE(torch.autograd.Function):
         ctx.save_for_backward(buf)
         ctx.C = buf.size(1) // 2
         ctx.ws = ws  # the loss partials (a deferred loss reads them at the step's end)
+        ctx.u = getattr(buf, "_gnnmp_u", None)  # dlogits / max(deg, 1), written by the same launch
         return loss
 
     @staticmethod
@@ -97,6 +98,7 @@ class _PrecomputedCE(torch.autograd.Function):
         ones = _ONES.get(g.device)
         if ones is not None and g.data_ptr() == ones.data_ptr():
             dl._gnnmp_dz = buf
+            dl._gnnmp_u = ctx.u
             return dl, None
         return dl * g, None
 
@@ -150,14 +152,16 @@ def sage_out_mean_ce(plan, z: torch.Tensor, C: int, bias, target):
     N, dev = z.size(0), z.device
     logits = torch.empty((N, C), dtype=torch.float32, device=dev)
     buf = torch.empty((N, 2 * C), dtype=torch.float32, device=dev)
+    u = torch.empty((N, C), dtype=torch.float32, device=dev)  # dlogits / max(deg, 1): meanᵀ as a plain sum
     loss = torch.empty((), dtype=torch.float32, device=dev)
     ws = _ws(_ce_ws_bytes(N), dev)
     nblk = max(1, -(-N // 256))
     deferred = defer_loss_sum(dev, ws, nblk, inv, loss)  # captured step with defer_loss: at its end
     _lib.call("gnn_sage_out_mean_ce_f32", plan.c_graph, plan.deg.data_ptr(), z.data_ptr(), int(z.stride(0)), int(C),
               _lib.ptr(bias), logits.data_ptr(), C, y.data_ptr(), m8.data_ptr(), w.data_ptr(), float(inv),
-              buf.data_ptr() + C * 4, 2 * C, None if deferred else loss.data_ptr(), ws.data_ptr(), ws.numel() * 4,
-              _lib.stream_handle(dev))
+              buf.data_ptr() + C * 4, 2 * C, u.data_ptr(), C, None if deferred else loss.data_ptr(), ws.data_ptr(),
+              ws.numel() * 4, _lib.stream_handle(dev))
+    buf._gnnmp_u = u
     return logits, (key, loss, buf, ws)
 
 

@@ -241,12 +241,15 @@ typedef enum {
  * partials in `workspace`, `loss` = Σ partials · inv_denom or left to gnn_masked_ce_finish /
  * gnn_adam_group.loss_partial when NULL), bit for bit as the two calls produce them.  Replaces
  * the F = 2 aggregation + the CE launch of the training step (src/train_gnn.py:192-199).
- * 1 <= C <= 4, ldz >= 2C; workspace: gnn_masked_ce_workspace_size(num_nodes). */
+ * 1 <= C <= 4, ldz >= 2C; workspace: gnn_masked_ce_workspace_size(num_nodes).  u (optional, ABI 20,
+ * [N, C], ldu >= C): dlogits / max(deg, 1) per row — the transposed mean's per-slot term, so the
+ * backward's meanᵀ(dlogits) is a plain CSC sum of u (gnn_aggregate_f32 SUM, transpose), bit for bit
+ * the MEAN_BWD result, without the per-slot degree gather and division. */
 gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* deg, const float* z, int64_t ldz, int32_t C,
                                     const float* bias, float* logits, int64_t ldo, const int64_t* y,
                                     const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
-                                    int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,
-                                    gnn_stream_t stream);
+                                    int64_t ld_d, float* u, int64_t ldu, float* loss, void* workspace,
+                                    size_t workspace_bytes, gnn_stream_t stream);
 
 /* Named forms of the above (what an FFI binding of SAGEConv would call). */
 gnn_status gnn_sage_mean_fwd_f32(const gnn_graph* g, const float* deg, const float* x, int64_t ldx,

@@ -44,6 +44,11 @@ def test_out_mean_ce_equals_two_launches(device, n, e, C):
     assert torch.equal(logits, ref_logits.detach())
     assert torch.equal(ce[1], ref_loss.detach())  # the loss: same partials, same finish
     assert torch.equal(ce[2][:, C:], ref_logits.grad)  # dlogits (unit upstream gradient)
+    # u = dlogits / max(deg, 1): its CSC sum is MEAN_BWD's meanᵀ(dlogits), bit for bit
+    u = ce[2]._gnnmp_u
+    assert torch.equal(u, ref_logits.grad / plan.deg.clamp(min=1.0).view(N, 1))
+    assert torch.equal(aggregate(plan, u, _lib.AGG_SUM, transpose=True),
+                       aggregate(plan, ref_logits.grad, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg))
     # vs the float64 oracle of the reference's loss (src/train_gnn.py:159-175)
     lo = pyg_ref.ce_loss(ref_logits.detach().double().cpu()[mask.cpu()], y.cpu()[mask.cpu()], w.double().cpu())
     assert abs(float(ce[1]) - float(lo)) <= 1e-5 * max(1.0, abs(float(lo)))
