@@ -196,6 +196,27 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
     return;
   }
   adam_stage(tb, L);
+  // this block's slice of the flattened parameters; its first pass's loads are issued here, before
+  // the norm's reduction (they do not depend on it: one round trip less on the launch's path)
+  const int64_t total = L.off[tb.n];
+  const int64_t per = (total + kAdamBlocks - 1) / kAdamBlocks;  // (an extra loss block: no slice)
+  const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(total, e0 + per);
+  const bool has = e0 < e1;  // block-uniform
+  int j[kAdamUnroll];
+  int64_t i[kAdamUnroll];
+  bool ok[kAdamUnroll];
+  float g0[kAdamUnroll], p[kAdamUnroll], m0[kAdamUnroll], v0[kAdamUnroll];
+  auto load_pass = [&](int64_t e) __attribute__((always_inline)) {
+    adam_locate(L, tb.n, e, e1, j, i, ok);
+#pragma unroll
+    for (int u = 0; u < kAdamUnroll; ++u) {  // every load of the pass issued first
+      g0[u] = L.g[j[u]][i[u]];
+      p[u] = L.p[j[u]][i[u]];
+      m0[u] = L.m[j[u]][i[u]];
+      v0[u] = L.v[j[u]][i[u]];
+    }
+  };
+  if (has) load_pass(e0 + threadIdx.x);
   {
     float tot = 0.f, nf = 0.f;
     constexpr int U = 4;  // every load of the first U·256 partials issued before the sums (clamped, no branch)
@@ -253,22 +274,8 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
   const float neg_step = (float)(-lr / bc1), bc2s = (float)sqrt(bc2);
   const float b2 = (float)beta2, omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
   const float epsf = (float)eps, wdf = (float)wd;
-  const int64_t total = L.off[tb.n];
-  const int64_t per = (total + kAdamBlocks - 1) / kAdamBlocks;  // (an extra loss block: no slice)
-  const int64_t e0 = (int64_t)blockIdx.x * per, e1 = min(total, e0 + per);
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += kAdamUnroll * kAdamThreads) {
-    int j[kAdamUnroll];
-    int64_t i[kAdamUnroll];
-    bool ok[kAdamUnroll];
-    adam_locate(L, tb.n, e, e1, j, i, ok);
-    float g0[kAdamUnroll], p[kAdamUnroll], m0[kAdamUnroll], v0[kAdamUnroll];
-#pragma unroll
-    for (int u = 0; u < kAdamUnroll; ++u) {  // every load of the pass issued first
-      g0[u] = L.g[j[u]][i[u]];
-      p[u] = L.p[j[u]][i[u]];
-      m0[u] = L.m[j[u]][i[u]];
-      v0[u] = L.v[j[u]][i[u]];
-    }
+  for (int64_t e = e0 + threadIdx.x; has && e < e1; e += kAdamUnroll * kAdamThreads) {
+    if (e != e0 + threadIdx.x) load_pass(e);  // (the first pass was loaded before the reduction)
 #pragma unroll
     for (int u = 0; u < kAdamUnroll; ++u) {
       if (!ok[u]) continue;
