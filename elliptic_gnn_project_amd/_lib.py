@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["GNNMP_LIB"]) if os.environ.get("GNNMP_LIB") else PKG_DIR / "libgnnmp.so"  # (GNNMP_LIB: A/B builds)
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -229,7 +229,8 @@ SIGNATURES = {
     "gnn_sage_mean_fwd_h2": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_i64, c_i64, c_i32,
-         c_ptr, c_i64, ctypes.c_float, ctypes.c_uint64, c_ptr, ctypes.POINTER(GnnGemmNTParams), c_ptr],
+         c_ptr, c_i64, ctypes.c_float, ctypes.c_uint64, c_ptr, ctypes.POINTER(GnnGemmNTParams),
+         ctypes.POINTER(GnnSplit), c_ptr],
     ),
     "gnn_sage_out_mean_ce_f32": (
         ctypes.c_int,

@@ -117,6 +117,12 @@ struct AggArgs {
   // K1 of the half-pair path may also carry the consuming NT's B-image prep (gnn_sage_mean_fwd_h2
   // prep_b): hp.blocks extra blocks at the front of the grid run ws_prep_h2_body, one per k-step
   H2Prep hp;
+  // K1 of the half-pair path, hub form (gnn_sage_mean_fwd_h2 hub): rows with deg > hub_deg
+  // (hubs[0, nhub)) have no slots in the main pass's ptr / nbr; one block each (nhub extra blocks
+  // after the prep blocks) walks the full row fptr / fnbr with its 4 waves and writes it
+  int32_t nhub; float hub_deg; const int32_t* hubs;
+  // ... and optionally balanced main-pass waves: wave k takes rows [wstart[k], wstart[k + 1]) (<= 64)
+  const int32_t* wstart;
   // gnn_sage_out_mean_ce_f32: the masked weighted CE of the finished rows (gnn_masked_ce_f32's
   // arithmetic) in the narrow kernel's epilogue: dlogits into ce_dl, per-256-row loss partials
   const int64_t* ce_y; const uint8_t* ce_mask; const float* ce_w; float ce_inv;
@@ -481,20 +487,111 @@ __global__ __launch_bounds__(256) void agg_flat_kernel(AggArgs a, int32_t rpg) {
 // v_readlane) and the next U neighbour ids are prefetched while the current U rows load.
 // PLN: y is written as a split image, no split partials: 3 = split-bf16 planes (hi / mid / lo
 // bf16), 2 = half-pair planes (hi / lo f16, gemm_common.hpp split_h2_pair); VEC even.
-template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, int PLN = 0>  // BF: x and y hold bf16 (no split partials)
+// One hub row of K1's half-pair store, by a whole block: wave w sums the row's slot groups
+// w, w + 4, w + 8, ... (U slots each, in slot order, the next group's ids loaded behind the
+// current rows), then wave 0 adds waves 1..3 in order, divides by max(deg, 1) and writes the
+// half-pair planes (zero padding columns) as agg_wave_kernel's flush does.  A strong-scaling
+// shard's degree-196 row walked by one wave was its K1's tail (profiles/r47_shards.txt).
+template <int VEC, int NCH>
+__device__ __forceinline__ void k1_hub_row(const AggArgs& a, int32_t r) {
+  constexpr int U = 8, W = 4;
+  __shared__ float red[(W - 1) * NCH * VEC * 64];  // [wave - 1][chunk][q][lane]: conflict-free
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int32_t beg = a.fptr[r], end = a.fptr[r + 1];  // end > beg: deg > hub_deg >= 1
+  const int nchunk = a.F / VEC;
+  int coff[NCH];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + 64 * i;
+    coff[i] = (c < nchunk ? c : 0) * VEC;
+  }
+  float acc[NCH][VEC];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) acc[i][q] = 0.0f;
+  int32_t n[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) n[u] = __builtin_amdgcn_readfirstlane(a.fnbr[min(beg + w * U + u, end - 1)]);
+  for (int32_t s = beg + w * U; s < end; s += W * U) {
+    float v[U][NCH][VEC];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) vload<VEC>(a.x + (int64_t)n[u] * a.ldx + coff[i], v[u][i]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) n[u] = __builtin_amdgcn_readfirstlane(a.fnbr[min(s + W * U + u, end - 1)]);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (s + u < end) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i)
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) acc[i][q] += v[u][i][q];
+      }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) red[(((w - 1) * NCH + i) * VEC + q) * 64 + lane] = acc[i][q];
+  }
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int ww = 0; ww < W - 1; ++ww)
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[i][q] += red[((ww * NCH + i) * VEC + q) * 64 + lane];
+  const float d = fmaxf(a.nodew[r], 1.0f);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + 64 * i;
+    if (!(c < nchunk || c * VEC < a.ywidth)) continue;
+    uint32_t wd[VEC / 2][2];
+#pragma unroll
+    for (int q = 0; q < VEC / 2; ++q) {
+      const float t0 = c < nchunk ? acc[i][2 * q] / d : 0.0f;
+      const float t1 = c < nchunk ? acc[i][2 * q + 1] / d : 0.0f;
+      split_h2_pair(t0 * a.yscale, t1 * a.yscale, wd[q][0], wd[q][1]);
+    }
+    uint16_t* dst = a.yp + (int64_t)r * a.ldy + c * VEC;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      if constexpr (VEC == 4) *reinterpret_cast<uint2*>(dst + p * a.yps) = make_uint2(wd[0][p], wd[1][p]);
+      else *reinterpret_cast<uint32_t*>(dst + p * a.yps) = wd[0][p];
+    }
+  }
+}
+
+// PCPP: columns per pass of the B prep riding along (ws_prep_h2_body CPP)
+template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, int PLN = 0, int PCPP = 1>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
   if constexpr (PLN == 2) {  // the NT's B prep rides along (blocks [0, hp.blocks), launched first)
     if ((int)blockIdx.x < a.hp.blocks) {
-      ws_prep_h2_body<256, 1>(a.hp, (int)blockIdx.x);
+      ws_prep_h2_body<256, PCPP>(a.hp, (int)blockIdx.x);
+      return;
+    }
+    if ((int)blockIdx.x < a.hp.blocks + a.nhub) {  // the hub rows, also launched early
+      k1_hub_row<VEC, NCH>(a, a.hubs[(int)blockIdx.x - a.hp.blocks]);
       return;
     }
   }
   const int lane = threadIdx.x & 63;
-  const int64_t bid = (int64_t)blockIdx.x - (PLN == 2 ? a.hp.blocks : 0);
+  const int64_t bid = (int64_t)blockIdx.x - (PLN == 2 ? a.hp.blocks + a.nhub : 0);
   const int64_t wave = (bid * 256 + threadIdx.x) >> 6;
-  const int64_t r0 = wave * rpg;
-  if (r0 >= a.nrows) return;
-  const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
+  int64_t r0 = wave * rpg;
+  int nrow;
+  if (PLN == 2 && a.wstart) {  // balanced waves (rpg = the wave count)
+    if (wave >= rpg) return;
+    r0 = __builtin_amdgcn_readfirstlane(a.wstart[wave]);
+    nrow = __builtin_amdgcn_readfirstlane(a.wstart[wave + 1]) - (int)r0;
+    if (nrow <= 0) return;
+  } else {
+    if (r0 >= a.nrows) return;
+    nrow = (int)min((int64_t)rpg, a.nrows - r0);
+  }
   const int nchunk = a.F / VEC;
   const int32_t myptr = a.ptr[r0 + min(lane, nrow)];
   const int32_t myrow = a.order ? a.order[r0 + min(lane, nrow - 1)] : (int32_t)(r0 + min(lane, nrow - 1));
@@ -525,7 +622,7 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
       const int c = lane + 64 * i;
       if constexpr (PLN != 0) {
         static_assert(VEC % 2 == 0, "planes are written in column pairs");
-        if (c < nchunk || c * VEC < a.ywidth) {
+        if ((PLN != 2 || !(d > a.hub_deg) || a.nhub == 0) && (c < nchunk || c * VEC < a.ywidth)) {  // (hub rows: k1_hub_row)
           uint32_t w[VEC / 2][3];
 #pragma unroll
           for (int q = 0; q < VEC / 2; ++q) {
@@ -1450,7 +1547,8 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
                                       void* img, int64_t ld, int64_t plane_stride, int64_t width, gnn_stream_t stream,
                                       const char* fn, uint32_t* keep_mask = nullptr, int64_t mask_cols = 0,
                                       float dropout_p = 0.f, uint64_t seed = 0, const uint64_t* seed_ptr = nullptr,
-                                      const gnn_gemm_nt_params* prep_b = nullptr, int32_t scale_exp = 0) {
+                                      const gnn_gemm_nt_params* prep_b = nullptr, int32_t scale_exp = 0,
+                                      const gnn_split* hub = nullptr) {
   if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or deg");
   if (scale_exp < -100 || scale_exp > 100) return fail(GNN_ERR_INVALID_ARG, fn, "scale_exp outside [-100, 100]");
   if (F < 2 || ldx < F || width < F || width > ld || plane_stride < g->num_nodes * ld)
@@ -1492,11 +1590,31 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
   const int vec = v4 ? 4 : 2;
   if (!v2 || F / vec <= 32 || ceil_div(width, vec) > 128)
     return fail(GNN_ERR_UNSUPPORTED, fn, "needs even F, 32 < F / vec, width / vec <= 128 and aligned rows");
+  if (hub && hub->num_long > 0) {  // the hub form: hub rows on blocks of their own
+    if (PLN != 2 || hub->order || hub->piece0 || !hub->ptr || !hub->long_seg || hub->seg_len < 1 ||
+        hub->num_long > g->num_nodes || (!hub->nbr && g->num_slots > 0))
+      return fail(GNN_ERR_INVALID_ARG, fn, "hub: a natural-order split (order, piece0 NULL) with ptr, nbr, long_seg, seg_len >= 1");
+    a.fptr = g->rowptr; a.fnbr = g->col;
+    a.ptr = hub->ptr; a.nbr = hub->nbr;
+    a.hubs = hub->long_seg; a.nhub = (int32_t)hub->num_long; a.hub_deg = (float)hub->seg_len;
+  }
+  if (hub && hub->piece_seg) {  // balanced main-pass waves (validated by the plan that built them)
+    if (PLN != 2 || hub->order || hub->piece0 || hub->num_pieces < 1 || hub->num_pieces > g->num_nodes)
+      return fail(GNN_ERR_INVALID_ARG, fn, "hub wave starts: 1 <= num_pieces <= num_nodes, natural order");
+    a.wstart = hub->piece_seg;
+  }
   if (a.nrows == 0) return GNN_OK;
-  const int rpw = 16;
-  const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256) + (unsigned)a.hp.blocks;
+  const int rpw = a.wstart ? (int)hub->num_pieces : 16;  // (balanced: the kernel's rpg is the wave count)
+  const int64_t nwaves = a.wstart ? hub->num_pieces : ceil_div(a.nrows, 16);
+  const unsigned wblocks = (unsigned)ceil_div(nwaves * 64, 256) + (unsigned)a.hp.blocks + (unsigned)a.nhub;
   hipStream_t st = (hipStream_t)stream;
-  if (vec == 4 && ceil_div(width, 4) <= 64)  // one pass per row (e.g. a 168-wide padded x: 42 lanes)
+  // the riding B prep's columns per pass: its 4·32/CPP dependent load rounds are K1's critical
+  // path on a short gather (a strong-scaling shard: CPP 4 took 7 us off the 8- and 4-way shard
+  // steps), while on a long one CPP 4's registers cost the gather occupancy (+4 us on the full
+  // graph; profiles/r50_k1_hub.txt)
+  if (vec == 4 && ceil_div(width, 4) <= 64 && PLN == 2 && a.hp.blocks > 0 && a.nrows <= 65536)
+    agg_wave_kernel<GNN_AGG_MEAN, 4, 1, false, 8, PLN, 4><<<wblocks, 256, 0, st>>>(a, rpw);
+  else if (vec == 4 && ceil_div(width, 4) <= 64)  // one pass per row (e.g. a 168-wide padded x: 42 lanes)
     agg_wave_kernel<GNN_AGG_MEAN, 4, 1, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
   else if (vec == 4) agg_wave_kernel<GNN_AGG_MEAN, 4, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
   else agg_wave_kernel<GNN_AGG_MEAN, 2, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
@@ -1513,9 +1631,9 @@ extern "C" gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg,
                                            int64_t F, void* img, int64_t ld, int64_t plane_stride, int64_t width,
                                            int32_t scale_exp, uint32_t* keep_mask, int64_t mask_cols, float dropout_p,
                                            uint64_t seed, const uint64_t* seed_ptr, const gnn_gemm_nt_params* prep_b,
-                                           gnn_stream_t stream) {
+                                           const gnn_split* hub, gnn_stream_t stream) {
   return sage_mean_fwd_image<2>(g, deg, x, ldx, F, img, ld, plane_stride, width, stream, __func__, keep_mask,
-                                mask_cols, dropout_p, seed, seed_ptr, prep_b, scale_exp);
+                                mask_cols, dropout_p, seed, seed_ptr, prep_b, scale_exp, hub);
 }
 
 extern "C" gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, float inv_denom, float* loss,

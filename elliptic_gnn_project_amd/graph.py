@@ -15,6 +15,9 @@ HBM layout of a plan (int32 throughout, N+1 / S entries):
       in degree order with order[N] (position -> segment), piece0[N], piece_seg[pieces],
       long_seg[long]   (K0b, graph_split.hip)
     dinv[N] f32                            GCN deg^-1/2 (REPLACE plans only)
+    hub (CSR, graphs of <= K1_HUB_MAX_N nodes): ptr[N+1] / nbr without the slots of the rows with
+      deg > K1_HUB_DEG, hubs[H] those rows, ws[W+1] balanced wave starts — K1's hub form
+      (gnn_sage_mean_fwd_h2 hub)
 """
 from __future__ import annotations
 
@@ -27,6 +30,14 @@ from . import _lib
 
 _ATTR = "_gnnmp_plans"
 SPLIT_LEN = 32  # slots per piece of a long segment (K0b)
+# K1's hub form (include/gnnmp.h gnn_sage_mean_fwd_h2 hub): K1 runs one wave per 16 rows, so its
+# time was set by its heaviest waves — the one holding a degree-~200 hub row, and waves whose 16
+# rows happen to be heavy (an average wave walks ~37 slots).  Rows with more than K1_HUB_DEG
+# slots go to blocks of their own, and the other rows to waves balanced by slots.  For graphs of
+# at most K1_HUB_MAX_N nodes (all, by default; GNNMP_K1_HUB_N overrides, for A/B).
+K1_HUB_DEG = int(os.environ.get("GNNMP_K1_HUB_DEG", "32"))
+K1_WAVE_ROWS = int(os.environ.get("GNNMP_K1_WAVE_ROWS", "16"))  # rows per wave on average (A/B)
+K1_HUB_MAX_N = int(os.environ.get("GNNMP_K1_HUB_N", str(1 << 62)))
 
 
 def _split_enabled() -> bool:
@@ -68,6 +79,47 @@ def _build_split(lib, ptr: torch.Tensor, nbr: torch.Tensor, n: int, T: int, dev)
     t["c"] = _lib.GnnSplit(T, 0, n_long, n_pieces, t["ptr"].data_ptr(), t["nbr"].data_ptr(),
                            t["piece0"].data_ptr(), t["piece_seg"].data_ptr(), t["long_seg"].data_ptr(),
                            _lib.ptr(t["order"]))
+    return t
+
+
+def _wave_starts(slots: torch.Tensor, n: int) -> torch.Tensor:
+    """Row boundaries of K1's balanced main-pass waves: as many waves as 16 rows each would take,
+    contiguous row ranges of about equal cost (slots + kappa per row: a row's flush costs about a
+    slot, and kappa >= mean degree / 2 keeps a wave under 63 rows), doubled until no wave holds
+    more than 63 rows (the kernel keeps one row pointer per lane)."""
+    kappa = max(1.0, float(slots.sum()) / max(n, 1) / 2.0)
+    cost = slots.to(torch.float64) + kappa
+    before = torch.cumsum(cost, 0) - cost  # cost of the rows before each row
+    waves = max(1, -(-n // K1_WAVE_ROWS))
+    while True:
+        target = float(cost.sum()) / waves
+        k = torch.arange(waves + 1, dtype=torch.float64, device=slots.device) * target
+        b = torch.searchsorted(before, k).clamp_(max=n)
+        b[0], b[-1] = 0, n
+        if int((b[1:] - b[:-1]).max()) <= 63 or waves >= n:
+            return b.to(torch.int32)
+        waves = min(2 * waves, n)
+
+
+def _build_hub(rowptr: torch.Tensor, col: torch.Tensor, deg: torch.Tensor, n: int, T: int):
+    """K1's hub form of the CSR: the rows with deg > T (deg: the plan's f32 slot counts, the array
+    K1 divides by), the CSR without their slots, in natural order, and the balanced main-pass
+    waves over what is left (include/gnnmp.h gnn_sage_mean_fwd_h2 hub)."""
+    hub = deg[:n] > T
+    nh = int(hub.sum())  # one sync per plan build
+    cnt = (rowptr[1:] - rowptr[:-1]).to(torch.int64)
+    left = torch.where(hub, 0, cnt)
+    t = {"ws": _wave_starts(left, n)}
+    if nh:
+        ptr = torch.zeros(n + 1, dtype=torch.int64, device=rowptr.device)
+        torch.cumsum(left, 0, out=ptr[1:])
+        keep = torch.repeat_interleave(~hub, cnt)
+        t.update(ptr=ptr.to(torch.int32), nbr=col[: keep.numel()][keep].contiguous(),
+                 hubs=torch.nonzero(hub).flatten().to(torch.int32))
+        if t["nbr"].numel() == 0:
+            t["nbr"] = torch.zeros(1, dtype=torch.int32, device=rowptr.device)
+    t["c"] = _lib.GnnSplit(T, 0, nh, t["ws"].numel() - 1, _lib.ptr(t.get("ptr")), _lib.ptr(t.get("nbr")), None,
+                           t["ws"].data_ptr(), _lib.ptr(t.get("hubs")), None)
     return t
 
 
@@ -142,6 +194,7 @@ class GraphPlan:
             _lib.check(lib.gnn_in_degree_f32(self.c_graph, self.deg.data_ptr(), _lib.stream_handle(dev)),
                        "gnn_in_degree_f32")
         self._dinv = None
+        self.hub = _build_hub(self.rowptr, self.col, self.deg, N, K1_HUB_DEG) if 0 < N <= K1_HUB_MAX_N else None
 
     @property
     def dinv(self) -> torch.Tensor:

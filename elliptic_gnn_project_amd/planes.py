@@ -21,6 +21,8 @@ ran in between.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -76,14 +78,16 @@ class SplitImage:
     def _exp_arg(self):
         return ()
 
-    def fill_mean(self, plan, x: torch.Tensor, keep=None, prep_b=None, x_pad=None) -> int:
+    def fill_mean(self, plan, x: torch.Tensor, keep=None, prep_b=None, x_pad=None, hub=True) -> int:
         """K1: planes of mean_{j->i} x[j] into columns [0, col2); returns the new generation.
         keep (half-pair images only): (mask [N, 4] int32, cols, p, seed, seed_ptr) — K1 also writes
         the dropout keep bits of the NT that reads this image (include/gnnmp.h gnn_sage_mean_fwd_h2).
         prep_b (half-pair images only): the GnnGemmNTParams of that NT (fused.gemm_nt b_stage
         "params"); its B-image prep runs inside K1's launch, the NT then runs with b_ready.
         x_pad: x padded with zero columns to the image's col2 (planes.x_padded): K1 gathers it
-        (16-byte pieces) and writes the agg half at full width, padding columns zero."""
+        (16-byte pieces) and writes the agg half at full width, padding columns zero.
+        hub (half-pair images only): the plan's hub form when it has one (graph.K1_HUB_MAX_N: the
+        hub rows on blocks of their own); False: one wave per 16 rows throughout."""
         from .aggregation import KernelTimer, agg_bytes
 
         e0 = KernelTimer.begin()
@@ -92,7 +96,9 @@ class SplitImage:
                 self.ps, self.col2)
         if self.nplanes == 2:
             km, cols, p, seed, sptr = keep if keep is not None else (None, 0, 0.0, 0, None)
-            args += (int(self.exp), _lib.ptr(km), int(cols), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(sptr), prep_b)
+            hs = getattr(plan, "hub", None) if hub else None
+            args += (int(self.exp), _lib.ptr(km), int(cols), float(p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(sptr), prep_b,
+                     ctypes.byref(hs["c"]) if hs is not None else None)
         elif prep_b is not None:
             raise ValueError("prep_b needs a half-pair image")
         _lib.call(self._mean_fn, *args, _lib.stream_handle(x.device))

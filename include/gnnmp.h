@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 20
+#define GNNMP_ABI_VERSION 21
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -222,13 +222,22 @@ gnn_status gnn_split_h2_f32(const float* x, int64_t ldx, int64_t rows, int64_t F
  * prep_b (optional): the params of the half-pair NT that reads this image (a_planes == img and
  * planes_exp == scale_exp); its B-image prep (gnn_gemm_nt_prep_b) runs inside this launch, on
  * extra blocks beside the gather, for a later gnn_gemm_nt_f32 of the same params with
- * b_ready = 1.  UNSUPPORTED when the params do not select the half-pair NT. */
+ * b_ready = 1.  UNSUPPORTED when the params do not select the half-pair NT.
+ * hub (optional, ABI 21; NULL or num_long == 0: one wave per 16 rows throughout): the rows r with
+ * deg[r] > hub->seg_len (hub->long_seg, num_long of them) are each walked by a block of their own
+ * (4 waves over interleaved 8-slot groups, summed in wave order) instead of by the wave holding
+ * them; hub->ptr / nbr are the CSR with those rows' slots removed (natural order: order and
+ * piece0 NULL; num_pieces, piece_seg unused).  For small graphs (a strong-scaling shard), where
+ * the one wave walking a hub row is the launch's tail.  Changes the hub rows' summation order
+ * (within the mean's rounding), not the other rows'.  hub->piece_seg (optional): [num_pieces + 1]
+ * non-decreasing row boundaries from 0 to num_nodes, wave k of the main pass taking rows
+ * [piece_seg[k], piece_seg[k + 1]) (at most 64; balanced by slots instead of 16 rows each). */
 struct gnn_gemm_nt_params;
 gnn_status gnn_sage_mean_fwd_h2(const gnn_graph* g, const float* deg, const float* x, int64_t ldx, int64_t F,
                                 void* img, int64_t ld, int64_t plane_stride, int64_t width, int32_t scale_exp,
                                 uint32_t* keep_mask, int64_t mask_cols, float dropout_p, uint64_t seed,
                                 const uint64_t* seed_ptr, const struct gnn_gemm_nt_params* prep_b,
-                                gnn_stream_t stream);
+                                const gnn_split* hub, gnn_stream_t stream);
 typedef enum {
   GNN_PLANES_SPLIT_BF16 = 0,  /* 3 bf16 planes hi / mid / lo (gnn_split_planes_f32) */
   GNN_PLANES_HALF_PAIR = 1    /* 2 f16 planes hi / lo (gnn_split_h2_f32) */

@@ -86,11 +86,127 @@ def test_mean_h2_equals_split_of_k1(device, n, e):
     im.img.fill_(1.0)
     for gen, ex in enumerate((0, 9, -3), start=1):  # K1 stores mean · 2^exp (the image's pre-scale)
         im.exp = ex
-        assert im.fill_mean(plan, x) == gen
+        assert im.fill_mean(plan, x, hub=False) == gen
         got = _planes_np(im)
         for p, want in enumerate(split_h2(agg, ex)):
             assert np.array_equal(got[p][:, :166], want), (p, ex)
             assert not got[p][:, 166:168].any()
+
+
+def _mean_hub_np(plan, x, T):
+    """Restatement of K1's hub form (gnn_sage_mean_fwd_h2 hub): a row with deg > T summed by 4
+    waves, wave w over the row's 8-slot groups w, w + 4, ... in slot order, the waves' sums then
+    added in wave order; every other row in slot order (float32 throughout); PyG's mean."""
+    rowptr, col, _ = (t.cpu().numpy() for t in plan.csr())
+    xs = x.cpu().numpy()
+    deg = plan.deg.cpu().numpy()[: x.size(0)]
+    out = np.zeros_like(xs)
+    for r in range(x.size(0)):
+        b, e = int(rowptr[r]), int(rowptr[r + 1])
+        if deg[r] > T:
+            acc = [np.zeros(xs.shape[1], np.float32) for _ in range(4)]
+            for s in range(b, e):
+                w = ((s - b) // 8) % 4
+                acc[w] = acc[w] + xs[col[s]]
+            tot = ((acc[0] + acc[1]) + acc[2]) + acc[3]
+        else:
+            tot = np.zeros(xs.shape[1], np.float32)
+            for s in range(b, e):
+                tot = tot + xs[col[s]]
+        out[r] = tot
+    return out / np.maximum(deg, np.float32(1.0))[:, None]
+
+
+@pytest.mark.parametrize("shape", ["ring_isolated", "star", "tiny", "many_hubs"])
+def test_mean_h2_hub_form_edge_graphs(device, shape):
+    """The hub form on edge-case graphs — no hub rows (balanced waves only: bit-identical to the
+    16-row waves), one degree-300 star centre, 3 nodes, every row a hub — vs the restatement."""
+    from elliptic_gnn_project_amd.graph import K1_HUB_DEG, get_plan
+    from elliptic_gnn_project_amd.planes import HalfPairImage
+
+    g = torch.Generator().manual_seed(5)
+    if shape == "ring_isolated":  # 3000 ring nodes, 500 isolated ones
+        n = 3500
+        src = torch.arange(3000)
+        ei = torch.stack([torch.cat([src, (src + 1) % 3000]), torch.cat([(src + 1) % 3000, src])])
+    elif shape == "star":
+        n = 1000
+        leaves = torch.arange(1, 301)
+        ei = torch.stack([torch.cat([leaves, torch.zeros(300, dtype=torch.long)]),
+                          torch.cat([torch.zeros(300, dtype=torch.long), leaves])])
+    elif shape == "tiny":
+        n = 3
+        ei = torch.tensor([[0, 1, 2, 2], [1, 2, 0, 1]])
+    else:  # 40 nodes, all-to-all: every row has 39 > K1_HUB_DEG slots
+        n = 40
+        a, b = torch.meshgrid(torch.arange(n), torch.arange(n), indexing="ij")
+        m = a != b
+        ei = torch.stack([a[m], b[m]])
+    plan = get_plan(ei.to(device), n)
+    x = (torch.randn(n, 166, generator=g) * 3).to(device)
+    im = HalfPairImage(n, 166, 166, device)
+    im.fill_x(x)
+    im.img.fill_(1.0)
+    im.fill_mean(plan, x)
+    got = _planes_np(im)
+    for p, w in enumerate(split_h2(_mean_hub_np(plan, x, K1_HUB_DEG), im.exp)):
+        assert np.array_equal(got[p][:, :166], w), p
+        assert not got[p][:, 166:168].any()
+    if shape == "ring_isolated":
+        assert plan.hub is not None and int(plan.hub["c"].num_long) == 0 and int(plan.hub["c"].num_pieces) > 1
+        im.fill_mean(plan, x, hub=False)
+        assert np.array_equal(_planes_np(im), got)
+
+
+@pytest.mark.parametrize("n,e,padded", [(5000, 6000, False), (20_000, 30_000, True)])
+def test_mean_h2_hub_form_vs_restatement(device, n, e, padded):
+    """K1's hub form (graph.K1_HUB_MAX_N: rows with deg > K1_HUB_DEG on blocks of their own): bit for
+    bit the half-pair split of the numpy restatement of its summation order, padding columns
+    zero; the ordinary rows bit-identical to the one-wave-per-16-rows K1, the hub rows within
+    1e-5 of it (another f32 summation order of up to ~200 terms); the keep bits and the NT B prep riding along unchanged."""
+    from elliptic_gnn_project_amd.fused import _nt_workspace, gemm_nt
+    from elliptic_gnn_project_amd.graph import K1_HUB_DEG
+    from elliptic_gnn_project_amd.planes import HalfPairImage, x_padded
+
+    data, plan, x = _plan_and_x(n, e, 31, device)
+    assert plan.hub is not None and int(plan.hub["c"].num_long) == int((plan.deg[: x.size(0)] > K1_HUB_DEG).sum()) > 0
+    hubs = plan.hub["hubs"].long().cpu().numpy()
+    want = _mean_hub_np(plan, x, K1_HUB_DEG)
+    im = HalfPairImage(x.size(0), x.size(1), x.size(1), device)
+    im.fill_x(x)
+    kw = dict(x_pad=x_padded(x, im.col2)) if padded else {}
+    for ex in (0, 7):
+        im.img.fill_(1.0)
+        im.exp = ex
+        im.fill_mean(plan, x, **kw)  # the hub form by default at this size
+        got = _planes_np(im)
+        for p, w in enumerate(split_h2(want, ex)):
+            assert np.array_equal(got[p][:, :166], w), (p, ex)
+            assert not got[p][:, 166:168].any()
+    hub_img = _planes_np(im)
+    im.fill_mean(plan, x, hub=False, **kw)
+    one = _planes_np(im)
+    rest = np.setdiff1d(np.arange(x.size(0)), hubs)
+    assert np.array_equal(hub_img[:, rest], one[:, rest])
+    rec = lambda g: g[0][:, :166].view(np.float16).astype(np.float64) + g[1][:, :166].view(np.float16) / 2048.0
+    a, b = rec(hub_img)[hubs], rec(one)[hubs]
+    assert np.abs(a - b).max() <= 1e-5 * np.abs(b).max()
+    # keep bits and the B prep of the consuming NT ride along with the hub blocks
+    n_out = 128
+    g = torch.Generator().manual_seed(4)
+    w1 = (torch.randn(n_out, x.size(1), generator=g) * 0.08).to(device)
+    w2 = (torch.randn(n_out, x.size(1), generator=g) * 0.08).to(device)
+    kb1, kb2 = (torch.zeros(x.size(0), 4, dtype=torch.int32, device=device) for _ in range(2))
+    im.fill_mean(plan, x, (kb1, n_out, 0.5, 3, None), hub=False, **kw)
+    nt = dict(w1=w1, w2=w2, bias=torch.randn(n_out, generator=g).to(device), relu=True, dropout_p=0.5, seed=9)
+    im.fill_mean(plan, x, **kw)
+    img0 = im.img.clone()
+    c_one = gemm_nt(None, None, n_out, planes=im, **nt)
+    ws = _nt_workspace(device, n_out, im.k1, im.k2)
+    prm = gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="params", **nt)
+    im.fill_mean(plan, x, (kb2, n_out, 0.5, 3, None), prep_b=prm, **kw)
+    assert torch.equal(kb1, kb2) and torch.equal(im.img, img0)
+    assert torch.equal(gemm_nt(None, None, n_out, planes=im, workspace=ws, b_stage="ready", **nt), c_one)
 
 
 def _operands(M, F, n, seed, wscale=0.08):

@@ -125,17 +125,17 @@ def test_k1_prep_b_needs_the_half_pair_nt(lib):
     args = (ctypes.byref(g), fake, fake, F, F, fake, ld, N * ld, 168, 3, None, 0, 0.0, 0, None)
     p.planes_format = _lib.PLANES_SPLIT_BF16  # not the half-pair NT
     p.planes_exp = 3
-    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 5
+    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None, None) == 5
     p.planes_format = _lib.PLANES_HALF_PAIR  # no workspace
-    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 5
+    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None, None) == 5
     p.planes_exp = 4  # the NT would undo another pre-scale than K1 applies
-    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 1
+    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None, None) == 1
     assert b"planes_exp" in lib.gnn_last_error()
     p.planes_exp = 3
     p.a_planes = fake + 4096  # another image
-    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None) == 1
+    assert lib.gnn_sage_mean_fwd_h2(*args, ctypes.byref(p), None, None) == 1
     bad = args[:9] + (101,) + args[10:]  # the pre-scale exponent's range
-    assert lib.gnn_sage_mean_fwd_h2(*bad, None, None) == 1
+    assert lib.gnn_sage_mean_fwd_h2(*bad, None, None, None) == 1
 
 
 STRUCTS = {
