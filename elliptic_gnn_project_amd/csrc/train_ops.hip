@@ -107,12 +107,13 @@ __device__ __forceinline__ void adam_stage(const AdamTable& tb, AdamLds& L) {
 // tensor ids and in-tensor offsets of elements e, e + T, ... (valid[u] marks real ones; the others
 // are clamped to the slice's LAST element, e1 - 1 >= every real one, so the walk only moves
 // forward and every load stays inside a tensor)
+template <int NTH = kAdamThreads>
 __device__ __forceinline__ void adam_locate(const AdamLds& L, int n, int64_t e, int64_t e1, int (&j)[kAdamUnroll],
                                             int64_t (&i)[kAdamUnroll], bool (&valid)[kAdamUnroll]) {
   int jj = 0;
 #pragma unroll
   for (int u = 0; u < kAdamUnroll; ++u) {
-    const int64_t eu = e + (int64_t)u * kAdamThreads;
+    const int64_t eu = e + (int64_t)u * NTH;
     valid[u] = eu < e1;
     const int64_t ec = valid[u] ? eu : e1 - 1;
     while (jj + 1 < n && ec >= L.off[jj + 1]) ++jj;
@@ -127,7 +128,7 @@ struct LossFinish {  // a deferred gnn_masked_ce_f32 loss (gnn_adam_group.loss_p
 // *lf.out = lf.scale · Σ lf.partial: sum_partials_kernel's loop and reduction, exactly (one block)
 __device__ __forceinline__ void finish_loss(const LossFinish& lf, float* sh) {
   float v = 0.f;
-  for (int i = threadIdx.x; i < lf.n; i += kAdamThreads) v += lf.partial[i];
+  for (int i = threadIdx.x; i < lf.n; i += kAdamThreads) v += threadIdx.x < kAdamThreads ? lf.partial[i] : 0.f;
   const float tl = block_sum(v, sh);
   if (threadIdx.x == 0) lf.out[0] = tl * lf.scale;
 }
@@ -180,20 +181,36 @@ __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, flo
 // reduce's (ABI 20: nblk = nb, nf_off = nb, step_off = 2 nb).  Every block sums them in the same
 // fixed order (lane-strided, then a butterfly per wave, then the 4 waves in order): for nblk <= 64
 // that is grad_sq's one-wave butterfly exactly.
-__global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, const float* __restrict__ partial,
-                                                                  int nblk, int nf_off, int step_off,
-                                                                  float* __restrict__ step,
-                                                                  double max_norm, double lr, double beta1,
-                                                                  double beta2, double eps, double wd,
-                                                                  float* __restrict__ norm_out, int skip_nonfinite,
-                                                                  int64_t* __restrict__ bump, LossFinish lf) {
-  __shared__ float coef_sh;
-  __shared__ int skip_sh;
-  __shared__ float red_sh[2][kAdamThreads / 64];
+// SELF (NTH = 1024, gradients of at most kSelfMax = 2^15 elements): no partials — every block sums Σg² and
+// the non-finite count over ALL the gradients itself, in one fixed order (thread t: elements
+// t, t + NTH, ... in order, 16 loads in flight; then the wave butterflies and the waves in order),
+// so every block holds the same norm and the grad_sq launch is saved.  The step count is read
+// from *step at the start and written by the block that finishes last (a vector atomic on the
+// workspace counter `done`, which that block resets to 0): no block reads it after it changed.
+constexpr int kSelfThreads = 1024;
+// (GCN's 21.6k gradient elements: 10.0 us vs 7.1 + 7.2 in two launches; SAGE-ResBN's ~41k: 16.6
+// vs 8.0 + 7.7 — the per-thread Σ passes grow with the count: profiles/r51_adam_one_launch.txt)
+constexpr int64_t kSelfMax = 1 << 15;
+static_assert(kSelfMax / 64 <= 4 * kSelfThreads, "a SELF block's Adam slice is one pass, loaded before the norm");
+template <int NTH = kAdamThreads, bool SELF = false>
+__global__ __launch_bounds__(NTH) void clip_adam_kernel(AdamTable tb, const float* __restrict__ partial,
+                                                        int nblk, int nf_off, int step_off,
+                                                        float* __restrict__ step,
+                                                        double max_norm, double lr, double beta1,
+                                                        double beta2, double eps, double wd,
+                                                        float* __restrict__ norm_out, int skip_nonfinite,
+                                                        int64_t* __restrict__ bump, LossFinish lf,
+                                                        unsigned* __restrict__ done = nullptr) {
+  __shared__ float coef_sh, snap_sh;
+  __shared__ int skip_sh, last_sh;
+  __shared__ float red_sh[2][NTH / 64];
   __shared__ AdamLds L;
   if (lf.partial && blockIdx.x == kAdamBlocks) {  // the extra block: a deferred CE loss, beside the update
     finish_loss(lf, &red_sh[0][0]);
     return;
+  }
+  if constexpr (SELF) {
+    if (threadIdx.x == 0) snap_sh = step[0];  // (the LDS store waits for the load: complete before `done`)
   }
   adam_stage(tb, L);
   // this block's slice of the flattened parameters; its first pass's loads are issued here, before
@@ -207,7 +224,7 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
   bool ok[kAdamUnroll];
   float g0[kAdamUnroll], p[kAdamUnroll], m0[kAdamUnroll], v0[kAdamUnroll];
   auto load_pass = [&](int64_t e) __attribute__((always_inline)) {
-    adam_locate(L, tb.n, e, e1, j, i, ok);
+    adam_locate<NTH>(L, tb.n, e, e1, j, i, ok);
 #pragma unroll
     for (int u = 0; u < kAdamUnroll; ++u) {  // every load of the pass issued first
       g0[u] = L.g[j[u]][i[u]];
@@ -219,28 +236,60 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
   if (has) load_pass(e0 + threadIdx.x);
   {
     float tot = 0.f, nf = 0.f;
-    constexpr int U = 4;  // every load of the first U·256 partials issued before the sums (clamped, no branch)
-    float pv[U], nv[U];
+    if constexpr (SELF) {  // Σg² over every gradient, this block's own fixed order
+      constexpr int SU = 16;
+      // the thread's elements increase, so the tensor walk only moves forward; the current tensor's
+      // [lo, hi) and pointer stay in registers (LDS is read only when a boundary is crossed)
+      int jj = 0;
+      int64_t lo = 0, hi = L.off[1];
+      const float* gp = L.g[0];
+      for (int64_t q0 = threadIdx.x; q0 < total; q0 += (int64_t)SU * NTH) {
+        float gv[SU];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = threadIdx.x + u * kAdamThreads, ic = min(i, nblk - 1);
-      pv[u] = partial[ic];
-      nv[u] = partial[nf_off + ic];
-    }
+        for (int u = 0; u < SU; ++u) {  // every load of the pass issued first (clamped)
+          const int64_t q = min(q0 + (int64_t)u * NTH, total - 1);
+          while (q >= hi && jj + 1 < tb.n) {
+            ++jj;
+            lo = hi;
+            hi = L.off[jj + 1];
+            gp = L.g[jj];
+          }
+          gv[u] = gp[q - lo];
+        }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool ok = threadIdx.x + u * kAdamThreads < nblk;
-      tot += ok ? pv[u] : 0.f;
-      nf += ok ? nv[u] : 0.f;
-    }
-    for (int i = threadIdx.x + U * kAdamThreads; i < nblk; i += kAdamThreads) {
-      tot += partial[i];
-      nf += partial[nf_off + i];
+        for (int u = 0; u < SU; ++u) {
+          const bool in = q0 + (int64_t)u * NTH < total;
+          tot = in ? fmaf(gv[u], gv[u], tot) : tot;
+          nf += (in && !isfinite(gv[u])) ? 1.f : 0.f;
+        }
+      }
+    } else {
+      constexpr int U = 4;  // every load of the first U·NTH partials issued before the sums (clamped, no branch)
+      float pv[U], nv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = threadIdx.x + u * NTH, ic = min(i, nblk - 1);
+        pv[u] = partial[ic];
+        nv[u] = partial[nf_off + ic];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = threadIdx.x + u * NTH < nblk;
+        tot += ok ? pv[u] : 0.f;
+        nf += ok ? nv[u] : 0.f;
+      }
+      for (int i = threadIdx.x + U * NTH; i < nblk; i += NTH) {
+        tot += partial[i];
+        nf += partial[nf_off + i];
+      }
     }
     for (int o = 32; o > 0; o >>= 1) {
       tot += __shfl_xor(tot, o);
       nf += __shfl_xor(nf, o);
     }
+    // SELF: this thread's gradient loads (the Σ pass and its slice's first Adam pass) have landed
+    // before the barrier behind which thread 0 counts the block as done (vmcnt(0))
+    if constexpr (SELF) __builtin_amdgcn_s_waitcnt(0x0f70);
     if ((threadIdx.x & 63) == 0) {
       red_sh[0][threadIdx.x >> 6] = tot;
       red_sh[1][threadIdx.x >> 6] = nf;
@@ -249,7 +298,7 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
     if (threadIdx.x == 0) {
       tot = red_sh[0][0];
       nf = red_sh[1][0];
-      for (int w = 1; w < kAdamThreads / 64; ++w) {
+      for (int w = 1; w < NTH / 64; ++w) {
         tot += red_sh[0][w];
         nf += red_sh[1][w];
       }
@@ -261,26 +310,54 @@ __global__ __launch_bounds__(kAdamThreads) void clip_adam_kernel(AdamTable tb, c
       skip_sh = skip;
       if (blockIdx.x == 0) {
         if (norm_out) norm_out[0] = norm;
-        step[0] = partial[step_off] + (skip ? 0.0f : 1.0f);
+        if constexpr (!SELF) step[0] = partial[step_off] + (skip ? 0.0f : 1.0f);
         if (bump) bump[0] = bump[0] + 1;  // no kernel of this launch reads it
+      }
+      if constexpr (SELF) {  // every block has read *step (snap_sh) and every gradient: the last one
+        last_sh = atomicAdd(done, 1u) == (unsigned)kAdamBlocks - 1u;  // to get here advances the step
+        if (last_sh) {
+          step[0] = snap_sh + (skip ? 0.0f : 1.0f);
+          atomicExch(done, 0u);
+        }
       }
     }
   }
   __syncthreads();
   if (skip_sh) return;  // block-uniform
+  if constexpr (SELF) {
+    // clip_grad_norm_'s in-place scaling of .grad: by the last block alone, once every block has
+    // summed the gradients (a block writing its own slice earlier would change what a slower block
+    // reads for its norm)
+    if (last_sh) {
+      const int64_t tot_n = L.off[tb.n];
+      const float cf = coef_sh;
+      int jj = 0;
+      int64_t lo = 0, hi = L.off[1];
+      float* gp = L.g[0];
+      for (int64_t q = threadIdx.x; q < tot_n; q += NTH) {
+        while (q >= hi && jj + 1 < tb.n) {
+          ++jj;
+          lo = hi;
+          hi = L.off[jj + 1];
+          gp = L.g[jj];
+        }
+        gp[q - lo] = gp[q - lo] * cf;
+      }
+    }
+  }
   const float coef = coef_sh;
-  const double t = (double)partial[step_off] + 1.0;
+  const double t = (double)(SELF ? snap_sh : partial[step_off]) + 1.0;
   const double bc1 = 1.0 - pow(beta1, t), bc2 = 1.0 - pow(beta2, t);
   const float neg_step = (float)(-lr / bc1), bc2s = (float)sqrt(bc2);
   const float b2 = (float)beta2, omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2);
   const float epsf = (float)eps, wdf = (float)wd;
-  for (int64_t e = e0 + threadIdx.x; has && e < e1; e += kAdamUnroll * kAdamThreads) {
+  for (int64_t e = e0 + threadIdx.x; has && e < e1; e += kAdamUnroll * NTH) {
     if (e != e0 + threadIdx.x) load_pass(e);  // (the first pass was loaded before the reduction)
 #pragma unroll
     for (int u = 0; u < kAdamUnroll; ++u) {
       if (!ok[u]) continue;
       float g = g0[u] * coef;
-      L.g[j[u]][i[u]] = g;  // clip_grad_norm_ scales .grad in place
+      if constexpr (!SELF) L.g[j[u]][i[u]] = g;  // clip_grad_norm_ scales .grad in place (SELF: above)
       if (wdf != 0.f) g = g + wdf * p[u];  // Adam (not AdamW) weight decay: grad.add(param, alpha=wd)
       const float m = fmaf(omb1, g - m0[u], m0[u]);  // exp_avg.lerp_(grad, 1 - beta1)
       const float v = v0[u] * b2 + omb2 * g * g;
@@ -338,9 +415,12 @@ extern "C" gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, f
   return GNN_OK;
 }
 
+// workspace: the grad_sq partials (2 kAdamBlocks + 1 floats), then the SELF form's block counter
+// (one word; zero before the first call, left zero by every call)
+constexpr size_t kAdamWsBytes = (2 * kAdamBlocks + 2) * sizeof(float);
 extern "C" gnn_status gnn_clip_adam_workspace_size(size_t* bytes) {
   if (!bytes) return fail(GNN_ERR_INVALID_ARG, __func__, "null");
-  *bytes = (2 * kAdamBlocks + 1) * sizeof(float);
+  *bytes = kAdamWsBytes;
   return GNN_OK;
 }
 
@@ -348,8 +428,7 @@ extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, 
                                         size_t workspace_bytes, gnn_stream_t stream) {
   if (!grp || !step || grp->num_tensors < 0 || grp->num_tensors > GNN_ADAM_MAX_TENSORS)
     return fail(GNN_ERR_INVALID_ARG, __func__, "bad group");
-  if (!workspace || workspace_bytes < (2 * kAdamBlocks + 1) * sizeof(float))
-    return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
+  if (!workspace || workspace_bytes < kAdamWsBytes) return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
   AdamTable tb{};
   tb.n = grp->num_tensors;
   tb.off[0] = 0;
@@ -371,6 +450,14 @@ extern "C" gnn_status gnn_clip_adam_f32(const gnn_adam_group* grp, float* step, 
                                                            grp->max_norm, grp->lr, grp->beta1, grp->beta2, grp->eps,
                                                            grp->weight_decay, norm_out, grp->skip_nonfinite,
                                                            grp->bump_counter, lf);
+    GNN_LAUNCH_CHECK();
+    return GNN_OK;
+  }
+  if (tb.off[tb.n] <= kSelfMax) {  // one launch: every block sums Σg² itself
+    unsigned* done = reinterpret_cast<unsigned*>(partial + 2 * kAdamBlocks + 1);
+    clip_adam_kernel<kSelfThreads, true><<<kAdamBlocks + (lf.partial ? 1 : 0), kSelfThreads, 0, st>>>(
+        tb, partial, 0, 0, 0, step, grp->max_norm, grp->lr, grp->beta1, grp->beta2, grp->eps, grp->weight_decay,
+        norm_out, grp->skip_nonfinite, grp->bump_counter, lf, done);
     GNN_LAUNCH_CHECK();
     return GNN_OK;
   }

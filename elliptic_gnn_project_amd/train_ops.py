@@ -270,7 +270,7 @@ class ClipAdam(torch.optim.Optimizer):
                     raise RuntimeError("ClipAdam runs on the GPU (libgnnmp)")
                 nb = _lib.c_size(0)
                 _lib.call("gnn_clip_adam_workspace_size", nb)
-                self._ws = _ws(int(nb.value), dev)
+                self._ws = torch.zeros(max(int(nb.value) // 4, 1), dtype=torch.float32, device=dev)  # (its counter word starts at 0)
                 self.last_norm = torch.zeros(1, dtype=torch.float32, device=dev)
             if "step_t" not in group:  # device step counter of this group (advanced by the kernel)
                 group["step_t"] = torch.zeros(1, dtype=torch.float32, device=dev)

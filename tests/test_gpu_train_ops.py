@@ -186,6 +186,9 @@ def _boundary_tables():
         out.append(sizes)
     out.append([1000 * 64 - 1, 1, 0, 999])  # total not a multiple of 64: a start one before a boundary
     out.append([3, 0, 5, 1])                # fewer elements than blocks: most slices empty
+    out.append([(1 << 15) - 7, 0, 7])       # the one-launch form's largest table (2^15 elements)
+    out.append([(1 << 15) + 5, 1000])       # past it: the Σg² pass, then the update (two launches)
+    out.append([(1 << 18) + 5, 1000])       # a large table (two launches)
     return out
 
 
@@ -232,5 +235,46 @@ def test_clip_adam_slice_boundaries(device, sizes, captured):
         torch.testing.assert_close(ob.last_norm[0], norm, rtol=1e-5, atol=0)
         for p, q in zip(pa, pb):
             torch.testing.assert_close(q.grad, p.grad, rtol=1e-6, atol=1e-9)
-            torch.testing.assert_close(q, p, rtol=1e-6, atol=1e-7)
+            # Adam's m / (sqrt(v) + eps) turns a 1-ulp difference of the clip coefficient (the norm
+            # is summed in another order) into up to ~lr on elements whose moments sit near eps:
+            # a handful per 10^4 in the 2^18-element tables; every other element within 1e-6
+            d = (q - p).detach().abs()
+            bad = d > 1e-7 + 1e-6 * p.abs()
+            assert int(bad.sum()) <= p.numel() // 10000 and (float(d.max()) if d.numel() else 0.0) <= 0.02
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("skip", [False, True])
+def test_clip_adam_one_launch_counter(device, skip):
+    """The one-launch form (gradients of <= 2^15 elements: every block sums Σg² itself, the last
+    block to finish advances the device step through the workspace's counter word): 6 eager steps
+    and 6 graph replays with a non-finite gradient in between (GradScaler's skip), the step count
+    exact and the counter word back at 0 after every call."""
+    from elliptic_gnn_project_amd.train_ops import ClipAdam
+
+    pb = _sized_params(device, [5000, 128, 7], 9)
+    ob = ClipAdam(pb, lr=0.01, max_norm=1.0, skip_nonfinite=skip)
+    want = 0
+    for it in range(6):
+        for q in pb:
+            q.grad = torch.full_like(q, 0.01)
+        if it == 3:
+            pb[1].grad[5] = float("inf")
+        ob.step()
+        want += 0 if (skip and it == 3) else 1
+        torch.cuda.synchronize()
+        assert float(ob.param_groups[0]["step_t"]) == want
+        assert int(ob._ws.view(torch.int32)[-1]) == 0
+    for q in pb:
+        q.grad.fill_(0.01)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(graph):
+        ob.step()
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(6):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert float(ob.param_groups[0]["step_t"]) == want + 6
+    assert int(ob._ws.view(torch.int32)[-1]) == 0
