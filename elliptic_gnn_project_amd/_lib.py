@@ -126,6 +126,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("mask", c_ptr), ("ldmask", c_i64), ("mask_scale", ctypes.c_float),
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
         ("planes_format", c_i32), ("keep_mask", c_ptr), ("b_ready", c_i32), ("planes_exp", c_i32),
+        ("colsum_part", c_ptr), ("colsum_cap", c_i64),
     ]
 
 
@@ -285,6 +286,8 @@ SIGNATURES = {
     "gnn_gemm_tn_sq_blocks": (ctypes.c_int, [c_i64, ctypes.POINTER(c_i32)]),
     "gnn_gemm_tn_f32": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams), c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_gemm_nt_planes_ok": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams)]),
+    "gnn_gemm_nt_colsum_blocks": (ctypes.c_int, [ctypes.POINTER(GnnGemmNTParams), ctypes.POINTER(c_i32)]),
+    "gnn_colsum_finish_f32": (ctypes.c_int, [c_ptr, c_i32, c_i64, c_ptr, c_ptr]),
     "gnn_gemm_tn_planes_ok": (ctypes.c_int, [ctypes.POINTER(GnnGemmTNParams)]),
     "gnn_colsum_workspace_size": (ctypes.c_int, [c_i64, c_i64, ctypes.POINTER(c_size)]),
     "gnn_colsum_f32": (ctypes.c_int, [c_i64, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr]),
@@ -292,6 +295,11 @@ SIGNATURES = {
     "gnn_masked_ce_f32": (
         ctypes.c_int,
         [c_i64, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr],
+    ),
+    "gnn_masked_ce_colsum_f32": (
+        ctypes.c_int,
+        [c_i64, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr,
+         c_ptr],
     ),
     "gnn_clip_adam_workspace_size": (ctypes.c_int, [ctypes.POINTER(c_size)]),
     "gnn_neighbor_sample_workspace_size": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_size)]),

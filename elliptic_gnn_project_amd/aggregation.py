@@ -180,6 +180,19 @@ def agg_bytes(plan: GraphPlan, F: int, mode: int, transpose: bool, has_addend, e
     return b
 
 
+def colsum_of(x: torch.Tensor) -> torch.Tensor:
+    """colsum(x), taken from the per-block column sums the kernel that wrote x left on it
+    (``x._gnnmp_colsum``: the masked CE's dlogits, gnn_masked_ce_colsum_f32) when it has them —
+    one small launch instead of a pass over x."""
+    part = getattr(x, "_gnnmp_colsum", None)
+    if part is not None and x.dim() == 2 and x.size(1) > 0 and part.numel() % x.size(1) == 0 and part.numel() > 0:
+        out = torch.empty(x.size(1), dtype=torch.float32, device=x.device)
+        _lib.call("gnn_colsum_finish_f32", part.data_ptr(), part.numel() // x.size(1), x.size(1), out.data_ptr(),
+                  _lib.stream_handle(x.device))
+        return out
+    return colsum(x)
+
+
 def colsum(x: torch.Tensor) -> torch.Tensor:
     """Deterministic column sum (bias gradients) via gnn_colsum_f32."""
     x = _as_f32_rows(x)
@@ -302,7 +315,7 @@ class _MaskedGCNAggregate(torch.autograd.Function):
         dm = None
         if ctx.needs_input_grad[1]:
             dm = (edge_dot(plan, dout, y) * norm_e)[: plan.num_edges]
-        db = colsum(dout) if ctx.has_bias and ctx.needs_input_grad[3] else None
+        db = colsum_of(dout) if ctx.has_bias and ctx.needs_input_grad[3] else None
         return dy, dm, None, db
 
 
@@ -330,7 +343,7 @@ class _GCNAggregate(torch.autograd.Function):
         plan = ctx.plan
         dy = aggregate(plan, dout, _lib.AGG_GCN, transpose=True, nodew=plan.dinv) \
             if ctx.needs_input_grad[0] else None
-        db = colsum(dout) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        db = colsum_of(dout) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return dy, None, db
 
 
@@ -421,7 +434,7 @@ class _GATAttention(torch.autograd.Function):
         # cols pass (CSC): id+map 8 + alpha/de 8H + dout row 4·fo per slot, dxh 4HC + scores 8H per node
         KernelTimer.end(t0, ("gat_bwd", heads, chans, fo),
                         S * (12 + 16 * heads + 4 * heads * chans + 4 * fo) + N * (8 + 16 * heads + 4 * F + 4 * fo))
-        db = colsum(dout) if has_bias and ctx.needs_input_grad[3] else None
+        db = colsum_of(dout) if has_bias and ctx.needs_input_grad[3] else None
         return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db) + (None,) * 9
 
 
@@ -486,7 +499,7 @@ class _GATAttentionMasked(torch.autograd.Function):
                   a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
                   dout.data_ptr(), _ld(dout), dxh.data_ptr(), _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(),
                   w_slot.data_ptr(), dw.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
-        db = colsum(dout) if has_bias and ctx.needs_input_grad[3] else None
+        db = colsum_of(dout) if has_bias and ctx.needs_input_grad[3] else None
         return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db, dw) + (None,) * 5
 
 

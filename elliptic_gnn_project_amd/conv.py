@@ -21,7 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .aggregation import (aggregate, colsum, gat_attention, gcn_aggregate, masked_gat_attention, masked_gcn_aggregate,
+from .aggregation import (aggregate, colsum, colsum_of, gat_attention, gcn_aggregate, masked_gat_attention, masked_gcn_aggregate,
                           masked_mean_aggregate, mean_aggregate)
 from .graph import GraphPlan, get_plan
 from .linear import Linear, linear, linear2, linear_stacked
@@ -69,7 +69,7 @@ class _MeanAggRootBias(torch.autograd.Function):
             dy = torch.empty((N, 2 * fo), dtype=torch.float32, device=dout.device)
             aggregate(plan, dout, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dy[:, :fo])
             dy[:, fo:].copy_(dout)
-        db = colsum(dout) if ctx.has_bias and ctx.needs_input_grad[1] else None
+        db = colsum_of(dout) if ctx.has_bias and ctx.needs_input_grad[1] else None
         return dy, db, None, None
 
 

@@ -1691,6 +1691,13 @@ extern "C" gnn_status gnn_colsum_workspace_size(int64_t rows, int64_t F, size_t*
   return GNN_OK;
 }
 
+extern "C" gnn_status gnn_colsum_finish_f32(const float* part, int32_t nblk, int64_t F, float* out,
+                                             gnn_stream_t stream) {
+  if (nblk < 1 || F < 1 || F > INT32_MAX || !part || !out) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
+  colsum_final_kernel<<<(unsigned)F, 256, 0, (hipStream_t)stream>>>((int32_t)F, nblk, part, out);
+  return hip_check(hipGetLastError(), __func__);
+}
+
 extern "C" gnn_status gnn_colsum_f32(int64_t rows, int64_t F, const float* x, int64_t ldx, float* out,
                                      void* workspace, size_t workspace_bytes, gnn_stream_t stream) {
   if (rows < 0 || F < 0 || F > INT32_MAX || (F > 0 && !out) || ldx < F)

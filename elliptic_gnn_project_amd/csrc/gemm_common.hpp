@@ -72,6 +72,7 @@ struct NTArgs {
   int32_t ap_h2;  // the image is a half-pair image (2 f16 planes hi / lo, gemm_ws.hip K7a-h)
   int32_t ap_exp; // half-pair: the image holds A · 2^ap_exp (undone in the epilogue's column scale)
   const uint32_t* kmask;  // optional dropout keep bits (half-pair NT): bit c of kmask[r·4 + c/32]
+  float* colsum_part;     // optional (skinny-K NT): per-block column sums of the stored C, [nb][Nc]
 };
 
 // the half-pair NT's B-image prep (ws_prep_h2_body below)
@@ -259,6 +260,7 @@ __device__ __forceinline__ uint32_t h2_scale_pair(uint32_t h, float s) {
 // VALU kernels for the narrow output-layer shapes (gemm_skinny.hip).  launch_nt_skinny returns
 // false (launching nothing) when the shape/epilogue is outside its envelope.
 bool launch_nt_skinny(const NTArgs& a, hipStream_t st);
+int nt_skinny_k_blocks(const NTArgs& a);  // grid of the skinny-K form (its colsum_part rows); 0: not that form
 int tn_skinny_blocks(int64_t M);
 bool tn_skinny_ok(const TNArgs& a);
 void launch_tn_skinny(const TNArgs& a, int nblk, hipStream_t st);

@@ -820,6 +820,16 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
   a.c_bf16 = p->c_dtype == GNN_DTYPE_BF16;
   a.mask = p->mask; a.ldmask = p->ldmask; a.mask_scale = p->mask_scale;
   if (p->mask && p->ldmask < p->N) return fail(GNN_ERR_INVALID_ARG, fn, "bad ldmask");
+  if (p->colsum_part) {  // ABI 21: the skinny-K form also writes C's per-block column sums
+    const int nb = nt_skinny_k_blocks(a);
+    if (nb == 0 || p->a_planes || phase != NT_PHASE_ALL)
+      return fail(GNN_ERR_UNSUPPORTED, fn, "colsum_part needs the skinny-K form (k1 <= 8, k2 = 0, 8 < N <= 256)");
+    if (p->colsum_cap < (int64_t)nb * p->N || (reinterpret_cast<uintptr_t>(p->colsum_part) & 3))
+      return fail(GNN_ERR_INVALID_ARG, fn, "colsum_cap < gnn_gemm_nt_colsum_blocks x N");
+    a.colsum_part = p->colsum_part;
+    if (!launch_nt_skinny(a, st)) return fail(GNN_ERR_UNSUPPORTED, fn, "colsum_part: not the skinny-K form");
+    return hip_check(hipGetLastError(), fn);
+  }
   if (p->a_planes) {
     if (p->planes_format != GNN_PLANES_SPLIT_BF16 && p->planes_format != GNN_PLANES_HALF_PAIR)
       return fail(GNN_ERR_INVALID_ARG, fn, "bad planes_format");
@@ -1074,6 +1084,13 @@ static NTArgs nt_image_args(const gnn_gemm_nt_params* p) {  // the fields the im
   a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
   a.ap_exp = a.ap_h2 ? p->planes_exp : 0;
   return a;
+}
+
+extern "C" gnn_status gnn_gemm_nt_colsum_blocks(const gnn_gemm_nt_params* p, int32_t* nb) {
+  if (!p || !nb) return fail(GNN_ERR_INVALID_ARG, __func__, "null");
+  NTArgs a = nt_image_args(p);
+  *nb = p->a_planes ? 0 : nt_skinny_k_blocks(a);
+  return GNN_OK;
 }
 
 extern "C" int gnn_gemm_nt_planes_ok(const gnn_gemm_nt_params* p) {

@@ -119,8 +119,12 @@ __global__ __launch_bounds__(256) void nt_skinny_n_kernel(NTArgs a, int lg_tpr) 
 
 // C[r, n0..n0+VEC) = Σ_{k<K} A[r, k] B[k, n0..]: B's K x VEC slice of a lane in registers,
 // the row's K values broadcast to its TPR lanes.
+// colsum_part (optional): block b's column sums of the C it stores, colsum_part[b·Nc + n] — each
+// thread sums its rows in order, the block's row groups are added in order through LDS (the bias
+// gradient of the layer whose masked input gradient this is: no separate pass over C)
 template <int VEC, int KK>
 __global__ __launch_bounds__(256) void nt_skinny_k_kernel(NTArgs a, int lg_tpr) {
+  __shared__ float csl[256 * VEC];
   const int TPR = 1 << lg_tpr;
   const int lig = threadIdx.x & (TPR - 1);
   const int rpb = 256 >> lg_tpr;
@@ -137,11 +141,13 @@ __global__ __launch_bounds__(256) void nt_skinny_k_kernel(NTArgs a, int lg_tpr) 
       b[k][i] = w;
     }
   const uint64_t seed = a.dropout ? nt_seed(a) : 0;
-  if (!col_ok) return;
+  float cs[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) cs[i] = 0.0f;
   // kSkU rows per thread per pass, their A values loaded together (clamped rows) before any store
   // (one row per pass left one dependent load → store round trip per row: 35 us for [203769, 64])
   const int64_t stride = (int64_t)gridDim.x * rpb;
-  for (int64_t r0 = (int64_t)blockIdx.x * rpb + (threadIdx.x >> lg_tpr); r0 < a.M; r0 += kSkU * stride) {
+  for (int64_t r0 = (int64_t)blockIdx.x * rpb + (threadIdx.x >> lg_tpr); col_ok && r0 < a.M; r0 += kSkU * stride) {
     float av[kSkU][KK];
 #pragma unroll
     for (int u = 0; u < kSkU; ++u) {
@@ -160,12 +166,25 @@ __global__ __launch_bounds__(256) void nt_skinny_k_kernel(NTArgs a, int lg_tpr) 
 #pragma unroll
         for (int k = 1; k < KK; ++k) s = fmaf(k < a.k1 ? av[u][k] : 0.0f, b[k][i], s);
         o[i] = nt_epi(a, s, r, n0 + i, seed);
+        cs[i] += o[i];
       }
       if (!a.c) continue;
       float* dst = a.c + r * a.ldc + n0;
       if constexpr (VEC == 4) *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
       else if constexpr (VEC == 2) *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
       else *dst = o[0];
+    }
+  }
+  if (!a.colsum_part) return;  // kernel-uniform
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) csl[i * 256 + threadIdx.x] = cs[i];
+  __syncthreads();
+  if ((threadIdx.x >> lg_tpr) == 0 && col_ok) {  // row group 0: the rpb groups' sums in order
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float t = csl[i * 256 + lig];
+      for (int g = 1; g < rpb; ++g) t += csl[i * 256 + g * TPR + lig];
+      if (n0 + i < a.Nc) a.colsum_part[(int64_t)blockIdx.x * a.Nc + n0 + i] = t;
     }
   }
 }
@@ -247,10 +266,24 @@ unsigned grid_for(int64_t M, int rpb, int64_t cap) {
 
 }  // namespace
 
+// the skinny-K form's VEC and grid (launch_nt_skinny below); 0 blocks: not that form
+static int skk_vec(const NTArgs& a) {
+  auto c_ok = [&](int v) { return a.Nc % v == 0 && (!a.c || (a.ldc % v == 0 && al(a.c, 4 * v))); };
+  return c_ok(4) ? 4 : (c_ok(2) ? 2 : 1);
+}
+int nt_skinny_k_blocks(const NTArgs& a) {
+  if (a.a_bf16 || a.c_bf16 || a.nproj > 0 || a.M == 0 || a.Nc <= SK_MAXN) return 0;
+  if (!(a.k2 == 0 && a.k1 <= SK_MAXN && a.Nc <= 64 * 4)) return 0;
+  const int lg = lg2ceil((a.Nc + skk_vec(a) - 1) / skk_vec(a));
+  if (lg > 8) return 0;
+  return (int)grid_for(ceil_div(a.M, kSkU), 256 >> lg, 8192);
+}
+
 bool launch_nt_skinny(const NTArgs& a, hipStream_t st) {
   if (a.a_bf16 || a.c_bf16 || a.nproj > 0 || a.M == 0) return false;
   const int K = a.k1 + a.k2;
   if (a.Nc <= SK_MAXN && K <= SK_KMAX) {
+    if (a.colsum_part) return false;  // (the column sums ride only in the skinny-K form)
     auto v_ok = [&](int v) {
       return a.k1 % v == 0 && a.lda1 % v == 0 && al(a.a1, 4 * v) &&
              (a.k2 == 0 || (a.k2 % v == 0 && a.lda2 % v == 0 && al(a.a2, 4 * v)));
@@ -270,8 +303,7 @@ bool launch_nt_skinny(const NTArgs& a, hipStream_t st) {
     return true;
   }
   if (a.k2 == 0 && a.k1 <= SK_MAXN && a.Nc <= 64 * 4) {
-    auto c_ok = [&](int v) { return a.Nc % v == 0 && (!a.c || (a.ldc % v == 0 && al(a.c, 4 * v))); };
-    const int VEC = c_ok(4) ? 4 : (c_ok(2) ? 2 : 1);
+    const int VEC = skk_vec(a);
     const int lg = lg2ceil((a.Nc + VEC - 1) / VEC);
     if (lg > 8) return false;
     const unsigned nb = grid_for(ceil_div(a.M, kSkU), 256 >> lg, 8192);

@@ -29,29 +29,44 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
 
 // loss_i = -w[y_i] · log_softmax(x_i)[y_i] on rows with mask_i (F.cross_entropy(weight=w,
 // reduction='none')); dx_i = w[y_i] · (softmax(x_i) - onehot(y_i)) · inv_denom there, 0 elsewhere.
-// partial[b] = Σ loss over block b's rows.
+// partial[b] = Σ loss over block b's rows.  colsum (optional, ABI 21): colsum[b·C + c] = Σ dx[:, c]
+// over block b's rows (the same fixed-order block sum): the output layer's bias gradient without
+// a pass over dlogits (gnn_colsum_finish_f32 adds the blocks).
 template <int CT>  // CT > 0: compile-time class count (registers); CT == 0: runtime C <= kMaxClasses
 __global__ __launch_bounds__(kCeThreads) void masked_ce_kernel(int64_t N, int Crt, const float* __restrict__ x,
                                                                int64_t ldx, const int64_t* __restrict__ y,
                                                                const uint8_t* __restrict__ mask,
                                                                const float* __restrict__ w, float inv_denom,
                                                                float* __restrict__ dx, int64_t ldd,
-                                                               float* __restrict__ partial) {
+                                                               float* __restrict__ partial,
+                                                               float* __restrict__ colsum = nullptr) {
   constexpr int CM = CT > 0 ? CT : kMaxClasses;
   const int C = CT > 0 ? CT : Crt;
   __shared__ float sh[kCeThreads / 64];
   const int64_t row = (int64_t)blockIdx.x * kCeThreads + threadIdx.x;
   float l = 0.f;
+  float dv[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) dv[c] = 0.f;
   if (row < N) {
     const int64_t t = y[row];
     const bool on = mask[row] != 0 && t >= 0 && t < C;
     float v[CM];
 #pragma unroll
     for (int c = 0; c < CM; ++c) v[c] = c < C ? x[row * ldx + c] : 0.f;
-    l = masked_ce_row<CM>(v, C, t, on, on ? w[t] : 0.f, inv_denom, dx + row * ldd);
+    l = masked_ce_row<CM>(v, C, t, on, on ? w[t] : 0.f, inv_denom, dx + row * ldd, dv);
   }
   const float t = block_sum(l, sh);
   if (threadIdx.x == 0) partial[blockIdx.x] = t;
+  if (colsum) {  // kernel-uniform
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      if (c >= C) break;
+      __syncthreads();  // sh reused
+      const float s = block_sum(dv[c], sh);
+      if (threadIdx.x == 0) colsum[(int64_t)blockIdx.x * C + c] = s;
+    }
+  }
 }
 
 // out[0] = scale · Σ_i partial[i], summed in a fixed order by one block.
@@ -402,6 +417,31 @@ extern "C" gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logit
                                                      partial);
   GNN_LAUNCH_CHECK();
   if (!loss) return GNN_OK;  // the partials stay in the workspace (gnn_masked_ce_finish / ClipAdam)
+  sum_partials_kernel<<<1, 256, 0, st>>>(partial, nblk, inv_denom, loss);
+  GNN_LAUNCH_CHECK();
+  return GNN_OK;
+}
+
+extern "C" gnn_status gnn_masked_ce_colsum_f32(int64_t N, int32_t C, const float* logits, int64_t ldx,
+                                               const int64_t* y, const uint8_t* mask, const float* class_w,
+                                               float inv_denom, float* dlogits, int64_t ld_d, float* loss,
+                                               void* workspace, size_t workspace_bytes, float* colsum,
+                                               gnn_stream_t stream) {
+  if (N < 1 || C < 1 || C > kMaxClasses || ldx < C || ld_d < C || !logits || !y || !mask || !class_w ||
+      !dlogits || !colsum)
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad args (N >= 1, 1 <= C <= 16, colsum)");
+  const int nblk = (int)ceil_div(N, kCeThreads);
+  if (!workspace || workspace_bytes < nblk * sizeof(float)) return fail(GNN_ERR_WORKSPACE, __func__, "workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* partial = static_cast<float*>(workspace);
+  if (C == 2)
+    masked_ce_kernel<2><<<nblk, kCeThreads, 0, st>>>(N, C, logits, ldx, y, mask, class_w, inv_denom, dlogits, ld_d,
+                                                     partial, colsum);
+  else
+    masked_ce_kernel<0><<<nblk, kCeThreads, 0, st>>>(N, C, logits, ldx, y, mask, class_w, inv_denom, dlogits, ld_d,
+                                                     partial, colsum);
+  GNN_LAUNCH_CHECK();
+  if (!loss) return GNN_OK;
   sum_partials_kernel<<<1, 256, 0, st>>>(partial, nblk, inv_denom, loss);
   GNN_LAUNCH_CHECK();
   return GNN_OK;

@@ -55,6 +55,9 @@ _K1_PAD = os.environ.get("GNNMP_K1_PAD", "1") != "0"
 # (profiles/r18h) 0.3692 vs 0.3637 ms per step in line — the captured fork / join costs more than
 # the prep it hides, as in round 3
 _SIDE_PREP = os.environ.get("GNNMP_SIDE_PREP", "0") == "1"
+# GCN backward: the skinny masked-gradient NT also writes its column sums (the layer below's bias
+# gradient, gnn_gemm_nt_params.colsum_part) instead of a separate colsum pass; GNNMP_NT_COLSUM=0: A/B
+_NT_COLSUM = os.environ.get("GNNMP_NT_COLSUM", "1") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -114,7 +117,7 @@ _BF_IMAGE = os.environ.get("GNNMP_BF_IMAGE", "1") != "0"
 
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
             out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None, mask=None, mask_scale=1.0,
-            planes=None, check_planes=False, keep_mask=None, workspace=None, b_stage=None):
+            planes=None, check_planes=False, keep_mask=None, workspace=None, b_stage=None, colsum=False):
     """C = epilogue([a1 | a2] · B) on the NT kernels; B = bt ([K, n] row-major) or, with bt None,
     [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2].
     bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too.
@@ -124,7 +127,10 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
     ``b_stage`` (image-A forms, with an explicit ``workspace``): "prep" launches only the B-image
     prep (gnn_gemm_nt_prep_b; returns None), "ready" only the GEMM over the image a "prep" call of
     the same weights left in ``workspace``; "params" launches nothing and returns the call's
-    GnnGemmNTParams (K1's prep_b: HalfPairImage.fill_mean)."""
+    GnnGemmNTParams (K1's prep_b: HalfPairImage.fill_mean).
+    ``colsum``: also return Σ_rows C ([n] f32) — on the skinny-K form its blocks write the column
+    sums as they store C (gnn_gemm_nt_params.colsum_part) and one small launch adds them
+    (gnn_colsum_finish_f32); otherwise a gnn_colsum_f32 pass over C.  Returns (C, Σ C)."""
     if planes is not None:
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
@@ -152,6 +158,13 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         *_planes_fields(planes), _lib.ptr(keep_mask), int(b_stage == "ready"),
         int(getattr(planes, "exp", 0)),
     )
+    part = None
+    if colsum and out is not None and b_stage is None and not check_planes:
+        nb = ctypes.c_int32(0)
+        _lib.call("gnn_gemm_nt_colsum_blocks", p, ctypes.byref(nb))
+        if nb.value > 0:
+            part = torch.empty(nb.value * n, dtype=torch.float32, device=dev)
+            p.colsum_part, p.colsum_cap = part.data_ptr(), part.numel()
     if check_planes:
         return bool(_lib.load().gnn_gemm_nt_planes_ok(p))
     if b_stage == "params":
@@ -178,6 +191,14 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
             prod = -1
         KernelTimer.records.append((("gemm_nt", M, k, n, ea, out.element_size() if out is not None else 0, prod),
                                     e0, e1, 2 * M * k * n))
+    if colsum:
+        from .aggregation import colsum as _colsum
+
+        if part is None:
+            return out, _colsum(out)
+        db = torch.empty(n, dtype=torch.float32, device=dev)
+        _lib.call("gnn_colsum_finish_f32", part.data_ptr(), part.numel() // n, n, db.data_ptr(), _lib.stream_handle(dev))
+        return out, db
     return out
 
 
@@ -551,7 +572,7 @@ class _FusedGCN(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dlogits):
-        from .aggregation import colsum
+        from .aggregation import colsum_of
 
         plan = ctx.plan
         L, p = ctx.meta
@@ -565,14 +586,18 @@ class _FusedGCN(torch.autograd.Function):
         g = dlogits if (dlogits.dim() == 2 and dlogits.stride(1) == 1 and dlogits.stride(0) >= dlogits.size(1)) \
             else dlogits.contiguous()
         dx = None
+        db_next = None  # Σ_rows g of the layer below, from the skinny NT that wrote g
         for l in range(L - 1, -1, -1):
             dy = aggregate(plan, g, _lib.AGG_GCN, transpose=True, nodew=dinv)
-            grads[2 * l + 1] = colsum(g)
+            grads[2 * l + 1] = db_next if db_next is not None else colsum_of(g)
+            db_next = None
             (dW, _), _, _, _ = gemm_tn_input(W[l].size(0), hs[l], dy) if l == 0 else gemm_tn(W[l].size(0), hs[l], g=dy)
             grads[2 * l] = dW
             fo, fi = W[l].shape
             if l > 0:  # W [fo, fi] is the row-major [K, N] operand of dh = dy · W
-                if fo <= 8 or fi <= 8:
+                if (fo <= 8 or fi <= 8) and _NT_COLSUM:  # (its column sums: the next layer's bias gradient)
+                    g, db_next = gemm_nt(dy, W[l], fi, mask=hs[l], mask_scale=scale, colsum=True)
+                elif fo <= 8 or fi <= 8:
                     g = gemm_nt(dy, W[l], fi, mask=hs[l], mask_scale=scale)
                 else:
                     g = gemm_nt(dy, W[l], fi)

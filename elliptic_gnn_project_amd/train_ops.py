@@ -11,6 +11,7 @@ Both run on the GPU only; the CPU path keeps the ATen ops.
 from __future__ import annotations
 
 import functools
+import os
 from typing import Iterable
 
 import torch
@@ -42,6 +43,12 @@ def unit_gradient(device) -> torch.Tensor:
     return t
 
 
+# the masked CE also writes its blocks' column sums of dlogits (gnn_masked_ce_colsum_f32): the
+# output layer's bias gradient without a pass over dlogits (GCN / GAT / SAGE-ResBN);
+# GNNMP_CE_COLSUM=0: A/B
+_CE_COLSUM = os.environ.get("GNNMP_CE_COLSUM", "1") != "0"
+
+
 class _MaskedCE(torch.autograd.Function):
     """dlogits is written into the right half of an [N, 2C] buffer (``dl._gnnmp_dz``): the fused
     SAGE backward needs dz = [meanᵀ(dlogits) | dlogits] and fills only the left half (no copy)."""
@@ -58,10 +65,14 @@ class _MaskedCE(torch.autograd.Function):
 
         nblk = max(1, -(-N // 256))  # gnn_masked_ce_f32's partials (256-row blocks)
         deferred = defer_loss_sum(logits.device, ws, nblk, float(inv_denom), loss)  # captured step: at its end
-        _lib.call("gnn_masked_ce_f32", N, C, logits.data_ptr(), C, y.data_ptr(), mask_u8.data_ptr(),
-                  class_w.data_ptr(), float(inv_denom), dl.data_ptr(), 2 * C,
-                  None if deferred else loss.data_ptr(), ws.data_ptr(), ws.numel() * 4,
-                  _lib.stream_handle(logits.device))
+        args = (N, C, logits.data_ptr(), C, y.data_ptr(), mask_u8.data_ptr(), class_w.data_ptr(), float(inv_denom),
+                dl.data_ptr(), 2 * C, None if deferred else loss.data_ptr(), ws.data_ptr(), ws.numel() * 4)
+        ctx.colsum = None
+        if N > 0 and _CE_COLSUM:  # the blocks' column sums of dlogits too: the output layer's bias gradient (colsum_of)
+            ctx.colsum = torch.empty(nblk * C, dtype=torch.float32, device=logits.device)
+            _lib.call("gnn_masked_ce_colsum_f32", *args, ctx.colsum.data_ptr(), _lib.stream_handle(logits.device))
+        else:
+            _lib.call("gnn_masked_ce_f32", *args, _lib.stream_handle(logits.device))
         ctx.save_for_backward(buf)
         ctx.C = C
         return loss
@@ -73,6 +84,8 @@ class _MaskedCE(torch.autograd.Function):
         ones = _ONES.get(g.device)
         if ones is not None and g.data_ptr() == ones.data_ptr():  # d(loss)/d(loss) = 1: dl as is
             dl._gnnmp_dz = buf
+            if ctx.colsum is not None:
+                dl._gnnmp_colsum = ctx.colsum
             return dl, None, None, None, None
         return dl * g, None, None, None, None
 

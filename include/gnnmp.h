@@ -421,9 +421,16 @@ typedef struct gnn_gemm_nt_params {
                                             (the call launches only the GEMM) */
   int32_t planes_exp;                    /* HALF_PAIR (ABI 19): the image holds A * 2^planes_exp
                                             (gnn_split_h2_f32 scale_exp); C is unscaled exactly */
+  float* colsum_part; int64_t colsum_cap; /* optional (ABI 21): the skinny-K form (k1 <= 8, k2 = 0,
+                                            8 < N <= 256; UNSUPPORTED otherwise) also writes the column
+                                            sums of the C it stores (after the whole epilogue), one row per
+                                            block: colsum_part[b * N + n], b < gnn_gemm_nt_colsum_blocks;
+                                            capacity colsum_cap floats.  gnn_colsum_finish_f32 then
+                                            gives Σ_rows C — a layer's bias gradient without a pass over C */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
+gnn_status gnn_gemm_nt_colsum_blocks(const gnn_gemm_nt_params* p, int32_t* nb);  /* 0: no column sums */
 gnn_status gnn_gemm_nt_workspace_size(int64_t N, int64_t k1, int64_t k2, size_t* bytes);
 gnn_status gnn_gemm_nt_f32(const gnn_gemm_nt_params* p, gnn_stream_t stream);
 /* The image-A forms' weight prep alone: writes the B image (split / half-pair / bf16 planes of
@@ -493,6 +500,9 @@ int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p);
 /* ------------------------------------------------------------------------ */
 /* out[c] = sum_r x[r, c]  (bias gradients; deterministic two-stage column sum). */
 gnn_status gnn_colsum_workspace_size(int64_t rows, int64_t F, size_t* bytes);
+/* out[f] = Σ_b part[b * F + f] over b < nblk in gnn_colsum_f32's fixed order (ABI 21: the column
+ * sums a skinny-K gnn_gemm_nt_f32 call wrote, gnn_gemm_nt_params.colsum_part) */
+gnn_status gnn_colsum_finish_f32(const float* part, int32_t nblk, int64_t F, float* out, gnn_stream_t stream);
 gnn_status gnn_colsum_f32(int64_t rows, int64_t F, const float* x, int64_t ldx, float* out,
                           void* workspace, size_t workspace_bytes, gnn_stream_t stream);
 
@@ -559,6 +569,13 @@ gnn_status gnn_masked_ce_workspace_size(int64_t N, size_t* bytes);
  * floats) and the loss is finished later — by gnn_masked_ce_finish, or inside a gnn_clip_adam_f32
  * call (gnn_adam_group.loss_partial) when nothing reads it before the optimizer (a captured step). */
 gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, float inv_denom, float* loss, gnn_stream_t stream);
+/* gnn_masked_ce_f32 (N >= 1) that also writes the per-256-row-block column sums of dlogits,
+ * colsum[b * C + c], b < ceil(N / 256) (ABI 21): gnn_colsum_finish_f32(colsum, ceil(N / 256), C, db)
+ * is then the output layer's bias gradient without a pass over dlogits. */
+gnn_status gnn_masked_ce_colsum_f32(int64_t N, int32_t C, const float* logits, int64_t ldx, const int64_t* y,
+                                    const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
+                                    int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,
+                                    float* colsum, gnn_stream_t stream);
 gnn_status gnn_masked_ce_f32(int64_t N, int32_t C, const float* logits, int64_t ldx, const int64_t* y,
                              const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
                              int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,

@@ -278,3 +278,59 @@ def test_clip_adam_one_launch_counter(device, skip):
     torch.cuda.synchronize()
     assert float(ob.param_groups[0]["step_t"]) == want + 6
     assert int(ob._ws.view(torch.int32)[-1]) == 0
+
+
+@pytest.mark.parametrize("M", [1, 1000, 203_769])
+@pytest.mark.parametrize("N", [64, 12, 128])
+def test_skinny_nt_column_sums(device, M, N):
+    """The skinny-K NT's per-block column sums (gnn_gemm_nt_params.colsum_part, ABI 21) finished by
+    gnn_colsum_finish_f32: Σ_rows C of the masked input gradient it stores (GCN's bias gradient of
+    the layer below) within 1e-6 of a float64 sum of that C, and C itself bit-identical to the call
+    without the sums."""
+    from elliptic_gnn_project_amd.fused import gemm_nt
+
+    g = torch.Generator().manual_seed(M + N)
+    dy = torch.randn(M, 2, generator=g).to(device)
+    W = torch.randn(2, N, generator=g).to(device)
+    h = torch.relu(torch.randn(M, N, generator=g)).to(device)
+    c0 = gemm_nt(dy, W, N, mask=h, mask_scale=2.0)
+    c1, db = gemm_nt(dy, W, N, mask=h, mask_scale=2.0, colsum=True)
+    assert torch.equal(c0, c1)
+    ref = c1.double().sum(0)
+    assert float((db.double() - ref).abs().max()) <= 1e-6 * max(1.0, float(c1.double().abs().sum(0).max()))
+
+
+@pytest.mark.parametrize("N,C", [(1, 2), (1000, 2), (203_769, 2), (5000, 3)])
+def test_ce_column_sums_are_the_bias_gradient(device, N, C):
+    """gnn_masked_ce_colsum_f32's per-block column sums of dlogits, finished by colsum_of: Σ_rows
+    dlogits within 1e-6 of a float64 sum (the output layer's bias gradient), dlogits and the loss
+    bit-identical to gnn_masked_ce_f32's."""
+    from elliptic_gnn_project_amd import train_ops
+    from elliptic_gnn_project_amd.aggregation import colsum_of
+    from elliptic_gnn_project_amd.train_ops import masked_cross_entropy, unit_gradient
+
+    g = torch.Generator().manual_seed(N + C)
+    x = (torch.randn(N, C, generator=g) * 3).to(device).requires_grad_(True)
+    y = torch.randint(0, C, (N,), generator=g).to(device)
+    m = (torch.rand(N, generator=g) < 0.6).to(device)
+    w = torch.rand(C, generator=g).to(device) + 0.5
+    res = []
+    for on in (True, False):
+        train_ops._CE_COLSUM = on
+        try:
+            x.grad = None
+            loss = masked_cross_entropy(x, y, m, w, denom=float(max(int(m.sum()), 1)))
+            seen = {}
+            h = x.register_hook(lambda gr: seen.setdefault("g", gr))
+            loss.backward(unit_gradient(device))
+            h.remove()
+            gr = seen["g"]
+            assert (getattr(gr, "_gnnmp_colsum", None) is not None) == on
+            res.append((float(loss), gr.clone(), colsum_of(gr)))
+        finally:
+            train_ops._CE_COLSUM = True
+    (la, ga, da), (lb, gb, db) = res
+    assert la == lb and torch.equal(ga, gb)
+    ref = ga.double().sum(0)
+    assert float((da.double() - ref).abs().max()) <= 1e-6 * max(1.0, float(ga.double().abs().sum(0).max()))
+    assert float((db.double() - ref).abs().max()) <= 1e-6 * max(1.0, float(ga.double().abs().sum(0).max()))

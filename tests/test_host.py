@@ -153,7 +153,7 @@ STRUCTS = {
                                                "workspace_bytes", "a_dtype", "c_dtype", "mask", "ldmask",
                                                "mask_scale", "a_planes", "planes_ld", "planes_stride",
                                                "planes_col2", "planes_format", "keep_mask",
-                                               "b_ready", "planes_exp"]),
+                                               "b_ready", "planes_exp", "colsum_part", "colsum_cap"]),
     "gnn_adam_tensor": ("GnnAdamTensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel"]),
     "gnn_adam_group": ("GnnAdamGroup", ["num_tensors", "lr", "beta1", "beta2", "eps", "weight_decay", "max_norm",
                                         "tensors", "skip_nonfinite", "bump_counter", "loss_partial", "loss_nblk",
