@@ -862,6 +862,12 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
   const int64_t rr = rok ? r : r0;
   float pdeg = 1.0f, padd[4] = {0.f, 0.f, 0.f, 0.f}, padd2[4] = {0.f, 0.f, 0.f, 0.f}, pbias[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (MODE == GNN_AGG_MEAN) pdeg = fmaxf(a.nodew[rr], 1.0f);
+  // GCN (F <= 2): the row's D^-1/2; each slot's message is (dinv_j · dinv_i) · x_j as in
+  // agg_group_kernel / contrib (the product of the two weights first, PyG's edge_weight), dinv_j
+  // staged in the LDS plane f = 2
+  static_assert(MODE != GNN_AGG_GCN || NF == 2, "GCN rows stage their slot weight in plane 2");
+  float wrow = 1.0f;
+  if constexpr (MODE == GNN_AGG_GCN) wrow = a.nodew[rr];
   if (a.add) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) padd[f] = a.add[rr * a.ld_add + (f < F ? f : 0)];
@@ -899,7 +905,7 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
 #pragma unroll
       for (int f = 0; f < NF; ++f) xv[i][f] = xr[f < F ? f : 0];
       dd[i] = 1.0f;
-      if constexpr (MODE == GNN_AGG_MEAN_BWD) dd[i] = a.nodew[nn[i]];
+      if constexpr (MODE == GNN_AGG_MEAN_BWD || MODE == GNN_AGG_GCN) dd[i] = a.nodew[nn[i]];
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -909,6 +915,7 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
         if constexpr (MODE == GNN_AGG_MEAN_BWD) v = v / fmaxf(dd[i], 1.0f);
         buf[f * kNarrowCap + lane + 64 * i] = v;
       }
+      if constexpr (MODE == GNN_AGG_GCN) buf[2 * kNarrowCap + lane + 64 * i] = dd[i];
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
@@ -917,19 +924,25 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
     const int32_t hi = COOP ? min(hi0, lo + CAP) : hi0;
     // 4 interleaved partial sums: a hub lane's LDS reads pipeline instead of chaining
     float q1[4] = {0.f, 0.f, 0.f, 0.f}, q2[4] = {0.f, 0.f, 0.f, 0.f}, q3[4] = {0.f, 0.f, 0.f, 0.f};
+    // a slot's staged value (GCN: its message, weighted here by the reading row's dinv)
+    auto sv_at = [&](int f, int32_t s, float wr) __attribute__((always_inline)) {
+      const float x = buf[f * kNarrowCap + (s - pb)];
+      if constexpr (MODE == GNN_AGG_GCN) return (buf[2 * kNarrowCap + (s - pb)] * wr) * x;
+      else return x;
+    };
     int32_t k = lo;
     for (; k + 3 < hi; k += 4) {
 #pragma unroll
       for (int f = 0; f < NF; ++f) {  // (features past NF are never staged: NF = 2 reads half)
-        acc[f] += buf[f * kNarrowCap + (k - pb)];
-        q1[f] += buf[f * kNarrowCap + (k + 1 - pb)];
-        q2[f] += buf[f * kNarrowCap + (k + 2 - pb)];
-        q3[f] += buf[f * kNarrowCap + (k + 3 - pb)];
+        acc[f] += sv_at(f, k, wrow);
+        q1[f] += sv_at(f, k + 1, wrow);
+        q2[f] += sv_at(f, k + 2, wrow);
+        q3[f] += sv_at(f, k + 3, wrow);
       }
     }
     for (; k < hi; ++k) {
 #pragma unroll
-      for (int f = 0; f < NF; ++f) acc[f] += buf[f * kNarrowCap + (k - pb)];
+      for (int f = 0; f < NF; ++f) acc[f] += sv_at(f, k, wrow);
     }
 #pragma unroll
     for (int f = 0; f < NF; ++f) acc[f] += (q1[f] + q2[f]) + q3[f];
@@ -939,12 +952,13 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
         const int L = __builtin_ctzll(longm);
         longm &= longm - 1;
         const int32_t s0 = __builtin_amdgcn_readlane(lo, L) + CAP, s1 = __builtin_amdgcn_readlane(hi0, L);
+        const float wL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wrow), L));
         float part[NF];
 #pragma unroll
         for (int f = 0; f < NF; ++f) part[f] = 0.f;
         for (int32_t k2 = s0 + lane; k2 < s1; k2 += 64) {
 #pragma unroll
-          for (int f = 0; f < NF; ++f) part[f] += buf[f * kNarrowCap + (k2 - pb)];
+          for (int f = 0; f < NF; ++f) part[f] += sv_at(f, k2, wL);
         }
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
@@ -1201,7 +1215,8 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
                        bool* pieces_done) {
   if (a.nrows == 0 || a.F == 0) return GNN_OK;
   if (sp) return launch_mode_split<MODE>(a, vec, st, sp);
-  if (a.F <= 4 && (MODE == GNN_AGG_MEAN || MODE == GNN_AGG_MEAN_BWD || MODE == GNN_AGG_SUM)) {
+  if ((a.F <= 4 && (MODE == GNN_AGG_MEAN || MODE == GNN_AGG_MEAN_BWD || MODE == GNN_AGG_SUM)) ||
+      (a.F <= 2 && MODE == GNN_AGG_GCN)) {  // (GCN: the 2-class logits and their transpose, r54)
     // slots staged per pass: 512 / 128 measured 15.3 / 17.2 us vs 16.1 at 256 (r10, warm)
     const unsigned nb = (unsigned)ceil_div(a.nrows, 256);
     // rows longer than 32 slots of a pass: the tail by the whole wave (r17 lab, SAGE preset F = 2:
@@ -1209,11 +1224,11 @@ gnn_status launch_mode(const AggArgs& a, int vec, hipStream_t st, const gnn_spli
 #ifdef GNNMP_AGG_LAB
     if (g_agg_lab_variant == 15) {
       if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2, 256, false><<<nb, 256, 0, st>>>(a);
-      else agg_narrow_lds_kernel<MODE, 4, 256, false><<<nb, 256, 0, st>>>(a);
+      else if constexpr (MODE != GNN_AGG_GCN) agg_narrow_lds_kernel<MODE, 4, 256, false><<<nb, 256, 0, st>>>(a);
     } else
 #endif
     if (a.F <= 2) agg_narrow_lds_kernel<MODE, 2, 256, true><<<nb, 256, 0, st>>>(a);
-    else agg_narrow_lds_kernel<MODE, 4, 256, true><<<nb, 256, 0, st>>>(a);
+    else if constexpr (MODE != GNN_AGG_GCN) agg_narrow_lds_kernel<MODE, 4, 256, true><<<nb, 256, 0, st>>>(a);
   } else if (a.F <= 8) {
     int64_t blocks = ceil_div(a.nrows * kGroup, 256);
     if (blocks > ((int64_t)1 << 20)) blocks = (int64_t)1 << 20;
