@@ -296,6 +296,11 @@ SIGNATURES = {
         ctypes.c_int,
         [c_i64, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr],
     ),
+    "gnn_gcn_out_ce_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
+         ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
+    ),
     "gnn_masked_ce_colsum_f32": (
         ctypes.c_int,
         [c_i64, c_i32, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr,

@@ -128,6 +128,7 @@ struct AggArgs {
   const int64_t* ce_y; const uint8_t* ce_mask; const float* ce_w; float ce_inv;
   float* ce_dl; int64_t ce_ldd; float* ce_part;
   float* ce_u; int64_t ce_ldu;  // optional: dl / max(deg, 1) per row (the transposed mean's per-slot term)
+  float* ce_cs;                 // optional: per-256-row-block column sums of dl, [block][C] (the bias gradient)
 };
 
 __device__ __forceinline__ uint64_t agg_seed(const AggArgs& a) {
@@ -996,11 +997,11 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
     const int64_t r = r0 + lane;
     const int C = a.F;
     float l = 0.f;
+    float dlv[4] = {0.f, 0.f, 0.f, 0.f};
     if (r < a.nrows) {  // masked_ce_kernel<C>: loss_r = -w[y]·log_softmax[y], dl = w[y]/n·(softmax - onehot)
       const int64_t tg = ce_t;
       const bool on = ce_m != 0 && tg >= 0 && tg < C;
       const float wt = tg == 0 ? ce_w[0] : tg == 1 ? ce_w[1] : tg == 2 ? ce_w[2] : ce_w[3];
-      float dlv[4] = {0.f, 0.f, 0.f, 0.f};
       l = masked_ce_row<4>(lg, C, tg, on, on ? wt : 0.f, a.ce_inv, a.ce_dl + r * a.ce_ldd, dlv);
       if (a.ce_u) {  // MEAN_BWD's v / max(deg, 1) of this row, the same division (deg is MEAN's nodew)
 #pragma unroll
@@ -1016,6 +1017,21 @@ __global__ __launch_bounds__(256) void agg_narrow_lds_kernel(AggArgs a) {
       float t = 0.f;
       for (int i = 0; i < 4; ++i) t += cesh[i];
       a.ce_part[blockIdx.x] = t;
+    }
+    if (a.ce_cs) {  // the block's column sums of dl: each wave's rows by its butterfly, the waves in order
+      __shared__ float cssh[4][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float v = c < C ? dlv[c] : 0.f;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) cssh[c][w] = v;
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < C) {
+        float t = 0.f;
+        for (int i = 0; i < 4; ++i) t += cssh[threadIdx.x][i];
+        a.ce_cs[(int64_t)blockIdx.x * C + threadIdx.x] = t;
+      }
     }
   }
 }
@@ -1687,6 +1703,33 @@ extern "C" gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* 
   else agg_narrow_lds_kernel<GNN_AGG_MEAN, 4, 256, true, true><<<(unsigned)nblk, 256, 0, st>>>(a);
   const gnn_status s = hip_check(hipGetLastError(), fn);
   if (s != GNN_OK || !loss) return s;  // loss NULL: the partials stay in the workspace (ClipAdam / finish)
+  return gnn_masked_ce_finish(partial, nblk, inv_denom, loss, stream);
+}
+
+extern "C" gnn_status gnn_gcn_out_ce_f32(const gnn_graph* g, const float* dinv, const float* t, int64_t ldt,
+                                         int32_t C, const float* bias, float* logits, int64_t ldo,
+                                         const int64_t* y, const uint8_t* mask, const float* class_w,
+                                         float inv_denom, float* dlogits, int64_t ld_d, float* colsum, float* loss,
+                                         void* workspace, size_t workspace_bytes, gnn_stream_t stream) {
+  const char* fn = __func__;
+  if (!g || !dinv) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or dinv");
+  if (C < 1 || C > 2 || ldt < C || ldo < C || ld_d < C) return fail(GNN_ERR_INVALID_ARG, fn, "needs 1 <= C <= 2");
+  const int64_t N = g->num_nodes;
+  if (N < 1 || !t || !logits || !y || !mask || !class_w || !dlogits) return fail(GNN_ERR_INVALID_ARG, fn, "null operand / N < 1");
+  if (!g->rowptr || (g->num_slots > 0 && !g->col)) return fail(GNN_ERR_INVALID_ARG, fn, "plan arrays null");
+  const int nblk = (int)ceil_div(N, 256);
+  if (!workspace || workspace_bytes < (size_t)nblk * sizeof(float)) return fail(GNN_ERR_WORKSPACE, fn, "workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* partial = static_cast<float*>(workspace);
+  AggArgs a{};
+  a.ptr = g->rowptr; a.nbr = g->col; a.nodew = dinv; a.heads = 1; a.chan = C;
+  a.x = t; a.ldx = ldt; a.y = logits; a.ldy = ldo; a.bias = bias;
+  a.nrows = N; a.F = C;
+  a.ce_y = y; a.ce_mask = mask; a.ce_w = class_w; a.ce_inv = inv_denom; a.ce_dl = dlogits; a.ce_ldd = ld_d;
+  a.ce_part = partial; a.ce_cs = colsum;
+  agg_narrow_lds_kernel<GNN_AGG_GCN, 2, 256, true, true><<<(unsigned)nblk, 256, 0, st>>>(a);
+  const gnn_status s = hip_check(hipGetLastError(), fn);
+  if (s != GNN_OK || !loss) return s;
   return gnn_masked_ce_finish(partial, nblk, inv_denom, loss, stream);
 }
 

@@ -58,6 +58,9 @@ _SIDE_PREP = os.environ.get("GNNMP_SIDE_PREP", "0") == "1"
 # GCN backward: the skinny masked-gradient NT also writes its column sums (the layer below's bias
 # gradient, gnn_gemm_nt_params.colsum_part) instead of a separate colsum pass; GNNMP_NT_COLSUM=0: A/B
 _NT_COLSUM = os.environ.get("GNNMP_NT_COLSUM", "1") != "0"
+# GCN's output aggregation and the step's masked CE in one launch (gnn_gcn_out_ce_f32) under a
+# fused_ce_target; GNNMP_GCN_CE=0: A/B
+_GCN_CE = os.environ.get("GNNMP_GCN_CE", "1") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -563,7 +566,18 @@ class _FusedGCN(torch.autograd.Function):
             hs.append(aggregate(plan, y, _lib.AGG_GCN, nodew=dinv, bias=b[l], relu=True,
                                 dropout_p=dropout_p, seed=seeds[l], seed_ptr=seed_ctr))
         y = gemm_nt(hs[-1], None, W[-1].size(0), w1=W[-1])
-        logits = aggregate(plan, y, _lib.AGG_GCN, nodew=dinv, bias=b[-1])
+        from .train_ops import ce_target, gcn_out_ce
+
+        tgt = ce_target()
+        if tgt is not None and any(ctx.needs_input_grad) and y.dtype == torch.float32 and y.size(1) <= 2 \
+                and y.size(0) > 0 and _GCN_CE:
+            # the step's masked CE in the output aggregation's launch (train_ops.fused_ce_target)
+            e0 = KernelTimer.begin()
+            logits, ce = gcn_out_ce(plan, y, b[-1], tgt)
+            KernelTimer.end(e0, ("agg", _lib.AGG_GCN, False, y.size(1)), agg_bytes(plan, y.size(1), _lib.AGG_GCN, False, False))
+            logits._gnnmp_ce = ce
+        else:
+            logits = aggregate(plan, y, _lib.AGG_GCN, nodew=dinv, bias=b[-1])
         ctx.plan = plan
         ctx.meta = (L, float(dropout_p))
         ctx.save_for_backward(*hs, *params)

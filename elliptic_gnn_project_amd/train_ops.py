@@ -102,6 +102,7 @@ class _PrecomputedCE(torch.autograd.Function):
         ctx.C = buf.size(1) // 2
         ctx.ws = ws  # the loss partials (a deferred loss reads them at the step's end)
         ctx.u = getattr(buf, "_gnnmp_u", None)  # dlogits / max(deg, 1), written by the same launch
+        ctx.colsum = getattr(buf, "_gnnmp_colsum", None)  # dlogits' block column sums (gcn_out_ce)
         return loss
 
     @staticmethod
@@ -112,6 +113,8 @@ class _PrecomputedCE(torch.autograd.Function):
         if ones is not None and g.data_ptr() == ones.data_ptr():
             dl._gnnmp_dz = buf
             dl._gnnmp_u = ctx.u
+            if ctx.colsum is not None:
+                dl._gnnmp_colsum = ctx.colsum
             return dl, None
         return dl * g, None
 
@@ -175,6 +178,31 @@ def sage_out_mean_ce(plan, z: torch.Tensor, C: int, bias, target):
               buf.data_ptr() + C * 4, 2 * C, u.data_ptr(), C, None if deferred else loss.data_ptr(), ws.data_ptr(),
               ws.numel() * 4, _lib.stream_handle(dev))
     buf._gnnmp_u = u
+    return logits, (key, loss, buf, ws)
+
+
+def gcn_out_ce(plan, t: torch.Tensor, bias, target):
+    """logits = Â·t + bias (GCN's output aggregation over a LOOPS_REPLACE plan, C <= 2) and the
+    target's masked CE in one launch (include/gnnmp.h gnn_gcn_out_ce_f32), dlogits' block column
+    sums beside them (the output bias gradient, aggregation.colsum_of).  Returns (logits, ce) — ce
+    for _PrecomputedCE."""
+    from .fused import defer_loss_sum
+
+    key, y, m8, w, inv = target
+    N, C, dev = t.size(0), t.size(1), t.device
+    logits = torch.empty((N, C), dtype=torch.float32, device=dev)
+    buf = torch.empty((N, 2 * C), dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    ws = _ws(_ce_ws_bytes(N), dev)
+    nblk = max(1, -(-N // 256))
+    cs = torch.empty(nblk * C, dtype=torch.float32, device=dev) if _CE_COLSUM else None
+    deferred = defer_loss_sum(dev, ws, nblk, inv, loss)
+    _lib.call("gnn_gcn_out_ce_f32", plan.c_graph, plan.dinv.data_ptr(), t.data_ptr(), int(t.stride(0)), int(C),
+              _lib.ptr(bias), logits.data_ptr(), C, y.data_ptr(), m8.data_ptr(), w.data_ptr(), float(inv),
+              buf.data_ptr() + C * 4, 2 * C, _lib.ptr(cs), None if deferred else loss.data_ptr(), ws.data_ptr(),
+              ws.numel() * 4, _lib.stream_handle(dev))
+    if cs is not None:
+        buf._gnnmp_colsum = cs
     return logits, (key, loss, buf, ws)
 
 

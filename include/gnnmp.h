@@ -572,6 +572,14 @@ gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, float inv_de
 /* gnn_masked_ce_f32 (N >= 1) that also writes the per-256-row-block column sums of dlogits,
  * colsum[b * C + c], b < ceil(N / 256) (ABI 21): gnn_colsum_finish_f32(colsum, ceil(N / 256), C, db)
  * is then the output layer's bias gradient without a pass over dlogits. */
+/* GCN's output layer and the masked CE in one launch (ABI 21): logits = Â·t + bias (gnn_aggregate_f32
+ * GCN over a LOOPS_REPLACE plan, dinv = gnn_gcn_norm_f32, 1 <= C <= 2) and gnn_masked_ce_f32 of
+ * them with its workspace contract (loss NULL: partials deferred); colsum (optional): the
+ * per-256-row-block column sums of dlogits as gnn_masked_ce_colsum_f32 writes them. */
+gnn_status gnn_gcn_out_ce_f32(const gnn_graph* g, const float* dinv, const float* t, int64_t ldt, int32_t C,
+                              const float* bias, float* logits, int64_t ldo, const int64_t* y, const uint8_t* mask,
+                              const float* class_w, float inv_denom, float* dlogits, int64_t ld_d, float* colsum,
+                              float* loss, void* workspace, size_t workspace_bytes, gnn_stream_t stream);
 gnn_status gnn_masked_ce_colsum_f32(int64_t N, int32_t C, const float* logits, int64_t ldx, const int64_t* y,
                                     const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
                                     int64_t ld_d, float* loss, void* workspace, size_t workspace_bytes,
