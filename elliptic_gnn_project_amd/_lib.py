@@ -236,7 +236,7 @@ SIGNATURES = {
     "gnn_sage_out_mean_ce_f32": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_ptr, c_ptr, c_i64, c_i32, c_ptr, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
-         ctypes.c_float, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_size, c_ptr],
+         ctypes.c_float, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
     "gnn_sage_mean_bwd_f32": (
         ctypes.c_int,

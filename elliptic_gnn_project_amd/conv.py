@@ -15,6 +15,7 @@ add_self_loops=True, fill_value='mean').  Anything else raises.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -25,6 +26,10 @@ from .aggregation import (aggregate, colsum, colsum_of, gat_attention, gcn_aggre
                           masked_mean_aggregate, mean_aggregate)
 from .graph import GraphPlan, get_plan
 from .linear import Linear, linear, linear2, linear_stacked
+
+# a transform-first output conv under the step's fused_ce_target runs its mean and the masked CE in
+# one launch (gnn_sage_out_mean_ce_f32, as the fused 2-layer SAGE does); GNNMP_OUT_CE=0: A/B
+_OUT_CE = os.environ.get("GNNMP_OUT_CE", "1") != "0"
 
 __all__ = ["SAGEConv", "GCNConv", "GATConv"]
 
@@ -49,6 +54,16 @@ class _MeanAggRootBias(torch.autograd.Function):
         ctx.plan = plan
         ctx.fo = fo
         ctx.has_bias = bias is not None
+        from .train_ops import ce_target, sage_out_mean_ce
+
+        tgt = ce_target()
+        if (tgt is not None and _OUT_CE and any(ctx.needs_input_grad) and fo <= 4 and y.size(0) > 0
+                and y.dtype == torch.float32 and y.stride(1) == 1):
+            # a network's output conv under the step's fused_ce_target (SAGE-ResBN): the mean and the
+            # masked CE in one launch, dlogits' column sums beside them (the bias gradient)
+            out, ce = sage_out_mean_ce(plan, y, fo, bias, tgt, colsum=True)
+            out._gnnmp_ce = ce
+            return out
         return aggregate(plan, y[:, :fo], _lib.AGG_MEAN, nodew=plan.deg, addend=y[:, fo:], bias=bias)
 
     @staticmethod
@@ -63,7 +78,11 @@ class _MeanAggRootBias(torch.autograd.Function):
         if (ctx.needs_input_grad[0] and buf is not None and buf.shape == (N, 2 * fo)
                 and dout.stride() == (2 * fo, 1) and dout.data_ptr() == buf.data_ptr() + fo * buf.element_size()):
             dy = buf
-            aggregate(plan, dout, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dy[:, :fo])
+            u = getattr(dout, "_gnnmp_u", None)
+            if u is not None and u.shape == (N, fo):  # dlogits / max(deg, 1) from the fused CE: meanᵀ = CSC sum
+                aggregate(plan, u, _lib.AGG_SUM, transpose=True, out=dy[:, :fo])
+            else:
+                aggregate(plan, dout, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dy[:, :fo])
         elif ctx.needs_input_grad[0]:
             dout = dout.contiguous()
             dy = torch.empty((N, 2 * fo), dtype=torch.float32, device=dout.device)

@@ -1674,7 +1674,7 @@ extern "C" gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* 
                                                int32_t C, const float* bias, float* logits, int64_t ldo,
                                                const int64_t* y, const uint8_t* mask, const float* class_w,
                                                float inv_denom, float* dlogits, int64_t ld_d, float* u, int64_t ldu,
-                                               float* loss, void* workspace, size_t workspace_bytes,
+                                               float* colsum, float* loss, void* workspace, size_t workspace_bytes,
                                                gnn_stream_t stream) {
   const char* fn = __func__;
   if (!g || !deg) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or deg");
@@ -1699,6 +1699,7 @@ extern "C" gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* 
   a.ce_part = partial;
   if (u && ldu < C) return fail(GNN_ERR_INVALID_ARG, fn, "ldu < C");
   a.ce_u = u; a.ce_ldu = ldu;
+  a.ce_cs = colsum;
   if (C <= 2) agg_narrow_lds_kernel<GNN_AGG_MEAN, 2, 256, true, true><<<(unsigned)nblk, 256, 0, st>>>(a);
   else agg_narrow_lds_kernel<GNN_AGG_MEAN, 4, 256, true, true><<<(unsigned)nblk, 256, 0, st>>>(a);
   const gnn_status s = hip_check(hipGetLastError(), fn);

@@ -159,9 +159,10 @@ def ce_target():
     return _CE_TARGET[0]
 
 
-def sage_out_mean_ce(plan, z: torch.Tensor, C: int, bias, target):
+def sage_out_mean_ce(plan, z: torch.Tensor, C: int, bias, target, colsum: bool = False):
     """logits = mean_{j->i} z[j, :C] + z[i, C:] + bias and the target's masked CE in one launch
-    (include/gnnmp.h gnn_sage_out_mean_ce_f32).  Returns (logits, ce) — ce for _PrecomputedCE."""
+    (include/gnnmp.h gnn_sage_out_mean_ce_f32).  Returns (logits, ce) — ce for _PrecomputedCE.
+    ``colsum``: also dlogits' block column sums (the output bias gradient, aggregation.colsum_of)."""
     from .fused import defer_loss_sum
 
     key, y, m8, w, inv = target
@@ -173,11 +174,14 @@ def sage_out_mean_ce(plan, z: torch.Tensor, C: int, bias, target):
     ws = _ws(_ce_ws_bytes(N), dev)
     nblk = max(1, -(-N // 256))
     deferred = defer_loss_sum(dev, ws, nblk, inv, loss)  # captured step with defer_loss: at its end
+    cs = torch.empty(nblk * C, dtype=torch.float32, device=dev) if (colsum and _CE_COLSUM) else None
     _lib.call("gnn_sage_out_mean_ce_f32", plan.c_graph, plan.deg.data_ptr(), z.data_ptr(), int(z.stride(0)), int(C),
               _lib.ptr(bias), logits.data_ptr(), C, y.data_ptr(), m8.data_ptr(), w.data_ptr(), float(inv),
-              buf.data_ptr() + C * 4, 2 * C, u.data_ptr(), C, None if deferred else loss.data_ptr(), ws.data_ptr(),
-              ws.numel() * 4, _lib.stream_handle(dev))
+              buf.data_ptr() + C * 4, 2 * C, u.data_ptr(), C, _lib.ptr(cs), None if deferred else loss.data_ptr(),
+              ws.data_ptr(), ws.numel() * 4, _lib.stream_handle(dev))
     buf._gnnmp_u = u
+    if cs is not None:
+        buf._gnnmp_colsum = cs
     return logits, (key, loss, buf, ws)
 
 

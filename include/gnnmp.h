@@ -253,11 +253,13 @@ typedef enum {
  * 1 <= C <= 4, ldz >= 2C; workspace: gnn_masked_ce_workspace_size(num_nodes).  u (optional, ABI 20,
  * [N, C], ldu >= C): dlogits / max(deg, 1) per row — the transposed mean's per-slot term, so the
  * backward's meanᵀ(dlogits) is a plain CSC sum of u (gnn_aggregate_f32 SUM, transpose), bit for bit
- * the MEAN_BWD result, without the per-slot degree gather and division. */
+ * the MEAN_BWD result, without the per-slot degree gather and division.  colsum (optional, ABI 21):
+ * dlogits' per-256-row-block column sums as gnn_masked_ce_colsum_f32 writes them (the output
+ * bias gradient through gnn_colsum_finish_f32: SAGE-ResBN's output conv). */
 gnn_status gnn_sage_out_mean_ce_f32(const gnn_graph* g, const float* deg, const float* z, int64_t ldz, int32_t C,
                                     const float* bias, float* logits, int64_t ldo, const int64_t* y,
                                     const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
-                                    int64_t ld_d, float* u, int64_t ldu, float* loss, void* workspace,
+                                    int64_t ld_d, float* u, int64_t ldu, float* colsum, float* loss, void* workspace,
                                     size_t workspace_bytes, gnn_stream_t stream);
 
 /* Named forms of the above (what an FFI binding of SAGEConv would call). */

@@ -177,3 +177,44 @@ def test_gcn_step_with_fused_ce_equals_separate(device, dropout, unit):
     assert torch.equal(l1, l2) and torch.equal(s1, s2)
     for k in g1:
         assert torch.equal(g1[k], g2[k]), k
+
+
+@pytest.mark.parametrize("unit", [False, True])
+def test_resbn_step_with_fused_out_ce_equals_separate(device, unit):
+    """SAGE-ResBN (configs[3]): its transform-first output conv runs the mean and the masked CE in
+    one launch under loss_fn.target (gnn_sage_out_mean_ce_f32 with dlogits' column sums; the
+    backward's meanᵀ as the CSC sum of u) — bit-identical logits, loss and gradients to the two
+    launches (conv._OUT_CE off)."""
+    from elliptic_gnn_project_amd import conv
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn, build_model
+    from elliptic_gnn_project_amd.train_ops import unit_gradient
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=6000, num_edges=7000, seed=8),
+                          dict(use_time_scalar=False, symmetrize_edges=True, train_window_k=8)).to(device)
+    cfg = dict(arch="sage_resbn", hidden_dim=64, layers=3, dropout=0.2, time_embed_dim=2, time_embed_type="sin",
+               max_timestep=49)
+    cw = pyg_ref.class_weight(data.y[data.train_mask].cpu())
+    denom = float(data.train_mask.sum())
+    res = []
+    for on in (True, False):
+        conv._OUT_CE = on
+        try:
+            torch.manual_seed(3)
+            model = build_model("sage_resbn", data.x.size(1), cfg).to(device)
+            loss_fn = _make_loss_fn({}, cw, model, 1, 34)
+            model.train()
+            torch.manual_seed(9)
+            with loss_fn.target(data.y, data.train_mask, denom):
+                logits = model(data.x, data.edge_index, data.timestep)
+            assert (getattr(logits, "_gnnmp_ce", None) is not None) == on
+            loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
+            loss.backward(unit_gradient(device)) if unit else loss.backward()
+            res.append((logits.detach().clone(), loss.detach().clone(),
+                        {k: p.grad.clone() for k, p in model.named_parameters()}))
+        finally:
+            conv._OUT_CE = True
+    (l1, s1, g1), (l2, s2, g2) = res
+    assert torch.equal(l1, l2) and torch.equal(s1, s2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
