@@ -338,6 +338,12 @@ SIGNATURES = {
         [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, ctypes.c_float, ctypes.c_uint64,
          c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
     ),
+    "gnn_bn_act_bwd_colsum_blocks": (ctypes.c_int, [c_i64, c_i64, ctypes.POINTER(c_i32)]),
+    "gnn_bn_act_bwd_colsum_f32": (
+        ctypes.c_int,
+        [c_ptr, c_i64, c_ptr, c_i64, c_i64, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, ctypes.c_float, ctypes.c_uint64,
+         c_ptr, c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_ptr],
+    ),
     "gnn_time_inject_sin_f32": (
         ctypes.c_int,
         [c_ptr, c_i64, c_i64, c_i64, c_ptr, c_i64, c_i64, c_ptr, c_i64, c_ptr],

@@ -214,24 +214,39 @@ __global__ __launch_bounds__(kBnThreads) void bn_bwd_partial_kernel(BnArgs a, in
 }
 
 // backward apply: dz = w·invstd·(dy − Σdy/n − x̂·Σdy·x̂/n)  (sums over every rank's rows)
+// colsum (optional, C <= kBnThreads): the block's column sums of the dz it stores, colsum[b·C + c]
+// (each thread's rows in order, the row lanes in order): the bias gradient of the conv below
+// (SAGE-ResBN layer 0's transform-first conv) without a pass over dz
 __global__ __launch_bounds__(kBnThreads) void bn_bwd_apply_kernel(BnArgs a, const float* __restrict__ sums,
-                                                                 const double* __restrict__ n_total) {
+                                                                 const double* __restrict__ n_total,
+                                                                 float* __restrict__ colsum = nullptr) {
+  __shared__ float csh[kBnThreads];
   const uint64_t seed = a.dropout ? bn_seed(a) : 0;
   const float inv_n = (float)(1.0 / *n_total);
   const int C = a.C;
   const int cols = C < kBnThreads ? C : kBnThreads;
   const int lanes = kBnThreads / cols;
   const int cl = threadIdx.x % cols, rl = threadIdx.x / cols;
-  if (rl >= lanes) return;
-  for (int cb = 0; cb < C; cb += cols) {
+  float cs = 0.f;
+  for (int cb = 0; rl < lanes && cb < C; cb += cols) {
     const int c = cb + cl;
     if (c >= C) break;
     const float k = a.weight[c] * a.invstd[c], s0 = sums[c] * inv_n, s1 = sums[C + c] * inv_n;
     for (int64_t r = (int64_t)blockIdx.x * lanes + rl; r < a.N; r += (int64_t)gridDim.x * lanes) {
       float dy, xh;
       bn_dy(a, seed, r, c, r * C + c, dy, xh);
-      a.out[r * a.ldo + c] = k * (dy - s0 - xh * s1);
+      const float v = k * (dy - s0 - xh * s1);
+      a.out[r * a.ldo + c] = v;
+      cs += v;
     }
+  }
+  if (!colsum) return;  // kernel-uniform (C <= kBnThreads: one column pass)
+  csh[threadIdx.x] = rl < lanes ? cs : 0.f;
+  __syncthreads();
+  if (rl == 0) {
+    float t = csh[cl];
+    for (int l = 1; l < lanes; ++l) t += csh[l * cols + cl];
+    colsum[(int64_t)blockIdx.x * C + cl] = t;
   }
 }
 
@@ -355,20 +370,49 @@ extern "C" gnn_status gnn_bn_act_bwd_reduce_f32(const float* dh, int64_t lddh, c
   return GNN_OK;
 }
 
+extern "C" gnn_status gnn_bn_act_bwd_colsum_blocks(int64_t N, int64_t C, int32_t* nb) {
+  if (!nb || N < 1 || C < 1) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
+  *nb = C <= kBnThreads ? (int32_t)bn_grid(N, C) : 0;
+  return GNN_OK;
+}
+
+static gnn_status bn_act_bwd(const char* fn, const float* dh, int64_t lddh, const float* z, int64_t ldz, int64_t N,
+                             int64_t C, const float* mean, const float* invstd, const float* weight, const float* bias,
+                             float dropout_p, uint64_t seed, const int64_t* seed_ptr, const float* sums,
+                             const double* n_total, float* dz, int64_t lddz, float* colsum, gnn_stream_t stream);
+
+extern "C" gnn_status gnn_bn_act_bwd_colsum_f32(const float* dh, int64_t lddh, const float* z, int64_t ldz, int64_t N,
+                                                int64_t C, const float* mean, const float* invstd, const float* weight,
+                                                const float* bias, float dropout_p, uint64_t seed,
+                                                const int64_t* seed_ptr, const float* sums, const double* n_total,
+                                                float* dz, int64_t lddz, float* colsum, gnn_stream_t stream) {
+  if (!colsum || C > kBnThreads || N < 1) return fail(GNN_ERR_INVALID_ARG, __func__, "colsum needs N >= 1, C <= 256");
+  return bn_act_bwd(__func__, dh, lddh, z, ldz, N, C, mean, invstd, weight, bias, dropout_p, seed, seed_ptr, sums,
+                    n_total, dz, lddz, colsum, stream);
+}
+
 extern "C" gnn_status gnn_bn_act_bwd_f32(const float* dh, int64_t lddh, const float* z, int64_t ldz, int64_t N, int64_t C,
                                          const float* mean, const float* invstd, const float* weight, const float* bias,
                                          float dropout_p, uint64_t seed, const int64_t* seed_ptr, const float* sums,
                                          const double* n_total, float* dz, int64_t lddz, gnn_stream_t stream) {
+  return bn_act_bwd(__func__, dh, lddh, z, ldz, N, C, mean, invstd, weight, bias, dropout_p, seed, seed_ptr, sums,
+                    n_total, dz, lddz, nullptr, stream);
+}
+
+static gnn_status bn_act_bwd(const char* fn, const float* dh, int64_t lddh, const float* z, int64_t ldz, int64_t N,
+                             int64_t C, const float* mean, const float* invstd, const float* weight, const float* bias,
+                             float dropout_p, uint64_t seed, const int64_t* seed_ptr, const float* sums,
+                             const double* n_total, float* dz, int64_t lddz, float* colsum, gnn_stream_t stream) {
+  const char* __func_name = fn;
   BnArgs a{};
-  gnn_status s = bn_args(__func__, N, C, mean, invstd, weight, bias, dropout_p, seed, seed_ptr, a);
+  gnn_status s = bn_args(__func_name, N, C, mean, invstd, weight, bias, dropout_p, seed, seed_ptr, a);
   if (s != GNN_OK) return s;
   if (!dh || !z || !sums || !dz || !n_total || lddh < C || ldz < C || lddz < C)
-    return fail(GNN_ERR_INVALID_ARG, __func__, "bad dh / z / sums / dz / n");
+    return fail(GNN_ERR_INVALID_ARG, __func_name, "bad dh / z / sums / dz / n");
   if (N == 0) return GNN_OK;
   a.dh = dh; a.lddh = lddh; a.z = z; a.ldz = ldz; a.out = dz; a.ldo = lddz;
-  bn_bwd_apply_kernel<<<bn_grid(N, C), kBnThreads, 0, (hipStream_t)stream>>>(a, sums, n_total);
-  GNN_LAUNCH_CHECK();
-  return GNN_OK;
+  bn_bwd_apply_kernel<<<bn_grid(N, C), kBnThreads, 0, (hipStream_t)stream>>>(a, sums, n_total, colsum);
+  return hip_check(hipGetLastError(), __func_name);
 }
 
 // ---- K13: SAGEResBNNet's input h0 = [x | sinusoid(t)] (src/models/gnn.py:145-160 the fixed

@@ -61,6 +61,9 @@ _NT_COLSUM = os.environ.get("GNNMP_NT_COLSUM", "1") != "0"
 # GCN's output aggregation and the step's masked CE in one launch (gnn_gcn_out_ce_f32) under a
 # fused_ce_target; GNNMP_GCN_CE=0: A/B
 _GCN_CE = os.environ.get("GNNMP_GCN_CE", "1") != "0"
+# K12's backward also writes dz's column sums (the bias gradient of the conv below, SAGE-ResBN
+# layer 0); GNNMP_BN_COLSUM=0: A/B
+_BN_COLSUM = os.environ.get("GNNMP_BN_COLSUM", "1") != "0"
 _SIDE_STREAMS = {}
 
 
@@ -903,8 +906,17 @@ class _BNActRes(torch.autograd.Function):
         # below assembles its GEMM gradient [meanᵀ(dz) | dz] in that buffer without a copy
         zbuf = torch.empty((N, 2 * C), dtype=torch.float32, device=dev)
         dz = zbuf[:, C:]
-        _lib.call("gnn_bn_act_bwd_f32", dh.data_ptr(), C, z.data_ptr(), C, N, C, *args, sums.data_ptr(),
-                  stats[2 * C:].data_ptr(), dz.data_ptr(), 2 * C, st)
+        nb = ctypes.c_int32(0)
+        if _BN_COLSUM and N > 0:
+            _lib.call("gnn_bn_act_bwd_colsum_blocks", N, C, ctypes.byref(nb))
+        if nb.value > 0:  # dz's block column sums too: the bias gradient of the conv below (colsum_of)
+            cs = torch.empty(nb.value * C, dtype=torch.float32, device=dev)
+            _lib.call("gnn_bn_act_bwd_colsum_f32", dh.data_ptr(), C, z.data_ptr(), C, N, C, *args, sums.data_ptr(),
+                      stats[2 * C:].data_ptr(), dz.data_ptr(), 2 * C, cs.data_ptr(), st)
+            dz._gnnmp_colsum = cs
+        else:
+            _lib.call("gnn_bn_act_bwd_f32", dh.data_ptr(), C, z.data_ptr(), C, N, C, *args, sums.data_ptr(),
+                      stats[2 * C:].data_ptr(), dz.data_ptr(), 2 * C, st)
         dz._gnnmp_dz = zbuf
         return dz, (dh if has_r else None), local[C:], local[:C], None, None, None, None, None
 

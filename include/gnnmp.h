@@ -549,6 +549,15 @@ gnn_status gnn_bn_act_bwd_f32(const float* dh, int64_t lddh, const float* z, int
                               const float* mean, const float* invstd, const float* weight, const float* bias,
                               float dropout_p, uint64_t seed, const int64_t* seed_ptr, const float* sums,
                               const double* n_total, float* dz, int64_t lddz, gnn_stream_t stream);
+/* The same, also writing the column sums of the dz it stores per block, colsum[b·C + c] for
+ * b < gnn_bn_act_bwd_colsum_blocks(N, C) (N >= 1, C <= 256; ABI 21): the bias gradient of the
+ * conv that produced z, through gnn_colsum_finish_f32, without a pass over dz. */
+gnn_status gnn_bn_act_bwd_colsum_blocks(int64_t N, int64_t C, int32_t* nb);
+gnn_status gnn_bn_act_bwd_colsum_f32(const float* dh, int64_t lddh, const float* z, int64_t ldz, int64_t N, int64_t C,
+                                     const float* mean, const float* invstd, const float* weight, const float* bias,
+                                     float dropout_p, uint64_t seed, const int64_t* seed_ptr, const float* sums,
+                                     const double* n_total, float* dz, int64_t lddz, float* colsum,
+                                     gnn_stream_t stream);
 
 /* K13: SAGEResBNNet's input with the fixed sinusoid time features, out = [x | te(t)] in one pass
  * (replaces SAGEResBN._time_embed / torch.cat of src/models/gnn.py:145-160, 172-176):

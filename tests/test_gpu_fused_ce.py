@@ -218,3 +218,48 @@ def test_resbn_step_with_fused_out_ce_equals_separate(device, unit):
     assert torch.equal(l1, l2) and torch.equal(s1, s2)
     for k in g1:
         assert torch.equal(g1[k], g2[k]), k
+
+
+def test_resbn_bn_colsum_bias_gradient(device):
+    """SAGE-ResBN: K12's backward writing dz's block column sums (gnn_bn_act_bwd_colsum_f32), which
+    become the layer-0 conv's bias gradient (colsum_of): every other gradient bit-identical to the
+    separate colsum pass, that bias gradient (a BN-cancelled sum: analytically 0) within 1e-6 of it
+    relative to Σ|dz|, and the logits / loss unchanged."""
+    from elliptic_gnn_project_amd import fused
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn, build_model
+    from elliptic_gnn_project_amd.train_ops import unit_gradient
+
+    data = prepare_inputs(synthetic_elliptic(num_nodes=6000, num_edges=7000, seed=8),
+                          dict(use_time_scalar=False, symmetrize_edges=True, train_window_k=8)).to(device)
+    cfg = dict(arch="sage_resbn", hidden_dim=64, layers=3, dropout=0.2, time_embed_dim=2, time_embed_type="sin",
+               max_timestep=49)
+    cw = pyg_ref.class_weight(data.y[data.train_mask].cpu())
+    denom = float(data.train_mask.sum())
+    res = []
+    for on in (True, False):
+        fused._BN_COLSUM = on
+        try:
+            torch.manual_seed(3)
+            model = build_model("sage_resbn", data.x.size(1), cfg).to(device)
+            loss_fn = _make_loss_fn({}, cw, model, 1, 34)
+            model.train()
+            torch.manual_seed(9)
+            with loss_fn.target(data.y, data.train_mask, denom):
+                logits = model(data.x, data.edge_index, data.timestep)
+            loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
+            loss.backward(unit_gradient(device))
+            res.append((logits.detach().clone(), loss.detach().clone(),
+                        {k: p.grad.clone() for k, p in model.named_parameters()}))
+        finally:
+            fused._BN_COLSUM = True
+    (l1, s1, g1), (l2, s2, g2) = res
+    assert torch.equal(l1, l2) and torch.equal(s1, s2)
+    bias0 = "convs.0.lin_l.bias"
+    assert bias0 in g1
+    for k in g1:
+        if k == bias0:
+            scale = float(g1["convs.0.lin_l.weight"].abs().max())
+            assert float((g1[k] - g2[k]).abs().max()) <= 1e-6 * max(1.0, scale), k
+        else:
+            assert torch.equal(g1[k], g2[k]), k
