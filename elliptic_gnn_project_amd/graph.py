@@ -36,7 +36,10 @@ SPLIT_LEN = 32  # slots per piece of a long segment (K0b)
 # slots go to blocks of their own, and the other rows to waves balanced by slots.  For graphs of
 # at most K1_HUB_MAX_N nodes (all, by default; GNNMP_K1_HUB_N overrides, for A/B).
 K1_HUB_DEG = int(os.environ.get("GNNMP_K1_HUB_DEG", "32"))
-K1_WAVE_ROWS = int(os.environ.get("GNNMP_K1_WAVE_ROWS", "16"))  # rows per wave on average (A/B)
+# rows per balanced wave on average: 8 on large graphs (the full headline graph: 0.2986 vs 0.3025
+# ms/step at 16, four interleaved repetitions, profiles/r58_k1_rows.txt), 16 on shard-sized ones
+# (the 8-way shard ~1 us better at 16, r50_k1_hub.txt); GNNMP_K1_WAVE_ROWS overrides (A/B)
+K1_WAVE_ROWS = int(os.environ.get("GNNMP_K1_WAVE_ROWS", "0"))
 K1_HUB_MAX_N = int(os.environ.get("GNNMP_K1_HUB_N", str(1 << 62)))
 
 
@@ -83,14 +86,16 @@ def _build_split(lib, ptr: torch.Tensor, nbr: torch.Tensor, n: int, T: int, dev)
 
 
 def _wave_starts(slots: torch.Tensor, n: int) -> torch.Tensor:
-    """Row boundaries of K1's balanced main-pass waves: as many waves as 16 rows each would take,
+    """Row boundaries of K1's balanced main-pass waves: as many waves as 8 (large graphs) or 16
+    rows each would take,
     contiguous row ranges of about equal cost (slots + kappa per row: a row's flush costs about a
     slot, and kappa >= mean degree / 2 keeps a wave under 63 rows), doubled until no wave holds
     more than 63 rows (the kernel keeps one row pointer per lane)."""
     kappa = max(1.0, float(slots.sum()) / max(n, 1) / 2.0)
     cost = slots.to(torch.float64) + kappa
     before = torch.cumsum(cost, 0) - cost  # cost of the rows before each row
-    waves = max(1, -(-n // K1_WAVE_ROWS))
+    rows = K1_WAVE_ROWS if K1_WAVE_ROWS > 0 else (8 if n > 65536 else 16)
+    waves = max(1, -(-n // rows))
     while True:
         target = float(cost.sum()) / waves
         k = torch.arange(waves + 1, dtype=torch.float64, device=slots.device) * target
