@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kAdamThreads) void grad_sq_kernel(AdamTable tb, flo
 // t, t + NTH, ... in order, 16 loads in flight; then the wave butterflies and the waves in order),
 // so every block holds the same norm and the grad_sq launch is saved.  The step count is read
 // from *step at the start and written by the block that finishes last (a vector atomic on the
-// workspace counter `done`, which that block resets to 0): no block reads it after it changed.
+// workspace counter `done`, a running count mod kAdamBlocks): no block reads it after it changed.
 constexpr int kSelfThreads = 1024;
 // (GCN's 21.6k gradient elements: 10.0 us vs 7.1 + 7.2 in two launches; SAGE-ResBN's ~41k: 16.6
 // vs 8.0 + 7.7 — the per-thread Σ passes grow with the count: profiles/r51_adam_one_launch.txt)
@@ -329,11 +329,11 @@ __global__ __launch_bounds__(NTH) void clip_adam_kernel(AdamTable tb, const floa
         if (bump) bump[0] = bump[0] + 1;  // no kernel of this launch reads it
       }
       if constexpr (SELF) {  // every block has read *step (snap_sh) and every gradient: the last one
-        last_sh = atomicAdd(done, 1u) == (unsigned)kAdamBlocks - 1u;  // to get here advances the step
-        if (last_sh) {
-          step[0] = snap_sh + (skip ? 0.0f : 1.0f);
-          atomicExch(done, 0u);
-        }
+        // to get here advances the step.  The counter is never reset: each launch adds exactly
+        // kAdamBlocks, so the block drawing old ≡ kAdamBlocks − 1 (mod kAdamBlocks) is the last one
+        // whatever value a previous launch left (no reset store a torn-down launch could skip)
+        last_sh = (atomicAdd(done, 1u) + 1u) % (unsigned)kAdamBlocks == 0u;
+        if (last_sh) step[0] = snap_sh + (skip ? 0.0f : 1.0f);
       }
     }
   }

@@ -254,7 +254,10 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     if sq is not None:
         from .train_ops import grad_sq_produced
 
-        grad_sq_produced(dev, (out, n_out, (lo, hi), _sq_blocks(n_out), sq[0], sq[1]))
+        # out._version: the gradients are views of out (AccumulateGrad adopts them detached, sharing
+        # its version counter), so any in-place edit between here and ClipAdam.step — GradScaler's
+        # unscale_, a mul_, an all-reduce — bumps it and voids the fold
+        grad_sq_produced(dev, (out, n_out, (lo, hi), _sq_blocks(n_out), sq[0], sq[1], out._version))
     if KernelTimer.active:
         e1.record()
         ea = 2 if bf else (4 if a1 is None else a1.element_size())
@@ -478,8 +481,11 @@ class _FusedSAGE(torch.autograd.Function):
 
         grad_sq_produced(dz.device, None)
         # 2 layers: the one TN below writes every parameter's gradient (dzsum[:C], Σ meanᵀ(dlogits),
-        # is not one of them) — Σg² for clip_grad_norm_ comes with its reduce
-        sq = grad_sq_request(dz.device) if L == 2 else None
+        # is not one of them) — Σg² for clip_grad_norm_ comes with its reduce.  Only on the
+        # unit-gradient path (dz is the CE's tagged buffer: loss.backward(unit_gradient)): a scaled
+        # loss (GradScaler) hands its gradients to unscale_, which rewrites them in place without
+        # bumping their version counter, so its Σg² must be read after that, by ClipAdam's own pass
+        sq = grad_sq_request(dz.device) if (L == 2 and dz is buf) else None
         g = None
         for l in range(L - 2, -1, -1):
             fo, fi = Wl[l].shape

@@ -199,7 +199,22 @@ class GraphPlan:
             _lib.check(lib.gnn_in_degree_f32(self.c_graph, self.deg.data_ptr(), _lib.stream_handle(dev)),
                        "gnn_in_degree_f32")
         self._dinv = None
-        self.hub = _build_hub(self.rowptr, self.col, self.deg, N, K1_HUB_DEG) if 0 < N <= K1_HUB_MAX_N else None
+        self._hub = False  # built on first use (only the half-pair K1 reads it)
+
+    @property
+    def hub(self):
+        """K1's hub form (include/gnnmp.h gnn_sage_mean_fwd_h2 hub), or None.  Built lazily, on the
+        first half-pair mean over this plan: GCN / GAT / REPLACE plans and the NeighborLoader's
+        per-batch plans never pay its host syncs and CSR copy.  Not buildable while a
+        stream is being captured — the warm-up forward that precedes every capture builds it."""
+        if self._hub is False:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("GraphPlan.hub is built by the first half-pair mean over the plan (host "
+                                   "syncs): run one eager forward before capturing the step")
+            N = self.num_nodes
+            self._hub = (_build_hub(self.rowptr, self.col, self.deg, N, K1_HUB_DEG)
+                         if 0 < N <= K1_HUB_MAX_N else None)
+        return self._hub
 
     @property
     def dinv(self) -> torch.Tensor:

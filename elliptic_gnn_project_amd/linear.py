@@ -8,12 +8,17 @@ dW (and db) and the NT kernel (B = W, row-major [K=out, N=in]) for the input gra
 
 ``linear2`` is the two-segment form ``[a1 | a2] · [W1 | W2]ᵀ + b`` — SAGEConv's
 ``lin_l(agg) + lin_r(x)`` as one GEMM with no concatenated copy of the operands.
+
+Shapes past the split-bf16 kernels' envelope (out > 128 or in > 384: e.g. ``hidden_dim: 256``,
+which build_model accepts, src/train_gnn.py:67-104) stay on the hand-written kernels too
+(``_TiledLinear``): the forward and the input gradient on the exact-f32 MFMA NT (B as the
+[K, N] row-major transpose, any N and K), the weight gradient as TN calls over ≤ 128-row blocks of
+dW and ≤ 384-column blocks of the input — never torch's hipBLASLt.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .fused import gemm_nt, gemm_nt_input, gemm_tn, gemm_tn_input
 
@@ -100,12 +105,73 @@ class _StackedLinear(torch.autograd.Function):
         return dx, dWl if need[1] else None, dWr if need[2] else None
 
 
+def _tn_blocks(segs, dy: torch.Tensor, want_db: bool):
+    """dW_s = dyᵀ · a_s for every segment a_s [M, k_s], and db = Σ_rows dy, as TN calls over ≤ MAX_OUT
+    output rows × ≤ MAX_IN input columns (row-strided views of dy and a_s read in place)."""
+    fo = dy.size(1)
+    dWs = [torch.empty((fo, a.size(1)), dtype=torch.float32, device=dy.device) for a in segs]
+    db = torch.empty(fo, dtype=torch.float32, device=dy.device) if want_db else None
+    for r0 in range(0, fo, MAX_OUT):
+        r1 = min(fo, r0 + MAX_OUT)
+        g = dy[:, r0:r1]
+        first = True
+        for a, dW in zip(segs, dWs):
+            for k0 in range(0, a.size(1), MAX_IN):
+                k1 = min(a.size(1), k0 + MAX_IN)
+                (d, _), dbb, _, _ = gemm_tn(r1 - r0, a[:, k0:k1], g=g)
+                dW[r0:r1, k0:k1].copy_(d)
+                if first and db is not None:
+                    db[r0:r1].copy_(dbb)
+                first = False
+    return dWs, db
+
+
+class _TiledLinear(torch.autograd.Function):
+    """``[a1 | a2] · [W1 | W2]ᵀ + b`` for shapes outside the split-bf16 envelope (see the module
+    docstring): exact-f32 MFMA NT forward / input gradient, blocked TN weight gradient."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+    def forward(ctx, a1, w1, bias, a2, w2):
+        a1 = _rows(a1)
+        a2 = _rows(a2) if a2 is not None else None
+        w = w1 if a2 is None else torch.cat([w1, w2], dim=1)
+        w = w.contiguous()
+        y = gemm_nt(a1, w.t().contiguous(), w.size(0), a2=a2, bias=bias, math="f32")
+        ctx.save_for_backward(a1, a2, w)
+        ctx.has_bias = bias is not None
+        ctx.k1 = w1.size(1)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        a1, a2, w = ctx.saved_tensors
+        dy = _rows(dy)
+        need = ctx.needs_input_grad
+        segs = [a1] if a2 is None else [a1, a2]
+        dWs, db = [None, None], None
+        if need[1] or need[2] or need[4]:
+            got, db = _tn_blocks(segs, dy, ctx.has_bias and need[2])
+            dWs[: len(got)] = got
+        da1 = da2 = None
+        if need[0] or need[3]:
+            dA = gemm_nt(dy, w, w.size(1), math="f32")  # [M, k1 + k2]
+            da1 = dA[:, : ctx.k1] if need[0] else None
+            da2 = dA[:, ctx.k1:] if (a2 is not None and need[3]) else None
+        return (da1, dWs[0] if need[1] else None, db if (ctx.has_bias and need[2]) else None,
+                da2, dWs[1] if need[4] else None)
+
+
 def linear_stacked(x: torch.Tensor, wl: torch.Tensor, wr: torch.Tensor) -> torch.Tensor:
     """``x · [wl ; wr]ᵀ`` (= F.linear(x, torch.cat([wl, wr]))) on the MFMA kernels."""
     if not x.is_cuda:
         raise RuntimeError("elliptic_gnn_project_amd.linear_stacked runs on the HIP device only")
-    if x.dim() != 2 or x.size(0) == 0 or wl.shape != wr.shape or not fits(wl.size(1), 2 * wl.size(0)):
-        return F.linear(x, torch.cat([wl, wr], dim=0))
+    if x.dim() != 2 or wl.shape != wr.shape:
+        raise ValueError(f"linear_stacked needs a 2-D input and equal weights, got {tuple(x.shape)}, "
+                         f"{tuple(wl.shape)}, {tuple(wr.shape)}")
+    if x.size(0) == 0 or not fits(wl.size(1), 2 * wl.size(0)):
+        return _TiledLinear.apply(x, torch.cat([wl, wr], dim=0), None, None, None)
     return _StackedLinear.apply(x, wl, wr)
 
 
@@ -113,8 +179,10 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
     """``F.linear`` on the MFMA kernels (HIP device, fp32 compute, 2-D input)."""
     if not x.is_cuda:
         raise RuntimeError("elliptic_gnn_project_amd.linear runs on the HIP device only")
-    if x.dim() != 2 or x.size(0) == 0 or not fits(weight.size(1), weight.size(0)):
-        return F.linear(x, weight, bias)  # outside the kernels' shape envelope: torch on the GPU
+    if x.dim() != 2:
+        raise ValueError(f"linear needs a 2-D input [N, in], got {tuple(x.shape)}")
+    if x.size(0) == 0 or not fits(weight.size(1), weight.size(0)):
+        return _TiledLinear.apply(x, weight, bias, None, None)  # outside the split-bf16 envelope
     return _MfmaLinear.apply(x, weight, bias, None, None)
 
 
@@ -124,7 +192,7 @@ def linear2(a1: torch.Tensor, a2: torch.Tensor, w1: torch.Tensor, w2: torch.Tens
     if not a1.is_cuda:
         raise RuntimeError("elliptic_gnn_project_amd.linear2 runs on the HIP device only")
     if a1.size(0) == 0 or not fits(w1.size(1) + w2.size(1), w1.size(0)):
-        return F.linear(a1, w1, bias) + F.linear(a2, w2)
+        return _TiledLinear.apply(a1, w1, bias, a2, w2)
     return _MfmaLinear.apply(a1, w1, bias, a2, w2)
 
 

@@ -238,7 +238,7 @@ def masked_cross_entropy(logits: torch.Tensor, y: torch.Tensor, mask: torch.Tens
 # partials and the step snapshot, and records what it wrote; the next ClipAdam.step takes the
 # record when its gradients are exactly views of that output — then its launch pair is one launch.
 _GRAD_SQ_REQ: dict = {}   # device -> (partials buffer, step tensor)
-_GRAD_SQ_DONE: dict = {}  # device -> (out, n_out, (skip_lo, skip_hi), nb, partials buffer, step tensor)
+_GRAD_SQ_DONE: dict = {}  # device -> (out, n_out, (skip_lo, skip_hi), nb, partials buffer, step tensor, out._version)
 _GRAD_SQ_CAP = 2048       # >= 2 nb + 1 for every TN output (Nr <= 128, K <= 384: nb <= 779)
 
 
@@ -256,8 +256,11 @@ def grad_sq_produced(device, rec) -> None:
 
 
 def _tiles(rec, ps) -> bool:
-    """The grads of ``ps`` are views of rec's out that tile [0, n_out) minus the skipped range."""
+    """The grads of ``ps`` are views of rec's out that tile [0, n_out) minus the skipped range, and
+    nothing wrote them in place since the producer recorded its Σg² (the version counter views share)."""
     out, n_out, (lo, hi) = rec[0], rec[1], rec[2]
+    if out._version != rec[6]:
+        return False
     base, sto, spans = out.data_ptr(), out.untyped_storage().data_ptr(), []
     for p in ps:
         g = p.grad  # (AccumulateGrad adopts the backward's views detached: same storage, no _base)

@@ -629,11 +629,13 @@ typedef struct {
                               tensors' gradients, with *step as sq_step: the call then launches only the
                               clip + Adam kernel (its Σg² pass is folded into the TN's reduce) */
 } gnn_adam_group;
-/* Workspace: 2·64 + 2 words, ZEROED before the first call (every call leaves it so).  Without
- * grad_sq_partial, gradients of at most 2^15 elements in all (GCN, GAT of the path) run as ONE
- * launch: each block sums Σg² over all of them itself, in one fixed order, and the last block to
- * finish advances *step (a vector atomic on the workspace's last word); larger ones run the Σg²
- * pass first (two launches).  ABI 21. */
+/* Workspace: 2·64 + 2 words, ZEROED before the first call.  Without grad_sq_partial, gradients of
+ * at most 2^15 elements in all (GCN, GAT of the path) run as ONE launch: each block sums Σg² over
+ * all of them itself, in one fixed order, and the last block to finish advances *step (a vector
+ * atomic on the workspace's last word, a running count: each call adds exactly 64 and the block
+ * that draws 63 mod 64 is the last, so a call that never completed cannot leave later calls
+ * without a last block — no reset is needed, re-zeroing the workspace is always safe between
+ * calls); larger ones run the Σg² pass first (two launches).  ABI 21. */
 gnn_status gnn_clip_adam_workspace_size(size_t* bytes);
 gnn_status gnn_clip_adam_f32(const gnn_adam_group* group, float* step, float* norm_out, void* workspace,
                              size_t workspace_bytes, gnn_stream_t stream);

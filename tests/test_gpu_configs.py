@@ -11,6 +11,8 @@ train_gnn.main / bench.py do) and unregistered; the largest shape also at the fu
     rec_k9           /root/reference/configs/rec_k9.yaml:10-13,36-38    (same shape, window 9)
     sage_l3          /root/reference/configs/sage_l3_k{6,10,14,18}.yaml SAGE 3L/128, dropout 0.3/0.4,
                      time scalar (in 166)
+    *_h256           hidden_dim 256 (any width build_model accepts, src/train_gnn.py:67-104): the
+                     convs' GEMMs past the split-bf16 kernels' 128-column envelope
 
 (The shipped configs set amp: true; the fused steps run fp32 under autocast — custom_fwd casts
 their inputs — which test_gpu_train_main.py covers; here the step runs fp32 directly.)
@@ -33,6 +35,14 @@ SHAPES = {
                    time_embed_type="sin", max_timestep=49, use_time_scalar=False, train_window_k=9),
     "sage_l3_k18": dict(arch="sage", hidden_dim=128, layers=3, dropout=0.4, use_time_scalar=True,
                         train_window_k=18),
+    # past the split-bf16 GEMMs' envelope (out > 128): linear._TiledLinear — exact-f32 MFMA NT,
+    # blocked TN — not torch's F.linear; dropout 0: the per-conv path
+    "sage_h256": dict(arch="sage", hidden_dim=256, layers=2, dropout=0.0, use_time_scalar=True,
+                      train_window_k=10),
+    "gcn_h256": dict(arch="gcn", hidden_dim=256, layers=2, dropout=0.0, use_time_scalar=True,
+                     train_window_k=10),
+    "gat_h256": dict(arch="gat", hidden_dim=256, heads=4, layers=2, dropout=0.0, use_time_scalar=True,
+                     train_window_k=10),
 }
 
 

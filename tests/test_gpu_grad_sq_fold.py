@@ -159,3 +159,68 @@ def test_no_fold_when_the_optimizer_holds_other_parameters(device):
         loss.backward(unit_gradient(device))
         opt.step()
         assert not opt.last_folded
+
+
+def test_grad_scaler_step_does_not_take_a_stale_fold(device):
+    """GradScaler's unscale_ rewrites .grad in place (without bumping the version
+    counter) between the backward and ClipAdam.step, so a Σg² folded into the backward's TN would
+    be 2^16 too large.  A scaled loss never requests the fold (only the unit-gradient path does):
+    scaler.step(ClipAdam) at init_scale 2^16 equals the unscaled, unfolded run."""
+    from elliptic_gnn_project_amd import train_ops
+    from elliptic_gnn_project_amd.train_ops import unit_gradient
+
+    runs = []
+    for scaled in (True, False):
+        data, model, opt, loss_fn, denom = _sage(device)
+        opt.skip_nonfinite = True
+        scaler = torch.amp.GradScaler("cuda", init_scale=2.0 ** 16, growth_interval=1_000_000, enabled=scaled)
+        folded = []
+        for it in range(4):
+            model.train()
+            opt.zero_grad(set_to_none=True)
+            if not scaled:
+                train_ops._GRAD_SQ_REQ.pop(device, None)
+            torch.manual_seed(200 + it)
+            with loss_fn.target(data.y, data.train_mask, denom):
+                logits = model(data.x, data.edge_index)
+            loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
+            if scaled:
+                scaler.scale(loss).backward()
+                scaler.step(opt)
+                scaler.update()
+            else:
+                loss.backward(unit_gradient(device))
+                opt.step()
+            folded.append(opt.last_folded)
+        runs.append((model, folded, float(opt.last_norm[0])))
+    (ma, fa, na), (mb, fb, nb) = runs
+    assert not any(fa) and not any(fb)
+    assert abs(na - nb) <= 1e-5 * nb
+    for (k, a), b in zip(ma.state_dict().items(), mb.state_dict().values()):
+        d = (a - b).abs()
+        bad = d > 1e-7 + 1e-5 * b.abs()
+        assert int(bad.sum()) <= max(1, a.numel() // 10000) and (float(d.max()) if d.numel() else 0.0) <= 5 * 0.01, k
+
+
+def test_in_place_grad_edit_voids_the_fold(device):
+    """An in-place edit of a folded gradient (here .grad.mul_(0.5)) bumps the version counter the
+    gradients share with the TN's output: ClipAdam runs its own Σg² pass on the edited values."""
+    from elliptic_gnn_project_amd.train_ops import unit_gradient
+
+    data, model, opt, loss_fn, denom = _sage(device)
+    for it in range(3):
+        model.train()
+        opt.zero_grad(set_to_none=True)
+        with loss_fn.target(data.y, data.train_mask, denom):
+            logits = model(data.x, data.edge_index)
+        loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
+        loss.backward(unit_gradient(device))
+        edit = it == 2
+        if edit:
+            for p in model.parameters():
+                p.grad.mul_(0.5)
+            ref = float(torch.linalg.vector_norm(torch.cat([p.grad.flatten() for p in model.parameters()])))
+        opt.step()
+        assert opt.last_folded == (it == 1)
+        if edit:
+            assert abs(float(opt.last_norm[0]) - ref) <= 1e-5 * ref
