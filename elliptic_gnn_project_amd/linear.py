@@ -11,9 +11,12 @@ dW (and db) and the NT kernel (B = W, row-major [K=out, N=in]) for the input gra
 
 Shapes past the split-bf16 kernels' envelope (out > 128 or in > 384: e.g. ``hidden_dim: 256``,
 which build_model accepts, src/train_gnn.py:67-104) stay on the hand-written kernels too
-(``_TiledLinear``): the forward and the input gradient on the exact-f32 MFMA NT (B as the
-[K, N] row-major transpose, any N and K), the weight gradient as TN calls over ≤ 128-row blocks of
-dW and ≤ 384-column blocks of the input — never torch's hipBLASLt.
+(``_TiledLinear``): the forward as split-bf16 NT calls over ≤ 128-column blocks of the output,
+the input gradient on the exact-f32 MFMA NT (B as the [K, N] row-major weight, any N and K — as
+_MfmaLinear's), the weight gradient as TN calls over ≤ 128-row blocks of dW and ≤ 384-column
+blocks of the input — never torch's hipBLASLt.  (The forward keeps the split-bf16 form's accuracy:
+the exact-f32 MFMA's k-ordered f32 chain, ~1e-6 relative on K = 173, moved SAGE-ResBN's BN
+outputs across ReLU ties at full size.)
 """
 from __future__ import annotations
 
@@ -128,16 +131,22 @@ def _tn_blocks(segs, dy: torch.Tensor, want_db: bool):
 
 class _TiledLinear(torch.autograd.Function):
     """``[a1 | a2] · [W1 | W2]ᵀ + b`` for shapes outside the split-bf16 envelope (see the module
-    docstring): exact-f32 MFMA NT forward / input gradient, blocked TN weight gradient."""
+    docstring): column-blocked NT forward, exact-f32 NT input gradient, blocked TN weight gradient."""
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, a1, w1, bias, a2, w2):
         a1 = _rows(a1)
         a2 = _rows(a2) if a2 is not None else None
+        w1 = w1.contiguous()
+        w2 = w2.contiguous() if w2 is not None else None
+        fo = w1.size(0)
+        y = torch.empty((a1.size(0), fo), dtype=torch.float32, device=a1.device)
+        for c0 in range(0, fo, MAX_OUT):  # ≤ 128 output columns per split-bf16 NT (rows of W: contiguous)
+            c1 = min(fo, c0 + MAX_OUT)
+            gemm_nt(a1, None, c1 - c0, a2=a2, w1=w1[c0:c1], w2=w2[c0:c1] if w2 is not None else None,
+                    bias=bias[c0:c1] if bias is not None else None, out=y[:, c0:c1])
         w = w1 if a2 is None else torch.cat([w1, w2], dim=1)
-        w = w.contiguous()
-        y = gemm_nt(a1, w.t().contiguous(), w.size(0), a2=a2, bias=bias, math="f32")
         ctx.save_for_backward(a1, a2, w)
         ctx.has_bias = bias is not None
         ctx.k1 = w1.size(1)
