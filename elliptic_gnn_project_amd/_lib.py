@@ -398,6 +398,10 @@ def ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else t.data_ptr()
 
 
+CALLS = [0]  # libgnnmp calls made so far (distributed.GradBucket tells gradient producers apart by it)
+
+
 def call(name: str, *args) -> None:
     lib = load()
+    CALLS[0] += 1
     check(getattr(lib, name)(*args), name)

@@ -822,7 +822,11 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
     for (int r = 0; r < 16; ++r) {
       const int row = wrow + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       const int64_t idx = s1 ? (int64_t)row * a.k1 + kp : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (kp - a.ap_col2);
-      if (row < a.Nr && (s1 || s2)) slab[idx] = acc[t][r] * gunsc;
+      if constexpr ((LAB & 128) != 0) {  // lab: no slab stores (one per wave keeps the chain live)
+        if (row < a.Nr && (s1 || s2) && acc[t][r] == 1.2345f) slab[idx] = 0.f;
+      } else {
+        if (row < a.Nr && (s1 || s2)) slab[idx] = acc[t][r] * gunsc;
+      }
     }
   }
   __syncthreads();

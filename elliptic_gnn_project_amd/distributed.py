@@ -130,17 +130,111 @@ def global_class_weight_and_count(y: torch.Tensor, train_mask: torch.Tensor, dis
 
 
 class GradBucket:
-    """Flat gradient buffer; every ``p.grad`` is a view into it (zero_grad(set_to_none=False))."""
+    """Flat gradient buffer; every ``p.grad`` is a view into it (zero_grad(set_to_none=False)).
 
-    def __init__(self, model: nn.Module):
-        self.params = [p for p in model.parameters() if p.requires_grad]
+    Overlap with the backward ("one fused bucket, overlapped with the last
+    backward kernels").  In a net whose layers are separate autograd nodes (SAGE-ResBN, GAT, the
+    per-conv paths) the later layers' gradients are final while the first layer's backward still
+    runs (its weight-gradient TN is the longest kernel of the backward).  The flat buffer is then
+    laid out as [early | late]: a post-accumulate hook on the early parameters issues the early
+    slice's all-reduce asynchronously (``async_op``: RCCL runs it on its own stream, inside a
+    captured step as a fork / join of the graph) as soon as the last of them has landed, and
+    ``allreduce_`` reduces the late slice and waits for both.  Two collectives instead of one, so
+    only worth it when the early gradients really come before the last producer:
+
+      early=None      observe the first backward — parameters whose gradients landed before the
+                      last batch of gradient producers (libgnnmp calls counted between the hooks,
+                      _lib.CALLS) form the early slice; one batch (a fused single-node net: SAGE
+                      2L, GCN) keeps one bucket
+      early=[names]   the early slice by parameter name (any backend; the CPU gloo tests)
+      overlap=False   one bucket, one collective after the backward (the round-5 form)
+
+    The re-layout happens inside the first ``allreduce_`` after the observation (values copied,
+    ``p.grad`` re-pointed); ``flat_in_param_order()`` gives the gradients in parameter order."""
+
+    def __init__(self, model: nn.Module, early=None, overlap: bool = True):
+        named = [(k, p) for k, p in model.named_parameters() if p.requires_grad]
+        self.names = [k for k, _ in named]
+        self.params = [p for _, p in named]
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.order = list(range(len(self.params)))  # flat layout: parameter indices in order
+        self._views()
+        self.overlap = bool(overlap) and len(self.params) > 1
+        self.n_early = 0          # parameters in the early slice (the first n_early of self.order)
+        self.early_elems = 0
+        self._arrivals = []       # (param index, _lib.CALLS) of the observed backward
+        self._landed = 0
+        self._work = None
+        self._dist = None
+        self._planned = False
+        self._want = None if early is None else set(early)
+        self._hooks = []
+        if self.overlap:
+            for i, p in enumerate(self.params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._hook_for(i)))
+
+    def _views(self) -> None:
         off = 0
-        for p in self.params:
+        for i in self.order:
+            p = self.params[i]
             p.grad = self.flat[off: off + p.numel()].view_as(p)
             off += p.numel()
+
+    def _hook_for(self, i: int):
+        def hook(_p):
+            if not self._planned:
+                from . import _lib
+                self._arrivals.append((i, _lib.CALLS[0]))
+                return
+            if i >= len(self._is_early) or not self._is_early[i]:
+                return
+            self._landed += 1
+            if self._landed == self.n_early and self._dist is not None and self._work is None:
+                d = self._dist
+                if d.get_backend() == "gloo" and torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                    return  # gloo cannot be captured: allreduce_ reduces it (the split-graph form)
+                self._work = d.all_reduce(self.flat[: self.early_elems], async_op=True)
+        return hook
+
+    def _plan(self) -> None:
+        """Choose the early slice from the observed arrivals (or the given names) and re-lay the
+        flat buffer out as [early | late], keeping the current gradient values."""
+        self._planned = True
+        idx = {k: i for i, k in enumerate(self.names)}
+        if self._want is not None:
+            early = [idx[k] for k in self.names if k in self._want]
+        else:
+            arr = self._arrivals
+            early = []
+            if arr and len({c for _, c in arr}) > 1:
+                last = arr[-1][1]
+                early = [i for i, c in arr if c < last]
+        late = [i for i in range(len(self.params)) if i not in set(early)]
+        self._is_early = [False] * len(self.params)
+        for i in early:
+            self._is_early[i] = True
+        if not early or not late:
+            self.n_early, self.early_elems = 0, 0
+            return
+        vals = [p.grad.detach().clone() for p in self.params]
+        self.order = early + late
+        self.n_early = len(early)
+        self.early_elems = sum(self.params[i].numel() for i in early)
+        self._views()
+        for p, v in zip(self.params, vals):
+            p.grad.copy_(v)
+
+    def flat_in_param_order(self) -> torch.Tensor:
+        return torch.cat([p.grad.detach().flatten() for p in self.params])
+
+    def arm(self, dist) -> None:
+        """Before the first backward: the early slice's hook may issue its collective on ``dist``
+        (later backwards use the ``dist`` of the previous ``allreduce_``)."""
+        self._dist = dist
+        self._landed = 0
+        self._work = None
 
     def allreduce_(self, dist) -> None:
         for p in self.params:  # re-attach if an optimizer set grads to None
@@ -148,7 +242,22 @@ class GradBucket:
                     p.grad.data_ptr() >= self.flat.data_ptr() + self.flat.numel() * 4:
                 raise RuntimeError("GradBucket: gradients detached from the flat buffer; "
                                    "use optimizer.zero_grad(set_to_none=False)")
-        dist.all_reduce(self.flat)
+        self._dist = dist  # the next backward's early hook issues on it
+        if not self.overlap or not self._planned:
+            dist.all_reduce(self.flat)
+            if self.overlap and (self._arrivals or self._want is not None):
+                self._plan()  # the next backward overlaps (values kept)
+            return
+        if self.n_early == 0:
+            dist.all_reduce(self.flat)
+            return
+        work, self._work = self._work, None
+        if work is None:  # the hook did not fire (not armed, a gloo capture, a missing gradient)
+            dist.all_reduce(self.flat[: self.early_elems])
+        dist.all_reduce(self.flat[self.early_elems:])
+        if work is not None:
+            work.wait()
+        self._landed = 0
 
 
 def global_batch_stats(x: torch.Tensor, dist) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:

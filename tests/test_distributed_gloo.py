@@ -164,6 +164,58 @@ def _rb_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+def _rb_overlap_worker(rank, world, port, out_path):
+    """As _rb_worker, three backwards through an overlapped GradBucket: the later layers'
+    gradients (convs.2, convs.1, the BN affines) in the early slice, all-reduced from their
+    post-accumulate hooks while layer 0's backward still runs."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full = _rb_data()
+    sh = gdist.shard_graph(full, world, rank)
+    cw, denom = gdist.global_class_weight_and_count(sh.y, sh.train_mask, dist)
+    model = OracleResBN(_rb_state(), _RB_HID, _RB_L, _rb_masks(full.num_nodes))
+    gdist.convert_sync_batchnorm(model, dist)
+    names = [k for k, _ in model.named_parameters()]
+    early = [k for k in names if k.startswith("bns.")] + \
+        [f"ps.{i}" for i, k in enumerate(model.conv_names) if not k.startswith(("convs.0.", "res_projs."))]
+    bucket = gdist.GradBucket(model, early=early)
+    issued = []
+    for it in range(3):
+        for p in model.parameters():
+            p.grad.zero_()
+        for bn in model.bns:  # the same BN running-stat state each pass
+            bn.reset_running_stats()
+        logits = model(sh.x, sh.edge_index, sh.timestep, sh.nodes)
+        tm = sh.train_mask
+        loss = torch.nn.functional.cross_entropy(logits[tm], sh.y[tm], weight=cw, reduction="none").sum() / denom
+        loss.backward()
+        issued.append(bucket._work is not None)
+        bucket.allreduce_(dist)
+    if rank == 0:
+        torch.save({"grad": bucket.flat_in_param_order(), "issued": issued, "n_early": bucket.n_early,
+                    "order": bucket.order}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_overlapped_bucket_matches_full_graph(tmp_path):
+    """the gradient all-reduce overlapped with the backward (two slices, the early
+    one issued from the hooks) still gives the full-graph gradient on every step."""
+    out_path = str(tmp_path / "rbo0.pt")
+    mp.spawn(_rb_overlap_worker, args=(2, _free_port(), out_path), nprocs=2, join=True)
+    got = torch.load(out_path, weights_only=True)
+    assert got["issued"] == [False, True, True]  # step 0 lays the buffer out, then the hooks issue
+    assert 0 < got["n_early"] < len(got["order"])
+    full = _rb_data()
+    model = OracleResBN(_rb_state(), _RB_HID, _RB_L, _rb_masks(full.num_nodes))
+    nodes = torch.arange(full.num_nodes)
+    logits = model(full.x, full.edge_index, full.timestep, nodes)
+    tm = full.train_mask
+    pyg_ref.ce_loss(logits[tm], full.y[tm], pyg_ref.class_weight(full.y[tm])).backward()
+    ref = torch.cat([p.grad.flatten() for p in model.parameters()])
+    assert float((got["grad"] - ref).norm() / ref.norm()) < 1e-5
+
+
 def test_two_rank_sage_resbn_partitioned_matches_full_graph(tmp_path):
     """rec_k8's claim: SAGE-ResBN with SyncBN inside the model, timestep-partitioned
     over 2 ranks with the global train divisor, gives the full-graph logits, gradients (every
