@@ -115,7 +115,7 @@ struct AggArgs {
   // r·kcols + c), computed here where the gather leaves the VALU idle
   uint32_t* kmask; int32_t kcols;
   // K1 of the half-pair path may also carry the consuming NT's B-image prep (gnn_sage_mean_fwd_h2
-  // prep_b): hp.blocks extra blocks at the front of the grid run ws_prep_h2_body, one per k-step
+  // prep_b): hp.gblocks extra blocks at the front of the grid run ws_prep_h2_cols, one wave per column
   H2Prep hp;
   // K1 of the half-pair path, hub form (gnn_sage_mean_fwd_h2 hub): rows with deg > hub_deg
   // (hubs[0, nhub)) have no slots in the main pass's ptr / nbr; one block each (nhub extra blocks
@@ -566,21 +566,20 @@ __device__ __forceinline__ void k1_hub_row(const AggArgs& a, int32_t r) {
   }
 }
 
-// PCPP: columns per pass of the B prep riding along (ws_prep_h2_body CPP)
-template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, int PLN = 0, int PCPP = 1>  // BF: x and y hold bf16 (no split partials)
+template <int MODE, int VEC, int NCH, bool BF = false, int U = 8, int PLN = 0>  // BF: x and y hold bf16 (no split partials)
 __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
-  if constexpr (PLN == 2) {  // the NT's B prep rides along (blocks [0, hp.blocks), launched first)
-    if ((int)blockIdx.x < a.hp.blocks) {
-      ws_prep_h2_body<256, PCPP>(a.hp, (int)blockIdx.x);
+  if constexpr (PLN == 2) {  // the NT's B prep rides along (blocks [0, hp.gblocks), launched first)
+    if ((int)blockIdx.x < a.hp.gblocks) {
+      ws_prep_h2_cols<256>(a.hp, (int)blockIdx.x);
       return;
     }
-    if ((int)blockIdx.x < a.hp.blocks + a.nhub) {  // the hub rows, also launched early
-      k1_hub_row<VEC, NCH>(a, a.hubs[(int)blockIdx.x - a.hp.blocks]);
+    if ((int)blockIdx.x < a.hp.gblocks + a.nhub) {  // the hub rows, also launched early
+      k1_hub_row<VEC, NCH>(a, a.hubs[(int)blockIdx.x - a.hp.gblocks]);
       return;
     }
   }
   const int lane = threadIdx.x & 63;
-  const int64_t bid = (int64_t)blockIdx.x - (PLN == 2 ? a.hp.blocks + a.nhub : 0);
+  const int64_t bid = (int64_t)blockIdx.x - (PLN == 2 ? a.hp.gblocks + a.nhub : 0);
   const int64_t wave = (bid * 256 + threadIdx.x) >> 6;
   int64_t r0 = wave * rpg;
   int nrow;
@@ -1612,6 +1611,7 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
       return fail(GNN_ERR_INVALID_ARG, fn, "prep_b: the NT must read this half-pair image (same planes_exp)");
     const gnn_status s = nt_h2_prep_from_params(prep_b, &a.hp, fn);
     if (s != GNN_OK) return s;
+    a.hp.gblocks = BN / 4;  // one wave per output column (ws_prep_h2_cols<256>)
   }
   auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
   const bool v4 = F % 4 == 0 && ldx % 4 == 0 && width % 4 == 0 && ld % 4 == 0 && plane_stride % 4 == 0 &&
@@ -1637,15 +1637,9 @@ static gnn_status sage_mean_fwd_image(const gnn_graph* g, const float* deg, cons
   if (a.nrows == 0) return GNN_OK;
   const int rpw = a.wstart ? (int)hub->num_pieces : 16;  // (balanced: the kernel's rpg is the wave count)
   const int64_t nwaves = a.wstart ? hub->num_pieces : ceil_div(a.nrows, 16);
-  const unsigned wblocks = (unsigned)ceil_div(nwaves * 64, 256) + (unsigned)a.hp.blocks + (unsigned)a.nhub;
+  const unsigned wblocks = (unsigned)ceil_div(nwaves * 64, 256) + (unsigned)a.hp.gblocks + (unsigned)a.nhub;
   hipStream_t st = (hipStream_t)stream;
-  // the riding B prep's columns per pass: its 4·32/CPP dependent load rounds are K1's critical
-  // path on a short gather (a strong-scaling shard: CPP 4 took 7 us off the 8- and 4-way shard
-  // steps), while on a long one CPP 4's registers cost the gather occupancy (+4 us on the full
-  // graph; profiles/r50_k1_hub.txt)
-  if (vec == 4 && ceil_div(width, 4) <= 64 && PLN == 2 && a.hp.blocks > 0 && a.nrows <= 65536)
-    agg_wave_kernel<GNN_AGG_MEAN, 4, 1, false, 8, PLN, 4><<<wblocks, 256, 0, st>>>(a, rpw);
-  else if (vec == 4 && ceil_div(width, 4) <= 64)  // one pass per row (e.g. a 168-wide padded x: 42 lanes)
+  if (vec == 4 && ceil_div(width, 4) <= 64)  // one pass per row (e.g. a 168-wide padded x: 42 lanes)
     agg_wave_kernel<GNN_AGG_MEAN, 4, 1, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
   else if (vec == 4) agg_wave_kernel<GNN_AGG_MEAN, 4, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);
   else agg_wave_kernel<GNN_AGG_MEAN, 2, 2, false, 8, PLN><<<wblocks, 256, 0, st>>>(a, rpw);

@@ -75,14 +75,15 @@ struct NTArgs {
   float* colsum_part;     // optional (skinny-K NT): per-block column sums of the stored C, [nb][Nc]
 };
 
-// the half-pair NT's B-image prep (ws_prep_h2_body below)
+// the half-pair NT's B-image prep (ws_prep_h2_cols below)
 struct H2Prep {
   const float* w1; const float* w2;  // w2 may be null (k2 = 0)
   int64_t ldw1, ldw2;
   int32_t k1, k2, Nc, col2;
-  int32_t blocks;                    // k-steps (= blocks of the prep)
+  int32_t blocks;                    // k-steps of the image
   uint4* img; float* colscale;
   float a_unscale;                   // 2^-ap_exp of the A image (folded into colscale)
+  int32_t gblocks;                   // 256-thread blocks of the column-form prep riding in K1 (0: none)
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
@@ -269,90 +270,78 @@ void launch_tn_skinny(const TNArgs& a, int nblk, hipStream_t st);
 // ---- the half-pair NT's B image (K7a-h).  Per k-step s, plane p (hi' = 2^11 hi, hi, lo), slot
 // 2n + khalf: the 8 halves of column n, k = 16s + 8·khalf .. +8, of w_n · 2^-e_n, where 2^-e_n
 // brings the column's largest |w| into [8, 16) (a power of two: exact); colscale[n] =
-// 2^(e_n - 11 - ap_exp), which also undoes the A image's pre-scale (written by the k-step-0
-// block).  One block per k-step; every block computes all column exponents (max |w_n| over the
-// whole K): NTH/64 waves, a wave's lanes across k (coalesced), in passes of 4 columns whose 48 loads per lane are all issued before the first use (indices
-// clamped into the operand, the excess masked to 0: no load sits behind a branch), then a wave
-// max per column; the block's own k-step is staged in LDS on the way.  (A per-thread walk down
-// each row spent ~30 us on dependent load latency; a linear sweep into LDS atomics ~40 us on
-// same-address ds_max conflicts.)  Needs k1, k2 <= 384 (nt_h2_ok: <= 336).
+// 2^(e_n - 11 - ap_exp), which also undoes the A image's pre-scale.
+// Column form (round 6): ONE WAVE PER OUTPUT COLUMN n — B's column n is row n of the Linear
+// weights, contiguous — so a wave loads its whole column (12 loads per lane, all issued before the
+// first use, indices clamped, the excess masked to 0), takes the max with a butterfly, stages the
+// column's image row in LDS and writes its 2·NKS (k-step, khalf) slots of all three planes.  One
+// load round trip per wave instead of the k-step form's all-columns sweep per block (32 / CPP
+// dependent rounds per wave: the riding prep was K1's critical path on a strong-scaling shard,
+// 22.0 vs 17.9 us gather alone at 8 shards).  The grid covers all BN columns (zeros past Nc);
+// the image is bit-identical to the k-step form's (the same per-element arithmetic; a max is
+// order-free).  Needs k1, k2 <= 384 and 16·NKS <= 384 (nt_h2_ok: <= 336).
 __device__ __forceinline__ float h2_col_exp2(float m) {  // 2^e with m · 2^-e in [8, 16); 1 for m = 0
   if (!(m > 0.f) || !isfinite(m)) return 1.0f;
   int E;
   frexpf(m, &E);  // m in [2^(E-1), 2^E)
   return ldexpf(1.0f, E - 4);
 }
-// CPP: columns per pass (12·CPP loads in flight per lane; K1's copy runs CPP = 1 so the gather
-// kernel it rides in keeps its register budget and occupancy)
-template <int NTH, int CPP = 4>
-__device__ __forceinline__ void ws_prep_h2_body(const H2Prep& a, int c) {
-  static_assert(NTH >= 256 && NTH % 256 == 0, "the write phase uses 256 threads");
-  constexpr int NW = NTH / 64, CPW = BN / NW;  // waves, columns per wave
-  static_assert(CPW % CPP == 0, "whole passes");
-  __shared__ float sc[BN];
-  __shared__ float slice[BN][17];  // this block's k-step of the image, [column][16 k] (+1: banks)
-  const int tid = threadIdx.x;
+template <int NTH>
+__device__ __forceinline__ void ws_prep_h2_cols(const H2Prep& a, int blk) {
+  constexpr int NW = NTH / 64;
+  constexpr int ROW = 16 * 24 + 4;                 // an image row (<= 384 columns) per wave
+  __shared__ float wrow[NW][ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = blk * NW + wave;                   // this wave's column
+  if (n >= BN) return;                             // (wave-uniform; no block barrier below)
+  const bool live = n < a.Nc;
+  const int nc = live ? n : 0;
   const int k1m = a.k1 - 1, k2m = a.k2 > 0 ? a.k2 - 1 : 0;
-  const float* w2b = a.w2 ? a.w2 : a.w1;
-  const int64_t ld2 = a.w2 ? a.ldw2 : a.ldw1;
-  for (int i = tid; i < BN * 17; i += NTH) (&slice[0][0])[i] = 0.f;
-  __syncthreads();
-  {
-    const int wave = tid >> 6, lane = tid & 63;
-#pragma unroll 1
-    for (int pass = 0; pass < CPW / CPP; ++pass) {
-      float v[CPP][12];
+  const float* w1 = a.w1 + (int64_t)nc * a.ldw1;
+  const float* w2 = (a.w2 ? a.w2 : a.w1) + (int64_t)nc * (a.w2 ? a.ldw2 : a.ldw1);
+  float v[12];
 #pragma unroll
-      for (int j = 0; j < CPP; ++j) {
-        const int nc = min(wave * CPW + pass * CPP + j, a.Nc - 1);
-        const float* w1 = a.w1 + (int64_t)nc * a.ldw1;
-        const float* w2 = w2b + (int64_t)nc * ld2;
+  for (int i = 0; i < 6; ++i) {
+    v[i] = w1[min(lane + 64 * i, k1m)];
+    v[6 + i] = w2[min(lane + 64 * i, k2m)];
+  }
+  float* row = wrow[wave];
+  const int ncols = 16 * a.blocks;
+  for (int kk = lane; kk < ncols; kk += 64) row[kk] = 0.f;
+  float m = 0.f;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          v[j][i] = w1[min(lane + 64 * i, k1m)];
-          v[j][6 + i] = w2[min(lane + 64 * i, k2m)];
-        }
-      }
+  for (int i = 0; i < 6; ++i) {
+    m = fmaxf(m, lane + 64 * i < a.k1 ? fabsf(v[i]) : 0.f);
+    m = fmaxf(m, lane + 64 * i < a.k2 ? fabsf(v[6 + i]) : 0.f);
+  }
 #pragma unroll
-      for (int j = 0; j < CPP; ++j) {
-        float m = 0.f;
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const float sc = live ? h2_col_exp2(m) : 1.0f;
+  if (lane == 0) a.colscale[n] = sc * (1.0f / 2048.0f) * a.a_unscale;  // powers of two: exact
+  // (the zeroing stores above precede these in this wave's LDS order)
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          m = fmaxf(m, lane + 64 * i < a.k1 ? fabsf(v[j][i]) : 0.f);
-          m = fmaxf(m, lane + 64 * i < a.k2 ? fabsf(v[j][6 + i]) : 0.f);
-        }
+  for (int i = 0; i < 6; ++i) {
+    const int k = lane + 64 * i;
+    if (live && k < a.k1) row[k] = v[i];
+    if (live && k < a.k2) row[a.col2 + k] = v[6 + i];
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's row is in LDS
+  __builtin_amdgcn_wave_barrier();
+  const float inv = 1.0f / sc;  // a power of two: exact
+  for (int q = lane; q < 2 * a.blocks; q += 64) {
+    const int s = q >> 1, kh = q & 1;
+    uint32_t hw[4], lw[4], pw[4];
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        const int n = wave * CPW + pass * CPP + j;
-        if (lane == 0) sc[n] = n < a.Nc ? h2_col_exp2(m) : 1.0f;
-        if (n < a.Nc) {  // the block's k-step: image column kk = 16c + t holds w1[kk] or w2[kk - col2]
-#pragma unroll
-          for (int i = 0; i < 6; ++i) {
-            const int k = lane + 64 * i, t1 = k - 16 * c, t2 = a.col2 + k - 16 * c;
-            if (k < a.k1 && t1 >= 0 && t1 < 16) slice[n][t1] = v[j][i];
-            if (k < a.k2 && t2 >= 0 && t2 < 16) slice[n][t2] = v[j][6 + i];
-          }
-        }
-      }
+    for (int j = 0; j < 4; ++j) {
+      const float v0 = row[16 * s + 8 * kh + 2 * j] * inv, v1 = row[16 * s + 8 * kh + 2 * j + 1] * inv;
+      split_h2_pair(v0, v1, hw[j], lw[j]);
+      pw[j] = h2_scale_pair(hw[j], 2048.0f);
     }
+    const int64_t slot = 2 * n + kh;
+    a.img[((int64_t)s * 3 + 0) * 256 + slot] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+    a.img[((int64_t)s * 3 + 1) * 256 + slot] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    a.img[((int64_t)s * 3 + 2) * 256 + slot] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
   }
-  __syncthreads();
-  if (c == 0 && tid < BN) a.colscale[tid] = sc[tid] * (1.0f / 2048.0f) * a.a_unscale;  // powers of two: exact
-  if (tid >= 256) return;
-  const int n = tid >> 1, kh = tid & 1;
-  const float inv = 1.0f / sc[n];  // a power of two: exact
-  uint32_t hw[4], lw[4], pw[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float v[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) v[q] = slice[n][8 * kh + 2 * j + q] * inv;
-    split_h2_pair(v[0], v[1], hw[j], lw[j]);
-    pw[j] = h2_scale_pair(hw[j], 2048.0f);
-  }
-  a.img[((int64_t)c * 3 + 0) * 256 + tid] = make_uint4(pw[0], pw[1], pw[2], pw[3]);
-  a.img[((int64_t)c * 3 + 1) * 256 + tid] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-  a.img[((int64_t)c * 3 + 2) * 256 + tid] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
 }
 constexpr int WS_PREP_THREADS = 1024;
 

@@ -620,12 +620,13 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   auto load_z = [&](int c) __attribute__((always_inline)) {
     if constexpr (!GF) rz = a.dz[(uint32_t)((ldbase(c) + zr) * (int)a.lddz + zqc)];
   };
-  auto put_z = [&](int k) __attribute__((always_inline)) {
+  auto put_zv = [&](int k, float v) __attribute__((always_inline)) {
     if constexpr (GF) return;
     const int mb = ldbase(k);
     const bool ok = tid < PT_ROWS * MAXPROJ && zq < a.nproj && zr >= (int)mbeg + k * PT_ROWS - mb && zr < (int)mend - mb;
-    if (T == 256 || tid < 256) dzL[k & 1][tid] = ok ? rz : 0.0f;
+    if (T == 256 || tid < 256) dzL[k & 1][tid] = ok ? v : 0.0f;
   };
+  auto put_z = [&](int k) __attribute__((always_inline)) { put_zv(k, rz); };
 
   float db = 0.f, dzs = 0.f;
   float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
@@ -770,11 +771,10 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
 #undef TH_FENCE
 
   if (nch > 0) {
-    if constexpr (!GF) rz = a.dz[(uint32_t)((ldbase(0) + zr) * (int)a.lddz + zqc)];
-    put_z(0);
-    load_z(min(1, clast));
-    put_z(1);
-    load_z(min(2, clast));
+    // every prologue load issued before the first use of any (round 6): chunk 0's A pieces and G
+    // rows, then the dz values of chunks 0..2 together — the dz ring's two LDS puts used to wait
+    // one round trip each before chunk 0's loads were even issued (the TN's fixed cost on a
+    // strong-scaling shard, where a block walks only ~8 chunks)
 #pragma unroll
     for (int j = 0; j < NPA; ++j) load_a(0, j, 0);
     if constexpr (RING == 2) {
@@ -783,6 +783,14 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
     }
     load_g(0, 0);
     if constexpr (RGN == 2) load_g(1, min(1, clast));
+    float rz0 = 0.f, rz1 = 0.f;
+    if constexpr (!GF) {
+      rz0 = a.dz[(uint32_t)((ldbase(0) + zr) * (int)a.lddz + zqc)];
+      rz1 = a.dz[(uint32_t)((ldbase(min(1, clast)) + zr) * (int)a.lddz + zqc)];
+    }
+    load_z(min(2, clast));
+    put_zv(0, rz0);
+    put_zv(1, rz1);
     scan_scale();     // (its barrier also publishes dzL)
 #pragma unroll
     for (int j = 0; j < NPA; ++j) put_a(0, j, 0);

@@ -1028,10 +1028,11 @@ __global__ __launch_bounds__(256) void gemm_nt_h2_kernel(NTArgs a, const uint4* 
   }
 }
 
-// B image of the half-pair NT (gemm_common.hpp ws_prep_h2_body): the standalone launch, one
-// 1024-thread block per k-step.  (K1 can also carry it: gnn_sage_mean_fwd_h2's prep_b.)
+// B image of the half-pair NT (gemm_common.hpp ws_prep_h2_cols): the standalone launch, one wave
+// per output column (BN / 16 blocks of 1024).  (K1 can also carry it: gnn_sage_mean_fwd_h2's prep_b.)
+constexpr int WS_PREP_GRID = BN / (WS_PREP_THREADS / 64);
 __global__ __launch_bounds__(WS_PREP_THREADS) void ws_prep_h2_kernel(H2Prep p) {
-  ws_prep_h2_body<WS_PREP_THREADS>(p, (int)blockIdx.x);  // (one 8-column pass: 9.5 vs 8.8 us, r19g)
+  ws_prep_h2_cols<WS_PREP_THREADS>(p, (int)blockIdx.x);
 }
 
 // ---------------------------------------------------------------- bf16 image form (K7a-b)
@@ -1398,7 +1399,7 @@ H2Prep h2_prep_of(const NTArgs& a, uint4* img) {
 template <int NKS>
 void launch_nt_h2_k(const NTArgs& a, uint4* img, hipStream_t st, int phase) {
   float* colscale = reinterpret_cast<float*>(img + NKS * 3 * 256);
-  if (phase & NT_PHASE_PREP) ws_prep_h2_kernel<<<NKS, WS_PREP_THREADS, 0, st>>>(h2_prep_of(a, img));
+  if (phase & NT_PHASE_PREP) ws_prep_h2_kernel<<<WS_PREP_GRID, WS_PREP_THREADS, 0, st>>>(h2_prep_of(a, img));
   if (!(phase & NT_PHASE_RUN)) return;
   const int ntiles = (int)ceil_div(a.M, WS_ROWS);
   const int grid = std::min(ntiles, ws_num_cus());

@@ -442,7 +442,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&g_bh, 21 * 3 * 256 * 16 + 128 * 4));
   g_cs = reinterpret_cast<float*>(g_bh + 21 * 3 * 256);  // the column scales follow the image (h2_prep_of)
   g_h = n; g_h.ap = imh; g_h.c = c2; g_h.z = z2;
-  ws_prep_h2_kernel<<<21, WS_PREP_THREADS>>>(h2_prep_of(g_h, g_bh));
+  ws_prep_h2_kernel<<<WS_PREP_GRID, WS_PREP_THREADS>>>(h2_prep_of(g_h, g_bh));
   const int ntiles = (int)ceil_div(M, 32);
 
   // accuracy: no dropout (deterministic), C vs float64 on sampled rows

@@ -39,7 +39,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 //   * 16-row tiles, v_mfma_f32_16x16x32_f16; 256-thread blocks, TWO per CU (grid 2 x CUs, 256
 //     registers per wave: __launch_bounds__(256, 2)).  Wave w owns columns 32w .. +32 as two
 //     16-column halves; its B fragments — planes hi and lo only, read from the 3-plane B image
-//     (ws_prep_h2_body) — stay in AGPRs: NK 32-deep k-steps x 2 planes x 2 halves x 4 = 176 (NK 11).
+//     (ws_prep_h2_cols) — stay in AGPRs: NK 32-deep k-steps x 2 planes x 2 halves x 4 = 176 (NK 11).
 //   * two accumulators per half instead of the hi' = 2^11 hi plane:
 //       x  += A_hi·B_lo + A_lo·B_hi,    hh += A_hi·B_hi,    C = (2^11 hh + x) · 2^(e_n - 11 - ap_exp)
 //     (= the 3-product form's sum, two chains per half: four independent MFMA chains per wave).
@@ -326,11 +326,12 @@ template <int LAB, int E = EPIF>
 void ring16() { gemm_nt_h2r_kernel<11, E, LAB><<<512, 256>>>(g_n, g_b, g_cs, g_nt16); }
 static const uint4* g_sa;
 static float4* g_sc;
-void stream() { stream_kernel<<<1024, 256>>>(g_sa, (int64_t)203769 * 336 * 2 * 2 / 16, g_sc, (int64_t)203769 * 128 / 4); }
+static int64_t g_M = 203769;
+void stream() { stream_kernel<<<1024, 256>>>(g_sa, g_M * 336 * 2 * 2 / 16, g_sc, g_M * 128 / 4); }
 
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? std::atoi(argv[1]) : 9;
-  const int64_t M = 203769, F = 166, LD = 336, NR = 128;
+  const int64_t M = argc > 2 ? std::atoll(argv[2]) : 203769, F = 166, LD = 336, NR = 128;  // M: shard sizes too
   std::vector<float> hx(M * LD, 0.f);
   {
     std::mt19937 g(1);
@@ -374,7 +375,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&g_b, 21 * 3 * 256 * 16 + 128 * 4));
   g_cs = reinterpret_cast<float*>(g_b + 21 * 3 * 256);
   g_n = n;
-  ws_prep_h2_kernel<<<21, WS_PREP_THREADS>>>(h2_prep_of(g_n, g_b));
+  ws_prep_h2_kernel<<<WS_PREP_GRID, WS_PREP_THREADS>>>(h2_prep_of(g_n, g_b));
+  g_M = M;
   g_nt32 = (int)ceil_div(M, 32);
   g_nt16 = (int)ceil_div(M, 16);
   g_sa = reinterpret_cast<const uint4*>(imh);

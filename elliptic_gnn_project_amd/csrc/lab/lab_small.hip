@@ -114,7 +114,7 @@ int main(int argc, char** argv) {
   uint4* bh;
   CK(hipMalloc(&bh, 21 * 3 * 256 * 16 + 128 * 4));
   float* cs = reinterpret_cast<float*>(bh + 21 * 3 * 256);
-  ws_prep_h2_kernel<<<21, WS_PREP_THREADS>>>(h2_prep_of(n, bh));
+  ws_prep_h2_kernel<<<WS_PREP_GRID, WS_PREP_THREADS>>>(h2_prep_of(n, bh));
   const int ntiles = (int)ceil_div(M, 32);
 
   const int64_t stride = (NR * 332 + NR + 4 * NR + 4 + 63) / 64 * 64;

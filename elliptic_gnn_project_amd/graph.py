@@ -35,10 +35,13 @@ SPLIT_LEN = 32  # slots per piece of a long segment (K0b)
 # rows happen to be heavy (an average wave walks ~37 slots).  Rows with more than K1_HUB_DEG
 # slots go to blocks of their own, and the other rows to waves balanced by slots.  For graphs of
 # at most K1_HUB_MAX_N nodes (all, by default; GNNMP_K1_HUB_N overrides, for A/B).
-K1_HUB_DEG = int(os.environ.get("GNNMP_K1_HUB_DEG", "32"))
+# (32 on large graphs; 16 on graphs of <= 65,536 nodes — a strong-scaling shard, whose gather is
+# latency-bound: shorter hub chains, profiles/r66_k1_sweep.txt); GNNMP_K1_HUB_DEG overrides (A/B)
+K1_HUB_DEG = int(os.environ.get("GNNMP_K1_HUB_DEG", "0"))
 # rows per balanced wave on average: 8 on large graphs (the full headline graph: 0.2986 vs 0.3025
-# ms/step at 16, four interleaved repetitions, profiles/r58_k1_rows.txt), 16 on shard-sized ones
-# (the 8-way shard ~1 us better at 16, r50_k1_hub.txt); GNNMP_K1_WAVE_ROWS overrides (A/B)
+# ms/step at 16, four interleaved repetitions, profiles/r58_k1_rows.txt), 4 on graphs of <= 32,768
+# nodes (the 8-way shard's gather 17.9 -> 14.1 us with hub degree 16, once the riding B prep no
+# longer set K1's length: r66_k1_sweep.txt); GNNMP_K1_WAVE_ROWS overrides (A/B)
 K1_WAVE_ROWS = int(os.environ.get("GNNMP_K1_WAVE_ROWS", "0"))
 K1_HUB_MAX_N = int(os.environ.get("GNNMP_K1_HUB_N", str(1 << 62)))
 
@@ -94,7 +97,7 @@ def _wave_starts(slots: torch.Tensor, n: int) -> torch.Tensor:
     kappa = max(1.0, float(slots.sum()) / max(n, 1) / 2.0)
     cost = slots.to(torch.float64) + kappa
     before = torch.cumsum(cost, 0) - cost  # cost of the rows before each row
-    rows = K1_WAVE_ROWS if K1_WAVE_ROWS > 0 else (8 if n > 65536 else 16)
+    rows = K1_WAVE_ROWS if K1_WAVE_ROWS > 0 else (4 if n <= 32768 else 8)
     waves = max(1, -(-n // rows))
     while True:
         target = float(cost.sum()) / waves
@@ -212,7 +215,8 @@ class GraphPlan:
                 raise RuntimeError("GraphPlan.hub is built by the first half-pair mean over the plan (host "
                                    "syncs): run one eager forward before capturing the step")
             N = self.num_nodes
-            self._hub = (_build_hub(self.rowptr, self.col, self.deg, N, K1_HUB_DEG)
+            T = K1_HUB_DEG if K1_HUB_DEG > 0 else (16 if N <= 65536 else 32)
+            self._hub = (_build_hub(self.rowptr, self.col, self.deg, N, T)
                          if 0 < N <= K1_HUB_MAX_N else None)
         return self._hub
 

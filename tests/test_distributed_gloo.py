@@ -72,7 +72,7 @@ def _worker(rank, world, port, out_path):
     gw = bn.weight.grad.clone()
     dist.all_reduce(gw)
     if rank == 0:
-        torch.save({"grad": bucket.flat.clone(), "bn_out0": out.detach(), "bn_dx0": rows.grad.clone(), "bn_dw": gw,
+        torch.save({"grad": bucket.flat_in_param_order(), "bn_out0": out.detach(), "bn_dx0": rows.grad.clone(), "bn_dw": gw,
                     "running_mean": bn.running_mean.clone(), "running_var": bn.running_var.clone()}, out_path)
     dist.barrier()
     dist.destroy_process_group()
@@ -156,7 +156,7 @@ def _rb_worker(rank, world, port, out_path):
     bucket.allreduce_(dist)
     glog = gdist.gather_rows(logits.detach(), sh.nodes, full.num_nodes, dist)
     if rank == 0:
-        torch.save({"grad": bucket.flat.clone(), "logits": glog, "denom": denom,
+        torch.save({"grad": bucket.flat_in_param_order(), "logits": glog, "denom": denom,
                     "rm": [bn.running_mean.clone() for bn in model.bns],
                     "rv": [bn.running_var.clone() for bn in model.bns],
                     "types": [type(bn).__name__ for bn in model.bns]}, out_path)

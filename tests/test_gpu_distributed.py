@@ -107,7 +107,7 @@ def _rank_worker(rank, world, port, out_path):
     bucket.allreduce_(dist)
     glog = gdist.gather_rows(logits.detach(), sh.nodes, full.num_nodes, dist)
     if rank == 0:
-        torch.save({"grad": bucket.flat.cpu(), "logits": glog.cpu(),
+        torch.save({"grad": bucket.flat_in_param_order().cpu(), "logits": glog.cpu(),
                     "rm": [bn.running_mean.cpu() for bn in model.bns],
                     "rv": [bn.running_var.cpu() for bn in model.bns]}, out_path)
     dist.barrier()

@@ -44,16 +44,14 @@ def _f64(params):
     return {k: v.double() if v.is_floating_point() else v for k, v in params.items()}
 
 
-@pytest.mark.parametrize("registered", [True, False])
-def test_full_size_sage_train_step_gradients(device, registered):
-    """configs[1] at full size, train mode: logits and all 6 parameter gradients.  registered: x
-    declared constant as bench.py / train_gnn.main do — layer 1 on the [agg | x] split image (the
-    benched path: K1 into the agg planes, the planes NT / TN); else the in-kernel split forms."""
+def _sage_step_vs_oracle(device, data, registered):
+    """configs[1] train step: logits and all 6 parameter gradients vs the float64 oracle under the
+    same dropout masks.  registered: x declared constant as bench.py / train_gnn.main do — layer 1
+    on the [agg | x] split image (the benched path: K1 into the agg planes, the planes NT / TN);
+    else the in-kernel split forms."""
     from elliptic_gnn_project_amd.gnn import SAGENet
     from elliptic_gnn_project_amd.planes import register_input
 
-    data = _graph(True)
-    assert data.edge_index.size(1) == 2 * E_FULL
     N = data.x.size(0)
     torch.manual_seed(5)
     model = SAGENet(166, 128, layers=2, dropout=0.5).to(device)
@@ -82,6 +80,31 @@ def test_full_size_sage_train_step_gradients(device, registered):
     assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
     for k, v in model.named_parameters():
         assert rel_l2(v.grad, grads[k]) < 1e-5, (k, rel_l2(v.grad, grads[k]))
+
+
+@pytest.mark.parametrize("registered", [True, False])
+def test_full_size_sage_train_step_gradients(device, registered):
+    """configs[1] at full size, train mode (the headline step)."""
+    data = _graph(True)
+    assert data.edge_index.size(1) == 2 * E_FULL
+    _sage_step_vs_oracle(device, data, registered)
+
+
+@pytest.mark.parametrize("ways", [8, 4])
+def test_full_size_sage_largest_shard(device, ways):
+    """configs[1] on the largest shard of the 8- / 4-way timestep partition — what one rank of the
+    strong-scaling run computes before its gradient all-reduce (bench.py --rehearse-shard): the
+    shard-sized schedule (K1 waves of ~4 rows, hub rows past degree 16, the column-form B prep)
+    against the float64 oracle, registered as the bench runs it."""
+    from elliptic_gnn_project_amd import distributed as gdist
+
+    full = _graph(True)
+    parts = gdist.partition_timesteps(full.timestep, full.edge_index, ways)
+    e_t = torch.bincount(full.timestep[full.edge_index[1]], minlength=int(full.timestep.max()) + 1)
+    r = max(range(ways), key=lambda i: int(sum(int(e_t[t]) for t in parts[i])))
+    sh = gdist.shard_graph(full, ways, r, parts=parts)
+    assert full.x.size(0) // (2 * ways) < sh.x.size(0) < 2 * full.x.size(0) // ways
+    _sage_step_vs_oracle(device, sh, True)
 
 
 @pytest.mark.parametrize("arch,hidden,heads", [("gcn", 64, 4), ("gat", 64, 4)])

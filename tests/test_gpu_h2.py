@@ -121,7 +121,7 @@ def _mean_hub_np(plan, x, T):
 def test_mean_h2_hub_form_edge_graphs(device, shape):
     """The hub form on edge-case graphs — no hub rows (balanced waves only: bit-identical to the
     16-row waves), one degree-300 star centre, 3 nodes, every row a hub — vs the restatement."""
-    from elliptic_gnn_project_amd.graph import K1_HUB_DEG, get_plan
+    from elliptic_gnn_project_amd.graph import get_plan
     from elliptic_gnn_project_amd.planes import HalfPairImage
 
     g = torch.Generator().manual_seed(5)
@@ -149,7 +149,8 @@ def test_mean_h2_hub_form_edge_graphs(device, shape):
     im.img.fill_(1.0)
     im.fill_mean(plan, x)
     got = _planes_np(im)
-    for p, w in enumerate(split_h2(_mean_hub_np(plan, x, K1_HUB_DEG), im.exp)):
+    T = int(plan.hub["c"].seg_len)  # the plan's hub degree (graph.K1_HUB_DEG: 16 / 32 by size)
+    for p, w in enumerate(split_h2(_mean_hub_np(plan, x, T), im.exp)):
         assert np.array_equal(got[p][:, :166], w), p
         assert not got[p][:, 166:168].any()
     if shape == "ring_isolated":
@@ -165,13 +166,13 @@ def test_mean_h2_hub_form_vs_restatement(device, n, e, padded):
     zero; the ordinary rows bit-identical to the one-wave-per-16-rows K1, the hub rows within
     1e-5 of it (another f32 summation order of up to ~200 terms); the keep bits and the NT B prep riding along unchanged."""
     from elliptic_gnn_project_amd.fused import _nt_workspace, gemm_nt
-    from elliptic_gnn_project_amd.graph import K1_HUB_DEG
     from elliptic_gnn_project_amd.planes import HalfPairImage, x_padded
 
     data, plan, x = _plan_and_x(n, e, 31, device)
-    assert plan.hub is not None and int(plan.hub["c"].num_long) == int((plan.deg[: x.size(0)] > K1_HUB_DEG).sum()) > 0
+    T = int(plan.hub["c"].seg_len)
+    assert plan.hub is not None and int(plan.hub["c"].num_long) == int((plan.deg[: x.size(0)] > T).sum()) > 0
     hubs = plan.hub["hubs"].long().cpu().numpy()
-    want = _mean_hub_np(plan, x, K1_HUB_DEG)
+    want = _mean_hub_np(plan, x, T)
     im = HalfPairImage(x.size(0), x.size(1), x.size(1), device)
     im.fill_x(x)
     kw = dict(x_pad=x_padded(x, im.col2)) if padded else {}
