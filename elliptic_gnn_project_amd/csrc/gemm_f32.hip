@@ -757,10 +757,15 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   }
 }
 
+// Blocks of the TN launches: at most 256 (one per CU), and no more than the 32-row chunks need at
+// the chunks-per-block that 256 blocks would take — every block has rows, so no block writes an
+// all-zero slab for the reduce to read back (a strong-scaling shard: 213 instead of 256 slabs at
+// 27,196 rows, -17 % of the slab traffic).
 int tn_blocks(int64_t M) {
-  int64_t chunks = ceil_div(M, 32);
-  int64_t nb = chunks < 256 ? chunks : 256;
-  return (int)(nb > 0 ? nb : 1);
+  const int64_t chunks = ceil_div(M, 32);
+  if (chunks <= 0) return 1;
+  const int64_t per = ceil_div(chunks, 256);
+  return (int)ceil_div(chunks, per);
 }
 
 }  // namespace
