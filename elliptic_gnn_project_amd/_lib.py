@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["GNNMP_LIB"]) if os.environ.get("GNNMP_LIB") else PKG_DIR / "libgnnmp.so"  # (GNNMP_LIB: A/B builds)
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -256,6 +256,10 @@ SIGNATURES = {
          c_ptr, c_ptr, c_ptr, c_i64, c_ptr],
     ),
     "gnn_gat_fwd_fused_f32": (ctypes.c_int, [ctypes.POINTER(GnnGraph), ctypes.POINTER(GnnGatFwdParams), c_ptr]),
+    "gnn_gat_out_ce_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), ctypes.POINTER(GnnGatFwdParams), c_ptr, c_ptr, c_ptr, ctypes.c_float, c_ptr, c_i64,
+         c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_gat_act_bwd_f32": (
         ctypes.c_int,
         [c_i64, c_i64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr,

@@ -10,6 +10,8 @@ reproducible run to run.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -354,6 +356,12 @@ def gcn_aggregate(y: torch.Tensor, edge_index: torch.Tensor, bias: torch.Tensor 
 
 
 # --------------------------------------------------------------------------- GAT
+# GATNet's output conv (heads 1, C <= 2) in the narrow slot-parallel form with the fused CE
+# (gnn_gat_out_ce_f32, round 6); GNNMP_GAT_NARROW=0: the lane-group kernel (A/B)
+_GAT_NARROW = os.environ.get("GNNMP_GAT_NARROW", "1") != "0"
+_GAT_CE = True  # the CE in the narrow form's launch under fused_ce_target (False: its own launch; A/B, tests)
+
+
 class _GATAttention(torch.autograd.Function):
     """K5/K6 with the scores formed in-kernel (gnn_gat_fwd_fused_f32) and, for GATNet's hidden
     layers, ELU + counter-hash dropout on the store; the backward undoes them in one elementwise
@@ -381,7 +389,17 @@ class _GATAttention(torch.autograd.Function):
             a_src.data_ptr(), a_dst.data_ptr(), alpha.data_ptr(), out.data_ptr(), _ld(out),
         )
         t0 = KernelTimer.begin()
-        _lib.call("gnn_gat_fwd_fused_f32", plan.c_graph, p, stream)
+        ce = None
+        if (heads == 1 and chans <= 2 and not concat and act == _lib.ACT_NONE and dropout_p == 0.0 and N > 0
+                and _GAT_NARROW):
+            # GATNet's output conv: the narrow slot-parallel form, and the step's masked CE in the
+            # same launch when the training forward declared it (train_ops.fused_ce_target)
+            from .train_ops import ce_target, gat_out
+
+            tgt = ce_target() if (_GAT_CE and any(ctx.needs_input_grad)) else None
+            ce = gat_out(plan, p, tgt)
+        else:
+            _lib.call("gnn_gat_fwd_fused_f32", plan.c_graph, p, stream)
         S = plan.num_slots
         # per slot: id 4 + xh row 4HC + alpha 8H (raw score, then normalised); per node: rowptr 4,
         # own xh row 4HC, a_src + a_dst 8H, out 4·fo
@@ -391,6 +409,8 @@ class _GATAttention(torch.autograd.Function):
         ctx.save_for_backward(xh, att_src, att_dst, a_src, a_dst, alpha, seed_ctr, out if post else None)
         ctx.meta = (plan, heads, chans, bool(concat), float(slope), bias is not None, int(act), float(dropout_p),
                     int(seed))
+        if ce is not None:
+            out._gnnmp_ce = ce  # masked_cross_entropy returns it (same operands) instead of launching
         return out
 
     @staticmethod

@@ -1022,6 +1022,249 @@ bool vec_ok(const void* p, int64_t ld, int v) {
   return ((uintptr_t)p % (uintptr_t)(4 * v)) == 0 && ld % v == 0;
 }
 
+// ---------------------------------------------------------------- the output layer, narrow (round 6)
+// GATNet's last conv, GATConv(hidden, C <= 2, heads=1, concat=False) (src/models/gnn.py:67, :75),
+// in the slot-parallel narrow form GCN's and SAGE's output layers have (aggregate.hip
+// agg_narrow_lds_kernel): a wave owns 64 consecutive rows, one per lane.  Its slots are staged
+// through LDS with lanes over SLOTS (neighbour ids, then their xh rows, all in flight together)
+// together with each slot's score a_src[j] = <xh[j], att_src> formed on the way; then each lane
+// walks its own row's slots in edge order with an online softmax over e = leaky(a_src[j] + a_dst[i])
+// (running max m, sum s and accumulator, rescaled when m grows), out = acc / (s + 1e-16) + bias.
+// Once a row ends inside a staging window its alpha = exp(e - m) / (s + 1e-16) is written from the
+// staged scores (slots of a row that began in an earlier window — a hub in a heavy wave — are
+// re-gathered); a_src / a_dst of the row are written beside.  CE: the
+// masked weighted cross entropy of the finished logits in the same launch (gnn_masked_ce_f32's
+// arithmetic and 256-row partials, dlogits' block column sums beside them), as
+// gnn_gcn_out_ce_f32 does for GCN.
+struct GatOutArgs {
+  const int32_t* rowptr; const int32_t* col;
+  int64_t N; int32_t C; float slope;
+  const float* xh; int64_t ld_xh;
+  const float* att_s; const float* att_d; const float* bias;
+  float* a_s; float* a_d; float* alpha;
+  float* out; int64_t ldo;
+  const int64_t* ce_y; const uint8_t* ce_mask; const float* ce_w; float ce_inv;
+  float* ce_dl; int64_t ce_ldd; float* ce_part; float* ce_cs;
+};
+template <bool CE>
+__global__ __launch_bounds__(256) void gat_out_narrow_kernel(GatOutArgs a) {
+  // no implicit FMA contraction: the CE and no-CE instances (and the window sizes) must round the
+  // softmax sums identically (tests: the fused-CE step bit-identical to the separate one)
+#pragma clang fp contract(off)
+  // CAP slots staged per wave and window (a wave's 64 rows: ~140 slots on Elliptic); a row that
+  // straddles two windows (a hub in a heavy wave) has its alpha re-gathered by all 64 lanes
+  constexpr int CAP = 256, LONG = 32;
+  __shared__ float sv[4][3 * CAP];  // per wave: xh[j][0], xh[j][1], a_src[j] of the staged slots
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + w) * 64;
+  const int C = a.C;
+  float lg[4] = {0.f, 0.f, 0.f, 0.f};
+  int64_t ce_t = -1;
+  uint8_t ce_m = 0;
+  float ce_w[2] = {0.f, 0.f};
+  if constexpr (!CE) {
+    if (r0 >= a.N) return;  // wave-uniform; no block barrier below
+  }
+  if (r0 < a.N) {
+    const int64_t r = r0 + lane;
+    const bool rok = r < a.N;
+    const int64_t rr = rok ? r : r0;
+    const int32_t pbeg = a.rowptr[rok ? r : a.N];
+    const int32_t pend = a.rowptr[rok ? r + 1 : a.N];
+    const int32_t base = __builtin_amdgcn_readfirstlane(a.rowptr[r0]);
+    const int32_t wend = __builtin_amdgcn_readfirstlane(a.rowptr[min(r0 + 64, a.N)]);
+    // the row's own operands up front (clamped indices): its xh (a_dst), att vectors, bias, CE
+    const float as0 = a.att_s[0], as1 = a.att_s[C > 1 ? 1 : 0];
+    const float ad0 = a.att_d[0], ad1 = a.att_d[C > 1 ? 1 : 0];
+    const float xi0 = a.xh[rr * a.ld_xh], xi1 = a.xh[rr * a.ld_xh + (C > 1 ? 1 : 0)];
+    float pb0 = 0.f, pb1 = 0.f;
+    if (a.bias) { pb0 = a.bias[0]; pb1 = a.bias[C > 1 ? 1 : 0]; }
+    if constexpr (CE) {
+      ce_t = a.ce_y[rr];
+      ce_m = a.ce_mask[rr];
+      ce_w[0] = a.ce_w[0];
+      ce_w[1] = a.ce_w[C > 1 ? 1 : 0];
+    }
+    const float adr = C > 1 ? xi0 * ad0 + xi1 * ad1 : xi0 * ad0;  // (xh_i * att_dst).sum(-1)
+    const float asr = C > 1 ? xi0 * as0 + xi1 * as1 : xi0 * as0;
+    float m = -INFINITY, s = 0.f, acc0 = 0.f, acc1 = 0.f;
+    float* buf = sv[w];
+    auto score = [&](int q, float ad) __attribute__((always_inline)) { return leaky(buf[2 * CAP + q] + ad, a.slope); };
+    constexpr int W = CAP, NI = W / 64;
+    for (int32_t pb = base; pb < wend; pb += W) {
+      const int32_t pe = min(pb + W, wend);
+      int32_t nn[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int32_t k = pb + lane + 64 * i;
+        nn[i] = a.col[k < pe ? k : pb];
+      }
+      float x0[NI], x1[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const float* xr = a.xh + (int64_t)nn[i] * a.ld_xh;
+        x0[i] = xr[0];
+        x1[i] = xr[C > 1 ? 1 : 0];
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        buf[lane + 64 * i] = x0[i];
+        buf[CAP + lane + 64 * i] = C > 1 ? x1[i] : 0.f;
+        buf[2 * CAP + lane + 64 * i] = C > 1 ? x0[i] * as0 + x1[i] * as1 : x0[i] * as0;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      const int32_t lo = max(pbeg, pb), hi0 = min(pend, pe);
+      const int32_t hi = min(hi0, lo + LONG);  // a lane walks at most LONG slots of its row per window
+      {  // the lane's slots of this window: their max first (independent LDS reads, no branch),
+         // one rescale of what earlier windows summed, then the exp-weighted sums in two chains
+        float mw = -INFINITY;
+        int32_t k = lo;
+        for (; k + 1 < hi; k += 2) mw = fmaxf(mw, fmaxf(score(k - pb, adr), score(k + 1 - pb, adr)));
+        if (k < hi) mw = fmaxf(mw, score(k - pb, adr));
+        const float mn = fmaxf(m, mw);
+        if (mn > m) {
+          const float sc = m == -INFINITY ? 0.f : fexp(m - mn);
+          s *= sc;
+          acc0 *= sc;
+          acc1 *= sc;
+          m = mn;
+        }
+        float s2 = 0.f, c02 = 0.f, c12 = 0.f;
+        for (k = lo; k + 1 < hi; k += 2) {
+          const float p = fexp(score(k - pb, adr) - m), p2 = fexp(score(k + 1 - pb, adr) - m);
+          s += p;
+          acc0 += p * buf[k - pb];
+          acc1 += p * buf[CAP + k - pb];
+          s2 += p2;
+          c02 += p2 * buf[k + 1 - pb];
+          c12 += p2 * buf[CAP + k + 1 - pb];
+        }
+        if (k < hi) {
+          const float p = fexp(score(k - pb, adr) - m);
+          s += p;
+          acc0 += p * buf[k - pb];
+          acc1 += p * buf[CAP + k - pb];
+        }
+        s += s2;
+        acc0 += c02;
+        acc1 += c12;
+      }
+      // the rest of each long row: all 64 lanes over its slots (one softmax state per lane, merged
+      // by xor butterflies: symmetric, every lane ends with the same state), then into lane L's;
+      // a row wholly inside this window gets its alpha written by all lanes right here
+      uint64_t longm = __ballot(hi0 - lo > LONG);
+      while (longm) {
+        const int L = __builtin_ctzll(longm);
+        longm &= longm - 1;
+        const int32_t s0 = __builtin_amdgcn_readlane(lo, L) + LONG, s1 = __builtin_amdgcn_readlane(hi0, L);
+        const float adL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adr), L));
+        float mw = -INFINITY, sw = 0.f, c0 = 0.f, c1 = 0.f;
+        for (int32_t k = s0 + lane; k < s1; k += 64) {
+          const float e = score(k - pb, adL);
+          const float mn = fmaxf(mw, e);
+          const float sc = fexp(mw - mn), p = fexp(e - mn);
+          sw = sw * sc + p;
+          c0 = c0 * sc + p * buf[k - pb];
+          c1 = c1 * sc + p * buf[CAP + k - pb];
+          mw = mn;
+        }
+        for (int o = 32; o >= 1; o >>= 1) {  // merge (m, s, c) pairs
+          const float mo = __shfl_xor(mw, o), so = __shfl_xor(sw, o), co0 = __shfl_xor(c0, o), co1 = __shfl_xor(c1, o);
+          const float mn = fmaxf(mw, mo);
+          const float ea = mw == -INFINITY ? 0.f : fexp(mw - mn), eb = mo == -INFINITY ? 0.f : fexp(mo - mn);
+          sw = sw * ea + so * eb;
+          c0 = c0 * ea + co0 * eb;
+          c1 = c1 * ea + co1 * eb;
+          mw = mn;
+        }
+        if (lane == L) {  // lane L's own state and the wave's
+          const float mn = fmaxf(m, mw);
+          const float ea = m == -INFINITY ? 0.f : fexp(m - mn), eb = mw == -INFINITY ? 0.f : fexp(mw - mn);
+          s = s * ea + sw * eb;
+          acc0 = acc0 * ea + c0 * eb;
+          acc1 = acc1 * ea + c1 * eb;
+          m = mn;
+        }
+        const int32_t bL = __builtin_amdgcn_readlane(pbeg, L), eL = __builtin_amdgcn_readlane(pend, L);
+        if (bL >= pb && eL <= pe) {  // the whole long row in this window: its alpha, by all lanes
+          const float mL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), L));
+          const float dL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), L)) + 1e-16f;
+          const float rL = frcp(dL);
+          for (int32_t k = bL + lane; k < eL; k += 64) a.alpha[k] = fexp(score(k - pb, adL) - mL) * rL;
+        }
+      }
+      const bool ends = pend > pb && pend <= pe;
+      if (ends && pbeg >= pb && hi0 - lo <= LONG) {  // a short row wholly in this window: its alpha
+        const float rd = frcp(s + 1e-16f);
+        for (int32_t k = lo; k < hi0; ++k) a.alpha[k] = fexp(score(k - pb, adr) - m) * rd;
+      }
+      // rows that began in an earlier window and end here: alpha re-gathered by all 64 lanes
+      uint64_t strad = __ballot(ends && pbeg < pb);
+      while (strad) {
+        const int L = __builtin_ctzll(strad);
+        strad &= strad - 1;
+        const int32_t bL = __builtin_amdgcn_readlane(pbeg, L), eL = __builtin_amdgcn_readlane(pend, L);
+        const float adL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(adr), L));
+        const float mL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), L));
+        const float dL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), L)) + 1e-16f;
+        for (int32_t k = bL + lane; k < eL; k += 64) {
+          const float* xr = a.xh + (int64_t)a.col[k] * a.ld_xh;
+          const float sj = C > 1 ? xr[0] * as0 + xr[1] * as1 : xr[0] * as0;  // (the staged scores' rounding)
+          a.alpha[k] = fexp(leaky(sj + adL, a.slope) - mL) * frcp(dL);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (rok) {
+      const float denom = s + 1e-16f;
+      const float o0 = acc0 / denom + pb0, o1 = acc1 / denom + pb1;
+      a.a_s[r] = asr;
+      a.a_d[r] = adr;
+      a.out[r * a.ldo] = o0;
+      if (C > 1) a.out[r * a.ldo + 1] = o1;
+      lg[0] = o0;
+      lg[1] = o1;
+    }
+  }
+  if constexpr (CE) {
+    const int64_t r = r0 + lane;
+    float l = 0.f;
+    float dlv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r < a.N) {  // masked_ce_kernel<C>: loss_r = -w[y]·log_softmax[y], dl = w[y]/n·(softmax - onehot)
+      const int64_t tg = ce_t;
+      const bool on = ce_m != 0 && tg >= 0 && tg < C;
+      const float wt = tg == 0 ? ce_w[0] : ce_w[1];
+      l = masked_ce_row<4>(lg, C, tg, on, on ? wt : 0.f, a.ce_inv, a.ce_dl + r * a.ce_ldd, dlv);
+    }
+    __shared__ float cesh[4];
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);  // train_ops.hip block_sum, same order
+    if (lane == 0) cesh[w] = l;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+      for (int i = 0; i < 4; ++i) t += cesh[i];
+      a.ce_part[blockIdx.x] = t;
+    }
+    if (a.ce_cs) {  // the block's column sums of dl: each wave's rows by its butterfly, the waves in order
+      __shared__ float cssh[2][4];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        float v = c < C ? dlv[c] : 0.f;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) cssh[c][w] = v;
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < C) {
+        float t = 0.f;
+        for (int i = 0; i < 4; ++i) t += cssh[threadIdx.x][i];
+        a.ce_cs[(int64_t)blockIdx.x * C + threadIdx.x] = t;
+      }
+    }
+  }
+}
+
 // Fast-path geometry, or false when the generic one-wave-per-row kernels must run
 // (more than 64 slots of VEC floats, or a head mean whose slots per head are not a power of two).
 bool gat_geom(int H, int C, int concat, std::initializer_list<std::pair<const void*, int64_t>> ops, GatGeom* g,
@@ -1372,4 +1615,43 @@ extern "C" gnn_status gnn_gat_bwd_ew_f32(const gnn_graph* g, int32_t H, int32_t 
   return gat_bwd_impl(__func__, g, H, C, concat, slope, xh, ld_xh, a_src, a_dst, att_src, att_dst, alpha, dout,
                       ld_dout, dxh, ld_dxh, d_att_src, d_att_dst, edge_w, d_edge_w, workspace, workspace_bytes,
                       stream);
+}
+
+extern "C" gnn_status gnn_masked_ce_finish(const float* partial, int32_t nblk, float inv_denom, float* loss,
+                                           gnn_stream_t stream);
+
+extern "C" gnn_status gnn_gat_out_ce_f32(const gnn_graph* g, const gnn_gat_fwd_params* p, const int64_t* y,
+                                         const uint8_t* mask, const float* class_w, float inv_denom, float* dlogits,
+                                         int64_t ld_d, float* colsum, float* loss, void* workspace,
+                                         size_t workspace_bytes, gnn_stream_t stream) {
+  const char* fn = __func__;
+  if (!g || !p) return fail(GNN_ERR_INVALID_ARG, fn, "null graph or params");
+  if (p->heads != 1 || p->chans < 1 || p->chans > 2 || p->concat || p->act != GNN_ACT_NONE || p->dropout_p != 0.0f ||
+      p->edge_w)
+    return fail(GNN_ERR_UNSUPPORTED, fn, "the narrow output form: heads 1, 1 <= C <= 2, no concat / act / dropout / edge_w");
+  const int64_t N = g->num_nodes;
+  if (p->ld_xh < p->chans || p->ldo < p->chans) return fail(GNN_ERR_INVALID_ARG, fn, "bad leading dimensions");
+  if (N < 1 || !p->xh || !p->att_src || !p->att_dst || !p->a_src || !p->a_dst || !p->alpha || !p->out || !g->rowptr ||
+      (g->num_slots > 0 && !g->col))
+    return fail(GNN_ERR_INVALID_ARG, fn, "null operand / N < 1");
+  const bool ce = y != nullptr;
+  if (ce && (!mask || !class_w || !dlogits || ld_d < p->chans)) return fail(GNN_ERR_INVALID_ARG, fn, "CE operands");
+  const int nblk = (int)ceil_div(N, 256);
+  if (ce && (!workspace || workspace_bytes < (size_t)nblk * sizeof(float)))
+    return fail(GNN_ERR_WORKSPACE, fn, "workspace too small");
+  GatOutArgs a{};
+  a.rowptr = g->rowptr; a.col = g->col; a.N = N; a.C = p->chans; a.slope = p->slope;
+  a.xh = p->xh; a.ld_xh = p->ld_xh; a.att_s = p->att_src; a.att_d = p->att_dst; a.bias = p->bias;
+  a.a_s = p->a_src; a.a_d = p->a_dst; a.alpha = p->alpha; a.out = p->out; a.ldo = p->ldo;
+  hipStream_t st = (hipStream_t)stream;
+  if (!ce) {
+    gat_out_narrow_kernel<false><<<(unsigned)nblk, 256, 0, st>>>(a);
+    return hip_check(hipGetLastError(), fn);
+  }
+  a.ce_y = y; a.ce_mask = mask; a.ce_w = class_w; a.ce_inv = inv_denom; a.ce_dl = dlogits; a.ce_ldd = ld_d;
+  a.ce_part = static_cast<float*>(workspace); a.ce_cs = colsum;
+  gat_out_narrow_kernel<true><<<(unsigned)nblk, 256, 0, st>>>(a);
+  const gnn_status s = hip_check(hipGetLastError(), fn);
+  if (s != GNN_OK || !loss) return s;  // loss NULL: the partials stay in the workspace (ClipAdam / finish)
+  return gnn_masked_ce_finish(static_cast<float*>(workspace), nblk, inv_denom, loss, stream);
 }

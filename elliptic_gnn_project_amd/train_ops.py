@@ -210,6 +210,34 @@ def gcn_out_ce(plan, t: torch.Tensor, bias, target):
     return logits, (key, loss, buf, ws)
 
 
+def gat_out(plan, p, target=None):
+    """GATNet's output conv (heads 1, C <= 2, no concat / act / dropout) in the narrow form
+    (include/gnnmp.h gnn_gat_out_ce_f32), ``p`` the GnnGatFwdParams of the call; with ``target`` the
+    masked CE in the same launch, dlogits' block column sums beside them.  Returns ce (for
+    _PrecomputedCE) or None."""
+    from .fused import defer_loss_sum
+
+    N, C = plan.num_nodes, int(p.chans)
+    dev = plan.device
+    if target is None:
+        _lib.call("gnn_gat_out_ce_f32", plan.c_graph, p, None, None, None, 0.0, None, 0, None, None, None, 0,
+                  _lib.stream_handle(dev))
+        return None
+    key, y, m8, w, inv = target
+    buf = torch.empty((N, 2 * C), dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    ws = _ws(_ce_ws_bytes(N), dev)
+    nblk = max(1, -(-N // 256))
+    cs = torch.empty(nblk * C, dtype=torch.float32, device=dev) if _CE_COLSUM else None
+    deferred = defer_loss_sum(dev, ws, nblk, inv, loss)
+    _lib.call("gnn_gat_out_ce_f32", plan.c_graph, p, y.data_ptr(), m8.data_ptr(), w.data_ptr(), float(inv),
+              buf.data_ptr() + C * 4, 2 * C, _lib.ptr(cs), None if deferred else loss.data_ptr(), ws.data_ptr(),
+              ws.numel() * 4, _lib.stream_handle(dev))
+    if cs is not None:
+        buf._gnnmp_colsum = cs
+    return (key, loss, buf, ws)
+
+
 def masked_cross_entropy(logits: torch.Tensor, y: torch.Tensor, mask: torch.Tensor, class_w: torch.Tensor,
                          denom: float | None = None) -> torch.Tensor:
     """Σ_{i: mask_i} CE_w(logits_i, y_i) / denom (denom defaults to mask.sum(): the reference's .mean()).

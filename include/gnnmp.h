@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 21
+#define GNNMP_ABI_VERSION 22
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -318,6 +318,16 @@ typedef struct {
                                              multiplied by edge_w[s] after the softmax */
 } gnn_gat_fwd_params;
 gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fwd_params* p, gnn_stream_t stream);
+/* GATNet's output conv (src/models/gnn.py:67,75: heads 1, C <= 2, concat False, no act / dropout /
+ * edge_w) in the narrow slot-parallel form, optionally with the masked CE in the same launch
+ * (round 6, ABI 22): out, a_src, a_dst and alpha exactly as gnn_gat_fwd_fused_f32 defines them
+ * (online softmax per row; fp32-close, not bitwise, to the lane-group kernel), then — y non-NULL —
+ * gnn_masked_ce_f32 of the logits with its workspace contract (loss NULL: partials deferred),
+ * dlogits, and colsum (optional) the per-256-row-block column sums of dlogits as
+ * gnn_masked_ce_colsum_f32 writes them.  N >= 1. */
+gnn_status gnn_gat_out_ce_f32(const gnn_graph* g, const gnn_gat_fwd_params* p, const int64_t* y, const uint8_t* mask,
+                              const float* class_w, float inv_denom, float* dlogits, int64_t ld_d, float* colsum,
+                              float* loss, void* workspace, size_t workspace_bytes, gnn_stream_t stream);
 
 /* Gradient through y = dropout(act(pre)) from y itself (F.elu / F.dropout backward, gnn.py:73-74):
  * dpre = dy * keep * 1/(1-p) * act'(pre), ELU' = 1 for y > 0 else exp(pre) = y*(1-p) + 1.

@@ -179,6 +179,44 @@ def test_gcn_step_with_fused_ce_equals_separate(device, dropout, unit):
         assert torch.equal(g1[k], g2[k]), k
 
 
+@pytest.mark.parametrize("dropout", [0.0, 0.5])
+@pytest.mark.parametrize("unit", [False, True])
+def test_gat_step_with_fused_ce_equals_separate(device, dropout, unit):
+    """GAT (configs[2] preset 2L 4x16): the output conv in the narrow form with the CE in its
+    launch (gnn_gat_out_ce_f32 under loss_fn.target) and with the CE in its own launch:
+    bit-identical logits, loss and every gradient (the output bias gradient from the fused
+    launch's dlogits column sums on the unit_gradient path included)."""
+    from elliptic_gnn_project_amd import aggregation
+    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn, build_model
+    from elliptic_gnn_project_amd.train_ops import unit_gradient
+
+    data = _data(4000, 5000, 9, device)
+    cw = pyg_ref.class_weight(data.y[data.train_mask].cpu())
+    denom = float(data.train_mask.sum())
+    res = []
+    for on in (True, False):
+        aggregation._GAT_CE = on
+        try:
+            torch.manual_seed(11)
+            model = build_model("gat", data.x.size(1), dict(hidden_dim=64, heads=4, layers=2, dropout=dropout)).to(device)
+            loss_fn = _make_loss_fn({}, cw, model, 1, 34)
+            model.train()
+            torch.manual_seed(5)
+            with loss_fn.target(data.y, data.train_mask, denom):
+                logits = model(data.x, data.edge_index)
+            assert (getattr(logits, "_gnnmp_ce", None) is not None) == on
+            loss = loss_fn.full(logits, data.y, data.train_mask, denom=denom)
+            loss.backward(unit_gradient(device)) if unit else loss.backward()
+            res.append((logits.detach().clone(), loss.detach().clone(),
+                        {k: p.grad.clone() for k, p in model.named_parameters()}))
+        finally:
+            aggregation._GAT_CE = True
+    (l1, s1, g1), (l2, s2, g2) = res
+    assert torch.equal(l1, l2) and torch.equal(s1, s2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+
+
 @pytest.mark.parametrize("unit", [False, True])
 def test_resbn_step_with_fused_out_ce_equals_separate(device, unit):
     """SAGE-ResBN (configs[3]): its transform-first output conv runs the mean and the masked CE in
