@@ -140,15 +140,16 @@ int main(int argc, char** argv) {
     gemm_nt_h2_kernel<21, EPIF, 6><<<std::min(ntiles, 256), 256>>>(n, bh, cs, ntiles);  // MFMA only
     gemm_nt_h2_kernel<21, EPIF, 7><<<std::min(ntiles, 256), 256>>>(n, bh, cs, ntiles);  // B load + frame only
     gemm_nt_h2_kernel<21, EPIF | 64, 0><<<std::min(ntiles, 128), 256>>>(n, bh, cs, ntiles);  // 128 blocks (tag 64)
-    for (int nb : {256, 128, 64}) {
+    for (int nb : {std::min(256, (int)ceil_div(ceil_div(M, 32), ceil_div(ceil_div(M, 32), 256))), 128, 64}) {
       TNArgs t = tn_args(nb);
-      if (nb == 256) {
+      if (nb > 128) {
         gemm_tn_h2_kernel<11, false, 0, 8><<<nb, 512>>>(t);
         gemm_tn_h2_kernel<11, false, 1, 8><<<nb, 512>>>(t);  // no MFMA
         gemm_tn_h2_kernel<11, false, 2, 8><<<nb, 512>>>(t);  // no staging
         gemm_tn_h2_kernel<11, false, 128, 8><<<nb, 512>>>(t);  // no slab stores
         gemm_tn_h2_kernel<11, false, 3, 8><<<nb, 512>>>(t);  // no MFMA, no staging: prologue + slab
         gemm_tn_h2_kernel<11, false, 131, 8><<<nb, 512>>>(t);  // prologue only
+        gemm_tn_h2_kernel<11, false, 16, 8><<<nb, 512>>>(t);  // A ring of two sets (3 chunks ahead)
         lab_reduce_kernel<256><<<rb, 256>>>(slab, stride, nb, out, nout);
       } else if (nb == 128) {
         gemm_tn_h2_kernel<11, false, 32, 8><<<nb, 512>>>(t);  // (tag 32: the same kernel at 128 blocks)
