@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["GNNMP_LIB"]) if os.environ.get("GNNMP_LIB") else PKG_DIR / "libgnnmp.so"  # (GNNMP_LIB: A/B builds)
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -24,6 +24,7 @@ DTYPE_BF16 = 1
 # gnn_gemm_math
 MATH_SPLIT_BF16 = 0
 MATH_F32 = 1
+MATH_HALF_PAIR = 2  # ABI 23: f32 operands split into half-pair f16 in the kernel (3 products)
 
 # gnn_planes_format
 PLANES_SPLIT_BF16 = 0
@@ -127,6 +128,7 @@ class GnnGemmNTParams(ctypes.Structure):
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
         ("planes_format", c_i32), ("keep_mask", c_ptr), ("b_ready", c_i32), ("planes_exp", c_i32),
         ("colsum_part", c_ptr), ("colsum_cap", c_i64),
+        ("row_exp", c_ptr),
     ]
 
 
@@ -145,6 +147,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("a_planes", c_ptr), ("planes_ld", c_i64), ("planes_stride", c_i64), ("planes_col2", c_i64),
         ("planes_format", c_i32), ("g_dtype", c_i32), ("planes_exp", c_i32),
         ("sq_partial", c_ptr), ("sq_step", c_ptr), ("sq_skip_lo", c_i64), ("sq_skip_hi", c_i64), ("sq_cap", c_i64),
+        ("row_exp", c_ptr),
     ]
 
 

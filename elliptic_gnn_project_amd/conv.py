@@ -30,6 +30,9 @@ from .linear import Linear, linear, linear2, linear_stacked
 # a transform-first output conv under the step's fused_ce_target runs its mean and the masked CE in
 # one launch (gnn_sage_out_mean_ce_f32, as the fused 2-layer SAGE does); GNNMP_OUT_CE=0: A/B
 _OUT_CE = os.environ.get("GNNMP_OUT_CE", "1") != "0"
+# the aggregate-first SAGEConv (SAGE-ResBN's hidden layers) on the in-kernel half-pair GEMMs
+# (GNN_MATH_HALF_PAIR, round 6); GNNMP_H2S=0 keeps them on split-bf16 (A/B)
+_H2S = os.environ.get("GNNMP_H2S", "1") != "0"
 
 __all__ = ["SAGEConv", "GCNConv", "GATConv"]
 
@@ -105,14 +108,20 @@ class _SAGEAggregateFirst(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
     def forward(ctx, x, wl, wr, bias, plan: GraphPlan, res: bool = False):
-        from .fused import gemm_nt
+        from .fused import gemm_nt, h2s_nt_ok
         from .linear import _rows
         x = _rows(x)
         agg = aggregate(plan, x, _lib.AGG_MEAN, nodew=plan.deg)
         wl = wl.contiguous()
         wr = wr.contiguous()
-        y = gemm_nt(agg, None, wl.size(0), a2=x, bias=bias, w1=wl, w2=wr)
-        ctx.save_for_backward(agg, x, wl, wr)
+        fi, fo = wl.size(1), wl.size(0)
+        # the half-pair GEMMs (3 f16 products, operands split in the kernel with per-row / per-block
+        # power-of-two scales: gnnmp.h GNN_MATH_HALF_PAIR) when all three shapes take them: the
+        # forward NT writes the row exponents of [agg | x] that the backward's TN bounds A with
+        h2 = _H2S and h2s_nt_ok(fo, fi, fi) and h2s_nt_ok(2 * fi, fo, 0) and fo % 4 == 0 and x.size(0) >= 16
+        rexp = torch.empty(x.size(0), dtype=torch.int32, device=x.device) if h2 else None
+        y = gemm_nt(agg, None, fo, a2=x, bias=bias, w1=wl, w2=wr, math="half_pair" if h2 else None, row_exp=rexp)
+        ctx.save_for_backward(agg, x, wl, wr, rexp)
         ctx.plan = plan
         ctx.has_bias = bias is not None
         ctx.res = bool(res)
@@ -123,17 +132,18 @@ class _SAGEAggregateFirst(torch.autograd.Function):
     def backward(ctx, dy, dr=None):
         from .fused import gemm_nt, gemm_tn
         from .linear import _rows
-        agg, x, wl, wr = ctx.saved_tensors
+        agg, x, wl, wr, rexp = ctx.saved_tensors
         plan = ctx.plan
         dy = _rows(dy)
         need = ctx.needs_input_grad
         dWl = dWr = db = dx = None
+        gmath = "half_pair" if rexp is not None else None
         if need[1] or need[2] or need[3]:
-            (dWl, dWr), db, _, _ = gemm_tn(wl.size(0), agg, x, g=dy)
+            (dWl, dWr), db, _, _ = gemm_tn(wl.size(0), agg, x, g=dy, math=gmath, row_exp=rexp)
         if need[0]:
             fi = wl.size(1)
             wt = torch.cat([wl.t(), wr.t()], dim=0)  # [2·F_in, F_out]: Linear-weight form, one copy kernel
-            d = gemm_nt(dy, None, 2 * fi, w1=wt)
+            d = gemm_nt(dy, None, 2 * fi, w1=wt, math=gmath)
             dx = aggregate(plan, d[:, :fi], _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, addend=d[:, fi:],
                            addend2=dr if (ctx.res and dr is not None) else None)
         return (dx, dWl if need[1] else None, dWr if need[2] else None,

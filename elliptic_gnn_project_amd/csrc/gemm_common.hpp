@@ -73,6 +73,7 @@ struct NTArgs {
   int32_t ap_exp; // half-pair: the image holds A · 2^ap_exp (undone in the epilogue's column scale)
   const uint32_t* kmask;  // optional dropout keep bits (half-pair NT): bit c of kmask[r·4 + c/32]
   float* colsum_part;     // optional (skinny-K NT): per-block column sums of the stored C, [nb][Nc]
+  int32_t* rowexp;        // optional (in-kernel half-pair NT): per-row exponents E_r, max |A[r,:]| < 2^E_r
 };
 
 // the half-pair NT's B-image prep (ws_prep_h2_cols below)
@@ -188,6 +189,7 @@ struct TNArgs {
   const uint16_t* ap; int32_t ap_ld; int32_t ap_col2; int64_t ap_ps;  // split image of [A1 | A2] (as NTArgs)
   int32_t ap_h2;  // half-pair image (2 f16 planes)
   int32_t ap_exp; // half-pair: the image holds A · 2^ap_exp (undone in the slab scale)
+  const int32_t* rowexp;  // in-kernel half-pair TN: per-row exponents bounding A's rows (the NT's)
 };
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,
@@ -195,6 +197,13 @@ struct TNArgs {
 void launch_nt_x3(const NTArgs& a, void* ws, size_t ws_bytes, hipStream_t st);
 size_t nt_x3_workspace(int64_t k1, int64_t k2);
 void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st);  // NPL = 3, or 1 when a_bf16
+// the in-kernel half-pair forms (GNN_MATH_HALF_PAIR, gemm_x3.hip): f32 operands split into f16
+// hi / lo with power-of-two scales (NT: per A row; TN: per row block), 3 products
+bool nt_h2s_ok(const NTArgs& a);
+size_t nt_h2s_workspace(int64_t k1, int64_t k2);
+void launch_nt_h2s(const NTArgs& a, void* ws, hipStream_t st);
+bool tn_h2s_ok(const TNArgs& a);
+void launch_tn_h2s(const TNArgs& a, int nblk, hipStream_t st);
 
 // weight-stationary persistent split-bf16 NT (gemm_ws.hip): B fragments resident in registers,
 // one block per CU sweeping 32-row tiles.  nt_ws_ok: the shapes/epilogues it takes.  `img`: at
@@ -217,6 +226,7 @@ H2Prep h2_prep_of(const NTArgs& a, uint4* img);  // the prep of the half-pair NT
 // *out filled when p selects the half-pair NT with a large enough workspace, else UNSUPPORTED
 gnn_status nt_h2_prep_from_params(const gnn_gemm_nt_params* p, H2Prep* out, const char* fn);
 void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st, int phase = NT_PHASE_ALL);
+void launch_prep_h2(const H2Prep& p, hipStream_t st);  // ws_prep_h2_kernel over p (gemm_ws.hip)
 bool tn_h2_ok(const TNArgs& a);
 void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st);
 bool tn_planes_ok(const TNArgs& a);

@@ -767,6 +767,15 @@ int tn_blocks(int64_t M) {
   const int64_t per = ceil_div(chunks, 256);
   return (int)ceil_div(chunks, per);
 }
+// the in-kernel half-pair TN at Nr <= 64, k1 + k2 <= 128 holds three blocks per CU (its LDS is
+// sized by its k-tiles and 64 G rows, 47 KB): three times the blocks, so three times the chunk loads
+// in flight per CU (its chunk loop is latency-bound: one 16-row chunk in flight per block)
+int tn_blocks2(int64_t M) {
+  const int64_t chunks = ceil_div(M, 32);
+  if (chunks <= 0) return 1;
+  const int64_t per = ceil_div(chunks, 768);
+  return (int)ceil_div(chunks, per);
+}
 
 }  // namespace
 }  // namespace gnnmp
@@ -792,9 +801,12 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
   if (p->dropout_p < 0.f || p->dropout_p >= 1.f) return fail(GNN_ERR_INVALID_ARG, fn, "dropout p in [0,1)");
   if (p->dropout_p > 0.f && (int64_t)p->M * (int64_t)p->N >= ((int64_t)1 << 32))
     return fail(GNN_ERR_UNSUPPORTED, fn, "dropout element index (rows x width) must be < 2^32");
-  if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, fn, "bad math mode");
+  if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32 && p->math != GNN_MATH_HALF_PAIR)
+    return fail(GNN_ERR_INVALID_ARG, fn, "bad math mode");
   if ((p->a_dtype != GNN_DTYPE_F32 && p->a_dtype != GNN_DTYPE_BF16) || (p->c_dtype != GNN_DTYPE_F32 && p->c_dtype != GNN_DTYPE_BF16))
     return fail(GNN_ERR_INVALID_ARG, fn, "bad dtype");
+  if (p->row_exp && (p->a_planes || p->colsum_part || phase != NT_PHASE_ALL))
+    return fail(GNN_ERR_UNSUPPORTED, fn, "row_exp needs the in-kernel half-pair NT over f32 A1 / A2");
   if (p->M == 0 && phase != NT_PHASE_PREP) return GNN_OK;
   NTArgs a{};
   a.M = p->M; a.Nc = (int32_t)p->N;
@@ -878,12 +890,22 @@ static gnn_status gemm_nt_dispatch(const gnn_gemm_nt_params* p, gnn_stream_t str
   if (phase != NT_PHASE_ALL)  // prep_b / b_ready: only the image-A kernels have a separate B image
     return fail(phase == NT_PHASE_PREP ? GNN_ERR_UNSUPPORTED : GNN_ERR_INVALID_ARG, fn,
                 "a separate B prep (prep_b / b_ready) needs an image-A kernel (gnn_gemm_nt_planes_ok)");
-  if (launch_nt_skinny(a, st)) return hip_check(hipGetLastError(), fn);  // Nc <= 8 or K <= 8
+  const bool h2s = p->math == GNN_MATH_HALF_PAIR && nt_h2s_ok(a) && p->workspace &&
+                   p->workspace_bytes >= nt_h2s_workspace(a.k1, a.k2);
+  if (p->row_exp && !h2s)  // (checked before the skinny forms: a caller asking for row_exp gets it or an error)
+    return fail(GNN_ERR_UNSUPPORTED, fn, "row_exp needs the in-kernel half-pair NT (GNN_MATH_HALF_PAIR, the w1/w2 "
+                                         "form, N <= 128, k1 / k2 multiples of 16, k1 + k2 <= 128, f32, a workspace)");
+  if (!p->row_exp && launch_nt_skinny(a, st)) return hip_check(hipGetLastError(), fn);  // Nc <= 8 or K <= 8
   if (p->mask) return fail(GNN_ERR_UNSUPPORTED, fn, "the mask epilogue needs a skinny shape (K <= 8 or N <= 8)");
   if (a.a_bf16 || a.c_bf16) {
     if (!a.a_bf16 || !a.w1 || a.Nc > BN || p->math == GNN_MATH_F32)
       return fail(GNN_ERR_UNSUPPORTED, fn, "bf16 NT needs bf16 A, the w1/w2 form, N <= 128 and split math");
     launch_nt_x3(a, p->workspace, p->workspace_bytes, st);
+    return hip_check(hipGetLastError(), fn);
+  }
+  if (h2s) {  // in-kernel half-pair (gemm_x3.hip, ABI 23)
+    a.rowexp = p->row_exp;
+    launch_nt_h2s(a, p->workspace, st);
     return hip_check(hipGetLastError(), fn);
   }
   if (p->math != GNN_MATH_F32 && a.w1 && a.Nc <= BN) {
@@ -919,6 +941,7 @@ extern "C" gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t 
   stride = (stride + 63) / 64 * 64;
   int64_t nb = tn_blocks(M);
   if (Nr <= 8 && nproj == 0) nb = std::max<int64_t>(nb, tn_skinny_blocks(M));  // gemm_skinny.hip
+  if (Nr <= 64 && Kc <= 128 && nproj == 0) nb = std::max<int64_t>(nb, tn_blocks2(M));  // the narrow half-pair TN
   *bytes = (size_t)nb * stride * sizeof(float);
   return GNN_OK;
 }
@@ -956,7 +979,8 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
     return fail(GNN_ERR_INVALID_ARG, __fn, "need g (or dz + proj)");
   }
   if (p->h && p->ldh < p->Nr) return fail(GNN_ERR_INVALID_ARG, __fn, "bad ldh");
-  if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32) return fail(GNN_ERR_INVALID_ARG, __fn, "bad math mode");
+  if (p->math != GNN_MATH_SPLIT_BF16 && p->math != GNN_MATH_F32 && p->math != GNN_MATH_HALF_PAIR)
+    return fail(GNN_ERR_INVALID_ARG, __fn, "bad math mode");
   if (p->gout && p->ldgout < p->Nr) return fail(GNN_ERR_INVALID_ARG, __fn, "bad ldgout");
   const int32_t nproj = p->dz ? p->nproj : 0;
   const int64_t Kc = p->k1 + p->k2;
@@ -1054,6 +1078,18 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   // the split kernel indexes rows with 32-bit element offsets and loads whole 16-row chunks
   if (a.a_bf16 && (p->math == GNN_MATH_F32 || (a.M + 32) * ldmax >= ((int64_t)1 << 31) || a.M < 16))
     return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 TN needs split math, M >= 16 and M*ld < 2^31");
+  a.rowexp = p->row_exp;
+  if (p->math == GNN_MATH_HALF_PAIR && tn_h2s_ok(a) && (a.M + 32) * ldmax < ((int64_t)1 << 31)) {
+    if (a.Nr <= 64 && Kc <= 128 && !nproj && workspace_bytes >= (size_t)tn_blocks2(a.M) * stride * sizeof(float)) {
+      nblk = tn_blocks2(a.M);
+      a.rows_per_block = ceil_div(ceil_div(a.M, 32), nblk) * 32;
+    }
+    launch_tn_h2s(a, nblk, st);  // in-kernel half-pair MFMA (gemm_x3.hip, ABI 23)
+    GNN_LAUNCH_CHECK();
+    slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nblk, out, n_out, sqo);
+    GNN_LAUNCH_CHECK();
+    return GNN_OK;
+  }
   if (p->math != GNN_MATH_F32 && (a.M + 32) * ldmax < ((int64_t)1 << 31) && a.M >= 16) {
     launch_tn_x3(a, nblk, st);  // split-bf16 MFMA (gemm_x3.hip)
     GNN_LAUNCH_CHECK();

@@ -1395,6 +1395,10 @@ H2Prep h2_prep_of(const NTArgs& a, uint4* img) {
   return p;
 }
 
+void launch_prep_h2(const H2Prep& p, hipStream_t st) {
+  ws_prep_h2_kernel<<<WS_PREP_GRID, WS_PREP_THREADS, 0, st>>>(p);
+}
+
 // workspace: the B image (NKS k-steps x 3 planes x 256 slots x 16 B), then the 128 column scales
 template <int NKS>
 void launch_nt_h2_k(const NTArgs& a, uint4* img, hipStream_t st, int phase) {

@@ -59,6 +59,29 @@ __device__ __forceinline__ floatx16 mfma_planes(const bf16x8 (&x)[NPL], const bf
 
 __device__ __forceinline__ bf16x8 lds_frag(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// ---- the in-kernel half-pair form (GNN_MATH_HALF_PAIR, round 6).  An f32 operand v, scaled by a
+// power of two s into |v·s| < 2^14 (A) or < 16 (G), is held as two f16 planes hi = RNE_f16(v·s),
+// lo = RNE_f16((v·s − hi)·2^11) (gemm_common.hpp split_h2_pair); the other operand carries three
+// (hi' = 2^11 hi, hi, lo), and a product is three f16 MFMAs, lo·hi + hi·lo + hi·hi' (the dropped
+// lo·lo is 2^-22 relative) — the arithmetic of the half-pair image kernels with the split done while
+// staging, so it serves operands that change every step (SAGE-ResBN's hidden layers).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f16x8 lds_frag16(const uint16_t* p) { return *reinterpret_cast<const f16x8*>(p); }
+__device__ __forceinline__ floatx16 mfma_h2(const f16x8& x_hi, const f16x8& x_lo, const f16x8& y_hi2,
+                                            const f16x8& y_hi, const f16x8& y_lo, floatx16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(x_lo, y_hi, c, 0, 0, 0);  // small terms first
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(x_hi, y_lo, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(x_hi, y_hi2, c, 0, 0, 0);
+  return c;
+}
+// 2^(14 − E) for a row bound m < 2^E (A rows into |v·s| < 2^14); E = 0 for m = 0, 128 non-finite
+__device__ __forceinline__ int h2_row_exp(float m) {
+  if (!isfinite(m)) return 128;
+  int E = 0;
+  if (m > 0.f) frexpf(m, &E);
+  return E;
+}
+
 // p + e elements of a buffer that holds f32 or (BF) bf16
 template <bool BF>
 __device__ __forceinline__ const float* elem_ptr(const float* p, int64_t e) {
@@ -150,6 +173,37 @@ __device__ __forceinline__ void x3_store_rows(uint16_t* L, int64_t r0, int64_t r
     uint16_t* d = L + r * PITCH + k;
 #pragma unroll
     for (int p = 0; p < NPL; ++p) {
+      if constexpr (U == 8) *reinterpret_cast<uint4*>(d + p * PL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+      else if constexpr (U == 4) *reinterpret_cast<uint2*>(d + p * PL) = make_uint2(w[0][p], w[1][p]);
+      else *reinterpret_cast<uint32_t*>(d + p * PL) = w[0][p];
+    }
+  }
+}
+
+// The half-pair form of x3_store_rows: unit i's row scaled by sc[i] (a power of two, exact), two
+// f16 planes hi / lo; zero outside (rows, klen).
+template <int U, int KC, int ROWS, int PITCH>
+__device__ __forceinline__ void h2_store_rows(uint16_t* L, int64_t r0, int64_t rows, int klen, const float* reg,
+                                              const float* sc) {
+  constexpr int UPR = KC / U;
+  constexpr int PL = ROWS * PITCH;
+#pragma unroll
+  for (int i = 0; i < ROWS * KC / 256 / U; ++i) {
+    const int v = threadIdx.x + 256 * i;
+    const int r = v / UPR;
+    const int k = (v % UPR) * U;
+    const bool rok = r0 + r < rows;
+    uint32_t w[U / 2][2];
+#pragma unroll
+    for (int j = 0; j < U / 2; ++j) {
+      const int kk = k + 2 * j;
+      const float e0 = (rok && kk < klen) ? reg[i * U + 2 * j] * sc[i] : 0.0f;
+      const float e1 = (rok && kk + 1 < klen) ? reg[i * U + 2 * j + 1] * sc[i] : 0.0f;
+      split_h2_pair(e0, e1, w[j][0], w[j][1]);
+    }
+    uint16_t* d = L + r * PITCH + k;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
       if constexpr (U == 8) *reinterpret_cast<uint4*>(d + p * PL) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
       else if constexpr (U == 4) *reinterpret_cast<uint2*>(d + p * PL) = make_uint2(w[0][p], w[1][p]);
       else *reinterpret_cast<uint32_t*>(d + p * PL) = w[0][p];
@@ -369,6 +423,107 @@ void launch_nt_x3_a(const NTArgs& a, int av, const uint4* bimg, hipStream_t st) 
   else launch_nt_x3_b<KC, TM, 1, AU, D>(a, bimg, st);
 }
 
+// ---- the in-kernel half-pair NT (GNN_MATH_HALF_PAIR, round 6): C = epi([A1 | A2] · [W1 | W2]ᵀ) for
+// f32 A changing every step (SAGE-ResBN's hidden layers: K = 128, N = 64 forward, K = 64, N = 128
+// for the input gradient).  Block: 128 rows x NTL·32 columns, 4 waves of 32 rows.  ALL NCH 16-deep
+// chunks of the block's A rows are loaded up front (8 floats per thread per chunk, every load in
+// flight at once: the chunk loop then waits only on LDS), which also gives each row its exponent
+// E_r (max_k |A[r,k]| < 2^E_r, a butterfly over the row's 4 lanes); A is staged per chunk as f16
+// hi / lo of A[r,:]·2^(14 − E_r) and B from the half-pair image (ws_prep_h2_cols, k-step s = chunk
+// s) two chunks ahead; three f16 products per k-step; the epilogue multiplies row r, column n by
+// 2^(E_r − 14)·2^(e_n − 11) (exact) before the shared bias / ReLU / dropout / projection epilogue.
+// NTL = 2 (N <= 64): the B columns past 64 are neither staged nor multiplied.
+template <int NCH, int NTL, int AV>
+__global__ __launch_bounds__(256) void gemm_nt_h2s_kernel(NTArgs a, const uint4* __restrict__ bimg) {
+  constexpr int KC = 16, P = KC + 8, BM = 128, AU = 4, UPR = KC / AU;
+  constexpr int NBC = NTL * 32;                    // B columns staged
+  constexpr int APL = BM * P, BPL = NBC * P;
+  constexpr int AREG = BM * KC / 256, NUA = AREG / AU;
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][2 * APL];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * BPL];
+  __shared__ float rsc[BM];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int nch1 = a.k1 / KC;
+  const uint64_t seed = a.seed_ptr ? (*a.seed_ptr) * 0x9E3779B97F4A7C15ull + a.seed : a.seed;
+  float ra[NCH][AREG];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const float* A = c < nch1 ? a.a1 : a.a2;
+    const int64_t lda = c < nch1 ? a.lda1 : a.lda2;
+    const int k0 = (c < nch1 ? c : c - nch1) * KC;
+    x3_load_rows<AV, AU, KC, BM>(A, lda, m0, a.M, k0, KC, ra[c]);
+  }
+  const bool bon = threadIdx.x < 2 * NBC;          // slot 2n + khalf of a staged column
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));  // (a plain vector: stays in registers)
+  u32x4v rb[2][3];
+  const u32x4v* bim = reinterpret_cast<const u32x4v*>(bimg);
+  auto load_b = [&](int s, int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) rb[s][p] = bim[((int64_t)c * 3 + p) * 256 + threadIdx.x];
+  };
+  load_b(0, 0);
+  load_b(1, min(1, NCH - 1));
+  // the row exponents (rows fixed across chunks: unit i holds row (tid + 256 i) / UPR)
+  float asc[NUA];
+  {
+    float mx[NUA];
+#pragma unroll
+    for (int i = 0; i < NUA; ++i) {
+      mx[i] = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < AU; ++j) mx[i] = fmaxf(mx[i], fabsf(ra[c][i * AU + j]));
+#pragma unroll
+      for (int o = 1; o < UPR; o <<= 1) mx[i] = fmaxf(mx[i], __shfl_xor(mx[i], o));
+      const int r = (threadIdx.x + 256 * i) / UPR;
+      const int E = h2_row_exp(mx[i]);
+      asc[i] = E == 128 ? 1.0f : ldexpf(1.0f, 14 - E);
+      if ((threadIdx.x % UPR) == 0) {
+        rsc[r] = E == 128 ? 1.0f : ldexpf(1.0f, E - 14);
+        if (a.rowexp && m0 + r < a.M) a.rowexp[m0 + r] = E;
+      }
+    }
+  }
+  floatx16 acc[1][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][t][r] = 0.0f;
+  const int fr = (lane & 31) * P + 8 * (lane >> 5);
+  const int bn = threadIdx.x >> 1, bkh = threadIdx.x & 1;
+  static_for<NCH>([&](auto cc) __attribute__((always_inline)) {  // (static: ra / rb stay in registers)
+    constexpr int c = decltype(cc)::value;
+    constexpr int buf = c & 1;
+    h2_store_rows<AU, KC, BM, P>(As[buf], m0, a.M, KC, ra[c], asc);
+    if (bon) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4v*>(&Bs[buf][p * BPL + bn * P + 8 * bkh]) = rb[buf][p];
+    }
+    __syncthreads();
+    if constexpr (c + 2 < NCH) load_b(buf, c + 2);
+    f16x8 af[2], bf[NTL][3];
+    const uint16_t* Ab = As[buf] + wave * 32 * P + fr;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) af[p] = lds_frag16(Ab + p * APL);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bf[t][p] = lds_frag16(Bs[buf] + fr + p * BPL + t * 32 * P);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) acc[0][t] = mfma_h2(af[0], af[1], bf[t][0], bf[t][1], bf[t][2], acc[0][t]);
+  });
+  const float* csc = reinterpret_cast<const float*>(bimg + (int64_t)NCH * 3 * 256);
+#pragma unroll
+  for (int t = 0; t < NTL; ++t) {  // undo the row and column scales (powers of two: exact)
+    const float cs = csc[t * 32 + (lane & 31)];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][t][r] *= rsc[wave * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)] * cs;
+  }
+  nt_epilogue<1, false>(a, acc, m0, 0, lane, wave, seed);
+}
+
 // ------------------------------------------------------------------------------------- TN
 constexpr int TMC = 16;            // rows per chunk = one MFMA k-step
 constexpr int TP = TMC + 8;        // bf16 per transposed LDS row (12 dwords: conflict-free b128)
@@ -391,13 +546,26 @@ constexpr int TX_AS = 3;           // A unit slots per thread (u = tid + 256·s 
 // (HBF) are read as bf16, G is rounded to bf16, one product per MFMA.
 // HALFN (Nr <= 64): waves 0-1 / 2-3 take the two 32-row halves of the output for the first /
 // second half of the k-tiles (KT per wave), instead of waves 2-3 running MFMAs on all-zero rows.
+// H2S (round 6, GNN_MATH_HALF_PAIR; the plain g form): the in-kernel half-pair form.  Before the
+// chunk loop (behind chunk 0's loads) the block takes E_A = max row_exp[r] over its rows (the
+// forward NT's row bounds of the same A) and E_G from max |g| over its rows (one pass, float4
+// pieces), stages A as f16 hi / lo of A·2^(14 − E_A) and G as hi' / hi / lo of G·2^(4 − E_G), runs
+// three products per k-tile, and writes acc·2^(E_A − 14)·2^(E_G − 15) to its slab (exact).
 template <bool PROJ, bool MASK, int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0,
-          bool GOUT = true, bool HALFN = false>
+          bool GOUT = true, bool HALFN = false, bool H2S = false>
 __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
+  static_assert(!H2S || (!PROJ && !MASK && !GOUT && NPL == 3 && !ABF && PIPE == 0), "half-pair: plain g form, f32");
   constexpr int NS = TX_AS + ((!PROJ && MASK) ? 2 : 1);  // + G slot (+ g slot)
   constexpr int GS = TX_AS;                              // the G slot index
-  __shared__ __attribute__((aligned(16))) uint16_t Gt[2][NPL * TGPL];
-  __shared__ __attribute__((aligned(16))) uint16_t At[2][NPL * TAPL];
+  constexpr int APN = H2S ? 2 : NPL;                     // A planes (H2S: hi, lo; G keeps 3: hi', hi, lo)
+  // A columns staged: the k-tiles the waves multiply (round 6: sized by KT, not KMAX — the narrow
+  // shapes then fit two blocks per CU, and a latency-bound chunk loop gets twice the loads in flight)
+  constexpr int KPM = (HALFN ? 2 * KT : KT) * 32;
+  constexpr int TAPLK = KPM * TP;
+  constexpr int TGPLK = (HALFN ? 64 : 128) * TP;  // G rows staged (HALFN: Nr <= 64)
+  __shared__ __attribute__((aligned(16))) uint16_t Gt[2][NPL * TGPLK];
+  __shared__ __attribute__((aligned(16))) uint16_t At[2][APN * TAPLK];
+  __shared__ float scan_red[2 * (TX_THREADS / 64)];
   __shared__ float Ps[MAXPROJ * 128];
   __shared__ float dzL[2][TX_THREADS];  // rows 0..63 used; all threads write (branch-free staging)
   const int tid = threadIdx.x;
@@ -438,8 +606,9 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   for (int sl = 0; sl < TX_AS; ++sl) {
     const int u = tid + TX_THREADS * sl;
     aon[sl] = u < 2 * KP;
-    // idle slots stage into column KMAX - 1: only read by a tile t >= nkt, whose dW is discarded
-    ak[sl] = aon[sl] ? u % KP : KMAX - 1;
+    // idle slots stage nothing (their loads read a fixed address; the LDS columns they would fill
+    // are only read by tiles t >= nkt, whose dW is discarded)
+    ak[sl] = aon[sl] ? u % KP : 0;
     oct[sl] = aon[sl] ? u / KP : 0;
     const int k = ak[sl];
     if (aon[sl] && k < a.k1) { base[sl] = elem_ptr<ABF>(a.a1, k); ld32[sl] = (int)a.lda1; }
@@ -483,12 +652,28 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 
   float db = 0.f, dzs = 0.f;
   float dw2[MAXPROJ] = {0.f, 0.f, 0.f, 0.f};
+  float sa = 1.f, sg = 1.f, una = 1.f, ung = 1.f;  // H2S: the block's A / G scales and their inverses
   auto put8 = [](uint16_t* dst, int plane, const float (&e)[8]) {
     uint32_t w[4][3];
 #pragma unroll
     for (int j = 0; j < 4; ++j) split_pair(e[2 * j], e[2 * j + 1], w[j]);
 #pragma unroll
     for (int p = 0; p < NPL; ++p)
+      *reinterpret_cast<uint4*>(dst + p * plane) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
+  };
+  // H2S: 8 values times the scale s as half-pair planes — NP = 2: hi, lo (A); NP = 3: hi', hi, lo (G)
+  auto put8h = [](uint16_t* dst, int plane, const float (&e)[8], float sc, auto npc) {
+    constexpr int NP = decltype(npc)::value;
+    uint32_t w[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t hi, lo;
+      split_h2_pair(e[2 * j] * sc, e[2 * j + 1] * sc, hi, lo);
+      if constexpr (NP == 3) { w[j][0] = h2_scale_pair(hi, 2048.0f); w[j][1] = hi; w[j][2] = lo; }
+      else { w[j][0] = hi; w[j][1] = lo; }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
       *reinterpret_cast<uint4*>(dst + p * plane) = make_uint4(w[0][p], w[1][p], w[2][p], w[3][p]);
   };
   auto store = [&](int d, int c) {
@@ -506,7 +691,11 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
     // and meet G = 0 there; columns >= Kc (padding, idle slots at KMAX - 1) only feed dW
     // columns that are never written out
 #pragma unroll
-    for (int sl = 0; sl < TX_AS; ++sl) put8(At[buf] + ak[sl] * TP + 8 * oct[sl], TAPL, rv[d][sl]);
+    for (int sl = 0; sl < TX_AS; ++sl) {
+      if (!aon[sl]) continue;  // (LDS stores only: the loads above stay unconditional)
+      if constexpr (H2S) put8h(At[buf] + ak[sl] * TP + 8 * oct[sl], TAPLK, rv[d][sl], sa, std::integral_constant<int, 2>{});
+      else put8(At[buf] + ak[sl] * TP + 8 * oct[sl], TAPLK, rv[d][sl]);
+    }
     float e[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -537,24 +726,45 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
       }
       e[i] = g;
     }
-    put8(Gt[buf] + gn * TP + 8 * go, TGPL, e);
+    if (HALFN && gn >= 64) return;  // (zero G columns past Nr <= 64: not staged)
+    if constexpr (H2S) put8h(Gt[buf] + gn * TP + 8 * go, TGPLK, e, sg, std::integral_constant<int, 3>{});
+    else put8(Gt[buf] + gn * TP + 8 * go, TGPLK, e);
   };
 
   const int fr = (lane & 31) * TP + 8 * (lane >> 5);
   auto compute = [&](int c) {
     const int buf = c & 1;
+    if constexpr (H2S) {  // G: hi', hi, lo; A: hi, lo
+      f16x8 gf[3], af[2][2];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) gf[p] = lds_frag16(Gt[buf] + p * TGPLK + ntile * 32 * TP + fr);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) af[0][p] = lds_frag16(At[buf] + p * TAPLK + t0 * 32 * TP + fr);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        if (t + 1 < KT) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p) af[(t + 1) & 1][p] = lds_frag16(At[buf] + p * TAPLK + (t0 + t + 1) * 32 * TP + fr);
+        }
+        // G_lo·A_hi + G_hi·A_lo + G_hi'·A_hi
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gf[2], af[t & 1][0], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gf[1], af[t & 1][1], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(gf[0], af[t & 1][0], acc[t], 0, 0, 0);
+      }
+      return;
+    }
     // software-pipelined: tile t+1's fragments are read before tile t's MFMAs issue, so with one
     // wave per SIMD the LDS latency hides behind the MFMAs instead of stalling every tile
     bf16x8 gf[NPL], af[2][NPL];
 #pragma unroll
-    for (int p = 0; p < NPL; ++p) gf[p] = lds_frag(Gt[buf] + p * TGPL + ntile * 32 * TP + fr);
+    for (int p = 0; p < NPL; ++p) gf[p] = lds_frag(Gt[buf] + p * TGPLK + ntile * 32 * TP + fr);
 #pragma unroll
-    for (int p = 0; p < NPL; ++p) af[0][p] = lds_frag(At[buf] + p * TAPL + t0 * 32 * TP + fr);
+    for (int p = 0; p < NPL; ++p) af[0][p] = lds_frag(At[buf] + p * TAPLK + t0 * 32 * TP + fr);
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       if (t + 1 < KT) {
 #pragma unroll
-        for (int p = 0; p < NPL; ++p) af[(t + 1) & 1][p] = lds_frag(At[buf] + p * TAPL + (t0 + t + 1) * 32 * TP + fr);
+        for (int p = 0; p < NPL; ++p) af[(t + 1) & 1][p] = lds_frag(At[buf] + p * TAPLK + (t0 + t + 1) * 32 * TP + fr);
       }
       acc[t] = mfma_planes<NPL>(gf, af[t & 1], acc[t]);
     }
@@ -568,6 +778,57 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) load(d, min(d, nch - 1));
+    if constexpr (H2S) {  // the block's bounds (behind chunk 0's loads): max row_exp, max |g|
+      // A: every row a chunk loads — from ldbase(0) = min(mbeg, M - 16), so a last block of < 16
+      // rows also bounds the earlier rows its clamped chunk re-reads (they meet G = 0, but an
+      // unbounded A there would overflow f16 and turn 0 · inf into NaN)
+      int ea = 0;
+      for (int64_t r = ldbase(0) + tid; r < mend; r += TX_THREADS) ea = max(ea, a.rowexp[r]);
+      float gm = 0.f;
+      const int n4 = a.Nr >> 2;
+      const int64_t npc = (mend - mbeg) * n4;
+      constexpr int SU = 8;
+      for (int64_t q0 = tid; q0 < npc; q0 += SU * TX_THREADS) {
+        float4 v[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const int64_t q = min(q0 + (int64_t)TX_THREADS * u, npc - 1);
+          const int64_t r = mbeg + q / n4;
+          v[u] = *reinterpret_cast<const float4*>(a.g + r * a.ldg + (q - (q / n4) * n4) * 4);
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+          const float m = fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w)));
+          gm = fmaxf(gm, q0 + (int64_t)TX_THREADS * u < npc ? m : 0.f);
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        ea = max(ea, __shfl_xor(ea, o));
+        gm = fmaxf(gm, __shfl_xor(gm, o));
+      }
+      if (lane == 0) {
+        scan_red[wave] = __int_as_float(ea);
+        scan_red[TX_THREADS / 64 + wave] = gm;
+      }
+    }
+  };
+  auto finish_scales = [&]() {  // after the prologue's barrier
+    if constexpr (H2S) {
+      int ea = __float_as_int(scan_red[0]);
+      float gm = scan_red[TX_THREADS / 64];
+#pragma unroll
+      for (int w = 1; w < TX_THREADS / 64; ++w) {
+        ea = max(ea, __float_as_int(scan_red[w]));
+        gm = fmaxf(gm, scan_red[TX_THREADS / 64 + w]);
+      }
+      const int eg = h2_row_exp(gm);
+      ea = min(ea, 127);
+      sa = ldexpf(1.0f, 14 - ea);
+      una = ldexpf(1.0f, ea - 14);
+      sg = eg == 128 ? 1.0f : ldexpf(1.0f, 4 - eg);  // |G · sg| < 16
+      ung = eg == 128 ? 1.0f / 2048.0f : ldexpf(1.0f, eg - 4 - 11);
+    }
   };
 
   // ---- this block's partial dW (segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2])
@@ -582,7 +843,7 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
         const int row = ntile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int64_t idx = col < a.k1 ? (int64_t)row * a.k1 + col
                                        : (int64_t)a.Nr * a.k1 + (int64_t)row * a.k2 + (col - a.k1);
-        if (row < a.Nr && col < Kc) slab[idx] = acc[t][r];
+        if (row < a.Nr && col < Kc) slab[idx] = H2S ? (acc[t][r] * una) * ung : acc[t][r];
       }
     }
   };
@@ -609,7 +870,8 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
 
   if (nch > 0) {
     prologue();
-    __syncthreads();  // Ps, dzL[0]
+    __syncthreads();  // Ps, dzL[0] (H2S: the scan partials)
+    finish_scales();
     if constexpr (PIPE != 0) {
       // software-pipelined order: between two barriers, chunk c+1 is staged into the other
       // buffers while chunk c's MFMAs run (PIPE == 2 adds interleave hints for the scheduler)
@@ -790,6 +1052,75 @@ void launch_tn_x3(const TNArgs& a, int nblk, hipStream_t st) {
   else if (nkt <= 8) launch_tn_x3_k<D, 8, 3, false, false, 0>(a, nblk, st);
   else if (nkt <= 11) launch_tn_x3_k<D, 11, 3, false, false, 0>(a, nblk, st);
   else launch_tn_x3_k<D, 12, 3, false, false, 0>(a, nblk, st);
+}
+
+// ---- the in-kernel half-pair forms (GNN_MATH_HALF_PAIR)
+bool nt_h2s_ok(const NTArgs& a) {
+  return !a.a_bf16 && !a.c_bf16 && a.w1 && !a.bt && a.Nc >= 1 && a.Nc <= BN && a.k1 % 16 == 0 && a.k2 % 16 == 0 &&
+         a.k1 + a.k2 >= 16 && a.k1 + a.k2 <= 128 && (a.k2 == 0 || a.w2) && !a.mask;
+}
+
+size_t nt_h2s_workspace(int64_t k1, int64_t k2) {  // the half-pair B image + BN column scales
+  return (size_t)(k1 / 16 + k2 / 16) * 3 * 256 * sizeof(uint4) + BN * sizeof(float);
+}
+
+void launch_nt_h2s(const NTArgs& a, void* ws, hipStream_t st) {
+  const int nch1 = a.k1 / 16, nch = nch1 + a.k2 / 16;
+  H2Prep p{};
+  p.w1 = a.w1; p.w2 = a.w2; p.ldw1 = a.ldw1; p.ldw2 = a.ldw2;
+  p.k1 = a.k1; p.k2 = a.k2; p.Nc = a.Nc; p.col2 = 16 * nch1;  // chunk c = k-step c
+  p.blocks = nch;
+  p.img = static_cast<uint4*>(ws);
+  p.colscale = reinterpret_cast<float*>(p.img + (size_t)nch * 3 * 256);
+  p.a_unscale = 1.0f;  // (the A scales are per row, undone in the kernel's epilogue)
+  launch_prep_h2(p, st);
+  auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
+  const bool v4 = (a.lda1 % 4 == 0) && al(a.a1, 16) && (a.k2 == 0 || ((a.lda2 % 4 == 0) && al(a.a2, 16)));
+  const bool v2 = (a.lda1 % 2 == 0) && al(a.a1, 8) && (a.k2 == 0 || ((a.lda2 % 2 == 0) && al(a.a2, 8)));
+  const dim3 grid((unsigned)ceil_div(a.M, 128));
+  const uint4* img = p.img;
+#define GNN_H2S_V(NCHV, NTLV)                                                                  \
+  do {                                                                                         \
+    if (v4) gemm_nt_h2s_kernel<NCHV, NTLV, 4><<<grid, 256, 0, st>>>(a, img);                  \
+    else if (v2) gemm_nt_h2s_kernel<NCHV, NTLV, 2><<<grid, 256, 0, st>>>(a, img);             \
+    else gemm_nt_h2s_kernel<NCHV, NTLV, 1><<<grid, 256, 0, st>>>(a, img);                     \
+  } while (0)
+#define GNN_H2S_N(NCHV) do { if (a.Nc <= 64) GNN_H2S_V(NCHV, 2); else GNN_H2S_V(NCHV, 4); } while (0)
+  switch (nch) {  // (nt_h2s_ok: 1 <= nch <= 8)
+    case 1: GNN_H2S_N(1); break;
+    case 2: GNN_H2S_N(2); break;
+    case 3: GNN_H2S_N(3); break;
+    case 4: GNN_H2S_N(4); break;
+    case 5: GNN_H2S_N(5); break;
+    case 6: GNN_H2S_N(6); break;
+    case 7: GNN_H2S_N(7); break;
+    default: GNN_H2S_N(8); break;
+  }
+#undef GNN_H2S_N
+#undef GNN_H2S_V
+}
+
+bool tn_h2s_ok(const TNArgs& a) {
+  auto al = [](const void* q, int b) { return (reinterpret_cast<uintptr_t>(q) % b) == 0; };
+  return a.rowexp && !a.dz && !a.h && !a.gout && a.g && !a.a_bf16 && !a.g_bf16 && a.Nr % 4 == 0 && a.Nr <= 128 &&
+         a.ldg % 4 == 0 && al(a.g, 16) && a.k1 + a.k2 <= KMAX && a.M >= 16;
+}
+
+void launch_tn_h2s(const TNArgs& a, int nblk, hipStream_t st) {
+  const int nkt = (a.k1 + a.k2 + 31) / 32;
+  constexpr int D = 1;
+#define GNN_TNH(KTV, HN) gemm_tn_x3_kernel<false, false, D, KTV, 3, false, false, 0, false, HN, true><<<nblk, TX_THREADS, 0, st>>>(a)
+  if (a.Nr <= 64) {  // the half-N mapping (as launch_tn_x3)
+    const int kh = (nkt + 1) / 2;
+    if (kh <= 2) GNN_TNH(2, true);
+    else if (kh <= 3) GNN_TNH(3, true);
+    else if (kh <= 4) GNN_TNH(4, true);
+    else GNN_TNH(6, true);
+  } else if (nkt <= 6) GNN_TNH(6, false);
+  else if (nkt <= 8) GNN_TNH(8, false);
+  else if (nkt <= 11) GNN_TNH(11, false);
+  else GNN_TNH(12, false);
+#undef GNN_TNH
 }
 
 }  // namespace gnnmp

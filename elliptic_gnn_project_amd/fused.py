@@ -78,7 +78,7 @@ MAX_PROJ = 4  # nproj = 2 * num_classes <= 4
 # K7 GEMM arithmetic (include/gnnmp.h gnn_gemm_math): "split_bf16" (default) runs every f32 operand
 # as hi+mid+lo bf16 terms on the bf16 matrix cores (6 products, fp32-accurate); "f32" runs the exact
 # f32 MFMA.  GNNMP_GEMM_MATH overrides the default.
-GEMM_MATH = {"split_bf16": _lib.MATH_SPLIT_BF16, "f32": _lib.MATH_F32}
+GEMM_MATH = {"split_bf16": _lib.MATH_SPLIT_BF16, "f32": _lib.MATH_F32, "half_pair": _lib.MATH_HALF_PAIR}
 _DEFAULT_MATH = GEMM_MATH[os.environ.get("GNNMP_GEMM_MATH", "split_bf16")]
 
 
@@ -121,9 +121,17 @@ def _planes_fields(planes):
 _BF_IMAGE = os.environ.get("GNNMP_BF_IMAGE", "1") != "0"
 
 
+def h2s_nt_ok(n: int, k1: int, k2: int, dtype=torch.float32) -> bool:
+    """Whether a w1/w2-form NT with math="half_pair" runs the in-kernel half-pair kernel (gemm_x3.hip
+    nt_h2s_ok; the skinny VALU shapes, n <= 8 or k <= 8, keep their own kernels): the shapes a
+    ``row_exp`` may be asked of."""
+    return dtype == torch.float32 and 8 < n <= 128 and k1 % 16 == 0 and k2 % 16 == 0 and 16 <= k1 + k2 <= 128
+
+
 def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, proj=None, z=None,
             out=None, want_c=True, seed_ptr=None, w1=None, w2=None, math=None, mask=None, mask_scale=1.0,
-            planes=None, check_planes=False, keep_mask=None, workspace=None, b_stage=None, colsum=False):
+            planes=None, check_planes=False, keep_mask=None, workspace=None, b_stage=None, colsum=False,
+            row_exp=None):
     """C = epilogue([a1 | a2] · B) on the NT kernels; B = bt ([K, n] row-major) or, with bt None,
     [w1 | w2]ᵀ read in place from PyTorch Linear weights w1 [n, k1], w2 [n, k2].
     bf16 A (the bf16-storage path) needs the w1/w2 form; C is then bf16 too.
@@ -136,7 +144,9 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
     GnnGemmNTParams (K1's prep_b: HalfPairImage.fill_mean).
     ``colsum``: also return Σ_rows C ([n] f32) — on the skinny-K form its blocks write the column
     sums as they store C (gnn_gemm_nt_params.colsum_part) and one small launch adds them
-    (gnn_colsum_finish_f32); otherwise a gnn_colsum_f32 pass over C.  Returns (C, Σ C)."""
+    (gnn_colsum_finish_f32); otherwise a gnn_colsum_f32 pass over C.  Returns (C, Σ C).
+    ``row_exp`` (int32 [M], math="half_pair", the shapes of h2s_nt_ok): receives the per-row
+    exponents of [a1 | a2] for a half-pair TN over the same operand (gemm_tn(row_exp=...))."""
     if planes is not None:
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
@@ -164,6 +174,8 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         *_planes_fields(planes), _lib.ptr(keep_mask), int(b_stage == "ready"),
         int(getattr(planes, "exp", 0)),
     )
+    if row_exp is not None:
+        p.row_exp = row_exp.data_ptr()
     part = None
     if colsum and out is not None and b_stage is None and not check_planes:
         nb = ctypes.c_int32(0)
@@ -191,7 +203,8 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
         # A split image is priced at the algorithmic f32 bytes; it moves 6 B / element.
         ea = 2 if bf else (4 if a1 is None else a1.element_size())
         prod = 0 if (_math(math) == _lib.MATH_F32 or w1 is None) else (1 if ea == 2 else 6)
-        if getattr(planes, "fmt", None) == _lib.PLANES_HALF_PAIR:
+        if getattr(planes, "fmt", None) == _lib.PLANES_HALF_PAIR or (
+                _math(math) == _lib.MATH_HALF_PAIR and planes is None and h2s_nt_ok(n, k1, k2, a1.dtype)):
             prod = 3  # f16 half-pair: 3 products
         if ea == 4 and proj is None and (n <= 8 or (k <= 8 and a2 is None)):
             prod = -1
@@ -209,12 +222,14 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
 
 
 def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gout=None, math=None,
-            planes=None, check_planes=False, sq=None, sq_skip=(0, 0)):
+            planes=None, check_planes=False, sq=None, sq_skip=(0, 0), row_exp=None):
     """((Gᵀ·a1, Gᵀ·a2), db, dzᵀ·h, dzsum) from one flat fp32 buffer — the MFMA TN kernel.
     ``planes``: A read from a split image (a1 / a2 may be None); ``check_planes`` as gemm_nt.
     ``sq`` = (partials buffer, step tensor) of train_ops.grad_sq_request: the reduce also writes
     the clip + Adam norm partials of the output outside ``sq_skip`` (indices into the flat output,
-    negative ones from its end), recorded by train_ops.grad_sq_produced."""
+    negative ones from its end), recorded by train_ops.grad_sq_produced.
+    ``row_exp``: the int32 row exponents a half-pair NT wrote for [a1 | a2]; with math="half_pair"
+    and the plain g form the TN then runs in half-pair arithmetic (gnn_gemm_tn_params.row_exp)."""
     if planes is not None:
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
@@ -238,6 +253,8 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         _lib.DTYPE_BF16 if any(t is not None and t.dtype == torch.bfloat16 for t in (g, gout)) else _lib.DTYPE_F32,
         int(getattr(planes, "exp", 0)),
     )
+    if row_exp is not None:
+        p.row_exp = row_exp.data_ptr()
     if check_planes:
         return bool(_lib.load().gnn_gemm_tn_planes_ok(p))
     out = torch.empty(n_out, dtype=torch.float32, device=dev)
@@ -262,7 +279,8 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         e1.record()
         ea = 2 if bf else (4 if a1 is None else a1.element_size())
         prod = 0 if _math(math) == _lib.MATH_F32 else (1 if ea == 2 else 6)
-        if getattr(planes, "fmt", None) == _lib.PLANES_HALF_PAIR:
+        if getattr(planes, "fmt", None) == _lib.PLANES_HALF_PAIR or (
+                _math(math) == _lib.MATH_HALF_PAIR and row_exp is not None and g is not None and dz is None):
             prod = 3
         if ea == 4 and nr <= 8 and dz is None and h is None and gout is None:
             prod = -1

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 22
+#define GNNMP_ABI_VERSION 23
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -383,7 +383,17 @@ typedef enum {
   GNN_MATH_SPLIT_BF16 = 0, /* default: every f32 operand split into hi+mid+lo bf16 terms, 6 products on
                               v_mfma_f32_32x32x16_bf16 (dropped terms <= ~2^-23 relative per product);
                               used for the w1/w2 NT form and the TN kernel, else falls back to: */
-  GNN_MATH_F32 = 1         /* exact f32 MFMA (v_mfma_f32_32x32x2_f32, a k-ordered fmaf chain) */
+  GNN_MATH_F32 = 1,        /* exact f32 MFMA (v_mfma_f32_32x32x2_f32, a k-ordered fmaf chain) */
+  GNN_MATH_HALF_PAIR = 2   /* (ABI 23) f32 operands split in the kernel into half-pair f16 terms
+                              (hi = RNE_f16(v·s), lo = RNE_f16((v·s − hi)·2^11)), 3 products on
+                              v_mfma_f32_32x32x16_f16, 2^-22 relative per operand, with power-of-two
+                              scales that keep every operand in f16 range: the NT per A row
+                              (max_k |A[r,k]| < 2^E_r, A[r,:]·2^(14−E_r)) and per B column; the TN per
+                              row block for A (from the NT's row_exp) and for G (a max|g| pass over
+                              the block's rows).  Taken by the w1/w2 NT (N <= 128, k1, k2 multiples of
+                              16, k1 + k2 <= 128, f32 A / C) and by the plain g-form TN given row_exp
+                              (Nr % 4 == 0, 16-byte aligned g rows); any other call runs as
+                              GNN_MATH_SPLIT_BF16 */
 } gnn_gemm_math;
 /* Skinny shapes run full-f32 VALU kernels whatever `math` says (the 2-class output layers,
  * gnn.py:23,66,124): NT with N <= 8 (K <= 384) or with K <= 8 (one A segment), f32 A/C and no
@@ -439,6 +449,10 @@ typedef struct gnn_gemm_nt_params {
                                             block: colsum_part[b * N + n], b < gnn_gemm_nt_colsum_blocks;
                                             capacity colsum_cap floats.  gnn_colsum_finish_f32 then
                                             gives Σ_rows C — a layer's bias gradient without a pass over C */
+  int32_t* row_exp;                      /* optional (ABI 23, GNN_MATH_HALF_PAIR form only): [M] per-row
+                                            exponents E_r with max_k |[A1|A2][r,k]| < 2^E_r (0 for a zero
+                                            row, 128 for a non-finite one) — the TN's A bound
+                                            (gnn_gemm_tn_params.row_exp) for the same operand */
 } gnn_gemm_nt_params;
 
 /* C = epilogue([A1|A2] · Bt). */
@@ -484,6 +498,10 @@ typedef struct {
                                             hand them to gnn_clip_adam_f32 (gnn_adam_group.grad_sq_partial) */
   const float* sq_step;
   int64_t sq_skip_lo, sq_skip_hi, sq_cap;
+  const int32_t* row_exp;                /* optional (ABI 23): [M] exponents bounding the rows of [A1|A2]
+                                            (max_k |A[r,k]| < 2^row_exp[r]), as a GNN_MATH_HALF_PAIR NT of
+                                            the same operand writes them; with math GNN_MATH_HALF_PAIR and
+                                            the plain g form the TN runs in half-pair arithmetic */
 } gnn_gemm_tn_params;
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).

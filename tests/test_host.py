@@ -153,7 +153,7 @@ STRUCTS = {
                                                "workspace_bytes", "a_dtype", "c_dtype", "mask", "ldmask",
                                                "mask_scale", "a_planes", "planes_ld", "planes_stride",
                                                "planes_col2", "planes_format", "keep_mask",
-                                               "b_ready", "planes_exp", "colsum_part", "colsum_cap"]),
+                                               "b_ready", "planes_exp", "colsum_part", "colsum_cap", "row_exp"]),
     "gnn_adam_tensor": ("GnnAdamTensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel"]),
     "gnn_adam_group": ("GnnAdamGroup", ["num_tensors", "lr", "beta1", "beta2", "eps", "weight_decay", "max_norm",
                                         "tensors", "skip_nonfinite", "bump_counter", "loss_partial", "loss_nblk",
@@ -163,7 +163,7 @@ STRUCTS = {
                                                "math", "a_dtype", "h_dtype", "a_planes", "planes_ld",
                                                "planes_stride", "planes_col2", "planes_format", "g_dtype",
                                                "planes_exp", "sq_partial", "sq_step", "sq_skip_lo", "sq_skip_hi",
-                                               "sq_cap"]),
+                                               "sq_cap", "row_exp"]),
 }
 
 
