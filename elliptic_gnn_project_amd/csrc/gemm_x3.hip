@@ -553,7 +553,7 @@ constexpr int TX_AS = 3;           // A unit slots per thread (u = tid + 256·s 
 // three products per k-tile, and writes acc·2^(E_A − 14)·2^(E_G − 15) to its slab (exact).
 template <bool PROJ, bool MASK, int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0,
           bool GOUT = true, bool HALFN = false, bool H2S = false>
-__global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
+__device__ __forceinline__ void gemm_tn_split_body(const TNArgs& a) {
   static_assert(!H2S || (!PROJ && !MASK && !GOUT && NPL == 3 && !ABF && PIPE == 0), "half-pair: plain g form, f32");
   constexpr int NS = TX_AS + ((!PROJ && MASK) ? 2 : 1);  // + G slot (+ g slot)
   constexpr int GS = TX_AS;                              // the G slot index
@@ -939,6 +939,18 @@ __global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
   side_write();
 }
 
+// the split-bf16 TN (NPL = 3: 6 products; NPL = 1: the bf16-storage form) and its in-kernel
+// half-pair form (GNN_MATH_HALF_PAIR), one body, two kernel names
+template <bool PROJ, bool MASK, int D, int KT, int NPL = 3, bool ABF = false, bool HBF = false, int PIPE = 0,
+          bool GOUT = true, bool HALFN = false>
+__global__ __launch_bounds__(TX_THREADS) void gemm_tn_x3_kernel(TNArgs a) {
+  gemm_tn_split_body<PROJ, MASK, D, KT, NPL, ABF, HBF, PIPE, GOUT, HALFN, false>(a);
+}
+template <int KT, bool HALFN>
+__global__ __launch_bounds__(TX_THREADS) void gemm_tn_h2s_kernel(TNArgs a) {
+  gemm_tn_split_body<false, false, 1, KT, 3, false, false, 0, false, HALFN, true>(a);
+}
+
 }  // namespace
 
 size_t nt_x3_workspace(int64_t k1, int64_t k2) {  // pre-split B image, 12 KB per 16-deep chunk
@@ -1108,8 +1120,7 @@ bool tn_h2s_ok(const TNArgs& a) {
 
 void launch_tn_h2s(const TNArgs& a, int nblk, hipStream_t st) {
   const int nkt = (a.k1 + a.k2 + 31) / 32;
-  constexpr int D = 1;
-#define GNN_TNH(KTV, HN) gemm_tn_x3_kernel<false, false, D, KTV, 3, false, false, 0, false, HN, true><<<nblk, TX_THREADS, 0, st>>>(a)
+#define GNN_TNH(KTV, HN) gemm_tn_h2s_kernel<KTV, HN><<<nblk, TX_THREADS, 0, st>>>(a)
   if (a.Nr <= 64) {  // the half-N mapping (as launch_tn_x3)
     const int kh = (nkt + 1) / 2;
     if (kh <= 2) GNN_TNH(2, true);
