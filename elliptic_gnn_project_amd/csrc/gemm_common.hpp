@@ -228,7 +228,7 @@ gnn_status nt_h2_prep_from_params(const gnn_gemm_nt_params* p, H2Prep* out, cons
 void launch_nt_h2(const NTArgs& a, uint4* img, hipStream_t st, int phase = NT_PHASE_ALL);
 void launch_prep_h2(const H2Prep& p, hipStream_t st);  // ws_prep_h2_kernel over p (gemm_ws.hip)
 bool tn_h2_ok(const TNArgs& a);
-void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st);
+void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st, bool ks = false);
 bool tn_planes_ok(const TNArgs& a);
 void launch_tn_planes(const TNArgs& a, int nblk, hipStream_t st);
 bool tn_img16_ok(const TNArgs& a);

@@ -20,6 +20,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "gemm_common.hpp"
 
@@ -767,6 +768,15 @@ int tn_blocks(int64_t M) {
   const int64_t per = ceil_div(chunks, 256);
   return (int)ceil_div(chunks, per);
 }
+// the largest M whose half-pair dz-form TN runs split-K block pairs (GNNMP_TN_KSPLIT_MAXM, A/B)
+static int64_t tn_ksplit_max_m() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("GNNMP_TN_KSPLIT_MAXM");
+    return e ? std::atoll(e) : (int64_t)32768;  // the 8-way shard (27k rows): TN + reduce 32.1 -> 30.9 us; 4-way (52k): slower
+  }();
+  return v;
+}
+
 // the in-kernel half-pair TN at Nr <= 64, k1 + k2 <= 128 holds three blocks per CU (its LDS is
 // sized by its k-tiles and 64 G rows, 47 KB): three times the blocks, so three times the chunk loads
 // in flight per CU (its chunk loop is latency-bound: one 16-row chunk in flight per block)
@@ -1037,9 +1047,17 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
     if (a.ap_exp < -100 || a.ap_exp > 100) return fail(GNN_ERR_INVALID_ARG, __fn, "planes_exp outside [-100, 100]");
     if (a.ap_h2) {  // the half-pair image: f16 hi / lo planes, 3 products
       if (p->math != GNN_MATH_F32 && tn_h2_ok(a)) {
-        launch_tn_h2(a, nblk, st);
+        // a shard-sized M (the dz form): split-K block pairs over half as many row blocks (round 6)
+        int nred = nblk;
+        const bool ks = a.dz && a.M <= tn_ksplit_max_m();
+        if (ks) {
+          const int64_t chunks = ceil_div(a.M, 32), per = ceil_div(chunks, 128);
+          nred = (int)ceil_div(chunks, per);
+          a.rows_per_block = per * 32;
+        }
+        launch_tn_h2(a, ks ? 2 * nred : nblk, st, ks);
         GNN_LAUNCH_CHECK();
-        slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nblk, out, n_out, sqo);
+        slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nred, out, n_out, sqo);
         GNN_LAUNCH_CHECK();
         return GNN_OK;
       }

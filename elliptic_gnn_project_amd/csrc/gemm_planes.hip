@@ -459,13 +459,19 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_planes_kernel(TNArgs a) {
 // gradient of GCN / GAT layer 1 and of SAGE-ResBN layer 0's conv and residual projection, dW =
 // Gᵀ·x over x's half-pair image), block scale from max |g| over the block's rows (one pass over
 // them before the chunk loop, behind chunk 0's loads), side sums: db = Σ G only.
-template <int KT, bool GOUT, int LAB = 0, int NW = 4, bool GF = false>
+// KS = 2 (round 6, strong-scaling shards): split-K across block pairs — blocks 2b and 2b + 1 take
+// the same rows and the first (KT + 1) / 2 / the remaining k-tiles, so a shard-sized M runs twice
+// the rows per block on every CU and writes half the slab partials (both blocks form the same G;
+// the side sums come from the first).  The block's A pieces cover only its k-range.
+template <int KT, bool GOUT, int LAB = 0, int NW = 4, bool GF = false, int KS = 1>
 __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(KS == 1 || (KS == 2 && NW == 8), "split-K: the 8-wave form");
   constexpr int T = 64 * NW;
   constexpr int NPA = (2 * PT_ROWS * (PT_MAXLD / 8) + T - 1) / T;  // A pieces per thread per chunk (6 / 3)
   constexpr int RP = PT_ROWS / (T / 128);                           // G rows per thread per chunk (8 / 4)
-  constexpr int KTW = NW == 4 ? KT : (KT + 1) / 2;                  // k-tiles per wave
+  constexpr int KTB = KS == 1 ? KT : (KT + 1) / 2;                   // k-tiles of a block (at most)
+  constexpr int KTW = NW == 4 ? KTB : (KTB + 1) / 2;                // k-tiles per wave
   __shared__ __attribute__((aligned(16))) uint16_t Gt[2][3 * PT_GPL];
   __shared__ __attribute__((aligned(16))) uint16_t At[2][2 * PT_APL];
   __shared__ float dzL[2][256];
@@ -483,14 +489,18 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int ld = a.ap_ld;
-  const int pr = ld >> 3;
-  const int64_t mbeg = (int64_t)blockIdx.x * a.rows_per_block;
+  const int kpart = KS == 1 ? 0 : (int)(blockIdx.x & 1);   // split-K: this block's k-range
+  const int rblk = KS == 1 ? (int)blockIdx.x : (int)(blockIdx.x >> 1);
+  const int kt0 = kpart * KTB;                              // first k-tile
+  const int ktb = KS == 1 ? KT : (kpart ? KT - KTB : KTB);  // k-tiles of this block
+  const int pr = min(4 * ktb, (ld - 32 * kt0) >> 3);        // 16-byte A pieces per row
+  const int64_t mbeg = (int64_t)rblk * a.rows_per_block;
   const int64_t mend = min(a.M, mbeg + a.rows_per_block);
   const int nch = mend > mbeg ? (int)((mend - mbeg + PT_ROWS - 1) / PT_ROWS) : 0;
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   const int wrow = 32 * (wave & 3);                             // this wave's dW rows
-  const int tbase = NW == 4 ? 0 : (wave >> 2) * KTW;            // and k-tiles [tbase, tbase + ntl)
-  const int ntl = NW == 4 ? KT : min(KTW, KT - tbase);
+  const int tbase = NW == 4 ? 0 : (wave >> 2) * KTW;            // and k-tiles [tbase, tbase + ntl) of the block
+  const int ntl = NW == 4 ? KT : max(0, min(KTW, ktb - tbase));
 
   floatx16 acc[KTW];
 #pragma unroll
@@ -508,7 +518,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
     const bool ok = q < 2 * per_plane;
     const int p = q / per_plane, rr = q - p * per_plane;
     const int row = rr / pr, c16 = rr - row * pr;
-    goff[j] = ok ? (uint32_t)(((int64_t)p * a.ap_ps + (int64_t)row * ld + 8 * c16) * 2) : 0u;
+    goff[j] = ok ? (uint32_t)(((int64_t)p * a.ap_ps + (int64_t)row * ld + 32 * kt0 + 8 * c16) * 2) : 0u;
     loff[j] = ok ? (uint32_t)((p * PT_APL + row * PT_AP + 8 * c16) * 2)
                  : (uint32_t)(((tid & 15) * PT_AP + PT_MAXLD + 8 * ((tid >> 4) & 1)) * 2);
   }
@@ -818,12 +828,12 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   }
 
   // ---- this block's partial dW (segment-major: dW1 = [Nr][k1] then dW2 = [Nr][k2])
-  float* slab = a.slab + (int64_t)blockIdx.x * a.slab_stride;
+  float* slab = a.slab + (int64_t)rblk * a.slab_stride;
   const int Kc = a.k1 + a.k2;
 #pragma unroll
   for (int t = 0; t < KTW; ++t) {
     if (NW == 8 && t >= ntl) break;  // wave-uniform
-    const int kp = (tbase + t) * 32 + (lane & 31);
+    const int kp = (kt0 + tbase + t) * 32 + (lane & 31);
     const bool s1 = kp < a.k1;
     const bool s2 = kp >= a.ap_col2 && kp < a.ap_col2 + a.k2;
 #pragma unroll
@@ -852,6 +862,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
     for (int o = 1; o < NGO; ++o) v += red[(o * 128 + col) * ns + f];
     return v;
   };
+  if (kpart != 0) return;  // (split-K: the side sums once per row block)
   if (tid < 128 && tid < a.Nr) {
     float* side = slab + (int64_t)a.Nr * Kc;
     side[tid] = comb(tid, 0);
@@ -1218,10 +1229,16 @@ bool tn_h2_ok(const TNArgs& a) {
 
 // 8 waves (two per SIMD, the k-tiles split between them): lab 102.3 -> 95.2 us on the headline
 // shape (profiles/r19_lab_h2.txt), the staging alone 93.4 — the kernel now runs at its stream
-void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st) {
+// ks: split-K block pairs (gemm_tn_h2_kernel KS = 2; nblk = 2 x the row blocks; the dz form)
+void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st, bool ks) {
   if (!a.dz) {  // the g form
     if (a.ap_ld == 176) gemm_tn_h2_kernel<6, false, 0, 8, true><<<nblk, 512, 0, st>>>(a);
     else gemm_tn_h2_kernel<11, false, 0, 8, true><<<nblk, 512, 0, st>>>(a);
+    return;
+  }
+  if (ks) {
+    if (a.gout) gemm_tn_h2_kernel<11, true, 0, 8, false, 2><<<nblk, 512, 0, st>>>(a);
+    else gemm_tn_h2_kernel<11, false, 0, 8, false, 2><<<nblk, 512, 0, st>>>(a);
     return;
   }
   if (a.gout) gemm_tn_h2_kernel<11, true, 0, 8><<<nblk, 512, 0, st>>>(a);
