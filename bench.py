@@ -275,7 +275,7 @@ def kernel_pattern(tag):
     import re
 
     if tag[0] == "gemm_nt":
-        return re.compile(r"gemm_nt_(planes|ws|img16|h2)_kernel<%d[,>]" % -(-tag[2] // 16))
+        return re.compile(r"gemm_nt_(planes|ws|img16|h2|h2s)_kernel<%d[,>]" % -(-tag[2] // 16))
     if tag[0] == "gemm_tn":
         kt = -(-tag[2] // 32)
         return re.compile(r"gemm_tn_(planes|img16)_kernel<\w+, \w+, %d,|gemm_tn_h2_kernel<%d," % (kt, kt))
