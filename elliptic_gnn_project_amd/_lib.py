@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["GNNMP_LIB"]) if os.environ.get("GNNMP_LIB") else PKG_DIR / "libgnnmp.so"  # (GNNMP_LIB: A/B builds)
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -170,6 +170,7 @@ class GnnGatFwdParams(ctypes.Structure):
         ("alpha", c_ptr),
         ("out", c_ptr), ("ldo", c_i64),
         ("edge_w", c_ptr),
+        ("proj", c_ptr), ("nproj", c_i32), ("z", c_ptr), ("ldz", c_i64),
     ]
 
 
@@ -274,6 +275,11 @@ SIGNATURES = {
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr,
          c_ptr, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr],
     ),
+    "gnn_gat_bwd_act_proj_f32": (
+        ctypes.c_int,
+        [ctypes.POINTER(GnnGraph), c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
+         c_i32, ctypes.c_float, ctypes.c_uint64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_ptr, c_i64,
+         c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_gat_bwd_act_f32": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,

@@ -17,7 +17,7 @@ import torch
 from . import _lib
 from .graph import GraphPlan, get_plan
 
-__all__ = ["mean_aggregate", "masked_mean_aggregate", "masked_gcn_aggregate", "edge_dot", "gcn_aggregate", "gat_attention", "aggregate", "colsum", "KernelTimer"]
+__all__ = ["mean_aggregate", "masked_mean_aggregate", "masked_gcn_aggregate", "edge_dot", "gcn_aggregate", "gat_attention", "gat_attention_proj", "aggregate", "colsum", "KernelTimer"]
 
 
 class KernelTimer:
@@ -456,6 +456,92 @@ class _GATAttention(torch.autograd.Function):
                         S * (12 + 16 * heads + 4 * heads * chans + 4 * fo) + N * (8 + 16 * heads + 4 * F + 4 * fo))
         db = colsum_of(dout) if has_bias and ctx.needs_input_grad[3] else None
         return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db) + (None,) * 9
+
+
+class _GATAttentionProj(torch.autograd.Function):
+    """A hidden GATConv (concat, dropout(ELU(.)) on its store) whose output h feeds only a bias-free
+    projection z = h · w_outᵀ — GATNet's last hidden layer and its output conv's ``lin``
+    (src/models/gnn.py:72-75).  The forward writes z beside the store (gnn_gat_fwd_params.proj,
+    ABI 24: the [N, 2] projection without reading h back); the backward forms dh = dz · w_out as each
+    row slice loads (gnn_gat_bwd_act_proj_f32: dh is never stored) and takes dW_out = dzᵀ · h with
+    the skinny TN.  Returns z; h stays internal (saved for the backward)."""
+
+    @staticmethod
+    @_custom_fwd
+    def forward(ctx, xh, att_src, att_dst, bias, w_out, plan: GraphPlan, heads: int, chans: int, slope: float,
+                act: int, dropout_p: float, seed: int, seed_ctr):
+        xh = _as_f32_rows(xh)
+        N = plan.num_nodes
+        dev = xh.device
+        att_src = att_src.contiguous().float()
+        att_dst = att_dst.contiguous().float()
+        w = w_out.contiguous().float()
+        F = heads * chans
+        a_src = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        a_dst = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        alpha = torch.empty((max(plan.num_slots, 1), heads), dtype=torch.float32, device=dev)
+        out = torch.empty((N, F), dtype=torch.float32, device=dev)
+        z = torch.empty((N, w.size(0)), dtype=torch.float32, device=dev)
+        b = bias.contiguous().float() if bias is not None else None
+        p = _lib.GnnGatFwdParams(
+            heads, chans, 1, float(slope), xh.data_ptr(), _ld(xh), att_src.data_ptr(), att_dst.data_ptr(),
+            _lib.ptr(b), int(act), float(dropout_p), int(seed) & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ctr),
+            a_src.data_ptr(), a_dst.data_ptr(), alpha.data_ptr(), out.data_ptr(), _ld(out), None,
+            w.data_ptr(), w.size(0), z.data_ptr(), _ld(z),
+        )
+        t0 = KernelTimer.begin()
+        _lib.call("gnn_gat_fwd_fused_f32", plan.c_graph, p, _lib.stream_handle(dev))
+        S = plan.num_slots
+        KernelTimer.end(t0, ("gat_fwd", heads, chans, F),
+                        S * (4 + 8 * heads + 4 * F) + N * (4 + 8 * heads + 4 * F + 4 * F + 4 * w.size(0)))
+        ctx.save_for_backward(xh, att_src, att_dst, a_src, a_dst, alpha, seed_ctr, out, w)
+        ctx.meta = (plan, heads, chans, float(slope), bias is not None, int(act), float(dropout_p), int(seed))
+        return z
+
+    @staticmethod
+    @_custom_bwd
+    def backward(ctx, dz):
+        from .fused import gemm_tn
+
+        xh, att_src, att_dst, a_src, a_dst, alpha, seed_ctr, out, w = ctx.saved_tensors
+        plan, heads, chans, slope, has_bias, act, dropout_p, seed = ctx.meta
+        dz = _as_f32_rows(dz)
+        dev = xh.device
+        N = plan.num_nodes
+        F = heads * chans
+        need = ctx.needs_input_grad
+        dW = None
+        if need[4]:  # dW_out = dzᵀ · h (the skinny TN)
+            (dW, _), _, _, _ = gemm_tn(w.size(0), out, g=dz)
+        dxh = torch.empty((N, F), dtype=torch.float32, device=dev)
+        datt_s = torch.empty(F, dtype=torch.float32, device=dev)
+        datt_d = torch.empty(F, dtype=torch.float32, device=dev)
+        dpre = torch.empty_like(out)
+        nb = _lib.c_size(0)
+        _lib.call("gnn_gat_bwd_workspace_size", N, plan.num_slots, heads, chans, nb)
+        ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+        t0 = KernelTimer.begin()
+        _lib.call("gnn_gat_bwd_act_proj_f32", plan.c_graph, heads, chans, slope, xh.data_ptr(), _ld(xh),
+                  a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
+                  act, dropout_p, seed & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ctr), out.data_ptr(), _ld(out),
+                  dz.data_ptr(), _ld(dz), w.data_ptr(), w.size(0), dpre.data_ptr(), _ld(dpre), dxh.data_ptr(),
+                  _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+        S = plan.num_slots
+        KernelTimer.end(t0, ("gat_bwd", heads, chans, F),
+                        S * (12 + 16 * heads + 4 * F + 4 * F) + N * (8 + 16 * heads + 4 * F + 4 * F))
+        db = colsum(dpre) if has_bias and need[3] else None
+        return (dxh, datt_s.view_as(att_src), datt_d.view_as(att_dst), db, dW) + (None,) * 8
+
+
+def gat_attention_proj(xh: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor, bias: torch.Tensor | None,
+                       w_out: torch.Tensor, edge_index: torch.Tensor, heads: int, chans: int,
+                       negative_slope: float = 0.2, act: int = _lib.ACT_NONE, dropout_p: float = 0.0, seed: int = 0,
+                       seed_ctr: torch.Tensor | None = None) -> torch.Tensor:
+    """z = gat_attention(xh, ..., concat=True, act, dropout) · w_outᵀ in one launch (and its backward
+    without dh): GATNet's last hidden layer feeding its output conv's ``lin`` (_GATAttentionProj)."""
+    plan = get_plan(edge_index, xh.size(0), _lib.LOOPS_REPLACE)
+    return _GATAttentionProj.apply(xh, att_src, att_dst, bias, w_out, plan, int(heads), int(chans),
+                                   float(negative_slope), int(act), float(dropout_p), int(seed), seed_ctr)
 
 
 def gat_attention(xh: torch.Tensor, att_src: torch.Tensor, att_dst: torch.Tensor, bias: torch.Tensor | None,

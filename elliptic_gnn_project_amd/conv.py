@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .aggregation import (aggregate, colsum, colsum_of, gat_attention, gcn_aggregate, masked_gat_attention, masked_gcn_aggregate,
+from .aggregation import (aggregate, colsum, colsum_of, gat_attention, gat_attention_proj, gcn_aggregate, masked_gat_attention, masked_gcn_aggregate,
                           masked_mean_aggregate, mean_aggregate)
 from .graph import GraphPlan, get_plan
 from .linear import Linear, linear, linear2, linear_stacked
@@ -314,6 +314,19 @@ class GATConv(nn.Module):
         act, p, seed, ctr = _post if _post is not None else (_lib.ACT_NONE, 0.0, 0, None)
         return gat_attention(xh, self.att_src, self.att_dst, self.bias, edge_index, self.heads,
                              self.out_channels, self.concat, self.negative_slope, act, p, seed, ctr)
+
+    def _forward_proj(self, x: torch.Tensor, edge_index: torch.Tensor, w_out: torch.Tensor, _post) -> torch.Tensor:
+        """forward(x, edge_index, _post=_post) · w_outᵀ with the projection on the attention kernel's
+        store (aggregation.gat_attention_proj) — internal to GATNet.forward: its last hidden layer and
+        the output conv's ``lin``."""
+        act, p, seed, ctr = _post
+        return gat_attention_proj(self.lin(x), self.att_src, self.att_dst, self.bias, w_out, edge_index,
+                                  self.heads, self.out_channels, self.negative_slope, act, p, seed, ctr)
+
+    def _forward_from_xh(self, xh: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
+        """forward() with ``lin(x)`` already given (GATNet.forward's fused projection)."""
+        return gat_attention(xh, self.att_src, self.att_dst, self.bias, edge_index, self.heads,
+                             self.out_channels, self.concat, self.negative_slope)
 
     def __repr__(self) -> str:
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels}, heads={self.heads})"

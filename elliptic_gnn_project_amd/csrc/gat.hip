@@ -93,6 +93,9 @@ struct GatArgs {
   float* dpre; int64_t ld_dpre;
   int32_t pe_act, pe_drop; uint32_t pe_thresh; float pe_scale, pe_keep;
   uint64_t pe_seed; const uint64_t* pe_seed_ptr;
+  // (ABI 24) dy given as dz · proj (dz [N, pnproj], proj [pnproj, F]): the output conv's lin
+  // backward formed as each row slice loads — GATNet's dh is never materialised
+  const float* pdz; int64_t ld_pdz; const float* pproj; int32_t pnproj;
 };
 
 // the row of group position pos (pos < N)
@@ -367,7 +370,11 @@ struct GatEpi {
   const uint64_t* seed_ptr;
   float* as_out;        // XS: a_src / a_dst written [N, H]
   float* ad_out;
+  // (ABI 24, concat layers) z = out · projᵀ beside the store: GATNet's output conv's lin on the
+  // hidden layer's stored rows (proj [nproj, F], nproj <= 4)
+  const float* proj; int32_t nproj; float* z; int64_t ldz;
 };
+
 
 __device__ __forceinline__ uint64_t gat_seed(const GatEpi& e) {
   return e.seed_ptr ? (*e.seed_ptr) * 0x9E3779B97F4A7C15ull + e.seed : e.seed;
@@ -399,6 +406,53 @@ __device__ __forceinline__ float vdot(const VecF<VEC>& x, const VecF<VEC>& w) {
 #pragma unroll
   for (int i = 1; i < VEC; ++i) s = fmaf(x.v[i], w.v[i], s);
   return s;
+}
+
+// z[r, q] = Σ_f o[f] · proj[q, f] over the row's stored slice: each phase-0 lane its VEC features
+// (pw: the lane's slice of proj's rows), summed over the FLp lanes of the row — the phase-0 lanes
+// of a group are its lanes 0 .. FLp - 1.  FLp == 16 (GATNet's 64-wide hidden rows at VEC 4): the
+// row is one DPP row, summed by two quad_perm steps and row_shr 4 / 8 into its lane 15 (no LDS
+// crossbar round trips); otherwise an xor butterfly, lane 0 holding the sum.  Every lane of the wave
+// calls it (lanes without a stored slice contribute 0); `own`: the row is this group's to store.
+template <int VEC, int NP>
+__device__ __forceinline__ void gat_store_proj(const GatEpi& e, const VecF<VEC>& o, bool on, const VecF<VEC> (&pw)[NP],
+                                               int FLp, int64_t r, bool own, int fl) {
+  float pz[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) pz[q] = on ? vdot<VEC>(o, pw[q]) : 0.f;
+  int wl = 0;
+  if (FLp == 16) {
+    wl = 15;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      float v = pz[q];
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, true));  // row_shr:4
+      v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xF, 0xF, true));  // row_shr:8
+      pz[q] = v;
+    }
+  } else {
+    for (int off = 1; off < FLp; off <<= 1) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) pz[q] += __shfl_xor(pz[q], off);
+    }
+  }
+  if (own && fl == wl) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q)
+      if (q < e.nproj) e.z[r * e.ldz + q] = pz[q];
+  }
+}
+// the lane's slice of proj's first NP rows (zeros past nproj or for lanes without a feature slot)
+template <int VEC, int NP>
+__device__ __forceinline__ void gat_load_proj(const GatEpi& e, bool ok, int F, int f0, VecF<VEC> (&pw)[NP]) {
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) pw[q].v[i] = 0.f;
+    if (ok && q < e.nproj) pw[q] = ldv<VEC>(e.proj + (int64_t)q * F + f0);
+  }
 }
 
 // Online softmax state of one slot-view lane: running max m, sum s and accumulator (both
@@ -578,14 +632,22 @@ __device__ void gat_fwd_long_row(const GatArgs& a, const GatGeom& g, const GatEp
   }
   const float rinv = frcp(tot.s + 1e-16f);
   if (a.concat) {
+    VecF<VEC> o;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) o.v[i] = 0.0f;
     if (sl.ok && sl.ep == 0) {
-      VecF<VEC> o;
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         const int f = sl.f0 + i;
         o.v[i] = gat_store_val(ep_, seed, tot.acc.v[i] * rinv + (a.bias ? a.bias[f] : 0.0f), r, f, Fo);
       }
       stv<VEC>(a.out + r * a.ldo + sl.f0, o);
+    }
+    // (the row's phase-0 lanes are threads 0 .. FLp - 1 of wave 0)
+    if (ep_.nproj > 0) {
+      VecF<VEC> pw[2];
+      gat_load_proj<VEC, 2>(ep_, sl.ok && sl.ep == 0, F, sl.f0, pw);
+      gat_store_proj<VEC, 2>(ep_, o, sl.ok && sl.ep == 0, pw, g.FLp, r, wave == 0 && sl.ep == 0, sl.fl);
     }
   } else {
     if (sl.ok && sl.ep == 0) {
@@ -611,8 +673,13 @@ __device__ void gat_fwd_long_row(const GatArgs& a, const GatGeom& g, const GatEp
 template <int VEC, bool XS>
 __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g, GatLong lg, GatEpi ep_) {
   __shared__ float sh[kLongLds];
+  __shared__ float psh[2 * 256];  // the store's projection rows (ep_.nproj > 0: proj [nproj <= 2][F <= 256])
   const int lane = threadIdx.x & 63;
   const int H = a.H, C = a.C, F = H * C;
+  if (ep_.nproj > 0) {  // (block-uniform, before the long-row split)
+    for (int i = threadIdx.x; i < 2 * F; i += 256) psh[(i / F) * 256 + i % F] = i / F < ep_.nproj ? ep_.proj[i] : 0.f;
+    __syncthreads();
+  }
   const int Fo = a.concat ? F : C;
   const uint64_t seed = ep_.dropout ? gat_seed(ep_) : 0;
   // attention vectors of this lane's feature slot (XS)
@@ -676,7 +743,23 @@ __global__ __launch_bounds__(256) void gat_fwd_group_kernel(GatArgs a, GatGeom g
         for (int i = 0; i < VEC; ++i) o.v[i] += __shfl_xor(o.v[i], off);
       }
     }
-    if (own && sl.ok && sl.ep == 0) {
+    const bool stor = own && sl.ok && sl.ep == 0;
+    if (a.concat && ep_.nproj > 0) {  // (wave-uniform) the stored rows' projection z = out · projᵀ
+      if (stor) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const int f = sl.f0 + i;
+          o.v[i] = gat_store_val(ep_, seed, o.v[i] + (a.bias ? a.bias[f] : 0.0f), r, f, Fo);
+        }
+        stv<VEC>(a.out + r * a.ldo + sl.f0, o);
+      }
+      VecF<VEC> pw[2];  // the lane's slice of the projection rows, from LDS (no registers held across rows)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) pw[q].v[i] = sl.ok ? psh[q * 256 + sl.f0 + i] : 0.f;
+      gat_store_proj<VEC, 2>(ep_, o, stor, pw, g.FLp, r, stor, sl.fl);
+    } else if (stor) {
       if (a.concat) {
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
@@ -774,7 +857,18 @@ __device__ __forceinline__ VecF<VEC> load_dO(const GatArgs& a, const SlotLane& s
   VecF<VEC> d;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) d.v[i] = 0.0f;
-  if (ok && sl.ok) d = ldv<VEC>(a.dout + r * a.ld_dout + (a.concat ? sl.f0 : sl.c0));
+  if (a.pdz) {  // dy = dz[r, :] · proj
+    if (ok && sl.ok) {
+      for (int q = 0; q < a.pnproj; ++q) {
+        const float zq = a.pdz[r * a.ld_pdz + q];
+        const VecF<VEC> w = ldv<VEC>(a.pproj + (int64_t)q * (a.H * a.C) + sl.f0);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) d.v[i] = fmaf(zq, w.v[i], d.v[i]);
+      }
+    }
+  } else if (ok && sl.ok) {
+    d = ldv<VEC>(a.dout + r * a.ld_dout + (a.concat ? sl.f0 : sl.c0));
+  }
   if (a.y && ok && sl.ok) {  // the store's backward (concat layers), as gat_act_bwd_kernel
     const VecF<VEC> yv = ldv<VEC>(a.y + r * a.ld_y + sl.f0);
     const uint64_t seed = a.pe_seed_ptr ? (*a.pe_seed_ptr) * 0x9E3779B97F4A7C15ull + a.pe_seed : a.pe_seed;
@@ -977,6 +1071,33 @@ __global__ __launch_bounds__(256) void gat_act_fwd_kernel(int64_t N, int32_t Fo,
     const int c = (int)(t - r * Fo);
     float* q = out + r * ldo + c;
     *q = gat_store_val(e, seed, *q, r, c, Fo);
+  }
+}
+
+// z = out · projᵀ row by row (the generic geometry's projection; the group kernels do it in their store)
+__global__ __launch_bounds__(256) void gat_proj_rows_kernel(int64_t N, int32_t F, const float* __restrict__ out,
+                                                            int64_t ldo, const float* __restrict__ proj, int32_t nproj,
+                                                            float* __restrict__ z, int64_t ldz) {
+  for (int64_t r = blockIdx.x * 256ll + threadIdx.x; r < N; r += (int64_t)gridDim.x * 256) {
+    for (int q = 0; q < nproj; ++q) {
+      float s = 0.f;
+      for (int f = 0; f < F; ++f) s = fmaf(out[r * ldo + f], proj[(int64_t)q * F + f], s);
+      z[r * ldz + q] = s;
+    }
+  }
+}
+
+// dy = dz · proj row by row (the generic geometry's dz-form backward)
+__global__ __launch_bounds__(256) void gat_dz_proj_kernel(int64_t N, int32_t F, const float* __restrict__ dz,
+                                                          int64_t lddz, const float* __restrict__ proj, int32_t nproj,
+                                                          float* __restrict__ dy, int64_t lddy) {
+  const int64_t total = N * F;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t r = t / F;
+    const int f = (int)(t - r * F);
+    float s = 0.f;
+    for (int q = 0; q < nproj; ++q) s = fmaf(dz[r * lddz + q], proj[(int64_t)q * F + f], s);
+    dy[r * lddy + f] = s;
   }
 }
 
@@ -1423,10 +1544,14 @@ extern "C" gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fw
   GatEpi ep = make_epi(p->act, p->dropout_p, p->seed, p->seed_ptr);
   ep.as_out = p->a_src;
   ep.ad_out = p->a_dst;
+  if (p->nproj < 0 || p->nproj > 4 || (p->nproj > 0 && (!concat || !p->proj || !p->z || p->ldz < p->nproj ||
+                                                          (reinterpret_cast<uintptr_t>(p->proj) & 15))))
+    return fail(GNN_ERR_INVALID_ARG, __func__, "proj: concat, nproj <= 4, proj (16-byte aligned) and z");
+  ep.proj = p->proj; ep.nproj = p->nproj; ep.z = p->z; ep.ldz = p->ldz;
   hipStream_t st = (hipStream_t)stream;
   GatGeom gg;
   int vec = 1;
-  if (!p->edge_w && idx24_ok(g, p->ld_xh, H) &&
+  if (!p->edge_w && idx24_ok(g, p->ld_xh, H) && (p->nproj == 0 || ((H * C) % 4 == 0 && p->nproj <= 2 && H * C <= 256)) &&
       gat_geom(H, C, concat, {{p->xh, p->ld_xh}, {p->out, p->ldo}, {p->att_src, 0}, {p->att_dst, 0}}, &gg, &vec)) {
     const GatLong lg = long_rows(g);
     const unsigned nb = group_blocks(a.N, gg.G, (int64_t)1 << 20) + (unsigned)lg.n;
@@ -1445,6 +1570,10 @@ extern "C" gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fw
   if (ep.act != GNN_ACT_NONE || ep.dropout) {
     const int32_t Fo = concat ? H * C : C;
     gat_act_fwd_kernel<<<elem_blocks(a.N * Fo), 256, 0, st>>>(a.N, Fo, p->out, p->ldo, ep);
+    GNN_LAUNCH_CHECK();
+  }
+  if (ep.nproj > 0) {
+    gat_proj_rows_kernel<<<elem_blocks(a.N), 256, 0, st>>>(a.N, H * C, p->out, p->ldo, ep.proj, ep.nproj, ep.z, ep.ldz);
     GNN_LAUNCH_CHECK();
   }
   return GNN_OK;
@@ -1486,7 +1615,8 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
   if (!g) return fail(GNN_ERR_INVALID_ARG, fn, "null graph");
   if (!pow2_heads(H)) return fail(GNN_ERR_UNSUPPORTED, fn, "heads must be a power of two <= 64");
   const int64_t F = (int64_t)H * C;
-  if (C < 1 || ld_xh < F || ld_dxh < F || ld_dout < (concat ? F : C))
+  const bool dzf = post && post->pdz;  // dy given as dz · proj (dout = dz, ld_dout its pitch)
+  if (C < 1 || ld_xh < F || ld_dxh < F || (dzf ? ld_dout < post->pnproj : ld_dout < (concat ? F : C)))
     return fail(GNN_ERR_INVALID_ARG, fn, "bad sizes");
   hipStream_t st = (hipStream_t)stream;
   if (g->num_nodes == 0) {
@@ -1513,8 +1643,8 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
   int vec = 1;
   const bool fuse = post != nullptr;  // the store's backward rides in the rows pass
   const int64_t F_ = (int64_t)H * C;
-  if (!edge_w && idx24_ok(g, ld_xh, H) &&
-      gat_geom(H, C, concat, {{xh, ld_xh}, {dout, ld_dout}, {dxh, ld_dxh}, {att_src, 0}, {att_dst, 0},
+  if (!edge_w && idx24_ok(g, ld_xh, H) && (!dzf || F % 4 == 0) &&
+      gat_geom(H, C, concat, {{xh, ld_xh}, {dzf ? nullptr : dout, dzf ? 0 : ld_dout}, {dxh, ld_dxh}, {att_src, 0}, {att_dst, 0},
                               {fuse ? post->y : nullptr, fuse ? post->ld_y : 0},
                               {fuse ? post->dpre : nullptr, fuse ? post->ld_dpre : 0}}, &gg, &vec)) {
     const GatLong lg = long_rows(g);
@@ -1526,6 +1656,7 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
       ar.pe_act = post->pe_act; ar.pe_drop = post->pe_drop; ar.pe_thresh = post->pe_thresh;
       ar.pe_scale = post->pe_scale; ar.pe_keep = post->pe_keep; ar.pe_seed = post->pe_seed;
       ar.pe_seed_ptr = post->pe_seed_ptr;
+      ar.pdz = post->pdz; ar.ld_pdz = post->ld_pdz; ar.pproj = post->pproj; ar.pnproj = post->pnproj;
       a.dout = post->dpre; a.ld_dout = post->ld_dpre;
     }
     switch (vec) {
@@ -1544,6 +1675,13 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
     gat_att_reduce_kernel<<<(unsigned)(2 * F), 256, 0, st>>>((int)F, (int)nbc, part, d_att_src, d_att_dst);
     GNN_LAUNCH_CHECK();
     return GNN_OK;
+  }
+  if (fuse && dzf) {  // generic geometry, dz form: dy = dz · proj into dpre first (the act pass below is in place)
+    gat_dz_proj_kernel<<<elem_blocks(a.N * F_), 256, 0, st>>>(a.N, (int32_t)F_, post->pdz, post->ld_pdz, post->pproj,
+                                                              post->pnproj, post->dpre, post->ld_dpre);
+    GNN_LAUNCH_CHECK();
+    dout = post->dpre;
+    ld_dout = post->ld_dpre;
   }
   if (fuse) {  // generic geometry: the store's backward as its own pass first
     GatEpi ep{};
@@ -1601,6 +1739,32 @@ extern "C" gnn_status gnn_gat_bwd_act_f32(const gnn_graph* g, int32_t H, int32_t
   post.pe_act = ep.act; post.pe_drop = ep.dropout; post.pe_thresh = ep.keep_thresh; post.pe_scale = ep.drop_scale;
   post.pe_keep = (float)(1.0 - (double)dropout_p); post.pe_seed = seed; post.pe_seed_ptr = seed_ptr;
   return gat_bwd_impl(__func__, g, H, C, 1, slope, xh, ld_xh, a_src, a_dst, att_src, att_dst, alpha, dy, ld_dy, dxh,
+                      ld_dxh, d_att_src, d_att_dst, nullptr, nullptr, workspace, workspace_bytes, stream, &post);
+}
+
+extern "C" gnn_status gnn_gat_bwd_act_proj_f32(const gnn_graph* g, int32_t H, int32_t C, float slope, const float* xh,
+                                               int64_t ld_xh, const float* a_src, const float* a_dst,
+                                               const float* att_src, const float* att_dst, const float* alpha, gnn_act act,
+                                               float dropout_p, uint64_t seed, const uint64_t* seed_ptr, const float* y,
+                                               int64_t ld_y, const float* dz, int64_t ld_dz, const float* proj,
+                                               int32_t nproj, float* dpre, int64_t ld_dpre, float* dxh, int64_t ld_dxh,
+                                               float* d_att_src, float* d_att_dst, void* workspace,
+                                               size_t workspace_bytes, gnn_stream_t stream) {
+  const int64_t F = (int64_t)H * C;
+  if (act != GNN_ACT_NONE && act != GNN_ACT_ELU) return fail(GNN_ERR_INVALID_ARG, __func__, "unknown act");
+  if (!(dropout_p >= 0.0f && dropout_p < 1.0f)) return fail(GNN_ERR_INVALID_ARG, __func__, "dropout_p not in [0, 1)");
+  if (!g || (g->num_nodes > 0 && (!y || !dpre || !dz || !proj)) || ld_y < F || ld_dpre < F || nproj < 1 || nproj > 4 ||
+      ld_dz < nproj || (reinterpret_cast<uintptr_t>(proj) & 15))
+    return fail(GNN_ERR_INVALID_ARG, __func__, "bad y / dpre / dz / proj");
+  if (dropout_p > 0.0f && g->num_nodes * F >= ((int64_t)1 << 32))
+    return fail(GNN_ERR_UNSUPPORTED, __func__, "dropout element index (rows x width) must be < 2^32");
+  GatArgs post{};
+  const GatEpi ep = make_epi(act, dropout_p, seed, seed_ptr);
+  post.y = y; post.ld_y = ld_y; post.dpre = dpre; post.ld_dpre = ld_dpre;
+  post.pe_act = ep.act; post.pe_drop = ep.dropout; post.pe_thresh = ep.keep_thresh; post.pe_scale = ep.drop_scale;
+  post.pe_keep = (float)(1.0 - (double)dropout_p); post.pe_seed = seed; post.pe_seed_ptr = seed_ptr;
+  post.pdz = dz; post.ld_pdz = ld_dz; post.pproj = proj; post.pnproj = nproj;
+  return gat_bwd_impl(__func__, g, H, C, 1, slope, xh, ld_xh, a_src, a_dst, att_src, att_dst, alpha, dz, ld_dz, dxh,
                       ld_dxh, d_att_src, d_att_dst, nullptr, nullptr, workspace, workspace_bytes, stream, &post);
 }
 

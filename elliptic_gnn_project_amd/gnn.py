@@ -126,12 +126,20 @@ class GATNet(_StackedConvNet):
         p = float(self.dropout) if self.training else 0.0
         seeds, ctr = _fused.dropout_seeds(len(self.convs), p, x)
         h = x
+        # the last hidden layer writes the output conv's lin(h) beside its store, and its backward
+        # forms dh from d lin(h) in the kernel (ABI 24): h is never read back or its gradient stored
+        proj = (_GAT_PROJ and hidden and last.heads == 1 and not last.concat and last.out_channels <= 4
+                and (hidden[-1].heads * hidden[-1].out_channels) % 4 == 0)
         for i, conv in enumerate(hidden):
-            h = conv(h, edge_index, _post=(_lib.ACT_ELU, p, seeds[i], ctr))
+            post = (_lib.ACT_ELU, p, seeds[i], ctr)
+            if proj and i == len(hidden) - 1:
+                return last._forward_from_xh(conv._forward_proj(h, edge_index, last.lin.weight, post), edge_index)
+            h = conv(h, edge_index, _post=post)
         return last(h, edge_index)
 
 
 _RES_FOLD = os.environ.get("GNNMP_RES_FOLD", "1") != "0"  # A/B: 0 = autograd adds the residual's gradient
+_GAT_PROJ = os.environ.get("GNNMP_GAT_PROJ", "1") != "0"  # A/B: 0 = the output conv's lin as its own GEMMs
 
 
 class SAGEResBNNet(nn.Module):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 23
+#define GNNMP_ABI_VERSION 24
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -316,6 +316,10 @@ typedef struct {
   const float* edge_w;                    /* optional [S]: explain mode (PyG propagate with
                                              `_explain`): every message alpha * xh[j] of CSR slot s is
                                              multiplied by edge_w[s] after the softmax */
+  const float* proj; int32_t nproj;       /* optional (ABI 24, concat layers): z = out · projᵀ written */
+  float* z; int64_t ldz;                  /* beside the store, proj [nproj, H·C] (16-byte aligned,
+                                             nproj <= 4) — GATNet's output conv's lin (gnn.py:75) on the
+                                             hidden layer's stored rows, so its input is never read back */
 } gnn_gat_fwd_params;
 gnn_status gnn_gat_fwd_fused_f32(const gnn_graph* g, const gnn_gat_fwd_params* p, gnn_stream_t stream);
 /* GATNet's output conv (src/models/gnn.py:67,75: heads 1, C <= 2, concat False, no act / dropout /
@@ -360,6 +364,17 @@ gnn_status gnn_gat_bwd_act_f32(const gnn_graph* g, int32_t H, int32_t C, float s
                                const float* dy, int64_t ld_dy, float* dpre, int64_t ld_dpre, float* dxh,
                                int64_t ld_dxh, float* d_att_src, float* d_att_dst, void* workspace,
                                size_t workspace_bytes, gnn_stream_t stream);
+
+/* (ABI 24) gnn_gat_bwd_act_f32 with dy given as dz · proj (dz [N, nproj], ld_dz; proj [nproj, H·C],
+ * 16-byte aligned, nproj <= 4): the backward of a hidden layer whose output fed a projection
+ * (gnn_gat_fwd_params.proj) — dy is formed as each row slice loads, never stored. */
+gnn_status gnn_gat_bwd_act_proj_f32(const gnn_graph* g, int32_t H, int32_t C, float slope, const float* xh,
+                                    int64_t ld_xh, const float* a_src, const float* a_dst, const float* att_src,
+                                    const float* att_dst, const float* alpha, gnn_act act, float dropout_p,
+                                    uint64_t seed, const uint64_t* seed_ptr, const float* y, int64_t ld_y,
+                                    const float* dz, int64_t ld_dz, const float* proj, int32_t nproj, float* dpre,
+                                    int64_t ld_dpre, float* dxh, int64_t ld_dxh, float* d_att_src, float* d_att_dst,
+                                    void* workspace, size_t workspace_bytes, gnn_stream_t stream);
 
 /* Explain-mode backward (messages scaled by edge_w[s], see gnn_gat_fwd_params.edge_w): as
  * gnn_gat_bwd_f32, plus d_edge_w[s] = sum_h alpha[s,h] * <dout_i(h), xh[j,h,:]> for every CSR slot. */

@@ -155,6 +155,10 @@ STRUCTS = {
                                                "planes_col2", "planes_format", "keep_mask",
                                                "b_ready", "planes_exp", "colsum_part", "colsum_cap", "row_exp"]),
     "gnn_adam_tensor": ("GnnAdamTensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel"]),
+    "gnn_gat_fwd_params": ("GnnGatFwdParams", ["heads", "chans", "concat", "slope", "xh", "ld_xh", "att_src",
+                                               "att_dst", "bias", "act", "dropout_p", "seed", "seed_ptr", "a_src",
+                                               "a_dst", "alpha", "out", "ldo", "edge_w", "proj", "nproj", "z",
+                                               "ldz"]),
     "gnn_adam_group": ("GnnAdamGroup", ["num_tensors", "lr", "beta1", "beta2", "eps", "weight_decay", "max_norm",
                                         "tensors", "skip_nonfinite", "bump_counter", "loss_partial", "loss_nblk",
                                         "loss_scale", "loss_out", "grad_sq_partial", "grad_sq_nblk"]),
