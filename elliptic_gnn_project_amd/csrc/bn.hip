@@ -123,6 +123,52 @@ __global__ __launch_bounds__(kBnThreads) void bn_merge_kernel(const T* __restric
   }
 }
 
+// Single device: the merge and the finalize in one launch — block c sums column c's Σz and Σz²
+// partials (bn_merge_kernel's order and LDS tree, bit for bit) and finalizes column c itself (a
+// column's mean / invstd / running stats need only its own two sums), so no block waits on another
+// and the separate finalize launch is gone.  Block 0 bumps num_batches_tracked.  Taken for a fixed
+// momentum only: the cumulative average (momentum None) reads num_batches_tracked in every column,
+// which block 0's bump could not be ordered against; SyncBN keeps the separate finalize too (its
+// stats are all-reduced in between).
+__global__ __launch_bounds__(kBnThreads) void bn_merge_finalize_kernel(const double* __restrict__ part, int nblk, int C,
+                                                                       int64_t N, double* __restrict__ stats, float eps,
+                                                                       float momentum, float* mean, float* invstd,
+                                                                       float* rmean, float* rvar, int64_t* nbt) {
+  __shared__ double red[2][kBnThreads];
+  const int c = blockIdx.x;
+  double s = 0, q = 0;
+  for (int b = threadIdx.x; b < nblk; b += kBnThreads) {
+    s += part[(int64_t)b * 2 * C + c];
+    q += part[(int64_t)b * 2 * C + C + c];
+  }
+  red[0][threadIdx.x] = s;
+  red[1][threadIdx.x] = q;
+  __syncthreads();
+  for (int h = kBnThreads / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + h];
+      red[1][threadIdx.x] += red[1][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    stats[c] = red[0][0];
+    stats[C + c] = red[1][0];
+    stats[2 * C] = (double)N;  // (every block writes the same value)
+    double loc[3];              // this column's sums and n, as bn_finalize_one reads them from stats
+    loc[0] = red[0][0];
+    loc[1] = red[1][0];
+    loc[2] = (double)N;
+    float m, is;
+    float* rm = rmean ? rmean + c : nullptr;
+    float* rv = rvar ? rvar + c : nullptr;
+    bn_finalize_one(0, loc, 1, eps, momentum, &m, &is, rm, rv, nbt);
+    mean[c] = m;
+    invstd[c] = is;
+    if (c == 0 && nbt) *nbt += 1;
+  }
+}
+
 __global__ __launch_bounds__(kBnThreads) void bn_finalize_kernel(const double* __restrict__ stats, int C, float eps,
                                                                 float momentum, float* mean, float* invstd, float* rmean,
                                                                 float* rvar, int64_t* nbt) {
@@ -310,6 +356,12 @@ extern "C" gnn_status gnn_bn_stats_f32(const float* z, int64_t ldz, int64_t N, i
   double* part = static_cast<double*>(workspace);
   bn_stats_partial_kernel<<<nblk, kBnThreads, 0, st>>>(a, R, part);
   GNN_LAUNCH_CHECK();
+  if (finalize && momentum >= 0.f) {
+    bn_merge_finalize_kernel<<<(unsigned)C, kBnThreads, 0, st>>>(part, nblk, (int)C, N, stats, eps, momentum, mean,
+                                                                 invstd, running_mean, running_var, num_batches_tracked);
+    GNN_LAUNCH_CHECK();
+    return GNN_OK;
+  }
   bn_merge_kernel<double, double><<<(unsigned)(2 * C), kBnThreads, 0, st>>>(part, nblk, (int)C, N, stats);
   GNN_LAUNCH_CHECK();
   if (finalize) {

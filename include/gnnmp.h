@@ -561,7 +561,8 @@ gnn_status gnn_colsum_f32(int64_t rows, int64_t F, const float* x, int64_t ldx, 
 gnn_status gnn_bn_workspace_size(int64_t C, size_t* bytes);
 /* Batch statistics of z [N, C]: stats (device float64 [2C + 1]) = [Σz | Σz² | N] — summable
  * across ranks (SyncBN: all-reduce them, then gnn_bn_finalize_f32).  finalize != 0 also does
- * gnn_bn_finalize_f32 in the same launch sequence (single device). */
+ * gnn_bn_finalize_f32 in the same launch sequence (single device; with momentum >= 0 the merge
+ * and the finalize are one launch). */
 gnn_status gnn_bn_stats_f32(const float* z, int64_t ldz, int64_t N, int64_t C, double* stats, int32_t finalize,
                             float eps, float momentum, float* mean, float* invstd, float* running_mean,
                             float* running_var, int64_t* num_batches_tracked, void* workspace,
