@@ -54,7 +54,13 @@ __device__ __forceinline__ void vstore(float* p, const float (&v)[VEC]) {
 // bf16 rows (bf16-storage path): VEC bf16 per lane-chunk widened to f32 / rounded back (RNE).
 template <int VEC>
 __device__ __forceinline__ void vload_bf(const uint16_t* p, float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
+  if constexpr (VEC == 8) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+    v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+    v[4] = __uint_as_float(t.z << 16); v[5] = __uint_as_float(t.z & 0xffff0000u);
+    v[6] = __uint_as_float(t.w << 16); v[7] = __uint_as_float(t.w & 0xffff0000u);
+  } else if constexpr (VEC == 4) {
     const uint2 t = *reinterpret_cast<const uint2*>(p);
     v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
     v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
@@ -70,7 +76,12 @@ __device__ __forceinline__ uint16_t to_bf16(float f) { return __builtin_bit_cast
 
 template <int VEC>
 __device__ __forceinline__ void vstore_bf(uint16_t* p, const float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
+  if constexpr (VEC == 8) {
+    *reinterpret_cast<uint4*>(p) = make_uint4((uint32_t)to_bf16(v[0]) | ((uint32_t)to_bf16(v[1]) << 16),
+                                              (uint32_t)to_bf16(v[2]) | ((uint32_t)to_bf16(v[3]) << 16),
+                                              (uint32_t)to_bf16(v[4]) | ((uint32_t)to_bf16(v[5]) << 16),
+                                              (uint32_t)to_bf16(v[6]) | ((uint32_t)to_bf16(v[7]) << 16));
+  } else if constexpr (VEC == 4) {
     *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)to_bf16(v[0]) | ((uint32_t)to_bf16(v[1]) << 16),
                                               (uint32_t)to_bf16(v[2]) | ((uint32_t)to_bf16(v[3]) << 16));
   } else if constexpr (VEC == 2) {
@@ -737,6 +748,125 @@ __global__ __launch_bounds__(256) void agg_wave_kernel(AggArgs a, int32_t rpg) {
     for (int u = 0; u < U; ++u) {
       n[u] = nn[u];
       if constexpr (SW) dn[u] = a.nodew[min((uint32_t)n[u], nmax)];
+    }
+  }
+  for (; j < nrow; ++j) flush(j);
+}
+
+// bf16 rows of at most 64 / G lane chunks (configs[4]'s F = 128 mean and meanᵀ: 32 chunks of 4 or
+// 16 of 8 bf16): the wave's G lane groups gather G consecutive slots per load instruction — group g
+// takes slot k + g — so every lane loads (the one-slot agg_wave_kernel leaves 64 − F/VEC lanes idle,
+// 32 of 64 at F = 128).  A group adds its own slots in plan order into its own accumulators; a row's
+// flush adds the groups' partials by a fixed xor tree over the groups (deterministic, but no longer
+// PyG's single sequential chain: the bf16 path stores the sum rounded to bf16 and its tests bound
+// it in bf16 ulps).  Neighbour ids and weights stay wave-uniform (scalar); a group selects its
+// slot's.  Modes SUM / MEAN / MEAN_BWD (their slot term needs no per-row weight).
+template <int MODE, int VEC, int G, int U = 8>
+__global__ __launch_bounds__(256) void agg_wave_group_bf16_kernel(AggArgs a, int32_t rpg) {
+  static_assert(MODE == GNN_AGG_SUM || MODE == GNN_AGG_MEAN || MODE == GNN_AGG_MEAN_BWD, "no per-row slot weight");
+  static_assert(G == 2 || G == 4, "2 or 4 lane groups");
+  constexpr int LG = 64 / G;  // lanes per group
+  constexpr int S = G * U;    // slots per walk step
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / LG;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t r0 = wave * rpg;
+  if (r0 >= a.nrows) return;
+  const int nrow = (int)min((int64_t)rpg, a.nrows - r0);
+  const int nchunk = a.F / VEC;
+  const int32_t myptr = a.ptr[r0 + min(lane, nrow)];
+  float mydeg = 1.0f;
+  if constexpr (MODE == GNN_AGG_MEAN) mydeg = a.nodew[r0 + min(lane, nrow - 1)];
+  const int c = lane % LG;
+  const int coff = (c < nchunk ? c : 0) * VEC;
+  const uint16_t* xb = reinterpret_cast<const uint16_t*>(a.x) + coff;
+  float acc[VEC];
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) acc[q] = 0.0f;
+  const uint64_t dseed = a.dropout ? agg_seed(a) : 0;
+  auto flush = [&](int j) {
+    float t[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      t[q] = acc[q] + __shfl_xor(acc[q], LG);                // groups (0 + 1), (2 + 3)
+      if constexpr (G == 4) t[q] = t[q] + __shfl_xor(t[q], 2 * LG);  // then (0 + 1) + (2 + 3)
+      acc[q] = 0.0f;
+    }
+    if (grp == 0 && c < nchunk) {
+      const int64_t r = r0 + j;
+      const int f0 = c * VEC;
+      if constexpr (MODE == GNN_AGG_MEAN) {
+        const float d = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mydeg), j)), 1.0f);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) t[q] = t[q] / d;
+      }
+      if (a.add) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) t[q] += a.add[r * a.ld_add + f0 + q];
+      }
+      if (a.bias) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) t[q] += a.bias[f0 + q];
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) t[q] = fmaxf(t[q], 0.0f);
+      }
+      if (a.dropout) agg_dropout<VEC>(a, dseed, r, f0, t);
+      vstore_bf<VEC>(reinterpret_cast<uint16_t*>(a.y) + r * a.ldy + f0, t);
+    }
+  };
+
+  const int32_t sbeg = __builtin_amdgcn_readlane(myptr, 0);
+  const int32_t send = __builtin_amdgcn_readlane(myptr, nrow);
+  int j = 0;
+  int32_t cend = __builtin_amdgcn_readlane(myptr, 1);
+  constexpr bool SW = MODE == GNN_AGG_MEAN_BWD;
+  const uint32_t nmax = (uint32_t)max<int64_t>(a.nrows - 1, 0);
+  int32_t n[S];
+#pragma unroll
+  for (int u = 0; u < S; ++u) n[u] = __builtin_amdgcn_readfirstlane(a.nbr[min(sbeg + u, max(send - 1, sbeg))]);
+  // this lane group's slot of each group of G: oid[m] = n[G·m + grp]; MEAN_BWD: the in-degree of
+  // that neighbour (U per lane, not G·U wave-uniform values), loaded one step ahead with the ids
+  int32_t oid[U];
+  float dn[U];
+#pragma unroll
+  for (int m = 0; m < U; ++m) {
+    oid[m] = n[G * m];
+#pragma unroll
+    for (int g = 1; g < G; ++g) oid[m] = grp == g ? n[G * m + g] : oid[m];
+    dn[m] = SW ? a.nodew[min((uint32_t)oid[m], nmax)] : 1.0f;
+  }
+  for (int32_t s = sbeg; s < send; s += S) {
+    float v[U][VEC];
+#pragma unroll
+    for (int m = 0; m < U; ++m) vload_bf<VEC>(xb + (int64_t)oid[m] * a.ldx, v[m]);
+    int32_t nn[S];  // the next step's ids, behind this step's row loads
+#pragma unroll
+    for (int u = 0; u < S; ++u) nn[u] = __builtin_amdgcn_readfirstlane(a.nbr[min(s + S + u, send - 1)]);
+#pragma unroll
+    for (int m = 0; m < U; ++m) {
+      if constexpr (SW) contrib_w<MODE, VEC, true>(a, dn[m], 0, v[m]);  // the lane's own slot's term, once
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int32_t k = s + G * m + g;
+        if (k >= send) break;  // wave-uniform
+        while (k >= cend) {
+          flush(j);
+          ++j;
+          cend = __builtin_amdgcn_readlane(myptr, j + 1);
+        }
+        const bool mine = grp == g;
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[q] = mine ? acc[q] + v[m][q] : acc[q];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < U; ++m) {
+      oid[m] = nn[G * m];
+#pragma unroll
+      for (int g = 1; g < G; ++g) oid[m] = grp == g ? nn[G * m + g] : oid[m];
+      if constexpr (SW) dn[m] = a.nodew[min((uint32_t)oid[m], nmax)];
     }
   }
   for (; j < nrow; ++j) flush(j);
@@ -1490,12 +1620,52 @@ extern "C" gnn_status gnn_aggregate_f32(const gnn_graph* g, const gnn_agg_params
 // in gnn_aggregate_f32; no long-segment split.  F <= 512.
 namespace gnnmp {
 namespace {
+// lane groups of the bf16 gather (agg_wave_group_bf16_kernel): 2 = two slots per load instruction
+// (VEC 4, F / 4 <= 32: configs[4]'s F = 128 mean 609 -> 496 us), 1 = one (agg_wave_kernel, 32 of 64
+// lanes at F = 128), 4 = four (VEC 8, F / 8 <= 16: measured slower, 786 us at occupancy 4 —
+// profiles/r99_bf_groups.txt); GNNMP_BF_GROUPS overrides (A/B)
+int bf16_groups() {
+  static const int v = [] {
+    const char* e = std::getenv("GNNMP_BF_GROUPS");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
+// rows wider than 32 chunks of 4 (configs[4]'s 168-wide layer-0 image half): the two-group form
+// over 16-byte pieces with U = 4 or 8 slot pairs per step, 0 = the one-slot kernel;
+// GNNMP_BF_WIDE_U overrides (A/B)
+int bf16_wide_u() {
+  static const int v = [] {
+    const char* e = std::getenv("GNNMP_BF_WIDE_U");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int MODE>
-gnn_status launch_bf16(const AggArgs& a, int vec, hipStream_t st) {
+gnn_status launch_bf16(const AggArgs& a, int vec, bool vec8, hipStream_t st) {
   if (a.nrows == 0 || a.F == 0) return GNN_OK;
   const int rpw = 16;
   const unsigned wblocks = (unsigned)ceil_div(ceil_div(a.nrows, rpw) * 64, 256);
   const int nchunk = a.F / vec;
+  if constexpr (MODE != GNN_AGG_GCN) {
+    const int grp = bf16_groups();
+    if (grp == 4 && vec8 && a.F / 8 <= 16) {
+      agg_wave_group_bf16_kernel<MODE, 8, 4, 4><<<wblocks, 256, 0, st>>>(a, rpw);
+      return hip_check(hipGetLastError(), "gnn_aggregate_bf16");
+    }
+    if (grp >= 2 && vec == 4 && nchunk <= 32) {
+      agg_wave_group_bf16_kernel<MODE, 4, 2><<<wblocks, 256, 0, st>>>(a, rpw);
+      return hip_check(hipGetLastError(), "gnn_aggregate_bf16");
+    }
+    const int wu = bf16_wide_u();
+    if (grp >= 2 && vec8 && a.F / 8 <= 32 && wu > 0) {  // 16-byte pieces, two slots per instruction
+      if (wu == 4) agg_wave_group_bf16_kernel<MODE, 8, 2, 4><<<wblocks, 256, 0, st>>>(a, rpw);
+      else agg_wave_group_bf16_kernel<MODE, 8, 2, 8><<<wblocks, 256, 0, st>>>(a, rpw);
+      return hip_check(hipGetLastError(), "gnn_aggregate_bf16");
+    }
+  }
   if (nchunk <= 64) {
     if (vec == 4) agg_wave_kernel<MODE, 4, 1, true><<<wblocks, 256, 0, st>>>(a, rpw);
     else if (vec == 2) agg_wave_kernel<MODE, 2, 1, true><<<wblocks, 256, 0, st>>>(a, rpw);
@@ -1547,13 +1717,14 @@ extern "C" gnn_status gnn_aggregate_bf16(const gnn_graph* g, const gnn_agg_param
     return aligned(x, 2 * v) && aligned(y, 2 * v) && aligned(p->addend, 4 * v);
   };
   const int vec = ok_vec(4) ? 4 : (ok_vec(2) ? 2 : 1);
+  const bool vec8 = ok_vec(8);
   if (F / vec > 128) return fail(GNN_ERR_UNSUPPORTED, __func__, "F too wide for the bf16 gather");
   hipStream_t st = (hipStream_t)stream;
   switch (p->mode) {
-    case GNN_AGG_SUM: return launch_bf16<GNN_AGG_SUM>(a, vec, st);
-    case GNN_AGG_MEAN: return launch_bf16<GNN_AGG_MEAN>(a, vec, st);
-    case GNN_AGG_MEAN_BWD: return launch_bf16<GNN_AGG_MEAN_BWD>(a, vec, st);
-    case GNN_AGG_GCN: return launch_bf16<GNN_AGG_GCN>(a, vec, st);
+    case GNN_AGG_SUM: return launch_bf16<GNN_AGG_SUM>(a, vec, vec8, st);
+    case GNN_AGG_MEAN: return launch_bf16<GNN_AGG_MEAN>(a, vec, vec8, st);
+    case GNN_AGG_MEAN_BWD: return launch_bf16<GNN_AGG_MEAN_BWD>(a, vec, vec8, st);
+    case GNN_AGG_GCN: return launch_bf16<GNN_AGG_GCN>(a, vec, vec8, st);
     default: return fail(GNN_ERR_INVALID_ARG, __func__, "unknown mode");
   }
 }
