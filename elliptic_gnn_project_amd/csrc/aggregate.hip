@@ -1623,22 +1623,12 @@ namespace {
 // lane groups of the bf16 gather (agg_wave_group_bf16_kernel): 2 = two slots per load instruction
 // (VEC 4, F / 4 <= 32: configs[4]'s F = 128 mean 609 -> 496 us), 1 = one (agg_wave_kernel, 32 of 64
 // lanes at F = 128), 4 = four (VEC 8, F / 8 <= 16: measured slower, 786 us at occupancy 4 —
-// profiles/r99_bf_groups.txt); GNNMP_BF_GROUPS overrides (A/B)
+// profiles/r99_bf_groups.txt; two groups over 16-byte pieces for the 168-wide layer-0 rows also
+// measured slower, +130-180 us per step); GNNMP_BF_GROUPS overrides (A/B)
 int bf16_groups() {
   static const int v = [] {
     const char* e = std::getenv("GNNMP_BF_GROUPS");
     return e ? std::atoi(e) : 2;
-  }();
-  return v;
-}
-
-// rows wider than 32 chunks of 4 (configs[4]'s 168-wide layer-0 image half): the two-group form
-// over 16-byte pieces with U = 4 or 8 slot pairs per step, 0 = the one-slot kernel;
-// GNNMP_BF_WIDE_U overrides (A/B)
-int bf16_wide_u() {
-  static const int v = [] {
-    const char* e = std::getenv("GNNMP_BF_WIDE_U");
-    return e ? std::atoi(e) : 0;
   }();
   return v;
 }
@@ -1657,12 +1647,6 @@ gnn_status launch_bf16(const AggArgs& a, int vec, bool vec8, hipStream_t st) {
     }
     if (grp >= 2 && vec == 4 && nchunk <= 32) {
       agg_wave_group_bf16_kernel<MODE, 4, 2><<<wblocks, 256, 0, st>>>(a, rpw);
-      return hip_check(hipGetLastError(), "gnn_aggregate_bf16");
-    }
-    const int wu = bf16_wide_u();
-    if (grp >= 2 && vec8 && a.F / 8 <= 32 && wu > 0) {  // 16-byte pieces, two slots per instruction
-      if (wu == 4) agg_wave_group_bf16_kernel<MODE, 8, 2, 4><<<wblocks, 256, 0, st>>>(a, rpw);
-      else agg_wave_group_bf16_kernel<MODE, 8, 2, 8><<<wblocks, 256, 0, st>>>(a, rpw);
       return hip_check(hipGetLastError(), "gnn_aggregate_bf16");
     }
   }
