@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["GNNMP_LIB"]) if os.environ.get("GNNMP_LIB") else PKG_DIR / "libgnnmp.so"  # (GNNMP_LIB: A/B builds)
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -148,7 +148,11 @@ class GnnGemmTNParams(ctypes.Structure):
         ("planes_format", c_i32), ("g_dtype", c_i32), ("planes_exp", c_i32),
         ("sq_partial", c_ptr), ("sq_step", c_ptr), ("sq_skip_lo", c_i64), ("sq_skip_hi", c_i64), ("sq_cap", c_i64),
         ("row_exp", c_ptr),
+        ("g_rowmax", c_ptr),  # ABI 25
     ]
+
+
+ROWMAX_ROWS = 16  # GNN_ROWMAX_ROWS (ABI 25)
 
 
 # gnn_act
@@ -279,7 +283,7 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,
          c_i32, ctypes.c_float, ctypes.c_uint64, c_ptr, c_ptr, c_i64, c_ptr, c_i64, c_ptr, c_i32, c_ptr, c_i64,
-         c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
+         c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_size, c_ptr]),
     "gnn_gat_bwd_act_f32": (
         ctypes.c_int,
         [ctypes.POINTER(GnnGraph), c_i32, c_i32, ctypes.c_float, c_ptr, c_i64, c_ptr, c_ptr, c_ptr, c_ptr, c_ptr,

@@ -359,6 +359,28 @@ def gcn_aggregate(y: torch.Tensor, edge_index: torch.Tensor, bias: torch.Tensor 
 # GATNet's output conv (heads 1, C <= 2) in the narrow slot-parallel form with the fused CE
 # (gnn_gat_out_ce_f32, round 6); GNNMP_GAT_NARROW=0: the lane-group kernel (A/B)
 _GAT_NARROW = os.environ.get("GNNMP_GAT_NARROW", "1") != "0"
+# GATNet: the hidden attention backward also writes max |dxh| per 16-row group for the lin's TN
+# (ABI 25); GNNMP_GAT_ROWMAX=0: the TN scans dxh itself (A/B)
+_GAT_ROWMAX = os.environ.get("GNNMP_GAT_ROWMAX", "1") != "0"
+
+
+def tag_rowmax(g: torch.Tensor, rowmax: torch.Tensor) -> None:
+    """Record on g the per-16-row maxima of |g| its producer wrote (gnn_gemm_tn_params.g_rowmax),
+    keyed on g's storage and version: any in-place edit of g voids them (rowmax_of)."""
+    g._gnnmp_rowmax = (rowmax, g.data_ptr(), g._version, tuple(g.shape), tuple(g.stride()))
+
+
+def rowmax_of(g: torch.Tensor):
+    """The row-group maxima tagged on g by its producer, if still valid for g's current data."""
+    t = getattr(g, "_gnnmp_rowmax", None)
+    if t is None:
+        return None
+    rowmax, ptr, ver, shape, stride = t
+    if g.data_ptr() != ptr or g._version != ver or tuple(g.shape) != shape or tuple(g.stride()) != stride:
+        return None
+    return rowmax
+
+
 _GAT_CE = True  # the CE in the narrow form's launch under fused_ce_target (False: its own launch; A/B, tests)
 
 
@@ -520,12 +542,20 @@ class _GATAttentionProj(torch.autograd.Function):
         nb = _lib.c_size(0)
         _lib.call("gnn_gat_bwd_workspace_size", N, plan.num_slots, heads, chans, nb)
         ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=dev)
+        # (ABI 25) max |dxh| per 16-row group, written as dxh is stored: the lin's weight-gradient TN
+        # (dW = dxhᵀ · x, the g form over x's half-pair image) takes its block scales from these
+        # instead of a pass over dxh (fused.gemm_tn reads the tag)
+        rowmax = torch.empty(max((N + _lib.ROWMAX_ROWS - 1) // _lib.ROWMAX_ROWS, 1), dtype=torch.int32,
+                             device=dev) if _GAT_ROWMAX and N > 0 else None
         t0 = KernelTimer.begin()
         _lib.call("gnn_gat_bwd_act_proj_f32", plan.c_graph, heads, chans, slope, xh.data_ptr(), _ld(xh),
                   a_src.data_ptr(), a_dst.data_ptr(), att_src.data_ptr(), att_dst.data_ptr(), alpha.data_ptr(),
                   act, dropout_p, seed & 0xFFFFFFFFFFFFFFFF, _lib.ptr(seed_ctr), out.data_ptr(), _ld(out),
                   dz.data_ptr(), _ld(dz), w.data_ptr(), w.size(0), dpre.data_ptr(), _ld(dpre), dxh.data_ptr(),
-                  _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_handle(dev))
+                  _ld(dxh), datt_s.data_ptr(), datt_d.data_ptr(), _lib.ptr(rowmax), ws.data_ptr(), ws.numel(),
+                  _lib.stream_handle(dev))
+        if rowmax is not None:
+            tag_rowmax(dxh, rowmax)
         S = plan.num_slots
         KernelTimer.end(t0, ("gat_bwd", heads, chans, F),
                         S * (12 + 16 * heads + 4 * F + 4 * F) + N * (8 + 16 * heads + 4 * F + 4 * F))

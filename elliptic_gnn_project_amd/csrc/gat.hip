@@ -96,6 +96,9 @@ struct GatArgs {
   // (ABI 24) dy given as dz · proj (dz [N, pnproj], proj [pnproj, F]): the output conv's lin
   // backward formed as each row slice loads — GATNet's dh is never materialised
   const float* pdz; int64_t ld_pdz; const float* pproj; int32_t pnproj;
+  // (ABI 25) float bits of max |dxh| per GNN_ROWMAX_ROWS-row group: zeroed by the rows pass,
+  // atomicMax'd by the cols pass as it stores dxh (max is order-free: deterministic)
+  uint32_t* dxh_rowmax;
 };
 
 // the row of group position pos (pos < N)
@@ -943,6 +946,7 @@ __global__ __launch_bounds__(256) void gat_bwd_rows_group_kernel(GatArgs a, GatG
     const float adr_ = a.a_d[(r < a.N ? r : 0) * H + sl.hs];
     const float adr = r < a.N ? adr_ : 0.0f;
     const bool own = r < a.N && end - beg <= lg.T;
+    if (a.dxh_rowmax && r < a.N && lig == 0 && (r & (GNN_ROWMAX_ROWS - 1)) == 0) a.dxh_rowmax[r / GNN_ROWMAX_ROWS] = 0u;
     if (!own) end = beg;
     if (own) store_dpre<VEC>(a, sl, r, dO);
     BwdSlot q0{0.0f, 0.0f, false}, q1{0.0f, 0.0f, false};
@@ -1020,6 +1024,17 @@ __global__ __launch_bounds__(256) void gat_bwd_cols_group_kernel(GatArgs a, GatG
         pd.v[i] += dadh * x.v[i];
       }
       stv<VEC>(a.dxh + j * a.ld_dxh + f0, acc);
+    }
+    if (a.dxh_rowmax) {  // kernel-uniform: max |dxh| over the wave's rpw rows (one row group when
+      // rpw <= GNN_ROWMAX_ROWS: the wave's first row is a multiple of rpw), one atomic per wave
+      float m = 0.0f;
+      if (valid && slot_ok && ep == 0) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) m = fmaxf(m, fabsf(acc.v[i]));
+      }
+      const int span = rpw <= GNN_ROWMAX_ROWS ? 64 : G;  // lanes whose rows share a group
+      for (int off = span >> 1; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+      if (valid && (lane & (span - 1)) == 0) atomicMax(a.dxh_rowmax + j / GNN_ROWMAX_ROWS, __float_as_uint(m));
     }
   }
   // block partial of d att_src / d att_dst: groups of a wave, then the 4 waves through LDS
@@ -1597,6 +1612,25 @@ extern "C" gnn_status gnn_gat_act_bwd_f32(int64_t N, int64_t F, gnn_act act, flo
   return GNN_OK;
 }
 
+namespace gnnmp {
+namespace {
+// max |x| over each GNN_ROWMAX_ROWS-row group of x [N, F] (float bits, one wave per group): the
+// generic kernels' dxh_rowmax (the group kernels form it as they store dxh)
+__global__ __launch_bounds__(256) void rowmax_group_kernel(const float* __restrict__ x, int64_t ld, int64_t N, int32_t F,
+                                                          uint32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t grp = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t r0 = grp * GNN_ROWMAX_ROWS;
+  if (r0 >= N) return;
+  const int64_t n = min<int64_t>(GNN_ROWMAX_ROWS, N - r0) * F;
+  float m = 0.0f;
+  for (int64_t e = lane; e < n; e += 64) m = fmaxf(m, fabsf(x[(r0 + e / F) * ld + e % F]));
+  for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if (lane == 0) out[grp] = __float_as_uint(m);
+}
+}  // namespace
+}  // namespace gnnmp
+
 extern "C" gnn_status gnn_gat_bwd_workspace_size(int64_t N, int64_t S, int32_t H, int32_t C, size_t* bytes) {
   if (!bytes || N < 0 || S < 0 || H < 1 || C < 1) return fail(GNN_ERR_INVALID_ARG, __func__, "bad args");
   SizerAdapter a;
@@ -1658,6 +1692,7 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
       ar.pe_seed_ptr = post->pe_seed_ptr;
       ar.pdz = post->pdz; ar.ld_pdz = post->ld_pdz; ar.pproj = post->pproj; ar.pnproj = post->pnproj;
       a.dout = post->dpre; a.ld_dout = post->ld_dpre;
+      ar.dxh_rowmax = a.dxh_rowmax = post->dxh_rowmax;
     }
     switch (vec) {
 #define GNN_GAT_BWD(V)                                                            \
@@ -1696,6 +1731,11 @@ gnn_status gat_bwd_impl(const char* fn, const gnn_graph* g, int32_t H, int32_t C
   GNN_LAUNCH_CHECK();
   gat_bwd_cols_kernel<<<row_blocks(a.N), 256, 0, st>>>(a);
   GNN_LAUNCH_CHECK();
+  if (post && post->dxh_rowmax) {  // the generic kernels: the row-group maxima in a pass of their own
+    rowmax_group_kernel<<<(unsigned)ceil_div(ceil_div(a.N, GNN_ROWMAX_ROWS), 4), 256, 0, st>>>(
+        dxh, ld_dxh, a.N, (int32_t)F_, post->dxh_rowmax);
+    GNN_LAUNCH_CHECK();
+  }
   int64_t nblk = a.N < kAttBlocks ? a.N : kAttBlocks;
   int64_t rpb = ceil_div(a.N, nblk);
   nblk = ceil_div(a.N, rpb);
@@ -1748,7 +1788,7 @@ extern "C" gnn_status gnn_gat_bwd_act_proj_f32(const gnn_graph* g, int32_t H, in
                                                float dropout_p, uint64_t seed, const uint64_t* seed_ptr, const float* y,
                                                int64_t ld_y, const float* dz, int64_t ld_dz, const float* proj,
                                                int32_t nproj, float* dpre, int64_t ld_dpre, float* dxh, int64_t ld_dxh,
-                                               float* d_att_src, float* d_att_dst, void* workspace,
+                                               float* d_att_src, float* d_att_dst, uint32_t* dxh_rowmax, void* workspace,
                                                size_t workspace_bytes, gnn_stream_t stream) {
   const int64_t F = (int64_t)H * C;
   if (act != GNN_ACT_NONE && act != GNN_ACT_ELU) return fail(GNN_ERR_INVALID_ARG, __func__, "unknown act");
@@ -1764,6 +1804,7 @@ extern "C" gnn_status gnn_gat_bwd_act_proj_f32(const gnn_graph* g, int32_t H, in
   post.pe_act = ep.act; post.pe_drop = ep.dropout; post.pe_thresh = ep.keep_thresh; post.pe_scale = ep.drop_scale;
   post.pe_keep = (float)(1.0 - (double)dropout_p); post.pe_seed = seed; post.pe_seed_ptr = seed_ptr;
   post.pdz = dz; post.ld_pdz = ld_dz; post.pproj = proj; post.pnproj = nproj;
+  post.dxh_rowmax = dxh_rowmax;
   return gat_bwd_impl(__func__, g, H, C, 1, slope, xh, ld_xh, a_src, a_dst, att_src, att_dst, alpha, dz, ld_dz, dxh,
                       ld_dxh, d_att_src, d_att_dst, nullptr, nullptr, workspace, workspace_bytes, stream, &post);
 }

@@ -190,6 +190,7 @@ struct TNArgs {
   int32_t ap_h2;  // half-pair image (2 f16 planes)
   int32_t ap_exp; // half-pair: the image holds A · 2^ap_exp (undone in the slab scale)
   const int32_t* rowexp;  // in-kernel half-pair TN: per-row exponents bounding A's rows (the NT's)
+  const uint32_t* growmax;  // (ABI 25) the g form's max |G| per GNN_ROWMAX_ROWS rows (float bits), or null
 };
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,

@@ -1046,6 +1046,9 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
     a.ap_exp = a.ap_h2 ? p->planes_exp : 0;
     if (a.ap_exp < -100 || a.ap_exp > 100) return fail(GNN_ERR_INVALID_ARG, __fn, "planes_exp outside [-100, 100]");
     if (a.ap_h2) {  // the half-pair image: f16 hi / lo planes, 3 products
+      // (ABI 25) the plain g form's block scale from the producer's row-group maxima (row blocks are
+      // whole 32-row chunks, so every block covers whole GNN_ROWMAX_ROWS groups)
+      a.growmax = (!a.dz && a.g) ? p->g_rowmax : nullptr;
       if (p->math != GNN_MATH_F32 && tn_h2_ok(a)) {
         // a shard-sized M (the dz form): split-K block pairs over half as many row blocks (round 6)
         int nred = nblk;

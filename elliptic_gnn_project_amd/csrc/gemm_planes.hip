@@ -542,7 +542,10 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   auto scan_scale = [&]() __attribute__((always_inline)) {  // run in the prologue, behind chunk 0's loads
     float zm = 0.f;
     const int nq = a.nproj;
-    if constexpr (GF) {  // max |g| over the block's rows: float4 pieces, 16 in flight per thread
+    if (GF && a.growmax) {  // (ABI 25) the producer's row-group maxima: ~50 words, not ~800 rows
+      const int64_t q1 = (mend + GNN_ROWMAX_ROWS - 1) / GNN_ROWMAX_ROWS;
+      for (int64_t q = mbeg / GNN_ROWMAX_ROWS + tid; q < q1; q += T) zm = fmaxf(zm, __uint_as_float(a.growmax[q]));
+    } else if constexpr (GF) {  // max |g| over the block's rows: float4 pieces, 16 in flight per thread
       constexpr int SU = 16;  // (the block's ~800 rows in two round trips: the scan is latency-bound)
       const int n4 = (a.Nr + 3) >> 2;
       const int64_t npc = (mend - mbeg) * n4;

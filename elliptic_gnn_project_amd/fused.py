@@ -255,6 +255,12 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
     )
     if row_exp is not None:
         p.row_exp = row_exp.data_ptr()
+    if g is not None and dz is None and planes is not None:
+        from .aggregation import rowmax_of
+
+        rm = rowmax_of(g)  # the producer's max |g| per 16-row group (ABI 25): no scan pass in the TN
+        if rm is not None:
+            p.g_rowmax = rm.data_ptr()
     if check_planes:
         return bool(_lib.load().gnn_gemm_tn_planes_ok(p))
     out = torch.empty(n_out, dtype=torch.float32, device=dev)

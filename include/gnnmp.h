@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 24
+#define GNNMP_ABI_VERSION 25
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -367,14 +367,18 @@ gnn_status gnn_gat_bwd_act_f32(const gnn_graph* g, int32_t H, int32_t C, float s
 
 /* (ABI 24) gnn_gat_bwd_act_f32 with dy given as dz · proj (dz [N, nproj], ld_dz; proj [nproj, H·C],
  * 16-byte aligned, nproj <= 4): the backward of a hidden layer whose output fed a projection
- * (gnn_gat_fwd_params.proj) — dy is formed as each row slice loads, never stored. */
+ * (gnn_gat_fwd_params.proj) — dy is formed as each row slice loads, never stored.
+ * (ABI 25) dxh_rowmax (optional, [ceil(N / GNN_ROWMAX_ROWS)] uint32): also the float bits of max |dxh|
+ * over each group of GNN_ROWMAX_ROWS rows — the g_rowmax of the weight-gradient TN of the layer's
+ * lin (dW = dxhᵀ · x), which then skips its own pass over dxh. */
 gnn_status gnn_gat_bwd_act_proj_f32(const gnn_graph* g, int32_t H, int32_t C, float slope, const float* xh,
                                     int64_t ld_xh, const float* a_src, const float* a_dst, const float* att_src,
                                     const float* att_dst, const float* alpha, gnn_act act, float dropout_p,
                                     uint64_t seed, const uint64_t* seed_ptr, const float* y, int64_t ld_y,
                                     const float* dz, int64_t ld_dz, const float* proj, int32_t nproj, float* dpre,
                                     int64_t ld_dpre, float* dxh, int64_t ld_dxh, float* d_att_src, float* d_att_dst,
-                                    void* workspace, size_t workspace_bytes, gnn_stream_t stream);
+                                    uint32_t* dxh_rowmax, void* workspace, size_t workspace_bytes,
+                                    gnn_stream_t stream);
 
 /* Explain-mode backward (messages scaled by edge_w[s], see gnn_gat_fwd_params.edge_w): as
  * gnn_gat_bwd_f32, plus d_edge_w[s] = sum_h alpha[s,h] * <dout_i(h), xh[j,h,:]> for every CSR slot. */
@@ -517,7 +521,17 @@ typedef struct {
                                             (max_k |A[r,k]| < 2^row_exp[r]), as a GNN_MATH_HALF_PAIR NT of
                                             the same operand writes them; with math GNN_MATH_HALF_PAIR and
                                             the plain g form the TN runs in half-pair arithmetic */
+  const uint32_t* g_rowmax;              /* optional (ABI 25), the plain g form over a half-pair image:
+                                            [ceil(M / GNN_ROWMAX_ROWS)] float bits of max |G| over each
+                                            group of GNN_ROWMAX_ROWS rows and all Nr columns (an upper
+                                            bound is enough), as gnn_gat_bwd_act_proj_f32 writes them for
+                                            its dxh: the TN takes its per-row-block power-of-two scale
+                                            from these instead of a pass over its G rows.  Exact maxima
+                                            give the scan's scale, so the result is bit-identical. */
 } gnn_gemm_tn_params;
+
+/* Row-group granularity of gnn_gemm_tn_params.g_rowmax (ABI 25). */
+#define GNN_ROWMAX_ROWS 16
 
 /* Weight gradient dW = Gᵀ·[A1|A2] summed over all M rows (split-M slabs + ordered reduce).
  * out (contiguous): dW1 = Gᵀ·A1 [Nr, k1] | dW2 = Gᵀ·A2 [Nr, k2] | db = Σ_m G [Nr] |
