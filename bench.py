@@ -599,7 +599,9 @@ def report(args, preset, full, E_global, data, dist, world, rank, dev, step, bf1
     value = E_global * args.steps / el
     roof, cpu = extras(value) if extras is not None else (None, None)
     if rank == 0:
-        scaling = "weak" if (world == 1 or args.scale == "weak") else "strong"
+        # the scale mode the N-GPU lines of the same command use (at N = 1 both modes run the one
+        # Elliptic graph): the driver's 1 -> 8 curve reads one label across its points
+        scaling = args.scale
         line = {
             "metric": preset.get("metric") or (METRIC if args.arch == "sage" else METRIC.replace("SAGE", args.arch.upper())),
             "value": value,
