@@ -15,7 +15,7 @@ import torch  # noqa: F401  (loads the HIP runtime before libgnnmp)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ["GNNMP_LIB"]) if os.environ.get("GNNMP_LIB") else PKG_DIR / "libgnnmp.so"  # (GNNMP_LIB: A/B builds)
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 # gnn_dtype
 DTYPE_F32 = 0
@@ -149,6 +149,7 @@ class GnnGemmTNParams(ctypes.Structure):
         ("sq_partial", c_ptr), ("sq_step", c_ptr), ("sq_skip_lo", c_i64), ("sq_skip_hi", c_i64), ("sq_cap", c_i64),
         ("row_exp", c_ptr),
         ("g_rowmax", c_ptr),  # ABI 25
+        ("dz_graph", c_ptr), ("dz_u", c_ptr), ("ldu", c_i64), ("dz_cols", c_i32),  # ABI 26
     ]
 
 

@@ -191,6 +191,8 @@ struct TNArgs {
   int32_t ap_exp; // half-pair: the image holds A · 2^ap_exp (undone in the slab scale)
   const int32_t* rowexp;  // in-kernel half-pair TN: per-row exponents bounding A's rows (the NT's)
   const uint32_t* growmax;  // (ABI 25) the g form's max |G| per GNN_ROWMAX_ROWS rows (float bits), or null
+  // (ABI 26) the half-pair dz form: dz[:, 0:ccols] formed in the TN as the CSC sum of u (null: read)
+  const int32_t* cptr; const int32_t* cnbr; const float* cu; int64_t ldu; int32_t ccols;
 };
 
 // split-bf16 ("x3": each f32 operand = hi + mid + lo bf16, 6 MFMA products) launchers,

@@ -777,6 +777,24 @@ static int64_t tn_ksplit_max_m() {
   return v;
 }
 
+// (ABI 26) the CSC sum of u inside the half-pair dz-form TN when each of its 8 waves walks at most
+// one 64-row group of the block's rows (shard-sized M: 8-way shard 0.0947 -> 0.0923 ms per step,
+// profiles/r105_csc_ab.txt); GNNMP_TN_CSC_INKERNEL=0 / 1 forces it off / on (A/B)
+// rows per block of the half-pair TN (dz: the dz form, split-K pairs at shard-sized M)
+static int64_t tn_h2_rows_per_block(int64_t M, bool dz) {
+  const int64_t chunks = ceil_div(M, 32);
+  if (dz && M <= tn_ksplit_max_m()) return ceil_div(chunks, 128) * 32;
+  return ceil_div(chunks, tn_blocks(M)) * 32;
+}
+static bool tn_csc_in_kernel(int64_t rows_per_block) {
+  static const int v = [] {
+    const char* e = std::getenv("GNNMP_TN_CSC_INKERNEL");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (v >= 0) return v != 0;
+  return (rows_per_block + 63) / 64 + 1 <= 8;  // groups a block's rows can touch <= its waves
+}
+
 // the in-kernel half-pair TN at Nr <= 64, k1 + k2 <= 128 holds three blocks per CU (its LDS is
 // sized by its k-tiles and 64 G rows, 47 KB): three times the blocks, so three times the chunk loads
 // in flight per CU (its chunk loop is latency-bound: one 16-row chunk in flight per block)
@@ -959,6 +977,19 @@ extern "C" gnn_status gnn_gemm_tn_workspace_size(int64_t M, int64_t Nr, int64_t 
 static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void* workspace,
                                    size_t workspace_bytes, gnn_stream_t stream);
 
+// (ABI 26) the folded CSC sum's arguments (dz_graph's CSC, dz_u, dz_cols); false when dz_graph is
+// given but cannot be taken (no dz form, no u, dz_cols outside 1..min(2, nproj), num_nodes != M)
+static bool tn_csc_args(const gnn_gemm_tn_params* p, TNArgs* a) {
+  a->cptr = nullptr; a->cnbr = nullptr; a->cu = nullptr; a->ldu = 0; a->ccols = 0;
+  const gnn_graph* cg = p->dz_graph;
+  if (!cg) return true;
+  if (!p->dz || !p->dz_u || !cg->colptr || !cg->row || cg->num_nodes != p->M || p->dz_cols < 1 || p->dz_cols > 2 ||
+      p->dz_cols > p->nproj || p->ldu < p->dz_cols)
+    return false;
+  a->cptr = cg->colptr; a->cnbr = cg->row; a->cu = p->dz_u; a->ldu = p->ldu; a->ccols = p->dz_cols;
+  return true;
+}
+
 static unsigned red_blocks(int64_t n_out) { return (unsigned)ceil_div(ceil_div(n_out, 4), kRedOut); }
 
 extern "C" gnn_status gnn_gemm_tn_sq_blocks(int64_t n_out, int32_t* nb) {
@@ -1020,6 +1051,8 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
   a.a2 = p->a2; a.lda2 = p->lda2; a.k2 = (int32_t)p->k2;
   a.slab = static_cast<float*>(workspace); a.slab_stride = stride;
   a.rows_per_block = ceil_div(ceil_div(p->M, 32), nblk) * 32;  // multiple of both chunk sizes
+  if (!tn_csc_args(p, &a))
+    return fail(GNN_ERR_INVALID_ARG, __fn, "dz_graph needs the dz form, dz_u, 1 <= dz_cols <= 2 and num_nodes == M");
   auto al8 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0; };
   const bool v2 = (a.k1 % 2 == 0) && (a.lda1 % 2 == 0) && al8(a.a1) &&
                   (a.k2 == 0 || ((a.k2 % 2 == 0) && (a.lda2 % 2 == 0) && al8(a.a2)));
@@ -1058,6 +1091,20 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
           nred = (int)ceil_div(chunks, per);
           a.rows_per_block = per * 32;
         }
+        if (a.rows_per_block != tn_h2_rows_per_block(a.M, a.dz != nullptr))
+          return fail(GNN_ERR_HIP, __fn, "internal: TN row-block rule mismatch");
+        if (a.cptr && !tn_csc_in_kernel(a.rows_per_block)) {
+          // (ABI 26) rows of more than one 64-row group per wave: the folded CSC sum would run two
+          // dependent gather rounds per wave ahead of the chunk loop (full configs[1] graph, 800 rows a
+          // block: TN 87 -> 94 us, profiles/r105_csc_ab.txt) — the separate narrow launch instead
+          gnn_agg_params ag{};
+          ag.mode = GNN_AGG_SUM;
+          ag.transpose = 1;
+          const gnn_status s = gnn_aggregate_f32(p->dz_graph, &ag, p->dz_u, p->ldu, p->dz_cols,
+                                                 const_cast<float*>(p->dz), p->lddz, stream);
+          if (s != GNN_OK) return s;
+          a.cptr = nullptr;
+        }
         launch_tn_h2(a, ks ? 2 * nred : nblk, st, ks);
         GNN_LAUNCH_CHECK();
         slab_reduce_kernel<<<red_blocks(n_out), 256, 0, st>>>(a.slab, stride, nred, out, n_out, sqo);
@@ -1067,6 +1114,10 @@ static gnn_status gemm_tn_dispatch(const gnn_gemm_tn_params* p, float* out, void
       if (planes_only) return fail(GNN_ERR_UNSUPPORTED, __fn, "half-pair image A outside the half-pair kernel's shapes");
       a.ap = nullptr;
     }
+  }
+  if (a.cptr)  // only the half-pair dz-form kernel forms dz's CSC columns itself
+    return fail(GNN_ERR_UNSUPPORTED, __fn, "dz_graph outside the half-pair dz-form TN (gnn_gemm_tn_planes_ok)");
+  if (p->a_planes) {
     if (a.ap && a.a_bf16) {  // a bf16 image (one plane): the bf16-storage form
       if (p->math == GNN_MATH_F32 || !tn_img16_ok(a))
         return fail(GNN_ERR_UNSUPPORTED, __fn, "bf16 image A outside the image kernel's shapes");
@@ -1189,9 +1240,13 @@ extern "C" int gnn_gemm_tn_planes_ok(const gnn_gemm_tn_params* p) {
   a.ap_col2 = (int32_t)std::min<int64_t>(p->planes_col2, INT32_MAX);
   a.ap_ps = p->planes_stride;
   a.ap_h2 = p->planes_format == GNN_PLANES_HALF_PAIR;
+  if (!tn_csc_args(p, &a)) return 0;
   if (a.ap_h2) {
     a.proj = p->proj; a.nproj = p->dz ? p->nproj : 0;
+    // (ABI 26) with dz_graph: 1 only when the kernel forms dz's CSC columns itself (a shard-sized
+    // row block); the call would otherwise launch the CSC sum first, which the caller can as well
+    if (a.cptr && !tn_csc_in_kernel(tn_h2_rows_per_block(a.M, true))) return 0;
     return tn_h2_ok(a) ? 1 : 0;
   }
-  return (a.a_bf16 ? tn_img16_ok(a) : tn_planes_ok(a)) ? 1 : 0;
+  return (!a.cptr && (a.a_bf16 ? tn_img16_ok(a) : tn_planes_ok(a))) ? 1 : 0;
 }

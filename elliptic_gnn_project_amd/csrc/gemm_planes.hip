@@ -439,6 +439,96 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_planes_kernel(TNArgs a) {
   if (PROJ && tid < a.nproj) slab[(int64_t)a.Nr * Kc + a.Nr + a.nproj * a.Nr + tid] = comb(tid, 1);
 }
 
+// (ABI 26) dz[r, 0:ccols] = Σ_{CSC slots s of row r} u[row[s], :] for the rows [mbeg, mend) of a
+// TN block — gnn_aggregate_f32(SUM, transpose) of u, i.e. aggregate.hip's agg_narrow_lds_kernel
+// <SUM, NF = 2, 256, COOP> restated for the TN's waves, bit for bit: the same 64-row groups (aligned
+// as that kernel's waves), the same 256-slot LDS passes from the group's first slot, the same four
+// interleaved partial sums per lane and the same whole-wave xor tree for slots past the first 32 of
+// a pass.  Wave w of the block takes groups w, w + NW, ...; a lane stores only its block's rows.
+// `buf`: 512 floats of LDS per wave.
+template <int NW>
+__device__ __forceinline__ void tn_csc_fold(const TNArgs& a, int64_t mbeg, int64_t mend, float* buf, int lane,
+                                            int wave) {
+  constexpr int CAP = 256, NI = CAP / 64, LCAP = 32;
+  const int F = a.ccols;
+  const int64_t nrows = a.M;
+  float* dz = const_cast<float*>(a.dz);
+  for (int64_t r0 = ((mbeg >> 6) + wave) * 64; r0 < mend; r0 += 64 * NW) {
+    const int64_t r = r0 + lane;
+    const bool rok = r < nrows;
+    const int32_t pbeg = a.cptr[rok ? r : nrows];
+    const int32_t pend = a.cptr[rok ? r + 1 : nrows];
+    const int32_t base = __builtin_amdgcn_readfirstlane(a.cptr[r0]);
+    const int32_t wend = __builtin_amdgcn_readfirstlane(a.cptr[min(r0 + 64, nrows)]);
+    float acc[2] = {0.f, 0.f};
+    for (int32_t pb = base; pb < wend; pb += CAP) {
+      const int32_t pe = min(pb + CAP, wend);
+      int32_t nn[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int32_t k = pb + lane + 64 * i;
+        nn[i] = a.cnbr[k < pe ? k : pb];
+      }
+      float xv[NI][2];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const float* xr = a.cu + (int64_t)nn[i] * a.ldu;
+#pragma unroll
+        for (int f = 0; f < 2; ++f) xv[i][f] = xr[f < F ? f : 0];
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) buf[f * CAP + lane + 64 * i] = f < F ? xv[i][f] : 0.0f;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      const int32_t lo = max(pbeg, pb), hi0 = min(pend, pe);
+      const int32_t hi = min(hi0, lo + LCAP);
+      float q1[2] = {0.f, 0.f}, q2[2] = {0.f, 0.f}, q3[2] = {0.f, 0.f};
+      int32_t k = lo;
+      for (; k + 3 < hi; k += 4) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          acc[f] += buf[f * CAP + (k - pb)];
+          q1[f] += buf[f * CAP + (k + 1 - pb)];
+          q2[f] += buf[f * CAP + (k + 2 - pb)];
+          q3[f] += buf[f * CAP + (k + 3 - pb)];
+        }
+      }
+      for (; k < hi; ++k) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) acc[f] += buf[f * CAP + (k - pb)];
+      }
+#pragma unroll
+      for (int f = 0; f < 2; ++f) acc[f] += (q1[f] + q2[f]) + q3[f];
+      uint64_t longm = __ballot(hi0 - lo > LCAP);  // the rest of each long row: all 64 lanes, strided
+      while (longm) {
+        const int L = __builtin_ctzll(longm);
+        longm &= longm - 1;
+        const int32_t s0 = __builtin_amdgcn_readlane(lo, L) + LCAP, s1 = __builtin_amdgcn_readlane(hi0, L);
+        float part[2] = {0.f, 0.f};
+        for (int32_t k2 = s0 + lane; k2 < s1; k2 += 64) {
+#pragma unroll
+          for (int f = 0; f < 2; ++f) part[f] += buf[f * CAP + (k2 - pb)];
+        }
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) part[f] += __shfl_xor(part[f], off);
+          if (lane == L) acc[f] += part[f];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (rok && r >= mbeg && r < mend) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+        if (f < F) dz[r * a.lddz + f] = acc[f];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ TN over a half-pair image
 // dW = Gᵀ·[A1 | A2] with A from a half-pair image (2 f16 planes hi / lo, gemm_ws.hip K7a-h) and
 // G — the dz form with the h mask, G = (dz·P) ⊙ [h > 0] / (1 - p), the SAGE preset's hidden
@@ -463,7 +553,11 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_planes_kernel(TNArgs a) {
 // the same rows and the first (KT + 1) / 2 / the remaining k-tiles, so a shard-sized M runs twice
 // the rows per block on every CU and writes half the slab partials (both blocks form the same G;
 // the side sums come from the first).  The block's A pieces cover only its k-range.
-template <int KT, bool GOUT, int LAB = 0, int NW = 4, bool GF = false, int KS = 1>
+// CSC (round 6, ABI 26; the dz form): the block first forms dz[:, 0:ccols] of its own rows — the
+// transposed mean of the output layer, Σ over each row's CSC slots of u[src] (u = dlogits / deg
+// from the CE launch) — with tn_csc_fold below, writes them to dz and reads them back as before:
+// the separate F = 2 CSC-sum launch of the step is gone.
+template <int KT, bool GOUT, int LAB = 0, int NW = 4, bool GF = false, int KS = 1, bool CSC = false>
 __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(KS == 1 || (KS == 2 && NW == 8), "split-K: the 8-wave form");
@@ -796,6 +890,10 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
     }
     load_g(0, 0);
     if constexpr (RGN == 2) load_g(1, min(1, clast));
+    if constexpr (CSC && !GF) {  // this block's dz[:, 0:ccols] (At is scratch until chunk 0's put)
+      tn_csc_fold<NW>(a, mbeg, mend, reinterpret_cast<float*>(&At[0][0]) + wave * 2 * 256, lane, wave);
+      __syncthreads();  // the block's dz rows written (a workgroup fence) before any wave reads them
+    }
     float rz0 = 0.f, rz1 = 0.f;
     if constexpr (!GF) {
       rz0 = a.dz[(uint32_t)((ldbase(0) + zr) * (int)a.lddz + zqc)];
@@ -1224,6 +1322,10 @@ bool tn_h2_ok(const TNArgs& a) {
   } else if (!a.dz || !a.proj || !a.h || a.nproj < 1 || a.ap_ld != 336) {
     return false;
   }
+  // (ABI 26) the folded CSC sum: dz form without gout, 1..2 columns inside dz's nproj
+  if (a.cptr && (gf || a.gout || !a.cnbr || !a.cu || a.ccols < 1 || a.ccols > 2 || a.ccols > a.nproj ||
+                 a.ldu < a.ccols || a.M * a.ldu >= ((int64_t)1 << 31)))
+    return false;
   if (a.k1 < 1 || a.k1 > a.ap_col2 || a.ap_col2 % 8 || a.ap_col2 + a.k2 > a.ap_ld) return false;
   if (a.ap_ps < a.M * (int64_t)a.ap_ld || 2 * a.ap_ps * 2 >= ((int64_t)1 << 31) || a.M < PT_ROWS) return false;
   const int64_t ldmax = gf ? a.ldg : std::max({a.ldh, a.lddz});
@@ -1237,6 +1339,11 @@ void launch_tn_h2(const TNArgs& a, int nblk, hipStream_t st, bool ks) {
   if (!a.dz) {  // the g form
     if (a.ap_ld == 176) gemm_tn_h2_kernel<6, false, 0, 8, true><<<nblk, 512, 0, st>>>(a);
     else gemm_tn_h2_kernel<11, false, 0, 8, true><<<nblk, 512, 0, st>>>(a);
+    return;
+  }
+  if (a.cptr) {  // (ABI 26) the CSC sum of u folded in (tn_h2_ok: no gout)
+    if (ks) gemm_tn_h2_kernel<11, false, 0, 8, false, 2, true><<<nblk, 512, 0, st>>>(a);
+    else gemm_tn_h2_kernel<11, false, 0, 8, false, 1, true><<<nblk, 512, 0, st>>>(a);
     return;
   }
   if (ks) {

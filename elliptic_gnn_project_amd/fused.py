@@ -55,6 +55,10 @@ _K1_PAD = os.environ.get("GNNMP_K1_PAD", "1") != "0"
 # (profiles/r18h) 0.3692 vs 0.3637 ms per step in line — the captured fork / join costs more than
 # the prep it hides, as in round 3
 _SIDE_PREP = os.environ.get("GNNMP_SIDE_PREP", "0") == "1"
+# The 2-layer SAGE backward: the layer-1 half-pair TN forms dz's meanᵀ half (the CSC sum of the CE's
+# u) itself, block by block (gnn_gemm_tn_params.dz_graph, ABI 26, bit for bit), instead of a separate
+# F = 2 CSC-sum launch before it; GNNMP_TN_CSC=0 keeps the separate launch (A/B)
+_TN_CSC = os.environ.get("GNNMP_TN_CSC", "1") != "0"
 # GCN backward: the skinny masked-gradient NT also writes its column sums (the layer below's bias
 # gradient, gnn_gemm_nt_params.colsum_part) instead of a separate colsum pass; GNNMP_NT_COLSUM=0: A/B
 _NT_COLSUM = os.environ.get("GNNMP_NT_COLSUM", "1") != "0"
@@ -222,14 +226,16 @@ def gemm_nt(a1, bt, n, a2=None, bias=None, relu=False, dropout_p=0.0, seed=0, pr
 
 
 def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gout=None, math=None,
-            planes=None, check_planes=False, sq=None, sq_skip=(0, 0), row_exp=None):
+            planes=None, check_planes=False, sq=None, sq_skip=(0, 0), row_exp=None, csc=None):
     """((Gᵀ·a1, Gᵀ·a2), db, dzᵀ·h, dzsum) from one flat fp32 buffer — the MFMA TN kernel.
     ``planes``: A read from a split image (a1 / a2 may be None); ``check_planes`` as gemm_nt.
     ``sq`` = (partials buffer, step tensor) of train_ops.grad_sq_request: the reduce also writes
     the clip + Adam norm partials of the output outside ``sq_skip`` (indices into the flat output,
     negative ones from its end), recorded by train_ops.grad_sq_produced.
     ``row_exp``: the int32 row exponents a half-pair NT wrote for [a1 | a2]; with math="half_pair"
-    and the plain g form the TN then runs in half-pair arithmetic (gnn_gemm_tn_params.row_exp)."""
+    and the plain g form the TN then runs in half-pair arithmetic (gnn_gemm_tn_params.row_exp).
+    ``csc`` = (plan, u): the half-pair dz-form TN forms dz[:, :u.size(1)] itself as the transposed
+    SUM of u over the plan (gnn_gemm_tn_params.dz_graph, ABI 26) instead of reading it."""
     if planes is not None:
         M, k1, k2, dev = planes.n, planes.k1, planes.k2, planes.img.device
     else:
@@ -261,6 +267,9 @@ def gemm_tn(nr, a1, a2=None, g=None, dz=None, proj=None, h=None, hscale=1.0, gou
         rm = rowmax_of(g)  # the producer's max |g| per 16-row group (ABI 25): no scan pass in the TN
         if rm is not None:
             p.g_rowmax = rm.data_ptr()
+    if csc is not None:
+        cplan, u = csc
+        p.dz_graph, p.dz_u, p.ldu, p.dz_cols = ctypes.addressof(cplan.c_graph), u.data_ptr(), _ld(u), u.size(1)
     if check_planes:
         return bool(_lib.load().gnn_gemm_tn_planes_ok(p))
     out = torch.empty(n_out, dtype=torch.float32, device=dev)
@@ -323,6 +332,24 @@ def gemm_nt_input(x: torch.Tensor, n: int, **kw):
     if im is not None and gemm_nt(None, None, n, planes=im, check_planes=True, **kw):
         return gemm_nt(None, None, n, planes=im, **kw)
     return gemm_nt(x, None, n, **kw)
+
+
+def _csc_fold(ctx, dz, u, hscale):
+    """(plan, u) when the 2-layer SAGE backward's one TN (layer 1, half-pair image, dz form, no input
+    gradient) takes the folded CSC sum of u (ABI 26), else None (the caller runs the CSC sum)."""
+    L = ctx.meta[0]
+    if not _TN_CSC or L != 2 or ctx.needs_input_grad[0] or ctx.bimgs[0] is not None:
+        return None
+    saved = ctx.saved_tensors
+    if saved[L] is not None or getattr(ctx, "image", None) is None or not isinstance(ctx.image[0], HalfPairImage):
+        return None  # layer 1 not on the half-pair image of [agg | x]
+    im = ctx.image[0]
+    hs1, Wl0 = saved[1], saved[2 * L - 1]
+    csc = (ctx.plan, u)
+    if not gemm_tn(Wl0.size(0), None, None, h=hs1, hscale=hscale, planes=im, check_planes=True, dz=dz, proj=ctx.P,
+                   csc=csc):
+        return None
+    return csc
 
 
 def gemm_tn_input(nr: int, x: torch.Tensor, g: torch.Tensor):
@@ -484,13 +511,16 @@ class _FusedSAGE(torch.autograd.Function):
         Wl, Wr = params[0::3], params[2::3]
         hscale = 1.0 / (1.0 - p) if p > 0 else 1.0
         N = dlogits.size(0)
+        csc_fold = None  # (plan, u) when the layer's TN forms dz's meanᵀ half itself (ABI 26)
         buf = getattr(dlogits, "_gnnmp_dz", None)  # the fused CE's [N, 2C] buffer, dlogits its right half
         if (buf is not None and buf.shape == (N, 2 * C) and dlogits.stride() == (2 * C, 1)
                 and dlogits.data_ptr() == buf.data_ptr() + C * buf.element_size()):
             dz = buf
             u = getattr(dlogits, "_gnnmp_u", None)  # dlogits / max(deg, 1) from the forward's CE launch
             if u is not None:  # meanᵀ as a plain CSC sum: MEAN_BWD's per-slot terms precomputed, same bits
-                aggregate(plan, u, _lib.AGG_SUM, transpose=True, out=dz[:, :C])
+                csc_fold = _csc_fold(ctx, dz, u, hscale)
+                if csc_fold is None:
+                    aggregate(plan, u, _lib.AGG_SUM, transpose=True, out=dz[:, :C])
             else:
                 aggregate(plan, dlogits, _lib.AGG_MEAN_BWD, transpose=True, nodew=plan.deg, out=dz[:, :C])
         else:
@@ -541,7 +571,7 @@ class _FusedSAGE(torch.autograd.Function):
                     a_l, im = aggregate(plan, hs[0], _lib.AGG_MEAN, nodew=plan.deg), None
             if l == L - 2:
                 dW, db, dW2, dzs = gemm_tn(fo, a_l, hs[l], dz=dz, proj=P, h=hs[l + 1], hscale=hscale,
-                                           gout=gout, planes=im, sq=sq, sq_skip=(-2 * C, -C))
+                                           gout=gout, planes=im, sq=sq, sq_skip=(-2 * C, -C), csc=csc_fold)
                 grads[3 * (L - 1) + 0] = dW2[:C]
                 grads[3 * (L - 1) + 1] = dzs[C:]
                 grads[3 * (L - 1) + 2] = dW2[C:]

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define GNNMP_ABI_VERSION 25
+#define GNNMP_ABI_VERSION 26
 
 typedef struct ihipStream_t* gnn_stream_t; /* == hipStream_t */
 
@@ -528,6 +528,19 @@ typedef struct {
                                             its dxh: the TN takes its per-row-block power-of-two scale
                                             from these instead of a pass over its G rows.  Exact maxima
                                             give the scan's scale, so the result is bit-identical. */
+  const gnn_graph* dz_graph;             /* optional (ABI 26), the half-pair dz form without gout: the TN
+                                            itself forms dz[:, 0:dz_cols] = Σ over each row's CSC slots of
+                                            dz_u[source, 0:dz_cols] — gnn_aggregate_f32(SUM, transpose) of
+                                            dz_u, bit for bit — and writes it into dz before using it, so
+                                            the caller skips that launch (the SAGE output layer's meanᵀ of
+                                            u = dlogits / deg, gnn_sage_out_mean_ce_f32).  Inside its
+                                            kernel when a row block is at most ~450 rows (a strong-scaling
+                                            shard), else by that aggregation launched first.  1 <= dz_cols
+                                            <= min(2, nproj), dz_graph->num_nodes == M; UNSUPPORTED outside
+                                            that kernel.  gnn_gemm_tn_planes_ok returns 1 for such
+                                            params only when the kernel forms the columns itself */
+  const float* dz_u; int64_t ldu;
+  int32_t dz_cols;
 } gnn_gemm_tn_params;
 
 /* Row-group granularity of gnn_gemm_tn_params.g_rowmax (ABI 25). */

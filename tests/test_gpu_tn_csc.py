@@ -1,0 +1,123 @@
+"""GPU: the 2-layer SAGE backward's layer-1 half-pair TN forming dz's meanᵀ half itself (ABI 26,
+gnn_gemm_tn_params.dz_graph: the CSC sum of the CE launch's u = dlogits / deg, block by block,
+gemm_planes.hip tn_csc_fold) — bit for bit the separate F = 2 CSC-sum launch it replaces
+(gnn_aggregate_f32 SUM, transpose): every gradient of the train step (src/train_gnn.py:187-209),
+on the full configs[1] graph, the largest 8-way shard (the split-K TN) and graphs whose CSC columns
+run past one 256-slot pass and past the 32 slots a lane walks (the whole-wave tail)."""
+import pytest
+import torch
+
+from oracle import pyg_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _elliptic(n, e, seed=9):
+    from elliptic_gnn_project_amd.dataset_elliptic import prepare_inputs, synthetic_elliptic
+
+    return prepare_inputs(synthetic_elliptic(num_nodes=n, num_edges=e, seed=seed),
+                          dict(use_time_scalar=True, symmetrize_edges=True, train_window_k=10))
+
+
+def _hub_graph(n=3000, seed=4):
+    """A random graph plus hub sources with 40 / 300 / 1500 out-edges (CSC columns of one lane's
+    32-slot walk, several 256-slot passes) and a run of isolated nodes."""
+    g = torch.Generator().manual_seed(seed)
+    src = torch.randint(0, n - 100, (4 * n,), generator=g)
+    dst = torch.randint(0, n - 100, (4 * n,), generator=g)
+    hubs = []
+    for h, d in ((7, 40), (700, 300), (1901, 1500)):
+        hubs.append(torch.stack([torch.full((d,), h), torch.randint(0, n, (d,), generator=g)]))
+    ei = torch.cat([torch.stack([src, dst])] + hubs, dim=1)
+    x = torch.randn(n, 166, generator=g)
+    y = torch.randint(0, 2, (n,), generator=g)
+    mask = torch.rand(n, generator=g) < 0.5
+    return x, ei, y, mask
+
+
+def _step_grads(device, x, ei, y, mask, fold, monkeypatch, dropout=0.5, in_kernel=True):
+    from elliptic_gnn_project_amd import _lib, fused
+    from elliptic_gnn_project_amd.planes import register_input
+    from elliptic_gnn_project_amd.train_gnn import _make_loss_fn, build_model
+    from elliptic_gnn_project_amd.train_ops import unit_gradient
+
+    calls = []
+    real = fused.aggregate
+
+    def spy(plan, t, mode, *a, **k):
+        if mode == _lib.AGG_SUM and k.get("transpose"):
+            calls.append(t.shape)
+        return real(plan, t, mode, *a, **k)
+
+    monkeypatch.setattr(fused, "_TN_CSC", fold)
+    monkeypatch.setattr(fused, "aggregate", spy)
+    x, ei, y, mask = x.to(device), ei.to(device), y.to(device), mask.to(device)
+    cw = pyg_ref.class_weight(y[mask].cpu())
+    denom = float(mask.sum())
+    torch.manual_seed(11)
+    model = build_model("sage", x.size(1), dict(hidden_dim=128, layers=2, dropout=dropout)).to(device)
+    loss_fn = _make_loss_fn({}, cw, model, 1, 34)
+    model.train()
+    torch.manual_seed(5)
+    xr = register_input(x)
+    with loss_fn.target(y, mask, denom):
+        logits = model(xr, ei)
+    loss = loss_fn.full(logits, y, mask, denom=denom)
+    loss.backward(unit_gradient(device))
+    torch.cuda.synchronize()
+    # with the fold on, the layer-1 TN formed meanᵀ(dlogits): no separate CSC-sum launch (only when
+    # its row blocks are shard-sized: gnn_gemm_tn_planes_ok declines the full graph's 800-row blocks)
+    assert (len(calls) == 0) == (fold and in_kernel), calls
+    return logits.detach().clone(), {k: p.grad.clone() for k, p in model.named_parameters()}
+
+
+def _check_equal(device, data, monkeypatch, in_kernel=True, **kw):
+    a = _step_grads(device, *data, fold=True, monkeypatch=monkeypatch, in_kernel=in_kernel, **kw)
+    b = _step_grads(device, *data, fold=False, monkeypatch=monkeypatch, **kw)
+    assert torch.equal(a[0], b[0])
+    for k in a[1]:
+        assert torch.equal(a[1][k], b[1][k]), k
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.5])
+def test_tn_csc_fold_small(device, monkeypatch, dropout):
+    d = _elliptic(4000, 5000)
+    _check_equal(device, (d.x, d.edge_index, d.y, d.train_mask), monkeypatch, dropout=dropout)
+
+
+def test_tn_csc_fold_hub_columns(device, monkeypatch):
+    _check_equal(device, _hub_graph(), monkeypatch)
+
+
+def test_tn_csc_fold_full_size(device, monkeypatch):
+    """The full graph: 800-row TN blocks keep the separate CSC-sum launch (the fold measured slower
+    there), the same bits either way."""
+    d = _elliptic(203_769, 234_355, seed=1)
+    _check_equal(device, (d.x, d.edge_index, d.y, d.train_mask), monkeypatch, in_kernel=False)
+
+
+@pytest.mark.parametrize("ways", [2, 4])
+def test_tn_csc_fold_shards_2_4(device, monkeypatch, ways):
+    """The largest 2- / 4-way shard (row blocks of ~416 / ~224 rows: one 64-row group per wave)."""
+    from elliptic_gnn_project_amd import distributed as gdist
+
+    full = _elliptic(203_769, 234_355, seed=1)
+    parts = gdist.partition_timesteps(full.timestep, full.edge_index, ways)
+    e_t = torch.bincount(full.timestep[full.edge_index[1]], minlength=int(full.timestep.max()) + 1)
+    r = max(range(ways), key=lambda i: int(sum(int(e_t[t]) for t in parts[i])))
+    sh = gdist.shard_graph(full, ways, r, parts=parts)
+    _check_equal(device, (sh.x, sh.edge_index, sh.y, sh.train_mask), monkeypatch)
+
+
+def test_tn_csc_fold_largest_shard(device, monkeypatch):
+    """The largest 8-way timestep shard: M <= 32768 runs the split-K TN pairs (both blocks of a
+    pair form the same rows)."""
+    from elliptic_gnn_project_amd import distributed as gdist
+
+    full = _elliptic(203_769, 234_355, seed=1)
+    parts = gdist.partition_timesteps(full.timestep, full.edge_index, 8)
+    e_t = torch.bincount(full.timestep[full.edge_index[1]], minlength=int(full.timestep.max()) + 1)
+    r = max(range(8), key=lambda i: int(sum(int(e_t[t]) for t in parts[i])))
+    sh = gdist.shard_graph(full, 8, r, parts=parts)
+    assert sh.x.size(0) <= 32768
+    _check_equal(device, (sh.x, sh.edge_index, sh.y, sh.train_mask), monkeypatch)

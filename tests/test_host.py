@@ -167,7 +167,8 @@ STRUCTS = {
                                                "math", "a_dtype", "h_dtype", "a_planes", "planes_ld",
                                                "planes_stride", "planes_col2", "planes_format", "g_dtype",
                                                "planes_exp", "sq_partial", "sq_step", "sq_skip_lo", "sq_skip_hi",
-                                               "sq_cap", "row_exp", "g_rowmax"]),
+                                               "sq_cap", "row_exp", "g_rowmax", "dz_graph", "dz_u", "ldu",
+                                               "dz_cols"]),
 }
 
 
