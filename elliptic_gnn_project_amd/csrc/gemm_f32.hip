@@ -791,6 +791,7 @@ static bool tn_csc_in_kernel(int64_t rows_per_block) {
     const char* e = std::getenv("GNNMP_TN_CSC_INKERNEL");
     return e ? std::atoi(e) : -1;
   }();
+  if (rows_per_block > 1792) return false;  // the block's dz rows staged in LDS (gemm_planes.hip dzb)
   if (v >= 0) return v != 0;
   return (rows_per_block + 63) / 64 + 1 <= 8;  // groups a block's rows can touch <= its waves
 }

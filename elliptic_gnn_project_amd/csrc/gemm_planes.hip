@@ -445,14 +445,18 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_planes_kernel(TNArgs a) {
 // as that kernel's waves), the same 256-slot LDS passes from the group's first slot, the same four
 // interleaved partial sums per lane and the same whole-wave xor tree for slots past the first 32 of
 // a pass.  Wave w of the block takes groups w, w + NW, ...; a lane stores only its block's rows.
-// `buf`: 512 floats of LDS per wave.
+// `buf`: 512 floats of LDS per wave.  The block's whole dz rows (the folded columns and the ones
+// read, q < nproj) also go to `dzb` ([row - mbeg][MAXPROJ], LDS), where the prologue's first two
+// chunks read them instead of a round trip to dz, and the return value is the lane's part of the
+// block scale's bound: max over its rows of Σ_q |dz[r][q]| in the scan's own order.
 template <int NW>
-__device__ __forceinline__ void tn_csc_fold(const TNArgs& a, int64_t mbeg, int64_t mend, float* buf, int lane,
-                                            int wave) {
+__device__ __forceinline__ float tn_csc_fold(const TNArgs& a, int64_t mbeg, int64_t mend, float* buf, float* dzb,
+                                             int lane, int wave) {
   constexpr int CAP = 256, NI = CAP / 64, LCAP = 32;
-  const int F = a.ccols;
+  const int F = a.ccols, nq = a.nproj;
   const int64_t nrows = a.M;
   float* dz = const_cast<float*>(a.dz);
+  float zm = 0.f;
   for (int64_t r0 = ((mbeg >> 6) + wave) * 64; r0 < mend; r0 += 64 * NW) {
     const int64_t r = r0 + lane;
     const bool rok = r < nrows;
@@ -460,6 +464,10 @@ __device__ __forceinline__ void tn_csc_fold(const TNArgs& a, int64_t mbeg, int64
     const int32_t pend = a.cptr[rok ? r + 1 : nrows];
     const int32_t base = __builtin_amdgcn_readfirstlane(a.cptr[r0]);
     const int32_t wend = __builtin_amdgcn_readfirstlane(a.cptr[min(r0 + 64, nrows)]);
+    float dv[MAXPROJ];  // the row's columns past the folded ones (clamped row / column, no branch)
+    const int64_t rc = min(r, nrows - 1);
+#pragma unroll
+    for (int q = 0; q < MAXPROJ; ++q) dv[q] = a.dz[rc * a.lddz + min(max(q, F), nq - 1)];
     float acc[2] = {0.f, 0.f};
     for (int32_t pb = base; pb < wend; pb += CAP) {
       const int32_t pe = min(pb + CAP, wend);
@@ -525,8 +533,19 @@ __device__ __forceinline__ void tn_csc_fold(const TNArgs& a, int64_t mbeg, int64
 #pragma unroll
       for (int f = 0; f < 2; ++f)
         if (f < F) dz[r * a.lddz + f] = acc[f];
+      float v[MAXPROJ];
+#pragma unroll
+      for (int q = 0; q < MAXPROJ; ++q) v[q] = q == 0 ? acc[0] : (q == 1 && F > 1) ? acc[1] : dv[q];
+      float sr = 0.f;  // (the scan's Σ_q |dz[r][q]|, same order)
+#pragma unroll
+      for (int q = 0; q < MAXPROJ; ++q) {
+        sr += q < nq ? fabsf(v[q]) : 0.f;
+        dzb[(r - mbeg) * MAXPROJ + q] = v[q];
+      }
+      zm = fmaxf(zm, sr);
     }
   }
+  return zm;
 }
 
 // ------------------------------------------------------------------ TN over a half-pair image
@@ -633,8 +652,9 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
   // read 4 per thread per pass with clamped indices and no branch around a load, so a pass is one
   // round trip (the first form's per-row loop waited on every row: ~5 us of the prologue)
   float gsc = 1.f, gunsc = 1.f;
+  float zm_fold = 0.f;  // CSC: the fold's part of the bound (the scan then reads no dz rows)
   auto scan_scale = [&]() __attribute__((always_inline)) {  // run in the prologue, behind chunk 0's loads
-    float zm = 0.f;
+    float zm = zm_fold;
     const int nq = a.nproj;
     if (GF && a.growmax) {  // (ABI 25) the producer's row-group maxima: ~50 words, not ~800 rows
       const int64_t q1 = (mend + GNN_ROWMAX_ROWS - 1) / GNN_ROWMAX_ROWS;
@@ -664,7 +684,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
         }
       }
     }
-    for (int64_t r0 = mbeg + tid; !GF && r0 < mend; r0 += 4 * T) {
+    for (int64_t r0 = mbeg + tid; !GF && !CSC && r0 < mend; r0 += 4 * T) {
       float v[4][MAXPROJ];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -890,12 +910,20 @@ __global__ __launch_bounds__(64 * NW) void gemm_tn_h2_kernel(TNArgs a) {
     }
     load_g(0, 0);
     if constexpr (RGN == 2) load_g(1, min(1, clast));
+    float* dzb = reinterpret_cast<float*>(&At[0][0]) + NW * 2 * 256;  // CSC: the block's dz rows
     if constexpr (CSC && !GF) {  // this block's dz[:, 0:ccols] (At is scratch until chunk 0's put)
-      tn_csc_fold<NW>(a, mbeg, mend, reinterpret_cast<float*>(&At[0][0]) + wave * 2 * 256, lane, wave);
+      zm_fold = tn_csc_fold<NW>(a, mbeg, mend, reinterpret_cast<float*>(&At[0][0]) + wave * 2 * 256, dzb, lane, wave);
       __syncthreads();  // the block's dz rows written (a workgroup fence) before any wave reads them
     }
     float rz0 = 0.f, rz1 = 0.f;
-    if constexpr (!GF) {
+    if constexpr (CSC && !GF) {  // chunks 0 and 1 from the fold's LDS rows (rows outside the block: masked)
+      auto dzb_at = [&](int c) __attribute__((always_inline)) {
+        const int64_t rl = ldbase(c) + zr - mbeg;
+        return (rl >= 0 && rl < mend - mbeg) ? dzb[rl * MAXPROJ + zq] : 0.f;
+      };
+      rz0 = dzb_at(0);
+      rz1 = dzb_at(min(1, clast));
+    } else if constexpr (!GF) {
       rz0 = a.dz[(uint32_t)((ldbase(0) + zr) * (int)a.lddz + zqc)];
       rz1 = a.dz[(uint32_t)((ldbase(min(1, clast)) + zr) * (int)a.lddz + zqc)];
     }
