@@ -121,3 +121,14 @@ def test_tn_csc_fold_largest_shard(device, monkeypatch):
     sh = gdist.shard_graph(full, 8, r, parts=parts)
     assert sh.x.size(0) <= 32768
     _check_equal(device, (sh.x, sh.edge_index, sh.y, sh.train_mask), monkeypatch)
+
+
+def test_tn_csc_call_side_launch_full_size(device, monkeypatch):
+    """dz_graph handed to gnn_gemm_tn_f32 where its kernel declines it (the full graph's 800-row
+    blocks): the call launches the CSC sum itself before the TN — the same bits, and no launch
+    left to the caller."""
+    from elliptic_gnn_project_amd import fused
+
+    monkeypatch.setattr(fused, "_csc_fold", lambda ctx, dz, u, hscale: (ctx.plan, u) if fused._TN_CSC else None)
+    d = _elliptic(203_769, 234_355, seed=1)
+    _check_equal(device, (d.x, d.edge_index, d.y, d.train_mask), monkeypatch)

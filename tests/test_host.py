@@ -207,3 +207,34 @@ def test_product_path_has_no_cpu_fallback():
     imp = re.compile(r"^\s*(from\s+oracle\b|import\s+oracle\b|from\s+\.+oracle\b)", re.M)
     for f in (ROOT / "elliptic_gnn_project_amd").rglob("*.py"):
         assert not imp.search(f.read_text()), f"{f} imports the oracle"
+
+
+def test_tn_dz_graph_is_checked(lib):
+    """ABI 26 gnn_gemm_tn_params.dz_graph (the TN forming dz's CSC columns itself) is refused before
+    any launch when it cannot be taken: dz_cols outside 1..min(2, nproj) or num_nodes != M
+    (INVALID_ARG), an operand form other than the half-pair dz-form kernel (UNSUPPORTED), and
+    gnn_gemm_tn_planes_ok reports 0 for it on a g-form call (pointers below are never read)."""
+    import ctypes
+
+    from elliptic_gnn_project_amd import _lib
+
+    fake, M = 1 << 20, 1000
+    g = _lib.GnnGraph(M, 4000, fake, fake, fake, fake, fake, None, None)
+    p = _lib.GnnGemmTNParams(M, 128, None, 0, fake, 4, fake, 4, fake, 128, 1.0, None, 0,
+                             fake, 166, 166, fake, 166, 166)
+    p.math = _lib.MATH_SPLIT_BF16
+    p.dz_graph, p.dz_u, p.ldu, p.dz_cols = ctypes.addressof(g), fake, 2, 3
+    ws_bytes = 1 << 30
+    assert lib.gnn_gemm_tn_f32(p, fake, fake, ws_bytes, None) == 1
+    assert b"dz_graph" in lib.gnn_last_error()
+    p.dz_cols = 2
+    g.num_nodes = M + 1
+    assert lib.gnn_gemm_tn_f32(p, fake, fake, ws_bytes, None) == 1
+    g.num_nodes = M
+    assert lib.gnn_gemm_tn_f32(p, fake, fake, ws_bytes, None) == 5  # f32 operands: not the half-pair kernel
+    assert b"dz_graph" in lib.gnn_last_error()
+    q = _lib.GnnGemmTNParams(M, 128, fake, 128)  # the plain g form over a half-pair image
+    q.math, q.a_planes, q.planes_ld, q.planes_stride, q.planes_col2 = _lib.MATH_SPLIT_BF16, fake, 336, M * 336, 168
+    q.k1, q.k2, q.planes_format = 166, 166, _lib.PLANES_HALF_PAIR
+    q.dz_graph, q.dz_u, q.ldu, q.dz_cols = ctypes.addressof(g), fake, 2, 2
+    assert lib.gnn_gemm_tn_planes_ok(q) == 0
