@@ -148,10 +148,14 @@ def _torchrun(args, timeout=300):
     return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
 
 
+@pytest.mark.parametrize("arch", ["sage_resbn", "sage"])
 @pytest.mark.parametrize("scale", ["weak", "strong"])
-def test_bench_two_rank_path(device, scale):
+def test_bench_two_rank_path(device, scale, arch):
+    """bench.py's N > 1 path (two ranks on the one card, gloo): configs[3] and the headline preset —
+    under strong scaling each rank's half of the graph runs the shard-sized schedule (the TN with
+    the folded CSC sum, ABI 26)."""
     r = _torchrun(["bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
-                   "--no-roofline", "--dist-backend", "gloo", "--arch", "sage_resbn", "--scale", scale])
+                   "--no-roofline", "--dist-backend", "gloo", "--arch", arch, "--scale", scale])
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     out = json.loads(line)
